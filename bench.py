@@ -1,0 +1,366 @@
+"""Benchmark of the BED decode -> standardize -> GRM hot path on MI355X.
+
+Metric (BASELINE.json): "SNPs/sec standardized (500k x 1M) + GRM GF/s at 1/2/4/8 GPUs".
+
+  value      = SNPs/s standardized, whole job: every rank decodes + Unit-standardizes its own
+               synthetic 500k-iid x 1M-SNP BED matrix (the UKBB shape of configs[4]), resident in
+               HBM as packed 2-bit codes, in blocks of 8192 SNPs into an f32 F-order block buffer
+               (weak scaling: per-GPU work fixed).  A step = one pass over the 1M SNPs.
+  roofline   = the decode kernel (k_decode_f<float>), HBM bound: algorithmic bytes per launch =
+               block * (ceil(N/4) + 4N) / its mean HIP-event duration, vs 8.0 TB/s.
+  grm        = SnpKernel GRM of configs[3] (50k iid x 500k SNP, Unit, block 10k, f32 MFMA): SNP
+               blocks round-robin over ranks, one RCCL all-reduce of the upper-triangle K tiles.
+               gflops uses N(N+1)M (SYRK work); roofline vs 157.3 TF FP32 MFMA.
+  cpu_baseline = the oracle's C/OpenMP decode + one-pass Unit standardize (the CPU restatement
+               of bed-reader's read + standardize_f32) on a sample of the same packed columns,
+               rank 0 only; grm.cpu_baseline = NumPy/OpenBLAS Z.dot(Z.T) (snpreader.py:655).
+
+Run: python bench.py [--gpus N --steps K --warmup W]; N > 1 under torch.distributed.run.
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "SNPs/sec standardized (500k×1M) + GRM GF/s at 1/2/4/8 GPUs"
+HBM_PEAK_GBS = 8000.0
+MFMA_F32_PEAK_TFLOPS = 157.3
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=3)
+    p.add_argument("--warmup", type=int, default=1)
+    p.add_argument("--n-iid", type=int, default=500_000)
+    p.add_argument("--n-sid", type=int, default=1_000_000)
+    p.add_argument("--block", type=int, default=8192)
+    p.add_argument("--grm-iid", type=int, default=50_000)
+    p.add_argument("--grm-sid", type=int, default=500_000)
+    p.add_argument("--grm-block", type=int, default=10_000)
+    p.add_argument("--skip-grm", action="store_true")
+    p.add_argument("--skip-cpu", action="store_true")
+    p.add_argument("--cpu-seconds", type=float, default=12.0)
+    p.add_argument("--seed", type=int, default=5)
+    return p.parse_args()
+
+
+class Dist:
+    """torch.distributed (gloo) for barriers / max-over-ranks / the RCCL id exchange."""
+
+    def __init__(self, gpus):
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+        self.pg = None
+        if self.world > 1:
+            import torch.distributed as dist
+
+            dist.init_process_group("gloo")
+            self.pg = dist
+        assert self.world == gpus or self.world == 1, "--gpus must match WORLD_SIZE"
+
+    def barrier(self):
+        if self.pg:
+            self.pg.barrier()
+
+    def max(self, x):
+        if not self.pg:
+            return x
+        import torch
+
+        t = torch.tensor([float(x)], dtype=torch.float64)
+        self.pg.all_reduce(t, op=self.pg.ReduceOp.MAX)
+        return float(t.item())
+
+    def bcast_bytes(self, b):
+        if not self.pg:
+            return b
+        obj = [b]
+        self.pg.broadcast_object_list(obj, src=0)
+        return obj[0]
+
+    def close(self):
+        if self.pg:
+            self.pg.destroy_process_group()
+
+
+class Dev:
+    def __init__(self, N, nbytes):
+        self.N = N
+        self.p = ctypes.c_void_p()
+        N.call("snpmi_dev_alloc", ctypes.byref(self.p), int(nbytes))
+
+    def free(self):
+        if self.p:
+            self.N.call("snpmi_dev_free", self.p)
+            self.p = None
+
+
+class Events:
+    def __init__(self, N, count):
+        self.N = N
+        self.ev = []
+        for _ in range(count):
+            e = ctypes.c_void_p()
+            N.call("snpmi_event_create", ctypes.byref(e))
+            self.ev.append(e)
+
+    def record(self, i):
+        self.N.call("snpmi_event_record", self.ev[i])
+
+    def ms(self, a, b):
+        out = ctypes.c_float()
+        self.N.call("snpmi_event_elapsed_ms", self.ev[a], self.ev[b], ctypes.byref(out))
+        return float(out.value)
+
+    def destroy(self):
+        for e in self.ev:
+            self.N.call("snpmi_event_destroy", e)
+
+
+def maf_table(n_iid):
+    # SnpGen's MAF curve (snpreader/snpgen.py:140-151); restated here so the product never
+    # imports the oracle
+    w0, w1 = -0.6482249, -8.49790398
+    x = np.logspace(np.log10(0.1 / n_iid), np.log10(0.5), 100, base=10)
+    y = np.exp(w0 * np.log(x) + w1)
+    cdf = np.cumsum(y / y.sum())
+    cdf[-1] = 1.0
+    return np.ascontiguousarray(x), np.ascontiguousarray(cdf)
+
+
+def synth(N, buf, pitch, n, sid0, m, seed, miss):
+    x, cdf = maf_table(n)
+    N.call("snpmi_dev_synth_bed", buf, pitch, n, sid0, m, seed, miss, N.ptr(x), N.ptr(cdf), len(x))
+
+
+# ---------------------------------------------------------------------------- leg 1: decode + standardize
+def leg_standardize(N, args, dist):
+    n, m, B = args.n_iid, args.n_sid, args.block
+    pitch = N.lib().snpmi_packed_pitch(n)
+    ld = (n + 15) // 16 * 16
+    packed = Dev(N, pitch * m)
+    synth(N, packed.p, pitch, n, dist.rank * m, m, args.seed, 0.01)
+    nblk = (m + B - 1) // B
+    lut, stats, out = Dev(N, B * 16), Dev(N, B * 8), Dev(N, B * ld * 4)
+    ev = Events(N, 2 + 2 * nblk)
+
+    def step(timed):
+        dec_ms = 0.0
+        if timed:
+            ev.record(0)
+        for k in range(nblk):
+            s0 = k * B
+            cnt = min(B, m - s0)
+            src = ctypes.c_void_p(packed.p.value + s0 * pitch)
+            N.call("snpmi_dev_snp_stats", src, pitch, n, cnt, 0, N.STD_UNIT, 0.0, 0.0, 0, N.DT_F32, stats.p, lut.p)
+            if timed:
+                ev.record(2 + 2 * k)
+            N.call("snpmi_dev_decode", src, pitch, n, cnt, lut.p, N.DT_F32, 0, out.p, ld)
+            if timed:
+                ev.record(3 + 2 * k)
+        if timed:
+            ev.record(1)
+        N.call("snpmi_stream_sync")
+        if timed:
+            dec_ms = sum(ev.ms(2 + 2 * k, 3 + 2 * k) for k in range(nblk))
+        return dec_ms
+
+    for _ in range(args.warmup):
+        step(False)
+    dist.barrier()
+    N.call("snpmi_stream_sync")
+    t0 = time.perf_counter()
+    dec_ms_total = 0.0
+    step_ms = []
+    for _ in range(args.steps):
+        dec_ms_total += step(True)
+        step_ms.append(ev.ms(0, 1))
+    N.call("snpmi_stream_sync")
+    dist.barrier()
+    wall = dist.max(time.perf_counter() - t0)
+    launches = args.steps * nblk
+    dec_mean_ms = dec_ms_total / launches
+    full_block_bytes = B * ((n + 3) // 4 + 4 * n)
+    total_bytes = m * ((n + 3) // 4 + 4 * n)
+    achieved_gbs = (total_bytes / nblk) / (dec_mean_ms * 1e-3) / 1e9
+    sample = None
+    if dist.rank == 0 and not args.skip_cpu:
+        ncols = 512
+        sample = np.empty((ncols, pitch), dtype=np.uint8)
+        N.call("snpmi_memcpy_d2h", N.ptr(sample), packed.p, sample.nbytes)
+    res = dict(wall=wall, step_ms=step_ms, dec_mean_ms=dec_mean_ms, achieved_gbs=achieved_gbs,
+               full_block_bytes=full_block_bytes, launches=launches, nblk=nblk, pitch=pitch, sample=sample)
+    ev.destroy()
+    for d in (packed, lut, stats, out):
+        d.free()
+    return res
+
+
+def cpu_baseline_standardize(args, sample, pitch):
+    """Oracle C/OpenMP decode + one-pass Unit standardize on a bounded sample (rank 0)."""
+    from oracle import oracle as O
+
+    n = args.n_iid
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    bpc = (n + 3) // 4
+    body = np.ascontiguousarray(sample[:, :bpc]).reshape(-1)
+    ncols = sample.shape[0]
+    done, t0 = 0, time.perf_counter()
+    while True:
+        O.decode_standardize(body, n, ncols, dtype=np.float32, num_threads=threads)
+        done += ncols
+        el = time.perf_counter() - t0
+        if el >= args.cpu_seconds or done >= 64 * ncols:
+            break
+    return {"value": done / el, "unit": "SNPs/s", "cores": threads, "kind": "port",
+            "sample": "%d reps x %d SNP columns x %d iids (first packed columns of the same synthetic matrix), "
+                      "f32 Unit, oracle/bed_oracle.c oracle_decode_standardize_f32, %.1f s" % (done // ncols, ncols, n, el)}
+
+
+# ---------------------------------------------------------------------------- leg 2: GRM
+def leg_grm(N, args, dist, rccl):
+    n, m, B = args.grm_iid, args.grm_sid, args.grm_block
+    pitch = N.lib().snpmi_packed_pitch(n)
+    blocks = [(s0, min(B, m - s0)) for s0 in range(0, m, B)]
+    mine = blocks[dist.rank::dist.world]
+    my_m = sum(c for _, c in mine)
+    packed = Dev(N, max(1, my_m) * pitch)
+    off = 0
+    for s0, c in mine:  # generate exactly the global SNP ids this rank owns
+        synth(N, ctypes.c_void_p(packed.p.value + off * pitch), pitch, n, s0, c, args.seed + 100, 0.01)
+        off += c
+    tile_bytes = N.lib().snpmi_grm_tile_bytes(n, N.DT_F32)
+    tiles = Dev(N, tile_bytes)
+    lut, stats = Dev(N, B * 16), Dev(N, B * 8)
+    ev = Events(N, 2 + 2 * max(1, len(mine)) + 2)
+
+    def run(timed, limit=None):
+        off = 0
+        todo = mine if limit is None else mine[:limit]
+        if not todo:
+            N.call("snpmi_dev_memset", tiles.p, 0, tile_bytes)
+        for k, (s0, c) in enumerate(todo):
+            src = ctypes.c_void_p(packed.p.value + off * pitch)
+            N.call("snpmi_dev_snp_stats", src, pitch, n, c, 0, N.STD_UNIT, 0.0, 0.0, 0, N.DT_F32, stats.p, lut.p)
+            if timed:
+                ev.record(2 + 2 * k)
+            N.call("snpmi_dev_syrk_packed", src, pitch, n, c, lut.p, N.DT_F32, tiles.p, int(k > 0))
+            if timed:
+                ev.record(3 + 2 * k)
+            off += c
+        if rccl and timed:
+            ev.record(len(ev.ev) - 2)
+            N.call("snpmi_rccl_allreduce_sum", tiles.p, tile_bytes // 4, N.DT_F32)
+            ev.record(len(ev.ev) - 1)
+        N.call("snpmi_stream_sync")
+
+    run(False, limit=1)  # warm-up: one block
+    dist.barrier()
+    t0 = time.perf_counter()
+    run(True)
+    dist.barrier()
+    wall = dist.max(time.perf_counter() - t0)
+    syrk_ms = [ev.ms(2 + 2 * k, 3 + 2 * k) for k in range(len(mine))]
+    allreduce_ms = ev.ms(len(ev.ev) - 2, len(ev.ev) - 1) if rccl else 0.0
+    # spot parity at scale: diag(K) == sum over SNPs of z^2 == count of polymorphic SNPs-ish is
+    # not exact; instead check symmetry-free invariant: trace(K) = sum_j n_obs_j (Unit: sum z^2 = n_obs)
+    tr = ctypes.c_double()
+    N.call("snpmi_dev_grm_trace", tiles.p, n, N.DT_F32, ctypes.byref(tr))
+    flops_full_block = n * (n + 1) * B
+    res = dict(wall=wall, syrk_ms=syrk_ms, allreduce_ms=allreduce_ms, trace=tr.value,
+               mean_tflops=(flops_full_block / (np.mean(syrk_ms) * 1e-3) / 1e12) if syrk_ms else 0.0, nblocks=len(blocks))
+    ev.destroy()
+    for d in (packed, tiles, lut, stats):
+        d.free()
+    return res
+
+
+def cpu_baseline_grm(args):
+    """NumPy Z.dot(Z.T) (OpenBLAS syrk, the reference's snpdata.py:203-206 / snpreader.py:655)."""
+    n, b = 10_000, 2048
+    rng = np.random.default_rng(0)
+    Z = rng.standard_normal((n, b)).astype(np.float32)
+    t0 = time.perf_counter()
+    reps = 0
+    while True:
+        Z.dot(Z.T)
+        reps += 1
+        el = time.perf_counter() - t0
+        if el > 4.0 or reps >= 8:
+            break
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)
+    return {"value": reps * n * (n + 1) * b / el / 1e9, "unit": "GF/s", "cores": threads, "kind": "port",
+            "sample": "%d x Z.dot(Z.T), Z = %d x %d f32 (NumPy/OpenBLAS), %.1f s" % (reps, n, b, el)}
+
+
+def main():
+    args = parse()
+    dist = Dist(args.gpus)
+    from pysnptools_amd import _native as N
+
+    N.call("snpmi_set_device", dist.local_rank)
+    rccl = False
+    if dist.world > 1 and not args.skip_grm:
+        uid = (ctypes.c_uint8 * 128)()
+        if dist.rank == 0:
+            N.call("snpmi_rccl_unique_id", uid, 128)
+        b = dist.bcast_bytes(bytes(uid))
+        uid = (ctypes.c_uint8 * 128).from_buffer_copy(b)
+        N.call("snpmi_rccl_init", dist.world, dist.rank, uid, 128)
+        rccl = True
+
+    r1 = leg_standardize(N, args, dist)
+    total_snps = args.n_sid * dist.world * args.steps
+    value = total_snps / r1["wall"]
+    grm = None
+    if not args.skip_grm:
+        r2 = leg_grm(N, args, dist, rccl)
+        n, m = args.grm_iid, args.grm_sid
+        gf = n * (n + 1) * m / r2["wall"] / 1e9
+        grm = {"workload": "cfg4: %d iid x %d SNP, Unit, block %d, f32 MFMA SYRK, SNP blocks round-robin over %d "
+                           "rank(s)%s" % (n, m, args.grm_block, dist.world, ", RCCL all-reduce of K tiles" if rccl else ""),
+               "gflops": gf, "snps_per_s": m / r2["wall"], "seconds": r2["wall"], "scaling": "strong",
+               "allreduce_ms": r2["allreduce_ms"], "trace_K": r2["trace"],
+               "roofline": {"bound": "mfma", "achieved": r2["mean_tflops"], "peak": MFMA_F32_PEAK_TFLOPS,
+                            "unit": "TFLOP/s", "frac": r2["mean_tflops"] / MFMA_F32_PEAK_TFLOPS, "traffic": None,
+                            "kernel": "f32k::k_syrk<true>", "per_launch_flops": n * (n + 1) * args.grm_block}}
+    if dist.rank == 0:
+        cpu = None
+        if not args.skip_cpu and r1["sample"] is not None:
+            cpu = cpu_baseline_standardize(args, r1["sample"], r1["pitch"])
+            if grm is not None:
+                grm["cpu_baseline"] = cpu_baseline_grm(args)
+        n = args.n_iid
+        line = {
+            "metric": METRIC, "value": value, "unit": "SNPs/s", "n_gpus": dist.world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": r1["wall"] / args.steps * 1e3, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "config": {"workload": "decode+Unit standardize, %d iid x %d SNP per GPU (packed BED resident in HBM, "
+                                   "SnpGen MAF curve, 1%% missing), block %d SNPs, f32 F-order" % (
+                                       n, args.n_sid, args.block),
+                       "n_iid": n, "n_sid_per_gpu": args.n_sid, "block": args.block,
+                       "parallelism": "snp-shard x%d" % dist.world},
+            "roofline": {"bound": "hbm", "achieved": r1["achieved_gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": r1["achieved_gbs"] / HBM_PEAK_GBS, "traffic": None,
+                         "kernel": "k_decode_f<float>", "per_launch_bytes": r1["full_block_bytes"],
+                         "mean_launch_ms": r1["dec_mean_ms"]},
+            "cpu_baseline": cpu,
+            "grm": grm,
+        }
+        print(json.dumps(line), flush=True)
+    if rccl:
+        N.call("snpmi_rccl_destroy")
+    dist.close()
+
+
+if __name__ == "__main__":
+    main()

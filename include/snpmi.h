@@ -1,0 +1,184 @@
+/*
+ * snpmi.h -- C ABI of libsnpmi.so, the MI355X-native (gfx950, HIP) implementation of
+ * PySnpTools' BED decode -> slice -> standardize -> SnpKernel GRM path.
+ *
+ * The reference crosses into native code through the Rust/PyO3 module `bed_reader`
+ * and NumPy BLAS; every host entry point below replaces one of those call sites
+ * (paths relative to /root/reference/pysnptools):
+ *
+ *   snpmi_bed_check              bed_reader.open_bed(...) format check    snpreader/bed.py:137-145
+ *   snpmi_bed_read_{f32,f64,i8}  open_bed(...).read(index,order,dtype)     snpreader/bed.py:337-343
+ *   snpmi_standardize_{f32,f64}  bed_reader.standardize_f32/f64(...)       standardizer/standardizer.py:114,120
+ *   snpmi_subset_*               bed_reader.subset_f64_f64/f32_f64/f32_f32 util/__init__.py:341-375
+ *   snpmi_bed_read_standardize_* Bed.read() + SnpData.standardize() fused  snpreader/snpreader.py:606-621
+ *   snpmi_grm_bed_{f32,f64}      SnpReader._read_kernel block loop         snpreader/snpreader.py:623-668
+ *   snpmi_grm_dense_{f32,f64}    SnpData._read_kernel (val.dot(val.T))     snpreader/snpdata.py:190-214
+ *   snpmi_diag_k_to_n_{f32,f64}  DiagKtoN._standardize_kernel              standardizer/diag_K_to_N.py:54-64
+ *
+ * Conventions (mirroring bed-reader's):
+ *   - The caller owns every host buffer; outputs are written in place.  Index arrays are
+ *     NumPy `uintp` (== uint64_t on LP64).  A NULL index array means "all, in order".
+ *   - `order_c` = 1 for C order (row-major, SNP fastest), 0 for F order (iid fastest).
+ *   - `stats` arrays are C-order [n_sid][2] = (mean, std) in the value dtype.
+ *   - Missing values decode to NaN (float) or -127 (int8).  count_a1 selects the A1 LUT
+ *     {2,NaN,1,0} instead of {0,NaN,1,2}.
+ *   - Every function returns 0 on success or one of the SNPMI_E_* codes; the message of
+ *     the calling thread's last failure is available from snpmi_last_error().
+ *   - `num_threads` sizes the host-side gather pool only; all arithmetic runs on the GPU.
+ *     There is no CPU fallback: without a HIP device every compute entry point fails
+ *     with SNPMI_E_HIP.
+ *   - K outputs are n_out x n_out, symmetric; order_c selects the layout of non-square
+ *     subsets produced by snpmi_kernel_subset_*.
+ */
+#ifndef SNPMI_H
+#define SNPMI_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SNPMI_OK 0
+#define SNPMI_E_ARG 1     /* bad argument (shape, dtype, order, NULL pointer)        */
+#define SNPMI_E_INDEX 2   /* iid/sid index out of range                              */
+#define SNPMI_E_FORMAT 3  /* not a SNP-major .bed file, or size mismatch             */
+#define SNPMI_E_IO 4      /* open/read/mmap failure                                  */
+#define SNPMI_E_HIP 5     /* HIP runtime error (includes "no device")                */
+#define SNPMI_E_NOMEM 6   /* device or pinned allocation failed                      */
+#define SNPMI_E_RCCL 7    /* RCCL error                                              */
+
+/* standardizer kinds (standardizer/{identity,unit,beta}.py) */
+#define SNPMI_STD_NONE 0  /* raw values (Identity)                                   */
+#define SNPMI_STD_UNIT 1  /* (x - mean) / std, NaN -> 0                              */
+#define SNPMI_STD_BETA 2  /* (x - mean) * BetaPDF(maf; a, b), NaN -> 0               */
+
+/* dtypes for the device-resident API */
+#define SNPMI_DT_F32 0
+#define SNPMI_DT_F64 1
+#define SNPMI_DT_I8 2
+
+/* ---------------------------------------------------------------- runtime */
+const char* snpmi_last_error(void);
+int snpmi_version(void);
+int snpmi_device_count(int* count);
+int snpmi_set_device(int device);            /* device used by later calls of this thread */
+int snpmi_get_device(int* device);
+int snpmi_release_cache(void);               /* free cached device/pinned scratch          */
+int snpmi_device_info(int device, char* name, size_t name_len, uint64_t* total_mem, int* cu_count);
+
+/* ---------------------------------------------------------------- BED reading (bed-reader read_*) */
+int snpmi_bed_check(const char* path, uint64_t n_iid, uint64_t n_sid);
+int snpmi_bed_read_f32(const char* path, uint64_t n_iid, uint64_t n_sid, int count_a1,
+                       const uint64_t* iid_idx, uint64_t n_out_iid, const uint64_t* sid_idx,
+                       uint64_t n_out_sid, int order_c, float* out, int num_threads);
+int snpmi_bed_read_f64(const char* path, uint64_t n_iid, uint64_t n_sid, int count_a1,
+                       const uint64_t* iid_idx, uint64_t n_out_iid, const uint64_t* sid_idx,
+                       uint64_t n_out_sid, int order_c, double* out, int num_threads);
+int snpmi_bed_read_i8(const char* path, uint64_t n_iid, uint64_t n_sid, int count_a1,
+                      const uint64_t* iid_idx, uint64_t n_out_iid, const uint64_t* sid_idx,
+                      uint64_t n_out_sid, int order_c, int8_t* out, int num_threads);
+
+/* ---------------------------------------------------------------- standardize (bed-reader standardize_*) */
+int snpmi_standardize_f32(float* val, uint64_t rows, uint64_t cols, int order_c, int is_beta,
+                          double a, double b, int apply_in_place, int use_stats, float* stats,
+                          int num_threads);
+int snpmi_standardize_f64(double* val, uint64_t rows, uint64_t cols, int order_c, int is_beta,
+                          double a, double b, int apply_in_place, int use_stats, double* stats,
+                          int num_threads);
+
+/* ---------------------------------------------------------------- subset (bed-reader subset_*) */
+/* out[i,j,q] = val[row_idx[i], col_idx[j], q]; val is rows x cols x k in in_order_c. */
+int snpmi_subset_f64_f64(const double* val, uint64_t rows, uint64_t cols, uint64_t k, int in_order_c,
+                         const uint64_t* row_idx, uint64_t n_rows, const uint64_t* col_idx,
+                         uint64_t n_cols, int out_order_c, double* out, int num_threads);
+int snpmi_subset_f32_f64(const float* val, uint64_t rows, uint64_t cols, uint64_t k, int in_order_c,
+                         const uint64_t* row_idx, uint64_t n_rows, const uint64_t* col_idx,
+                         uint64_t n_cols, int out_order_c, double* out, int num_threads);
+int snpmi_subset_f32_f32(const float* val, uint64_t rows, uint64_t cols, uint64_t k, int in_order_c,
+                         const uint64_t* row_idx, uint64_t n_rows, const uint64_t* col_idx,
+                         uint64_t n_cols, int out_order_c, float* out, int num_threads);
+
+/* ---------------------------------------------------------------- fused read + standardize */
+int snpmi_bed_read_standardize_f32(const char* path, uint64_t n_iid, uint64_t n_sid, int count_a1,
+                                   const uint64_t* iid_idx, uint64_t n_out_iid, const uint64_t* sid_idx,
+                                   uint64_t n_out_sid, int order_c, int std_kind, double a, double b,
+                                   int use_stats, float* stats, float* out, int num_threads);
+int snpmi_bed_read_standardize_f64(const char* path, uint64_t n_iid, uint64_t n_sid, int count_a1,
+                                   const uint64_t* iid_idx, uint64_t n_out_iid, const uint64_t* sid_idx,
+                                   uint64_t n_out_sid, int order_c, int std_kind, double a, double b,
+                                   int use_stats, double* stats, double* out, int num_threads);
+
+/* ---------------------------------------------------------------- GRM (SnpKernel) */
+/* K_out: n_out_iid x n_out_iid (symmetric).  stats: [n_out_sid][2] in/out (in if use_stats).
+ * diag_k_to_n != 0 additionally applies DiagKtoN on the device and returns the factor. */
+int snpmi_grm_bed_f32(const char* path, uint64_t n_iid, uint64_t n_sid, int count_a1,
+                      const uint64_t* iid_idx, uint64_t n_out_iid, const uint64_t* sid_idx,
+                      uint64_t n_out_sid, int std_kind, double a, double b, int use_stats,
+                      float* stats, int diag_k_to_n, double* factor, float* K_out, int num_threads);
+int snpmi_grm_bed_f64(const char* path, uint64_t n_iid, uint64_t n_sid, int count_a1,
+                      const uint64_t* iid_idx, uint64_t n_out_iid, const uint64_t* sid_idx,
+                      uint64_t n_out_sid, int std_kind, double a, double b, int use_stats,
+                      double* stats, int diag_k_to_n, double* factor, double* K_out, int num_threads);
+int snpmi_grm_dense_f32(const float* val, uint64_t rows, uint64_t cols, int order_c, int std_kind,
+                        double a, double b, int use_stats, float* stats, int diag_k_to_n,
+                        double* factor, float* K_out);
+int snpmi_grm_dense_f64(const double* val, uint64_t rows, uint64_t cols, int order_c, int std_kind,
+                        double a, double b, int use_stats, double* stats, int diag_k_to_n,
+                        double* factor, double* K_out);
+int snpmi_diag_k_to_n_f32(float* K, uint64_t n, double* factor);
+int snpmi_diag_k_to_n_f64(double* K, uint64_t n, double* factor);
+
+/* ---------------------------------------------------------------- device-resident API
+ * Buffers below are device pointers from snpmi_dev_alloc; work is enqueued on the
+ * library's per-device stream (use snpmi_stream_sync / events).  Packed BED data on the
+ * device is [n_sid][pitch] bytes with pitch % 64 == 0 (snpmi_packed_pitch). */
+uint64_t snpmi_packed_pitch(uint64_t n_iid);
+int snpmi_dev_alloc(void** ptr, uint64_t bytes);
+int snpmi_dev_free(void* ptr);
+int snpmi_dev_memset(void* ptr, int value, uint64_t bytes);
+int snpmi_memcpy_h2d(void* dst, const void* src, uint64_t bytes);
+int snpmi_memcpy_d2h(void* dst, const void* src, uint64_t bytes);
+int snpmi_stream_sync(void);
+int snpmi_event_create(void** ev);
+int snpmi_event_destroy(void* ev);
+int snpmi_event_record(void* ev);
+int snpmi_event_elapsed_ms(void* start, void* stop, float* ms);
+
+/* counter-based synthetic genotypes (SnpGen MAF curve, snpreader/snpgen.py:140-151) */
+int snpmi_dev_synth_bed(uint8_t* packed, uint64_t pitch, uint64_t n_iid, uint64_t sid0, uint64_t n_sid,
+                        uint64_t seed, double miss_rate, const double* maf_x, const double* maf_cdf,
+                        int n_pts);
+/* per-SNP code counts -> stats [n_sid][2] (dtype) and value LUT [n_sid][4] (dtype) */
+int snpmi_dev_snp_stats(const uint8_t* packed, uint64_t pitch, uint64_t n_iid, uint64_t n_sid,
+                        int count_a1, int std_kind, double a, double b, int use_stats, int dtype,
+                        void* stats, void* lut);
+/* packed + LUT -> values, column j at out + j*ld (F) or row i at out + i*ld (C) */
+int snpmi_dev_decode(const uint8_t* packed, uint64_t pitch, uint64_t n_iid, uint64_t n_sid,
+                     const void* lut, int dtype, int order_c, void* out, uint64_t ld);
+/* iid gather: dst column j = src column j restricted to iids idx[0..n_out) */
+int snpmi_dev_repack(const uint8_t* src, uint64_t src_pitch, uint64_t n_src_iid, const uint64_t* idx,
+                     uint64_t n_out_iid, uint64_t n_sid, uint8_t* dst, uint64_t dst_pitch);
+/* GRM tiles: K_tiles holds the upper-triangle 128x128 tiles of an n x n K
+ * (snpmi_grm_tile_bytes); accumulate != 0 adds to it. */
+uint64_t snpmi_grm_tile_bytes(uint64_t n_iid, int dtype);
+int snpmi_dev_syrk_packed(const uint8_t* packed, uint64_t pitch, uint64_t n_iid, uint64_t n_sid,
+                          const void* lut, int dtype, void* K_tiles, int accumulate);
+int snpmi_dev_syrk_dense(const void* Z, uint64_t ldz, uint64_t n_iid, uint64_t n_sid, int dtype,
+                         void* K_tiles, int accumulate);
+/* tiles -> K[ri[r], ci[c]] (ri/ci NULL = identity), scaled by `scale` */
+int snpmi_dev_grm_extract(const void* K_tiles, uint64_t n_iid, int dtype, const uint64_t* ri, uint64_t nr,
+                          const uint64_t* ci, uint64_t nc, int order_c, double scale, void* out);
+int snpmi_dev_grm_trace(const void* K_tiles, uint64_t n_iid, int dtype, double* trace);
+
+/* ---------------------------------------------------------------- RCCL (one process per GPU) */
+int snpmi_rccl_unique_id(uint8_t* id, uint64_t id_len);   /* id_len >= 128 */
+int snpmi_rccl_init(int nranks, int rank, const uint8_t* id, uint64_t id_len);
+int snpmi_rccl_allreduce_sum(void* buf, uint64_t count, int dtype);
+int snpmi_rccl_destroy(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SNPMI_H */

@@ -1,0 +1,765 @@
+// libsnpmi C ABI (include/snpmi.h): host orchestration of the BED -> GRM path on one GPU.
+//
+// Data flow of every file-backed entry point (one SNP chunk at a time):
+//   mmap(.bed) --gather selected columns, pitch-padded--> pinned host buffer
+//     --H2D--> packed codes in HBM --[k_repack: iid subset]--> k_snp_stats (stats + LUT)
+//     --> k_decode_f/c (values)  or  MFMA SYRK into upper-triangle K tiles
+//     --> D2H into the caller's NumPy buffer.
+// The packed codes are 16x (f32) / 32x (f64) smaller than the values, so only packed bytes
+// cross PCIe on the way in.
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cmath>
+#include <cstdlib>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include "snpmi_internal.hpp"
+
+namespace snpmi {
+
+// ====================================================================== errors / devices
+static thread_local std::string g_last_error;
+void set_last_error(const std::string& msg) { g_last_error = msg; }
+
+static std::mutex g_dev_mutex;
+static std::vector<Device*> g_devices;
+static thread_local int g_cur_dev = -1;
+
+static int default_device() {
+    const char* e = std::getenv("PST_DEVICE");
+    return e ? std::atoi(e) : 0;
+}
+
+static int num_devices() {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+Device& device() {
+    if (g_cur_dev < 0) g_cur_dev = default_device();
+    std::lock_guard<std::mutex> lk(g_dev_mutex);
+    const int n = num_devices();
+    SNPMI_REQUIRE(n > 0, SNPMI_E_HIP, "no HIP device available (libsnpmi has no CPU fallback)");
+    SNPMI_REQUIRE(g_cur_dev < n, SNPMI_E_ARG, "device index out of range");
+    if ((int)g_devices.size() < n) g_devices.resize(n, nullptr);
+    Device*& d = g_devices[g_cur_dev];
+    SNPMI_HIP(hipSetDevice(g_cur_dev));
+    if (!d) {
+        d = new Device();
+        d->id = g_cur_dev;
+        SNPMI_HIP(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
+        hipDeviceProp_t p;
+        SNPMI_HIP(hipGetDeviceProperties(&p, g_cur_dev));
+        d->cu_count = p.multiProcessorCount;
+    }
+    return *d;
+}
+
+hipStream_t stream() { return device().stream; }
+
+void* Device::get(Slot s, size_t bytes) {
+    if (bytes == 0) bytes = 256;
+    if (cap[s] < bytes) {
+        if (buf[s]) SNPMI_HIP(hipFree(buf[s]));
+        buf[s] = nullptr;
+        cap[s] = 0;
+        size_t want = round_up(bytes, 1 << 20);
+        if (hipMalloc(&buf[s], want) != hipSuccess) {
+            (void)hipGetLastError();
+            buf[s] = nullptr;
+            throw Error(SNPMI_E_NOMEM, "hipMalloc of " + std::to_string(want) + " bytes failed");
+        }
+        cap[s] = want;
+    }
+    return buf[s];
+}
+
+void Device::release() {
+    for (int s = 0; s < S_NUM; s++) {
+        if (buf[s]) (void)hipFree(buf[s]);
+        buf[s] = nullptr;
+        cap[s] = 0;
+    }
+}
+
+// pinned staging (two slots so a chunk can be gathered while the previous one uploads)
+static std::mutex g_pin_mutex;
+static void* g_pin[4] = {};
+static size_t g_pin_cap[4] = {};
+
+void* pinned(int slot, size_t bytes) {
+    std::lock_guard<std::mutex> lk(g_pin_mutex);
+    if (g_pin_cap[slot] < bytes) {
+        if (g_pin[slot]) (void)hipHostFree(g_pin[slot]);
+        g_pin[slot] = nullptr;
+        g_pin_cap[slot] = 0;
+        size_t want = round_up(bytes, 1 << 20);
+        if (hipHostMalloc(&g_pin[slot], want, hipHostMallocDefault) != hipSuccess) {
+            (void)hipGetLastError();
+            throw Error(SNPMI_E_NOMEM, "pinned allocation failed");
+        }
+        g_pin_cap[slot] = want;
+    }
+    return g_pin[slot];
+}
+
+void release_pinned() {
+    std::lock_guard<std::mutex> lk(g_pin_mutex);
+    for (int s = 0; s < 4; s++) {
+        if (g_pin[s]) (void)hipHostFree(g_pin[s]);
+        g_pin[s] = nullptr;
+        g_pin_cap[s] = 0;
+    }
+}
+
+// one API call at a time per process: scratch slots and the stream are shared
+static std::recursive_mutex g_call_mutex;
+
+// ====================================================================== host helpers
+static int resolve_threads(int num_threads) {
+    if (num_threads > 0) return std::min(num_threads, 64);
+    unsigned hc = std::thread::hardware_concurrency();
+    return (int)std::max(1u, std::min(hc, 16u));
+}
+
+template <class F>
+static void parallel_for(uint64_t n, int nthreads, F&& fn) {
+    if (n == 0) return;
+    nthreads = (int)std::min<uint64_t>((uint64_t)nthreads, n);
+    if (nthreads <= 1 || n < 64) {
+        for (uint64_t i = 0; i < n; i++) fn(i);
+        return;
+    }
+    std::atomic<uint64_t> next(0);
+    std::vector<std::thread> th;
+    th.reserve(nthreads);
+    for (int t = 0; t < nthreads; t++)
+        th.emplace_back([&] {
+            for (;;) {
+                uint64_t s = next.fetch_add(64);
+                if (s >= n) break;
+                uint64_t e = std::min(n, s + 64);
+                for (uint64_t i = s; i < e; i++) fn(i);
+            }
+        });
+    for (auto& t : th) t.join();
+}
+
+struct BedMap {
+    int fd = -1;
+    const uint8_t* base = nullptr;
+    size_t size = 0;
+    uint64_t bpc = 0;
+    ~BedMap() {
+        if (base) munmap((void*)base, size);
+        if (fd >= 0) close(fd);
+    }
+    const uint8_t* column(uint64_t s) const { return base + 3 + s * bpc; }
+};
+
+// bed-reader's open_bed format check (magic 6C 1B 01 = SNP-major) + size check.
+static void open_bed(BedMap& m, const char* path, uint64_t n_iid, uint64_t n_sid) {
+    SNPMI_REQUIRE(path != nullptr, SNPMI_E_ARG, "path is NULL");
+    m.fd = open(path, O_RDONLY);
+    SNPMI_REQUIRE(m.fd >= 0, SNPMI_E_IO, std::string("cannot open ") + path);
+    struct stat st;
+    SNPMI_REQUIRE(fstat(m.fd, &st) == 0, SNPMI_E_IO, std::string("cannot stat ") + path);
+    m.size = (size_t)st.st_size;
+    m.bpc = ceil_div(n_iid, 4);
+    SNPMI_REQUIRE(m.size >= 3, SNPMI_E_FORMAT, std::string("file too short to be a .bed file: ") + path);
+    void* p = mmap(nullptr, m.size, PROT_READ, MAP_SHARED, m.fd, 0);
+    SNPMI_REQUIRE(p != MAP_FAILED, SNPMI_E_IO, std::string("mmap failed: ") + path);
+    m.base = (const uint8_t*)p;
+    SNPMI_REQUIRE(m.base[0] == 0x6C && m.base[1] == 0x1B, SNPMI_E_FORMAT,
+                  std::string("not a PLINK .bed file (bad magic): ") + path);
+    SNPMI_REQUIRE(m.base[2] == 0x01, SNPMI_E_FORMAT,
+                  std::string("only SNP-major .bed files are supported: ") + path);
+    SNPMI_REQUIRE(m.size == 3 + n_sid * m.bpc, SNPMI_E_FORMAT,
+                  std::string(".bed size does not match .fam/.bim counts: ") + path);
+    (void)madvise(p, m.size, MADV_SEQUENTIAL);
+}
+
+static void check_index(const uint64_t* idx, uint64_t n, uint64_t bound, const char* what) {
+    if (!idx) return;
+    for (uint64_t i = 0; i < n; i++)
+        SNPMI_REQUIRE(idx[i] < bound, SNPMI_E_INDEX,
+                      std::string(what) + " index " + std::to_string(idx[i]) + " out of range (count " +
+                          std::to_string(bound) + ")");
+}
+
+static bool is_identity(const uint64_t* idx, uint64_t n, uint64_t bound) {
+    if (!idx) return true;
+    if (n != bound) return false;
+    for (uint64_t i = 0; i < n; i++)
+        if (idx[i] != i) return false;
+    return true;
+}
+
+// Gather SNP columns [c0, c0+cnt) of the selection into `dst` with `pitch` bytes each.
+static void gather_columns(const BedMap& m, const uint64_t* sid_idx, uint64_t c0, uint64_t cnt, uint64_t pitch,
+                           uint8_t* dst, int nthreads) {
+    parallel_for(cnt, nthreads, [&](uint64_t j) {
+        const uint64_t s = sid_idx ? sid_idx[c0 + j] : c0 + j;
+        uint8_t* d = dst + j * pitch;
+        std::memcpy(d, m.column(s), m.bpc);
+        if (pitch > m.bpc) std::memset(d + m.bpc, 0, pitch - m.bpc);
+    });
+}
+
+// Device-side iid selection state for one call.
+struct IidPlan {
+    uint64_t n_in, n_out, pitch_in, pitch_out;
+    bool repack;
+    uint64_t* idx_dev = nullptr;
+};
+
+static IidPlan plan_iids(Device& d, const uint64_t* iid_idx, uint64_t n_iid, uint64_t n_out) {
+    IidPlan p;
+    p.n_in = n_iid;
+    p.n_out = iid_idx ? n_out : n_iid;
+    p.pitch_in = packed_pitch(n_iid);
+    p.pitch_out = packed_pitch(p.n_out);
+    p.repack = !is_identity(iid_idx, p.n_out, n_iid);
+    if (p.repack && p.n_out) {
+        p.idx_dev = (uint64_t*)d.get(Device::S_IDX, p.n_out * 8);
+        SNPMI_HIP(hipMemcpyAsync(p.idx_dev, iid_idx, p.n_out * 8, hipMemcpyHostToDevice, d.stream));
+    }
+    return p;
+}
+
+// Upload SNP chunk [c0, c0+cnt) and return the device packed buffer for the selected iids.
+static const uint8_t* stage_chunk(Device& d, const BedMap& m, const uint64_t* sid_idx, uint64_t c0, uint64_t cnt,
+                                  const IidPlan& p, int nthreads) {
+    uint8_t* host = (uint8_t*)pinned(0, cnt * p.pitch_in);
+    SNPMI_HIP(hipStreamSynchronize(d.stream));  // previous chunk's upload has consumed `host`
+    gather_columns(m, sid_idx, c0, cnt, p.pitch_in, host, nthreads);
+    uint8_t* dev = (uint8_t*)d.get(Device::S_PACKED, cnt * p.pitch_in);
+    SNPMI_HIP(hipMemcpyAsync(dev, host, cnt * p.pitch_in, hipMemcpyHostToDevice, d.stream));
+    if (!p.repack) return dev;
+    uint8_t* dev2 = (uint8_t*)d.get(Device::S_PACKED2, cnt * p.pitch_out);
+    launch_repack(dev, p.pitch_in, p.n_in, p.idx_dev, p.n_out, cnt, dev2, p.pitch_out, nullptr, d.stream);
+    return dev2;
+}
+
+template <typename T>
+struct DT;
+template <>
+struct DT<float> {
+    static constexpr int v = SNPMI_DT_F32;
+};
+template <>
+struct DT<double> {
+    static constexpr int v = SNPMI_DT_F64;
+};
+template <>
+struct DT<int8_t> {
+    static constexpr int v = SNPMI_DT_I8;
+};
+
+static uint64_t chunk_snps(uint64_t per_snp_bytes, uint64_t budget = 1ull << 30) {
+    uint64_t c = std::max<uint64_t>(1, budget / std::max<uint64_t>(per_snp_bytes, 1));
+    return std::min<uint64_t>(c, 1ull << 16);
+}
+
+// ====================================================================== BED read (+ standardize)
+template <typename T>
+static void bed_read_impl(const char* path, uint64_t n_iid, uint64_t n_sid, int count_a1, const uint64_t* iid_idx,
+                          uint64_t n_out_iid, const uint64_t* sid_idx, uint64_t n_out_sid, int order_c, int std_kind,
+                          double a, double b, int use_stats, T* stats, T* out, int num_threads) {
+    std::lock_guard<std::recursive_mutex> lk(g_call_mutex);
+    SNPMI_REQUIRE(out != nullptr || (n_out_iid == 0 || n_out_sid == 0), SNPMI_E_ARG, "out is NULL");
+    BedMap m;
+    open_bed(m, path, n_iid, n_sid);
+    const uint64_t n_out = iid_idx ? n_out_iid : n_iid;
+    const uint64_t m_out = sid_idx ? n_out_sid : n_sid;
+    check_index(iid_idx, n_out, n_iid, "iid");
+    check_index(sid_idx, m_out, n_sid, "sid");
+    if (m_out == 0) return;
+    Device& d = device();
+    const int nthreads = resolve_threads(num_threads);
+    IidPlan p = plan_iids(d, iid_idx, n_iid, n_out);
+    const int dt = DT<T>::v;
+    const uint64_t ldF = round_up(std::max<uint64_t>(n_out, 1), 16);
+    const uint64_t C = chunk_snps(p.pitch_in + p.pitch_out + ldF * sizeof(T));
+    for (uint64_t c0 = 0; c0 < m_out; c0 += C) {
+        const uint64_t cnt = std::min(C, m_out - c0);
+        const uint8_t* packed = stage_chunk(d, m, sid_idx, c0, cnt, p, nthreads);
+        T* lut = (T*)d.get(Device::S_LUT, cnt * 4 * sizeof(T));
+        T* st_dev = (T*)d.get(Device::S_STATS, cnt * 2 * sizeof(T));
+        if (std_kind != SNPMI_STD_NONE && use_stats)
+            SNPMI_HIP(hipMemcpyAsync(st_dev, stats + 2 * c0, cnt * 2 * sizeof(T), hipMemcpyHostToDevice, d.stream));
+        launch_snp_stats(packed, p.pitch_out, n_out, cnt, count_a1, std_kind, a, b, use_stats, dt, st_dev, lut,
+                         d.stream);
+        if (n_out > 0) {
+            if (!order_c) {
+                T* dev_out = (T*)d.get(Device::S_OUT, cnt * ldF * sizeof(T));
+                launch_decode(packed, p.pitch_out, n_out, cnt, lut, dt, 0, dev_out, ldF, d.stream);
+                SNPMI_HIP(hipMemcpy2DAsync(out + c0 * n_out, n_out * sizeof(T), dev_out, ldF * sizeof(T),
+                                           n_out * sizeof(T), cnt, hipMemcpyDeviceToHost, d.stream));
+            } else {
+                T* dev_out = (T*)d.get(Device::S_OUT, cnt * n_out * sizeof(T));
+                launch_decode(packed, p.pitch_out, n_out, cnt, lut, dt, 1, dev_out, cnt, d.stream);
+                SNPMI_HIP(hipMemcpy2DAsync(out + c0, m_out * sizeof(T), dev_out, cnt * sizeof(T), cnt * sizeof(T),
+                                           n_out, hipMemcpyDeviceToHost, d.stream));
+            }
+        }
+        if (std_kind != SNPMI_STD_NONE && !use_stats)
+            SNPMI_HIP(hipMemcpyAsync(stats + 2 * c0, st_dev, cnt * 2 * sizeof(T), hipMemcpyDeviceToHost, d.stream));
+        SNPMI_HIP(hipStreamSynchronize(d.stream));
+    }
+}
+
+// ====================================================================== dense standardize / subset
+template <typename T>
+static void standardize_impl(T* val, uint64_t rows, uint64_t cols, int order_c, int is_beta, double a, double b,
+                             int apply_in_place, int use_stats, T* stats) {
+    std::lock_guard<std::recursive_mutex> lk(g_call_mutex);
+    SNPMI_REQUIRE(stats != nullptr, SNPMI_E_ARG, "stats is NULL");
+    if (cols == 0) return;
+    Device& d = device();
+    const size_t bytes = rows * cols * sizeof(T);
+    T* dv = (T*)d.get(Device::S_DENSE, bytes);
+    T* ds = (T*)d.get(Device::S_STATS, cols * 2 * sizeof(T));
+    SNPMI_HIP(hipMemcpyAsync(dv, val, bytes, hipMemcpyHostToDevice, d.stream));
+    if (use_stats) SNPMI_HIP(hipMemcpyAsync(ds, stats, cols * 2 * sizeof(T), hipMemcpyHostToDevice, d.stream));
+    launch_dense_standardize(dv, rows, cols, order_c ? cols : rows, order_c, DT<T>::v,
+                             is_beta ? SNPMI_STD_BETA : SNPMI_STD_UNIT, a, b, use_stats, ds, d.stream);
+    if (apply_in_place) SNPMI_HIP(hipMemcpyAsync(val, dv, bytes, hipMemcpyDeviceToHost, d.stream));
+    if (!use_stats) SNPMI_HIP(hipMemcpyAsync(stats, ds, cols * 2 * sizeof(T), hipMemcpyDeviceToHost, d.stream));
+    SNPMI_HIP(hipStreamSynchronize(d.stream));
+}
+
+template <typename S, typename D>
+static void subset_impl(const S* val, uint64_t rows, uint64_t cols, uint64_t k, int in_c, const uint64_t* ri,
+                        uint64_t nr, const uint64_t* ci, uint64_t nc, int out_c, D* out) {
+    std::lock_guard<std::recursive_mutex> lk(g_call_mutex);
+    SNPMI_REQUIRE(k >= 1, SNPMI_E_ARG, "k must be >= 1");
+    SNPMI_REQUIRE(ri && ci, SNPMI_E_ARG, "subset needs explicit row and column indices");
+    check_index(ri, nr, rows, "row");
+    check_index(ci, nc, cols, "col");
+    if (nr * nc == 0) return;
+    Device& d = device();
+    const size_t in_bytes = rows * cols * k * sizeof(S);
+    S* dv = (S*)d.get(Device::S_DENSE, in_bytes);
+    uint64_t* dri = (uint64_t*)d.get(Device::S_IDX, nr * 8);
+    uint64_t* dci = (uint64_t*)d.get(Device::S_IDX2, nc * 8);
+    D* dout = (D*)d.get(Device::S_OUT, nr * nc * k * sizeof(D));
+    SNPMI_HIP(hipMemcpyAsync(dv, val, in_bytes, hipMemcpyHostToDevice, d.stream));
+    SNPMI_HIP(hipMemcpyAsync(dri, ri, nr * 8, hipMemcpyHostToDevice, d.stream));
+    SNPMI_HIP(hipMemcpyAsync(dci, ci, nc * 8, hipMemcpyHostToDevice, d.stream));
+    launch_subset(dv, DT<S>::v, rows, cols, k, in_c, dri, nr, dci, nc, out_c, dout, DT<D>::v, d.stream);
+    SNPMI_HIP(hipMemcpyAsync(out, dout, nr * nc * k * sizeof(D), hipMemcpyDeviceToHost, d.stream));
+    SNPMI_HIP(hipStreamSynchronize(d.stream));
+}
+
+// ====================================================================== GRM
+// Finish a GRM held as tiles on the device: optional DiagKtoN, then K (n x n) to the host,
+// extracted in row blocks so the device never needs a second full-size K.
+template <typename T>
+static void grm_finish(Device& d, const T* tiles, uint64_t n, int diag_k_to_n, double* factor, T* K_out) {
+    double scale = 1.0;
+    if (diag_k_to_n) {
+        double* tr = (double*)d.get(Device::S_RED, 64);
+        launch_grm_trace(tiles, n, DT<T>::v, tr, d.stream);
+        double trace = 0;
+        SNPMI_HIP(hipMemcpyAsync(&trace, tr, 8, hipMemcpyDeviceToHost, d.stream));
+        SNPMI_HIP(hipStreamSynchronize(d.stream));
+        const double f = (double)n / trace;
+        if (factor) *factor = f;
+        if (std::fabs(f - 1.0) > 1e-15) scale = f;  // diag_K_to_N.py:56-59
+    }
+    if (n == 0) return;
+    const uint64_t rows_per = std::max<uint64_t>(1, std::min<uint64_t>(n, (1ull << 30) / (n * sizeof(T))));
+    std::vector<uint64_t> ri(rows_per);
+    uint64_t* dri = (uint64_t*)d.get(Device::S_IDX2, rows_per * 8);
+    for (uint64_t r0 = 0; r0 < n; r0 += rows_per) {
+        const uint64_t nr = std::min(rows_per, n - r0);
+        for (uint64_t r = 0; r < nr; r++) ri[r] = r0 + r;
+        T* dk = (T*)d.get(Device::S_K, nr * n * sizeof(T));
+        SNPMI_HIP(hipStreamSynchronize(d.stream));  // ri reused across blocks
+        SNPMI_HIP(hipMemcpyAsync(dri, ri.data(), nr * 8, hipMemcpyHostToDevice, d.stream));
+        launch_grm_extract(tiles, n, DT<T>::v, dri, nr, nullptr, n, 1, scale, dk, d.stream);
+        SNPMI_HIP(hipMemcpyAsync(K_out + r0 * n, dk, nr * n * sizeof(T), hipMemcpyDeviceToHost, d.stream));
+    }
+    SNPMI_HIP(hipStreamSynchronize(d.stream));
+}
+
+template <typename T>
+static void grm_bed_impl(const char* path, uint64_t n_iid, uint64_t n_sid, int count_a1, const uint64_t* iid_idx,
+                         uint64_t n_out_iid, const uint64_t* sid_idx, uint64_t n_out_sid, int std_kind, double a,
+                         double b, int use_stats, T* stats, int diag_k_to_n, double* factor, T* K_out,
+                         int num_threads) {
+    std::lock_guard<std::recursive_mutex> lk(g_call_mutex);
+    BedMap m;
+    open_bed(m, path, n_iid, n_sid);
+    const uint64_t n_out = iid_idx ? n_out_iid : n_iid;
+    const uint64_t m_out = sid_idx ? n_out_sid : n_sid;
+    check_index(iid_idx, n_out, n_iid, "iid");
+    check_index(sid_idx, m_out, n_sid, "sid");
+    SNPMI_REQUIRE(K_out != nullptr || n_out == 0, SNPMI_E_ARG, "K_out is NULL");
+    SNPMI_REQUIRE(stats != nullptr || std_kind == SNPMI_STD_NONE || m_out == 0, SNPMI_E_ARG, "stats is NULL");
+    Device& d = device();
+    const int nthreads = resolve_threads(num_threads);
+    const int dt = DT<T>::v;
+    IidPlan p = plan_iids(d, iid_idx, n_iid, n_out);
+    const uint64_t tile_bytes = n_tiles_upper(n_out) * kTile * kTile * sizeof(T);
+    T* tiles = (T*)d.get(Device::S_TILES, tile_bytes);
+    if (m_out == 0 || n_out == 0) SNPMI_HIP(hipMemsetAsync(tiles, 0, tile_bytes, d.stream));
+    const uint64_t C = chunk_snps(p.pitch_in + p.pitch_out, 1ull << 30);
+    for (uint64_t c0 = 0; c0 < m_out && n_out > 0; c0 += C) {
+        const uint64_t cnt = std::min(C, m_out - c0);
+        const uint8_t* packed = stage_chunk(d, m, sid_idx, c0, cnt, p, nthreads);
+        T* lut = (T*)d.get(Device::S_LUT, cnt * 4 * sizeof(T));
+        T* st_dev = (T*)d.get(Device::S_STATS, cnt * 2 * sizeof(T));
+        if (std_kind != SNPMI_STD_NONE && use_stats)
+            SNPMI_HIP(hipMemcpyAsync(st_dev, stats + 2 * c0, cnt * 2 * sizeof(T), hipMemcpyHostToDevice, d.stream));
+        launch_snp_stats(packed, p.pitch_out, n_out, cnt, count_a1, std_kind, a, b, use_stats, dt, st_dev, lut,
+                         d.stream);
+        launch_syrk_packed(packed, p.pitch_out, n_out, cnt, lut, dt, tiles, c0 > 0, d.stream);
+        if (std_kind != SNPMI_STD_NONE && !use_stats)
+            SNPMI_HIP(hipMemcpyAsync(stats + 2 * c0, st_dev, cnt * 2 * sizeof(T), hipMemcpyDeviceToHost, d.stream));
+    }
+    if (n_out == 0 && std_kind != SNPMI_STD_NONE && !use_stats) {
+        for (uint64_t j = 0; j < m_out; j++) stats[2 * j] = stats[2 * j + 1] = (T)NAN;
+    }
+    grm_finish(d, tiles, n_out, diag_k_to_n, factor, K_out);
+}
+
+template <typename T>
+static void grm_dense_impl(const T* val, uint64_t rows, uint64_t cols, int order_c, int std_kind, double a, double b,
+                           int use_stats, T* stats, int diag_k_to_n, double* factor, T* K_out) {
+    std::lock_guard<std::recursive_mutex> lk(g_call_mutex);
+    SNPMI_REQUIRE(K_out != nullptr || rows == 0, SNPMI_E_ARG, "K_out is NULL");
+    Device& d = device();
+    const int dt = DT<T>::v;
+    const uint64_t ldz = n_tiles_1d(std::max<uint64_t>(rows, 1)) * kTile;
+    T* Z = (T*)d.get(Device::S_DENSE, ldz * std::max<uint64_t>(cols, 1) * sizeof(T));
+    if (cols > 0 && rows > 0) {
+        if (!order_c) {
+            SNPMI_HIP(hipMemcpy2DAsync(Z, ldz * sizeof(T), val, rows * sizeof(T), rows * sizeof(T), cols,
+                                       hipMemcpyHostToDevice, d.stream));
+        } else {
+            T* Zc = (T*)d.get(Device::S_DENSE2, rows * cols * sizeof(T));
+            SNPMI_HIP(hipMemcpyAsync(Zc, val, rows * cols * sizeof(T), hipMemcpyHostToDevice, d.stream));
+            launch_transpose_to_f(Zc, rows, cols, dt, Z, ldz, d.stream);
+        }
+    }
+    if (std_kind != SNPMI_STD_NONE && cols > 0) {
+        T* ds = (T*)d.get(Device::S_STATS, cols * 2 * sizeof(T));
+        if (use_stats) SNPMI_HIP(hipMemcpyAsync(ds, stats, cols * 2 * sizeof(T), hipMemcpyHostToDevice, d.stream));
+        launch_dense_standardize(Z, rows, cols, ldz, 0, dt, std_kind, a, b, use_stats, ds, d.stream);
+        if (!use_stats) SNPMI_HIP(hipMemcpyAsync(stats, ds, cols * 2 * sizeof(T), hipMemcpyDeviceToHost, d.stream));
+    }
+    const uint64_t tile_bytes = n_tiles_upper(rows) * kTile * kTile * sizeof(T);
+    T* tiles = (T*)d.get(Device::S_TILES, tile_bytes);
+    if (rows > 0) launch_syrk_dense(Z, ldz, rows, cols, dt, tiles, 0, d.stream);
+    grm_finish(d, tiles, rows, diag_k_to_n, factor, K_out);
+}
+
+template <typename T>
+static void diag_k_to_n_impl(T* K, uint64_t n, double* factor) {
+    std::lock_guard<std::recursive_mutex> lk(g_call_mutex);
+    if (n == 0) return;
+    Device& d = device();
+    T* dk = (T*)d.get(Device::S_K, n * n * sizeof(T));
+    double* tr = (double*)d.get(Device::S_RED, 64);
+    SNPMI_HIP(hipMemcpyAsync(dk, K, n * n * sizeof(T), hipMemcpyHostToDevice, d.stream));
+    launch_dense_trace(dk, n, DT<T>::v, tr, d.stream);
+    double trace = 0;
+    SNPMI_HIP(hipMemcpyAsync(&trace, tr, 8, hipMemcpyDeviceToHost, d.stream));
+    SNPMI_HIP(hipStreamSynchronize(d.stream));
+    const double f = (double)n / trace;
+    if (factor) *factor = f;
+    if (std::fabs(f - 1.0) > 1e-15) {
+        launch_dense_scale(dk, n * n, DT<T>::v, f, d.stream);
+        SNPMI_HIP(hipMemcpyAsync(K, dk, n * n * sizeof(T), hipMemcpyDeviceToHost, d.stream));
+        SNPMI_HIP(hipStreamSynchronize(d.stream));
+    }
+}
+
+}  // namespace snpmi
+
+// ====================================================================== exported C ABI
+using namespace snpmi;
+
+extern "C" {
+
+const char* snpmi_last_error(void) { return g_last_error.c_str(); }
+int snpmi_version(void) { return 1; }
+
+int snpmi_device_count(int* count) {
+    return guarded([&] {
+        SNPMI_REQUIRE(count != nullptr, SNPMI_E_ARG, "count is NULL");
+        *count = num_devices();
+        (void)hipGetLastError();
+    });
+}
+
+int snpmi_set_device(int dev) {
+    return guarded([&] {
+        SNPMI_REQUIRE(dev >= 0 && dev < num_devices(), SNPMI_E_ARG, "device index out of range");
+        g_cur_dev = dev;
+        (void)device();
+    });
+}
+
+int snpmi_get_device(int* dev) {
+    return guarded([&] {
+        SNPMI_REQUIRE(dev != nullptr, SNPMI_E_ARG, "dev is NULL");
+        *dev = g_cur_dev < 0 ? default_device() : g_cur_dev;
+    });
+}
+
+int snpmi_release_cache(void) {
+    return guarded([&] {
+        std::lock_guard<std::recursive_mutex> lk(g_call_mutex);
+        std::lock_guard<std::mutex> lk2(g_dev_mutex);
+        for (Device* d : g_devices)
+            if (d) {
+                SNPMI_HIP(hipSetDevice(d->id));
+                SNPMI_HIP(hipStreamSynchronize(d->stream));
+                d->release();
+            }
+        release_pinned();
+    });
+}
+
+int snpmi_device_info(int dev, char* name, size_t name_len, uint64_t* total_mem, int* cu_count) {
+    return guarded([&] {
+        hipDeviceProp_t p;
+        SNPMI_HIP(hipGetDeviceProperties(&p, dev));
+        if (name && name_len) {
+            std::strncpy(name, p.gcnArchName, name_len - 1);
+            name[name_len - 1] = 0;
+        }
+        if (total_mem) *total_mem = p.totalGlobalMem;
+        if (cu_count) *cu_count = p.multiProcessorCount;
+    });
+}
+
+int snpmi_bed_check(const char* path, uint64_t n_iid, uint64_t n_sid) {
+    return guarded([&] {
+        BedMap m;
+        open_bed(m, path, n_iid, n_sid);
+    });
+}
+
+#define SNPMI_BED_READ(SUFFIX, T)                                                                                  \
+    int snpmi_bed_read_##SUFFIX(const char* path, uint64_t n_iid, uint64_t n_sid, int count_a1,                  \
+                                const uint64_t* iid_idx, uint64_t n_out_iid, const uint64_t* sid_idx,             \
+                                uint64_t n_out_sid, int order_c, T* out, int num_threads) {                       \
+        return guarded([&] {                                                                                       \
+            bed_read_impl<T>(path, n_iid, n_sid, count_a1, iid_idx, n_out_iid, sid_idx, n_out_sid, order_c,       \
+                             SNPMI_STD_NONE, 0.0, 0.0, 0, (T*)nullptr, out, num_threads);                         \
+        });                                                                                                        \
+    }
+SNPMI_BED_READ(f32, float)
+SNPMI_BED_READ(f64, double)
+SNPMI_BED_READ(i8, int8_t)
+
+#define SNPMI_BED_READ_STD(SUFFIX, T)                                                                              \
+    int snpmi_bed_read_standardize_##SUFFIX(const char* path, uint64_t n_iid, uint64_t n_sid, int count_a1,      \
+                                            const uint64_t* iid_idx, uint64_t n_out_iid, const uint64_t* sid_idx, \
+                                            uint64_t n_out_sid, int order_c, int std_kind, double a, double b,    \
+                                            int use_stats, T* stats, T* out, int num_threads) {                   \
+        return guarded([&] {                                                                                       \
+            SNPMI_REQUIRE(std_kind == SNPMI_STD_NONE || stats != nullptr, SNPMI_E_ARG, "stats is NULL");          \
+            bed_read_impl<T>(path, n_iid, n_sid, count_a1, iid_idx, n_out_iid, sid_idx, n_out_sid, order_c,       \
+                             std_kind, a, b, use_stats, stats, out, num_threads);                                 \
+        });                                                                                                        \
+    }
+SNPMI_BED_READ_STD(f32, float)
+SNPMI_BED_READ_STD(f64, double)
+
+int snpmi_standardize_f32(float* val, uint64_t rows, uint64_t cols, int order_c, int is_beta, double a, double b,
+                          int apply_in_place, int use_stats, float* stats, int) {
+    return guarded([&] { standardize_impl<float>(val, rows, cols, order_c, is_beta, a, b, apply_in_place, use_stats, stats); });
+}
+int snpmi_standardize_f64(double* val, uint64_t rows, uint64_t cols, int order_c, int is_beta, double a, double b,
+                          int apply_in_place, int use_stats, double* stats, int) {
+    return guarded([&] { standardize_impl<double>(val, rows, cols, order_c, is_beta, a, b, apply_in_place, use_stats, stats); });
+}
+
+int snpmi_subset_f64_f64(const double* val, uint64_t rows, uint64_t cols, uint64_t k, int in_c, const uint64_t* ri,
+                         uint64_t nr, const uint64_t* ci, uint64_t nc, int out_c, double* out, int) {
+    return guarded([&] { subset_impl<double, double>(val, rows, cols, k, in_c, ri, nr, ci, nc, out_c, out); });
+}
+int snpmi_subset_f32_f64(const float* val, uint64_t rows, uint64_t cols, uint64_t k, int in_c, const uint64_t* ri,
+                         uint64_t nr, const uint64_t* ci, uint64_t nc, int out_c, double* out, int) {
+    return guarded([&] { subset_impl<float, double>(val, rows, cols, k, in_c, ri, nr, ci, nc, out_c, out); });
+}
+int snpmi_subset_f32_f32(const float* val, uint64_t rows, uint64_t cols, uint64_t k, int in_c, const uint64_t* ri,
+                         uint64_t nr, const uint64_t* ci, uint64_t nc, int out_c, float* out, int) {
+    return guarded([&] { subset_impl<float, float>(val, rows, cols, k, in_c, ri, nr, ci, nc, out_c, out); });
+}
+
+#define SNPMI_GRM_BED(SUFFIX, T)                                                                                    \
+    int snpmi_grm_bed_##SUFFIX(const char* path, uint64_t n_iid, uint64_t n_sid, int count_a1,                    \
+                               const uint64_t* iid_idx, uint64_t n_out_iid, const uint64_t* sid_idx,              \
+                               uint64_t n_out_sid, int std_kind, double a, double b, int use_stats, T* stats,     \
+                               int diag, double* factor, T* K_out, int num_threads) {                             \
+        return guarded([&] {                                                                                        \
+            grm_bed_impl<T>(path, n_iid, n_sid, count_a1, iid_idx, n_out_iid, sid_idx, n_out_sid, std_kind, a, b,  \
+                            use_stats, stats, diag, factor, K_out, num_threads);                                   \
+        });                                                                                                         \
+    }
+SNPMI_GRM_BED(f32, float)
+SNPMI_GRM_BED(f64, double)
+
+int snpmi_grm_dense_f32(const float* val, uint64_t rows, uint64_t cols, int order_c, int std_kind, double a, double b,
+                        int use_stats, float* stats, int diag, double* factor, float* K_out) {
+    return guarded([&] { grm_dense_impl<float>(val, rows, cols, order_c, std_kind, a, b, use_stats, stats, diag, factor, K_out); });
+}
+int snpmi_grm_dense_f64(const double* val, uint64_t rows, uint64_t cols, int order_c, int std_kind, double a,
+                        double b, int use_stats, double* stats, int diag, double* factor, double* K_out) {
+    return guarded([&] { grm_dense_impl<double>(val, rows, cols, order_c, std_kind, a, b, use_stats, stats, diag, factor, K_out); });
+}
+int snpmi_diag_k_to_n_f32(float* K, uint64_t n, double* factor) {
+    return guarded([&] { diag_k_to_n_impl<float>(K, n, factor); });
+}
+int snpmi_diag_k_to_n_f64(double* K, uint64_t n, double* factor) {
+    return guarded([&] { diag_k_to_n_impl<double>(K, n, factor); });
+}
+
+// ---------------------------------------------------------------------- device-resident API
+uint64_t snpmi_packed_pitch(uint64_t n_iid) { return packed_pitch(n_iid); }
+uint64_t snpmi_grm_tile_bytes(uint64_t n_iid, int dtype) {
+    return n_tiles_upper(n_iid) * kTile * kTile * dtype_size(dtype);
+}
+
+int snpmi_dev_alloc(void** ptr, uint64_t bytes) {
+    return guarded([&] {
+        SNPMI_REQUIRE(ptr != nullptr, SNPMI_E_ARG, "ptr is NULL");
+        (void)device();
+        if (hipMalloc(ptr, bytes ? bytes : 256) != hipSuccess) {
+            (void)hipGetLastError();
+            throw Error(SNPMI_E_NOMEM, "hipMalloc of " + std::to_string(bytes) + " bytes failed");
+        }
+    });
+}
+int snpmi_dev_free(void* ptr) {
+    return guarded([&] {
+        (void)device();
+        SNPMI_HIP(hipFree(ptr));
+    });
+}
+int snpmi_dev_memset(void* ptr, int value, uint64_t bytes) {
+    return guarded([&] { SNPMI_HIP(hipMemsetAsync(ptr, value, bytes, stream())); });
+}
+int snpmi_memcpy_h2d(void* dst, const void* src, uint64_t bytes) {
+    return guarded([&] {
+        SNPMI_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, stream()));
+        SNPMI_HIP(hipStreamSynchronize(stream()));
+    });
+}
+int snpmi_memcpy_d2h(void* dst, const void* src, uint64_t bytes) {
+    return guarded([&] {
+        SNPMI_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, stream()));
+        SNPMI_HIP(hipStreamSynchronize(stream()));
+    });
+}
+int snpmi_stream_sync(void) {
+    return guarded([&] { SNPMI_HIP(hipStreamSynchronize(stream())); });
+}
+int snpmi_event_create(void** ev) {
+    return guarded([&] {
+        (void)device();
+        SNPMI_HIP(hipEventCreate((hipEvent_t*)ev));
+    });
+}
+int snpmi_event_destroy(void* ev) {
+    return guarded([&] { SNPMI_HIP(hipEventDestroy((hipEvent_t)ev)); });
+}
+int snpmi_event_record(void* ev) {
+    return guarded([&] { SNPMI_HIP(hipEventRecord((hipEvent_t)ev, stream())); });
+}
+int snpmi_event_elapsed_ms(void* start, void* stop, float* ms) {
+    return guarded([&] {
+        SNPMI_HIP(hipEventSynchronize((hipEvent_t)stop));
+        SNPMI_HIP(hipEventElapsedTime(ms, (hipEvent_t)start, (hipEvent_t)stop));
+    });
+}
+
+int snpmi_dev_synth_bed(uint8_t* packed, uint64_t pitch, uint64_t n_iid, uint64_t sid0, uint64_t n_sid, uint64_t seed,
+                        double miss_rate, const double* maf_x, const double* maf_cdf, int n_pts) {
+    return guarded([&] {
+        SNPMI_REQUIRE(pitch % 4 == 0 && pitch >= ceil_div(n_iid, 4), SNPMI_E_ARG, "bad pitch");
+        SNPMI_REQUIRE(n_pts > 0 && n_pts <= 1024, SNPMI_E_ARG, "bad MAF table");
+        Device& d = device();
+        double* tab = (double*)d.get(Device::S_RED, 2 * n_pts * sizeof(double));
+        SNPMI_HIP(hipMemcpyAsync(tab, maf_x, n_pts * 8, hipMemcpyHostToDevice, d.stream));
+        SNPMI_HIP(hipMemcpyAsync(tab + n_pts, maf_cdf, n_pts * 8, hipMemcpyHostToDevice, d.stream));
+        launch_synth(packed, pitch, n_iid, sid0, n_sid, seed, miss_rate, tab, tab + n_pts, n_pts, d.stream);
+        SNPMI_HIP(hipStreamSynchronize(d.stream));
+    });
+}
+
+int snpmi_dev_snp_stats(const uint8_t* packed, uint64_t pitch, uint64_t n_iid, uint64_t n_sid, int count_a1,
+                        int std_kind, double a, double b, int use_stats, int dtype, void* stats, void* lut) {
+    return guarded([&] {
+        SNPMI_REQUIRE(pitch % 64 == 0 && pitch >= ceil_div(n_iid, 4), SNPMI_E_ARG, "pitch must be snpmi_packed_pitch");
+        launch_snp_stats(packed, pitch, n_iid, n_sid, count_a1, std_kind, a, b, use_stats, dtype, stats, lut, stream());
+    });
+}
+
+int snpmi_dev_decode(const uint8_t* packed, uint64_t pitch, uint64_t n_iid, uint64_t n_sid, const void* lut,
+                     int dtype, int order_c, void* out, uint64_t ld) {
+    return guarded([&] {
+        SNPMI_REQUIRE(pitch % 64 == 0 && pitch >= ceil_div(n_iid, 4), SNPMI_E_ARG, "pitch must be snpmi_packed_pitch");
+        if (!order_c) SNPMI_REQUIRE(ld % 16 == 0 && ld >= n_iid, SNPMI_E_ARG, "F-order ld must be >= n_iid, % 16");
+        else SNPMI_REQUIRE(ld >= n_sid, SNPMI_E_ARG, "C-order ld must be >= n_sid");
+        launch_decode(packed, pitch, n_iid, n_sid, lut, dtype, order_c, out, ld, stream());
+    });
+}
+
+int snpmi_dev_repack(const uint8_t* src, uint64_t src_pitch, uint64_t n_src, const uint64_t* idx, uint64_t n_out,
+                     uint64_t n_sid, uint8_t* dst, uint64_t dst_pitch) {
+    return guarded([&] {
+        SNPMI_REQUIRE(dst_pitch % 64 == 0 && dst_pitch >= ceil_div(n_out, 4), SNPMI_E_ARG, "bad dst pitch");
+        launch_repack(src, src_pitch, n_src, idx, n_out, n_sid, dst, dst_pitch, nullptr, stream());
+    });
+}
+
+int snpmi_dev_syrk_packed(const uint8_t* packed, uint64_t pitch, uint64_t n_iid, uint64_t n_sid, const void* lut,
+                          int dtype, void* K_tiles, int accumulate) {
+    return guarded([&] {
+        SNPMI_REQUIRE(dtype == SNPMI_DT_F32 || dtype == SNPMI_DT_F64, SNPMI_E_ARG, "GRM dtype must be f32/f64");
+        SNPMI_REQUIRE(pitch % 64 == 0 && pitch >= ceil_div(n_iid, 4), SNPMI_E_ARG, "pitch must be snpmi_packed_pitch");
+        launch_syrk_packed(packed, pitch, n_iid, n_sid, lut, dtype, K_tiles, accumulate, stream());
+    });
+}
+
+int snpmi_dev_syrk_dense(const void* Z, uint64_t ldz, uint64_t n_iid, uint64_t n_sid, int dtype, void* K_tiles,
+                         int accumulate) {
+    return guarded([&] {
+        SNPMI_REQUIRE(dtype == SNPMI_DT_F32 || dtype == SNPMI_DT_F64, SNPMI_E_ARG, "GRM dtype must be f32/f64");
+        launch_syrk_dense(Z, ldz, n_iid, n_sid, dtype, K_tiles, accumulate, stream());
+    });
+}
+
+int snpmi_dev_grm_extract(const void* K_tiles, uint64_t n_iid, int dtype, const uint64_t* ri, uint64_t nr,
+                          const uint64_t* ci, uint64_t nc, int order_c, double scale, void* out) {
+    return guarded([&] {
+        launch_grm_extract(K_tiles, n_iid, dtype, ri, nr, ci, nc, order_c, scale, out, stream());
+    });
+}
+
+int snpmi_dev_grm_trace(const void* K_tiles, uint64_t n_iid, int dtype, double* trace) {
+    return guarded([&] {
+        Device& d = device();
+        double* tr = (double*)d.get(Device::S_RED, 64);
+        launch_grm_trace(K_tiles, n_iid, dtype, tr, d.stream);
+        SNPMI_HIP(hipMemcpyAsync(trace, tr, 8, hipMemcpyDeviceToHost, d.stream));
+        SNPMI_HIP(hipStreamSynchronize(d.stream));
+    });
+}
+
+}  // extern "C"

@@ -1,0 +1,715 @@
+// Memory-bound kernels of the BED path (gfx950):
+//   k_snp_stats      packed codes -> per-SNP counts -> stats + 4-entry value LUT
+//   k_decode_f/_c    packed codes + LUT -> values (F or C order)
+//   k_repack         iid gather of packed columns (arbitrary iid index lists)
+//   k_std_dense_*    standardize an arbitrary float matrix in place (SnpData.standardize)
+//   k_subset         sub_matrix gather (util/__init__.py:271-393)
+//   k_grm_extract    upper-triangle GRM tiles -> K[ri, ci] (symmetric mirror + scale)
+//   k_synth          counter-based synthetic genotypes
+// Reference semantics: SURVEY.md Appendix B; bed-reader call sites bed.py:337-343,
+// standardizer.py:90-211.  Built with -ffp-contract=off: the stats/LUT arithmetic is f64,
+// rounded once to the output dtype, and must not be contracted into FMAs.
+#include "snpmi_internal.hpp"
+
+namespace snpmi {
+namespace {
+
+constexpr int kWave = 64;
+constexpr int kBlock = 256;
+
+__device__ __forceinline__ double stats_mean_std(double n, double s1, double s2, double* sd_out) {
+    if (n == 0.0) {
+        *sd_out = __builtin_nan("");
+        return __builtin_nan("");
+    }
+    double m = s1 / n;
+    double var = s2 / n - m * m;
+    double sd = sqrt(var);
+    if (!(sd > 0.0)) sd = __builtin_inf();
+    *sd_out = sd;
+    return m;
+}
+
+// Beta(a,b) density at the folded MAF (standardizer.py:199-205); f64.
+__device__ __forceinline__ double beta_weight(double mean, double a, double b) {
+    double maf = mean / 2.0;
+    if (maf > 0.5) maf = 1.0 - maf;
+    if (!(maf >= 0.0 && maf <= 1.0)) return 0.0;
+    double lbeta = lgamma(a) + lgamma(b) - lgamma(a + b);
+    return pow(maf, a - 1.0) * pow(1.0 - maf, b - 1.0) / exp(lbeta);
+}
+
+// value of code c (count_A1 selects the A1 LUT); -1 = missing
+__device__ __forceinline__ int code_value(int c, int count_a1) {
+    // count_A1=False {0,-,1,2}; count_A1=True {2,-,1,0}
+    if (c == 1) return -1;
+    int v = (c == 0) ? 0 : (c == 2 ? 1 : 2);
+    return count_a1 ? 2 - v : v;
+}
+
+template <typename T>
+__device__ __forceinline__ T lut_missing() { return (T)__builtin_nan(""); }
+template <>
+__device__ __forceinline__ int8_t lut_missing<int8_t>() { return (int8_t)-127; }
+
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, kWave);
+    return v;
+}
+__device__ __forceinline__ double wave_sum_f64(double v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, kWave);
+    return v;
+}
+
+// ------------------------------------------------------------------ per-SNP stats + LUT
+// One wave per SNP column; 16-byte loads (64 iids per lane-load).
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_snp_stats(const uint8_t* __restrict__ packed, uint64_t pitch,
+                                                      uint64_t n, uint64_t m, int count_a1, int std_kind,
+                                                      double a, double b, int use_stats, T* __restrict__ stats,
+                                                      T* __restrict__ lut) {
+    const int lane = threadIdx.x & (kWave - 1);
+    const uint64_t s = (uint64_t)blockIdx.x * (kBlock / kWave) + (threadIdx.x / kWave);
+    if (s >= m) return;
+    if (std_kind == SNPMI_STD_NONE) {
+        if (lane < 4) {
+            int v = code_value(lane, count_a1);
+            lut[4 * s + lane] = v < 0 ? lut_missing<T>() : (T)v;
+        }
+        return;
+    }
+    double mean, sd;
+    if (use_stats) {
+        mean = (double)stats[2 * s];
+        sd = (double)stats[2 * s + 1];
+    } else {
+        const uint4* col = reinterpret_cast<const uint4*>(packed + s * pitch);
+        const uint64_t nq = (n + 63) / 64;
+        uint32_t c1 = 0, c2 = 0, c3 = 0;
+        for (uint64_t q = lane; q < nq; q += kWave) {
+            uint4 v = col[q];
+            uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                uint32_t w = w4[k];
+                uint32_t lo = w & 0x55555555u, hi = (w >> 1) & 0x55555555u;
+                uint64_t ib = q * 64 + 16 * k;
+                if (ib + 16 > n) {
+                    uint64_t valid = n > ib ? n - ib : 0;
+                    uint32_t mk = ((1u << (2 * valid)) - 1u) & 0x55555555u;  // valid < 16 here
+                    lo &= mk;
+                    hi &= mk;
+                }
+                c3 += __popc(lo & hi);
+                c2 += __popc(hi & ~lo);
+                c1 += __popc(lo & ~hi);
+            }
+        }
+        c1 = wave_sum_u32(c1);
+        c2 = wave_sum_u32(c2);
+        c3 = wave_sum_u32(c3);
+        uint64_t c0 = n - c1 - c2 - c3;
+        uint64_t chi = count_a1 ? c0 : c3;  // count of value 2
+        double nobs = (double)(n - c1);
+        mean = stats_mean_std(nobs, (double)(c2 + 2 * chi), (double)(c2 + 4 * chi), &sd);
+        if (lane == 0) {
+            stats[2 * s] = (T)mean;
+            stats[2 * s + 1] = (T)sd;
+        }
+    }
+    if (lane < 4) {
+        double w = std_kind == SNPMI_STD_BETA ? beta_weight(mean, a, b) : 0.0;
+        bool zero_col = std_kind == SNPMI_STD_BETA && use_stats && __builtin_isinf(sd);
+        int v = code_value(lane, count_a1);
+        double x;
+        if (v < 0 || zero_col) x = 0.0;
+        else if (std_kind == SNPMI_STD_BETA) x = ((double)v - mean) * w;
+        else x = ((double)v - mean) / sd;
+        lut[4 * s + lane] = (T)x;
+    }
+}
+
+// ------------------------------------------------------------------ decode, F order
+template <typename T>
+__device__ __forceinline__ T sel4(T l0, T l1, T l2, T l3, uint32_t c) {
+    return (c & 2u) ? ((c & 1u) ? l3 : l2) : ((c & 1u) ? l1 : l0);
+}
+
+// Wave work item = (column j, chunk of 1024 iids).  Each lane loads one dword (16 iids);
+// codes are redistributed with ds_bpermute so every store instruction writes 1 KiB
+// contiguous (f32: 4 rounds of float4; f64: 8 rounds of double2; i8: one 16-B store).
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_decode_f(const uint8_t* __restrict__ packed, uint64_t pitch, uint64_t n,
+                                                     uint64_t m, const T* __restrict__ lut, T* __restrict__ out,
+                                                     uint64_t ld) {
+    const int lane = threadIdx.x & (kWave - 1);
+    const uint64_t chunks = (n + 1023) / 1024;
+    const uint64_t total = chunks * m;
+    const uint64_t nwaves = (uint64_t)gridDim.x * (kBlock / kWave);
+    for (uint64_t it = (uint64_t)blockIdx.x * (kBlock / kWave) + threadIdx.x / kWave; it < total; it += nwaves) {
+        const uint64_t j = it / chunks, c = it - j * chunks;
+        const uint64_t i0 = c * 1024;
+        const uint32_t* col = reinterpret_cast<const uint32_t*>(packed + j * pitch);
+        const uint32_t w = (i0 + 16 * (uint64_t)lane < n) ? col[c * 64 + lane] : 0u;
+        const T l0 = lut[4 * j], l1 = lut[4 * j + 1], l2 = lut[4 * j + 2], l3 = lut[4 * j + 3];
+        T* o = out + j * ld + i0;
+        if constexpr (sizeof(T) == 4) {
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                uint32_t src = __shfl(w, r * 16 + (lane >> 2), kWave);
+                uint32_t byte = (src >> (8 * (lane & 3))) & 0xffu;
+                const uint64_t i = i0 + r * 256 + 4 * lane;
+                float4 v;
+                v.x = sel4(l0, l1, l2, l3, byte & 3u);
+                v.y = sel4(l0, l1, l2, l3, (byte >> 2) & 3u);
+                v.z = sel4(l0, l1, l2, l3, (byte >> 4) & 3u);
+                v.w = sel4(l0, l1, l2, l3, byte >> 6);
+                if (i + 4 <= n) {
+                    *reinterpret_cast<float4*>(o + r * 256 + 4 * lane) = v;
+                } else {
+                    float e[4] = {v.x, v.y, v.z, v.w};
+                    for (int t = 0; t < 4; t++)
+                        if (i + t < n) o[r * 256 + 4 * lane + t] = e[t];
+                }
+            }
+        } else if constexpr (sizeof(T) == 8) {
+#pragma unroll
+            for (int r = 0; r < 8; r++) {
+                uint32_t src = __shfl(w, r * 8 + (lane >> 3), kWave);
+                uint32_t byte = (src >> (8 * ((lane >> 1) & 3))) & 0xffu;
+                uint32_t sh = 4 * (lane & 1);
+                const uint64_t i = i0 + r * 128 + 2 * lane;
+                double2 v;
+                v.x = sel4(l0, l1, l2, l3, (byte >> sh) & 3u);
+                v.y = sel4(l0, l1, l2, l3, (byte >> (sh + 2)) & 3u);
+                if (i + 2 <= n) {
+                    *reinterpret_cast<double2*>(o + r * 128 + 2 * lane) = v;
+                } else if (i < n) {
+                    o[r * 128 + 2 * lane] = v.x;
+                }
+            }
+        } else {
+            // int8: lane writes 16 bytes for its own dword; byte LUT via v_perm_b32
+            const uint32_t lw = (uint32_t)(uint8_t)l0 | ((uint32_t)(uint8_t)l1 << 8) |
+                                ((uint32_t)(uint8_t)l2 << 16) | ((uint32_t)(uint8_t)l3 << 24);
+            uint32_t q[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                uint32_t b = (w >> (8 * k)) & 0xffu;
+                uint32_t selb = (b & 3u) | ((b & 0xCu) << 6) | ((b & 0x30u) << 12) | ((b & 0xC0u) << 18);
+                q[k] = __builtin_amdgcn_perm(0u, lw, selb);
+            }
+            const uint64_t i = i0 + 16 * lane;
+            if (i + 16 <= n) {
+                *reinterpret_cast<uint4*>(o + 16 * lane) = make_uint4(q[0], q[1], q[2], q[3]);
+            } else if (i < n) {
+                const uint8_t* qb = reinterpret_cast<const uint8_t*>(q);
+                for (uint64_t t = 0; i + t < n; t++) reinterpret_cast<uint8_t*>(o)[16 * lane + t] = qb[t];
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------------ decode, C order
+// Tile = 64 SNPs x 64 iids staged in LDS, rows written SNP-fastest.
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_decode_c(const uint8_t* __restrict__ packed, uint64_t pitch, uint64_t n,
+                                                     uint64_t m, const T* __restrict__ lut, T* __restrict__ out,
+                                                     uint64_t ld) {
+    __shared__ uint32_t sh[64][5];
+    __shared__ T shl[64][4];
+    const int t = threadIdx.x;
+    const uint64_t tiles_i = (n + 63) / 64, tiles_j = (m + 63) / 64;
+    const uint64_t nwords = (n + 15) / 16;
+    for (uint64_t tile = blockIdx.x; tile < tiles_i * tiles_j; tile += gridDim.x) {
+        const uint64_t tj = tile / tiles_i, ti = tile - tj * tiles_i;
+        const uint64_t i0 = ti * 64, j0 = tj * 64;
+        {
+            const int cj = t >> 2, dw = t & 3;
+            uint32_t w = 0;
+            if (j0 + cj < m && i0 / 16 + dw < nwords)
+                w = reinterpret_cast<const uint32_t*>(packed + (j0 + cj) * pitch)[i0 / 16 + dw];
+            sh[cj][dw] = w;
+            if (t < 64 && j0 + t < m) {
+#pragma unroll
+                for (int k = 0; k < 4; k++) shl[t][k] = lut[4 * (j0 + t) + k];
+            }
+        }
+        __syncthreads();
+        const int jj = t & 63, r0 = t >> 6;
+        if (j0 + jj < m) {
+#pragma unroll 4
+            for (int q = 0; q < 16; q++) {
+                const int r = r0 + 4 * q;
+                if (i0 + r < n) {
+                    uint32_t code = (sh[jj][r >> 4] >> (2 * (r & 15))) & 3u;
+                    out[(i0 + r) * ld + j0 + jj] = shl[jj][code];
+                }
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// ------------------------------------------------------------------ iid gather (repack)
+__global__ __launch_bounds__(kBlock) void k_repack(const uint8_t* __restrict__ src, uint64_t sp,
+                                                   const uint64_t* __restrict__ idx, uint64_t n_out, uint64_t m,
+                                                   uint8_t* __restrict__ dst, uint64_t dp) {
+    const uint64_t nd = (n_out + 15) / 16;
+    const uint64_t total = nd * m;
+    for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+         t += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t j = t / nd, d = t - j * nd;
+        const uint8_t* col = src + j * sp;
+        uint32_t w = 0;
+#pragma unroll 4
+        for (int k = 0; k < 16; k++) {
+            const uint64_t r = 16 * d + k;
+            if (r < n_out) {
+                const uint64_t i = idx[r];
+                w |= (uint32_t)((col[i >> 2] >> (2 * (i & 3))) & 3u) << (2 * k);
+            }
+        }
+        reinterpret_cast<uint32_t*>(dst + j * dp)[d] = w;
+    }
+}
+
+// ------------------------------------------------------------------ dense standardize
+template <typename T>
+__device__ __forceinline__ T apply_one(T x, double mean, double sd, int is_beta, double w, bool zero_col) {
+    if (x != x || zero_col) return (T)0;
+    double d = (double)x - mean;
+    return (T)(is_beta ? d * w : d / sd);
+}
+
+// F order: one wave per column.
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_std_dense_f(T* __restrict__ val, uint64_t rows, uint64_t cols,
+                                                        uint64_t ld, int std_kind, double a, double b, int use_stats,
+                                                        T* __restrict__ stats) {
+    const int lane = threadIdx.x & (kWave - 1);
+    const uint64_t nwaves = (uint64_t)gridDim.x * (kBlock / kWave);
+    const int is_beta = std_kind == SNPMI_STD_BETA;
+    for (uint64_t j = (uint64_t)blockIdx.x * (kBlock / kWave) + threadIdx.x / kWave; j < cols; j += nwaves) {
+        T* c = val + j * ld;
+        double mean, sd;
+        if (use_stats) {
+            mean = (double)stats[2 * j];
+            sd = (double)stats[2 * j + 1];
+        } else {
+            double n = 0, s1 = 0, s2 = 0;
+            for (uint64_t i = lane; i < rows; i += kWave) {
+                T x = c[i];
+                if (x == x) {
+                    double dx = (double)x;
+                    n += 1.0;
+                    s1 += dx;
+                    s2 += dx * dx;
+                }
+            }
+            n = wave_sum_f64(n);
+            s1 = wave_sum_f64(s1);
+            s2 = wave_sum_f64(s2);
+            mean = stats_mean_std(n, s1, s2, &sd);
+            if (lane == 0) {
+                stats[2 * j] = (T)mean;
+                stats[2 * j + 1] = (T)sd;
+            }
+        }
+        const double w = is_beta ? beta_weight(mean, a, b) : 0.0;
+        const bool zero_col = is_beta && use_stats && __builtin_isinf(sd);
+        for (uint64_t i = lane; i < rows; i += kWave) c[i] = apply_one(c[i], mean, sd, is_beta, w, zero_col);
+    }
+}
+
+// C order: a block owns 64 adjacent columns; lanes walk columns, waves walk rows.
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_std_dense_c(T* __restrict__ val, uint64_t rows, uint64_t cols,
+                                                        uint64_t ld, int std_kind, double a, double b, int use_stats,
+                                                        T* __restrict__ stats) {
+    __shared__ double red[3][4][64];
+    __shared__ double fin[2][64];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int is_beta = std_kind == SNPMI_STD_BETA;
+    for (uint64_t j0 = (uint64_t)blockIdx.x * 64; j0 < cols; j0 += (uint64_t)gridDim.x * 64) {
+        const uint64_t j = j0 + lane;
+        const bool ok = j < cols;
+        if (use_stats) {
+            if (wv == 0 && ok) {
+                fin[0][lane] = (double)stats[2 * j];
+                fin[1][lane] = (double)stats[2 * j + 1];
+            }
+        } else {
+            double n = 0, s1 = 0, s2 = 0;
+            if (ok)
+                for (uint64_t i = wv; i < rows; i += 4) {
+                    T x = val[i * ld + j];
+                    if (x == x) {
+                        double dx = (double)x;
+                        n += 1.0;
+                        s1 += dx;
+                        s2 += dx * dx;
+                    }
+                }
+            red[0][wv][lane] = n;
+            red[1][wv][lane] = s1;
+            red[2][wv][lane] = s2;
+            __syncthreads();
+            if (wv == 0) {
+                double tn = 0, t1 = 0, t2 = 0;
+                for (int q = 0; q < 4; q++) {
+                    tn += red[0][q][lane];
+                    t1 += red[1][q][lane];
+                    t2 += red[2][q][lane];
+                }
+                double sd;
+                double mean = stats_mean_std(tn, t1, t2, &sd);
+                fin[0][lane] = mean;
+                fin[1][lane] = sd;
+                if (ok) {
+                    stats[2 * j] = (T)mean;
+                    stats[2 * j + 1] = (T)sd;
+                }
+            }
+        }
+        __syncthreads();
+        if (ok) {
+            const double mean = fin[0][lane], sd = fin[1][lane];
+            const double w = is_beta ? beta_weight(mean, a, b) : 0.0;
+            const bool zero_col = is_beta && use_stats && __builtin_isinf(sd);
+            for (uint64_t i = wv; i < rows; i += 4) val[i * ld + j] = apply_one(val[i * ld + j], mean, sd, is_beta, w, zero_col);
+        }
+        __syncthreads();
+    }
+}
+
+// ------------------------------------------------------------------ sub_matrix gather
+template <typename S, typename D>
+__global__ __launch_bounds__(kBlock) void k_subset(const S* __restrict__ in, uint64_t rows, uint64_t cols, uint64_t k,
+                                                   int in_c, const uint64_t* __restrict__ ri, uint64_t nr,
+                                                   const uint64_t* __restrict__ ci, uint64_t nc, int out_c,
+                                                   D* __restrict__ out) {
+    const uint64_t total = nr * nc * k;
+    for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+         t += (uint64_t)gridDim.x * blockDim.x) {
+        uint64_t i, j, q;
+        if (out_c) {
+            q = t % k;
+            const uint64_t rest = t / k;
+            j = rest % nc;
+            i = rest / nc;
+        } else {
+            i = t % nr;
+            const uint64_t rest = t / nr;
+            j = rest % nc;
+            q = rest / nc;
+        }
+        const uint64_t r = ri[i], c = ci[j];
+        const uint64_t src = in_c ? (r * cols + c) * k + q : r + rows * (c + cols * q);
+        out[t] = (D)in[src];
+    }
+}
+
+// ------------------------------------------------------------------ C -> F transpose (64x64 LDS tiles)
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_transpose(const T* __restrict__ in, uint64_t rows, uint64_t cols,
+                                                      T* __restrict__ out, uint64_t ld) {
+    __shared__ T tile[64][65];
+    const uint64_t tr = (rows + 63) / 64, tc = (cols + 63) / 64;
+    const int x = threadIdx.x & 63, y = threadIdx.x >> 6;
+    for (uint64_t b = blockIdx.x; b < tr * tc; b += gridDim.x) {
+        const uint64_t bi = b % tr, bj = b / tr;
+        for (int q = y; q < 64; q += 4) {
+            const uint64_t i = bi * 64 + q, j = bj * 64 + x;
+            tile[q][x] = (i < rows && j < cols) ? in[i * cols + j] : (T)0;
+        }
+        __syncthreads();
+        for (int q = y; q < 64; q += 4) {
+            const uint64_t j = bj * 64 + q, i = bi * 64 + x;
+            if (i < rows && j < cols) out[j * ld + i] = tile[x][q];
+        }
+        __syncthreads();
+    }
+}
+
+// ------------------------------------------------------------------ GRM tiles -> K
+__device__ __forceinline__ uint64_t tile_index(uint64_t ti, uint64_t tj) { return tj * (tj + 1) / 2 + ti; }
+
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_grm_extract(const T* __restrict__ tiles, const uint64_t* __restrict__ ri,
+                                                        uint64_t nr, const uint64_t* __restrict__ ci, uint64_t nc,
+                                                        int out_c, double scale, T* __restrict__ out) {
+    const uint64_t total = nr * nc;
+    for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+         t += (uint64_t)gridDim.x * blockDim.x) {
+        uint64_t r, c;
+        if (out_c) {
+            r = t / nc;
+            c = t - r * nc;
+        } else {
+            c = t / nr;
+            r = t - c * nr;
+        }
+        uint64_t i = ri ? ri[r] : r, j = ci ? ci[c] : c;
+        if (i > j) {
+            const uint64_t s = i;
+            i = j;
+            j = s;
+        }
+        const T v = tiles[tile_index(i / kTile, j / kTile) * (kTile * kTile) + (i % kTile) * kTile + (j % kTile)];
+        out[t] = scale == 1.0 ? v : (T)((double)v * scale);
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_grm_trace(const T* __restrict__ tiles, uint64_t n, double* trace) {
+    __shared__ double red[kBlock / kWave];
+    double s = 0;
+    for (uint64_t i = threadIdx.x; i < n; i += blockDim.x)
+        s += (double)tiles[tile_index(i / kTile, i / kTile) * (kTile * kTile) + (i % kTile) * (kTile + 1)];
+    s = wave_sum_f64(s);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double t = 0;
+        for (int q = 0; q < kBlock / kWave; q++) t += red[q];
+        *trace = t;
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_dense_trace(const T* __restrict__ K, uint64_t n, double* trace) {
+    __shared__ double red[kBlock / kWave];
+    double s = 0;
+    for (uint64_t i = threadIdx.x; i < n; i += blockDim.x) s += (double)K[i * n + i];
+    s = wave_sum_f64(s);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double t = 0;
+        for (int q = 0; q < kBlock / kWave; q++) t += red[q];
+        *trace = t;
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_scale(T* __restrict__ p, uint64_t count, double scale) {
+    for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < count; t += (uint64_t)gridDim.x * blockDim.x)
+        p[t] = (T)((double)p[t] * scale);
+}
+
+// ------------------------------------------------------------------ synthetic genotypes
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+
+// CPU twin: oracle/bed_oracle.c oracle_synth_bed (bit-identical by construction).
+__global__ __launch_bounds__(kBlock) void k_synth(uint8_t* __restrict__ packed, uint64_t pitch, uint64_t n,
+                                                  uint64_t sid0, uint64_t m, uint64_t seed, double miss_rate,
+                                                  const double* __restrict__ maf_x, const double* __restrict__ maf_cdf,
+                                                  int n_pts) {
+    const uint64_t nd = pitch / 4;
+    const uint64_t total = nd * m;
+    for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+         t += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t j = t / nd, d = t - j * nd;
+        const uint64_t sid = sid0 + j;
+        uint32_t w = 0;
+        if (16 * d < n) {
+            const uint64_t h = splitmix64(seed * 0xD1B54A32D192ED03ull ^ (sid + 1) * 0x8CB92BA72F3D8DD7ull);
+            const double u = (double)(h >> 11) * (1.0 / 9007199254740992.0);
+            int lo = 0, hi = n_pts - 1;  // first k with u <= cdf[k], capped at n_pts-1
+            while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                if (u > maf_cdf[mid]) lo = mid + 1;
+                else hi = mid;
+            }
+            const double maf = maf_x[lo];
+            const double p2 = maf * maf, p1 = 2.0 * maf * (1.0 - maf);
+            const double sc = 4294967296.0;
+            const double t2 = p2 * sc, t12 = (p2 + p1) * sc, tm = miss_rate * sc;
+            const uint32_t th2 = t2 >= sc ? 0xFFFFFFFFu : (uint32_t)t2;
+            const uint32_t th12 = t12 >= sc ? 0xFFFFFFFFu : (uint32_t)t12;
+            const uint32_t thm = tm >= sc ? 0xFFFFFFFFu : (uint32_t)tm;
+            const uint64_t kb = (seed + 0x632BE59BD9B4E019ull) ^ (sid * 0x9E6C63D0676A9A99ull);
+            for (int k = 0; k < 16; k++) {
+                const uint64_t i = 16 * d + k;
+                if (i >= n) break;
+                const uint64_t hh = splitmix64(kb ^ (i * 0xC2B2AE3D27D4EB4Full));
+                const uint32_t ug = (uint32_t)hh, um = (uint32_t)(hh >> 32);
+                uint32_t code = um < thm ? 1u : (ug < th2 ? 3u : (ug < th12 ? 2u : 0u));
+                w |= code << (2 * k);
+            }
+        }
+        reinterpret_cast<uint32_t*>(packed + j * pitch)[d] = w;
+    }
+}
+
+inline unsigned grid_for(uint64_t work, uint64_t per_block, unsigned cap = 65536) {
+    uint64_t g = (work + per_block - 1) / per_block;
+    if (g < 1) g = 1;
+    if (g > cap) g = cap;
+    return (unsigned)g;
+}
+
+}  // namespace
+
+// ====================================================================== launchers
+#define SNPMI_LAUNCH_CHECK() SNPMI_HIP(hipGetLastError())
+
+void launch_snp_stats(const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m, int count_a1, int std_kind,
+                      double a, double b, int use_stats, int dtype, void* stats, void* lut, hipStream_t st) {
+    if (m == 0) return;
+    const unsigned g = (unsigned)ceil_div(m, kBlock / kWave);
+    if (dtype == SNPMI_DT_F32)
+        k_snp_stats<float><<<g, kBlock, 0, st>>>(packed, pitch, n, m, count_a1, std_kind, a, b, use_stats,
+                                                  (float*)stats, (float*)lut);
+    else if (dtype == SNPMI_DT_F64)
+        k_snp_stats<double><<<g, kBlock, 0, st>>>(packed, pitch, n, m, count_a1, std_kind, a, b, use_stats,
+                                                   (double*)stats, (double*)lut);
+    else
+        k_snp_stats<int8_t><<<g, kBlock, 0, st>>>(packed, pitch, n, m, count_a1, SNPMI_STD_NONE, a, b, 0,
+                                                   (int8_t*)stats, (int8_t*)lut);
+    SNPMI_LAUNCH_CHECK();
+}
+
+void launch_decode(const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m, const void* lut, int dtype,
+                   int order_c, void* out, uint64_t ld, hipStream_t st) {
+    if (m == 0 || n == 0) return;
+    if (!order_c) {
+        const uint64_t items = ceil_div(n, 1024) * m;
+        const unsigned g = grid_for(items, kBlock / kWave, 256 * 16);
+        if (dtype == SNPMI_DT_F32)
+            k_decode_f<float><<<g, kBlock, 0, st>>>(packed, pitch, n, m, (const float*)lut, (float*)out, ld);
+        else if (dtype == SNPMI_DT_F64)
+            k_decode_f<double><<<g, kBlock, 0, st>>>(packed, pitch, n, m, (const double*)lut, (double*)out, ld);
+        else
+            k_decode_f<int8_t><<<g, kBlock, 0, st>>>(packed, pitch, n, m, (const int8_t*)lut, (int8_t*)out, ld);
+    } else {
+        const uint64_t tiles = ceil_div(n, 64) * ceil_div(m, 64);
+        const unsigned g = grid_for(tiles, 1, 256 * 8);
+        if (dtype == SNPMI_DT_F32)
+            k_decode_c<float><<<g, kBlock, 0, st>>>(packed, pitch, n, m, (const float*)lut, (float*)out, ld);
+        else if (dtype == SNPMI_DT_F64)
+            k_decode_c<double><<<g, kBlock, 0, st>>>(packed, pitch, n, m, (const double*)lut, (double*)out, ld);
+        else
+            k_decode_c<int8_t><<<g, kBlock, 0, st>>>(packed, pitch, n, m, (const int8_t*)lut, (int8_t*)out, ld);
+    }
+    SNPMI_LAUNCH_CHECK();
+}
+
+void launch_repack(const uint8_t* src, uint64_t src_pitch, uint64_t, const uint64_t* idx, uint64_t n_out,
+                   uint64_t n_sid, uint8_t* dst, uint64_t dst_pitch, int*, hipStream_t st) {
+    if (n_sid == 0) return;
+    SNPMI_HIP(hipMemsetAsync(dst, 0, n_sid * dst_pitch, st));
+    if (n_out == 0) return;
+    const unsigned g = grid_for(ceil_div(n_out, 16) * n_sid, kBlock);
+    k_repack<<<g, kBlock, 0, st>>>(src, src_pitch, idx, n_out, n_sid, dst, dst_pitch);
+    SNPMI_LAUNCH_CHECK();
+}
+
+void launch_dense_standardize(void* val, uint64_t rows, uint64_t cols, uint64_t ld, int order_c, int dtype,
+                              int std_kind, double a, double b, int use_stats, void* stats, hipStream_t st) {
+    if (cols == 0 || std_kind == SNPMI_STD_NONE) return;
+    if (!order_c) {
+        const unsigned g = grid_for(cols, kBlock / kWave);
+        if (dtype == SNPMI_DT_F32)
+            k_std_dense_f<float><<<g, kBlock, 0, st>>>((float*)val, rows, cols, ld, std_kind, a, b, use_stats,
+                                                       (float*)stats);
+        else
+            k_std_dense_f<double><<<g, kBlock, 0, st>>>((double*)val, rows, cols, ld, std_kind, a, b, use_stats,
+                                                        (double*)stats);
+    } else {
+        const unsigned g = grid_for(cols, 64);
+        if (dtype == SNPMI_DT_F32)
+            k_std_dense_c<float><<<g, kBlock, 0, st>>>((float*)val, rows, cols, ld, std_kind, a, b, use_stats,
+                                                       (float*)stats);
+        else
+            k_std_dense_c<double><<<g, kBlock, 0, st>>>((double*)val, rows, cols, ld, std_kind, a, b, use_stats,
+                                                        (double*)stats);
+    }
+    SNPMI_LAUNCH_CHECK();
+}
+
+void launch_subset(const void* in, int in_dt, uint64_t rows, uint64_t cols, uint64_t k, int in_c, const uint64_t* ri,
+                   uint64_t nr, const uint64_t* ci, uint64_t nc, int out_c, void* out, int out_dt, hipStream_t st) {
+    const uint64_t total = nr * nc * k;
+    if (total == 0) return;
+    const unsigned g = grid_for(total, kBlock);
+    if (in_dt == SNPMI_DT_F64 && out_dt == SNPMI_DT_F64)
+        k_subset<double, double><<<g, kBlock, 0, st>>>((const double*)in, rows, cols, k, in_c, ri, nr, ci, nc, out_c,
+                                                       (double*)out);
+    else if (in_dt == SNPMI_DT_F32 && out_dt == SNPMI_DT_F64)
+        k_subset<float, double><<<g, kBlock, 0, st>>>((const float*)in, rows, cols, k, in_c, ri, nr, ci, nc, out_c,
+                                                      (double*)out);
+    else if (in_dt == SNPMI_DT_F32 && out_dt == SNPMI_DT_F32)
+        k_subset<float, float><<<g, kBlock, 0, st>>>((const float*)in, rows, cols, k, in_c, ri, nr, ci, nc, out_c,
+                                                     (float*)out);
+    else
+        throw Error(SNPMI_E_ARG, "unsupported subset dtype pair");
+    SNPMI_LAUNCH_CHECK();
+}
+
+void launch_transpose_to_f(const void* in, uint64_t rows, uint64_t cols, int dtype, void* out, uint64_t ld,
+                           hipStream_t st) {
+    if (rows == 0 || cols == 0) return;
+    const unsigned g = grid_for(ceil_div(rows, 64) * ceil_div(cols, 64), 1, 256 * 8);
+    if (dtype == SNPMI_DT_F32)
+        k_transpose<float><<<g, kBlock, 0, st>>>((const float*)in, rows, cols, (float*)out, ld);
+    else
+        k_transpose<double><<<g, kBlock, 0, st>>>((const double*)in, rows, cols, (double*)out, ld);
+    SNPMI_LAUNCH_CHECK();
+}
+
+void launch_grm_extract(const void* tiles, uint64_t, int dtype, const uint64_t* ri, uint64_t nr, const uint64_t* ci,
+                        uint64_t nc, int order_c, double scale, void* out, hipStream_t st) {
+    if (nr == 0 || nc == 0) return;
+    const unsigned g = grid_for(nr * nc, kBlock, 256 * 32);
+    if (dtype == SNPMI_DT_F32)
+        k_grm_extract<float><<<g, kBlock, 0, st>>>((const float*)tiles, ri, nr, ci, nc, order_c, scale, (float*)out);
+    else
+        k_grm_extract<double><<<g, kBlock, 0, st>>>((const double*)tiles, ri, nr, ci, nc, order_c, scale,
+                                                    (double*)out);
+    SNPMI_LAUNCH_CHECK();
+}
+
+void launch_grm_trace(const void* tiles, uint64_t n, int dtype, double* trace_dev, hipStream_t st) {
+    if (dtype == SNPMI_DT_F32)
+        k_grm_trace<float><<<1, kBlock, 0, st>>>((const float*)tiles, n, trace_dev);
+    else
+        k_grm_trace<double><<<1, kBlock, 0, st>>>((const double*)tiles, n, trace_dev);
+    SNPMI_LAUNCH_CHECK();
+}
+
+void launch_dense_trace(const void* K, uint64_t n, int dtype, double* trace_dev, hipStream_t st) {
+    if (dtype == SNPMI_DT_F32)
+        k_dense_trace<float><<<1, kBlock, 0, st>>>((const float*)K, n, trace_dev);
+    else
+        k_dense_trace<double><<<1, kBlock, 0, st>>>((const double*)K, n, trace_dev);
+    SNPMI_LAUNCH_CHECK();
+}
+
+void launch_dense_scale(void* p, uint64_t count, int dtype, double scale, hipStream_t st) {
+    if (count == 0) return;
+    const unsigned g = grid_for(count, kBlock, 256 * 32);
+    if (dtype == SNPMI_DT_F32)
+        k_scale<float><<<g, kBlock, 0, st>>>((float*)p, count, scale);
+    else
+        k_scale<double><<<g, kBlock, 0, st>>>((double*)p, count, scale);
+    SNPMI_LAUNCH_CHECK();
+}
+
+void launch_synth(uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t sid0, uint64_t m, uint64_t seed,
+                  double miss_rate, const double* maf_x, const double* maf_cdf, int n_pts, hipStream_t st) {
+    if (m == 0) return;
+    const unsigned g = grid_for(pitch / 4 * m, kBlock, 256 * 32);
+    k_synth<<<g, kBlock, 0, st>>>(packed, pitch, n, sid0, m, seed, miss_rate, maf_x, maf_cdf, n_pts);
+    SNPMI_LAUNCH_CHECK();
+}
+
+}  // namespace snpmi

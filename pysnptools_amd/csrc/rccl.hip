@@ -1,0 +1,63 @@
+// RCCL over xGMI for the SNP-sharded GRM: one process per GPU, each rank
+// accumulates the upper-triangle K tiles of its SNP blocks, then one in-place
+// ncclAllReduce(sum) of the tile buffer produces K on every rank.  The unique id is
+// exchanged by the caller (bench.py uses torch.distributed's gloo store for that).
+#include <rccl/rccl.h>
+
+#include "snpmi_internal.hpp"
+
+namespace {
+ncclComm_t g_comm = nullptr;
+
+#define SNPMI_NCCL(expr)                                                                     \
+    do {                                                                                     \
+        ncclResult_t r_ = (expr);                                                            \
+        if (r_ != ncclSuccess)                                                               \
+            throw ::snpmi::Error(SNPMI_E_RCCL, std::string(#expr) + ": " + ncclGetErrorString(r_)); \
+    } while (0)
+}  // namespace
+
+using namespace snpmi;
+
+extern "C" {
+
+int snpmi_rccl_unique_id(uint8_t* id, uint64_t id_len) {
+    return guarded([&] {
+        SNPMI_REQUIRE(id && id_len >= sizeof(ncclUniqueId), SNPMI_E_ARG, "id buffer too small");
+        ncclUniqueId u;
+        SNPMI_NCCL(ncclGetUniqueId(&u));
+        std::memcpy(id, &u, sizeof(u));
+    });
+}
+
+int snpmi_rccl_init(int nranks, int rank, const uint8_t* id, uint64_t id_len) {
+    return guarded([&] {
+        SNPMI_REQUIRE(id && id_len >= sizeof(ncclUniqueId), SNPMI_E_ARG, "id buffer too small");
+        SNPMI_REQUIRE(g_comm == nullptr, SNPMI_E_ARG, "RCCL communicator already initialised");
+        (void)device();
+        ncclUniqueId u;
+        std::memcpy(&u, id, sizeof(u));
+        SNPMI_NCCL(ncclCommInitRank(&g_comm, nranks, u, rank));
+    });
+}
+
+int snpmi_rccl_allreduce_sum(void* buf, uint64_t count, int dtype) {
+    return guarded([&] {
+        SNPMI_REQUIRE(g_comm != nullptr, SNPMI_E_ARG, "RCCL communicator not initialised");
+        ncclDataType_t t = dtype == SNPMI_DT_F64 ? ncclFloat64 : ncclFloat32;
+        SNPMI_REQUIRE(dtype == SNPMI_DT_F32 || dtype == SNPMI_DT_F64, SNPMI_E_ARG, "all-reduce dtype must be f32/f64");
+        SNPMI_NCCL(ncclAllReduce(buf, buf, count, t, ncclSum, g_comm, stream()));
+    });
+}
+
+int snpmi_rccl_destroy(void) {
+    return guarded([&] {
+        if (g_comm) {
+            SNPMI_HIP(hipStreamSynchronize(stream()));
+            SNPMI_NCCL(ncclCommDestroy(g_comm));
+            g_comm = nullptr;
+        }
+    });
+}
+
+}  // extern "C"

@@ -1,0 +1,111 @@
+// Internal declarations shared by the libsnpmi translation units.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+
+#include "../../include/snpmi.h"
+
+namespace snpmi {
+
+// ------------------------------------------------------------------ errors
+struct Error : std::runtime_error {
+    int code;
+    Error(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+void set_last_error(const std::string& msg);
+
+#define SNPMI_HIP(expr)                                                                     \
+    do {                                                                                    \
+        hipError_t e_ = (expr);                                                             \
+        if (e_ != hipSuccess)                                                               \
+            throw ::snpmi::Error(SNPMI_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+#define SNPMI_REQUIRE(cond, code, msg)                 \
+    do {                                               \
+        if (!(cond)) throw ::snpmi::Error(code, msg);  \
+    } while (0)
+
+// Run `body` translating exceptions into status codes + thread-local messages.
+template <class F>
+int guarded(F&& body) {
+    try {
+        body();
+        return SNPMI_OK;
+    } catch (const Error& e) {
+        set_last_error(e.what());
+        return e.code;
+    } catch (const std::bad_alloc&) {
+        set_last_error("host allocation failed");
+        return SNPMI_E_NOMEM;
+    } catch (const std::exception& e) {
+        set_last_error(e.what());
+        return SNPMI_E_ARG;
+    }
+}
+
+// ------------------------------------------------------------------ geometry
+constexpr int kTile = 128;                      // GRM tile edge (iids)
+inline uint64_t ceil_div(uint64_t a, uint64_t b) { return (a + b - 1) / b; }
+inline uint64_t round_up(uint64_t a, uint64_t b) { return ceil_div(a, b) * b; }
+inline uint64_t packed_pitch(uint64_t n_iid) { return round_up(ceil_div(n_iid, 4), 64); }
+inline uint64_t n_tiles_1d(uint64_t n) { return ceil_div(n, kTile); }
+inline uint64_t n_tiles_upper(uint64_t n) { uint64_t t = n_tiles_1d(n); return t * (t + 1) / 2; }
+inline size_t dtype_size(int dt) { return dt == SNPMI_DT_F64 ? 8 : dt == SNPMI_DT_F32 ? 4 : 1; }
+
+// ------------------------------------------------------------------ per-device state
+struct Device {
+    int id = -1;
+    hipStream_t stream = nullptr;
+    int cu_count = 0;
+    // grow-only scratch slots
+    enum Slot { S_PACKED, S_PACKED2, S_IDX, S_IDX2, S_LUT, S_STATS, S_OUT, S_TILES, S_K, S_DENSE,
+                S_DENSE2, S_RED, S_NUM };
+    void* buf[S_NUM] = {};
+    size_t cap[S_NUM] = {};
+    void* get(Slot s, size_t bytes);
+    void release();
+};
+
+Device& device();                 // current device of this thread (lazily initialised)
+hipStream_t stream();
+
+// pinned host staging buffers (grow-only, per thread)
+void* pinned(int slot, size_t bytes);
+void release_pinned();
+
+// ------------------------------------------------------------------ kernel launchers (kernels.hip)
+void launch_snp_stats(const uint8_t* packed, uint64_t pitch, uint64_t n_iid, uint64_t n_sid, int count_a1,
+                      int std_kind, double a, double b, int use_stats, int dtype, void* stats, void* lut,
+                      hipStream_t st);
+void launch_decode(const uint8_t* packed, uint64_t pitch, uint64_t n_iid, uint64_t n_sid, const void* lut,
+                   int dtype, int order_c, void* out, uint64_t ld, hipStream_t st);
+void launch_repack(const uint8_t* src, uint64_t src_pitch, uint64_t n_src, const uint64_t* idx, uint64_t n_out,
+                   uint64_t n_sid, uint8_t* dst, uint64_t dst_pitch, int* err_flag, hipStream_t st);
+void launch_dense_standardize(void* val, uint64_t rows, uint64_t cols, uint64_t ld, int order_c, int dtype,
+                              int std_kind, double a, double b, int use_stats, void* stats, hipStream_t st);
+void launch_subset(const void* in, int in_dt, uint64_t rows, uint64_t cols, uint64_t k, int in_order_c,
+                   const uint64_t* ri, uint64_t nr, const uint64_t* ci, uint64_t nc, int out_order_c,
+                   void* out, int out_dt, hipStream_t st);
+void launch_transpose_to_f(const void* in, uint64_t rows, uint64_t cols, int dtype, void* out, uint64_t ld,
+                           hipStream_t st);
+void launch_grm_extract(const void* tiles, uint64_t n, int dtype, const uint64_t* ri, uint64_t nr,
+                        const uint64_t* ci, uint64_t nc, int order_c, double scale, void* out, hipStream_t st);
+void launch_grm_trace(const void* tiles, uint64_t n, int dtype, double* trace_dev, hipStream_t st);
+void launch_dense_scale(void* p, uint64_t count, int dtype, double scale, hipStream_t st);
+void launch_dense_trace(const void* K, uint64_t n, int dtype, double* trace_dev, hipStream_t st);
+void launch_synth(uint8_t* packed, uint64_t pitch, uint64_t n_iid, uint64_t sid0, uint64_t n_sid, uint64_t seed,
+                  double miss_rate, const double* maf_x_dev, const double* maf_cdf_dev, int n_pts, hipStream_t st);
+
+// ------------------------------------------------------------------ MFMA SYRK (syrk.hip)
+void launch_syrk_packed(const uint8_t* packed, uint64_t pitch, uint64_t n_iid, uint64_t n_sid, const void* lut,
+                        int dtype, void* tiles, int accumulate, hipStream_t st);
+void launch_syrk_dense(const void* Z, uint64_t ldz, uint64_t n_iid, uint64_t n_sid, int dtype, void* tiles,
+                       int accumulate, hipStream_t st);
+
+}  // namespace snpmi

@@ -1,0 +1,390 @@
+// SnpKernel GRM on the MFMA cores: K_tiles += Z Z^T over one block of SNPs.
+//
+// Reference: SnpReader._read_kernel (snpreader.py:637-668) computes K = sum_b Z_b Z_b^T with
+// NumPy (OpenBLAS ?syrk for the whole-matrix case, snpdata.py:203-206).  Here:
+//   * K is held as the upper-triangle 128x128 tiles of the symmetric N x N matrix
+//     (tile (ti,tj), ti <= tj, at index tj*(tj+1)/2 + ti, row-major inside) -- half the
+//     HBM bytes, and the unit of the RCCL all-reduce.
+//   * one workgroup (4 waves, 2x2) owns one tile; each wave owns 64x64 of it.
+//   * f32: v_mfma_f32_32x32x2_f32 (exact f32 FMA chain), 2x2 MFMA tiles per wave, BK=32.
+//     f64: v_mfma_f64_16x16x4_f64, 4x4 MFMA tiles per wave, BK=16.
+//   * operand tiles are staged in LDS as [k][iid] (iid contiguous), double-buffered with a
+//     register prefetch of stage s+1 under the MFMAs of stage s.
+//   * PACKED loader: reads 2-bit codes straight from the packed BED block (32 bytes per SNP
+//     per 128-iid tile) and expands them through the per-SNP 4-entry LUT written by
+//     k_snp_stats -- decode + Unit/Beta standardization fused into the GEMM staging, so the
+//     standardized Z never exists in HBM.  DENSE loader: an F-order float matrix (SnpData).
+#include "snpmi_internal.hpp"
+
+namespace snpmi {
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef double f64x4 __attribute__((ext_vector_type(4)));
+
+constexpr int BM = kTile;  // 128
+
+__device__ __forceinline__ void tile_coords(uint64_t L, uint32_t& ti, uint32_t& tj) {
+    uint64_t j = (uint64_t)((sqrt(8.0 * (double)L + 1.0) - 1.0) * 0.5);
+    while ((j + 1) * (j + 2) / 2 <= L) j++;
+    while (j * (j + 1) / 2 > L) j--;
+    tj = (uint32_t)j;
+    ti = (uint32_t)(L - j * (j + 1) / 2);
+}
+
+template <typename T>
+__device__ __forceinline__ T sel4(T l0, T l1, T l2, T l3, uint32_t c) {
+    return (c & 2u) ? ((c & 1u) ? l3 : l2) : ((c & 1u) ? l1 : l0);
+}
+
+// ====================================================================== f32
+namespace f32k {
+constexpr int BK = 32;
+constexpr int LDA = BM;  // floats per LDS row
+
+struct PRegs {
+    uint32_t w;  // 16 codes
+    float4 lut;
+};
+
+__device__ __forceinline__ void load_dense(const float* __restrict__ Z, uint64_t ldz, uint64_t kdim, uint64_t k0,
+                                           uint64_t i0, uint64_t j0, float4 (&ra)[4], float4 (&rb)[4]) {
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const int f = t + 256 * q;
+        const int k = f >> 5, i4 = f & 31;
+        const bool ok = k0 + k < kdim;
+        const uint64_t kk = ok ? k0 + k : kdim - 1;  // clamped address, value zeroed below
+        float4 va = *reinterpret_cast<const float4*>(Z + kk * ldz + i0 + 4 * i4);
+        float4 vb = *reinterpret_cast<const float4*>(Z + kk * ldz + j0 + 4 * i4);
+        if (!ok) {
+            va = make_float4(0.f, 0.f, 0.f, 0.f);
+            vb = va;
+        }
+        ra[q] = va;
+        rb[q] = vb;
+    }
+}
+
+__device__ __forceinline__ void store_dense(float* As, float* Bs, const float4 (&ra)[4], const float4 (&rb)[4]) {
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const int f = t + 256 * q;
+        const int k = f >> 5, i4 = f & 31;
+        *reinterpret_cast<float4*>(As + k * LDA + 4 * i4) = ra[q];
+        *reinterpret_cast<float4*>(Bs + k * LDA + 4 * i4) = rb[q];
+    }
+}
+
+// packed: 256 threads; op = t>>7 (A: rows i0, B: rows j0); 128 threads x 2 dwords cover
+// BK=32 SNPs x 8 dwords (128 iids).
+__device__ __forceinline__ void load_packed(const uint8_t* __restrict__ P, uint64_t pitch, uint64_t kdim, uint64_t k0,
+                                            uint64_t i0, uint64_t j0, const float* __restrict__ lut, PRegs (&r)[2]) {
+    const int t = threadIdx.x;
+    const int op = t >> 7, tt = t & 127;
+    const uint64_t base = op ? j0 : i0;
+#pragma unroll
+    for (int q = 0; q < 2; q++) {
+        const int dw = tt + 128 * q;
+        const int k = dw >> 3, d = dw & 7;
+        const uint64_t kk = k0 + k;
+        if (kk < kdim) {
+            r[q].w = *reinterpret_cast<const uint32_t*>(P + kk * pitch + base / 4 + 4 * d);
+            r[q].lut = *reinterpret_cast<const float4*>(lut + 4 * kk);
+        } else {
+            r[q].w = 0;
+            r[q].lut = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    }
+}
+
+__device__ __forceinline__ void store_packed(float* As, float* Bs, const PRegs (&r)[2]) {
+    const int t = threadIdx.x;
+    const int op = t >> 7, tt = t & 127;
+    float* S = op ? Bs : As;
+#pragma unroll
+    for (int q = 0; q < 2; q++) {
+        const int dw = tt + 128 * q;
+        const int k = dw >> 3, d = dw & 7;
+        const uint32_t w = r[q].w;
+        const float l0 = r[q].lut.x, l1 = r[q].lut.y, l2 = r[q].lut.z, l3 = r[q].lut.w;
+#pragma unroll
+        for (int v = 0; v < 4; v++) {
+            float4 o;
+            o.x = sel4(l0, l1, l2, l3, (w >> (8 * v)) & 3u);
+            o.y = sel4(l0, l1, l2, l3, (w >> (8 * v + 2)) & 3u);
+            o.z = sel4(l0, l1, l2, l3, (w >> (8 * v + 4)) & 3u);
+            o.w = sel4(l0, l1, l2, l3, (w >> (8 * v + 6)) & 3u);
+            *reinterpret_cast<float4*>(S + k * LDA + 16 * d + 4 * v) = o;
+        }
+    }
+}
+
+__device__ __forceinline__ void compute(const float* As, const float* Bs, f32x16 (&acc)[2][2], int wm, int wn,
+                                        int lane) {
+    const int kr = lane >> 5, c = lane & 31;
+#pragma unroll
+    for (int kk = 0; kk < BK / 2; kk++) {
+        const int row = (2 * kk + kr) * LDA;
+        const float a0 = As[row + wm * 64 + c];
+        const float a1 = As[row + wm * 64 + 32 + c];
+        const float b0 = Bs[row + wn * 64 + c];
+        const float b1 = Bs[row + wn * 64 + 32 + c];
+        acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
+        acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
+        acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
+        acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
+    }
+}
+
+template <bool PACKED>
+__global__ __launch_bounds__(256, 2) void k_syrk(const void* __restrict__ src, uint64_t ld, uint64_t kdim,
+                                                 const float* __restrict__ lut, float* __restrict__ tiles,
+                                                 int accumulate) {
+    __shared__ __attribute__((aligned(16))) float lds[2][2][BK * LDA];
+    uint32_t ti, tj;
+    tile_coords(blockIdx.x, ti, tj);
+    const uint64_t i0 = (uint64_t)ti * BM, j0 = (uint64_t)tj * BM;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int wm = wave >> 1, wn = wave & 1;
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int x = 0; x < 2; x++)
+#pragma unroll
+        for (int y = 0; y < 2; y++) acc[x][y] = (f32x16){};
+
+    const uint64_t nst = (kdim + BK - 1) / BK;
+    float4 ra[4], rb[4];
+    PRegs rp[2];
+    if constexpr (PACKED) {
+        load_packed((const uint8_t*)src, ld, kdim, 0, i0, j0, lut, rp);
+        store_packed(lds[0][0], lds[0][1], rp);
+    } else {
+        load_dense((const float*)src, ld, kdim, 0, i0, j0, ra, rb);
+        store_dense(lds[0][0], lds[0][1], ra, rb);
+    }
+    __syncthreads();
+    for (uint64_t s = 0; s < nst; s++) {
+        const int buf = s & 1;
+        const bool more = s + 1 < nst;
+        if (more) {
+            if constexpr (PACKED) load_packed((const uint8_t*)src, ld, kdim, (s + 1) * BK, i0, j0, lut, rp);
+            else load_dense((const float*)src, ld, kdim, (s + 1) * BK, i0, j0, ra, rb);
+        }
+        compute(lds[buf][0], lds[buf][1], acc, wm, wn, lane);
+        if (more) {
+            if constexpr (PACKED) store_packed(lds[buf ^ 1][0], lds[buf ^ 1][1], rp);
+            else store_dense(lds[buf ^ 1][0], lds[buf ^ 1][1], ra, rb);
+        }
+        __syncthreads();
+    }
+    // epilogue: C/D layout of 32x32 MFMA: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
+    float* T = tiles + (uint64_t)blockIdx.x * (BM * BM);
+#pragma unroll
+    for (int mt = 0; mt < 2; mt++)
+#pragma unroll
+        for (int nt = 0; nt < 2; nt++)
+#pragma unroll
+            for (int r = 0; r < 16; r++) {
+                const int row = wm * 64 + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+                const int col = wn * 64 + nt * 32 + (lane & 31);
+                float* p = T + row * BM + col;
+                const float v = acc[mt][nt][r];
+                *p = accumulate ? *p + v : v;
+            }
+}
+}  // namespace f32k
+
+// ====================================================================== f64
+namespace f64k {
+constexpr int BK = 16;
+constexpr int LDA = BM + 16;  // doubles per LDS row: +32 dwords shifts row k+1 by half the banks
+
+struct PRegs {
+    uint32_t w;
+    double l[4];
+};
+
+__device__ __forceinline__ void load_dense(const double* __restrict__ Z, uint64_t ldz, uint64_t kdim, uint64_t k0,
+                                           uint64_t i0, uint64_t j0, double2 (&ra)[4], double2 (&rb)[4]) {
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const int f = t + 256 * q;
+        const int k = f >> 6, i2 = f & 63;
+        const bool ok = k0 + k < kdim;
+        const uint64_t kk = ok ? k0 + k : kdim - 1;
+        double2 va = *reinterpret_cast<const double2*>(Z + kk * ldz + i0 + 2 * i2);
+        double2 vb = *reinterpret_cast<const double2*>(Z + kk * ldz + j0 + 2 * i2);
+        if (!ok) {
+            va = make_double2(0.0, 0.0);
+            vb = va;
+        }
+        ra[q] = va;
+        rb[q] = vb;
+    }
+}
+
+__device__ __forceinline__ void store_dense(double* As, double* Bs, const double2 (&ra)[4], const double2 (&rb)[4]) {
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const int f = t + 256 * q;
+        const int k = f >> 6, i2 = f & 63;
+        *reinterpret_cast<double2*>(As + k * LDA + 2 * i2) = ra[q];
+        *reinterpret_cast<double2*>(Bs + k * LDA + 2 * i2) = rb[q];
+    }
+}
+
+// packed: op = t>>7; 128 threads cover BK=16 SNPs x 8 dwords.
+__device__ __forceinline__ void load_packed(const uint8_t* __restrict__ P, uint64_t pitch, uint64_t kdim, uint64_t k0,
+                                            uint64_t i0, uint64_t j0, const double* __restrict__ lut, PRegs& r) {
+    const int t = threadIdx.x;
+    const int op = t >> 7, tt = t & 127;
+    const int k = tt >> 3, d = tt & 7;
+    const uint64_t base = op ? j0 : i0;
+    const uint64_t kk = k0 + k;
+    if (kk < kdim) {
+        r.w = *reinterpret_cast<const uint32_t*>(P + kk * pitch + base / 4 + 4 * d);
+        const double2 x = *reinterpret_cast<const double2*>(lut + 4 * kk);
+        const double2 y = *reinterpret_cast<const double2*>(lut + 4 * kk + 2);
+        r.l[0] = x.x;
+        r.l[1] = x.y;
+        r.l[2] = y.x;
+        r.l[3] = y.y;
+    } else {
+        r.w = 0;
+        r.l[0] = r.l[1] = r.l[2] = r.l[3] = 0.0;
+    }
+}
+
+__device__ __forceinline__ void store_packed(double* As, double* Bs, const PRegs& r) {
+    const int t = threadIdx.x;
+    const int op = t >> 7, tt = t & 127;
+    const int k = tt >> 3, d = tt & 7;
+    double* S = op ? Bs : As;
+#pragma unroll
+    for (int v = 0; v < 8; v++) {
+        double2 o;
+        o.x = sel4(r.l[0], r.l[1], r.l[2], r.l[3], (r.w >> (4 * v)) & 3u);
+        o.y = sel4(r.l[0], r.l[1], r.l[2], r.l[3], (r.w >> (4 * v + 2)) & 3u);
+        *reinterpret_cast<double2*>(S + k * LDA + 16 * d + 2 * v) = o;
+    }
+}
+
+__device__ __forceinline__ void compute(const double* As, const double* Bs, f64x4 (&acc)[4][4], int wm, int wn,
+                                        int lane) {
+    const int kr = lane >> 4, c = lane & 15;
+#pragma unroll
+    for (int kk = 0; kk < BK / 4; kk++) {
+        const int row = (4 * kk + kr) * LDA;
+        double a[4], b[4];
+#pragma unroll
+        for (int x = 0; x < 4; x++) {
+            a[x] = As[row + wm * 64 + 16 * x + c];
+            b[x] = Bs[row + wn * 64 + 16 * x + c];
+        }
+#pragma unroll
+        for (int x = 0; x < 4; x++)
+#pragma unroll
+            for (int y = 0; y < 4; y++) acc[x][y] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[x], b[y], acc[x][y], 0, 0, 0);
+    }
+}
+
+template <bool PACKED>
+__global__ __launch_bounds__(256, 2) void k_syrk(const void* __restrict__ src, uint64_t ld, uint64_t kdim,
+                                                 const double* __restrict__ lut, double* __restrict__ tiles,
+                                                 int accumulate) {
+    __shared__ __attribute__((aligned(16))) double lds[2][2][BK * LDA];
+    uint32_t ti, tj;
+    tile_coords(blockIdx.x, ti, tj);
+    const uint64_t i0 = (uint64_t)ti * BM, j0 = (uint64_t)tj * BM;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int wm = wave >> 1, wn = wave & 1;
+    f64x4 acc[4][4];
+#pragma unroll
+    for (int x = 0; x < 4; x++)
+#pragma unroll
+        for (int y = 0; y < 4; y++) acc[x][y] = (f64x4){};
+
+    const uint64_t nst = (kdim + BK - 1) / BK;
+    double2 ra[4], rb[4];
+    PRegs rp;
+    if constexpr (PACKED) {
+        load_packed((const uint8_t*)src, ld, kdim, 0, i0, j0, lut, rp);
+        store_packed(lds[0][0], lds[0][1], rp);
+    } else {
+        load_dense((const double*)src, ld, kdim, 0, i0, j0, ra, rb);
+        store_dense(lds[0][0], lds[0][1], ra, rb);
+    }
+    __syncthreads();
+    for (uint64_t s = 0; s < nst; s++) {
+        const int buf = s & 1;
+        const bool more = s + 1 < nst;
+        if (more) {
+            if constexpr (PACKED) load_packed((const uint8_t*)src, ld, kdim, (s + 1) * BK, i0, j0, lut, rp);
+            else load_dense((const double*)src, ld, kdim, (s + 1) * BK, i0, j0, ra, rb);
+        }
+        compute(lds[buf][0], lds[buf][1], acc, wm, wn, lane);
+        if (more) {
+            if constexpr (PACKED) store_packed(lds[buf ^ 1][0], lds[buf ^ 1][1], rp);
+            else store_dense(lds[buf ^ 1][0], lds[buf ^ 1][1], ra, rb);
+        }
+        __syncthreads();
+    }
+    // epilogue: f64 16x16x4 C/D layout: col = lane&15, row = (lane>>4) + 4*r
+    double* T = tiles + (uint64_t)blockIdx.x * (BM * BM);
+#pragma unroll
+    for (int x = 0; x < 4; x++)
+#pragma unroll
+        for (int y = 0; y < 4; y++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const int row = wm * 64 + 16 * x + (lane >> 4) + 4 * r;
+                const int col = wn * 64 + 16 * y + (lane & 15);
+                double* p = T + row * BM + col;
+                const double v = acc[x][y][r];
+                *p = accumulate ? *p + v : v;
+            }
+}
+}  // namespace f64k
+
+}  // namespace
+
+void launch_syrk_packed(const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m, const void* lut, int dtype,
+                        void* tiles, int accumulate, hipStream_t st) {
+    const uint64_t nt = n_tiles_upper(n);
+    if (nt == 0) return;
+    SNPMI_REQUIRE(nt < (1ull << 31), SNPMI_E_ARG, "too many GRM tiles for one launch");
+    if (m == 0) {
+        if (!accumulate) SNPMI_HIP(hipMemsetAsync(tiles, 0, nt * BM * BM * dtype_size(dtype), st));
+        return;
+    }
+    if (dtype == SNPMI_DT_F32)
+        f32k::k_syrk<true><<<(unsigned)nt, 256, 0, st>>>(packed, pitch, m, (const float*)lut, (float*)tiles, accumulate);
+    else
+        f64k::k_syrk<true><<<(unsigned)nt, 256, 0, st>>>(packed, pitch, m, (const double*)lut, (double*)tiles,
+                                                          accumulate);
+    SNPMI_HIP(hipGetLastError());
+}
+
+void launch_syrk_dense(const void* Z, uint64_t ldz, uint64_t n, uint64_t m, int dtype, void* tiles, int accumulate,
+                       hipStream_t st) {
+    const uint64_t nt = n_tiles_upper(n);
+    if (nt == 0) return;
+    SNPMI_REQUIRE(nt < (1ull << 31), SNPMI_E_ARG, "too many GRM tiles for one launch");
+    SNPMI_REQUIRE(ldz % 4 == 0 && ldz >= n_tiles_1d(n) * BM, SNPMI_E_ARG, "dense GRM operand needs padded ldz");
+    if (m == 0) {
+        if (!accumulate) SNPMI_HIP(hipMemsetAsync(tiles, 0, nt * BM * BM * dtype_size(dtype), st));
+        return;
+    }
+    if (dtype == SNPMI_DT_F32)
+        f32k::k_syrk<false><<<(unsigned)nt, 256, 0, st>>>(Z, ldz, m, nullptr, (float*)tiles, accumulate);
+    else
+        f64k::k_syrk<false><<<(unsigned)nt, 256, 0, st>>>(Z, ldz, m, nullptr, (double*)tiles, accumulate);
+    SNPMI_HIP(hipGetLastError());
+}
+
+}  // namespace snpmi

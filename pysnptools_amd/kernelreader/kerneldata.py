@@ -1,0 +1,43 @@
+"""In-memory kernel (reference kernelreader/kerneldata.py)."""
+import numpy as np
+
+from pysnptools_amd.kernelreader.kernelreader import KernelReader
+from pysnptools_amd.kernelstandardizer import DiagKtoN
+from pysnptools_amd.pstreader import PstData
+
+
+class KernelData(KernelReader, PstData):
+    def __init__(self, iid=None, iid0=None, iid1=None, val=None, name=None, parent_string=None, xp=None):
+        self._val = None
+        assert (iid is None) != (iid0 is None and iid1 is None), "Either 'iid' or both 'iid0' 'iid1' must be provided."
+        assert name is None or parent_string is None, "Can't set both 'name' and the deprecated 'parent_string'"
+        ids = lambda x: PstData._fixup_input(x, empty_creator=lambda ignore: np.empty([0, 2], dtype="str"), dtype="str")
+        if iid is not None:
+            self._row = ids(iid)
+            self._col = self._row
+        else:
+            self._row = ids(iid0)
+            self._col = ids(iid1)
+        empty = lambda count: np.empty([count, 0], dtype="str")
+        self._row_property = PstData._fixup_input(None, count=len(self._row), empty_creator=empty, dtype="str")
+        self._col_property = PstData._fixup_input(None, count=len(self._col), empty_creator=empty, dtype="str")
+        self._val = PstData._fixup_input_val(val, row_count=len(self._row), col_count=len(self._col))
+        self._assert_iid0_iid1(check_val=True)
+        self._name = name or parent_string or ""
+        self._std_string_list = []
+
+    @property
+    def val(self):
+        return self._val
+
+    @val.setter
+    def val(self, new_value):
+        self._val = PstData._fixup_input_val(new_value, row_count=len(self._row), col_count=len(self._col))
+        self._assert_iid0_iid1(check_val=True)
+
+    def allclose(self, value, equal_nan=True):
+        return PstData.allclose(self, value, equal_nan=equal_nan)
+
+    def standardize(self, standardizer=DiagKtoN(), return_trained=False, force_python_only=False, num_threads=None):
+        return standardizer.standardize(self, return_trained=return_trained, force_python_only=force_python_only,
+                                        num_threads=num_threads)

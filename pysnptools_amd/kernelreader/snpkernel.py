@@ -1,0 +1,112 @@
+"""SnpKernel: the lazy GRM of a SnpReader + standardizer (reference kernelreader/snpkernel.py).
+
+Reading it runs the fused GPU GRM (SnpReader._read_kernel); for constant (trained)
+standardizers an iid subset is pushed down to the SNP reader so only the requested
+individuals are decoded (snpkernel.py:81-82, 98-99).
+"""
+import logging
+
+import numpy as np
+
+from pysnptools_amd.kernelreader.kerneldata import KernelData
+from pysnptools_amd.kernelreader.kernelreader import KernelReader
+from pysnptools_amd.kernelstandardizer import DiagKtoN
+from pysnptools_amd.standardizer import Identity as SS_Identity
+
+
+class SnpKernel(KernelReader):
+    def __init__(self, snpreader, standardizer=None, block_size=None):
+        super(SnpKernel, self).__init__()
+        assert standardizer is not None, "'standardizer' must be provided"
+        self.snpreader = snpreader
+        self.standardizer = standardizer
+        self.block_size = block_size
+
+    @property
+    def row(self):
+        return self.snpreader.iid
+
+    @property
+    def col(self):
+        return self._col if hasattr(self, "_col") else self.snpreader.iid
+
+    def __repr__(self):
+        return self._internal_repr(self.standardizer)
+
+    def _internal_repr(self, standardizer):
+        s = "SnpKernel({0},standardizer={1}".format(self.snpreader, standardizer)
+        if self.block_size is not None:
+            s += ",block_size={0}".format(self.block_size)
+        return s + ")"
+
+    def copyinputs(self, copier):
+        copier.input(self.snpreader)
+        copier.input(self.standardizer)
+
+    def _read(self, row_index_or_none, col_index_or_none, order, dtype, force_python_only, view_ok, num_threads):
+        dtype = np.dtype(dtype)
+        if (self.standardizer.is_constant and row_index_or_none is not None and col_index_or_none is not None
+                and np.array_equal(row_index_or_none, col_index_or_none)):
+            return self.snpreader[row_index_or_none, :]._read_kernel(self.standardizer, self.block_size, order, dtype,
+                                                                     force_python_only, view_ok,
+                                                                     num_threads=num_threads)
+        whole = self.snpreader._read_kernel(self.standardizer, self.block_size, order, dtype, force_python_only,
+                                            view_ok, num_threads=num_threads)
+        val, _ = self._apply_sparray_or_slice_to_val(whole, row_index_or_none, col_index_or_none, order, dtype,
+                                                     force_python_only, num_threads)
+        return val
+
+    def __getitem__(self, iid_indexer_and_snp_indexer):
+        if isinstance(iid_indexer_and_snp_indexer, tuple):
+            row_index_or_none, col_index_or_none = iid_indexer_and_snp_indexer
+        else:
+            row_index_or_none = col_index_or_none = iid_indexer_and_snp_indexer
+        if (self.standardizer.is_constant and row_index_or_none is not None and col_index_or_none is not None
+                and np.array_equal(row_index_or_none, col_index_or_none)):
+            return SnpKernel(self.snpreader[row_index_or_none, :], self.standardizer, block_size=self.block_size)
+        return KernelReader.__getitem__(self, iid_indexer_and_snp_indexer)
+
+    def _read_with_standardizing(self, to_kerneldata, kernel_standardizer=DiagKtoN(), return_trained=False,
+                                 num_threads=None):
+        """(K, snp_trained, kernel_trained) as FaST-LMM uses it (snpkernel.py:104-132).  With the
+        default DiagKtoN, the trace and scale run on the GPU before K is copied out."""
+        logging.info("Starting '_read_with_standardizing'")
+        if to_kerneldata:
+            from pysnptools_amd.standardizer import DiagKtoNTrained
+            from pysnptools_amd.standardizer.diag_K_to_N import DiagKtoN as _DiagKtoN
+
+            fused = type(kernel_standardizer) is _DiagKtoN
+            res = self.snpreader._read_kernel(self.standardizer, block_size=self.block_size, return_trained=True,
+                                              num_threads=num_threads, _diag_k_to_n=fused)
+            val, snp_trained = res[0], res[1]
+            kernel = KernelData(iid=self.snpreader.iid, val=val, name=str(self))
+            if fused and res[2] is not None:
+                kernel_trained = DiagKtoNTrained(res[2])
+            else:
+                kernel, kernel_trained = kernel.standardize(kernel_standardizer, return_trained=True,
+                                                            num_threads=num_threads)
+        else:
+            snpdata, snp_trained = self.snpreader.read().standardize(self.standardizer, return_trained=True,
+                                                                     num_threads=num_threads)
+            snpdata, kernel_trained = snpdata.standardize(kernel_standardizer, return_trained=True,
+                                                          num_threads=num_threads)
+            kernel = SnpKernel(snpdata, SS_Identity())
+        logging.info("Ending '_read_with_standardizing'")
+        return (kernel, snp_trained, kernel_trained) if return_trained else kernel
+
+    @property
+    def sid(self):
+        return self.snpreader.sid
+
+    @property
+    def sid_count(self):
+        return self.snpreader.sid_count
+
+    @property
+    def pos(self):
+        return self.snpreader.pos
+
+    def read_snps(self, order="F", dtype=np.float64, force_python_only=False, view_ok=False, num_threads=None):
+        return self.snpreader.read(order=order, dtype=np.dtype(dtype), force_python_only=force_python_only,
+                                   view_ok=view_ok, num_threads=num_threads).standardize(self.standardizer,
+                                                                                          num_threads=num_threads)

@@ -1,0 +1,3 @@
+from pysnptools_amd.pstreader.pstreader import PstReader
+from pysnptools_amd.pstreader.pstdata import PstData
+from pysnptools_amd.pstreader._subset import _PstSubset

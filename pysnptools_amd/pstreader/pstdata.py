@@ -1,0 +1,109 @@
+"""In-memory matrix (reference pstreader/pstdata.py): ids, properties and a ``val`` ndarray."""
+import numpy as np
+
+from pysnptools_amd.pstreader.pstreader import PstReader
+
+
+def _empty_ids(count):
+    return np.empty([count or 0, 0], dtype="str")
+
+
+class PstData(PstReader):
+    """A PstReader whose values are already in memory."""
+
+    def __init__(self, row, col, val, row_property=None, col_property=None, name=None, parent_string=None,
+                 copyinputs_function=None):
+        super(PstData, self).__init__()
+        self._val = None
+        self._row = PstData._fixup_input(row)
+        self._col = PstData._fixup_input(col)
+        if self._row.dtype == self._col.dtype and np.array_equal(self._row, self._col):
+            self._col = self._row
+        self._row_property = PstData._fixup_input(row_property, count=len(self._row))
+        self._col_property = PstData._fixup_input(col_property, count=len(self._col))
+        self._val = PstData._fixup_input_val(val, row_count=len(self._row), col_count=len(self._col))
+        self._name = name or parent_string or ""
+
+    @staticmethod
+    def _fixup_input(input, count=None, empty_creator=_empty_ids, dtype=None):
+        if input is None or len(input) == 0:
+            input = empty_creator(count)
+        elif not isinstance(input, np.ndarray):
+            input = np.array(input, dtype=dtype)
+        assert count is None or len(input) == count, "Expect length of {0} for input {1}".format(count, input)
+        return input
+
+    @staticmethod
+    def _fixup_input_val(input, row_count, col_count, empty_creator=None, _require_float32_64=True, xp=None):
+        if input is None:
+            assert row_count == 0 or col_count == 0, "If val is None, either row_count or col_count must be 0"
+            input = np.empty([row_count, col_count], dtype=np.float64)
+        elif not isinstance(input, np.ndarray):
+            input = np.array(input, dtype=np.float64)
+        elif _require_float32_64 and input.dtype not in (np.float32, np.float64):
+            input = np.array(input, dtype=np.float64)
+        assert len(input.shape) in (2, 3), "Expect val to be two or three dimensional."
+        assert input.shape[0] == row_count, \
+            "Expect number of rows ({0}) in val to match the number of row names given ({1})".format(input.shape[0], row_count)
+        assert input.shape[1] == col_count, \
+            "Expect number of columns ({0}) in val to match the number of column names given ({1})".format(input.shape[1], col_count)
+        return input
+
+    def __repr__(self):
+        return "{0}({1})".format(self.__class__.__name__, self._name) if self._name else "{0}()".format(self.__class__.__name__)
+
+    @property
+    def row(self):
+        return self._row
+
+    @property
+    def col(self):
+        return self._col
+
+    @property
+    def row_property(self):
+        return self._row_property
+
+    @property
+    def col_property(self):
+        return self._col_property
+
+    @property
+    def val(self):
+        return self._val
+
+    @val.setter
+    def val(self, new_value):
+        self._val = PstData._fixup_input_val(new_value, row_count=len(self._row), col_count=len(self._col))
+
+    @property
+    def val_shape(self):
+        return None if self._val.ndim == 2 else self._val.shape[2]
+
+    def copyinputs(self, copier):
+        pass
+
+    def __eq__(a, b):
+        return a.allclose(b, equal_nan=False)
+
+    def allclose(self, value, equal_nan=True):
+        def same(x, y):
+            if x.dtype.kind == "f" and y.dtype.kind == "f":
+                return x.shape == y.shape and np.allclose(x, y, equal_nan=True)
+            return np.array_equal(x, y)
+
+        try:
+            return (same(self.row, value.row) and same(self.col, value.col)
+                    and same(self.row_property, value.row_property) and same(self.col_property, value.col_property)
+                    and np.allclose(self.val, value.val, equal_nan=equal_nan))
+        except Exception:
+            return False
+
+    _read_accepts_slices = True
+
+    def _read(self, row_index_or_none, col_index_or_none, order, dtype, force_python_only, view_ok, num_threads):
+        val, shares = self._apply_sparray_or_slice_to_val(self.val, row_index_or_none, col_index_or_none, order,
+                                                          dtype, force_python_only, num_threads)
+        if shares and not view_ok:
+            val = val.copy(order="K")
+        return val

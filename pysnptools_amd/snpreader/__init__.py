@@ -1,0 +1,3 @@
+from pysnptools_amd.snpreader.snpreader import SnpReader
+from pysnptools_amd.snpreader.snpdata import SnpData
+from pysnptools_amd.snpreader.bed import Bed

@@ -1,0 +1,229 @@
+"""SnpReader: iid x sid genotype readers and the GRM entry point (reference snpreader/snpreader.py).
+
+``_read_kernel`` (snpreader.py:623-668) is where the hot path is dispatched:
+
+* a ``Bed`` (optionally sliced) with Unit/Beta/trained/Identity standardization runs as ONE
+  native call, ``snpmi_grm_bed_{f32,f64}``: packed codes are uploaded once, standardized
+  through per-SNP LUTs inside the MFMA SYRK staging, and K accumulates in HBM;
+* an in-memory ``SnpData`` runs ``snpmi_grm_dense_{f32,f64}`` (standardize + SYRK on the GPU);
+* anything else (custom readers or standardizers) follows the reference's block loop,
+  each block's Z Z^T still computed on the GPU.
+
+``block_size`` keeps its meaning for the generic loop; the native paths chunk SNPs
+internally (the result differs only by floating-point summation order).
+"""
+import logging
+import warnings
+
+import numpy as np
+
+from pysnptools_amd import _native as N
+from pysnptools_amd.pstreader import PstReader
+from pysnptools_amd.util import get_num_threads
+
+
+class SnpReader(PstReader):
+    """Reader of a matrix of SNP values: rows are individuals (iid), columns SNPs (sid)."""
+
+    def __init__(self, *args, **kwargs):
+        super(SnpReader, self).__init__(*args, **kwargs)
+
+    @property
+    def iid(self):
+        return self.row
+
+    @property
+    def iid_count(self):
+        return self.row_count
+
+    @property
+    def sid(self):
+        return self.col
+
+    @property
+    def sid_count(self):
+        return self.col_count
+
+    @property
+    def pos(self):
+        return self.col_property
+
+    @property
+    def row_property(self):
+        if not hasattr(self, "_row_property"):
+            self._row_property = np.empty((self.row_count, 0))
+        return self._row_property
+
+    def _read(self, iid_index_or_none, sid_index_or_none, order, dtype, force_python_only, view_ok, num_threads):
+        raise NotImplementedError
+
+    def read(self, order="F", dtype=np.float64, force_python_only=False, view_ok=False, num_threads=None,
+             _require_float32_64=True):
+        """Values as a :class:`SnpData` (order 'F' | 'C' | 'A', dtype float64 | float32 [| int8 for Bed])."""
+        from pysnptools_amd.snpreader.snpdata import SnpData
+
+        dtype = np.dtype(dtype)
+        val = self._read(None, None, order, dtype, force_python_only, view_ok, num_threads)
+        return SnpData(self.iid, self.sid, val, pos=self.pos, name=str(self), _require_float32_64=_require_float32_64)
+
+    def iid_to_index(self, list):
+        return self.row_to_index(list)
+
+    def sid_to_index(self, list):
+        return self.col_to_index(list)
+
+    def __getitem__(self, iid_indexer_and_snp_indexer):
+        from pysnptools_amd.snpreader._subset import _SnpSubset
+
+        iid_indexer, snp_indexer = iid_indexer_and_snp_indexer
+        return _SnpSubset(self, iid_indexer, snp_indexer)
+
+    def read_kernel(self, standardizer=None, block_size=None, order="A", dtype=np.float64, force_python_only=False,
+                    view_ok=False, num_threads=None):
+        """The iid x iid kernel (GRM) of the standardized SNPs, as a KernelData."""
+        assert standardizer is not None, "'standardizer' must be provided"
+        from pysnptools_amd.kernelreader import SnpKernel
+
+        snpkernel = SnpKernel(self, standardizer=standardizer, block_size=block_size)
+        return snpkernel.read(order, np.dtype(dtype), force_python_only, view_ok, num_threads)
+
+    def kernel(self, standardizer, allowlowrank=False, block_size=10000, blocksize=None, num_threads=None):
+        warnings.warn(".kernel(...) is deprecated. Use '.read_kernel(...).val", DeprecationWarning)
+        if blocksize is not None:
+            block_size = blocksize
+        return self._read_kernel(standardizer, block_size=block_size, num_threads=num_threads)
+
+    # ------------------------------------------------------------------ GRM
+    @staticmethod
+    def _as_snpdata(snpreader, standardizer, force_python_only, order, dtype, num_threads):
+        """(standardized SnpData, trained standardizer), reusing in-memory data when possible
+        (snpreader.py:606-621)."""
+        from pysnptools_amd import standardizer as stdizer
+
+        dtype = np.dtype(dtype)
+        if (hasattr(snpreader, "val") and snpreader.val.dtype == dtype and isinstance(standardizer, stdizer.Identity)
+                and (order == "A" or (order == "C" and snpreader.val.flags["C_CONTIGUOUS"])
+                     or (order == "F" and snpreader.val.flags["F_CONTIGUOUS"]))):
+            return snpreader, stdizer.Identity()
+        return snpreader.read(order=order, dtype=dtype).standardize(standardizer, return_trained=True,
+                                                                    force_python_only=force_python_only,
+                                                                    num_threads=num_threads)
+
+    def _read_kernel(self, standardizer, block_size=None, order="A", dtype=np.float64, force_python_only=False,
+                     view_ok=False, return_trained=False, num_threads=None, _diag_k_to_n=False):
+        dtype = np.dtype(dtype)
+        fast = _native_grm(self, standardizer, dtype, num_threads, _diag_k_to_n)
+        if fast is not None:
+            K, trained, factor = fast
+            K = K.T if order == "F" else K  # K is exactly symmetric: .T is its F-contiguous form
+            if _diag_k_to_n:
+                return K, trained, factor
+            return (K, trained) if return_trained else K
+        K, trained = self._read_kernel_blocks(standardizer, block_size, order, dtype, force_python_only, num_threads)
+        if _diag_k_to_n:
+            return K, trained, None
+        return (K, trained) if return_trained else K
+
+    def _read_kernel_blocks(self, standardizer, block_size, order, dtype, force_python_only, num_threads):
+        """The reference's generic loop (snpreader.py:629-668) for readers/standardizers the
+        fused path does not cover; each block's Z Z^T runs on the GPU."""
+        from pysnptools_amd import standardizer as stdizer
+
+        if block_size is None or self.sid_count <= block_size or self.sid_count <= self.iid_count:
+            data, trained = SnpReader._as_snpdata(self, standardizer, force_python_only, "A", dtype, num_threads)
+            K = data._read_kernel(stdizer.Identity(), order=order, dtype=dtype, view_ok=False, num_threads=num_threads)
+            return K, trained
+        K = np.zeros([self.iid_count, self.iid_count], dtype=dtype, order="C" if order == "A" else order)
+        trained_list = []
+        logging.info("reading %d SNPs in blocks of %d", self.sid_count, block_size)
+        for start in range(0, self.sid_count, block_size):
+            data, trained = SnpReader._as_snpdata(self[:, start:start + block_size], standardizer, force_python_only,
+                                                  "A", dtype, num_threads)
+            trained_list.append(trained)
+            K += data._read_kernel(stdizer.Identity(), order=order, dtype=dtype, view_ok=False, num_threads=num_threads)
+        return K, standardizer._merge_trained(trained_list)
+
+    def copyinputs(self, copier):
+        raise NotImplementedError
+
+    @staticmethod
+    def _name_of_other_file(filename, remove_suffix, add_suffix):
+        if filename.lower().endswith(remove_suffix.lower()):
+            filename = filename[0:-1 - len(remove_suffix)]
+        return filename + "." + add_suffix
+
+    @property
+    def val_shape(self):
+        return None
+
+
+# ---------------------------------------------------------------------- native dispatch
+def _resolve(reader):
+    """(innermost reader, absolute iid index or None, absolute sid index or None)."""
+    from pysnptools_amd.pstreader._subset import _PstSubset
+
+    if isinstance(reader, _PstSubset):
+        base, r0, c0 = _resolve(reader._internal)
+        reader._run_once()
+        rows, cols = reader._composed_indices(None, None)
+        rows = rows if r0 is None else (r0 if rows is None else r0[rows])
+        cols = cols if c0 is None else (c0 if cols is None else c0[cols])
+        return base, rows, cols
+    return reader, None, None
+
+
+def _trained_from(standardizer, kind, a, b, sid, stats):
+    from pysnptools_amd import standardizer as stdizer
+
+    if kind == N.STD_NONE:
+        return stdizer.Identity()
+    if isinstance(standardizer, (stdizer.UnitTrained, stdizer.BetaTrained)):
+        return standardizer
+    if kind == N.STD_UNIT:
+        return stdizer.UnitTrained(sid, stats)
+    return stdizer.BetaTrained(standardizer.a, standardizer.b, sid, stats)
+
+
+def _native_grm(reader, standardizer, dtype, num_threads, diag_k_to_n):
+    """Fused GPU GRM for Bed / SnpData sources; None when not applicable."""
+    from pysnptools_amd.snpreader.bed import Bed
+    from pysnptools_amd.standardizer.standardizer import _std_args
+
+    if dtype not in (np.float32, np.float64):
+        return None
+    args = _std_args(standardizer)
+    if args is None:
+        return None
+    kind, a, b, use_stats, given, _ = args
+    base, rows, cols = _resolve(reader)
+    sid = reader.sid
+    if use_stats:
+        stats = np.ascontiguousarray(standardizer.stats_for(sid), dtype=dtype)
+    else:
+        stats = np.empty((len(sid), 2), dtype=dtype)
+    n = reader.iid_count
+    K = np.empty((n, n), dtype=dtype)
+    factor = np.full(1, np.nan, dtype=np.float64)
+    fptr = factor.ctypes.data_as(N.ctypes.POINTER(N.ctypes.c_double))
+    sfx = N.suffix(dtype)
+    if isinstance(base, Bed):
+        base._run_once()
+        ri, ci = N.index_array(rows), N.index_array(cols)
+        N.call("snpmi_grm_bed_" + sfx, base.filename.encode(), base.iid_count, base.sid_count, int(bool(base.count_A1)),
+               N.ptr(ri), n, N.ptr(ci), len(sid), kind, a, b, int(use_stats), N.ptr(stats), int(bool(diag_k_to_n)),
+               fptr, N.ptr(K), get_num_threads(num_threads))
+    elif hasattr(base, "val") and base.val.ndim == 2:
+        if rows is None and cols is None:
+            val = base.val
+        else:
+            val = base._read(rows, cols, "A", base.val.dtype, False, True, num_threads)
+        val = val if val.dtype == dtype else val.astype(dtype, order="K")
+        if not (val.flags["C_CONTIGUOUS"] or val.flags["F_CONTIGUOUS"]):
+            val = np.ascontiguousarray(val)
+        order_c = 1 if val.flags["C_CONTIGUOUS"] else 0
+        N.call("snpmi_grm_dense_" + sfx, N.ptr(val), val.shape[0], val.shape[1], order_c, kind, a, b, int(use_stats),
+               N.ptr(stats), int(bool(diag_k_to_n)), fptr, N.ptr(K))
+    else:
+        return None
+    trained = _trained_from(standardizer, kind, a, b, sid, stats)
+    return K, trained, float(factor[0])

@@ -1,0 +1,40 @@
+"""Unit standardizer: mean 0, std 1 per SNP, missing -> 0 (reference standardizer/unit.py)."""
+import warnings
+
+import numpy as np
+
+from pysnptools_amd.standardizer.standardizer import Standardizer
+
+
+class Unit(Standardizer):
+    def __init__(self):
+        super(Unit, self).__init__()
+
+    def __repr__(self):
+        return "{0}()".format(self.__class__.__name__)
+
+    def standardize(self, snps, block_size=None, return_trained=False, force_python_only=False, num_threads=None):
+        from pysnptools_amd.standardizer.unittrained import UnitTrained
+
+        if block_size is not None:
+            warnings.warn("block_size is deprecated (and not needed, since standardization is in-place",
+                          DeprecationWarning)
+        if hasattr(snps, "val"):
+            val = snps.val
+        else:
+            warnings.warn("standardizing an ndarray instead of a SnpData is deprecated", DeprecationWarning)
+            val = snps
+        stats = self._standardize_unit_and_beta(val, is_beta=False, a=np.nan, b=np.nan, apply_in_place=True,
+                                                use_stats=False, stats=None, num_threads=num_threads,
+                                                force_python_only=force_python_only)
+        if return_trained:
+            assert hasattr(snps, "val"), "return_trained=True requires that snps be a SnpData"
+            return snps, UnitTrained(snps.sid, stats)
+        return snps
+
+    def _merge_trained(self, trained_list):
+        from pysnptools_amd.standardizer.unittrained import UnitTrained
+
+        sid = np.concatenate([t.sid for t in trained_list])
+        stats = np.concatenate([t.stats for t in trained_list])
+        return UnitTrained(sid, stats)

@@ -1,0 +1,400 @@
+"""Parity of the HIP path (through the C ABI / mirrored API) with the oracle and the
+reference goldens.  Bars: decode/indexing bit-exact; standardized values f32 within 1e-5
+relative (f64 within 1e-10); GRM max|dK| / max diag(K_ref) <= 1e-5 (f32), 1e-10 (f64)."""
+import ctypes
+import os
+import tempfile
+
+import numpy as np
+import pytest
+
+from conftest import DATA, GOLDEN
+from oracle import oracle as O
+from pysnptools_amd import _native as N
+from pysnptools_amd.kernelreader import KernelData, SnpKernel
+from pysnptools_amd.snpreader import Bed, SnpData
+from pysnptools_amd.standardizer import Beta, BetaTrained, DiagKtoN, Identity, Unit, UnitTrained
+from pysnptools_amd.util import sub_matrix
+
+pytestmark = pytest.mark.gpu
+
+SHAPES = {"n300": (300, 1015), "snpgen": (1000, 5), "dist_x": (100, 100), "toydata": (500, 10000)}
+
+
+def g(name):
+    return np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False)
+
+
+def bed(name, count_A1=False):
+    return Bed(os.path.join(DATA, name + ".bed"), count_A1=count_A1)
+
+
+def body(name):
+    return O.read_bed_bytes(os.path.join(DATA, name + ".bed"))
+
+
+def from_i8(v):
+    out = v.astype(np.float64)
+    out[v == -127] = np.nan
+    return out
+
+
+def rel_close(got, exp, tol):
+    got = np.asarray(got, dtype=np.float64)
+    exp = np.asarray(exp, dtype=np.float64)
+    assert got.shape == exp.shape
+    both_nan = np.isnan(got) & np.isnan(exp)
+    d = np.abs(got - exp)
+    bound = tol * np.maximum(np.abs(exp), 1e-30)
+    bad = ~(both_nan | (d <= bound) | ((exp == 0) & (d <= tol)))
+    assert not bad.any(), "max rel err %g at %s" % ((d / np.maximum(np.abs(exp), 1e-30))[bad].max(), np.argwhere(bad)[:3])
+
+
+def grm_close(K, Kref, tol):
+    Kref = np.asarray(Kref, dtype=np.float64)
+    scale = np.abs(np.diag(Kref)).max()
+    err = np.abs(np.asarray(K, dtype=np.float64) - Kref).max() / scale
+    assert err <= tol, "GRM max|dK|/max diag = %g > %g" % (err, tol)
+    rel_close(np.diag(K), np.diag(Kref), tol)
+
+
+def test_device_visible():
+    assert N.device_count() >= 1
+
+
+# ---------------------------------------------------------------------------------- decode
+@pytest.mark.parametrize("name", ["n300", "snpgen", "dist_x", "toydata"])
+@pytest.mark.parametrize("dtype", [np.float32, np.float64, np.int8])
+@pytest.mark.parametrize("order", ["F", "C"])
+def test_decode_bit_exact(name, dtype, order):
+    n, m = SHAPES[name]
+    got = bed(name).read(order=order, dtype=dtype, _require_float32_64=False).val
+    assert got.dtype == dtype and got.flags[order + "_CONTIGUOUS"] and got.shape == (n, m)
+    exp = O.decode(body(name), n, m, order=order, dtype=dtype)
+    if name != "toydata":
+        assert np.array_equal(O.decode(body(name), n, m, dtype=np.int8), g(name)["val_i8"])
+    assert np.array_equal(got, exp, equal_nan=True)
+
+
+def test_decode_count_a1():
+    got = bed("n300", count_A1=True).read(dtype=np.int8, _require_float32_64=False).val
+    assert np.array_equal(got, g("n300")["val_a1_i8"])
+    f = bed("n300", count_A1=True).read(dtype=np.float32).val
+    assert np.array_equal(f, 2 - from_i8(g("n300")["val_i8"]).astype(np.float32), equal_nan=True)
+
+
+@pytest.mark.parametrize("order", ["F", "C"])
+@pytest.mark.parametrize("dtype", [np.float32, np.float64, np.int8])
+def test_decode_subsets(order, dtype):
+    b = bed("n300")
+    full = O.decode(body("n300"), 300, 1015, dtype=dtype)
+    rng = np.random.default_rng(0)
+    perm = rng.permutation(300)[:123]
+    cases = [(slice(None, None, -2), slice(1014, 0, -2)), (perm, slice(3, 900, 7)), ([5], [7]),
+             (np.arange(300) % 3 == 0, [-1, 0, 500]), (slice(10, 11), slice(None))]
+    for ri, ci in cases:
+        sub = b[ri, ci]
+        got = sub.read(order=order, dtype=dtype, _require_float32_64=False).val
+        rows = np.arange(300)[ri]
+        cols = np.arange(1015)[ci]
+        assert np.array_equal(got, full[np.ix_(np.atleast_1d(rows), np.atleast_1d(cols))], equal_nan=True)
+    with pytest.raises(IndexError):
+        b[[300], :].read()
+
+
+@pytest.mark.parametrize("n_iid", [1, 2, 3, 5, 17, 297, 298, 299])
+def test_decode_padding_round_trip(n_iid):
+    """N % 4 != 0: the last byte's pad bits must be ignored (test.py:689-746)."""
+    v = from_i8(g("n300")["val_i8"][:n_iid, :33])
+    d = SnpData(iid=[["f", str(i)] for i in range(n_iid)], sid=["s%d" % j for j in range(33)], val=v)
+    with tempfile.TemporaryDirectory() as tmp:
+        b = Bed.write(os.path.join(tmp, "p.bed"), d, count_A1=False)
+        for dtype in (np.float32, np.float64):
+            for order in ("F", "C"):
+                assert np.array_equal(b.read(order=order, dtype=dtype).val, v.astype(dtype), equal_nan=True)
+        st = b.read(dtype=np.float64).standardize(Unit(), return_trained=True)[1].stats
+        ref = v.copy(order="F")
+        np.testing.assert_array_equal(st, O.standardize_native(ref))
+
+
+# ---------------------------------------------------------------------------------- standardize
+@pytest.mark.parametrize("name", ["n300", "snpgen"])
+@pytest.mark.parametrize("tag,dtype,tol", [("f64", np.float64, 1e-10), ("f32", np.float32, 1e-5)])
+@pytest.mark.parametrize("order", ["F", "C"])
+def test_standardize_vs_reference(name, tag, dtype, tol, order):
+    G = g(name)
+    for std, key in ((Unit(), "unit"), (Beta(1, 25), "beta")):
+        d, tr = bed(name).read(order=order, dtype=dtype).standardize(std, return_trained=True)
+        rel_close(d.val, G["%s_%s" % (key, tag)], tol)
+        rel_close(tr.stats, G["%s_stats_%s" % (key, tag)], tol)
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+@pytest.mark.parametrize("order", ["F", "C"])
+def test_unit_standardize_bit_exact_vs_oracle(dtype, order):
+    v = O.decode(body("n300"), 300, 1015, dtype=dtype, order=order)
+    st = O.standardize_native(v)
+    d, tr = bed("n300").read(order=order, dtype=dtype).standardize(Unit(), return_trained=True)
+    assert np.array_equal(d.val, v)
+    assert np.array_equal(np.asarray(tr.stats), st)
+    vb = O.decode(body("n300"), 300, 1015, dtype=dtype, order=order)
+    O.standardize_native(vb, True, 1, 25)
+    db = bed("n300").read(order=order, dtype=dtype).standardize(Beta(1, 25))
+    rel_close(db.val, vb, 1e-12 if dtype == np.float64 else 1e-6)
+
+
+def test_doctest_goldens():
+    """standardizer.py:17-42, beta.py:23, snpkernel.py:41, kernelreader.py:293."""
+    b = bed("n300")
+    assert "%.6f" % b.read().standardize(Unit()).val[0, 0] == "0.229416"
+    assert "%.6f" % b.read().standardize(Beta(1, 25)).val[0, 0] == "0.680802"
+    train, tr = Unit().standardize(b[range(10, 300), :].read(), return_trained=True)
+    assert "%.6f" % train.val[0, 0] == "0.233550"
+    np.testing.assert_allclose(tr.stats[0], [1.94827586, 0.22146953], atol=1e-8)
+    test = b[range(0, 10), :].read().standardize(tr)
+    assert test.val[0, 0] == 0.23354968324845735
+    k = bed("toydata").read_kernel(Unit())
+    assert "%.6f" % k.val[0, 0] == "9923.069928"
+    kd = SnpKernel(bed("toydata"), Unit()).read().standardize()
+    assert "%.6f" % kd.val[0, 0] == "0.992307"
+
+
+def test_trained_apply_vs_reference():
+    G = g("n300")
+    b = bed("n300")
+    for std, key in ((Unit(), "unit"), (Beta(1, 25), "beta")):
+        _, tr = b[10:, :].read().standardize(std, return_trained=True)
+        rel_close(tr.stats, G[key + "_train_stats"], 1e-12)
+        te = b[:10, :].read().standardize(tr)
+        rel_close(te.val, G[key + "_test"], 1e-10)
+
+
+@pytest.mark.parametrize("tag,dtype,tol", [("f64", np.float64, 1e-10), ("f32", np.float32, 1e-5)])
+@pytest.mark.parametrize("order", ["F", "C"])
+def test_edge_cases(tag, dtype, tol, order):
+    """NaN, SNC and all-missing columns; train then apply (kernelreader/test.py:56-111)."""
+    G = g("edge")
+    for std, key in ((Unit(), "unit"), (Beta(2, 10), "beta")):
+        k = "%s_%s_%s" % (key, tag, order)
+        x0 = SnpData(iid=[["a", str(i)] for i in range(3)], sid=[str(j) for j in range(20)],
+                     val=np.array(G["x0"], dtype=dtype, order=order))
+        x0, tr = x0.standardize(std, return_trained=True)
+        rel_close(x0.val, G[k + "_train"], tol)
+        rel_close(tr.stats, G[k + "_stats"], tol)
+        assert np.isinf(tr.stats[1, 1]) and np.all(x0.val[:, 1] == 0) and x0.val[0, 2] == 0
+        assert np.all(x0.val[:, 5] == 0)
+        x1 = SnpData(iid=[["b", str(i)] for i in range(2)], sid=[str(j) for j in range(20)],
+                     val=np.array(G["x1"], dtype=dtype, order=order))
+        x1.standardize(tr)
+        rel_close(x1.val, G[k + "_apply"], tol)
+
+
+def test_fused_read_standardize_abi():
+    """snpmi_bed_read_standardize_* == decode then standardize (oracle), bit-exact for Unit."""
+    for dtype in (np.float32, np.float64):
+        exp, st_exp = O.decode_standardize(body("n300"), 300, 1015, dtype=dtype)
+        out = np.empty((300, 1015), dtype=dtype, order="F")
+        st = np.empty((1015, 2), dtype=dtype)
+        N.call("snpmi_bed_read_standardize_" + N.suffix(dtype), os.path.join(DATA, "n300.bed").encode(), 300, 1015, 0,
+               None, 0, None, 0, 0, N.STD_UNIT, 0.0, 0.0, 0, N.ptr(st), N.ptr(out), 0)
+        assert np.array_equal(out, exp) and np.array_equal(st, st_exp)
+
+
+# ---------------------------------------------------------------------------------- subset
+def test_sub_matrix():
+    np.random.seed(0)
+    m = np.random.rand(12, 7)
+    s = sub_matrix(m, [0, 2, 11], [6, 5, 4, 3, 2, 1, 0])
+    assert s.shape == (3, 7) and m[2, 0] == s[1, 6]
+    for order in ("C", "F", "A"):
+        for src in (m, np.asfortranarray(m), m.astype(np.float32)):
+            for dt in (np.float32, np.float64):
+                if src.dtype == np.float64 and dt == np.float32:
+                    continue
+                got = sub_matrix(src, [3, 1], [0, 6, 2], order=order, dtype=dt)
+                assert np.array_equal(got, src[np.ix_([3, 1], [0, 6, 2])].astype(dt))
+    m3 = np.random.rand(5, 4, 3)
+    assert np.array_equal(sub_matrix(m3, [4, 0], [1, 3]), m3[np.ix_([4, 0], [1, 3])])
+
+
+# ---------------------------------------------------------------------------------- GRM
+@pytest.mark.parametrize("dtype,tol", [(np.float64, 1e-10), (np.float32, 1e-5)])
+@pytest.mark.parametrize("block_size", [None, 100])
+def test_grm_n300_vs_reference(dtype, tol, block_size):
+    G = g("n300")
+    b = bed("n300")
+    k = b.read_kernel(Unit(), block_size=block_size, dtype=dtype)
+    assert k.val.dtype == dtype
+    grm_close(k.val, G["K_unit"], tol)
+    kb = b.read_kernel(Beta(1, 25), block_size=block_size, dtype=dtype)
+    grm_close(kb.val, G["K_beta"], tol)
+    kd, _, diag = SnpKernel(b, Unit(), block_size=block_size)._read_with_standardizing(to_kerneldata=True,
+                                                                                       return_trained=True)
+    np.testing.assert_allclose(diag.factor, G["diag_factor"], rtol=1e-12)
+    grm_close(kd.val, G["K_unit_diag"], 1e-10)
+
+
+def test_grm_symmetry_and_orders():
+    b = bed("n300")
+    for order in ("C", "F", "A"):
+        for dtype in (np.float32, np.float64):
+            v = b.read_kernel(Unit(), order=order, dtype=dtype).val
+            assert v.dtype == dtype and np.array_equal(v, v.T)
+            if order != "A":
+                assert v.flags[order + "_CONTIGUOUS"]
+
+
+def test_grm_dist_x_and_toydata():
+    D = g("dist_x")
+    grm_close(bed("dist_x").read_kernel(Unit()).val, D["K_unit"], 1e-10)
+    grm_close(bed("dist_x").read_kernel(Beta(1, 25), block_size=7).val, D["K_beta"], 1e-10)
+    T = g("toydata")
+    for dtype, tol in ((np.float64, 1e-10), (np.float32, 1e-5)):
+        K = bed("toydata").read_kernel(Unit(), block_size=1000, dtype=dtype).val.astype(np.float64)
+        scale = np.abs(T["K_diag"]).max()
+        assert np.abs(K[:64] - T["K_rows"]).max() / scale <= tol
+        rel_close(np.diag(K), T["K_diag"], tol)
+        assert np.abs(K.sum(1) - T["K_rowsum"]).max() / (scale * 500) <= tol
+
+
+def test_grm_identity_raw_values():
+    """Identity standardizer on raw decoded values (NaN propagates as in NumPy dot)."""
+    b = bed("n300")[:, :200]
+    raw = O.decode(body("n300"), 300, 1015, sid_index=np.arange(200))
+    K = b.read_kernel(Identity()).val
+    ref = raw.dot(raw.T)
+    grm_close(K, ref, 1e-12)
+
+
+def test_grm_subsets_and_pushdown():
+    b = bed("toydata")
+    whole = b.read_kernel(Unit()).val
+    sub = SnpKernel(b, Unit())[::2, ::2].read().val   # kernelreader/test.py:235-247
+    np.testing.assert_allclose(sub, whole[::2, ::2], rtol=1e-10, atol=1e-9)
+    sub2 = SnpKernel(b, Unit())[::2].read().val
+    np.testing.assert_allclose(sub2, whole[::2, ::2], rtol=1e-10, atol=1e-9)
+    # iid subset read through the fused path (repack kernel) == oracle on the subset
+    rows = np.arange(499, 0, -3)
+    Ks = b[rows, 100:2100].read_kernel(Unit()).val
+    # oracle over the SNP range 100:2100 only
+    Z = O.decode(body("toydata"), 500, 10000, iid_index=rows, sid_index=np.arange(100, 2100))
+    O.standardize_native(Z)
+    grm_close(Ks, Z.dot(Z.T), 1e-10)
+    # constant standardizer: the iid subset is pushed down
+    _, tr = b.read().standardize(Unit(), return_trained=True)
+    k3 = SnpKernel(b, tr)[[5, 1, 9]].read().val
+    Z = O.decode(body("toydata"), 500, 10000, iid_index=[5, 1, 9])
+    O.standardize_native(Z, use_stats=True, stats=np.asarray(tr.stats))
+    grm_close(k3, Z.dot(Z.T), 1e-10)
+
+
+def test_grm_dense_snpdata_vs_reference():
+    G = g("edge")
+    xr = G["xr"]
+    for dtype, tol in ((np.float64, 1e-10), (np.float32, 1e-5)):
+        for order in ("F", "C"):
+            d = SnpData(iid=[["a", str(i)] for i in range(7)], sid=[str(j) for j in range(20)],
+                        val=np.array(xr, dtype=dtype, order=order))
+            for std, key in ((Unit(), "unit"), (Beta(1, 25), "beta")):
+                k = d.read_kernel(std, block_size=1, dtype=dtype)
+                grm_close(k.val, G["K_%s_xr" % key], tol)
+            assert np.array_equal(d.val, np.array(xr, dtype=dtype), equal_nan=True)  # input untouched
+
+
+def test_merge_std_block_size_invariance():
+    """kernelreader/test.py:44-54: block_size=1 == block_size=None."""
+    np.random.seed(0)
+    val = np.array(np.random.randint(3, size=[3, 20]), dtype=np.float64, order="F")
+    sd = SnpData(iid=[["0", "0"], ["1", "1"], ["2", "2"]], sid=[str(i) for i in range(20)], val=val)
+    for std in (Beta(2, 10), Unit()):
+        k0, t0, d0 = SnpKernel(sd, std, block_size=1)._read_with_standardizing(to_kerneldata=True, return_trained=True)
+        k1, t1, d1 = SnpKernel(sd, std, block_size=None)._read_with_standardizing(to_kerneldata=True, return_trained=True)
+        np.testing.assert_array_almost_equal(k0.val, k1.val, decimal=10)
+        np.testing.assert_array_almost_equal(t0.stats, t1.stats, decimal=10)
+        assert abs(d0.factor - d1.factor) < 1e-7
+
+
+def test_kerneldata_diag_k_to_n():
+    kd = KernelData(iid=[["0", "0"], ["1", "1"], ["2", "2"]], val=[[1, 2, 3], [4, 5, 6], [7, 8, 9]])
+    kd = kd.standardize()
+    assert abs(np.diag(kd.val).sum() - 3) < 1e-7  # kernelreader/test.py:221-229
+
+
+@pytest.mark.parametrize("n", [1, 127, 128, 129, 255, 257, 600])
+def test_grm_tile_edges(n):
+    """Odd tile coverage: N not a multiple of the 128-iid tile, 1 SNP .. several chunks."""
+    rng = np.random.default_rng(n)
+    val = rng.integers(0, 3, size=(n, 37)).astype(np.float64)
+    val[rng.random(val.shape) < 0.05] = np.nan
+    d = SnpData(iid=[["a", str(i)] for i in range(n)], sid=["s%d" % j for j in range(37)], val=val)
+    for dtype, tol in ((np.float64, 1e-10), (np.float32, 1e-5)):
+        Z = val.astype(dtype).copy(order="F")
+        O.standardize_native(Z)
+        ref = Z.astype(np.float64).dot(Z.astype(np.float64).T)
+        grm_close(d.read_kernel(Unit(), dtype=dtype).val, ref, tol)
+        with tempfile.TemporaryDirectory() as tmp:
+            b = Bed.write(os.path.join(tmp, "t.bed"), d, count_A1=False)
+            grm_close(b.read_kernel(Unit(), dtype=dtype).val, ref, tol)
+
+
+# ---------------------------------------------------------------------------------- device API
+class Dev:
+    """Tiny RAII helper over snpmi_dev_alloc/free."""
+
+    def __init__(self, nbytes):
+        self.p = ctypes.c_void_p()
+        N.call("snpmi_dev_alloc", ctypes.byref(self.p), int(nbytes))
+        self.nbytes = nbytes
+
+    def __del__(self):
+        try:
+            N.call("snpmi_dev_free", self.p)
+        except Exception:
+            pass
+
+    def get(self, arr):
+        N.call("snpmi_memcpy_d2h", N.ptr(arr), self.p, arr.nbytes)
+        return arr
+
+    def put(self, arr):
+        N.call("snpmi_memcpy_h2d", self.p, N.ptr(np.ascontiguousarray(arr)), arr.nbytes)
+
+
+def synth_dev(n, m, seed, miss=0.01, sid0=0):
+    pitch = N.lib().snpmi_packed_pitch(n)
+    buf = Dev(pitch * m)
+    x, cdf = O.maf_table(n)
+    N.call("snpmi_dev_synth_bed", buf.p, pitch, n, sid0, m, seed, miss, N.ptr(x), N.ptr(cdf), len(x))
+    return buf, pitch
+
+
+def test_device_synth_matches_oracle():
+    for n in (1003, 4096):
+        buf, pitch = synth_dev(n, 50, 11, sid0=7)
+        got = buf.get(np.empty((50, pitch), dtype=np.uint8))
+        exp = O.synth_bed(11, n, 7, 50, 0.01, pitch=pitch)
+        assert np.array_equal(got, exp)
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+def test_device_decode_standardize_large_properties(dtype):
+    """10k x 2k synthetic: sampled columns bit-exact vs oracle; every column mean~0 / var~1."""
+    n, m = 10000, 2000
+    buf, pitch = synth_dev(n, m, 2)
+    host = buf.get(np.empty((m, pitch), dtype=np.uint8))
+    sz = np.dtype(dtype).itemsize
+    ld = (n + 15) // 16 * 16
+    lut, st, out = Dev(m * 4 * sz), Dev(m * 2 * sz), Dev(m * ld * sz)
+    dt = N.dt_code(dtype)
+    N.call("snpmi_dev_snp_stats", buf.p, pitch, n, m, 0, N.STD_UNIT, 0.0, 0.0, 0, dt, st.p, lut.p)
+    N.call("snpmi_dev_decode", buf.p, pitch, n, m, lut.p, dt, 0, out.p, ld)
+    vals = out.get(np.empty((m, ld), dtype=dtype))[:, :n]
+    stats = st.get(np.empty((m, 2), dtype=dtype))
+    cols = np.random.default_rng(0).choice(m, 64, replace=False)
+    packed = host[:, : (n + 3) // 4].reshape(-1)
+    exp, est = O.decode_standardize(packed, n, m, sid_index=cols, dtype=dtype)
+    assert np.array_equal(vals[cols].T, exp) and np.array_equal(stats[cols], est)
+    v64 = vals.astype(np.float64)
+    poly = np.isfinite(stats[:, 1])
+    assert np.abs(v64.sum(1)[poly]).max() < 1e-2 * n ** 0.5
+    assert np.all(v64[~poly] == 0)
