@@ -44,15 +44,16 @@ def rel_close(got, exp, tol):
     exp = np.asarray(exp, dtype=np.float64)
     assert got.shape == exp.shape
     both_nan = np.isnan(got) & np.isnan(exp)
-    d = np.abs(got - exp)
+    with np.errstate(invalid="ignore"):
+        d = np.abs(got - exp)
     bound = tol * np.maximum(np.abs(exp), 1e-30)
-    bad = ~(both_nan | (d <= bound) | ((exp == 0) & (d <= tol)))
+    bad = ~(both_nan | (got == exp) | (d <= bound) | ((exp == 0) & (d <= tol)))
     assert not bad.any(), "max rel err %g at %s" % ((d / np.maximum(np.abs(exp), 1e-30))[bad].max(), np.argwhere(bad)[:3])
 
 
 def grm_close(K, Kref, tol):
     Kref = np.asarray(Kref, dtype=np.float64)
-    scale = np.abs(np.diag(Kref)).max()
+    scale = max(np.abs(np.diag(Kref)).max(), 1.0)
     err = np.abs(np.asarray(K, dtype=np.float64) - Kref).max() / scale
     assert err <= tol, "GRM max|dK|/max diag = %g > %g" % (err, tol)
     rel_close(np.diag(K), np.diag(Kref), tol)
