@@ -67,6 +67,8 @@ int snpmi_set_device(int device);            /* device used by later calls of th
 int snpmi_get_device(int* device);
 int snpmi_release_cache(void);               /* free cached device/pinned scratch          */
 int snpmi_device_info(int device, char* name, size_t name_len, uint64_t* total_mem, int* cu_count);
+/* tuning hook: select a kernel variant by name ("decode"); 0 = default.  For A/B benches. */
+int snpmi_set_kernel_variant(const char* kernel, int variant);
 
 /* ---------------------------------------------------------------- BED reading (bed-reader read_*) */
 int snpmi_bed_check(const char* path, uint64_t n_iid, uint64_t n_sid);
@@ -157,6 +159,10 @@ int snpmi_dev_snp_stats(const uint8_t* packed, uint64_t pitch, uint64_t n_iid, u
 /* packed + LUT -> values, column j at out + j*ld (F) or row i at out + i*ld (C) */
 int snpmi_dev_decode(const uint8_t* packed, uint64_t pitch, uint64_t n_iid, uint64_t n_sid,
                      const void* lut, int dtype, int order_c, void* out, uint64_t ld);
+/* fused per-SNP stats + decode (f32, F order): one pass per column, LUT/stats written too */
+int snpmi_dev_decode_standardize(const uint8_t* packed, uint64_t pitch, uint64_t n_iid, uint64_t n_sid,
+                                 int count_a1, int std_kind, double a, double b, int use_stats, int dtype,
+                                 void* stats, void* lut, void* out, uint64_t ld);
 /* iid gather: dst column j = src column j restricted to iids idx[0..n_out) */
 int snpmi_dev_repack(const uint8_t* src, uint64_t src_pitch, uint64_t n_src_iid, const uint64_t* idx,
                      uint64_t n_out_iid, uint64_t n_sid, uint8_t* dst, uint64_t dst_pitch);

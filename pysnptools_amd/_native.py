@@ -31,6 +31,7 @@ _SIGS = {
     "snpmi_release_cache": [],
     "snpmi_device_info": [_i32, ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_uint64),
                           ctypes.POINTER(ctypes.c_int)],
+    "snpmi_set_kernel_variant": [_cp, _i32],
     "snpmi_bed_check": [_cp, _u64, _u64],
     "snpmi_bed_read_f32": [_cp, _u64, _u64, _i32, _vp, _u64, _vp, _u64, _i32, _vp, _i32],
     "snpmi_bed_read_f64": [_cp, _u64, _u64, _i32, _vp, _u64, _vp, _u64, _i32, _vp, _i32],
@@ -67,6 +68,7 @@ _SIGS = {
     "snpmi_dev_synth_bed": [_vp, _u64, _u64, _u64, _u64, _u64, _f64, _vp, _vp, _i32],
     "snpmi_dev_snp_stats": [_vp, _u64, _u64, _u64, _i32, _i32, _f64, _f64, _i32, _i32, _vp, _vp],
     "snpmi_dev_decode": [_vp, _u64, _u64, _u64, _vp, _i32, _i32, _vp, _u64],
+    "snpmi_dev_decode_standardize": [_vp, _u64, _u64, _u64, _i32, _i32, _f64, _f64, _i32, _i32, _vp, _vp, _vp, _u64],
     "snpmi_dev_repack": [_vp, _u64, _u64, _vp, _u64, _u64, _vp, _u64],
     "snpmi_dev_syrk_packed": [_vp, _u64, _u64, _u64, _vp, _i32, _vp, _i32],
     "snpmi_dev_syrk_dense": [_vp, _u64, _u64, _u64, _i32, _vp, _i32],

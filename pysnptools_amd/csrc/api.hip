@@ -545,6 +545,14 @@ int snpmi_device_info(int dev, char* name, size_t name_len, uint64_t* total_mem,
     });
 }
 
+int snpmi_set_kernel_variant(const char* kernel, int variant) {
+    return guarded([&] {
+        SNPMI_REQUIRE(kernel != nullptr, SNPMI_E_ARG, "kernel name is NULL");
+        if (std::strcmp(kernel, "decode") == 0) g_variant_decode = variant;
+        else throw Error(SNPMI_E_ARG, std::string("unknown kernel ") + kernel);
+    });
+}
+
 int snpmi_bed_check(const char* path, uint64_t n_iid, uint64_t n_sid) {
     return guarded([&] {
         BedMap m;
@@ -717,6 +725,18 @@ int snpmi_dev_decode(const uint8_t* packed, uint64_t pitch, uint64_t n_iid, uint
         if (!order_c) SNPMI_REQUIRE(ld % 16 == 0 && ld >= n_iid, SNPMI_E_ARG, "F-order ld must be >= n_iid, % 16");
         else SNPMI_REQUIRE(ld >= n_sid, SNPMI_E_ARG, "C-order ld must be >= n_sid");
         launch_decode(packed, pitch, n_iid, n_sid, lut, dtype, order_c, out, ld, stream());
+    });
+}
+
+int snpmi_dev_decode_standardize(const uint8_t* packed, uint64_t pitch, uint64_t n_iid, uint64_t n_sid,
+                                 int count_a1, int std_kind, double a, double b, int use_stats, int dtype,
+                                 void* stats, void* lut, void* out, uint64_t ld) {
+    return guarded([&] {
+        SNPMI_REQUIRE(dtype == SNPMI_DT_F32, SNPMI_E_ARG, "fused decode+standardize is f32 only");
+        SNPMI_REQUIRE(pitch % 64 == 0 && pitch >= ceil_div(n_iid, 4), SNPMI_E_ARG, "pitch must be snpmi_packed_pitch");
+        SNPMI_REQUIRE(ld % 16 == 0 && ld >= n_iid, SNPMI_E_ARG, "F-order ld must be >= n_iid, % 16");
+        launch_decode_std_fused(packed, pitch, n_iid, n_sid, count_a1, std_kind, a, b, use_stats, stats, lut, out, ld,
+                                stream());
     });
 }
 

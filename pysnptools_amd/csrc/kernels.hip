@@ -138,75 +138,231 @@ __device__ __forceinline__ T sel4(T l0, T l1, T l2, T l3, uint32_t c) {
 }
 
 // Wave work item = (column j, chunk of 1024 iids).  Each lane loads one dword (16 iids);
-// codes are redistributed with ds_bpermute so every store instruction writes 1 KiB
-// contiguous (f32: 4 rounds of float4; f64: 8 rounds of double2; i8: one 16-B store).
-template <typename T>
+// codes are redistributed with ds_bpermute (__shfl) so every store instruction writes 1 KiB
+// contiguous (f32: 4 rounds of 16-B stores; f64: 8 rounds; i8: one 16-B store per lane).
+// U items per wave per iteration with all U loads issued first (memory-level parallelism);
+// stores are non-temporal (write-once stream).  Measured on MI355X (tools/ubench.py):
+// U=4 + nt + 8 blocks per 4 waves of work-cap -> 5.2 TB/s vs 3.6 TB/s for U=1, plain stores.
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+typedef double f64x2_t __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+
+template <typename V>
+__device__ __forceinline__ void store_nt(V* p, const V& v) {
+    __builtin_nontemporal_store(v, p);
+}
+
+template <typename T, int U>
 __global__ __launch_bounds__(kBlock) void k_decode_f(const uint8_t* __restrict__ packed, uint64_t pitch, uint64_t n,
                                                      uint64_t m, const T* __restrict__ lut, T* __restrict__ out,
                                                      uint64_t ld) {
     const int lane = threadIdx.x & (kWave - 1);
     const uint64_t chunks = (n + 1023) / 1024;
     const uint64_t total = chunks * m;
+    const uint64_t groups = (total + U - 1) / U;
     const uint64_t nwaves = (uint64_t)gridDim.x * (kBlock / kWave);
-    for (uint64_t it = (uint64_t)blockIdx.x * (kBlock / kWave) + threadIdx.x / kWave; it < total; it += nwaves) {
-        const uint64_t j = it / chunks, c = it - j * chunks;
-        const uint64_t i0 = c * 1024;
-        const uint32_t* col = reinterpret_cast<const uint32_t*>(packed + j * pitch);
-        const uint32_t w = (i0 + 16 * (uint64_t)lane < n) ? col[c * 64 + lane] : 0u;
-        const T l0 = lut[4 * j], l1 = lut[4 * j + 1], l2 = lut[4 * j + 2], l3 = lut[4 * j + 3];
-        T* o = out + j * ld + i0;
-        if constexpr (sizeof(T) == 4) {
+    for (uint64_t gi = (uint64_t)blockIdx.x * (kBlock / kWave) + threadIdx.x / kWave; gi < groups; gi += nwaves) {
+        uint32_t w[U];
+        uint64_t jv[U], cv[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const uint64_t it = gi * U + u;
+            const uint64_t j = it / chunks, c = it - j * chunks;
+            jv[u] = j;
+            cv[u] = c;
+            const bool ok = it < total && (c * 1024 + 16 * (uint64_t)lane < n);
+            w[u] = ok ? reinterpret_cast<const uint32_t*>(packed + j * pitch)[c * 64 + lane] : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            if (gi * U + u >= total) break;
+            const uint64_t j = jv[u], i0 = cv[u] * 1024;
+            const T l0 = lut[4 * j], l1 = lut[4 * j + 1], l2 = lut[4 * j + 2], l3 = lut[4 * j + 3];
+            T* o = out + j * ld + i0;
+            if constexpr (sizeof(T) == 4) {
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    const uint32_t src = __shfl(w[u], r * 16 + (lane >> 2), kWave);
+                    const uint32_t byte = (src >> (8 * (lane & 3))) & 0xffu;
+                    const uint64_t i = i0 + r * 256 + 4 * lane;
+                    f32x4_t v;
+                    v.x = sel4(l0, l1, l2, l3, byte & 3u);
+                    v.y = sel4(l0, l1, l2, l3, (byte >> 2) & 3u);
+                    v.z = sel4(l0, l1, l2, l3, (byte >> 4) & 3u);
+                    v.w = sel4(l0, l1, l2, l3, byte >> 6);
+                    if (i + 4 <= n) {
+                        store_nt(reinterpret_cast<f32x4_t*>(o + r * 256 + 4 * lane), v);
+                    } else {
+                        for (int t = 0; t < 4; t++)
+                            if (i + t < n) o[r * 256 + 4 * lane + t] = v[t];
+                    }
+                }
+            } else if constexpr (sizeof(T) == 8) {
+#pragma unroll
+                for (int r = 0; r < 8; r++) {
+                    const uint32_t src = __shfl(w[u], r * 8 + (lane >> 3), kWave);
+                    const uint32_t byte = (src >> (8 * ((lane >> 1) & 3))) & 0xffu;
+                    const uint32_t sh = 4 * (lane & 1);
+                    const uint64_t i = i0 + r * 128 + 2 * lane;
+                    f64x2_t v;
+                    v.x = sel4(l0, l1, l2, l3, (byte >> sh) & 3u);
+                    v.y = sel4(l0, l1, l2, l3, (byte >> (sh + 2)) & 3u);
+                    if (i + 2 <= n) {
+                        store_nt(reinterpret_cast<f64x2_t*>(o + r * 128 + 2 * lane), v);
+                    } else if (i < n) {
+                        o[r * 128 + 2 * lane] = v.x;
+                    }
+                }
+            } else {
+                // int8: lane writes 16 bytes for its own dword; byte LUT via v_perm_b32
+                const uint32_t lw = (uint32_t)(uint8_t)l0 | ((uint32_t)(uint8_t)l1 << 8) |
+                                    ((uint32_t)(uint8_t)l2 << 16) | ((uint32_t)(uint8_t)l3 << 24);
+                u32x4_t q;
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const uint32_t bb = (w[u] >> (8 * k)) & 0xffu;
+                    const uint32_t selb = (bb & 3u) | ((bb & 0xCu) << 6) | ((bb & 0x30u) << 12) | ((bb & 0xC0u) << 18);
+                    q[k] = __builtin_amdgcn_perm(0u, lw, selb);
+                }
+                const uint64_t i = i0 + 16 * lane;
+                if (i + 16 <= n) {
+                    store_nt(reinterpret_cast<u32x4_t*>(o + 16 * lane), q);
+                } else if (i < n) {
+                    for (uint64_t t = 0; i + t < n; t++)
+                        reinterpret_cast<uint8_t*>(o)[16 * lane + t] = (uint8_t)(q[t >> 2] >> (8 * (t & 3)));
+                }
+            }
+        }
+    }
+}
+
+// Fused stats + decode, one workgroup per SNP column (large N): pass 1 counts the codes
+// (packed column read once from HBM), the LUT is built in f64 by one lane, pass 2 re-reads
+// the column (L2 / Infinity-Cache resident) and streams the values out with non-temporal
+// 16-B stores.  Saves the separate k_snp_stats launch and its HBM read.
+template <int U>
+__global__ __launch_bounds__(kBlock) void k_decode_std_col_f32(const uint8_t* __restrict__ packed, uint64_t pitch,
+                                                               uint64_t n, int count_a1, int std_kind, double a,
+                                                               double b, int use_stats, float* __restrict__ stats,
+                                                               float* __restrict__ lut_out, float* __restrict__ out,
+                                                               uint64_t ld) {
+    __shared__ uint32_t red[3][kBlock / kWave];
+    __shared__ float lutsh[4];
+    const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
+    const uint64_t j = blockIdx.x;
+    const uint8_t* colp = packed + j * pitch;
+    if (std_kind == SNPMI_STD_NONE) {
+        if (threadIdx.x < 4) {
+            int v = code_value(threadIdx.x, count_a1);
+            lutsh[threadIdx.x] = v < 0 ? __builtin_nanf("") : (float)v;
+        }
+    } else {
+        double mean = 0, sd = 0;
+        if (!use_stats) {
+            const uint4* col = reinterpret_cast<const uint4*>(colp);
+            const uint64_t nq = (n + 63) / 64;
+            uint32_t c1 = 0, c2 = 0, c3 = 0;
+            for (uint64_t q0 = threadIdx.x; q0 < nq; q0 += kBlock * 4) {
+                uint4 vv[4];
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    const uint64_t q = q0 + (uint64_t)u * kBlock;
+                    vv[u] = q < nq ? col[q] : make_uint4(0, 0, 0, 0);
+                }
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    const uint64_t q = q0 + (uint64_t)u * kBlock;
+                    uint32_t w4[4] = {vv[u].x, vv[u].y, vv[u].z, vv[u].w};
+#pragma unroll
+                    for (int k = 0; k < 4; k++) {
+                        uint32_t w = w4[k];
+                        uint32_t lo = w & 0x55555555u, hi = (w >> 1) & 0x55555555u;
+                        const uint64_t ib = q * 64 + 16 * k;
+                        if (ib + 16 > n) {
+                            const uint64_t valid = n > ib ? n - ib : 0;
+                            const uint32_t mk = valid >= 16 ? 0xFFFFFFFFu : (((1u << (2 * valid)) - 1u) & 0x55555555u);
+                            lo &= mk;
+                            hi &= mk;
+                        }
+                        c3 += __popc(lo & hi);
+                        c2 += __popc(hi & ~lo);
+                        c1 += __popc(lo & ~hi);
+                    }
+                }
+            }
+            c1 = wave_sum_u32(c1);
+            c2 = wave_sum_u32(c2);
+            c3 = wave_sum_u32(c3);
+            if (lane == 0) {
+                red[0][wave] = c1;
+                red[1][wave] = c2;
+                red[2][wave] = c3;
+            }
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                uint64_t t1 = 0, t2 = 0, t3 = 0;
+                for (int q = 0; q < kBlock / kWave; q++) {
+                    t1 += red[0][q];
+                    t2 += red[1][q];
+                    t3 += red[2][q];
+                }
+                const uint64_t c0 = n - t1 - t2 - t3, chi = count_a1 ? c0 : t3;
+                mean = stats_mean_std((double)(n - t1), (double)(t2 + 2 * chi), (double)(t2 + 4 * chi), &sd);
+                stats[2 * j] = (float)mean;
+                stats[2 * j + 1] = (float)sd;
+            }
+        } else if (threadIdx.x == 0) {
+            mean = (double)stats[2 * j];
+            sd = (double)stats[2 * j + 1];
+        }
+        if (threadIdx.x == 0) {
+            const double w = std_kind == SNPMI_STD_BETA ? beta_weight(mean, a, b) : 0.0;
+            const bool zero_col = std_kind == SNPMI_STD_BETA && use_stats && __builtin_isinf(sd);
+            for (int c = 0; c < 4; c++) {
+                const int v = code_value(c, count_a1);
+                double x;
+                if (v < 0 || zero_col) x = 0.0;
+                else if (std_kind == SNPMI_STD_BETA) x = ((double)v - mean) * w;
+                else x = ((double)v - mean) / sd;
+                lutsh[c] = (float)x;
+            }
+        }
+    }
+    __syncthreads();
+    const float l0 = lutsh[0], l1 = lutsh[1], l2 = lutsh[2], l3 = lutsh[3];
+    if (threadIdx.x < 4 && lut_out) lut_out[4 * j + threadIdx.x] = lutsh[threadIdx.x];
+    const uint64_t chunks = (n + 1023) / 1024;
+    const uint32_t* col = reinterpret_cast<const uint32_t*>(colp);
+    float* ocol = out + j * ld;
+    for (uint64_t c0 = (uint64_t)wave * U; c0 < chunks; c0 += (uint64_t)(kBlock / kWave) * U) {
+        uint32_t w[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const uint64_t c = c0 + u;
+            w[u] = (c < chunks && c * 1024 + 16 * (uint64_t)lane < n) ? col[c * 64 + lane] : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const uint64_t c = c0 + u;
+            if (c >= chunks) break;
+            const uint64_t i0 = c * 1024;
+            float* o = ocol + i0;
 #pragma unroll
             for (int r = 0; r < 4; r++) {
-                uint32_t src = __shfl(w, r * 16 + (lane >> 2), kWave);
-                uint32_t byte = (src >> (8 * (lane & 3))) & 0xffu;
+                const uint32_t src = __shfl(w[u], r * 16 + (lane >> 2), kWave);
+                const uint32_t byte = (src >> (8 * (lane & 3))) & 0xffu;
                 const uint64_t i = i0 + r * 256 + 4 * lane;
-                float4 v;
+                f32x4_t v;
                 v.x = sel4(l0, l1, l2, l3, byte & 3u);
                 v.y = sel4(l0, l1, l2, l3, (byte >> 2) & 3u);
                 v.z = sel4(l0, l1, l2, l3, (byte >> 4) & 3u);
                 v.w = sel4(l0, l1, l2, l3, byte >> 6);
                 if (i + 4 <= n) {
-                    *reinterpret_cast<float4*>(o + r * 256 + 4 * lane) = v;
+                    __builtin_nontemporal_store(v, reinterpret_cast<f32x4_t*>(o + r * 256 + 4 * lane));
                 } else {
-                    float e[4] = {v.x, v.y, v.z, v.w};
                     for (int t = 0; t < 4; t++)
-                        if (i + t < n) o[r * 256 + 4 * lane + t] = e[t];
+                        if (i + t < n) o[r * 256 + 4 * lane + t] = v[t];
                 }
-            }
-        } else if constexpr (sizeof(T) == 8) {
-#pragma unroll
-            for (int r = 0; r < 8; r++) {
-                uint32_t src = __shfl(w, r * 8 + (lane >> 3), kWave);
-                uint32_t byte = (src >> (8 * ((lane >> 1) & 3))) & 0xffu;
-                uint32_t sh = 4 * (lane & 1);
-                const uint64_t i = i0 + r * 128 + 2 * lane;
-                double2 v;
-                v.x = sel4(l0, l1, l2, l3, (byte >> sh) & 3u);
-                v.y = sel4(l0, l1, l2, l3, (byte >> (sh + 2)) & 3u);
-                if (i + 2 <= n) {
-                    *reinterpret_cast<double2*>(o + r * 128 + 2 * lane) = v;
-                } else if (i < n) {
-                    o[r * 128 + 2 * lane] = v.x;
-                }
-            }
-        } else {
-            // int8: lane writes 16 bytes for its own dword; byte LUT via v_perm_b32
-            const uint32_t lw = (uint32_t)(uint8_t)l0 | ((uint32_t)(uint8_t)l1 << 8) |
-                                ((uint32_t)(uint8_t)l2 << 16) | ((uint32_t)(uint8_t)l3 << 24);
-            uint32_t q[4];
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                uint32_t b = (w >> (8 * k)) & 0xffu;
-                uint32_t selb = (b & 3u) | ((b & 0xCu) << 6) | ((b & 0x30u) << 12) | ((b & 0xC0u) << 18);
-                q[k] = __builtin_amdgcn_perm(0u, lw, selb);
-            }
-            const uint64_t i = i0 + 16 * lane;
-            if (i + 16 <= n) {
-                *reinterpret_cast<uint4*>(o + 16 * lane) = make_uint4(q[0], q[1], q[2], q[3]);
-            } else if (i < n) {
-                const uint8_t* qb = reinterpret_cast<const uint8_t*>(q);
-                for (uint64_t t = 0; i + t < n; t++) reinterpret_cast<uint8_t*>(o)[16 * lane + t] = qb[t];
             }
         }
     }
@@ -560,6 +716,8 @@ inline unsigned grid_for(uint64_t work, uint64_t per_block, unsigned cap = 65536
 }  // namespace
 
 // ====================================================================== launchers
+int g_variant_decode = 0;  // tuning hook (snpmi_set_kernel_variant); no variants at present
+
 #define SNPMI_LAUNCH_CHECK() SNPMI_HIP(hipGetLastError())
 
 void launch_snp_stats(const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m, int count_a1, int std_kind,
@@ -582,14 +740,15 @@ void launch_decode(const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m
                    int order_c, void* out, uint64_t ld, hipStream_t st) {
     if (m == 0 || n == 0) return;
     if (!order_c) {
-        const uint64_t items = ceil_div(n, 1024) * m;
-        const unsigned g = grid_for(items, kBlock / kWave, 256 * 16);
+        // 4 work items per wave; 8x more blocks than resident waves can hold (measured best)
+        const uint64_t waves = ceil_div(ceil_div(n, 1024) * m, 4);
+        const unsigned g = grid_for(waves, kBlock / kWave, 256 * 16 * 8);
         if (dtype == SNPMI_DT_F32)
-            k_decode_f<float><<<g, kBlock, 0, st>>>(packed, pitch, n, m, (const float*)lut, (float*)out, ld);
+            k_decode_f<float, 4><<<g, kBlock, 0, st>>>(packed, pitch, n, m, (const float*)lut, (float*)out, ld);
         else if (dtype == SNPMI_DT_F64)
-            k_decode_f<double><<<g, kBlock, 0, st>>>(packed, pitch, n, m, (const double*)lut, (double*)out, ld);
+            k_decode_f<double, 4><<<g, kBlock, 0, st>>>(packed, pitch, n, m, (const double*)lut, (double*)out, ld);
         else
-            k_decode_f<int8_t><<<g, kBlock, 0, st>>>(packed, pitch, n, m, (const int8_t*)lut, (int8_t*)out, ld);
+            k_decode_f<int8_t, 4><<<g, kBlock, 0, st>>>(packed, pitch, n, m, (const int8_t*)lut, (int8_t*)out, ld);
     } else {
         const uint64_t tiles = ceil_div(n, 64) * ceil_div(m, 64);
         const unsigned g = grid_for(tiles, 1, 256 * 8);
@@ -600,6 +759,15 @@ void launch_decode(const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m
         else
             k_decode_c<int8_t><<<g, kBlock, 0, st>>>(packed, pitch, n, m, (const int8_t*)lut, (int8_t*)out, ld);
     }
+    SNPMI_LAUNCH_CHECK();
+}
+
+void launch_decode_std_fused(const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m, int count_a1,
+                             int std_kind, double a, double b, int use_stats, void* stats, void* lut, void* out,
+                             uint64_t ld, hipStream_t st) {
+    if (m == 0 || n == 0) return;
+    k_decode_std_col_f32<4><<<(unsigned)m, kBlock, 0, st>>>(packed, pitch, n, count_a1, std_kind, a, b, use_stats,
+                                                            (float*)stats, (float*)lut, (float*)out, ld);
     SNPMI_LAUNCH_CHECK();
 }
 

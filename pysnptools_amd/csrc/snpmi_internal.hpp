@@ -80,11 +80,15 @@ void* pinned(int slot, size_t bytes);
 void release_pinned();
 
 // ------------------------------------------------------------------ kernel launchers (kernels.hip)
+extern int g_variant_decode;
 void launch_snp_stats(const uint8_t* packed, uint64_t pitch, uint64_t n_iid, uint64_t n_sid, int count_a1,
                       int std_kind, double a, double b, int use_stats, int dtype, void* stats, void* lut,
                       hipStream_t st);
 void launch_decode(const uint8_t* packed, uint64_t pitch, uint64_t n_iid, uint64_t n_sid, const void* lut,
                    int dtype, int order_c, void* out, uint64_t ld, hipStream_t st);
+void launch_decode_std_fused(const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m, int count_a1,
+                             int std_kind, double a, double b, int use_stats, void* stats, void* lut, void* out,
+                             uint64_t ld, hipStream_t st);
 void launch_repack(const uint8_t* src, uint64_t src_pitch, uint64_t n_src, const uint64_t* idx, uint64_t n_out,
                    uint64_t n_sid, uint8_t* dst, uint64_t dst_pitch, int* err_flag, hipStream_t st);
 void launch_dense_standardize(void* val, uint64_t rows, uint64_t cols, uint64_t ld, int order_c, int dtype,

@@ -1,0 +1,86 @@
+"""A/B microbenchmarks of single kernels (interleaved rounds in ONE process, HIP events).
+
+  python tools/ubench.py decode [--n 500000 --m 8192 --variants 0,1,2,3,4,5,6]
+  python tools/ubench.py syrk   [--n 50000 --m 10000]
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from pysnptools_amd import _native as N  # noqa: E402
+from bench import Dev, Events, synth  # noqa: E402
+
+
+def decode(args):
+    n, m = args.n, args.m
+    pitch = N.lib().snpmi_packed_pitch(n)
+    ld = (n + 15) // 16 * 16
+    packed = Dev(N, pitch * m)
+    synth(N, packed.p, pitch, n, 0, m, 3, 0.01)
+    lut, st, out = Dev(N, m * 16), Dev(N, m * 8), Dev(N, m * ld * 4)
+    N.call("snpmi_dev_snp_stats", packed.p, pitch, n, m, 0, N.STD_UNIT, 0.0, 0.0, 0, N.DT_F32, st.p, lut.p)
+    variants = [int(v) for v in args.variants.split(",")]
+    ev = Events(N, 2)
+    res = {v: [] for v in variants}
+    ref = None
+    for rnd in range(args.rounds):
+        for v in variants:
+            if v >= 0:
+                N.call("snpmi_set_kernel_variant", b"decode", v)
+                ev.record(0)
+                N.call("snpmi_dev_snp_stats", packed.p, pitch, n, m, 0, N.STD_UNIT, 0.0, 0.0, 0, N.DT_F32, st.p, lut.p)
+                N.call("snpmi_dev_decode", packed.p, pitch, n, m, lut.p, N.DT_F32, 0, out.p, ld)
+                ev.record(1)
+            else:
+                ev.record(0)
+                N.call("snpmi_dev_decode_standardize", packed.p, pitch, n, m, 0, N.STD_UNIT, 0.0, 0.0, 0, N.DT_F32,
+                       st.p, lut.p, out.p, ld)
+                ev.record(1)
+            res[v].append(ev.ms(0, 1))
+            if rnd == 0:
+                chk = np.empty(4 * ld, dtype=np.float32)
+                N.call("snpmi_memcpy_d2h", N.ptr(chk), ctypes.c_void_p(out.p.value + (m - 4) * ld * 4), chk.nbytes)
+                if ref is None:
+                    ref = chk.copy()
+                assert np.array_equal(chk, ref), "variant %d output differs" % v
+    nbytes = m * ((n + 3) // 4 + 4 * n)
+    for v in variants:
+        t = np.median(res[v])
+        print(json.dumps({"kernel": "stats+decode" if v >= 0 else "fused", "variant": v, "median_ms": t, "min_ms": min(res[v]),
+                          "GBps": nbytes / t / 1e6, "frac_8TBs": nbytes / t / 1e6 / 8000}))
+
+
+def syrk(args):
+    n, m = args.n, args.m
+    pitch = N.lib().snpmi_packed_pitch(n)
+    packed = Dev(N, pitch * m)
+    synth(N, packed.p, pitch, n, 0, m, 3, 0.01)
+    lut, st = Dev(N, m * 16), Dev(N, m * 8)
+    tiles = Dev(N, N.lib().snpmi_grm_tile_bytes(n, N.DT_F32))
+    N.call("snpmi_dev_snp_stats", packed.p, pitch, n, m, 0, N.STD_UNIT, 0.0, 0.0, 0, N.DT_F32, st.p, lut.p)
+    ev = Events(N, 2)
+    ts = []
+    for rnd in range(args.rounds):
+        ev.record(0)
+        N.call("snpmi_dev_syrk_packed", packed.p, pitch, n, m, lut.p, N.DT_F32, tiles.p, 0)
+        ev.record(1)
+        ts.append(ev.ms(0, 1))
+    t = np.median(ts)
+    print(json.dumps({"kernel": "syrk_f32", "n": n, "m": m, "median_ms": t, "TFLOPs": n * (n + 1) * m / t / 1e9,
+                      "frac": n * (n + 1) * m / t / 1e9 / 157.3}))
+
+
+if __name__ == "__main__":
+    p = argparse.ArgumentParser()
+    p.add_argument("what")
+    p.add_argument("--n", type=int, default=500000)
+    p.add_argument("--m", type=int, default=8192)
+    p.add_argument("--rounds", type=int, default=7)
+    p.add_argument("--variants", default="0,1,2,3,4,5,6")
+    a = p.parse_args()
+    {"decode": decode, "syrk": syrk}[a.what](a)
