@@ -549,6 +549,7 @@ int snpmi_set_kernel_variant(const char* kernel, int variant) {
     return guarded([&] {
         SNPMI_REQUIRE(kernel != nullptr, SNPMI_E_ARG, "kernel name is NULL");
         if (std::strcmp(kernel, "decode") == 0) g_variant_decode = variant;
+        else if (std::strcmp(kernel, "syrk") == 0) g_variant_syrk = variant;
         else throw Error(SNPMI_E_ARG, std::string("unknown kernel ") + kernel);
     });
 }

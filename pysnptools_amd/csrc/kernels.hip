@@ -132,9 +132,14 @@ __global__ __launch_bounds__(kBlock) void k_snp_stats(const uint8_t* __restrict_
 }
 
 // ------------------------------------------------------------------ decode, F order
+// 4-entry LUT select, written so hipcc emits three v_cndmask (no divergent branches:
+// the nested-ternary form compiled to exec-mask branches around every element).
 template <typename T>
 __device__ __forceinline__ T sel4(T l0, T l1, T l2, T l3, uint32_t c) {
-    return (c & 2u) ? ((c & 1u) ? l3 : l2) : ((c & 1u) ? l1 : l0);
+    const bool b0 = (c & 1u) != 0, b1 = (c & 2u) != 0;
+    const T lo = b0 ? l1 : l0;
+    const T hi = b0 ? l3 : l2;
+    return b1 ? hi : lo;
 }
 
 // Wave work item = (column j, chunk of 1024 iids).  Each lane loads one dword (16 iids);

@@ -81,6 +81,7 @@ void release_pinned();
 
 // ------------------------------------------------------------------ kernel launchers (kernels.hip)
 extern int g_variant_decode;
+extern int g_variant_syrk;
 void launch_snp_stats(const uint8_t* packed, uint64_t pitch, uint64_t n_iid, uint64_t n_sid, int count_a1,
                       int std_kind, double a, double b, int use_stats, int dtype, void* stats, void* lut,
                       hipStream_t st);

@@ -32,26 +32,27 @@ __device__ __forceinline__ void tile_coords(uint64_t L, uint32_t& ti, uint32_t& 
     ti = (uint32_t)(L - j * (j + 1) / 2);
 }
 
+// 4-entry LUT select, written so hipcc emits three v_cndmask (no divergent branches:
+// the nested-ternary form compiled to exec-mask branches around every element).
 template <typename T>
 __device__ __forceinline__ T sel4(T l0, T l1, T l2, T l3, uint32_t c) {
-    return (c & 2u) ? ((c & 1u) ? l3 : l2) : ((c & 1u) ? l1 : l0);
+    const bool b0 = (c & 1u) != 0, b1 = (c & 2u) != 0;
+    const T lo = b0 ? l1 : l0;
+    const T hi = b0 ? l3 : l2;
+    return b1 ? hi : lo;
 }
 
 // ====================================================================== f32
 namespace f32k {
-constexpr int BK = 32;
 constexpr int LDA = BM;  // floats per LDS row
 
-struct PRegs {
-    uint32_t w;  // 16 codes
-    float4 lut;
-};
-
+// dense: F-order Z, ldz % 4 == 0; thread t moves float4 #(t + 256 q) of the BK x 128 tile
+template <int BK>
 __device__ __forceinline__ void load_dense(const float* __restrict__ Z, uint64_t ldz, uint64_t kdim, uint64_t k0,
-                                           uint64_t i0, uint64_t j0, float4 (&ra)[4], float4 (&rb)[4]) {
+                                           uint64_t i0, uint64_t j0, float4 (&ra)[BK / 8], float4 (&rb)[BK / 8]) {
     const int t = threadIdx.x;
 #pragma unroll
-    for (int q = 0; q < 4; q++) {
+    for (int q = 0; q < BK / 8; q++) {
         const int f = t + 256 * q;
         const int k = f >> 5, i4 = f & 31;
         const bool ok = k0 + k < kdim;
@@ -67,10 +68,11 @@ __device__ __forceinline__ void load_dense(const float* __restrict__ Z, uint64_t
     }
 }
 
-__device__ __forceinline__ void store_dense(float* As, float* Bs, const float4 (&ra)[4], const float4 (&rb)[4]) {
+template <int BK>
+__device__ __forceinline__ void store_dense(float* As, float* Bs, const float4 (&ra)[BK / 8], const float4 (&rb)[BK / 8]) {
     const int t = threadIdx.x;
 #pragma unroll
-    for (int q = 0; q < 4; q++) {
+    for (int q = 0; q < BK / 8; q++) {
         const int f = t + 256 * q;
         const int k = f >> 5, i4 = f & 31;
         *reinterpret_cast<float4*>(As + k * LDA + 4 * i4) = ra[q];
@@ -78,15 +80,22 @@ __device__ __forceinline__ void store_dense(float* As, float* Bs, const float4 (
     }
 }
 
-// packed: 256 threads; op = t>>7 (A: rows i0, B: rows j0); 128 threads x 2 dwords cover
-// BK=32 SNPs x 8 dwords (128 iids).
+// packed: op = t>>7 (A: rows i0, B: rows j0); 128 threads x BK/16 dwords cover
+// BK SNPs x 8 dwords (128 iids); each dword expands to 16 floats through the SNP's LUT.
+struct PRegs {
+    uint32_t w;
+    float4 lut;
+};
+
+template <int BK>
 __device__ __forceinline__ void load_packed(const uint8_t* __restrict__ P, uint64_t pitch, uint64_t kdim, uint64_t k0,
-                                            uint64_t i0, uint64_t j0, const float* __restrict__ lut, PRegs (&r)[2]) {
+                                            uint64_t i0, uint64_t j0, const float* __restrict__ lut,
+                                            PRegs (&r)[BK / 16]) {
     const int t = threadIdx.x;
     const int op = t >> 7, tt = t & 127;
     const uint64_t base = op ? j0 : i0;
 #pragma unroll
-    for (int q = 0; q < 2; q++) {
+    for (int q = 0; q < BK / 16; q++) {
         const int dw = tt + 128 * q;
         const int k = dw >> 3, d = dw & 7;
         const uint64_t kk = k0 + k;
@@ -100,28 +109,34 @@ __device__ __forceinline__ void load_packed(const uint8_t* __restrict__ P, uint6
     }
 }
 
-__device__ __forceinline__ void store_packed(float* As, float* Bs, const PRegs (&r)[2]) {
+// The 4 float4 stores of a thread are rotated by (d>>1) so the 8 lanes of each
+// ds_write_b128 group hit 8 distinct 16-B bank slots (conflict-free; was 4-way).
+template <int BK>
+__device__ __forceinline__ void store_packed(float* As, float* Bs, const PRegs (&r)[BK / 16]) {
     const int t = threadIdx.x;
     const int op = t >> 7, tt = t & 127;
     float* S = op ? Bs : As;
 #pragma unroll
-    for (int q = 0; q < 2; q++) {
+    for (int q = 0; q < BK / 16; q++) {
         const int dw = tt + 128 * q;
         const int k = dw >> 3, d = dw & 7;
         const uint32_t w = r[q].w;
         const float l0 = r[q].lut.x, l1 = r[q].lut.y, l2 = r[q].lut.z, l3 = r[q].lut.w;
 #pragma unroll
         for (int v = 0; v < 4; v++) {
+            const int vv = (v + (d >> 1)) & 3;
+            const uint32_t b = w >> (8 * vv);
             float4 o;
-            o.x = sel4(l0, l1, l2, l3, (w >> (8 * v)) & 3u);
-            o.y = sel4(l0, l1, l2, l3, (w >> (8 * v + 2)) & 3u);
-            o.z = sel4(l0, l1, l2, l3, (w >> (8 * v + 4)) & 3u);
-            o.w = sel4(l0, l1, l2, l3, (w >> (8 * v + 6)) & 3u);
-            *reinterpret_cast<float4*>(S + k * LDA + 16 * d + 4 * v) = o;
+            o.x = sel4(l0, l1, l2, l3, b & 3u);
+            o.y = sel4(l0, l1, l2, l3, (b >> 2) & 3u);
+            o.z = sel4(l0, l1, l2, l3, (b >> 4) & 3u);
+            o.w = sel4(l0, l1, l2, l3, (b >> 6) & 3u);
+            *reinterpret_cast<float4*>(S + k * LDA + 16 * d + 4 * vv) = o;
         }
     }
 }
 
+template <int BK>
 __device__ __forceinline__ void compute(const float* As, const float* Bs, f32x16 (&acc)[2][2], int wm, int wn,
                                         int lane) {
     const int kr = lane >> 5, c = lane & 31;
@@ -139,10 +154,10 @@ __device__ __forceinline__ void compute(const float* As, const float* Bs, f32x16
     }
 }
 
-template <bool PACKED>
-__global__ __launch_bounds__(256, 2) void k_syrk(const void* __restrict__ src, uint64_t ld, uint64_t kdim,
-                                                 const float* __restrict__ lut, float* __restrict__ tiles,
-                                                 int accumulate) {
+template <bool PACKED, int BK, int MINB>
+__global__ __launch_bounds__(256, MINB) void k_syrk(const void* __restrict__ src, uint64_t ld, uint64_t kdim,
+                                                    const float* __restrict__ lut, float* __restrict__ tiles,
+                                                    int accumulate) {
     __shared__ __attribute__((aligned(16))) float lds[2][2][BK * LDA];
     uint32_t ti, tj;
     tile_coords(blockIdx.x, ti, tj);
@@ -156,27 +171,27 @@ __global__ __launch_bounds__(256, 2) void k_syrk(const void* __restrict__ src, u
         for (int y = 0; y < 2; y++) acc[x][y] = (f32x16){};
 
     const uint64_t nst = (kdim + BK - 1) / BK;
-    float4 ra[4], rb[4];
-    PRegs rp[2];
+    float4 ra[BK / 8], rb[BK / 8];
+    PRegs rp[BK / 16 > 0 ? BK / 16 : 1];
     if constexpr (PACKED) {
-        load_packed((const uint8_t*)src, ld, kdim, 0, i0, j0, lut, rp);
-        store_packed(lds[0][0], lds[0][1], rp);
+        load_packed<BK>((const uint8_t*)src, ld, kdim, 0, i0, j0, lut, rp);
+        store_packed<BK>(lds[0][0], lds[0][1], rp);
     } else {
-        load_dense((const float*)src, ld, kdim, 0, i0, j0, ra, rb);
-        store_dense(lds[0][0], lds[0][1], ra, rb);
+        load_dense<BK>((const float*)src, ld, kdim, 0, i0, j0, ra, rb);
+        store_dense<BK>(lds[0][0], lds[0][1], ra, rb);
     }
     __syncthreads();
     for (uint64_t s = 0; s < nst; s++) {
         const int buf = s & 1;
         const bool more = s + 1 < nst;
         if (more) {
-            if constexpr (PACKED) load_packed((const uint8_t*)src, ld, kdim, (s + 1) * BK, i0, j0, lut, rp);
-            else load_dense((const float*)src, ld, kdim, (s + 1) * BK, i0, j0, ra, rb);
+            if constexpr (PACKED) load_packed<BK>((const uint8_t*)src, ld, kdim, (s + 1) * BK, i0, j0, lut, rp);
+            else load_dense<BK>((const float*)src, ld, kdim, (s + 1) * BK, i0, j0, ra, rb);
         }
-        compute(lds[buf][0], lds[buf][1], acc, wm, wn, lane);
+        compute<BK>(lds[buf][0], lds[buf][1], acc, wm, wn, lane);
         if (more) {
-            if constexpr (PACKED) store_packed(lds[buf ^ 1][0], lds[buf ^ 1][1], rp);
-            else store_dense(lds[buf ^ 1][0], lds[buf ^ 1][1], ra, rb);
+            if constexpr (PACKED) store_packed<BK>(lds[buf ^ 1][0], lds[buf ^ 1][1], rp);
+            else store_dense<BK>(lds[buf ^ 1][0], lds[buf ^ 1][1], ra, rb);
         }
         __syncthreads();
     }
@@ -185,15 +200,18 @@ __global__ __launch_bounds__(256, 2) void k_syrk(const void* __restrict__ src, u
 #pragma unroll
     for (int mt = 0; mt < 2; mt++)
 #pragma unroll
-        for (int nt = 0; nt < 2; nt++)
+        for (int nt = 0; nt < 2; nt++) {
+            float* base = T + (wm * 64 + mt * 32 + 4 * (lane >> 5)) * BM + wn * 64 + nt * 32 + (lane & 31);
+            if (accumulate) {  // wave-uniform branch; 16 loads in flight, then 16 stores
+                float old[16];
 #pragma unroll
-            for (int r = 0; r < 16; r++) {
-                const int row = wm * 64 + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-                const int col = wn * 64 + nt * 32 + (lane & 31);
-                float* p = T + row * BM + col;
-                const float v = acc[mt][nt][r];
-                *p = accumulate ? *p + v : v;
+                for (int r = 0; r < 16; r++) old[r] = base[((r & 3) + 8 * (r >> 2)) * BM];
+#pragma unroll
+                for (int r = 0; r < 16; r++) acc[mt][nt][r] += old[r];
             }
+#pragma unroll
+            for (int r = 0; r < 16; r++) base[((r & 3) + 8 * (r >> 2)) * BM] = acc[mt][nt][r];
+        }
 }
 }  // namespace f32k
 
@@ -339,19 +357,24 @@ __global__ __launch_bounds__(256, 2) void k_syrk(const void* __restrict__ src, u
 #pragma unroll
     for (int x = 0; x < 4; x++)
 #pragma unroll
-        for (int y = 0; y < 4; y++)
+        for (int y = 0; y < 4; y++) {
+            double* base = T + (wm * 64 + 16 * x + (lane >> 4)) * BM + wn * 64 + 16 * y + (lane & 15);
+            if (accumulate) {
+                double old[4];
 #pragma unroll
-            for (int r = 0; r < 4; r++) {
-                const int row = wm * 64 + 16 * x + (lane >> 4) + 4 * r;
-                const int col = wn * 64 + 16 * y + (lane & 15);
-                double* p = T + row * BM + col;
-                const double v = acc[x][y][r];
-                *p = accumulate ? *p + v : v;
+                for (int r = 0; r < 4; r++) old[r] = base[4 * r * BM];
+#pragma unroll
+                for (int r = 0; r < 4; r++) acc[x][y][r] += old[r];
             }
+#pragma unroll
+            for (int r = 0; r < 4; r++) base[4 * r * BM] = acc[x][y][r];
+        }
 }
 }  // namespace f64k
 
 }  // namespace
+
+int g_variant_syrk = 0;  // tuning hook (snpmi_set_kernel_variant "syrk")
 
 void launch_syrk_packed(const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m, const void* lut, int dtype,
                         void* tiles, int accumulate, hipStream_t st) {
@@ -362,8 +385,16 @@ void launch_syrk_packed(const uint8_t* packed, uint64_t pitch, uint64_t n, uint6
         if (!accumulate) SNPMI_HIP(hipMemsetAsync(tiles, 0, nt * BM * BM * dtype_size(dtype), st));
         return;
     }
-    if (dtype == SNPMI_DT_F32)
-        f32k::k_syrk<true><<<(unsigned)nt, 256, 0, st>>>(packed, pitch, m, (const float*)lut, (float*)tiles, accumulate);
+    if (dtype == SNPMI_DT_F32) {
+        const float* L = (const float*)lut;
+        float* Tt = (float*)tiles;
+        // BK=16 (32 KB LDS, 123 VGPRs) lets 4 blocks share a CU: 118 TFLOP/s vs 112 for BK=32
+        // at 2 blocks/CU (tools/ubench.py syrk, N=32768, 10k SNPs)
+        switch (g_variant_syrk) {
+            case 1: f32k::k_syrk<true, 32, 2><<<(unsigned)nt, 256, 0, st>>>(packed, pitch, m, L, Tt, accumulate); break;
+            default: f32k::k_syrk<true, 16, 4><<<(unsigned)nt, 256, 0, st>>>(packed, pitch, m, L, Tt, accumulate);
+        }
+    }
     else
         f64k::k_syrk<true><<<(unsigned)nt, 256, 0, st>>>(packed, pitch, m, (const double*)lut, (double*)tiles,
                                                           accumulate);
@@ -381,7 +412,7 @@ void launch_syrk_dense(const void* Z, uint64_t ldz, uint64_t n, uint64_t m, int 
         return;
     }
     if (dtype == SNPMI_DT_F32)
-        f32k::k_syrk<false><<<(unsigned)nt, 256, 0, st>>>(Z, ldz, m, nullptr, (float*)tiles, accumulate);
+        f32k::k_syrk<false, 16, 4><<<(unsigned)nt, 256, 0, st>>>(Z, ldz, m, nullptr, (float*)tiles, accumulate);
     else
         f64k::k_syrk<false><<<(unsigned)nt, 256, 0, st>>>(Z, ldz, m, nullptr, (double*)tiles, accumulate);
     SNPMI_HIP(hipGetLastError());

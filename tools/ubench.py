@@ -57,22 +57,38 @@ def decode(args):
 
 def syrk(args):
     n, m = args.n, args.m
+    dt = N.DT_F64 if args.dtype == "f64" else N.DT_F32
+    esz = 8 if dt == N.DT_F64 else 4
+    peak = 78.6 if dt == N.DT_F64 else 157.3
     pitch = N.lib().snpmi_packed_pitch(n)
     packed = Dev(N, pitch * m)
     synth(N, packed.p, pitch, n, 0, m, 3, 0.01)
-    lut, st = Dev(N, m * 16), Dev(N, m * 8)
-    tiles = Dev(N, N.lib().snpmi_grm_tile_bytes(n, N.DT_F32))
-    N.call("snpmi_dev_snp_stats", packed.p, pitch, n, m, 0, N.STD_UNIT, 0.0, 0.0, 0, N.DT_F32, st.p, lut.p)
+    lut, st = Dev(N, m * 4 * esz), Dev(N, m * 2 * esz)
+    tiles = Dev(N, N.lib().snpmi_grm_tile_bytes(n, dt))
+    N.call("snpmi_dev_snp_stats", packed.p, pitch, n, m, 0, N.STD_UNIT, 0.0, 0.0, 0, dt, st.p, lut.p)
     ev = Events(N, 2)
-    ts = []
+    variants = [int(v) for v in args.variants.split(",")]
+    ts = {v: [] for v in variants}
+    ref = None
+    nt_bytes = N.lib().snpmi_grm_tile_bytes(n, dt)
     for rnd in range(args.rounds):
-        ev.record(0)
-        N.call("snpmi_dev_syrk_packed", packed.p, pitch, n, m, lut.p, N.DT_F32, tiles.p, 0)
-        ev.record(1)
-        ts.append(ev.ms(0, 1))
-    t = np.median(ts)
-    print(json.dumps({"kernel": "syrk_f32", "n": n, "m": m, "median_ms": t, "TFLOPs": n * (n + 1) * m / t / 1e9,
-                      "frac": n * (n + 1) * m / t / 1e9 / 157.3}))
+        for v in variants:
+            N.call("snpmi_set_kernel_variant", b"syrk", v)
+            ev.record(0)
+            N.call("snpmi_dev_syrk_packed", packed.p, pitch, n, m, lut.p, dt, tiles.p, 0)
+            ev.record(1)
+            ts[v].append(ev.ms(0, 1))
+            if rnd == 0:
+                chk = np.empty(min(nt_bytes // esz, 1 << 22), dtype=np.float64 if esz == 8 else np.float32)
+                N.call("snpmi_memcpy_d2h", N.ptr(chk), tiles.p, chk.nbytes)
+                if ref is None:
+                    ref = chk.copy()
+                err = np.abs(chk.astype(np.float64) - ref).max() / max(np.abs(ref).max(), 1)
+                assert err < 1e-5, "variant %d differs: %g" % (v, err)
+    for v in variants:
+        t = np.median(ts[v])
+        print(json.dumps({"kernel": "syrk_" + args.dtype, "variant": v, "n": n, "m": m, "median_ms": t,
+                          "TFLOPs": n * (n + 1) * m / t / 1e9, "frac": n * (n + 1) * m / t / 1e9 / peak}))
 
 
 if __name__ == "__main__":
@@ -81,6 +97,11 @@ if __name__ == "__main__":
     p.add_argument("--n", type=int, default=500000)
     p.add_argument("--m", type=int, default=8192)
     p.add_argument("--rounds", type=int, default=7)
+    p.add_argument("--dtype", default="f32")
     p.add_argument("--variants", default="0,1,2,3,4,5,6")
+    p.add_argument("--set-variant", default=None, help="kernel=variant applied once before the run")
     a = p.parse_args()
+    if a.set_variant:
+        k, v = a.set_variant.split("=")
+        N.call("snpmi_set_kernel_variant", k.encode(), int(v))
     {"decode": decode, "syrk": syrk}[a.what](a)
