@@ -230,8 +230,10 @@ def cpu_baseline_standardize(args, sample, pitch):
 def leg_grm(N, args, dist, rccl):
     n, m, B = args.grm_iid, args.grm_sid, args.grm_block
     pitch = N.lib().snpmi_packed_pitch(n)
-    blocks = [(s0, min(B, m - s0)) for s0 in range(0, m, B)]
-    mine = blocks[dist.rank::dist.world]
+    from pysnptools_amd.shard import rank_blocks, snp_blocks
+
+    blocks = snp_blocks(m, B)
+    mine = rank_blocks(m, B, dist.rank, dist.world)
     my_m = sum(c for _, c in mine)
     packed = Dev(N, max(1, my_m) * pitch)
     off = 0

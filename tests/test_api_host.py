@@ -130,3 +130,20 @@ def test_writer_round_trip_via_oracle(n_iid):
         from pysnptools_amd.snpreader._write import encode_codes
 
         encode_codes(np.array([[0.5]]))
+
+
+def test_bed_reader_compat_surface():
+    """The shim exposes every bed_reader name PySnpTools imports, with metadata parsing."""
+    import inspect
+
+    import pysnptools_amd.bed_reader_compat as br
+
+    for name in ("open_bed", "to_bed", "standardize_f32", "standardize_f64", "subset_f64_f64", "subset_f32_f64",
+                 "subset_f32_f32", "get_num_threads"):
+        assert hasattr(br, name)
+    assert list(inspect.signature(br.standardize_f32).parameters) == [
+        "val", "is_beta", "a", "b", "apply_in_place", "use_stats", "stats", "num_threads"]
+    with br.open_bed(os.path.join(DATA, "n300.bed"), count_A1=False) as ob:
+        assert ob.iid_count == 300 and ob.sid_count == 1015
+        assert ob.fid[0] == "POP1" and len(ob.sid) == 1015 and ob.chromosome[0] == "1"
+    assert br.get_num_threads(3) == 3
