@@ -49,47 +49,64 @@ def parse():
     p.add_argument("--skip-cpu", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--seed", type=int, default=5)
+    p.add_argument("--force-rccl", action="store_true", help="build the RCCL communicator even at world size 1")
     return p.parse_args()
 
 
 class Dist:
-    """torch.distributed (gloo) for barriers / max-over-ranks / the RCCL id exchange."""
+    """Control plane for one process per GPU WITHOUT torch: importing torch would load its own
+    libamdhip64.so.7 (ROCm 7.0) next to libsnpmi's (ROCm 7.2) -- same SONAME, two runtimes.
+    torch.distributed.run only launches the processes; the ncclUniqueId is handed from rank 0
+    to the others through a node-local file keyed by the launcher's pid, and barriers /
+    max-over-ranks are RCCL all-reduces of a scalar."""
 
-    def __init__(self, gpus):
+    def __init__(self, gpus, N, force_rccl=False):
+        self.N = N
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
         self.local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-        self.pg = None
-        if self.world > 1:
-            import torch.distributed as dist
-
-            dist.init_process_group("gloo")
-            self.pg = dist
         assert self.world == gpus or self.world == 1, "--gpus must match WORLD_SIZE"
+        N.call("snpmi_set_device", self.local_rank)
+        self.rccl = False
+        if self.world > 1 or force_rccl:
+            import tempfile
+
+            key = "snpmi_rccl_%d_%s.id" % (os.getppid(), os.environ.get("MASTER_PORT", "0"))
+            path = os.path.join(tempfile.gettempdir(), key)
+            uid = (ctypes.c_uint8 * 128)()
+            if self.rank == 0:
+                N.call("snpmi_rccl_unique_id", uid, 128)
+                with open(path + ".tmp", "wb") as f:
+                    f.write(bytes(uid))
+                os.replace(path + ".tmp", path)
+            else:
+                t0 = time.time()
+                while not os.path.exists(path):
+                    if time.time() - t0 > 300:
+                        raise TimeoutError("rank %d: no RCCL id from rank 0 at %s" % (self.rank, path))
+                    time.sleep(0.05)
+                with open(path, "rb") as f:
+                    uid = (ctypes.c_uint8 * 128).from_buffer_copy(f.read(128))
+            N.call("snpmi_rccl_init", self.world, self.rank, uid, 128)
+            self.rccl = True
+            self.barrier()
+            if self.rank == 0:
+                os.remove(path)
 
     def barrier(self):
-        if self.pg:
-            self.pg.barrier()
+        if self.rccl:
+            self.N.call("snpmi_rccl_barrier")
 
     def max(self, x):
-        if not self.pg:
+        if not self.rccl:
             return x
-        import torch
-
-        t = torch.tensor([float(x)], dtype=torch.float64)
-        self.pg.all_reduce(t, op=self.pg.ReduceOp.MAX)
-        return float(t.item())
-
-    def bcast_bytes(self, b):
-        if not self.pg:
-            return b
-        obj = [b]
-        self.pg.broadcast_object_list(obj, src=0)
-        return obj[0]
+        v = (ctypes.c_double * 1)(float(x))
+        self.N.call("snpmi_rccl_host_allreduce_f64", v, 1, 1)
+        return float(v[0])
 
     def close(self):
-        if self.pg:
-            self.pg.destroy_process_group()
+        if self.rccl:
+            self.N.call("snpmi_rccl_destroy")
 
 
 class Dev:
@@ -306,19 +323,10 @@ def cpu_baseline_grm(args):
 
 def main():
     args = parse()
-    dist = Dist(args.gpus)
     from pysnptools_amd import _native as N
 
-    N.call("snpmi_set_device", dist.local_rank)
-    rccl = False
-    if dist.world > 1 and not args.skip_grm:
-        uid = (ctypes.c_uint8 * 128)()
-        if dist.rank == 0:
-            N.call("snpmi_rccl_unique_id", uid, 128)
-        b = dist.bcast_bytes(bytes(uid))
-        uid = (ctypes.c_uint8 * 128).from_buffer_copy(b)
-        N.call("snpmi_rccl_init", dist.world, dist.rank, uid, 128)
-        rccl = True
+    dist = Dist(args.gpus, N, args.force_rccl)
+    rccl = dist.rccl
 
     r1 = leg_standardize(N, args, dist)
     total_snps = args.n_sid * dist.world * args.steps
@@ -359,8 +367,6 @@ def main():
             "grm": grm,
         }
         print(json.dumps(line), flush=True)
-    if rccl:
-        N.call("snpmi_rccl_destroy")
     dist.close()
 
 

@@ -182,6 +182,9 @@ int snpmi_dev_grm_trace(const void* K_tiles, uint64_t n_iid, int dtype, double* 
 int snpmi_rccl_unique_id(uint8_t* id, uint64_t id_len);   /* id_len >= 128 */
 int snpmi_rccl_init(int nranks, int rank, const uint8_t* id, uint64_t id_len);
 int snpmi_rccl_allreduce_sum(void* buf, uint64_t count, int dtype);
+/* host-value all-reduce (op 0 = sum, 1 = max) of f64 scalars, synchronous; barrier = 1-elem sum */
+int snpmi_rccl_host_allreduce_f64(double* values, uint64_t count, int op);
+int snpmi_rccl_barrier(void);
 int snpmi_rccl_destroy(void);
 
 #ifdef __cplusplus

@@ -50,6 +50,24 @@ int snpmi_rccl_allreduce_sum(void* buf, uint64_t count, int dtype) {
     });
 }
 
+int snpmi_rccl_host_allreduce_f64(double* values, uint64_t count, int op) {
+    return guarded([&] {
+        SNPMI_REQUIRE(g_comm != nullptr, SNPMI_E_ARG, "RCCL communicator not initialised");
+        SNPMI_REQUIRE(values != nullptr && count > 0 && count <= 4096, SNPMI_E_ARG, "bad host all-reduce buffer");
+        Device& d = device();
+        double* buf = (double*)d.get(Device::S_RED, count * sizeof(double));
+        SNPMI_HIP(hipMemcpyAsync(buf, values, count * sizeof(double), hipMemcpyHostToDevice, d.stream));
+        SNPMI_NCCL(ncclAllReduce(buf, buf, count, ncclFloat64, op == 1 ? ncclMax : ncclSum, g_comm, d.stream));
+        SNPMI_HIP(hipMemcpyAsync(values, buf, count * sizeof(double), hipMemcpyDeviceToHost, d.stream));
+        SNPMI_HIP(hipStreamSynchronize(d.stream));
+    });
+}
+
+int snpmi_rccl_barrier(void) {
+    double one = 1.0;
+    return snpmi_rccl_host_allreduce_f64(&one, 1, 0);
+}
+
 int snpmi_rccl_destroy(void) {
     return guarded([&] {
         if (g_comm) {
