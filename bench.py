@@ -209,13 +209,19 @@ def leg_standardize(N, args, dist):
     full_block_bytes = B * ((n + 3) // 4 + 4 * n)
     total_bytes = m * ((n + 3) // 4 + 4 * n)
     achieved_gbs = (total_bytes / nblk) / (dec_mean_ms * 1e-3) / 1e9
-    sample = None
+    sample = gpu_cols = None
     if dist.rank == 0 and not args.skip_cpu:
-        ncols = 512
+        # parity sample: the first 512 columns, re-decoded by the same kernels (untimed)
+        ncols = min(512, m)
         sample = np.empty((ncols, pitch), dtype=np.uint8)
         N.call("snpmi_memcpy_d2h", N.ptr(sample), packed.p, sample.nbytes)
+        N.call("snpmi_dev_snp_stats", packed.p, pitch, n, ncols, 0, N.STD_UNIT, 0.0, 0.0, 0, N.DT_F32, stats.p, lut.p)
+        N.call("snpmi_dev_decode", packed.p, pitch, n, ncols, lut.p, N.DT_F32, 0, out.p, ld)
+        gpu_cols = np.empty((ncols, ld), dtype=np.float32)
+        N.call("snpmi_memcpy_d2h", N.ptr(gpu_cols), out.p, gpu_cols.nbytes)
     res = dict(wall=wall, step_ms=step_ms, dec_mean_ms=dec_mean_ms, achieved_gbs=achieved_gbs,
-               full_block_bytes=full_block_bytes, launches=launches, nblk=nblk, pitch=pitch, sample=sample)
+               full_block_bytes=full_block_bytes, launches=launches, nblk=nblk, pitch=pitch, sample=sample,
+               gpu_cols=gpu_cols)
     ev.destroy()
     for d in (packed, lut, stats, out):
         d.free()
@@ -233,12 +239,12 @@ def cpu_baseline_standardize(args, sample, pitch):
     ncols = sample.shape[0]
     done, t0 = 0, time.perf_counter()
     while True:
-        O.decode_standardize(body, n, ncols, dtype=np.float32, num_threads=threads)
+        ref, _ = O.decode_standardize(body, n, ncols, dtype=np.float32, num_threads=threads)
         done += ncols
         el = time.perf_counter() - t0
         if el >= args.cpu_seconds or done >= 64 * ncols:
             break
-    return {"value": done / el, "unit": "SNPs/s", "cores": threads, "kind": "port",
+    return ref, {"value": done / el, "unit": "SNPs/s", "cores": threads, "kind": "port",
             "sample": "%d reps x %d SNP columns x %d iids (first packed columns of the same synthetic matrix), "
                       "f32 Unit, oracle/bed_oracle.c oracle_decode_standardize_f32, %.1f s" % (done // ncols, ncols, n, el)}
 
@@ -297,6 +303,22 @@ def leg_grm(N, args, dist, rccl):
     flops_full_block = n * (n + 1) * B
     res = dict(wall=wall, syrk_ms=syrk_ms, allreduce_ms=allreduce_ms, trace=tr.value,
                mean_tflops=(flops_full_block / (np.mean(syrk_ms) * 1e-3) / 1e12) if syrk_ms else 0.0, nblocks=len(blocks))
+    if dist.rank == 0 and not args.skip_cpu and my_m > 0:
+        # parity sample (untimed): K rows 0..63 of the GRM of this rank's first 512 SNPs
+        cm, rows = min(512, my_m), 64
+        N.call("snpmi_dev_snp_stats", packed.p, pitch, n, cm, 0, N.STD_UNIT, 0.0, 0.0, 0, N.DT_F32, stats.p, lut.p)
+        N.call("snpmi_dev_syrk_packed", packed.p, pitch, n, cm, lut.p, N.DT_F32, tiles.p, 0)
+        ri = np.arange(rows, dtype=np.uint64)
+        dri, dout = Dev(N, rows * 8), Dev(N, rows * n * 4)
+        N.call("snpmi_memcpy_h2d", dri.p, N.ptr(ri), ri.nbytes)
+        N.call("snpmi_dev_grm_extract", tiles.p, n, N.DT_F32, dri.p, rows, None, n, 1, 1.0, dout.p)
+        krows = np.empty((rows, n), dtype=np.float32)
+        N.call("snpmi_memcpy_d2h", N.ptr(krows), dout.p, krows.nbytes)
+        sample = np.empty((cm, pitch), dtype=np.uint8)
+        N.call("snpmi_memcpy_d2h", N.ptr(sample), packed.p, sample.nbytes)
+        res["parity_sample"] = (krows, sample, cm, (blocks[dist.rank][0] if mine else 0))
+        dri.free()
+        dout.free()
     ev.destroy()
     for d in (packed, tiles, lut, stats):
         d.free()
@@ -321,6 +343,36 @@ def cpu_baseline_grm(args):
             "sample": "%d x Z.dot(Z.T), Z = %d x %d f32 (NumPy/OpenBLAS), %.1f s" % (reps, n, b, el)}
 
 
+def grm_parity(args, krows, sample, cm, sid0):
+    """Oracle (f64, reference one-pass Unit + NumPy Z Z^T) vs the GPU's f32 K rows."""
+    from oracle import oracle as O
+
+    n = args.grm_iid
+    bpc = (n + 3) // 4
+    Z = O.decode(np.ascontiguousarray(sample[:, :bpc]).reshape(-1), n, cm, dtype=np.float64)
+    O.standardize_native(Z)
+    rows = krows.shape[0]
+    ref = Z[:rows].dot(Z.T)
+    scale = np.abs(np.diag(ref[:, :rows])).max()
+    err = float(np.abs(krows.astype(np.float64) - ref).max() / scale)
+    return {"check": "K rows 0..%d over %d SNPs (first of this rank's blocks), %d iids: GPU f32 MFMA vs oracle f64"
+                     % (rows - 1, cm, n), "max_abs_err_over_max_diag": err, "pass": err <= 1e-5}
+
+
+def pmc_traffic(kernel, leg, n_iid, block):
+    """Per-launch HBM bytes of ``kernel`` from the committed PMC summary, when its profile was
+    taken at this configuration (tools/profile.sh + tools/traffic_summary.py); else None."""
+    path = os.path.join(ROOT, "profiles", "traffic.json")
+    try:
+        d = json.load(open(path))
+        e = d[kernel][leg]
+        if d.get("_config", {}).get(leg) == [n_iid, block]:
+            return e["traffic_bytes"]
+    except Exception:
+        pass
+    return None
+
+
 def main():
     args = parse()
     from pysnptools_amd import _native as N
@@ -341,14 +393,21 @@ def main():
                "gflops": gf, "snps_per_s": m / r2["wall"], "seconds": r2["wall"], "scaling": "strong",
                "allreduce_ms": r2["allreduce_ms"], "trace_K": r2["trace"],
                "roofline": {"bound": "mfma", "achieved": r2["mean_tflops"], "peak": MFMA_F32_PEAK_TFLOPS,
-                            "unit": "TFLOP/s", "frac": r2["mean_tflops"] / MFMA_F32_PEAK_TFLOPS, "traffic": None,
+                            "unit": "TFLOP/s", "frac": r2["mean_tflops"] / MFMA_F32_PEAK_TFLOPS,
+                            "traffic": pmc_traffic("f32k::k_syrk<true>", "grm", n, args.grm_block),
                             "kernel": "f32k::k_syrk<true>", "per_launch_flops": n * (n + 1) * args.grm_block}}
     if dist.rank == 0:
         cpu = None
+        parity = None
         if not args.skip_cpu and r1["sample"] is not None:
-            cpu = cpu_baseline_standardize(args, r1["sample"], r1["pitch"])
+            ref, cpu = cpu_baseline_standardize(args, r1["sample"], r1["pitch"])
+            same = np.array_equal(r1["gpu_cols"][:, :args.n_iid].T, ref)
+            parity = {"check": "first %d SNP columns x %d iids: GPU stats+decode vs oracle decode+one-pass "
+                               "Unit (f32)" % (ref.shape[1], ref.shape[0]), "bit_exact": bool(same)}
             if grm is not None:
                 grm["cpu_baseline"] = cpu_baseline_grm(args)
+                if r2.get("parity_sample") is not None:
+                    grm["parity"] = grm_parity(args, *r2["parity_sample"])
         n = args.n_iid
         line = {
             "metric": METRIC, "value": value, "unit": "SNPs/s", "n_gpus": dist.world, "steps": args.steps,
@@ -360,10 +419,12 @@ def main():
                        "n_iid": n, "n_sid_per_gpu": args.n_sid, "block": args.block,
                        "parallelism": "snp-shard x%d" % dist.world},
             "roofline": {"bound": "hbm", "achieved": r1["achieved_gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": r1["achieved_gbs"] / HBM_PEAK_GBS, "traffic": None,
+                         "frac": r1["achieved_gbs"] / HBM_PEAK_GBS,
+                         "traffic": pmc_traffic("k_decode_f<float>", "dec", n, args.block),
                          "kernel": "k_decode_f<float>", "per_launch_bytes": r1["full_block_bytes"],
                          "mean_launch_ms": r1["dec_mean_ms"]},
             "cpu_baseline": cpu,
+            "parity": parity,
             "grm": grm,
         }
         print(json.dumps(line), flush=True)

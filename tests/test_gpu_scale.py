@@ -1,0 +1,89 @@
+"""BASELINE configs[1] and configs[2] at full size on the GPU (device-resident synthetic BED).
+
+Checks that do not need a CPU pass over the whole matrix:
+  * sampled columns of every 8192-SNP block bit-exact (Unit) / <=1e-6 rel (Beta) vs the oracle
+    on the same packed bytes;
+  * every column: sum_i z_ij == 0 and (Unit) sum_i z_ij^2 == n_obs for polymorphic SNPs,
+    missing -> exactly 0, SNC -> all zeros -- to f32 rounding.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from pysnptools_amd import _native as N
+
+pytestmark = pytest.mark.gpu
+
+
+class Dev:
+    def __init__(self, nbytes):
+        self.p = ctypes.c_void_p()
+        N.call("snpmi_dev_alloc", ctypes.byref(self.p), int(nbytes))
+
+    def __del__(self):
+        try:
+            N.call("snpmi_dev_free", self.p)
+        except Exception:
+            pass
+
+    def at(self, off):
+        return ctypes.c_void_p(self.p.value + off)
+
+
+def run_config(n, m, seed, miss, std_kind, a, b, block=8192, samples=12):
+    pitch = N.lib().snpmi_packed_pitch(n)
+    ld = (n + 15) // 16 * 16
+    packed = Dev(pitch * m)
+    x, cdf = O.maf_table(n)
+    N.call("snpmi_dev_synth_bed", packed.p, pitch, n, 0, m, seed, miss, N.ptr(x), N.ptr(cdf), len(x))
+    lut, st, out = Dev(block * 16), Dev(block * 8), Dev(block * ld * 4)
+    rng = np.random.default_rng(seed)
+    bpc = (n + 3) // 4
+    n_poly = 0
+    for s0 in range(0, m, block):
+        cnt = min(block, m - s0)
+        N.call("snpmi_dev_snp_stats", packed.at(s0 * pitch), pitch, n, cnt, 0, std_kind, a, b, 0, N.DT_F32, st.p, lut.p)
+        N.call("snpmi_dev_decode", packed.at(s0 * pitch), pitch, n, cnt, lut.p, N.DT_F32, 0, out.p, ld)
+        stats = np.empty((cnt, 2), dtype=np.float32)
+        N.call("snpmi_memcpy_d2h", N.ptr(stats), st.p, stats.nbytes)
+        cols = np.sort(rng.choice(cnt, size=min(samples, cnt), replace=False))
+        got = np.empty((len(cols), ld), dtype=np.float32)
+        pk = np.empty((len(cols), pitch), dtype=np.uint8)
+        for q, c in enumerate(cols):
+            N.call("snpmi_memcpy_d2h", N.ptr(got[q]), out.at(int(c) * ld * 4), ld * 4)
+            N.call("snpmi_memcpy_d2h", N.ptr(pk[q]), packed.at((s0 + int(c)) * pitch), pitch)
+        body = np.ascontiguousarray(pk[:, :bpc]).reshape(-1)
+        exp, est = O.decode_standardize(body, n, len(cols), is_beta=std_kind == N.STD_BETA, a=a, b=b,
+                                        dtype=np.float32)
+        assert np.array_equal(est, stats[cols])
+        g = got[:, :n].T
+        if std_kind == N.STD_UNIT:
+            assert np.array_equal(g, exp)
+        else:
+            np.testing.assert_allclose(g, exp, rtol=1e-6, atol=1e-7)
+        # properties of the sampled columns
+        raw = O.decode(body, n, len(cols))
+        miss_mask = np.isnan(raw)
+        assert np.all(g[miss_mask] == 0)
+        g64 = g.astype(np.float64)
+        poly = np.isfinite(stats[cols, 1])
+        n_poly += int(poly.sum())
+        scale = np.abs(g64).max(0) + 1e-30
+        assert np.all(np.abs(g64.sum(0))[poly] <= 1e-5 * n * scale[poly])
+        if std_kind == N.STD_UNIT:
+            nobs = (~miss_mask).sum(0)
+            np.testing.assert_allclose((g64 ** 2).sum(0)[poly], nobs[poly], rtol=1e-5)
+            assert np.all(g64[:, ~poly] == 0)
+    return n_poly
+
+
+def test_config1_10k_x_100k_unit():
+    """BASELINE configs[1]: synthetic BED 10k iid x 100k SNP, Unit, f32."""
+    assert run_config(10_000, 100_000, seed=2, miss=0.01, std_kind=N.STD_UNIT, a=0.0, b=0.0) > 0
+
+
+def test_config2_100k_x_1m_beta():
+    """BASELINE configs[2]: 100k iid x 1M SNP, Beta(1,25) + NaN impute (21.8% missing, snpgen.py:166)."""
+    assert run_config(100_000, 1_000_000, seed=3, miss=0.218, std_kind=N.STD_BETA, a=1.0, b=25.0, samples=4) > 0

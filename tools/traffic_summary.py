@@ -1,0 +1,57 @@
+"""Summarise rocprofv3 PMC passes (FETCH_SIZE / WRITE_SIZE) into per-launch HBM traffic.
+
+Correction (MI355X_MICROARCH.md §HBM): on gfx950 FETCH_SIZE reports half of the bytes of a
+wide coalesced streaming read, so read bytes = 2 * FETCH_SIZE * 1024; WRITE_SIZE is exact for
+16-B-per-lane streaming stores; both counters are in KiB.
+Usage: python tools/traffic_summary.py <prof_dir> <out.json>
+"""
+import collections
+import csv
+import json
+import os
+import sys
+
+KERNELS = {"k_decode_f<float, 4>": "k_decode_f<float>", "k_decode_f<float": "k_decode_f<float>",
+           "f32k::k_syrk<true": "f32k::k_syrk<true>", "k_snp_stats<float>": "k_snp_stats<float>"}
+
+
+def short(name):
+    for k, v in KERNELS.items():
+        if k in name:
+            return v
+    return None
+
+
+def load(path, counter):
+    by = collections.defaultdict(list)
+    for r in csv.DictReader(open(path)):
+        s = short(r["Kernel_Name"])
+        if s and r["Counter_Name"] == counter:
+            by[s].append(float(r["Counter_Value"]) * 1024.0)
+    return by
+
+
+def main(prof, out):
+    res = {}
+    for leg in ("dec", "grm"):
+        f = load(os.path.join(prof, leg + "_FETCH_SIZE", "run_counter_collection.csv"), "FETCH_SIZE")
+        w = load(os.path.join(prof, leg + "_WRITE_SIZE", "run_counter_collection.csv"), "WRITE_SIZE")
+        for k in f:
+            # full launches only: the largest write volume (drops the partial tail block)
+            wv = sorted(w.get(k, [0.0]))
+            fv = sorted(f[k])
+            full_w = [x for x in wv if x >= 0.95 * wv[-1]]
+            full_f = [x for x in fv if x >= 0.95 * fv[-1]]
+            read_b = 2.0 * sum(full_f) / len(full_f)
+            write_b = sum(full_w) / len(full_w)
+            res.setdefault(k, {})[leg] = {"read_bytes": read_b, "write_bytes": write_b,
+                                          "traffic_bytes": read_b + write_b, "launches": len(fv)}
+    res["_config"] = {"dec": [500000, 8192], "grm": [50000, 10000]}  # tools/profile.sh settings
+    res["_source"] = ("rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes (tools/profile.sh); "
+                      "read = 2*FETCH_SIZE (gfx950 correction), per full launch")
+    json.dump(res, open(out, "w"), indent=1)
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2])
