@@ -42,6 +42,22 @@ __device__ __forceinline__ T sel4(T l0, T l1, T l2, T l3, uint32_t c) {
     return b1 ? hi : lo;
 }
 
+// v_bfi_b32: (m & a) | (~m & b).  hipcc does not form it from the C expression (it emits
+// and/or/not/xor), so it is issued directly; a plain VOP3 VALU op needs no wait states.
+__device__ __forceinline__ uint32_t bfi(uint32_t m, uint32_t a, uint32_t b) {
+    uint32_t r;
+    asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(m), "v"(a), "v"(b));
+    return r;
+}
+
+// 2-bit code at bit `sh` of w -> one of four 32-bit LUT words, 5 VALU per value:
+// two v_bfe_i32 (bit -> 0 / ~0 mask) and three v_bfi_b32 selects (no v_cmp / VCC traffic).
+__device__ __forceinline__ float sel4m(uint32_t l0, uint32_t l1, uint32_t l2, uint32_t l3, uint32_t w, uint32_t sh) {
+    const uint32_t m0 = (uint32_t)__builtin_amdgcn_sbfe((int)w, sh, 1u);
+    const uint32_t m1 = (uint32_t)__builtin_amdgcn_sbfe((int)w, sh + 1u, 1u);
+    return __uint_as_float(bfi(m1, bfi(m0, l3, l2), bfi(m0, l1, l0)));
+}
+
 // ====================================================================== f32
 namespace f32k {
 constexpr int LDA = BM;  // floats per LDS row
@@ -213,7 +229,260 @@ __global__ __launch_bounds__(256, MINB) void k_syrk(const void* __restrict__ src
             for (int r = 0; r < 16; r++) base[((r & 3) + 8 * (r >> 2)) * BM] = acc[mt][nt][r];
         }
 }
+
+// Interleaved variant (PACKED only): the expansion of stage s+1's codes is spread between
+// the MFMAs of stage s -- 4 values + one ds_write_b128 after every second k-pair -- so the
+// VALU work issues while the wave's MFMAs execute instead of as a separate phase before the
+// barrier.  Loads for stage s+1 are issued at the top of stage s.
+template <int MINB, int ABL = 0>
+__global__ __launch_bounds__(256, MINB) void k_syrk_il(const uint8_t* __restrict__ P, uint64_t pitch, uint64_t kdim,
+                                                       const float* __restrict__ lut, float* __restrict__ tiles,
+                                                       int accumulate) {
+    constexpr int BK = 16;
+    __shared__ __attribute__((aligned(16))) float lds[2][2][BK * LDA];
+    uint32_t ti, tj;
+    tile_coords(blockIdx.x, ti, tj);
+    const uint64_t i0 = (uint64_t)ti * BM, j0 = (uint64_t)tj * BM;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int wm = wave >> 1, wn = wave & 1;
+    const int t = threadIdx.x, op = t >> 7, tt = t & 127;
+    const int kq = tt >> 3, d = tt & 7;  // this thread's (k, dword) of the staged tile
+    const uint64_t base = op ? j0 : i0;
+    const int kr = lane >> 5, c = lane & 31;
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int x = 0; x < 2; x++)
+#pragma unroll
+        for (int y = 0; y < 2; y++) acc[x][y] = (f32x16){};
+    const uint64_t nst = (kdim + BK - 1) / BK;
+
+    auto load = [&](uint64_t k0, uint32_t& w, float4& l) {
+        const uint64_t kk = k0 + kq;
+        if constexpr (ABL == 1 || ABL == 3 || ABL == 4) {
+            w = (uint32_t)(kk * 0x9E3779B9u) ^ (uint32_t)t;
+            l = make_float4(0.5f, 0.f, -0.25f, 1.0f);
+            return;
+        }
+        if (kk < kdim) {
+            w = *reinterpret_cast<const uint32_t*>(P + kk * pitch + base / 4 + 4 * d);
+            l = *reinterpret_cast<const float4*>(lut + 4 * kk);
+        } else {
+            w = 0;
+            l = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    };
+    auto expand = [&](float* S, uint32_t w, const float4& l, int v) {
+        const int vv = (v + (d >> 1)) & 3;
+        if constexpr (ABL == 4) {
+            *reinterpret_cast<float4*>(S + kq * LDA + 16 * d + 4 * vv) = l;
+            return;
+        }
+        const uint32_t b = w >> (8 * vv);
+        float4 o;
+        o.x = sel4(l.x, l.y, l.z, l.w, b & 3u);
+        o.y = sel4(l.x, l.y, l.z, l.w, (b >> 2) & 3u);
+        o.z = sel4(l.x, l.y, l.z, l.w, (b >> 4) & 3u);
+        o.w = sel4(l.x, l.y, l.z, l.w, (b >> 6) & 3u);
+        if constexpr (ABL == 3) {
+            asm volatile("" ::"v"(o.x), "v"(o.y), "v"(o.z), "v"(o.w));
+            return;
+        }
+        *reinterpret_cast<float4*>(S + kq * LDA + 16 * d + 4 * vv) = o;
+    };
+    auto kpair = [&](const float* As, const float* Bs, int kk) {
+        const int row = (2 * kk + kr) * LDA;
+        const float a0 = As[row + wm * 64 + c];
+        const float a1 = As[row + wm * 64 + 32 + c];
+        const float b0 = Bs[row + wn * 64 + c];
+        const float b1 = Bs[row + wn * 64 + 32 + c];
+        acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
+        acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
+        acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
+        acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
+    };
+
+    uint32_t w;
+    float4 l;
+    load(0, w, l);
+#pragma unroll
+    for (int v = 0; v < 4; v++) expand(op ? lds[0][1] : lds[0][0], w, l, v);
+    __syncthreads();
+    for (uint64_t s = 0; s < nst; s++) {
+        const int buf = s & 1;
+        const bool more = s + 1 < nst;
+        if (more) load((s + 1) * BK, w, l);
+        const float* As = lds[buf][0];
+        const float* Bs = lds[buf][1];
+        float* S = op ? lds[buf ^ 1][1] : lds[buf ^ 1][0];
+#pragma unroll
+        for (int kk = 0; kk < BK / 2; kk++) {
+            kpair(As, Bs, kk);
+            if constexpr (ABL == 2) {
+                if (more && kk == BK / 2 - 1) asm volatile("" ::"v"(w), "v"(l.x), "v"(l.y), "v"(l.z), "v"(l.w));
+            } else {
+                if (more && (kk & 1)) expand(S, w, l, kk >> 1);
+            }
+        }
+        __syncthreads();
+    }
+    float* T = tiles + (uint64_t)blockIdx.x * (BM * BM);
+#pragma unroll
+    for (int mt = 0; mt < 2; mt++)
+#pragma unroll
+        for (int nt = 0; nt < 2; nt++) {
+            float* bp = T + (wm * 64 + mt * 32 + 4 * (lane >> 5)) * BM + wn * 64 + nt * 32 + (lane & 31);
+            if (accumulate) {
+                float old[16];
+#pragma unroll
+                for (int r = 0; r < 16; r++) old[r] = bp[((r & 3) + 8 * (r >> 2)) * BM];
+#pragma unroll
+                for (int r = 0; r < 16; r++) acc[mt][nt][r] += old[r];
+            }
+#pragma unroll
+            for (int r = 0; r < 16; r++) bp[((r & 3) + 8 * (r >> 2)) * BM] = acc[mt][nt][r];
+        }
+}
+
+// Diagnostic ablations (tuning only, wrong results): ABL=1 compute + barrier, no staging;
+// ABL=2 compute only.
+template <int ABL>
+__global__ __launch_bounds__(256, 4) void k_syrk_ablate(const uint8_t* __restrict__ P, uint64_t pitch, uint64_t kdim,
+                                                        const float* __restrict__ lut, float* __restrict__ tiles,
+                                                        int accumulate) {
+    constexpr int BK = 16;
+    __shared__ __attribute__((aligned(16))) float lds[2][2][BK * LDA];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int wm = wave >> 1, wn = wave & 1;
+    for (int i = threadIdx.x; i < 2 * 2 * BK * LDA; i += 256) (&lds[0][0][0])[i] = (float)(i & 7) * 0.25f;
+    __syncthreads();
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int x = 0; x < 2; x++)
+#pragma unroll
+        for (int y = 0; y < 2; y++) acc[x][y] = (f32x16){};
+    const uint64_t nst = (kdim + BK - 1) / BK;
+    for (uint64_t s = 0; s < nst; s++) {
+        const int buf = s & 1;
+        compute<BK>(lds[buf][0], lds[buf][1], acc, wm, wn, lane);
+        if constexpr (ABL == 1) __syncthreads();
+    }
+    float* T = tiles + (uint64_t)blockIdx.x * (BM * BM);
+#pragma unroll
+    for (int mt = 0; mt < 2; mt++)
+#pragma unroll
+        for (int nt = 0; nt < 2; nt++) {
+            float* bp = T + (wm * 64 + mt * 32 + 4 * (lane >> 5)) * BM + wn * 64 + nt * 32 + (lane & 31);
+#pragma unroll
+            for (int r = 0; r < 16; r++) bp[((r & 3) + 8 * (r >> 2)) * BM] = acc[mt][nt][r];
+        }
+}
 }  // namespace f32k
+
+// ====================================================================== f32, 256x256 blocks
+// 8 waves (2 x 4), each 128 x 64 = 4 x 2 MFMA 32x32 tiles.  Per MFMA this stages half the
+// codes of the 128x128 kernel (the 2-bit -> f32 LUT expansion is VALU, and gfx950 runs the
+// f32 MFMA at the f32 VALU rate, so expansion instructions directly displace MFMAs).
+// Output goes to the same 128x128 upper-triangle tile store: wave (wm, wn) of block
+// (bi, bj) owns 128-tile (2bi + wm, 2bj + wn/2); lower-quadrant / out-of-range waves skip.
+namespace f32w {
+constexpr int BW = 256, BK = 16, LDA = 256;
+
+template <int MINB>
+__global__ __launch_bounds__(512, MINB) void k_syrk256(const uint8_t* __restrict__ P, uint64_t pitch, uint64_t n,
+                                                      uint64_t kdim, const float* __restrict__ lut,
+                                                      float* __restrict__ tiles, int accumulate) {
+    __shared__ __attribute__((aligned(16))) float lds[2][2][BK * LDA];
+    uint32_t bi, bj;
+    tile_coords(blockIdx.x, bi, bj);
+    const uint64_t i0 = (uint64_t)bi * BW, j0 = (uint64_t)bj * BW;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int wm = wave >> 2, wn = wave & 3;
+    const int t = threadIdx.x, op = t >> 8, tt = t & 255;
+    const int kq = tt >> 4, d = tt & 15;
+    const uint64_t base = op ? j0 : i0;
+    const int kr = lane >> 5, c = lane & 31;
+    f32x16 acc[4][2];
+#pragma unroll
+    for (int x = 0; x < 4; x++)
+#pragma unroll
+        for (int y = 0; y < 2; y++) acc[x][y] = (f32x16){};
+    const uint64_t nst = (kdim + BK - 1) / BK;
+
+    uint32_t w;
+    float4 l;
+    auto load = [&](uint64_t k0) {
+        const uint64_t kk = k0 + kq;
+        if (kk < kdim) {
+            w = *reinterpret_cast<const uint32_t*>(P + kk * pitch + base / 4 + 4 * d);
+            l = *reinterpret_cast<const float4*>(lut + 4 * kk);
+        } else {
+            w = 0;
+            l = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    };
+    auto store = [&](float* S) {
+        const uint32_t u0 = __float_as_uint(l.x), u1 = __float_as_uint(l.y), u2 = __float_as_uint(l.z),
+                       u3 = __float_as_uint(l.w);
+#pragma unroll
+        for (int v = 0; v < 4; v++) {
+            const int vv = (v + (d >> 1)) & 3;  // conflict-free ds_write_b128 slots
+            const uint32_t sh = 8 * vv;
+            float4 o;
+            o.x = sel4m(u0, u1, u2, u3, w, sh);
+            o.y = sel4m(u0, u1, u2, u3, w, sh + 2);
+            o.z = sel4m(u0, u1, u2, u3, w, sh + 4);
+            o.w = sel4m(u0, u1, u2, u3, w, sh + 6);
+            *reinterpret_cast<float4*>(S + kq * LDA + 16 * d + 4 * vv) = o;
+        }
+    };
+
+    load(0);
+    store(op ? lds[0][1] : lds[0][0]);
+    __syncthreads();
+    for (uint64_t s = 0; s < nst; s++) {
+        const int buf = s & 1;
+        const bool more = s + 1 < nst;
+        if (more) load((s + 1) * BK);
+        const float* As = lds[buf][0];
+        const float* Bs = lds[buf][1];
+#pragma unroll
+        for (int kk = 0; kk < BK / 2; kk++) {
+            const int row = (2 * kk + kr) * LDA;
+            float a[4], b[2];
+#pragma unroll
+            for (int x = 0; x < 4; x++) a[x] = As[row + wm * 128 + 32 * x + c];
+#pragma unroll
+            for (int y = 0; y < 2; y++) b[y] = Bs[row + wn * 64 + 32 * y + c];
+#pragma unroll
+            for (int x = 0; x < 4; x++)
+#pragma unroll
+                for (int y = 0; y < 2; y++)
+                    acc[x][y] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[x], b[y], acc[x][y], 0, 0, 0);
+        }
+        if (more) store(op ? lds[buf ^ 1][1] : lds[buf ^ 1][0]);
+        __syncthreads();
+    }
+    const uint64_t nt128 = (n + 127) / 128;
+    const uint64_t ti = 2 * (uint64_t)bi + wm, tj = 2 * (uint64_t)bj + (wn >> 1);
+    if (ti > tj || tj >= nt128) return;  // wave-uniform
+    float* T = tiles + (tj * (tj + 1) / 2 + ti) * (uint64_t)(BM * BM);
+#pragma unroll
+    for (int x = 0; x < 4; x++)
+#pragma unroll
+        for (int y = 0; y < 2; y++) {
+            float* bp = T + (32 * x + 4 * (lane >> 5)) * BM + (wn & 1) * 64 + 32 * y + (lane & 31);
+            if (accumulate) {
+                float old[16];
+#pragma unroll
+                for (int r = 0; r < 16; r++) old[r] = bp[((r & 3) + 8 * (r >> 2)) * BM];
+#pragma unroll
+                for (int r = 0; r < 16; r++) acc[x][y][r] += old[r];
+            }
+#pragma unroll
+            for (int r = 0; r < 16; r++) bp[((r & 3) + 8 * (r >> 2)) * BM] = acc[x][y][r];
+        }
+}
+}  // namespace f32w
 
 // ====================================================================== f64
 namespace f64k {
@@ -388,10 +657,24 @@ void launch_syrk_packed(const uint8_t* packed, uint64_t pitch, uint64_t n, uint6
     if (dtype == SNPMI_DT_F32) {
         const float* L = (const float*)lut;
         float* Tt = (float*)tiles;
-        // BK=16 (32 KB LDS, 123 VGPRs) lets 4 blocks share a CU: 118 TFLOP/s vs 112 for BK=32
-        // at 2 blocks/CU (tools/ubench.py syrk, N=32768, 10k SNPs)
-        switch (g_variant_syrk) {
+        // Kernel choice (tools/ubench.py syrk, MI355X): 256x256 / 8 waves reaches 129 TFLOP/s at
+        // N=50k (82%) vs 118 for 128x128 / 4 waves; below ~4k iids the 256 tiles leave CUs idle.
+        const uint64_t nb = ceil_div(n, 256);
+        int v = g_variant_syrk;
+        if (v == 0) v = n >= 4096 ? 4 : 5;
+        switch (v) {
             case 1: f32k::k_syrk<true, 32, 2><<<(unsigned)nt, 256, 0, st>>>(packed, pitch, m, L, Tt, accumulate); break;
+            case 2: f32k::k_syrk_il<4><<<(unsigned)nt, 256, 0, st>>>(packed, pitch, m, L, Tt, accumulate); break;
+            case 3: f32k::k_syrk_il<3><<<(unsigned)nt, 256, 0, st>>>(packed, pitch, m, L, Tt, accumulate); break;
+            case 4:
+                f32w::k_syrk256<1><<<(unsigned)(nb * (nb + 1) / 2), 512, 0, st>>>(packed, pitch, n, m, L, Tt, accumulate);
+                break;
+            case 10: f32k::k_syrk_ablate<1><<<(unsigned)nt, 256, 0, st>>>(packed, pitch, m, L, Tt, accumulate); break;
+            case 11: f32k::k_syrk_ablate<2><<<(unsigned)nt, 256, 0, st>>>(packed, pitch, m, L, Tt, accumulate); break;
+            case 12: f32k::k_syrk_il<4, 1><<<(unsigned)nt, 256, 0, st>>>(packed, pitch, m, L, Tt, accumulate); break;
+            case 13: f32k::k_syrk_il<4, 2><<<(unsigned)nt, 256, 0, st>>>(packed, pitch, m, L, Tt, accumulate); break;
+            case 14: f32k::k_syrk_il<4, 3><<<(unsigned)nt, 256, 0, st>>>(packed, pitch, m, L, Tt, accumulate); break;
+            case 15: f32k::k_syrk_il<4, 4><<<(unsigned)nt, 256, 0, st>>>(packed, pitch, m, L, Tt, accumulate); break;
             default: f32k::k_syrk<true, 16, 4><<<(unsigned)nt, 256, 0, st>>>(packed, pitch, m, L, Tt, accumulate);
         }
     }

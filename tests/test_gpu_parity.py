@@ -221,7 +221,7 @@ def test_sub_matrix():
 # ---------------------------------------------------------------------------------- GRM
 @pytest.mark.parametrize("dtype,tol", [(np.float64, 1e-10), (np.float32, 1e-5)])
 @pytest.mark.parametrize("block_size", [None, 100])
-def test_grm_n300_vs_reference(dtype, tol, block_size):
+def test_grm_n300_vs_reference(dtype, tol, block_size, syrk_variant):
     G = g("n300")
     b = bed("n300")
     k = b.read_kernel(Unit(), block_size=block_size, dtype=dtype)
@@ -245,7 +245,7 @@ def test_grm_symmetry_and_orders():
                 assert v.flags[order + "_CONTIGUOUS"]
 
 
-def test_grm_dist_x_and_toydata():
+def test_grm_dist_x_and_toydata(syrk_variant):
     D = g("dist_x")
     grm_close(bed("dist_x").read_kernel(Unit()).val, D["K_unit"], 1e-10)
     grm_close(bed("dist_x").read_kernel(Beta(1, 25), block_size=7).val, D["K_beta"], 1e-10)
@@ -267,7 +267,7 @@ def test_grm_identity_raw_values():
     grm_close(K, ref, 1e-12)
 
 
-def test_grm_subsets_and_pushdown():
+def test_grm_subsets_and_pushdown(syrk_variant):
     b = bed("toydata")
     whole = b.read_kernel(Unit()).val
     sub = SnpKernel(b, Unit())[::2, ::2].read().val   # kernelreader/test.py:235-247
@@ -321,9 +321,18 @@ def test_kerneldata_diag_k_to_n():
     assert abs(np.diag(kd.val).sum() - 3) < 1e-7  # kernelreader/test.py:221-229
 
 
-@pytest.mark.parametrize("n", [1, 127, 128, 129, 255, 257, 600])
-def test_grm_tile_edges(n):
-    """Odd tile coverage: N not a multiple of the 128-iid tile, 1 SNP .. several chunks."""
+@pytest.fixture(params=[0, 4, 5], ids=["auto", "syrk256", "syrk128"])
+def syrk_variant(request):
+    """Run a test under each f32 SYRK kernel (0 = size-based choice, 4 = 256x256 tiles,
+    5 = 128x128 tiles); restores the default afterwards."""
+    N.call("snpmi_set_kernel_variant", b"syrk", request.param)
+    yield request.param
+    N.call("snpmi_set_kernel_variant", b"syrk", 0)
+
+
+@pytest.mark.parametrize("n", [1, 127, 128, 129, 255, 256, 257, 383, 600])
+def test_grm_tile_edges(n, syrk_variant):
+    """Odd tile coverage: N not a multiple of the 128/256-iid tiles, 1 SNP .. several chunks."""
     rng = np.random.default_rng(n)
     val = rng.integers(0, 3, size=(n, 37)).astype(np.float64)
     val[rng.random(val.shape) < 0.05] = np.nan
