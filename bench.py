@@ -46,6 +46,10 @@ def parse():
     p.add_argument("--grm-sid", type=int, default=500_000)
     p.add_argument("--grm-block", type=int, default=10_000)
     p.add_argument("--skip-grm", action="store_true")
+    p.add_argument("--grm5", choices=["auto", "on", "off"], default="auto",
+                   help="cfg5 tile-partitioned GRM leg (auto: when WORLD_SIZE >= 4)")
+    p.add_argument("--grm5-iid", type=int, default=500_000)
+    p.add_argument("--grm5-sid", type=int, default=8192)
     p.add_argument("--skip-cpu", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--seed", type=int, default=5)
@@ -325,6 +329,68 @@ def leg_grm(N, args, dist, rccl):
     return res
 
 
+# ---------------------------------------------------------------------------- leg 3: cfg5 partitioned GRM
+def leg_grm5(N, args, dist):
+    """configs[4] shape: 500k iids, K (500 GB upper triangle f32) partitioned over ranks as
+    256x256 blocks; every rank holds the same packed SNP block (same seed) and computes only
+    its blocks -- no reduction.  One timed pass over --grm5-sid SNPs (GRM time is linear in M)."""
+    n, m = args.grm5_iid, args.grm5_sid
+    pitch = N.lib().snpmi_packed_pitch(n)
+    nloc = N.lib().snpmi_grm_part_blocks(n, dist.rank, dist.world)
+    packed = Dev(N, pitch * m)
+    synth(N, packed.p, pitch, n, 0, m, args.seed + 200, 0.01)
+    lut, stats = Dev(N, m * 16), Dev(N, m * 8)
+    blocks = Dev(N, max(nloc, 1) * 256 * 256 * 4)
+    ev = Events(N, 2)
+    N.call("snpmi_dev_snp_stats", packed.p, pitch, n, m, 0, N.STD_UNIT, 0.0, 0.0, 0, N.DT_F32, stats.p, lut.p)
+    N.call("snpmi_stream_sync")
+    dist.barrier()
+    t0 = time.perf_counter()
+    ev.record(0)
+    N.call("snpmi_dev_snp_stats", packed.p, pitch, n, m, 0, N.STD_UNIT, 0.0, 0.0, 0, N.DT_F32, stats.p, lut.p)
+    N.call("snpmi_dev_syrk_packed_part", packed.p, pitch, n, m, lut.p, dist.rank, dist.world, blocks.p, 0)
+    ev.record(1)
+    N.call("snpmi_stream_sync")
+    dist.barrier()
+    wall = dist.max(time.perf_counter() - t0)
+    kern_ms = ev.ms(0, 1)
+    res = {"wall": wall, "kernel_ms": kern_ms, "n_local_blocks": nloc}
+    if dist.rank == 0 and not args.skip_cpu and nloc > 0:
+        r0, c0 = ctypes.c_uint64(), ctypes.c_uint64()
+        N.call("snpmi_grm_part_coords", n, 0, dist.world, 0, ctypes.byref(r0), ctypes.byref(c0))
+        blk = np.empty((256, 256), dtype=np.float32)
+        N.call("snpmi_memcpy_d2h", N.ptr(blk), blocks.p, blk.nbytes)
+        sample = np.empty((m, pitch), dtype=np.uint8)
+        N.call("snpmi_memcpy_d2h", N.ptr(sample), packed.p, sample.nbytes)
+        res["parity_sample"] = (blk, sample, r0.value, c0.value)
+    ev.destroy()
+    for d in (packed, lut, stats, blocks):
+        d.free()
+    return res
+
+
+def grm5_parity(args, blk, sample, row0, col0):
+    """Oracle (f64) for one 256x256 block of the partitioned K: decode only its 512 iids."""
+    from oracle import oracle as O
+
+    n, m = args.grm5_iid, args.grm5_sid
+    bpc = (n + 3) // 4
+    body = np.ascontiguousarray(sample[:, :bpc]).reshape(-1)
+    rows = np.arange(row0, min(row0 + 256, n))
+    cols = np.arange(col0, min(col0 + 256, n))
+    # stats use every iid; the block needs only its rows/cols
+    full_stats = O.snp_stats(body, n, m)
+    Zr = O.decode(body, n, m, iid_index=rows)
+    Zc = O.decode(body, n, m, iid_index=cols)
+    O.standardize_native(Zr, use_stats=True, stats=full_stats)
+    O.standardize_native(Zc, use_stats=True, stats=full_stats)
+    ref = Zr.dot(Zc.T)
+    scale = max(np.abs(np.diag(ref)).max() if row0 == col0 else np.abs(ref).max(), 1.0)
+    err = float(np.abs(blk[:len(rows), :len(cols)].astype(np.float64) - ref).max() / scale)
+    return {"check": "rank 0 block 0 (rows %d.., cols %d..) over %d SNPs x %d iids: GPU f32 vs oracle f64"
+                     % (row0, col0, m, n), "max_abs_err_over_scale": err, "pass": err <= 1e-5}
+
+
 def cpu_baseline_grm(args):
     """NumPy Z.dot(Z.T) (OpenBLAS syrk, the reference's snpdata.py:203-206 / snpreader.py:655)."""
     n, b = 10_000, 2048
@@ -396,6 +462,22 @@ def main():
                             "unit": "TFLOP/s", "frac": r2["mean_tflops"] / MFMA_F32_PEAK_TFLOPS,
                             "traffic": pmc_traffic("f32k::k_syrk<true>", "grm", n, args.grm_block),
                             "kernel": "f32k::k_syrk<true>", "per_launch_flops": n * (n + 1) * args.grm_block}}
+    grm5 = None
+    run5 = args.grm5 == "on" or (args.grm5 == "auto" and dist.world >= 4 and not args.skip_grm)
+    if run5:
+        r3 = leg_grm5(N, args, dist)
+        n5, m5 = args.grm5_iid, args.grm5_sid
+        gf5 = n5 * (n5 + 1) * m5 / r3["wall"] / 1e9
+        grm5 = {"workload": "cfg5: %d iid x %d SNP (one block of the 1M), Unit, f32 MFMA, K as 256x256 blocks "
+                            "partitioned over %d rank(s), no reduction" % (n5, m5, dist.world),
+                "gflops": gf5, "seconds": r3["wall"], "scaling": "strong",
+                "blocks_on_rank0": r3["n_local_blocks"], "K_bytes_per_rank": r3["n_local_blocks"] * 256 * 256 * 4,
+                "roofline": {"bound": "mfma", "achieved": gf5 / 1e3 / dist.world, "peak": MFMA_F32_PEAK_TFLOPS,
+                             "unit": "TFLOP/s per GPU", "frac": gf5 / 1e3 / dist.world / MFMA_F32_PEAK_TFLOPS,
+                             "traffic": None, "kernel": "f32w::k_syrk256<1,true>"},
+                "projected_seconds_1M_snps": r3["wall"] * 1_000_000 / m5}
+        if r3.get("parity_sample") is not None:
+            grm5["parity"] = grm5_parity(args, *r3["parity_sample"])
     if dist.rank == 0:
         cpu = None
         parity = None
@@ -426,6 +508,7 @@ def main():
             "cpu_baseline": cpu,
             "parity": parity,
             "grm": grm,
+            "grm5": grm5,
         }
         print(json.dumps(line), flush=True)
     dist.close()

@@ -171,6 +171,15 @@ int snpmi_dev_repack(const uint8_t* src, uint64_t src_pitch, uint64_t n_src_iid,
 uint64_t snpmi_grm_tile_bytes(uint64_t n_iid, int dtype);
 int snpmi_dev_syrk_packed(const uint8_t* packed, uint64_t pitch, uint64_t n_iid, uint64_t n_sid,
                           const void* lut, int dtype, void* K_tiles, int accumulate);
+/* cfg5 mode (K too large to replicate): rank `part_rank` of `part_world` owns the
+ * 256x256 blocks L = b*part_world + part_rank (b = 0..n_local-1) of the upper-triangle block
+ * list of the n x n K and stores each as a full row-major 256x256 f32 block at blocks + b*65536.
+ * Every rank reads all SNPs; no reduction is needed. */
+uint64_t snpmi_grm_part_blocks(uint64_t n_iid, int part_rank, int part_world);
+int snpmi_grm_part_coords(uint64_t n_iid, int part_rank, int part_world, uint64_t local_block,
+                          uint64_t* row0, uint64_t* col0);
+int snpmi_dev_syrk_packed_part(const uint8_t* packed, uint64_t pitch, uint64_t n_iid, uint64_t n_sid,
+                               const void* lut, int part_rank, int part_world, void* blocks, int accumulate);
 int snpmi_dev_syrk_dense(const void* Z, uint64_t ldz, uint64_t n_iid, uint64_t n_sid, int dtype,
                          void* K_tiles, int accumulate);
 /* tiles -> K[ri[r], ci[c]] (ri/ci NULL = identity), scaled by `scale` */

@@ -290,3 +290,22 @@ int oracle_synth_bed(uint64_t seed, uint64_t n_iid, uint64_t sid0, uint64_t n_si
     }
     return 0;
 }
+
+/* Per-SNP code counts (c0, c1=missing, c2, c3) over all iids, and the one-pass stats they give
+ * (same formula as above; f64).  Lets a checker get the stats of a wide matrix without
+ * materialising the decoded values. */
+int oracle_snp_stats(const uint8_t* body, uint64_t n_iid, uint64_t n_sid, int count_a1, double* stats,
+                     int num_threads) {
+    uint64_t bpc = (n_iid + 3) / 4;
+    set_threads(num_threads);
+    _Pragma("omp parallel for schedule(dynamic, 4)")
+    for (int64_t j = 0; j < (int64_t)n_sid; j++) {
+        const uint8_t* col = body + (uint64_t)j * bpc;
+        uint64_t cnt[4] = {0, 0, 0, 0};
+        for (uint64_t i = 0; i < n_iid; i++) cnt[code_at(col, i)]++;
+        uint64_t c_hi = count_a1 ? cnt[0] : cnt[3];
+        stats_from_sums((double)(n_iid - cnt[1]), (double)(cnt[2] + 2 * c_hi), (double)(cnt[2] + 4 * c_hi),
+                        &stats[2 * j], &stats[2 * j + 1]);
+    }
+    return 0;
+}

@@ -58,6 +58,8 @@ def lib():
             fn = getattr(L, name)
             fn.argtypes = [vp, u64, u64, u64, i32, vp, u64, vp, u64, i32, vp]
             fn.restype = i32
+        L.oracle_snp_stats.argtypes = [vp, u64, u64, i32, vp, i32]
+        L.oracle_snp_stats.restype = i32
         L.oracle_beta_pdf.argtypes = [f64, f64, f64]
         L.oracle_beta_pdf.restype = f64
         L.oracle_synth_bed.argtypes = [u64, u64, u64, u64, u64, vp, vp, i32, f64, vp, i32]
@@ -121,6 +123,14 @@ def decode_standardize(body, n_iid, n_sid, is_beta=False, a=np.nan, b=np.nan, co
     fn(_ptr(np.ascontiguousarray(body)), n_iid, n_sid, int(bool(count_A1)), _ptr(sid), len(sid),
        int(bool(is_beta)), float(a), float(b), _ptr(out), _ptr(stats), num_threads)
     return out, stats
+
+
+def snp_stats(body, n_iid, n_sid, count_A1=False, num_threads=0):
+    """One-pass (mean, std) per SNP in f64 from code counts, without decoding the matrix."""
+    stats = np.empty((n_sid, 2), dtype=np.float64)
+    lib().oracle_snp_stats(_ptr(np.ascontiguousarray(body)), n_iid, n_sid, int(bool(count_A1)), _ptr(stats),
+                           num_threads)
+    return stats
 
 
 # ----------------------------------------------------------------------------- standardize

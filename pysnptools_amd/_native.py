@@ -71,6 +71,9 @@ _SIGS = {
     "snpmi_dev_decode_standardize": [_vp, _u64, _u64, _u64, _i32, _i32, _f64, _f64, _i32, _i32, _vp, _vp, _vp, _u64],
     "snpmi_dev_repack": [_vp, _u64, _u64, _vp, _u64, _u64, _vp, _u64],
     "snpmi_dev_syrk_packed": [_vp, _u64, _u64, _u64, _vp, _i32, _vp, _i32],
+    "snpmi_grm_part_blocks": [_u64, _i32, _i32],
+    "snpmi_grm_part_coords": [_u64, _i32, _i32, _u64, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)],
+    "snpmi_dev_syrk_packed_part": [_vp, _u64, _u64, _u64, _vp, _i32, _i32, _vp, _i32],
     "snpmi_dev_syrk_dense": [_vp, _u64, _u64, _u64, _i32, _vp, _i32],
     "snpmi_dev_grm_extract": [_vp, _u64, _i32, _vp, _u64, _vp, _u64, _i32, _f64, _vp],
     "snpmi_dev_grm_trace": [_vp, _u64, _i32, _dp],
@@ -83,7 +86,7 @@ _SIGS = {
     "snpmi_last_error": [],
 }
 _RESTYPES = {"snpmi_last_error": ctypes.c_char_p, "snpmi_packed_pitch": ctypes.c_uint64,
-             "snpmi_grm_tile_bytes": ctypes.c_uint64}
+             "snpmi_grm_tile_bytes": ctypes.c_uint64, "snpmi_grm_part_blocks": ctypes.c_uint64}
 
 _lib = None
 _load_error = None

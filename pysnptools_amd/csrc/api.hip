@@ -758,6 +758,34 @@ int snpmi_dev_syrk_packed(const uint8_t* packed, uint64_t pitch, uint64_t n_iid,
     });
 }
 
+uint64_t snpmi_grm_part_blocks(uint64_t n_iid, int part_rank, int part_world) {
+    if (part_world < 1 || part_rank < 0 || part_rank >= part_world) return 0;
+    return grm_part_blocks(n_iid, part_rank, part_world);
+}
+
+int snpmi_grm_part_coords(uint64_t n_iid, int part_rank, int part_world, uint64_t local_block, uint64_t* row0,
+                          uint64_t* col0) {
+    return guarded([&] {
+        SNPMI_REQUIRE(part_world >= 1 && part_rank >= 0 && part_rank < part_world, SNPMI_E_ARG, "bad partition");
+        SNPMI_REQUIRE(local_block < grm_part_blocks(n_iid, part_rank, part_world), SNPMI_E_INDEX, "block out of range");
+        const uint64_t L = local_block * part_world + part_rank;
+        uint64_t j = (uint64_t)((std::sqrt(8.0 * (double)L + 1.0) - 1.0) * 0.5);
+        while ((j + 1) * (j + 2) / 2 <= L) j++;
+        while (j * (j + 1) / 2 > L) j--;
+        if (row0) *row0 = (L - j * (j + 1) / 2) * 256;
+        if (col0) *col0 = j * 256;
+    });
+}
+
+int snpmi_dev_syrk_packed_part(const uint8_t* packed, uint64_t pitch, uint64_t n_iid, uint64_t n_sid, const void* lut,
+                               int part_rank, int part_world, void* blocks, int accumulate) {
+    return guarded([&] {
+        SNPMI_REQUIRE(part_world >= 1 && part_rank >= 0 && part_rank < part_world, SNPMI_E_ARG, "bad partition");
+        SNPMI_REQUIRE(pitch % 64 == 0 && pitch >= ceil_div(n_iid, 4), SNPMI_E_ARG, "pitch must be snpmi_packed_pitch");
+        launch_syrk_packed_part(packed, pitch, n_iid, n_sid, lut, part_rank, part_world, blocks, accumulate, stream());
+    });
+}
+
 int snpmi_dev_syrk_dense(const void* Z, uint64_t ldz, uint64_t n_iid, uint64_t n_sid, int dtype, void* K_tiles,
                          int accumulate) {
     return guarded([&] {

@@ -110,6 +110,9 @@ void launch_synth(uint8_t* packed, uint64_t pitch, uint64_t n_iid, uint64_t sid0
 // ------------------------------------------------------------------ MFMA SYRK (syrk.hip)
 void launch_syrk_packed(const uint8_t* packed, uint64_t pitch, uint64_t n_iid, uint64_t n_sid, const void* lut,
                         int dtype, void* tiles, int accumulate, hipStream_t st);
+uint64_t grm_part_blocks(uint64_t n, int rank, int world);
+void launch_syrk_packed_part(const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m, const void* lut,
+                             int rank, int world, void* blocks, int accumulate, hipStream_t st);
 void launch_syrk_dense(const void* Z, uint64_t ldz, uint64_t n_iid, uint64_t n_sid, int dtype, void* tiles,
                        int accumulate, hipStream_t st);
 

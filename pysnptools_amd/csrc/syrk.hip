@@ -387,13 +387,17 @@ __global__ __launch_bounds__(256, 4) void k_syrk_ablate(const uint8_t* __restric
 namespace f32w {
 constexpr int BW = 256, BK = 16, LDA = 256;
 
-template <int MINB>
+// LOCAL (cfg5, K too large to replicate): this rank owns blocks L = blockIdx.x * world + rank
+// of the upper-triangle block list and writes each as a full 256x256 row-major block at
+// tiles + blockIdx.x * 65536 (no cross-rank reduction is needed).
+template <int MINB, bool LOCAL = false>
 __global__ __launch_bounds__(512, MINB) void k_syrk256(const uint8_t* __restrict__ P, uint64_t pitch, uint64_t n,
                                                       uint64_t kdim, const float* __restrict__ lut,
-                                                      float* __restrict__ tiles, int accumulate) {
+                                                      float* __restrict__ tiles, int accumulate,
+                                                      uint32_t part_rank = 0, uint32_t part_world = 1) {
     __shared__ __attribute__((aligned(16))) float lds[2][2][BK * LDA];
     uint32_t bi, bj;
-    tile_coords(blockIdx.x, bi, bj);
+    tile_coords(LOCAL ? (uint64_t)blockIdx.x * part_world + part_rank : (uint64_t)blockIdx.x, bi, bj);
     const uint64_t i0 = (uint64_t)bi * BW, j0 = (uint64_t)bj * BW;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int wm = wave >> 2, wn = wave & 3;
@@ -462,24 +466,32 @@ __global__ __launch_bounds__(512, MINB) void k_syrk256(const uint8_t* __restrict
         if (more) store(op ? lds[buf ^ 1][1] : lds[buf ^ 1][0]);
         __syncthreads();
     }
-    const uint64_t nt128 = (n + 127) / 128;
-    const uint64_t ti = 2 * (uint64_t)bi + wm, tj = 2 * (uint64_t)bj + (wn >> 1);
-    if (ti > tj || tj >= nt128) return;  // wave-uniform
-    float* T = tiles + (tj * (tj + 1) / 2 + ti) * (uint64_t)(BM * BM);
+    float* T;
+    uint64_t ldo;
+    if constexpr (LOCAL) {
+        T = tiles + (uint64_t)blockIdx.x * (BW * BW) + (uint64_t)(wm * 128) * BW + (wn >> 1) * 128;
+        ldo = BW;
+    } else {
+        const uint64_t nt128 = (n + 127) / 128;
+        const uint64_t ti = 2 * (uint64_t)bi + wm, tj = 2 * (uint64_t)bj + (wn >> 1);
+        if (ti > tj || tj >= nt128) return;  // wave-uniform
+        T = tiles + (tj * (tj + 1) / 2 + ti) * (uint64_t)(BM * BM);
+        ldo = BM;
+    }
 #pragma unroll
     for (int x = 0; x < 4; x++)
 #pragma unroll
         for (int y = 0; y < 2; y++) {
-            float* bp = T + (32 * x + 4 * (lane >> 5)) * BM + (wn & 1) * 64 + 32 * y + (lane & 31);
+            float* bp = T + (32 * x + 4 * (lane >> 5)) * ldo + (wn & 1) * 64 + 32 * y + (lane & 31);
             if (accumulate) {
                 float old[16];
 #pragma unroll
-                for (int r = 0; r < 16; r++) old[r] = bp[((r & 3) + 8 * (r >> 2)) * BM];
+                for (int r = 0; r < 16; r++) old[r] = bp[((r & 3) + 8 * (r >> 2)) * ldo];
 #pragma unroll
                 for (int r = 0; r < 16; r++) acc[x][y][r] += old[r];
             }
 #pragma unroll
-            for (int r = 0; r < 16; r++) bp[((r & 3) + 8 * (r >> 2)) * BM] = acc[x][y][r];
+            for (int r = 0; r < 16; r++) bp[((r & 3) + 8 * (r >> 2)) * ldo] = acc[x][y][r];
         }
 }
 }  // namespace f32w
@@ -681,6 +693,25 @@ void launch_syrk_packed(const uint8_t* packed, uint64_t pitch, uint64_t n, uint6
     else
         f64k::k_syrk<true><<<(unsigned)nt, 256, 0, st>>>(packed, pitch, m, (const double*)lut, (double*)tiles,
                                                           accumulate);
+    SNPMI_HIP(hipGetLastError());
+}
+
+uint64_t grm_part_blocks(uint64_t n, int rank, int world) {
+    const uint64_t nb = ceil_div(n, 256), total = nb * (nb + 1) / 2;
+    return total > (uint64_t)rank ? (total - rank + world - 1) / world : 0;
+}
+
+void launch_syrk_packed_part(const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m, const void* lut,
+                             int rank, int world, void* blocks, int accumulate, hipStream_t st) {
+    const uint64_t nloc = grm_part_blocks(n, rank, world);
+    if (nloc == 0) return;
+    SNPMI_REQUIRE(nloc < (1ull << 31), SNPMI_E_ARG, "too many GRM blocks for one launch");
+    if (m == 0) {
+        if (!accumulate) SNPMI_HIP(hipMemsetAsync(blocks, 0, nloc * 256 * 256 * sizeof(float), st));
+        return;
+    }
+    f32w::k_syrk256<1, true><<<(unsigned)nloc, 512, 0, st>>>(packed, pitch, n, m, (const float*)lut, (float*)blocks,
+                                                             accumulate, (uint32_t)rank, (uint32_t)world);
     SNPMI_HIP(hipGetLastError());
 }
 

@@ -147,3 +147,26 @@ def test_bed_reader_compat_surface():
         assert ob.iid_count == 300 and ob.sid_count == 1015
         assert ob.fid[0] == "POP1" and len(ob.sid) == 1015 and ob.chromosome[0] == "1"
     assert br.get_num_threads(3) == 3
+
+
+@pytest.mark.parametrize("n,world", [(1, 1), (256, 2), (300, 3), (1000, 4), (5000, 8), (500000, 8)])
+def test_grm_partition_covers_upper_triangle_once(n, world):
+    """cfg5 block ownership (snpmi_grm_part_*): disjoint, complete, balanced (pure host arithmetic)."""
+    import ctypes
+
+    from pysnptools_amd import _native as N
+
+    nb = (n + 255) // 256
+    total = nb * (nb + 1) // 2
+    counts = [N.lib().snpmi_grm_part_blocks(n, r, world) for r in range(world)]
+    assert sum(counts) == total and max(counts) - min(counts) <= 1
+    if total > 20000:
+        return
+    seen = set()
+    r0, c0 = ctypes.c_uint64(), ctypes.c_uint64()
+    for r in range(world):
+        for b in range(counts[r]):
+            N.call("snpmi_grm_part_coords", n, r, world, b, ctypes.byref(r0), ctypes.byref(c0))
+            assert r0.value <= c0.value and c0.value < nb * 256
+            seen.add((r0.value, c0.value))
+    assert len(seen) == total

@@ -408,3 +408,39 @@ def test_device_decode_standardize_large_properties(dtype):
     poly = np.isfinite(stats[:, 1])
     assert np.abs(v64.sum(1)[poly]).max() < 1e-2 * n ** 0.5
     assert np.all(v64[~poly] == 0)
+
+
+@pytest.mark.parametrize("n,world", [(300, 1), (700, 3), (1100, 4)])
+def test_grm_partitioned_blocks_assemble_k(n, world):
+    """cfg5 mode: every rank's 256x256 blocks (simulated ranks on one GPU) assemble to K."""
+    rng = np.random.default_rng(n)
+    val = rng.integers(0, 3, size=(n, 45)).astype(np.float64)
+    val[rng.random(val.shape) < 0.03] = np.nan
+    d = SnpData(iid=[["a", str(i)] for i in range(n)], sid=["s%d" % j for j in range(45)], val=val)
+    Z = val.astype(np.float32).copy(order="F")
+    O.standardize_native(Z)
+    ref = Z.astype(np.float64).dot(Z.astype(np.float64).T)
+    with tempfile.TemporaryDirectory() as tmp:
+        Bed.write(os.path.join(tmp, "p.bed"), d, count_A1=False)
+        body = O.read_bed_bytes(os.path.join(tmp, "p.bed"))
+    pitch = N.lib().snpmi_packed_pitch(n)
+    host = np.zeros((45, pitch), dtype=np.uint8)
+    bpc = (n + 3) // 4
+    host[:, :bpc] = body.reshape(45, bpc)
+    packed = Dev(host.nbytes)
+    packed.put(host)
+    lut, st = Dev(45 * 16), Dev(45 * 8)
+    N.call("snpmi_dev_snp_stats", packed.p, pitch, n, 45, 0, N.STD_UNIT, 0.0, 0.0, 0, N.DT_F32, st.p, lut.p)
+    K = np.full((((n + 255) // 256) * 256,) * 2, np.nan)
+    r0, c0 = ctypes.c_uint64(), ctypes.c_uint64()
+    for r in range(world):
+        nloc = N.lib().snpmi_grm_part_blocks(n, r, world)
+        blocks = Dev(max(nloc, 1) * 256 * 256 * 4)
+        N.call("snpmi_dev_syrk_packed_part", packed.p, pitch, n, 45, lut.p, r, world, blocks.p, 0)
+        out = blocks.get(np.empty((max(nloc, 1), 256, 256), dtype=np.float32))
+        for b in range(nloc):
+            N.call("snpmi_grm_part_coords", n, r, world, b, ctypes.byref(r0), ctypes.byref(c0))
+            i, j = r0.value, c0.value
+            K[i:i + 256, j:j + 256] = out[b]
+            K[j:j + 256, i:i + 256] = out[b].T
+    grm_close(K[:n, :n], ref, 1e-5)

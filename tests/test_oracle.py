@@ -79,6 +79,12 @@ def test_standardize_vs_reference_python(name, tag, dtype, tol, order):
         np.testing.assert_allclose(v, G["%s_%s" % (std, tag)], rtol=tol, atol=tol)
 
 
+def test_snp_stats_matches_standardize():
+    st = O.snp_stats(body("n300"), 300, 1015)
+    v = O.decode(body("n300"), 300, 1015)
+    assert np.array_equal(st, O.standardize_native(v), equal_nan=True)
+
+
 def test_fused_decode_standardize_equals_two_step():
     for dtype in (np.float64, np.float32):
         for is_beta in (False, True):
