@@ -331,49 +331,70 @@ def leg_grm(N, args, dist, rccl):
 
 # ---------------------------------------------------------------------------- leg 3: cfg5 partitioned GRM
 def leg_grm5(N, args, dist):
-    """configs[4] shape: 500k iids, K (500 GB upper triangle f32) partitioned over ranks as
-    256x256 blocks; every rank holds the same packed SNP block (same seed) and computes only
-    its blocks -- no reduction.  One timed pass over --grm5-sid SNPs (GRM time is linear in M)."""
-    n, m = args.grm5_iid, args.grm5_sid
+    """configs[4] shape: 500k iids, K (500 GB upper triangle f32)
+    partitioned over ranks as 256x256 blocks.  Per SNP block each rank uploads ITS 1/p of the
+    packed columns from pinned host memory, ncclAllGather rebuilds the packed block on every
+    rank, then stats + the fused SYRK fill only the rank's own K blocks -- no reduction.
+    One timed block of --grm5-sid SNPs (GRM time is linear in M)."""
+    n, p = args.grm5_iid, dist.world
+    m = (args.grm5_sid + p - 1) // p * p
+    ms = m // p
     pitch = N.lib().snpmi_packed_pitch(n)
-    nloc = N.lib().snpmi_grm_part_blocks(n, dist.rank, dist.world)
+    nloc = N.lib().snpmi_grm_part_blocks(n, dist.rank, p)
     packed = Dev(N, pitch * m)
-    synth(N, packed.p, pitch, n, 0, m, args.seed + 200, 0.01)
+    mine = packed.p.value + dist.rank * ms * pitch
+    # the rank's shard of the .bed, staged in page-locked memory (untimed, like reading the file)
+    host = ctypes.c_void_p()
+    N.call("snpmi_host_alloc", ctypes.byref(host), ms * pitch)
+    synth(N, mine, pitch, n, dist.rank * ms, ms, args.seed + 200, 0.01)
+    N.call("snpmi_memcpy_d2h", host, mine, ms * pitch)
+    N.call("snpmi_dev_memset", packed.p, 0, pitch * m)
     lut, stats = Dev(N, m * 16), Dev(N, m * 8)
     blocks = Dev(N, max(nloc, 1) * 256 * 256 * 4)
-    ev = Events(N, 2)
-    N.call("snpmi_dev_snp_stats", packed.p, pitch, n, m, 0, N.STD_UNIT, 0.0, 0.0, 0, N.DT_F32, stats.p, lut.p)
+    ev = Events(N, 4)
     N.call("snpmi_stream_sync")
     dist.barrier()
     t0 = time.perf_counter()
     ev.record(0)
-    N.call("snpmi_dev_snp_stats", packed.p, pitch, n, m, 0, N.STD_UNIT, 0.0, 0.0, 0, N.DT_F32, stats.p, lut.p)
-    N.call("snpmi_dev_syrk_packed_part", packed.p, pitch, n, m, lut.p, dist.rank, dist.world, blocks.p, 0)
+    N.call("snpmi_memcpy_h2d", mine, host, ms * pitch)
     ev.record(1)
+    if dist.rccl:
+        N.call("snpmi_rccl_allgather", mine, packed.p, ms * pitch)
+    ev.record(2)
+    N.call("snpmi_dev_snp_stats", packed.p, pitch, n, m, 0, N.STD_UNIT, 0.0, 0.0, 0, N.DT_F32, stats.p, lut.p)
+    N.call("snpmi_dev_syrk_packed_part", packed.p, pitch, n, m, lut.p, dist.rank, p, blocks.p, 0)
+    ev.record(3)
     N.call("snpmi_stream_sync")
     dist.barrier()
     wall = dist.max(time.perf_counter() - t0)
-    kern_ms = ev.ms(0, 1)
-    res = {"wall": wall, "kernel_ms": kern_ms, "n_local_blocks": nloc}
+    res = {"wall": wall, "h2d_ms": ev.ms(0, 1), "allgather_ms": ev.ms(1, 2), "syrk_ms": ev.ms(2, 3),
+           "n_local_blocks": nloc, "m": m}
     if dist.rank == 0 and not args.skip_cpu and nloc > 0:
         r0, c0 = ctypes.c_uint64(), ctypes.c_uint64()
-        N.call("snpmi_grm_part_coords", n, 0, dist.world, 0, ctypes.byref(r0), ctypes.byref(c0))
+        N.call("snpmi_grm_part_coords", n, 0, p, 0, ctypes.byref(r0), ctypes.byref(c0))
         blk = np.empty((256, 256), dtype=np.float32)
         N.call("snpmi_memcpy_d2h", N.ptr(blk), blocks.p, blk.nbytes)
         sample = np.empty((m, pitch), dtype=np.uint8)
         N.call("snpmi_memcpy_d2h", N.ptr(sample), packed.p, sample.nbytes)
+        # the gathered block must equal the whole block generated in one piece
+        synth(N, packed.p, pitch, n, 0, m, args.seed + 200, 0.01)
+        whole = np.empty_like(sample)
+        N.call("snpmi_memcpy_d2h", N.ptr(whole), packed.p, whole.nbytes)
+        res["gather_exact"] = bool(np.array_equal(sample, whole))
+        del whole
         res["parity_sample"] = (blk, sample, r0.value, c0.value)
     ev.destroy()
+    N.call("snpmi_host_free", host)
     for d in (packed, lut, stats, blocks):
         d.free()
     return res
 
 
-def grm5_parity(args, blk, sample, row0, col0):
+def grm5_parity(args, m, blk, sample, row0, col0):
     """Oracle (f64) for one 256x256 block of the partitioned K: decode only its 512 iids."""
     from oracle import oracle as O
 
-    n, m = args.grm5_iid, args.grm5_sid
+    n = args.grm5_iid
     bpc = (n + 3) // 4
     body = np.ascontiguousarray(sample[:, :bpc]).reshape(-1)
     rows = np.arange(row0, min(row0 + 256, n))
@@ -460,16 +481,18 @@ def main():
                "allreduce_ms": r2["allreduce_ms"], "trace_K": r2["trace"],
                "roofline": {"bound": "mfma", "achieved": r2["mean_tflops"], "peak": MFMA_F32_PEAK_TFLOPS,
                             "unit": "TFLOP/s", "frac": r2["mean_tflops"] / MFMA_F32_PEAK_TFLOPS,
-                            "traffic": pmc_traffic("f32k::k_syrk<true>", "grm", n, args.grm_block),
-                            "kernel": "f32k::k_syrk<true>", "per_launch_flops": n * (n + 1) * args.grm_block}}
+                            "traffic": pmc_traffic("f32w::k_syrk256", "grm", n, args.grm_block),
+                            "kernel": "f32w::k_syrk256<1,false>", "per_launch_flops": n * (n + 1) * args.grm_block}}
     grm5 = None
     run5 = args.grm5 == "on" or (args.grm5 == "auto" and dist.world >= 4 and not args.skip_grm)
     if run5:
         r3 = leg_grm5(N, args, dist)
-        n5, m5 = args.grm5_iid, args.grm5_sid
+        n5, m5 = args.grm5_iid, r3["m"]
         gf5 = n5 * (n5 + 1) * m5 / r3["wall"] / 1e9
-        grm5 = {"workload": "cfg5: %d iid x %d SNP (one block of the 1M), Unit, f32 MFMA, K as 256x256 blocks "
-                            "partitioned over %d rank(s), no reduction" % (n5, m5, dist.world),
+        grm5 = {"workload": "cfg5: %d iid x %d SNP (one block of the 1M), Unit, f32 MFMA; each rank uploads 1/%d "
+                            "of the packed block from pinned host, RCCL all-gather, K as 256x256 blocks "
+                            "partitioned over %d rank(s), no reduction" % (n5, m5, dist.world, dist.world),
+                "h2d_ms": r3["h2d_ms"], "allgather_ms": r3["allgather_ms"], "syrk_ms": r3["syrk_ms"],
                 "gflops": gf5, "seconds": r3["wall"], "scaling": "strong",
                 "blocks_on_rank0": r3["n_local_blocks"], "K_bytes_per_rank": r3["n_local_blocks"] * 256 * 256 * 4,
                 "roofline": {"bound": "mfma", "achieved": gf5 / 1e3 / dist.world, "peak": MFMA_F32_PEAK_TFLOPS,
@@ -477,7 +500,9 @@ def main():
                              "traffic": None, "kernel": "f32w::k_syrk256<1,true>"},
                 "projected_seconds_1M_snps": r3["wall"] * 1_000_000 / m5}
         if r3.get("parity_sample") is not None:
-            grm5["parity"] = grm5_parity(args, *r3["parity_sample"])
+            grm5["parity"] = grm5_parity(args, m5, *r3["parity_sample"])
+            grm5["parity"]["gathered_block_bit_exact"] = r3["gather_exact"]
+            grm5["parity"]["pass"] = grm5["parity"]["pass"] and r3["gather_exact"]
     if dist.rank == 0:
         cpu = None
         parity = None

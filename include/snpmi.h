@@ -82,6 +82,30 @@ int snpmi_bed_read_i8(const char* path, uint64_t n_iid, uint64_t n_sid, int coun
                       const uint64_t* iid_idx, uint64_t n_out_iid, const uint64_t* sid_idx,
                       uint64_t n_out_sid, int order_c, int8_t* out, int num_threads);
 
+/* ---------------------------------------------------------------- .fam/.bim metadata (host, threaded)
+ * Replaces the text parsing behind bed-reader open_bed's properties (fid/iid/sid/chromosome/
+ * cm_position/bp_position; snpreader/bed.py:137-194).  Lines are split on whitespace, blank
+ * lines skipped.  scan: number of rows and the widest field of columns 0..n_cols-1 (every line
+ * must have >= min_fields fields, else SNPMI_E_FORMAT).  strings: column `col` as fixed-width
+ * NUL-padded rows of `width` bytes.  f64: column `col` parsed as a float (SNPMI_E_FORMAT if
+ * it is not one).  No GPU is needed. */
+int snpmi_text_scan(const char* path, int min_fields, int n_cols, uint64_t* n_rows, uint64_t* widths,
+                    int num_threads);
+int snpmi_text_strings(const char* path, int col, uint64_t n_rows, uint64_t width, char* out, int num_threads);
+int snpmi_text_f64(const char* path, int col, uint64_t n_rows, double* out, int num_threads);
+
+/* ---------------------------------------------------------------- BED writing (bed-reader to_bed body)
+ * Replaces the genotype half of `to_bed(filepath, val, properties, count_A1, ...)`
+ * (snpreader/bed.py:300-314); the .fam/.bim text is written by the host.  val is
+ * n_iid x n_sid (F or C order); values must be 0, 1, 2 or missing (NaN; -127 for int8),
+ * anything else -> SNPMI_E_ARG (ValueError) and no file is left behind. */
+int snpmi_bed_write_f32(const char* path, const float* val, uint64_t n_iid, uint64_t n_sid, int order_c,
+                        int count_a1, int num_threads);
+int snpmi_bed_write_f64(const char* path, const double* val, uint64_t n_iid, uint64_t n_sid, int order_c,
+                        int count_a1, int num_threads);
+int snpmi_bed_write_i8(const char* path, const int8_t* val, uint64_t n_iid, uint64_t n_sid, int order_c,
+                       int count_a1, int num_threads);
+
 /* ---------------------------------------------------------------- standardize (bed-reader standardize_*) */
 int snpmi_standardize_f32(float* val, uint64_t rows, uint64_t cols, int order_c, int is_beta,
                           double a, double b, int apply_in_place, int use_stats, float* stats,
@@ -139,6 +163,9 @@ int snpmi_diag_k_to_n_f64(double* K, uint64_t n, double* factor);
 uint64_t snpmi_packed_pitch(uint64_t n_iid);
 int snpmi_dev_alloc(void** ptr, uint64_t bytes);
 int snpmi_dev_free(void* ptr);
+/* page-locked host memory (the staging side of streamed SNP blocks) */
+int snpmi_host_alloc(void** ptr, uint64_t bytes);
+int snpmi_host_free(void* ptr);
 int snpmi_dev_memset(void* ptr, int value, uint64_t bytes);
 int snpmi_memcpy_h2d(void* dst, const void* src, uint64_t bytes);
 int snpmi_memcpy_d2h(void* dst, const void* src, uint64_t bytes);
@@ -163,6 +190,11 @@ int snpmi_dev_decode(const uint8_t* packed, uint64_t pitch, uint64_t n_iid, uint
 int snpmi_dev_decode_standardize(const uint8_t* packed, uint64_t pitch, uint64_t n_iid, uint64_t n_sid,
                                  int count_a1, int std_kind, double a, double b, int use_stats, int dtype,
                                  void* stats, void* lut, void* out, uint64_t ld);
+/* values (dtype, F: column j at val + j*ld with ld % 16 == 0; C: row i at val + i*ld) -> packed
+ * codes; *bad_values (if non-NULL; synchronises) = number of waves that saw a value outside
+ * {0,1,2,missing} (0 = all valid) */
+int snpmi_dev_encode(const void* val, int dtype, int order_c, uint64_t ld, uint64_t n_iid, uint64_t n_sid,
+                     int count_a1, uint8_t* packed, uint64_t pitch, uint64_t* bad_values);
 /* iid gather: dst column j = src column j restricted to iids idx[0..n_out) */
 int snpmi_dev_repack(const uint8_t* src, uint64_t src_pitch, uint64_t n_src_iid, const uint64_t* idx,
                      uint64_t n_out_iid, uint64_t n_sid, uint8_t* dst, uint64_t dst_pitch);
@@ -191,6 +223,9 @@ int snpmi_dev_grm_trace(const void* K_tiles, uint64_t n_iid, int dtype, double* 
 int snpmi_rccl_unique_id(uint8_t* id, uint64_t id_len);   /* id_len >= 128 */
 int snpmi_rccl_init(int nranks, int rank, const uint8_t* id, uint64_t id_len);
 int snpmi_rccl_allreduce_sum(void* buf, uint64_t count, int dtype);
+/* cfg5: every rank contributes bytes_per_rank bytes; recv gets them concatenated in rank
+ * order (send may alias recv + rank * bytes_per_rank) */
+int snpmi_rccl_allgather(const void* send, void* recv, uint64_t bytes_per_rank);
 /* host-value all-reduce (op 0 = sum, 1 = max) of f64 scalars, synchronous; barrier = 1-elem sum */
 int snpmi_rccl_host_allreduce_f64(double* values, uint64_t count, int op);
 int snpmi_rccl_barrier(void);

@@ -12,6 +12,7 @@ restatements that the reference itself runs in NumPy:
   ``K += Z_b.dot(Z_b.T)`` over SNP blocks, float64 by default.
 * ``diag_k_to_n``         -- ``DiagKtoN._standardize_kernel`` (diag_K_to_N.py:54-64).
 * ``maf_table``           -- SnpGen's MAF distribution (snpreader/snpgen.py:140-151).
+* ``encode``              -- bed-reader ``to_bed``'s 2-bit encoder (Bed.write, bed.py:300-314).
 
 Pinning: tests/test_oracle.py checks every function here against the reference's own
 fixtures and against golden vectors made by running the reference (tools/make_golden.py).
@@ -131,6 +132,31 @@ def snp_stats(body, n_iid, n_sid, count_A1=False, num_threads=0):
     lib().oracle_snp_stats(_ptr(np.ascontiguousarray(body)), n_iid, n_sid, int(bool(count_A1)), _ptr(stats),
                            num_threads)
     return stats
+
+
+def encode(val, count_A1=False):
+    """bed-reader to_bed's body encoder restated (called from bed.py:300-314): n_iid x n_sid values
+    -> SNP-major packed bytes [n_sid, ceil(n_iid/4)].  count_A1=False: 0->00, 1->10, 2->11,
+    missing->01 (count_A1=True swaps 0/2); pad codes 00.  Pinned against the reference-written
+    generate/gen1.bed, gen4.bed (N % 4 == 2) and the N300 .bed (tests/test_oracle.py)."""
+    val = np.asarray(val)
+    n, m = val.shape
+    if val.dtype == np.int8:
+        miss = val == -127
+        v = val.astype(np.int16)
+    else:
+        miss = np.isnan(val)
+        v = np.where(miss, 0, val)
+    if not np.all(miss | (v == 0) | (v == 1) | (v == 2)):
+        raise ValueError("Expect values to be 0, 1, 2 or missing")
+    lut = np.array([3, 2, 0], dtype=np.uint8) if count_A1 else np.array([0, 2, 3], dtype=np.uint8)
+    codes = np.where(miss, np.uint8(1), lut[np.clip(v, 0, 2).astype(np.intp)]).astype(np.uint8)
+    bpc = (n + 3) // 4
+    padded = np.zeros((bpc * 4, m), dtype=np.uint8)
+    padded[:n] = codes
+    q = padded.reshape(bpc, 4, m)
+    packed = q[:, 0] | (q[:, 1] << 2) | (q[:, 2] << 4) | (q[:, 3] << 6)
+    return np.ascontiguousarray(packed.T)
 
 
 # ----------------------------------------------------------------------------- standardize

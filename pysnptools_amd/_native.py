@@ -36,6 +36,12 @@ _SIGS = {
     "snpmi_bed_read_f32": [_cp, _u64, _u64, _i32, _vp, _u64, _vp, _u64, _i32, _vp, _i32],
     "snpmi_bed_read_f64": [_cp, _u64, _u64, _i32, _vp, _u64, _vp, _u64, _i32, _vp, _i32],
     "snpmi_bed_read_i8": [_cp, _u64, _u64, _i32, _vp, _u64, _vp, _u64, _i32, _vp, _i32],
+    "snpmi_text_scan": [_cp, _i32, _i32, ctypes.POINTER(ctypes.c_uint64), _vp, _i32],
+    "snpmi_text_strings": [_cp, _i32, _u64, _u64, _vp, _i32],
+    "snpmi_text_f64": [_cp, _i32, _u64, _vp, _i32],
+    "snpmi_bed_write_f32": [_cp, _vp, _u64, _u64, _i32, _i32, _i32],
+    "snpmi_bed_write_f64": [_cp, _vp, _u64, _u64, _i32, _i32, _i32],
+    "snpmi_bed_write_i8": [_cp, _vp, _u64, _u64, _i32, _i32, _i32],
     "snpmi_standardize_f32": [_vp, _u64, _u64, _i32, _i32, _f64, _f64, _i32, _i32, _vp, _i32],
     "snpmi_standardize_f64": [_vp, _u64, _u64, _i32, _i32, _f64, _f64, _i32, _i32, _vp, _i32],
     "snpmi_subset_f64_f64": [_vp, _u64, _u64, _u64, _i32, _vp, _u64, _vp, _u64, _i32, _vp, _i32],
@@ -57,6 +63,8 @@ _SIGS = {
     "snpmi_grm_tile_bytes": [_u64, _i32],
     "snpmi_dev_alloc": [ctypes.POINTER(ctypes.c_void_p), _u64],
     "snpmi_dev_free": [_vp],
+    "snpmi_host_alloc": [ctypes.POINTER(ctypes.c_void_p), _u64],
+    "snpmi_host_free": [_vp],
     "snpmi_dev_memset": [_vp, _i32, _u64],
     "snpmi_memcpy_h2d": [_vp, _vp, _u64],
     "snpmi_memcpy_d2h": [_vp, _vp, _u64],
@@ -69,6 +77,7 @@ _SIGS = {
     "snpmi_dev_snp_stats": [_vp, _u64, _u64, _u64, _i32, _i32, _f64, _f64, _i32, _i32, _vp, _vp],
     "snpmi_dev_decode": [_vp, _u64, _u64, _u64, _vp, _i32, _i32, _vp, _u64],
     "snpmi_dev_decode_standardize": [_vp, _u64, _u64, _u64, _i32, _i32, _f64, _f64, _i32, _i32, _vp, _vp, _vp, _u64],
+    "snpmi_dev_encode": [_vp, _i32, _i32, _u64, _u64, _u64, _i32, _vp, _u64, ctypes.POINTER(ctypes.c_uint64)],
     "snpmi_dev_repack": [_vp, _u64, _u64, _vp, _u64, _u64, _vp, _u64],
     "snpmi_dev_syrk_packed": [_vp, _u64, _u64, _u64, _vp, _i32, _vp, _i32],
     "snpmi_grm_part_blocks": [_u64, _i32, _i32],
@@ -80,6 +89,7 @@ _SIGS = {
     "snpmi_rccl_unique_id": [_vp, _u64],
     "snpmi_rccl_init": [_i32, _i32, _vp, _u64],
     "snpmi_rccl_allreduce_sum": [_vp, _u64, _i32],
+    "snpmi_rccl_allgather": [_vp, _vp, _u64],
     "snpmi_rccl_host_allreduce_f64": [_vp, _u64, _i32],
     "snpmi_rccl_barrier": [],
     "snpmi_rccl_destroy": [],

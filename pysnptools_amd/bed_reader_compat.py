@@ -27,12 +27,14 @@ def get_num_threads(num_threads=None):
     return _policy(num_threads)
 
 
-def _table(path):
-    import pandas as pd
+def _columns(path, ncols=6):
+    """The 6 whitespace-delimited PLINK columns of a .fam/.bim as str arrays (C parser)."""
+    from pysnptools_amd.snpreader.bed import _text_scan, _text_strings
 
-    if os.path.getsize(path) == 0:
-        return None
-    return pd.read_csv(path, sep=r"\s+", header=None, dtype=str, keep_default_na=False)
+    rows, w = _text_scan(path, ncols, ncols)
+    if rows == 0:
+        return []
+    return [_text_strings(path, c, rows, w[c]) for c in range(ncols)]
 
 
 class open_bed(object):
@@ -61,14 +63,12 @@ class open_bed(object):
 
     def _famc(self):
         if self._fam_cols is None:
-            t = _table(self._fam)
-            self._fam_cols = [] if t is None else [t[c].to_numpy(dtype=str) for c in t.columns]
+            self._fam_cols = _columns(self._fam)
         return self._fam_cols
 
     def _bimc(self):
         if self._bim_cols is None:
-            t = _table(self._bim)
-            self._bim_cols = [] if t is None else [t[c].to_numpy(dtype=str) for c in t.columns]
+            self._bim_cols = _columns(self._bim)
         return self._bim_cols
 
     def _prop(self, name, fam, col, conv=None):

@@ -317,6 +317,66 @@ static void bed_read_impl(const char* path, uint64_t n_iid, uint64_t n_sid, int 
     }
 }
 
+// ====================================================================== BED write (to_bed body)
+// Values (caller's host array, n_iid x n_sid, F or C) -> .bed file: magic + SNP-major packed
+// columns of ceil(n/4) bytes.  SNP chunks go H2D, are encoded by k_encode_f/c, and come back
+// as packed bytes (16x / 32x smaller) that are written with one fwrite per chunk.
+template <typename T>
+static void bed_write_impl(const char* path, const T* val, uint64_t n, uint64_t m, int order_c, int count_a1) {
+    std::lock_guard<std::recursive_mutex> lk(g_call_mutex);
+    SNPMI_REQUIRE(path != nullptr, SNPMI_E_ARG, "path is NULL");
+    SNPMI_REQUIRE(val != nullptr || n == 0 || m == 0, SNPMI_E_ARG, "val is NULL");
+    Device& d = device();
+    FILE* f = std::fopen(path, "wb");
+    SNPMI_REQUIRE(f != nullptr, SNPMI_E_IO, std::string("cannot create ") + path);
+    struct Closer {
+        FILE*& f;
+        const char* path;
+        bool ok = false;
+        ~Closer() {
+            if (f) std::fclose(f);
+            if (!ok) std::remove(path);
+        }
+    } closer{f, path};
+    const uint8_t magic[3] = {0x6C, 0x1B, 0x01};
+    SNPMI_REQUIRE(std::fwrite(magic, 1, 3, f) == 3, SNPMI_E_IO, std::string("write failed: ") + path);
+    const uint64_t bpc = ceil_div(n, 4), pitch = packed_pitch(n);
+    const int dt = DT<T>::v;
+    unsigned int* bad_dev = (unsigned int*)d.get(Device::S_RED, 256);
+    if (n > 0 && m > 0) {
+        const uint64_t ldF = round_up(n, 16);
+        const uint64_t C = order_c ? std::min<uint64_t>(round_up(chunk_snps(n * sizeof(T) + pitch), 64), 1ull << 16)
+                                   : chunk_snps(ldF * sizeof(T) + pitch);
+        for (uint64_t c0 = 0; c0 < m; c0 += C) {
+            const uint64_t cnt = std::min(C, m - c0);
+            T* dev_val = (T*)d.get(Device::S_DENSE, cnt * (order_c ? n : ldF) * sizeof(T));
+            uint8_t* dev_packed = (uint8_t*)d.get(Device::S_PACKED, cnt * pitch);
+            uint8_t* host = (uint8_t*)pinned(0, cnt * bpc);
+            SNPMI_HIP(hipMemsetAsync(bad_dev, 0, sizeof(unsigned int), d.stream));
+            if (!order_c) {
+                SNPMI_HIP(hipMemcpy2DAsync(dev_val, ldF * sizeof(T), val + c0 * n, n * sizeof(T), n * sizeof(T), cnt,
+                                           hipMemcpyHostToDevice, d.stream));
+                launch_encode(dev_val, dt, 0, ldF, n, cnt, count_a1, dev_packed, pitch, bad_dev, d.stream);
+            } else {
+                SNPMI_HIP(hipMemcpy2DAsync(dev_val, cnt * sizeof(T), val + c0, m * sizeof(T), cnt * sizeof(T), n,
+                                           hipMemcpyHostToDevice, d.stream));
+                launch_encode(dev_val, dt, 1, cnt, n, cnt, count_a1, dev_packed, pitch, bad_dev, d.stream);
+            }
+            unsigned int bad = 0;
+            SNPMI_HIP(hipMemcpyAsync(&bad, bad_dev, sizeof(bad), hipMemcpyDeviceToHost, d.stream));
+            SNPMI_HIP(hipMemcpy2DAsync(host, bpc, dev_packed, pitch, bpc, cnt, hipMemcpyDeviceToHost, d.stream));
+            SNPMI_HIP(hipStreamSynchronize(d.stream));
+            SNPMI_REQUIRE(bad == 0, SNPMI_E_ARG,
+                          "Expect values to be 0, 1, 2 or missing (NaN, or -127 for int8)");
+            SNPMI_REQUIRE(std::fwrite(host, 1, cnt * bpc, f) == cnt * bpc, SNPMI_E_IO,
+                          std::string("write failed: ") + path);
+        }
+    }
+    SNPMI_REQUIRE(std::fclose(f) == 0, SNPMI_E_IO, std::string("write failed: ") + path);
+    f = nullptr;
+    closer.ok = true;
+}
+
 // ====================================================================== dense standardize / subset
 template <typename T>
 static void standardize_impl(T* val, uint64_t rows, uint64_t cols, int order_c, int is_beta, double a, double b,
@@ -588,6 +648,34 @@ SNPMI_BED_READ(i8, int8_t)
 SNPMI_BED_READ_STD(f32, float)
 SNPMI_BED_READ_STD(f64, double)
 
+#define SNPMI_BED_WRITE(SUFFIX, T)                                                                                 \
+    int snpmi_bed_write_##SUFFIX(const char* path, const T* val, uint64_t n_iid, uint64_t n_sid, int order_c,    \
+                                 int count_a1, int) {                                                               \
+        return guarded([&] { bed_write_impl<T>(path, val, n_iid, n_sid, order_c, count_a1); });                   \
+    }
+SNPMI_BED_WRITE(f32, float)
+SNPMI_BED_WRITE(f64, double)
+SNPMI_BED_WRITE(i8, int8_t)
+
+int snpmi_dev_encode(const void* val, int dtype, int order_c, uint64_t ld, uint64_t n_iid, uint64_t n_sid,
+                     int count_a1, uint8_t* packed, uint64_t pitch, uint64_t* bad_values) {
+    return guarded([&] {
+        SNPMI_REQUIRE(pitch % 64 == 0 && pitch >= ceil_div(n_iid, 4), SNPMI_E_ARG, "pitch must be a multiple of 64 >= ceil(n/4)");
+        SNPMI_REQUIRE(order_c || ld % 16 == 0, SNPMI_E_ARG, "F-order ld must be a multiple of 16");
+        SNPMI_REQUIRE(order_c ? ld >= n_sid : ld >= n_iid, SNPMI_E_ARG, "ld too small");
+        Device& d = device();
+        unsigned int* bad_dev = (unsigned int*)d.get(Device::S_RED, 256);
+        SNPMI_HIP(hipMemsetAsync(bad_dev, 0, sizeof(unsigned int), d.stream));
+        launch_encode(val, dtype, order_c, ld, n_iid, n_sid, count_a1, packed, pitch, bad_dev, d.stream);
+        if (bad_values) {
+            unsigned int bad = 0;
+            SNPMI_HIP(hipMemcpyAsync(&bad, bad_dev, sizeof(bad), hipMemcpyDeviceToHost, d.stream));
+            SNPMI_HIP(hipStreamSynchronize(d.stream));
+            *bad_values = bad;
+        }
+    });
+}
+
 int snpmi_standardize_f32(float* val, uint64_t rows, uint64_t cols, int order_c, int is_beta, double a, double b,
                           int apply_in_place, int use_stats, float* stats, int) {
     return guarded([&] { standardize_impl<float>(val, rows, cols, order_c, is_beta, a, b, apply_in_place, use_stats, stats); });
@@ -652,6 +740,22 @@ int snpmi_dev_alloc(void** ptr, uint64_t bytes) {
             (void)hipGetLastError();
             throw Error(SNPMI_E_NOMEM, "hipMalloc of " + std::to_string(bytes) + " bytes failed");
         }
+    });
+}
+int snpmi_host_alloc(void** ptr, uint64_t bytes) {
+    return guarded([&] {
+        SNPMI_REQUIRE(ptr != nullptr, SNPMI_E_ARG, "ptr is NULL");
+        (void)device();
+        if (hipHostMalloc(ptr, bytes ? bytes : 256, hipHostMallocDefault) != hipSuccess) {
+            (void)hipGetLastError();
+            throw Error(SNPMI_E_NOMEM, "hipHostMalloc of " + std::to_string(bytes) + " bytes failed");
+        }
+    });
+}
+int snpmi_host_free(void* ptr) {
+    return guarded([&] {
+        (void)device();
+        SNPMI_HIP(hipHostFree(ptr));
     });
 }
 int snpmi_dev_free(void* ptr) {

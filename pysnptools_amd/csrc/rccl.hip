@@ -1,6 +1,8 @@
 // RCCL over xGMI for the SNP-sharded GRM: one process per GPU, each rank
 // accumulates the upper-triangle K tiles of its SNP blocks, then one in-place
-// ncclAllReduce(sum) of the tile buffer produces K on every rank.  The unique id is
+// ncclAllReduce(sum) of the tile buffer produces K on every rank.  In the K-partitioned
+// mode (cfg5) each rank uploads 1/p of a packed SNP block and ncclAllGather rebuilds the
+// whole block on every rank (packed codes are 16x smaller than the f32 values).  The unique id is
 // exchanged by the caller (bench.py uses torch.distributed's gloo store for that).
 #include <rccl/rccl.h>
 
@@ -47,6 +49,14 @@ int snpmi_rccl_allreduce_sum(void* buf, uint64_t count, int dtype) {
         ncclDataType_t t = dtype == SNPMI_DT_F64 ? ncclFloat64 : ncclFloat32;
         SNPMI_REQUIRE(dtype == SNPMI_DT_F32 || dtype == SNPMI_DT_F64, SNPMI_E_ARG, "all-reduce dtype must be f32/f64");
         SNPMI_NCCL(ncclAllReduce(buf, buf, count, t, ncclSum, g_comm, stream()));
+    });
+}
+
+int snpmi_rccl_allgather(const void* send, void* recv, uint64_t bytes_per_rank) {
+    return guarded([&] {
+        SNPMI_REQUIRE(g_comm != nullptr, SNPMI_E_ARG, "RCCL communicator not initialised");
+        SNPMI_REQUIRE(send != nullptr && recv != nullptr, SNPMI_E_ARG, "all-gather buffer is NULL");
+        SNPMI_NCCL(ncclAllGather(send, recv, bytes_per_rank, ncclUint8, g_comm, stream()));
     });
 }
 

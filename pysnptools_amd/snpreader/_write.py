@@ -1,8 +1,9 @@
 """BED writer (reference Bed.write -> bed-reader to_bed, bed.py:229-316).
 
-SURVEY.md §8(f) row f2 ("next"): the 2-bit encoder runs vectorised on the host for now;
-it is used to write fixtures, not on the decode/standardize/GRM path.
+SURVEY.md §8(f) row f2: the 2-bit encoder runs on the GPU (csrc/encode.hip, C ABI
+snpmi_bed_write_*); the .fam/.bim text is written here.
 Inverse LUT: count_A1=False 0->00, 1->10, 2->11, missing->01; count_A1=True swaps 0/2.
+Values other than 0, 1, 2 or missing raise ValueError and leave no .bed behind.
 """
 import numpy as np
 
@@ -13,35 +14,25 @@ def _fmt(x):
     return str(int(x)) if float(x).is_integer() else repr(float(x))
 
 
-def encode_codes(val, count_A1=False):
-    """iid x sid values -> SNP-major packed bytes [sid, ceil(iid/4)]."""
+def write_bed_body(filename, val, count_A1):
+    """Genotype half of bed-reader's to_bed: values -> .bed on the GPU (snpmi_bed_write_*)."""
+    from pysnptools_amd import _native as N
+
     val = np.asarray(val)
+    if val.dtype not in (np.float32, np.float64, np.int8):
+        val = val.astype(np.float64)
+    if not (val.flags["C_CONTIGUOUS"] or val.flags["F_CONTIGUOUS"]):
+        val = np.asfortranarray(val)
     n, m = val.shape
-    if val.dtype == np.int8:
-        miss = val == -127
-        v = val.astype(np.int16)
-    else:
-        miss = np.isnan(val)
-        v = np.where(miss, 0, val)
-    ok = miss | (v == 0) | (v == 1) | (v == 2)
-    if not np.all(ok):
-        raise ValueError("Expect values to be 0, 1, 2 or missing")
-    lut = np.array([3, 2, 0], dtype=np.uint8) if count_A1 else np.array([0, 2, 3], dtype=np.uint8)
-    codes = np.where(miss, np.uint8(1), lut[np.clip(v, 0, 2).astype(np.intp)]).astype(np.uint8)  # n x m
-    bpc = (n + 3) // 4
-    padded = np.zeros((bpc * 4, m), dtype=np.uint8)
-    padded[:n] = codes
-    q = padded.reshape(bpc, 4, m)
-    packed = q[:, 0] | (q[:, 1] << 2) | (q[:, 2] << 4) | (q[:, 3] << 6)
-    return np.ascontiguousarray(packed.T)
+    order_c = 1 if val.flags["C_CONTIGUOUS"] and not val.flags["F_CONTIGUOUS"] else 0
+    fn = "snpmi_bed_write_" + {np.dtype(np.float32): "f32", np.dtype(np.float64): "f64",
+                               np.dtype(np.int8): "i8"}[val.dtype]
+    N.call(fn, filename.encode(), N.ptr(val), n, m, order_c, int(bool(count_A1)), 0)
 
 
 def write_bed(filename, snpdata, count_A1, reverse_chrom_map):
     base = filename[:-4] if filename.lower().endswith(".bed") else filename
-    packed = encode_codes(snpdata.val, count_A1)
-    with open(filename, "wb") as f:
-        f.write(bytes([0x6C, 0x1B, 0x01]))
-        f.write(packed.tobytes())
+    write_bed_body(filename, snpdata.val, count_A1)
     with open(base + ".fam", "w") as f:
         for fid, iid in snpdata.iid:
             f.write("{0} {1} 0 0 0 0\n".format(fid, iid))

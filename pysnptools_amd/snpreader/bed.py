@@ -18,14 +18,40 @@ plink_chrom_map = {"X": 23, "Y": 24, "XY": 25, "MT": 26}
 reverse_plink_chrom_map = {23: "X", 24: "Y", 25: "XY", 26: "MT"}
 
 
-def _read_table(path, ncols_expected):
-    """Whitespace-delimited text table -> list of string columns."""
-    import pandas as pd
+def _text_scan(path, min_fields, n_cols, num_threads=None):
+    import ctypes
 
-    if os.path.getsize(path) == 0:
-        return [np.empty(0, dtype=str) for _ in range(ncols_expected)]
-    df = pd.read_csv(path, sep=r"\s+", header=None, dtype=str, keep_default_na=False, engine="c")
-    return [df[c].to_numpy(dtype=str) for c in df.columns]
+    rows = ctypes.c_uint64()
+    widths = np.zeros(max(n_cols, 1), dtype=np.uint64)
+    N.call("snpmi_text_scan", path.encode(), min_fields, n_cols, ctypes.byref(rows), N.ptr(widths),
+           get_num_threads(num_threads))
+    return rows.value, widths
+
+
+def _text_bytes(path, col, rows, width, num_threads=None):
+    """Column ``col`` of a whitespace-delimited file as fixed-width bytes (C parser, f1)."""
+    width = max(int(width), 1)
+    raw = np.empty(rows, dtype="S%d" % width)
+    N.call("snpmi_text_strings", path.encode(), col, rows, width, N.ptr(raw), get_num_threads(num_threads))
+    return raw
+
+
+def _to_str(raw):
+    try:
+        return raw.astype(str)
+    except UnicodeDecodeError:
+        return np.char.decode(raw, "utf-8")
+
+
+def _text_strings(path, col, rows, width, num_threads=None):
+    """Column ``col`` of a whitespace-delimited file as a NumPy str array."""
+    return _to_str(_text_bytes(path, col, rows, width, num_threads))
+
+
+def _text_f64(path, col, rows, num_threads=None):
+    out = np.empty(rows, dtype=np.float64)
+    N.call("snpmi_text_f64", path.encode(), col, rows, N.ptr(out), get_num_threads(num_threads))
+    return out
 
 
 class Bed(SnpReader):
@@ -59,14 +85,16 @@ class Bed(SnpReader):
             if self._original_iid is not None:
                 self._row = np.array(self._original_iid, dtype="str").reshape(-1, 2)
             else:
-                cols = _read_table(self.fam_filename, 6)
-                self._row = np.array([cols[0], cols[1]], dtype="str").T.reshape(-1, 2)
+                rows, w = _text_scan(self.fam_filename, 2, 2, self._num_threads)
+                fid = _text_strings(self.fam_filename, 0, rows, w[0], self._num_threads)
+                iid = _text_strings(self.fam_filename, 1, rows, w[1], self._num_threads)
+                self._row = np.array([fid, iid], dtype="str").T.reshape(-1, 2)
         return self._row
 
-    def _bim(self):
-        if not hasattr(self, "_bim_cols"):
-            self._bim_cols = _read_table(self.bim_filename, 6)
-        return self._bim_cols
+    def _bim_scan(self):
+        if not hasattr(self, "_bim_shape"):
+            self._bim_shape = _text_scan(self.bim_filename, 4, 2, self._num_threads)
+        return self._bim_shape
 
     @property
     def col(self):
@@ -74,7 +102,8 @@ class Bed(SnpReader):
             if self._original_sid is not None:
                 self._col = np.array(self._original_sid, dtype="str")
             else:
-                self._col = np.array(self._bim()[1], dtype="str")
+                rows, w = self._bim_scan()
+                self._col = _text_strings(self.bim_filename, 1, rows, w[1], self._num_threads)
         return self._col
 
     @property
@@ -83,15 +112,21 @@ class Bed(SnpReader):
             if self._original_pos is not None:
                 pos = np.array(self._original_pos, dtype=float).reshape(-1, 3)
             else:
-                bim = self._bim()
-                chrom = np.array(bim[0], dtype=object)
-                for key, value in self.chrom_map.items():
-                    chrom[chrom == key] = value
-                pos = np.array([chrom.astype("float"), bim[2].astype("float"), bim[3].astype("float")]).T
-                pos = pos.reshape(-1, 3)
+                rows, w = self._bim_scan()
+                pos = np.empty((rows, 3), dtype=np.float64)
+                pos[:, 0] = self._chromosomes(_text_bytes(self.bim_filename, 0, rows, w[0], self._num_threads))
+                pos[:, 1] = _text_f64(self.bim_filename, 2, rows, self._num_threads)
+                pos[:, 2] = _text_f64(self.bim_filename, 3, rows, self._num_threads)
             pos[pos == 0] = np.nan  # PLINK's missing chromosome/position
             self._col_property = pos
         return self._col_property
+
+    def _chromosomes(self, chrom):
+        """chrom_map then float(), per distinct value (bed.py:180-186; ValueError for e.g. 'chrBAD')."""
+        uniq, inv = np.unique(chrom, return_inverse=True)
+        names = _to_str(uniq)
+        vals = np.array([float(self.chrom_map.get(u, u)) for u in names], dtype=np.float64)
+        return vals[inv.reshape(-1)] if len(uniq) else np.empty(0)
 
     def _run_once(self):
         if self._ran_once:

@@ -112,26 +112,6 @@ def test_snpkernel_pushdown_rules():
     assert isinstance(k2, SnpKernel) and k2.iid_count == 3  # constant: pushed down (snpkernel.py:98-99)
 
 
-@pytest.mark.parametrize("n_iid", [1, 2, 3, 5, 297, 298, 299, 300])
-def test_writer_round_trip_via_oracle(n_iid):
-    """Bed.write's encoder against the oracle decoder, including N % 4 != 0 padding."""
-    g = np.load(os.path.join(GOLDEN, "n300.npz"))
-    v = g["val_i8"][:n_iid, :40].astype(np.float64)
-    v[g["val_i8"][:n_iid, :40] == -127] = np.nan
-    d = SnpData(iid=[["f", str(i)] for i in range(n_iid)], sid=["s%d" % j for j in range(40)], val=v)
-    with tempfile.TemporaryDirectory() as tmp:
-        for a1 in (False, True):
-            p = os.path.join(tmp, "rt.bed")
-            b = Bed.write(p, d, count_A1=a1)
-            assert b.iid_count == n_iid and b.sid_count == 40
-            back = O.decode(O.read_bed_bytes(p), n_iid, 40, count_A1=a1)
-            assert np.array_equal(back, v, equal_nan=True)
-    with pytest.raises(ValueError):
-        from pysnptools_amd.snpreader._write import encode_codes
-
-        encode_codes(np.array([[0.5]]))
-
-
 def test_bed_reader_compat_surface():
     """The shim exposes every bed_reader name PySnpTools imports, with metadata parsing."""
     import inspect

@@ -444,3 +444,100 @@ def test_grm_partitioned_blocks_assemble_k(n, world):
             K[i:i + 256, j:j + 256] = out[b]
             K[j:j + 256, i:i + 256] = out[b].T
     grm_close(K[:n, :n], ref, 1e-5)
+
+
+# ---------------------------------------------------------------------------------- BED writer (§8f f2)
+def _write_bytes(val, count_A1=False):
+    from pysnptools_amd.snpreader._write import write_bed_body
+
+    with tempfile.TemporaryDirectory() as tmp:
+        p = os.path.join(tmp, "w.bed")
+        write_bed_body(p, val, count_A1)
+        return O.read_bed_bytes(p)
+
+
+@pytest.mark.parametrize("name,n_iid", [("gen1", 190), ("gen4", 198), ("n300", 300)])
+@pytest.mark.parametrize("dtype", [np.float64, np.float32, np.int8])
+@pytest.mark.parametrize("order", ["F", "C"])
+def test_bed_write_reproduces_reference_files(name, n_iid, dtype, order):
+    """The HIP encoder rewrites files the reference itself wrote, byte for byte (pad bits incl.)."""
+    v8 = g("generate")[name + "_val_i8"] if name != "n300" else g("n300")["val_i8"]
+    val = v8 if dtype == np.int8 else from_i8(v8).astype(dtype)
+    val = np.array(val, order=order)
+    assert np.array_equal(_write_bytes(val), body(name))
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 5, 255, 256, 257, 1023, 1024, 1025, 1030, 4099])
+@pytest.mark.parametrize("m", [1, 63, 65, 130])
+def test_bed_write_shapes_vs_oracle(n, m):
+    rng = np.random.default_rng(n * 1000 + m)
+    v = rng.integers(0, 3, size=(n, m)).astype(np.float64)
+    v[rng.random((n, m)) < 0.05] = np.nan
+    for count_A1 in (False, True):
+        exp = O.encode(v, count_A1).reshape(-1)
+        for dtype in (np.float32, np.float64):
+            for order in ("F", "C"):
+                got = _write_bytes(np.array(v, dtype=dtype, order=order), count_A1)
+                assert np.array_equal(got, exp), (dtype, order, count_A1)
+
+
+@pytest.mark.parametrize("bad", [0.5, -1.0, 3.0, np.inf])
+def test_bed_write_rejects_bad_values(bad):
+    v = np.zeros((10, 4))
+    v[7, 2] = bad
+    with tempfile.TemporaryDirectory() as tmp:
+        p = os.path.join(tmp, "bad.bed")
+        from pysnptools_amd.snpreader._write import write_bed_body
+
+        with pytest.raises(ValueError):
+            write_bed_body(p, v, False)
+        assert not os.path.exists(p)
+        v8 = np.zeros((10, 4), dtype=np.int8)
+        v8[3, 1] = 5
+        with pytest.raises(ValueError):
+            write_bed_body(p, v8, False)
+        assert not os.path.exists(p)
+
+
+def test_bed_write_snpdata_round_trip_and_metadata():
+    """Bed.write (bed.py:229-316): .bed by the HIP encoder, .fam/.bim text, read back exactly."""
+    b = bed("n300")
+    d = b[:, ::3].read()
+    with tempfile.TemporaryDirectory() as tmp:
+        for a1 in (False, True):
+            w = Bed.write(os.path.join(tmp, "rt.bed"), d, count_A1=a1)
+            back = w.read()
+            assert np.array_equal(back.val, d.val, equal_nan=True)
+            assert np.array_equal(back.iid, d.iid) and np.array_equal(back.sid, d.sid)
+            np.testing.assert_array_equal(back.pos, d.pos)
+
+
+@pytest.mark.parametrize("order_c", [0, 1])
+def test_dev_encode_large(order_c):
+    """Grid-stride paths of k_encode_f/c at a size with many waves per CU."""
+    n, m = 20011, 700
+    pitch = N.lib().snpmi_packed_pitch(n)
+    rng = np.random.default_rng(7 + order_c)
+    v = rng.integers(0, 3, size=(n, m)).astype(np.float32)
+    v[rng.random((n, m)) < 0.01] = np.nan
+    if order_c:
+        host, ld = np.ascontiguousarray(v), m
+    else:
+        ld = (n + 15) // 16 * 16
+        host = np.zeros((m, ld), dtype=np.float32)
+        host[:, :n] = v.T
+    dv, dp = ctypes.c_void_p(), ctypes.c_void_p()
+    N.call("snpmi_dev_alloc", ctypes.byref(dv), host.nbytes)
+    N.call("snpmi_dev_alloc", ctypes.byref(dp), pitch * m)
+    try:
+        N.call("snpmi_memcpy_h2d", dv, N.ptr(host), host.nbytes)
+        bad = ctypes.c_uint64(99)
+        N.call("snpmi_dev_encode", dv, N.DT_F32, order_c, ld, n, m, 0, dp, pitch, ctypes.byref(bad))
+        out = np.empty((m, pitch), dtype=np.uint8)
+        N.call("snpmi_memcpy_d2h", N.ptr(out), dp, out.nbytes)
+    finally:
+        N.call("snpmi_dev_free", dv)
+        N.call("snpmi_dev_free", dp)
+    assert bad.value == 0
+    bpc = (n + 3) // 4
+    assert np.array_equal(out[:, :bpc], O.encode(v))

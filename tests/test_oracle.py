@@ -24,7 +24,8 @@ def from_i8(v):
 
 
 @pytest.mark.parametrize("name,n_iid,n_sid", [("n300", 300, 1015), ("snpgen", 1000, 5),
-                                               ("dist_x", 100, 100), ("toydata", 500, 10000)])
+                                               ("dist_x", 100, 100), ("toydata", 500, 10000),
+                                               ("gen1", 190, 20), ("gen4", 198, 20)])
 def test_shape_from_fam_bim(name, n_iid, n_sid):
     assert O.bed_shape(os.path.join(DATA, name + ".bed")) == (n_iid, n_sid)
 
@@ -42,6 +43,28 @@ def test_decode_bit_exact(name, dtype, order):
         assert np.array_equal(got, exp)
     else:
         assert np.array_equal(got, from_i8(exp).astype(dtype), equal_nan=True)
+
+
+@pytest.mark.parametrize("name,n_iid", [("gen1", 190), ("gen4", 198)])
+def test_decode_and_encode_writer_files(name, n_iid):
+    """gen1/gen4.bed were written by the reference's Bed.write (util/generate.py:207-240) with
+    N % 4 == 2: decode matches snp_gen's values and the encoder reproduces every byte."""
+    exp = g("generate")[name + "_val_i8"]
+    got = O.decode(body(name), n_iid, 20, dtype=np.int8)
+    assert np.array_equal(got, exp)
+    assert np.array_equal(O.encode(from_i8(exp)).reshape(-1), body(name))
+    assert np.array_equal(O.encode(exp).reshape(-1), body(name))
+
+
+def test_encode_reproduces_n300_file_and_a1_round_trip():
+    v = g("n300")["val_i8"]
+    assert np.array_equal(O.encode(from_i8(v)).reshape(-1), body("n300"))  # NaN -> 01
+    for n in (1, 2, 3, 5, 297):
+        x = from_i8(v[:n, :40])
+        back = O.decode(O.encode(x, count_A1=True).reshape(-1), n, 40, count_A1=True)
+        assert np.array_equal(back, x, equal_nan=True)
+    with pytest.raises(ValueError):
+        O.encode(np.array([[0.5]]))
 
 
 def test_decode_count_a1():

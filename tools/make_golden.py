@@ -160,6 +160,21 @@ def main():
     np.savez_compressed(os.path.join(OUT, "toydata.npz"), K_rows=kfix[:64].copy(), K_diag=np.diag(kfix).copy(),
                         K_rowsum=kfix.sum(1), K00=np.array(kfix[0, 0]))
 
+    # ------------------------------------------------------------------ writer-produced BEDs with N % 4 != 0
+    # util/generate.py:207-240: gen1/gen4.bed were written by the reference (Bed.write of
+    # snp_gen output, count_A1=False); they pin the encoder's bytes incl. the pad bits.
+    from pysnptools.util.generate import snp_gen
+
+    g = {}
+    for name, kw in (("gen1", dict(fst=0, dfr=.5, iid_count=200, sid_count=20, maf_low=.05, seed=5)),
+                     ("gen4", dict(fst=.1, dfr=.01, iid_count=200, sid_count=20, maf_low=.1, seed=5))):
+        copy_triple(REF + "/tests/datasets/generate/" + name, name)
+        sd_gen = snp_gen(**kw)
+        assert np.array_equal(sd_gen.val, decode(REF + "/tests/datasets/generate/%s.bed" % name, sd_gen.iid_count),
+                              equal_nan=True)
+        g[name + "_val_i8"] = to_i8(sd_gen.val)
+    np.savez_compressed(os.path.join(OUT, "generate.npz"), **g)
+
     # ------------------------------------------------------------------ edge matrices (kernelreader/test.py:56-111 style)
     g = {}
     np.random.seed(0)
