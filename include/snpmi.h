@@ -153,6 +153,23 @@ int snpmi_grm_dense_f32(const float* val, uint64_t rows, uint64_t cols, int orde
 int snpmi_grm_dense_f64(const double* val, uint64_t rows, uint64_t cols, int order_c, int std_kind,
                         double a, double b, int use_stats, double* stats, int diag_k_to_n,
                         double* factor, double* K_out);
+/* GRM over several .bed files that share the iids -- DistributedBed / _MergeSIDs pieces,
+ * per-chromosome shards (distributedbed.py:16-207, pstreader/_mergecols.py:117-159, reached
+ * from SnpReader._read_kernel snpreader.py:623-668 on a merged reader).  begin ->
+ * add_bed (any number; stats per file as in snpmi_grm_bed_*) -> end (DiagKtoN + copy-out).
+ * For one process per GPU, add this rank's files, then all-reduce the session tiles
+ * (snpmi_grm_session_tiles + snpmi_rccl_allreduce_sum) before end. */
+int snpmi_grm_begin(uint64_t n_out_iid, int dtype);
+int snpmi_grm_add_bed_f32(const char* path, uint64_t n_iid, uint64_t n_sid, int count_a1,
+                          const uint64_t* iid_idx, uint64_t n_out_iid, const uint64_t* sid_idx,
+                          uint64_t n_out_sid, int std_kind, double a, double b, int use_stats,
+                          float* stats, int num_threads);
+int snpmi_grm_add_bed_f64(const char* path, uint64_t n_iid, uint64_t n_sid, int count_a1,
+                          const uint64_t* iid_idx, uint64_t n_out_iid, const uint64_t* sid_idx,
+                          uint64_t n_out_sid, int std_kind, double a, double b, int use_stats,
+                          double* stats, int num_threads);
+int snpmi_grm_session_tiles(void** tiles, uint64_t* count);   /* device tiles + element count */
+int snpmi_grm_end(int diag_k_to_n, double* factor, void* K_out);
 int snpmi_diag_k_to_n_f32(float* K, uint64_t n, double* factor);
 int snpmi_diag_k_to_n_f64(double* K, uint64_t n, double* factor);
 

@@ -452,28 +452,25 @@ static void grm_finish(Device& d, const T* tiles, uint64_t n, int diag_k_to_n, d
     SNPMI_HIP(hipStreamSynchronize(d.stream));
 }
 
+// Accumulate the SNP columns of one .bed into upper-triangle tiles (first = overwrite).
+// Returns true if anything was written.
 template <typename T>
-static void grm_bed_impl(const char* path, uint64_t n_iid, uint64_t n_sid, int count_a1, const uint64_t* iid_idx,
-                         uint64_t n_out_iid, const uint64_t* sid_idx, uint64_t n_out_sid, int std_kind, double a,
-                         double b, int use_stats, T* stats, int diag_k_to_n, double* factor, T* K_out,
-                         int num_threads) {
-    std::lock_guard<std::recursive_mutex> lk(g_call_mutex);
+static bool grm_add_bed(Device& d, T* tiles, bool first, const char* path, uint64_t n_iid, uint64_t n_sid,
+                        int count_a1, const uint64_t* iid_idx, uint64_t n_out_iid, const uint64_t* sid_idx,
+                        uint64_t n_out_sid, int std_kind, double a, double b, int use_stats, T* stats,
+                        int num_threads) {
     BedMap m;
     open_bed(m, path, n_iid, n_sid);
     const uint64_t n_out = iid_idx ? n_out_iid : n_iid;
     const uint64_t m_out = sid_idx ? n_out_sid : n_sid;
     check_index(iid_idx, n_out, n_iid, "iid");
     check_index(sid_idx, m_out, n_sid, "sid");
-    SNPMI_REQUIRE(K_out != nullptr || n_out == 0, SNPMI_E_ARG, "K_out is NULL");
     SNPMI_REQUIRE(stats != nullptr || std_kind == SNPMI_STD_NONE || m_out == 0, SNPMI_E_ARG, "stats is NULL");
-    Device& d = device();
     const int nthreads = resolve_threads(num_threads);
     const int dt = DT<T>::v;
     IidPlan p = plan_iids(d, iid_idx, n_iid, n_out);
-    const uint64_t tile_bytes = n_tiles_upper(n_out) * kTile * kTile * sizeof(T);
-    T* tiles = (T*)d.get(Device::S_TILES, tile_bytes);
-    if (m_out == 0 || n_out == 0) SNPMI_HIP(hipMemsetAsync(tiles, 0, tile_bytes, d.stream));
     const uint64_t C = chunk_snps(p.pitch_in + p.pitch_out, 1ull << 30);
+    bool wrote = false;
     for (uint64_t c0 = 0; c0 < m_out && n_out > 0; c0 += C) {
         const uint64_t cnt = std::min(C, m_out - c0);
         const uint8_t* packed = stage_chunk(d, m, sid_idx, c0, cnt, p, nthreads);
@@ -483,14 +480,46 @@ static void grm_bed_impl(const char* path, uint64_t n_iid, uint64_t n_sid, int c
             SNPMI_HIP(hipMemcpyAsync(st_dev, stats + 2 * c0, cnt * 2 * sizeof(T), hipMemcpyHostToDevice, d.stream));
         launch_snp_stats(packed, p.pitch_out, n_out, cnt, count_a1, std_kind, a, b, use_stats, dt, st_dev, lut,
                          d.stream);
-        launch_syrk_packed(packed, p.pitch_out, n_out, cnt, lut, dt, tiles, c0 > 0, d.stream);
+        launch_syrk_packed(packed, p.pitch_out, n_out, cnt, lut, dt, tiles, !(first && !wrote), d.stream);
+        wrote = true;
         if (std_kind != SNPMI_STD_NONE && !use_stats)
             SNPMI_HIP(hipMemcpyAsync(stats + 2 * c0, st_dev, cnt * 2 * sizeof(T), hipMemcpyDeviceToHost, d.stream));
     }
     if (n_out == 0 && std_kind != SNPMI_STD_NONE && !use_stats) {
         for (uint64_t j = 0; j < m_out; j++) stats[2 * j] = stats[2 * j + 1] = (T)NAN;
     }
+    SNPMI_HIP(hipStreamSynchronize(d.stream));
+    return wrote;
+}
+
+template <typename T>
+static void grm_bed_impl(const char* path, uint64_t n_iid, uint64_t n_sid, int count_a1, const uint64_t* iid_idx,
+                         uint64_t n_out_iid, const uint64_t* sid_idx, uint64_t n_out_sid, int std_kind, double a,
+                         double b, int use_stats, T* stats, int diag_k_to_n, double* factor, T* K_out,
+                         int num_threads) {
+    std::lock_guard<std::recursive_mutex> lk(g_call_mutex);
+    const uint64_t n_out = iid_idx ? n_out_iid : n_iid;
+    SNPMI_REQUIRE(K_out != nullptr || n_out == 0, SNPMI_E_ARG, "K_out is NULL");
+    Device& d = device();
+    const uint64_t tile_bytes = n_tiles_upper(n_out) * kTile * kTile * sizeof(T);
+    T* tiles = (T*)d.get(Device::S_TILES, tile_bytes);
+    if (!grm_add_bed<T>(d, tiles, true, path, n_iid, n_sid, count_a1, iid_idx, n_out_iid, sid_idx, n_out_sid,
+                        std_kind, a, b, use_stats, stats, num_threads))
+        SNPMI_HIP(hipMemsetAsync(tiles, 0, tile_bytes, d.stream));
     grm_finish(d, tiles, n_out, diag_k_to_n, factor, K_out);
+}
+
+// ---------------------------------------------------------------------- GRM session (several .bed files)
+struct GrmSession {
+    bool active = false;
+    bool wrote = false;
+    uint64_t n = 0;
+    int dtype = SNPMI_DT_F32;
+};
+static GrmSession g_session;
+
+static void* session_tiles(Device& d) {
+    return d.get(Device::S_SESSION, n_tiles_upper(g_session.n) * kTile * kTile * dtype_size(g_session.dtype));
 }
 
 template <typename T>
@@ -673,6 +702,72 @@ int snpmi_dev_encode(const void* val, int dtype, int order_c, uint64_t ld, uint6
             SNPMI_HIP(hipStreamSynchronize(d.stream));
             *bad_values = bad;
         }
+    });
+}
+
+int snpmi_grm_begin(uint64_t n_out_iid, int dtype) {
+    return guarded([&] {
+        std::lock_guard<std::recursive_mutex> lk(g_call_mutex);
+        SNPMI_REQUIRE(dtype == SNPMI_DT_F32 || dtype == SNPMI_DT_F64, SNPMI_E_ARG, "GRM dtype must be f32 or f64");
+        Device& d = device();
+        g_session = GrmSession{true, false, n_out_iid, dtype};
+        (void)session_tiles(d);
+    });
+}
+
+#define SNPMI_GRM_ADD(SUFFIX, T, DTV)                                                                               \
+    int snpmi_grm_add_bed_##SUFFIX(const char* path, uint64_t n_iid, uint64_t n_sid, int count_a1,                 \
+                                   const uint64_t* iid_idx, uint64_t n_out_iid, const uint64_t* sid_idx,            \
+                                   uint64_t n_out_sid, int std_kind, double a, double b, int use_stats, T* stats,   \
+                                   int num_threads) {                                                                \
+        return guarded([&] {                                                                                         \
+            std::lock_guard<std::recursive_mutex> lk(g_call_mutex);                                                  \
+            SNPMI_REQUIRE(g_session.active, SNPMI_E_ARG, "no GRM session (call snpmi_grm_begin)");                  \
+            SNPMI_REQUIRE(g_session.dtype == DTV, SNPMI_E_ARG, "dtype differs from snpmi_grm_begin");               \
+            SNPMI_REQUIRE((iid_idx ? n_out_iid : n_iid) == g_session.n, SNPMI_E_ARG,                                \
+                          "iid count differs from snpmi_grm_begin");                                                 \
+            Device& d = device();                                                                                    \
+            T* tiles = (T*)session_tiles(d);                                                                         \
+            if (grm_add_bed<T>(d, tiles, !g_session.wrote, path, n_iid, n_sid, count_a1, iid_idx, n_out_iid,        \
+                               sid_idx, n_out_sid, std_kind, a, b, use_stats, stats, num_threads))                   \
+                g_session.wrote = true;                                                                              \
+        });                                                                                                          \
+    }
+SNPMI_GRM_ADD(f32, float, SNPMI_DT_F32)
+SNPMI_GRM_ADD(f64, double, SNPMI_DT_F64)
+
+int snpmi_grm_session_tiles(void** tiles, uint64_t* count) {
+    return guarded([&] {
+        std::lock_guard<std::recursive_mutex> lk(g_call_mutex);
+        SNPMI_REQUIRE(g_session.active, SNPMI_E_ARG, "no GRM session (call snpmi_grm_begin)");
+        Device& d = device();
+        void* t = session_tiles(d);
+        const uint64_t cnt = n_tiles_upper(g_session.n) * kTile * kTile;
+        if (!g_session.wrote) {
+            SNPMI_HIP(hipMemsetAsync(t, 0, cnt * dtype_size(g_session.dtype), d.stream));
+            SNPMI_HIP(hipStreamSynchronize(d.stream));
+            g_session.wrote = true;
+        }
+        if (tiles) *tiles = t;
+        if (count) *count = cnt;
+    });
+}
+
+int snpmi_grm_end(int diag_k_to_n, double* factor, void* K_out) {
+    return guarded([&] {
+        std::lock_guard<std::recursive_mutex> lk(g_call_mutex);
+        SNPMI_REQUIRE(g_session.active, SNPMI_E_ARG, "no GRM session (call snpmi_grm_begin)");
+        SNPMI_REQUIRE(K_out != nullptr || g_session.n == 0, SNPMI_E_ARG, "K_out is NULL");
+        Device& d = device();
+        void* t = session_tiles(d);
+        if (!g_session.wrote)
+            SNPMI_HIP(hipMemsetAsync(t, 0, n_tiles_upper(g_session.n) * kTile * kTile * dtype_size(g_session.dtype),
+                                     d.stream));
+        g_session.active = false;
+        if (g_session.dtype == SNPMI_DT_F32)
+            grm_finish(d, (const float*)t, g_session.n, diag_k_to_n, factor, (float*)K_out);
+        else
+            grm_finish(d, (const double*)t, g_session.n, diag_k_to_n, factor, (double*)K_out);
     });
 }
 

@@ -573,6 +573,35 @@ __device__ __forceinline__ void store_packed(double* As, double* Bs, const PRegs
     }
 }
 
+// same, with the select done on the two 32-bit halves by v_bfi_b32 (8 VALU per value)
+__device__ __forceinline__ void store_packed_bfi(double* As, double* Bs, const PRegs& r) {
+    const int t = threadIdx.x;
+    const int op = t >> 7, tt = t & 127;
+    const int k = tt >> 3, d = tt & 7;
+    double* S = op ? Bs : As;
+    uint32_t lo[4], hi[4];
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+        const uint64_t u = (uint64_t)__double_as_longlong(r.l[c]);
+        lo[c] = (uint32_t)u;
+        hi[c] = (uint32_t)(u >> 32);
+    }
+#pragma unroll
+    for (int v = 0; v < 8; v++) {
+        double o[2];
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            const uint32_t sh = 4 * v + 2 * h;
+            const uint32_t m0 = (uint32_t)__builtin_amdgcn_sbfe((int)r.w, sh, 1u);
+            const uint32_t m1 = (uint32_t)__builtin_amdgcn_sbfe((int)r.w, sh + 1u, 1u);
+            const uint32_t a = bfi(m1, bfi(m0, lo[3], lo[2]), bfi(m0, lo[1], lo[0]));
+            const uint32_t b = bfi(m1, bfi(m0, hi[3], hi[2]), bfi(m0, hi[1], hi[0]));
+            o[h] = __longlong_as_double((long long)(((uint64_t)b << 32) | a));
+        }
+        *reinterpret_cast<double2*>(S + k * LDA + 16 * d + 2 * v) = make_double2(o[0], o[1]);
+    }
+}
+
 __device__ __forceinline__ void compute(const double* As, const double* Bs, f64x4 (&acc)[4][4], int wm, int wn,
                                         int lane) {
     const int kr = lane >> 4, c = lane & 15;
@@ -592,7 +621,8 @@ __device__ __forceinline__ void compute(const double* As, const double* Bs, f64x
     }
 }
 
-template <bool PACKED>
+// MODE 0: production; 1: bfi select; 10: compute only (ablation); 11: loader only (ablation)
+template <bool PACKED, int MODE = 0>
 __global__ __launch_bounds__(256, 2) void k_syrk(const void* __restrict__ src, uint64_t ld, uint64_t kdim,
                                                  const double* __restrict__ lut, double* __restrict__ tiles,
                                                  int accumulate) {
@@ -621,15 +651,19 @@ __global__ __launch_bounds__(256, 2) void k_syrk(const void* __restrict__ src, u
     __syncthreads();
     for (uint64_t s = 0; s < nst; s++) {
         const int buf = s & 1;
-        const bool more = s + 1 < nst;
+        const bool more = s + 1 < nst && MODE != 10;
         if (more) {
             if constexpr (PACKED) load_packed((const uint8_t*)src, ld, kdim, (s + 1) * BK, i0, j0, lut, rp);
             else load_dense((const double*)src, ld, kdim, (s + 1) * BK, i0, j0, ra, rb);
         }
-        compute(lds[buf][0], lds[buf][1], acc, wm, wn, lane);
+        if constexpr (MODE != 11) compute(lds[buf][0], lds[buf][1], acc, wm, wn, lane);
         if (more) {
-            if constexpr (PACKED) store_packed(lds[buf ^ 1][0], lds[buf ^ 1][1], rp);
-            else store_dense(lds[buf ^ 1][0], lds[buf ^ 1][1], ra, rb);
+            if constexpr (PACKED) {
+                if constexpr (MODE == 1) store_packed_bfi(lds[buf ^ 1][0], lds[buf ^ 1][1], rp);
+                else store_packed(lds[buf ^ 1][0], lds[buf ^ 1][1], rp);
+            } else {
+                store_dense(lds[buf ^ 1][0], lds[buf ^ 1][1], ra, rb);
+            }
         }
         __syncthreads();
     }
@@ -690,9 +724,16 @@ void launch_syrk_packed(const uint8_t* packed, uint64_t pitch, uint64_t n, uint6
             default: f32k::k_syrk<true, 16, 4><<<(unsigned)nt, 256, 0, st>>>(packed, pitch, m, L, Tt, accumulate);
         }
     }
-    else
-        f64k::k_syrk<true><<<(unsigned)nt, 256, 0, st>>>(packed, pitch, m, (const double*)lut, (double*)tiles,
-                                                          accumulate);
+    else {
+        const double* L = (const double*)lut;
+        double* Tt = (double*)tiles;
+        switch (g_variant_syrk) {
+            case 1: f64k::k_syrk<true, 1><<<(unsigned)nt, 256, 0, st>>>(packed, pitch, m, L, Tt, accumulate); break;
+            case 10: f64k::k_syrk<true, 10><<<(unsigned)nt, 256, 0, st>>>(packed, pitch, m, L, Tt, accumulate); break;
+            case 11: f64k::k_syrk<true, 11><<<(unsigned)nt, 256, 0, st>>>(packed, pitch, m, L, Tt, accumulate); break;
+            default: f64k::k_syrk<true><<<(unsigned)nt, 256, 0, st>>>(packed, pitch, m, L, Tt, accumulate);
+        }
+    }
     SNPMI_HIP(hipGetLastError());
 }
 

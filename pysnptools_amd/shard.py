@@ -26,3 +26,84 @@ def merge_order(n_sid, block_size, world):
     for b, _ in enumerate(snp_blocks(n_sid, block_size)):
         out.append((b % world, b // world))
     return out
+
+
+def rank_pieces(piece_sizes, rank, world):
+    """Piece indices rank ``rank`` of ``world`` owns when a DistributedBed's pieces (SNP shards
+    of unequal size) are spread over GPUs: largest piece first onto the least-loaded rank
+    (ties -> lowest rank), a deterministic plan every rank computes identically."""
+    assert 0 <= rank < world
+    order = sorted(range(len(piece_sizes)), key=lambda k: (-int(piece_sizes[k]), k))
+    load = [0] * world
+    owner = {}
+    for k in order:
+        r = min(range(world), key=lambda q: (load[q], q))
+        owner[k] = r
+        load[r] += int(piece_sizes[k])
+    return sorted(k for k, r in owner.items() if r == rank)
+
+
+def grm_pieces(reader, standardizer, rank, world, dtype="float32", diag_k_to_n=False, num_threads=None):
+    """GRM of a DistributedBed / _MergeSIDs of Beds with one process per GPU.
+
+    Rank ``rank`` streams only its pieces (``rank_pieces``) through the fused
+    decode->standardize->MFMA SYRK into a device-resident K; one RCCL all-reduce of the
+    upper-triangle tiles (``snpmi_rccl_allreduce_sum``) sums the ranks; every rank then
+    extracts the full K (with DiagKtoN if asked).  The per-SNP stats each rank computed are
+    summed the same way (zeros for SNPs a rank did not own).  The RCCL communicator must be
+    initialised (``snpmi_rccl_init``) when world > 1.
+    Returns (K, trained standardizer, DiagKtoN factor or NaN)."""
+    import ctypes
+
+    import numpy as np
+
+    from pysnptools_amd import _native as N
+    from pysnptools_amd.snpreader.snpreader import _add_pieces, _bed_pieces, _resolve, _trained_from
+    from pysnptools_amd.standardizer.standardizer import _std_args
+
+    dtype = np.dtype(dtype)
+    args = _std_args(standardizer)
+    assert args is not None, "grm_pieces supports Unit/Beta/UnitTrained/BetaTrained/Identity"
+    kind, a, b, use_stats, _, _ = args
+    base, rows, cols = _resolve(reader)
+    merged = _bed_pieces(base)
+    assert merged is not None, "grm_pieces needs a DistributedBed or a _MergeSIDs of Beds"
+    sid = reader.sid
+    n = reader.iid_count
+    stats = (np.ascontiguousarray(standardizer.stats_for(sid), dtype=dtype) if use_stats
+             else np.zeros((len(sid), 2), dtype=dtype))
+    mine = set(rank_pieces(merged.col_count_list, rank, world))
+    K = np.empty((n, n), dtype=dtype)
+    factor = np.full(1, np.nan, dtype=np.float64)
+    N.call("snpmi_grm_begin", n, N.dt_code(dtype))
+    try:
+        _add_pieces(merged, rows, cols, n, kind, a, b, use_stats, stats, dtype, num_threads, only=mine)
+        if world > 1:
+            tiles, count = ctypes.c_void_p(), ctypes.c_uint64()
+            N.call("snpmi_grm_session_tiles", ctypes.byref(tiles), ctypes.byref(count))
+            N.call("snpmi_rccl_allreduce_sum", tiles, count.value, N.dt_code(dtype))
+            N.call("snpmi_stream_sync")
+            if kind != N.STD_NONE and not use_stats:
+                stats = _allreduce_host(N, stats)
+    finally:
+        N.call("snpmi_grm_end", int(bool(diag_k_to_n)), factor.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
+               N.ptr(K))
+    return K, _trained_from(standardizer, kind, a, b, sid, stats), float(factor[0])
+
+
+def _allreduce_host(N, arr):
+    """Sum a host array over ranks through a device buffer + RCCL (stats of owned SNPs)."""
+    import ctypes
+
+    import numpy as np
+
+    buf = np.ascontiguousarray(arr, dtype=np.float64)
+    dev = ctypes.c_void_p()
+    N.call("snpmi_dev_alloc", ctypes.byref(dev), buf.nbytes)
+    try:
+        N.call("snpmi_memcpy_h2d", dev, N.ptr(buf), buf.nbytes)
+        N.call("snpmi_rccl_allreduce_sum", dev, buf.size, N.DT_F64)
+        N.call("snpmi_memcpy_d2h", N.ptr(buf), dev, buf.nbytes)
+    finally:
+        N.call("snpmi_dev_free", dev)
+    return buf.astype(arr.dtype)

@@ -9,9 +9,11 @@ import numpy as np
 
 
 def _fmt(x):
+    """.bim number: Python float text ("1.0", "9270273.0"), as in the reference-written
+    tests/datasets/distributed_bed_test1 pieces; NaN -> "0.0" (PLINK missing, bed.py:254)."""
     if x != x:
-        return "0"
-    return str(int(x)) if float(x).is_integer() else repr(float(x))
+        return "0.0"
+    return repr(float(x))
 
 
 def write_bed_body(filename, val, count_A1):

@@ -184,6 +184,47 @@ def _trained_from(standardizer, kind, a, b, sid, stats):
     return stdizer.BetaTrained(standardizer.a, standardizer.b, sid, stats)
 
 
+def _bed_pieces(base):
+    """The _MergeSIDs behind a DistributedBed / _MergeSIDs whose pieces are all Beds, else None."""
+    from pysnptools_amd.snpreader._mergesids import _MergeSIDs
+    from pysnptools_amd.snpreader.bed import Bed
+    from pysnptools_amd.snpreader.distributedbed import DistributedBed
+
+    if isinstance(base, DistributedBed):
+        base._run_once()
+        base = base._merge
+    if isinstance(base, _MergeSIDs) and all(isinstance(r, Bed) for r in base.reader_list):
+        base._run_once()
+        return base
+    return None
+
+
+def _add_pieces(merged, rows, cols, n, kind, a, b, use_stats, stats, dtype, num_threads, only=None):
+    """snpmi_grm_add_bed_* for every piece holding requested SNPs (``only``: piece subset)."""
+    sfx = N.suffix(dtype)
+    col_index = np.arange(merged.col_count) if cols is None else np.asarray(cols)
+    ri = N.index_array(rows)
+    for k, here, rel in merged._pieces(col_index):
+        if only is not None and k not in only:
+            continue
+        piece = merged.reader_list[k]
+        pst = np.ascontiguousarray(stats[here])
+        N.call("snpmi_grm_add_bed_" + sfx, piece.filename.encode(), merged.row_count,
+               int(merged.col_count_list[k]), int(bool(piece.count_A1)), N.ptr(ri), n, N.ptr(N.index_array(rel)),
+               len(rel), kind, a, b, int(use_stats), N.ptr(pst), get_num_threads(num_threads))
+        if not use_stats:
+            stats[here] = pst
+
+
+def _grm_pieces(merged, rows, cols, n, kind, a, b, use_stats, stats, diag_k_to_n, fptr, K, dtype, num_threads):
+    """One GPU session over the pieces: K accumulates in HBM across files (snpmi_grm_begin/add/end)."""
+    N.call("snpmi_grm_begin", n, N.dt_code(dtype))
+    try:
+        _add_pieces(merged, rows, cols, n, kind, a, b, use_stats, stats, dtype, num_threads)
+    finally:
+        N.call("snpmi_grm_end", int(bool(diag_k_to_n)), fptr, N.ptr(K))
+
+
 def _native_grm(reader, standardizer, dtype, num_threads, diag_k_to_n):
     """Fused GPU GRM for Bed / SnpData sources; None when not applicable."""
     from pysnptools_amd.snpreader.bed import Bed
@@ -206,7 +247,10 @@ def _native_grm(reader, standardizer, dtype, num_threads, diag_k_to_n):
     factor = np.full(1, np.nan, dtype=np.float64)
     fptr = factor.ctypes.data_as(N.ctypes.POINTER(N.ctypes.c_double))
     sfx = N.suffix(dtype)
-    if isinstance(base, Bed):
+    merged = _bed_pieces(base)
+    if merged is not None:
+        _grm_pieces(merged, rows, cols, n, kind, a, b, use_stats, stats, diag_k_to_n, fptr, K, dtype, num_threads)
+    elif isinstance(base, Bed):
         base._run_once()
         ri, ci = N.index_array(rows), N.index_array(cols)
         N.call("snpmi_grm_bed_" + sfx, base.filename.encode(), base.iid_count, base.sid_count, int(bool(base.count_A1)),

@@ -76,3 +76,103 @@ def sub_matrix(val, row_index_list, col_index_list, order="A", dtype=np.float64,
     if out.dtype != dtype:
         out = out.astype(dtype, order=eff)
     return out
+
+
+# ---------------------------------------------------------------------- iid intersection (util/__init__.py:18-265)
+def _all_same(iids_list):
+    for a, b in zip(iids_list[:-1], iids_list[1:]):
+        if not np.array_equal(a, b):
+            return False
+    return True
+
+
+def intersect_ids(idslist):
+    """(deprecated in the reference) N x L int array: for each iid present in every non-None
+    list, its index in each list (-1 for None lists); rows ordered by the first non-None
+    list's index, then sorted on column 0 as the reference does (util/__init__.py:221-265).
+    A repeated id takes the index of its last occurrence."""
+    L = len(idslist)
+    observed = np.array([ids is not None for ids in idslist], dtype=bool)
+    order = []
+    index = {}
+    first = True
+    for k, ids in enumerate(idslist):
+        if ids is None:
+            continue
+        ids = np.asarray(ids)
+        keys = list(zip(ids[:, 0].tolist(), ids[:, 1].tolist()))
+        if first:
+            first = False
+            for i, key in enumerate(keys):
+                if key not in index:
+                    order.append(key)
+                entry = np.full(L, np.nan)
+                entry[k] = i
+                index[key] = entry
+        else:
+            for i, key in enumerate(keys):
+                e = index.get(key)
+                if e is not None:
+                    e[k] = i
+    indarr = np.array([index[key] for key in order], dtype=float).reshape(len(order), L)
+    indarr[:, ~observed] = -1
+    indarr = indarr[~np.isnan(indarr).any(1)]
+    indarr = np.array(indarr, dtype=int)
+    return indarr[indarr[:, 0].argsort()]
+
+
+def _reindex_snpkernel(snpkernel, iididx, is_test=False):
+    """Intersect BEFORE standardizing: the SNP reader is iid-subset, so the GRM decodes only
+    those iids (the iid-gather path of snpmi_grm_bed_*, k_repack)."""
+    from pysnptools_amd.kernelreader import SnpKernel
+
+    assert not is_test, "test kernels (iid1 != iid0) are not on the GRM path"
+    return SnpKernel(snpkernel.snpreader[iididx, :], snpkernel.standardizer, block_size=snpkernel.block_size)
+
+
+def _reindex_phen_dict(phen_dict, iididx):
+    vals = phen_dict["vals"]
+    phen_dict["vals"] = vals[iididx] if vals.ndim == 1 else vals[iididx, :]
+    phen_dict["iid"] = phen_dict["iid"][iididx]
+    return phen_dict
+
+
+def intersect_apply(data_list, sort_by_dataset=True, intersect_before_standardize=True, is_test=False):
+    """Restrict every dataset to the iids they all share, in one consistent order
+    (util/__init__.py:18-173).  Accepts None, SnpReader, KernelReader (SnpKernel: subset
+    before standardization when ``intersect_before_standardize``), phenotype dicts
+    {'iid','vals'} and (val, iid) tuples; returns the list unchanged if the iids already agree."""
+    from pysnptools_amd.kernelreader import SnpKernel
+
+    iid_list, reindex_list = [], []
+    for data in data_list:
+        if data is None:
+            iid, reindex = None, (lambda data, idx: None)
+        elif intersect_before_standardize and isinstance(data, SnpKernel):
+            iid = data.iid1 if is_test else data.iid0
+            reindex = (lambda data, idx, t=is_test: _reindex_snpkernel(data, idx, t))
+        elif isinstance(data, dict):
+            iid, reindex = data["iid"], _reindex_phen_dict
+        elif isinstance(data, tuple):
+            iid = data[1]
+            reindex = (lambda data, idx: (data[0][idx], data[1][idx]))
+        elif hasattr(data, "iid1") and is_test:
+            iid, reindex = data.iid1, (lambda data, idx: data[:, idx])
+        else:
+            iid = data.iid
+            square = hasattr(data, "col") and iid is data.col
+            reindex = (lambda data, idx: data[idx]) if square else (lambda data, idx: data[idx, :])
+        iid_list.append(iid)
+        reindex_list.append(reindex)
+    if len(iid_list) == 0:
+        raise Exception("Expect a least one input item")
+    if _all_same(iid_list):
+        return data_list
+    indarr = intersect_ids(iid_list)
+    assert indarr.shape[0] > 0, "no individuals remain after intersection, check that ids match in files"
+    if sort_by_dataset:
+        for k, iid in enumerate(iid_list):
+            if iid is not None:
+                indarr = indarr[np.argsort(indarr[:, k])]
+                break
+    return [reindex_list[k](data_list[k], indarr[:, k]) for k in range(indarr.shape[1])]

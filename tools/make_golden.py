@@ -155,6 +155,7 @@ def main():
     t10 = np.load(REF + "/pysnptools/examples/toydata10.snp.npz", allow_pickle=False)["val"]
     assert np.array_equal(tv[:, :10], t10, equal_nan=True)
     kfix = np.load(REF + "/pysnptools/examples/toydata.kernel.npz", allow_pickle=False)["val"]
+    shutil.copyfile(REF + "/pysnptools/examples/toydata.kernel.npz", os.path.join(DATA, "toydata.kernel.npz"))
     kref = sd(np.array(tv, order="F")).read_kernel(Unit(), block_size=1000, force_python_only=True).val
     assert np.abs(kref - kfix).max() < 1e-9
     np.savez_compressed(os.path.join(OUT, "toydata.npz"), K_rows=kfix[:64].copy(), K_diag=np.diag(kfix).copy(),
@@ -174,6 +175,35 @@ def main():
                               equal_nan=True)
         g[name + "_val_i8"] = to_i8(sd_gen.val)
     np.savez_compressed(os.path.join(OUT, "generate.npz"), **g)
+
+    # intersect_apply (util/__init__.py:18-173) on the reference's doctest inputs
+    from pysnptools.snpreader import Pheno
+    from pysnptools.util import intersect_apply, intersect_ids
+
+    bed_iid = np.loadtxt(REF + "/tests/datasets/all_chr.maf0.001.N300.fam", dtype=str, usecols=(0, 1))
+    pheno = Pheno(REF + "/tests/datasets/phenSynthFrom22.23.N300.randcidorder.txt", missing="").read()
+    cov = Pheno(REF + "/tests/datasets/all_chr.maf0.001.covariates.N300.txt", missing="").read()
+    rng = np.random.RandomState(1)
+    drop = np.sort(rng.choice(300, 40, replace=False))
+    sub_iid = np.delete(bed_iid, drop, axis=0)[::-1]
+    g = {"bed_iid": bed_iid.astype("S"), "pheno_iid": pheno.iid.astype("S"), "pheno_val": pheno.val,
+         "cov_iid": cov.iid.astype("S"), "cov_val": cov.val, "sub_iid": sub_iid.astype("S")}
+    for tag, lists in (("a", [None, bed_iid, pheno.iid, cov.iid]), ("b", [sub_iid, bed_iid, pheno.iid]),
+                       ("c", [pheno.iid, None, sub_iid])):
+        g["ind_" + tag] = intersect_ids(lists)
+        for sort in (True, False):
+            outs = intersect_apply([None if x is None else (np.arange(len(x)), x) for x in lists],
+                                   sort_by_dataset=sort)
+            g["out_%s_%d" % (tag, sort)] = np.array([o[0] for o in outs if o is not None])
+    np.savez_compressed(os.path.join(OUT, "intersect.npz"), **g)
+
+    # DistributedBed written by the reference (distributedbed.py:285-300): 44 count_A1=True pieces
+    dst = os.path.join(DATA, "distributed_bed_test1")
+    if os.path.exists(dst):
+        shutil.rmtree(dst)
+    shutil.copytree(REF + "/tests/datasets/distributed_bed_test1", dst)
+    for f in os.listdir(dst):
+        os.chmod(os.path.join(dst, f), 0o644)
 
     # ------------------------------------------------------------------ edge matrices (kernelreader/test.py:56-111 style)
     g = {}
