@@ -574,6 +574,10 @@ __device__ __forceinline__ void store_packed(double* As, double* Bs, const PRegs
 }
 
 // same, with the select done on the two 32-bit halves by v_bfi_b32 (8 VALU per value)
+// ROT: write chunk (v + (d>>1) + 4(k&1)) & 7 at step v so that each 16-lane quarter of the
+// wave hits 16 distinct 4-bank groups (row stride 288 dwords = 32 mod 64 banks; without
+// the rotation all 64 lanes of a ds_write_b128 land on 2 groups).
+template <int V0 = 0, int V1 = 8, bool ROT = false>
 __device__ __forceinline__ void store_packed_bfi(double* As, double* Bs, const PRegs& r) {
     const int t = threadIdx.x;
     const int op = t >> 7, tt = t & 127;
@@ -586,8 +590,10 @@ __device__ __forceinline__ void store_packed_bfi(double* As, double* Bs, const P
         lo[c] = (uint32_t)u;
         hi[c] = (uint32_t)(u >> 32);
     }
+    const int rot = ROT ? (d >> 1) + 4 * (k & 1) : 0;
 #pragma unroll
-    for (int v = 0; v < 8; v++) {
+    for (int v0 = V0; v0 < V1; v0++) {
+        const int v = (v0 + rot) & 7;
         double o[2];
 #pragma unroll
         for (int h = 0; h < 2; h++) {
@@ -621,7 +627,36 @@ __device__ __forceinline__ void compute(const double* As, const double* Bs, f64x
     }
 }
 
-// MODE 0: production; 1: bfi select; 10: compute only (ablation); 11: loader only (ablation)
+// compute() with the next stage's LDS store (bfi select) spread between its MFMA groups, so
+// the select VALU issues while the wave's own MFMAs are in flight instead of after them.
+template <bool ROT = false>
+__device__ __forceinline__ void compute_store(const double* As, const double* Bs, f64x4 (&acc)[4][4], int wm, int wn,
+                                              int lane, double* Ns, double* Nb, const PRegs& r, bool more) {
+    const int kr = lane >> 4, c = lane & 15;
+#pragma unroll
+    for (int kk = 0; kk < BK / 4; kk++) {
+        const int row = (4 * kk + kr) * LDA;
+        double a[4], b[4];
+#pragma unroll
+        for (int x = 0; x < 4; x++) {
+            a[x] = As[row + wm * 64 + 16 * x + c];
+            b[x] = Bs[row + wn * 64 + 16 * x + c];
+        }
+#pragma unroll
+        for (int x = 0; x < 4; x++)
+#pragma unroll
+            for (int y = 0; y < 4; y++) acc[x][y] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[x], b[y], acc[x][y], 0, 0, 0);
+        if (more) {
+            if (kk == 0) store_packed_bfi<0, 2, ROT>(Ns, Nb, r);
+            if (kk == 1) store_packed_bfi<2, 4, ROT>(Ns, Nb, r);
+            if (kk == 2) store_packed_bfi<4, 6, ROT>(Ns, Nb, r);
+            if (kk == 3) store_packed_bfi<6, 8, ROT>(Ns, Nb, r);
+        }
+    }
+}
+
+// MODE 0: production; 1: bfi select; 2: bfi select interleaved with the MFMAs;
+// 10: compute only (ablation); 11: loader only (ablation)
 template <bool PACKED, int MODE = 0>
 __global__ __launch_bounds__(256, 2) void k_syrk(const void* __restrict__ src, uint64_t ld, uint64_t kdim,
                                                  const double* __restrict__ lut, double* __restrict__ tiles,
@@ -644,6 +679,8 @@ __global__ __launch_bounds__(256, 2) void k_syrk(const void* __restrict__ src, u
     if constexpr (PACKED) {
         load_packed((const uint8_t*)src, ld, kdim, 0, i0, j0, lut, rp);
         store_packed(lds[0][0], lds[0][1], rp);
+        if constexpr (MODE == 3)
+            if (nst > 1) load_packed((const uint8_t*)src, ld, kdim, BK, i0, j0, lut, rp);
     } else {
         load_dense((const double*)src, ld, kdim, 0, i0, j0, ra, rb);
         store_dense(lds[0][0], lds[0][1], ra, rb);
@@ -651,10 +688,26 @@ __global__ __launch_bounds__(256, 2) void k_syrk(const void* __restrict__ src, u
     __syncthreads();
     for (uint64_t s = 0; s < nst; s++) {
         const int buf = s & 1;
-        const bool more = s + 1 < nst && MODE != 10;
+        const bool more = s + 1 < nst && MODE != 10 && MODE != 3;
         if (more) {
             if constexpr (PACKED) load_packed((const uint8_t*)src, ld, kdim, (s + 1) * BK, i0, j0, lut, rp);
             else load_dense((const double*)src, ld, kdim, (s + 1) * BK, i0, j0, ra, rb);
+        }
+        if constexpr ((MODE == 2 || MODE == 4) && PACKED) {
+            compute_store<MODE == 4>(lds[buf][0], lds[buf][1], acc, wm, wn, lane, lds[buf ^ 1][0], lds[buf ^ 1][1], rp,
+                                     more);
+            __syncthreads();
+            continue;
+        }
+        if constexpr (MODE == 3 && PACKED) {
+            // prefetch distance 2: rp holds stage s+1 (loaded one stage ago), rq gets stage s+2
+            PRegs rq;
+            if (s + 2 < nst) load_packed((const uint8_t*)src, ld, kdim, (s + 2) * BK, i0, j0, lut, rq);
+            compute_store(lds[buf][0], lds[buf][1], acc, wm, wn, lane, lds[buf ^ 1][0], lds[buf ^ 1][1], rp,
+                          s + 1 < nst);
+            rp = rq;
+            __syncthreads();
+            continue;
         }
         if constexpr (MODE != 11) compute(lds[buf][0], lds[buf][1], acc, wm, wn, lane);
         if (more) {
@@ -727,11 +780,17 @@ void launch_syrk_packed(const uint8_t* packed, uint64_t pitch, uint64_t n, uint6
     else {
         const double* L = (const double*)lut;
         double* Tt = (double*)tiles;
+        // tools/ubench.py syrk --dtype f64 (N=32768, 8192 SNPs): 5 = plain loader 51.3 TFLOP/s,
+        // 2 = select interleaved with the MFMAs 56.1, 0 = that + bank-rotated LDS stores 60.5
+        // (77% of 78.6); 10 = MFMA-only ablation 71.5.
         switch (g_variant_syrk) {
             case 1: f64k::k_syrk<true, 1><<<(unsigned)nt, 256, 0, st>>>(packed, pitch, m, L, Tt, accumulate); break;
+            case 2: f64k::k_syrk<true, 2><<<(unsigned)nt, 256, 0, st>>>(packed, pitch, m, L, Tt, accumulate); break;
+            case 3: f64k::k_syrk<true, 3><<<(unsigned)nt, 256, 0, st>>>(packed, pitch, m, L, Tt, accumulate); break;
+            case 5: f64k::k_syrk<true, 0><<<(unsigned)nt, 256, 0, st>>>(packed, pitch, m, L, Tt, accumulate); break;
             case 10: f64k::k_syrk<true, 10><<<(unsigned)nt, 256, 0, st>>>(packed, pitch, m, L, Tt, accumulate); break;
             case 11: f64k::k_syrk<true, 11><<<(unsigned)nt, 256, 0, st>>>(packed, pitch, m, L, Tt, accumulate); break;
-            default: f64k::k_syrk<true><<<(unsigned)nt, 256, 0, st>>>(packed, pitch, m, L, Tt, accumulate);
+            default: f64k::k_syrk<true, 4><<<(unsigned)nt, 256, 0, st>>>(packed, pitch, m, L, Tt, accumulate);
         }
     }
     SNPMI_HIP(hipGetLastError());

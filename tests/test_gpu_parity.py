@@ -323,8 +323,9 @@ def test_kerneldata_diag_k_to_n():
 
 @pytest.fixture(params=[0, 4, 5], ids=["auto", "syrk256", "syrk128"])
 def syrk_variant(request):
-    """Run a test under each f32 SYRK kernel (0 = size-based choice, 4 = 256x256 tiles,
-    5 = 128x128 tiles); restores the default afterwards."""
+    """Run a test under each SYRK kernel -- f32: 0 = size-based choice, 4 = 256x256 tiles,
+    5 = 128x128 tiles; f64: 0/4 = interleaved bank-rotated loader, 5 = plain loader --
+    and restore the default afterwards."""
     N.call("snpmi_set_kernel_variant", b"syrk", request.param)
     yield request.param
     N.call("snpmi_set_kernel_variant", b"syrk", 0)
