@@ -56,6 +56,7 @@ Device& device() {
         d = new Device();
         d->id = g_cur_dev;
         SNPMI_HIP(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
+        for (auto& e : d->staged) SNPMI_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         hipDeviceProp_t p;
         SNPMI_HIP(hipGetDeviceProperties(&p, g_cur_dev));
         d->cu_count = p.multiProcessorCount;
@@ -92,8 +93,9 @@ void Device::release() {
 
 // pinned staging (two slots so a chunk can be gathered while the previous one uploads)
 static std::mutex g_pin_mutex;
-static void* g_pin[4] = {};
-static size_t g_pin_cap[4] = {};
+constexpr int kPinSlots = 6;  // 0/1: H2D staging, 2: stats, 3: unused, 4/5: D2H bounce
+static void* g_pin[kPinSlots] = {};
+static size_t g_pin_cap[kPinSlots] = {};
 
 void* pinned(int slot, size_t bytes) {
     std::lock_guard<std::mutex> lk(g_pin_mutex);
@@ -113,7 +115,7 @@ void* pinned(int slot, size_t bytes) {
 
 void release_pinned() {
     std::lock_guard<std::mutex> lk(g_pin_mutex);
-    for (int s = 0; s < 4; s++) {
+    for (int s = 0; s < kPinSlots; s++) {
         if (g_pin[s]) (void)hipHostFree(g_pin[s]);
         g_pin[s] = nullptr;
         g_pin_cap[s] = 0;
@@ -131,10 +133,10 @@ static int resolve_threads(int num_threads) {
 }
 
 template <class F>
-static void parallel_for(uint64_t n, int nthreads, F&& fn) {
+static void parallel_for(uint64_t n, int nthreads, F&& fn, uint64_t grain = 64) {
     if (n == 0) return;
     nthreads = (int)std::min<uint64_t>((uint64_t)nthreads, n);
-    if (nthreads <= 1 || n < 64) {
+    if (nthreads <= 1 || n < grain) {
         for (uint64_t i = 0; i < n; i++) fn(i);
         return;
     }
@@ -144,13 +146,63 @@ static void parallel_for(uint64_t n, int nthreads, F&& fn) {
     for (int t = 0; t < nthreads; t++)
         th.emplace_back([&] {
             for (;;) {
-                uint64_t s = next.fetch_add(64);
+                uint64_t s = next.fetch_add(grain);
                 if (s >= n) break;
-                uint64_t e = std::min(n, s + 64);
+                uint64_t e = std::min(n, s + grain);
                 for (uint64_t i = s; i < e; i++) fn(i);
             }
         });
     for (auto& t : th) t.join();
+}
+
+// Device -> pageable host copy of `rows` rows of `width` bytes (device pitch spitch, host
+// pitch dpitch).  A plain hipMemcpy to pageable memory runs at ~16 GB/s (the runtime's own
+// bounce + a single-threaded copy); here 256 MiB pieces DMA into two pinned bounce buffers
+// while host threads copy the previous piece out, so PCIe and the host copy overlap.
+static void d2h_rows(Device& d, void* dst, size_t dpitch, const void* src, size_t spitch, size_t width, size_t rows,
+                     int nthreads) {
+    if (rows == 0 || width == 0) return;
+    const size_t total = width * rows;
+    if (total < (32u << 20)) {
+        SNPMI_HIP(hipMemcpy2DAsync(dst, dpitch, src, spitch, width, rows, hipMemcpyDeviceToHost, d.stream));
+        SNPMI_HIP(hipStreamSynchronize(d.stream));
+        return;
+    }
+    const size_t per = std::max<size_t>(1, (256u << 20) / width);
+    uint8_t* bounce[2] = {(uint8_t*)pinned(4, per * width), (uint8_t*)pinned(5, per * width)};
+    hipEvent_t* ev = d.staged;  // reuse: no H2D staging is in flight here (callers sync first)
+    auto drain = [&](size_t r0, size_t nr, int slot) {
+        SNPMI_HIP(hipEventSynchronize(ev[slot]));
+        const uint8_t* b = bounce[slot];
+        uint8_t* o = (uint8_t*)dst + r0 * dpitch;
+        if (dpitch == width) {
+            const size_t bytes = nr * width, per_t = round_up(ceil_div(bytes, (size_t)nthreads), 4096);
+            parallel_for(
+                ceil_div(bytes, per_t), nthreads,
+                [&](uint64_t q) {
+                    const size_t a = q * per_t, e = std::min(bytes, a + per_t);
+                    std::memcpy(o + a, b + a, e - a);
+                },
+                1);
+        } else {
+            parallel_for(
+                nr, nthreads, [&](uint64_t r) { std::memcpy(o + r * dpitch, b + r * width, width); },
+                std::max<uint64_t>(1, (1u << 20) / width));
+        }
+    };
+    size_t prev_r0 = 0, prev_n = 0;
+    int i = 0;
+    for (size_t r0 = 0; r0 < rows; r0 += per, i++) {
+        const size_t nr = std::min(per, rows - r0);
+        const int slot = i & 1;
+        SNPMI_HIP(hipMemcpy2DAsync(bounce[slot], width, (const uint8_t*)src + r0 * spitch, spitch, width, nr,
+                                   hipMemcpyDeviceToHost, d.stream));
+        SNPMI_HIP(hipEventRecord(ev[slot], d.stream));
+        if (i > 0) drain(prev_r0, prev_n, slot ^ 1);
+        prev_r0 = r0;
+        prev_n = nr;
+    }
+    drain(prev_r0, prev_n, (i - 1) & 1);
 }
 
 struct BedMap {
@@ -236,13 +288,17 @@ static IidPlan plan_iids(Device& d, const uint64_t* iid_idx, uint64_t n_iid, uin
 }
 
 // Upload SNP chunk [c0, c0+cnt) and return the device packed buffer for the selected iids.
+// Chunks alternate between two pinned host buffers and two device buffers (slot = chunk
+// parity), so the host gathers chunk c+1 from the mmap while the GPU still computes on
+// chunk c: the only wait is for the H2D that last read this pinned slot (two chunks ago).
 static const uint8_t* stage_chunk(Device& d, const BedMap& m, const uint64_t* sid_idx, uint64_t c0, uint64_t cnt,
-                                  const IidPlan& p, int nthreads) {
-    uint8_t* host = (uint8_t*)pinned(0, cnt * p.pitch_in);
-    SNPMI_HIP(hipStreamSynchronize(d.stream));  // previous chunk's upload has consumed `host`
+                                  const IidPlan& p, int nthreads, int slot) {
+    SNPMI_HIP(hipEventSynchronize(d.staged[slot]));
+    uint8_t* host = (uint8_t*)pinned(slot, cnt * p.pitch_in);
     gather_columns(m, sid_idx, c0, cnt, p.pitch_in, host, nthreads);
-    uint8_t* dev = (uint8_t*)d.get(Device::S_PACKED, cnt * p.pitch_in);
+    uint8_t* dev = (uint8_t*)d.get(slot ? Device::S_PACKED_B : Device::S_PACKED, cnt * p.pitch_in);
     SNPMI_HIP(hipMemcpyAsync(dev, host, cnt * p.pitch_in, hipMemcpyHostToDevice, d.stream));
+    SNPMI_HIP(hipEventRecord(d.staged[slot], d.stream));
     if (!p.repack) return dev;
     uint8_t* dev2 = (uint8_t*)d.get(Device::S_PACKED2, cnt * p.pitch_out);
     launch_repack(dev, p.pitch_in, p.n_in, p.idx_dev, p.n_out, cnt, dev2, p.pitch_out, nullptr, d.stream);
@@ -289,9 +345,9 @@ static void bed_read_impl(const char* path, uint64_t n_iid, uint64_t n_sid, int 
     const int dt = DT<T>::v;
     const uint64_t ldF = round_up(std::max<uint64_t>(n_out, 1), 16);
     const uint64_t C = chunk_snps(p.pitch_in + p.pitch_out + ldF * sizeof(T));
-    for (uint64_t c0 = 0; c0 < m_out; c0 += C) {
+    for (uint64_t c0 = 0, ci = 0; c0 < m_out; c0 += C, ci++) {
         const uint64_t cnt = std::min(C, m_out - c0);
-        const uint8_t* packed = stage_chunk(d, m, sid_idx, c0, cnt, p, nthreads);
+        const uint8_t* packed = stage_chunk(d, m, sid_idx, c0, cnt, p, nthreads, (int)(ci & 1));
         T* lut = (T*)d.get(Device::S_LUT, cnt * 4 * sizeof(T));
         T* st_dev = (T*)d.get(Device::S_STATS, cnt * 2 * sizeof(T));
         if (std_kind != SNPMI_STD_NONE && use_stats)
@@ -302,13 +358,12 @@ static void bed_read_impl(const char* path, uint64_t n_iid, uint64_t n_sid, int 
             if (!order_c) {
                 T* dev_out = (T*)d.get(Device::S_OUT, cnt * ldF * sizeof(T));
                 launch_decode(packed, p.pitch_out, n_out, cnt, lut, dt, 0, dev_out, ldF, d.stream);
-                SNPMI_HIP(hipMemcpy2DAsync(out + c0 * n_out, n_out * sizeof(T), dev_out, ldF * sizeof(T),
-                                           n_out * sizeof(T), cnt, hipMemcpyDeviceToHost, d.stream));
+                d2h_rows(d, out + c0 * n_out, n_out * sizeof(T), dev_out, ldF * sizeof(T), n_out * sizeof(T), cnt,
+                         nthreads);
             } else {
                 T* dev_out = (T*)d.get(Device::S_OUT, cnt * n_out * sizeof(T));
                 launch_decode(packed, p.pitch_out, n_out, cnt, lut, dt, 1, dev_out, cnt, d.stream);
-                SNPMI_HIP(hipMemcpy2DAsync(out + c0, m_out * sizeof(T), dev_out, cnt * sizeof(T), cnt * sizeof(T),
-                                           n_out, hipMemcpyDeviceToHost, d.stream));
+                d2h_rows(d, out + c0, m_out * sizeof(T), dev_out, cnt * sizeof(T), cnt * sizeof(T), n_out, nthreads);
             }
         }
         if (std_kind != SNPMI_STD_NONE && !use_stats)
@@ -447,7 +502,7 @@ static void grm_finish(Device& d, const T* tiles, uint64_t n, int diag_k_to_n, d
         SNPMI_HIP(hipStreamSynchronize(d.stream));  // ri reused across blocks
         SNPMI_HIP(hipMemcpyAsync(dri, ri.data(), nr * 8, hipMemcpyHostToDevice, d.stream));
         launch_grm_extract(tiles, n, DT<T>::v, dri, nr, nullptr, n, 1, scale, dk, d.stream);
-        SNPMI_HIP(hipMemcpyAsync(K_out + r0 * n, dk, nr * n * sizeof(T), hipMemcpyDeviceToHost, d.stream));
+        d2h_rows(d, K_out + r0 * n, n * sizeof(T), dk, n * sizeof(T), n * sizeof(T), nr, resolve_threads(0));
     }
     SNPMI_HIP(hipStreamSynchronize(d.stream));
 }
@@ -469,26 +524,32 @@ static bool grm_add_bed(Device& d, T* tiles, bool first, const char* path, uint6
     const int nthreads = resolve_threads(num_threads);
     const int dt = DT<T>::v;
     IidPlan p = plan_iids(d, iid_idx, n_iid, n_out);
-    const uint64_t C = chunk_snps(p.pitch_in + p.pitch_out, 1ull << 30);
+    // ~0.5 GiB of packed codes per chunk keeps >= 2 chunks in flight for cfg4-sized inputs
+    const uint64_t C = chunk_snps(p.pitch_in + p.pitch_out, 1ull << 29);
+    const bool has_stats = std_kind != SNPMI_STD_NONE && m_out > 0 && n_out > 0;
+    // stats go through pinned memory so the D2H/H2D copies stay asynchronous
+    T* st_host = has_stats ? (T*)pinned(2, m_out * 2 * sizeof(T)) : nullptr;
+    if (has_stats && use_stats) std::memcpy(st_host, stats, m_out * 2 * sizeof(T));
     bool wrote = false;
-    for (uint64_t c0 = 0; c0 < m_out && n_out > 0; c0 += C) {
+    for (uint64_t c0 = 0, ci = 0; c0 < m_out && n_out > 0; c0 += C, ci++) {
         const uint64_t cnt = std::min(C, m_out - c0);
-        const uint8_t* packed = stage_chunk(d, m, sid_idx, c0, cnt, p, nthreads);
+        const uint8_t* packed = stage_chunk(d, m, sid_idx, c0, cnt, p, nthreads, (int)(ci & 1));
         T* lut = (T*)d.get(Device::S_LUT, cnt * 4 * sizeof(T));
         T* st_dev = (T*)d.get(Device::S_STATS, cnt * 2 * sizeof(T));
-        if (std_kind != SNPMI_STD_NONE && use_stats)
-            SNPMI_HIP(hipMemcpyAsync(st_dev, stats + 2 * c0, cnt * 2 * sizeof(T), hipMemcpyHostToDevice, d.stream));
+        if (has_stats && use_stats)
+            SNPMI_HIP(hipMemcpyAsync(st_dev, st_host + 2 * c0, cnt * 2 * sizeof(T), hipMemcpyHostToDevice, d.stream));
         launch_snp_stats(packed, p.pitch_out, n_out, cnt, count_a1, std_kind, a, b, use_stats, dt, st_dev, lut,
                          d.stream);
         launch_syrk_packed(packed, p.pitch_out, n_out, cnt, lut, dt, tiles, !(first && !wrote), d.stream);
         wrote = true;
-        if (std_kind != SNPMI_STD_NONE && !use_stats)
-            SNPMI_HIP(hipMemcpyAsync(stats + 2 * c0, st_dev, cnt * 2 * sizeof(T), hipMemcpyDeviceToHost, d.stream));
+        if (has_stats && !use_stats)
+            SNPMI_HIP(hipMemcpyAsync(st_host + 2 * c0, st_dev, cnt * 2 * sizeof(T), hipMemcpyDeviceToHost, d.stream));
     }
+    SNPMI_HIP(hipStreamSynchronize(d.stream));
+    if (has_stats && !use_stats) std::memcpy(stats, st_host, m_out * 2 * sizeof(T));
     if (n_out == 0 && std_kind != SNPMI_STD_NONE && !use_stats) {
         for (uint64_t j = 0; j < m_out; j++) stats[2 * j] = stats[2 * j + 1] = (T)NAN;
     }
-    SNPMI_HIP(hipStreamSynchronize(d.stream));
     return wrote;
 }
 

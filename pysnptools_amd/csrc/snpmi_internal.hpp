@@ -65,8 +65,9 @@ struct Device {
     int cu_count = 0;
     // grow-only scratch slots
     enum Slot { S_PACKED, S_PACKED2, S_IDX, S_IDX2, S_LUT, S_STATS, S_OUT, S_TILES, S_K, S_DENSE,
-                S_DENSE2, S_RED, S_SESSION, S_NUM };
+                S_DENSE2, S_RED, S_SESSION, S_PACKED_B, S_NUM };
     void* buf[S_NUM] = {};
+    hipEvent_t staged[2] = {};  // recorded after the H2D that last read pinned slot 0 / 1
     size_t cap[S_NUM] = {};
     void* get(Slot s, size_t bytes);
     void release();

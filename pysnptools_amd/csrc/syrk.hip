@@ -390,7 +390,12 @@ constexpr int BW = 256, BK = 16, LDA = 256;
 // LOCAL (cfg5, K too large to replicate): this rank owns blocks L = blockIdx.x * world + rank
 // of the upper-triangle block list and writes each as a full 256x256 row-major block at
 // tiles + blockIdx.x * 65536 (no cross-rank reduction is needed).
-template <int MINB, bool LOCAL = false>
+// IL: the next stage's LUT expansion + ds_write is split into 4 pieces issued between the
+// MFMA groups of the current stage (after kk = 1, 3, 5, 7) instead of after all of them.
+// ROT: odd SNP rows of the LDS panels are stored rotated by 32 floats, so the two k-rows one
+// ds_read_b32 of the MFMA A/B operands touches (lanes 0-31: row 2kk, lanes 32-63: row
+// 2kk+1; rows are 1 KiB = a multiple of the 64-bank width) land on disjoint banks.
+template <int MINB, bool LOCAL = false, bool IL = false, bool ROT = false>
 __global__ __launch_bounds__(512, MINB) void k_syrk256(const uint8_t* __restrict__ P, uint64_t pitch, uint64_t n,
                                                       uint64_t kdim, const float* __restrict__ lut,
                                                       float* __restrict__ tiles, int accumulate,
@@ -424,6 +429,19 @@ __global__ __launch_bounds__(512, MINB) void k_syrk256(const uint8_t* __restrict
             l = make_float4(0.f, 0.f, 0.f, 0.f);
         }
     };
+    auto store_part = [&](float* S, int v) {
+        const uint32_t u0 = __float_as_uint(l.x), u1 = __float_as_uint(l.y), u2 = __float_as_uint(l.z),
+                       u3 = __float_as_uint(l.w);
+        const int vv = (v + (d >> 1)) & 3;
+        const uint32_t sh = 8 * vv;
+        float4 o;
+        o.x = sel4m(u0, u1, u2, u3, w, sh);
+        o.y = sel4m(u0, u1, u2, u3, w, sh + 2);
+        o.z = sel4m(u0, u1, u2, u3, w, sh + 4);
+        o.w = sel4m(u0, u1, u2, u3, w, sh + 6);
+        const int col = ROT ? ((16 * d + 4 * vv + 32 * (kq & 1)) & (LDA - 1)) : 16 * d + 4 * vv;
+        *reinterpret_cast<float4*>(S + kq * LDA + col) = o;
+    };
     auto store = [&](float* S) {
         const uint32_t u0 = __float_as_uint(l.x), u1 = __float_as_uint(l.y), u2 = __float_as_uint(l.z),
                        u3 = __float_as_uint(l.w);
@@ -436,7 +454,8 @@ __global__ __launch_bounds__(512, MINB) void k_syrk256(const uint8_t* __restrict
             o.y = sel4m(u0, u1, u2, u3, w, sh + 2);
             o.z = sel4m(u0, u1, u2, u3, w, sh + 4);
             o.w = sel4m(u0, u1, u2, u3, w, sh + 6);
-            *reinterpret_cast<float4*>(S + kq * LDA + 16 * d + 4 * vv) = o;
+            const int col = ROT ? ((16 * d + 4 * vv + 32 * (kq & 1)) & (LDA - 1)) : 16 * d + 4 * vv;
+            *reinterpret_cast<float4*>(S + kq * LDA + col) = o;
         }
     };
 
@@ -453,17 +472,23 @@ __global__ __launch_bounds__(512, MINB) void k_syrk256(const uint8_t* __restrict
         for (int kk = 0; kk < BK / 2; kk++) {
             const int row = (2 * kk + kr) * LDA;
             float a[4], b[2];
+            const int rot = ROT ? 32 * kr : 0;
 #pragma unroll
-            for (int x = 0; x < 4; x++) a[x] = As[row + wm * 128 + 32 * x + c];
+            for (int x = 0; x < 4; x++) a[x] = As[row + ((wm * 128 + 32 * x + rot) & (LDA - 1)) + c];
 #pragma unroll
-            for (int y = 0; y < 2; y++) b[y] = Bs[row + wn * 64 + 32 * y + c];
+            for (int y = 0; y < 2; y++) b[y] = Bs[row + ((wn * 64 + 32 * y + rot) & (LDA - 1)) + c];
 #pragma unroll
             for (int x = 0; x < 4; x++)
 #pragma unroll
                 for (int y = 0; y < 2; y++)
                     acc[x][y] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[x], b[y], acc[x][y], 0, 0, 0);
+            if constexpr (IL) {
+                if (more && (kk & 1)) store_part(op ? lds[buf ^ 1][1] : lds[buf ^ 1][0], kk >> 1);
+            }
         }
-        if (more) store(op ? lds[buf ^ 1][1] : lds[buf ^ 1][0]);
+        if constexpr (!IL) {
+            if (more) store(op ? lds[buf ^ 1][1] : lds[buf ^ 1][0]);
+        }
         __syncthreads();
     }
     float* T;
@@ -767,6 +792,14 @@ void launch_syrk_packed(const uint8_t* packed, uint64_t pitch, uint64_t n, uint6
             case 3: f32k::k_syrk_il<3><<<(unsigned)nt, 256, 0, st>>>(packed, pitch, m, L, Tt, accumulate); break;
             case 4:
                 f32w::k_syrk256<1><<<(unsigned)(nb * (nb + 1) / 2), 512, 0, st>>>(packed, pitch, n, m, L, Tt, accumulate);
+                break;
+            case 6:
+                f32w::k_syrk256<1, false, true>
+                    <<<(unsigned)(nb * (nb + 1) / 2), 512, 0, st>>>(packed, pitch, n, m, L, Tt, accumulate);
+                break;
+            case 7:
+                f32w::k_syrk256<1, false, false, true>
+                    <<<(unsigned)(nb * (nb + 1) / 2), 512, 0, st>>>(packed, pitch, n, m, L, Tt, accumulate);
                 break;
             case 10: f32k::k_syrk_ablate<1><<<(unsigned)nt, 256, 0, st>>>(packed, pitch, m, L, Tt, accumulate); break;
             case 11: f32k::k_syrk_ablate<2><<<(unsigned)nt, 256, 0, st>>>(packed, pitch, m, L, Tt, accumulate); break;

@@ -1,0 +1,91 @@
+"""End-to-end (file-backed, PCIe-inclusive) timings of the mirrored API on one GPU.
+
+Writes a synthetic cfg4-shaped .bed (default 50k iids x 100k SNPs, SnpGen MAF curve, 1%
+missing; packed bytes generated on the GPU and written once), then times what a PySnpTools
+user calls:
+  * Bed(...).read_kernel(Unit(), dtype=float32)  -> snpmi_grm_bed_f32 (gather from the page
+    cache, H2D of packed codes, fused decode+standardize+SYRK, K copied back)
+  * Bed(...)[:, :B].read(dtype=float32)           -> snpmi_bed_read_f32 (values cross PCIe)
+and reports them beside the device-resident figures bench.py measures.  Prints JSON lines.
+Usage: python tools/bench_file.py [--n-iid 50000] [--n-sid 100000] [--dir /tmp]
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import tempfile
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def write_bed(N, path, n, m, seed):
+    from bench import Dev, synth
+
+    pitch = N.lib().snpmi_packed_pitch(n)
+    bpc = (n + 3) // 4
+    step = max(1, (1 << 30) // pitch)
+    dev = Dev(N, pitch * min(step, m))
+    host = np.empty((min(step, m), pitch), dtype=np.uint8)
+    with open(path + ".bed", "wb") as f:
+        f.write(bytes([0x6C, 0x1B, 0x01]))
+        for s0 in range(0, m, step):
+            cnt = min(step, m - s0)
+            synth(N, dev.p, pitch, n, s0, cnt, seed, 0.01)
+            N.call("snpmi_memcpy_d2h", N.ptr(host), dev.p, cnt * pitch)
+            f.write(np.ascontiguousarray(host[:cnt, :bpc]).tobytes())
+    dev.free()
+    with open(path + ".fam", "w") as f:
+        f.write("".join("f%d i%d 0 0 0 0\n" % (i, i) for i in range(n)))
+    with open(path + ".bim", "w") as f:
+        f.write("".join("1\ts%d\t0\t%d\tA\tC\n" % (j, j + 1) for j in range(m)))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n-iid", type=int, default=50_000)
+    ap.add_argument("--n-sid", type=int, default=100_000)
+    ap.add_argument("--read-block", type=int, default=10_000)
+    ap.add_argument("--dir", default=tempfile.gettempdir())
+    ap.add_argument("--seed", type=int, default=4)
+    args = ap.parse_args()
+    from pysnptools_amd import _native as N
+    from pysnptools_amd.snpreader import Bed
+    from pysnptools_amd.standardizer import Unit
+
+    n, m = args.n_iid, args.n_sid
+    with tempfile.TemporaryDirectory(dir=args.dir) as d:
+        base = os.path.join(d, "cfg4")
+        t0 = time.perf_counter()
+        write_bed(N, base, n, m, args.seed)
+        t_write = time.perf_counter() - t0
+        bed = Bed(base + ".bed", count_A1=False)
+        bed.iid, bed.sid  # metadata outside the timed region
+        # warm the page cache and the library (first call allocates scratch)
+        bed[:, :2000].read_kernel(Unit(), dtype=np.float32)
+        t0 = time.perf_counter()
+        K = bed.read_kernel(Unit(), dtype=np.float32)
+        t_grm = time.perf_counter() - t0
+        flops = n * (n + 1) * m
+        print(json.dumps({"bench": "file-backed GRM (Bed.read_kernel, f32)", "n_iid": n, "n_sid": m,
+                          "seconds": t_grm, "TFLOPs_end_to_end": flops / t_grm / 1e12,
+                          "packed_GB": m * ((n + 3) // 4) / 1e9, "K_GB": n * n * 4 / 1e9,
+                          "bed_write_s": t_write, "trace": float(np.trace(K.val))}), flush=True)
+        del K
+        B = args.read_block
+        sub = bed[:, :B]
+        sub.read(dtype=np.float32)
+        t0 = time.perf_counter()
+        v = sub.read(dtype=np.float32)
+        t_read = time.perf_counter() - t0
+        print(json.dumps({"bench": "file-backed read (Bed[:, :B].read, f32, F)", "n_iid": n, "snps": B,
+                          "seconds": t_read, "snps_per_s": B / t_read, "out_GB_per_s": v.val.nbytes / t_read / 1e9}),
+              flush=True)
+
+
+if __name__ == "__main__":
+    main()
