@@ -481,8 +481,9 @@ def main():
                "allreduce_ms": r2["allreduce_ms"], "trace_K": r2["trace"],
                "roofline": {"bound": "mfma", "achieved": r2["mean_tflops"], "peak": MFMA_F32_PEAK_TFLOPS,
                             "unit": "TFLOP/s", "frac": r2["mean_tflops"] / MFMA_F32_PEAK_TFLOPS,
-                            "traffic": pmc_traffic("f32w::k_syrk256", "grm", n, args.grm_block),
-                            "kernel": "f32w::k_syrk256<1,false>", "per_launch_flops": n * (n + 1) * args.grm_block}}
+                            "traffic": pmc_traffic("f32w::k_syrk256d", "grm", n, args.grm_block),
+                            "kernel": "f32w::k_syrk256d<false,16,2> (time per block includes k_decode_f of the "
+                                      "block into Z, ~0.2%)", "per_launch_flops": n * (n + 1) * args.grm_block}}
     grm5 = None
     run5 = args.grm5 == "on" or (args.grm5 == "auto" and dist.world >= 4 and not args.skip_grm)
     if run5:
@@ -497,7 +498,7 @@ def main():
                 "blocks_on_rank0": r3["n_local_blocks"], "K_bytes_per_rank": r3["n_local_blocks"] * 256 * 256 * 4,
                 "roofline": {"bound": "mfma", "achieved": gf5 / 1e3 / dist.world, "peak": MFMA_F32_PEAK_TFLOPS,
                              "unit": "TFLOP/s per GPU", "frac": gf5 / 1e3 / dist.world / MFMA_F32_PEAK_TFLOPS,
-                             "traffic": None, "kernel": "f32w::k_syrk256<1,true>"},
+                             "traffic": None, "kernel": "f32w::k_syrk256d<true,16,2>"},
                 "projected_seconds_1M_snps": r3["wall"] * 1_000_000 / m5}
         if r3.get("parity_sample") is not None:
             grm5["parity"] = grm5_parity(args, m5, *r3["parity_sample"])

@@ -476,6 +476,52 @@ static void subset_impl(const S* val, uint64_t rows, uint64_t cols, uint64_t k, 
 }
 
 // ====================================================================== GRM
+// f32 GRM of a packed SNP block, N >= 4096: two phases per sub-block of SNPs -- k_decode_f
+// writes the standardized block Z (f32, F order, ld = round_up(N, 256)) to HBM (0.4 ms per
+// 10k SNPs at N=50k), then the dense SYRK streams Z into LDS with global_load_lds and runs
+// MFMA-only (no VALU in its loader): 136.7 TFLOP/s vs 130.9 for the fused LUT-expanding
+// kernel (tools/ubench.py syrk / syrk_dense, N=50k, 10k SNPs).  Sub-blocks keep Z <= 16 GiB.
+static bool use_two_phase(int dt, uint64_t n) {
+    return dt == SNPMI_DT_F32 && n >= 4096 && (g_variant_syrk == 0 || g_variant_syrk == 20);
+}
+
+template <class F>
+static void for_z_blocks(Device& d, const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m, const float* lut,
+                         F&& syrk) {
+    const uint64_t ldz = round_up(n, 256);
+    uint64_t sub = std::min<uint64_t>(m, std::max<uint64_t>(256, (16ull << 30) / (ldz * 4)));
+    sub = std::min<uint64_t>(m, std::max<uint64_t>(16, sub / 16 * 16));
+    float* Z = (float*)d.get(Device::S_ZBLK, sub * ldz * 4);
+    if (ldz > n)  // pad iids read by the last 256-iid panel: keep them finite (they only feed K(i,j), i or j >= n)
+        SNPMI_HIP(hipMemset2DAsync(Z + n, ldz * 4, 0, (ldz - n) * 4, sub, d.stream));
+    for (uint64_t s0 = 0; s0 < m; s0 += sub) {
+        const uint64_t cnt = std::min(sub, m - s0);
+        launch_decode(packed + s0 * pitch, pitch, n, cnt, lut + 4 * s0, SNPMI_DT_F32, 0, Z, ldz, d.stream);
+        syrk(Z, ldz, cnt, s0 > 0);
+    }
+}
+
+static void syrk_packed_auto(Device& d, const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m,
+                             const void* lut, int dt, void* tiles, int accumulate) {
+    if (!use_two_phase(dt, n) || m == 0) {
+        launch_syrk_packed(packed, pitch, n, m, lut, dt, tiles, accumulate, d.stream);
+        return;
+    }
+    for_z_blocks(d, packed, pitch, n, m, (const float*)lut, [&](const float* Z, uint64_t ldz, uint64_t cnt, bool more) {
+        launch_syrk_dense(Z, ldz, n, cnt, SNPMI_DT_F32, tiles, accumulate || more, d.stream);
+    });
+}
+
+static void syrk_packed_part_auto(Device& d, const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m,
+                                  const float* lut, int rank, int world, void* blocks, int accumulate) {
+    if (!use_two_phase(SNPMI_DT_F32, n) || m == 0) {
+        launch_syrk_packed_part(packed, pitch, n, m, lut, rank, world, blocks, accumulate, d.stream);
+        return;
+    }
+    for_z_blocks(d, packed, pitch, n, m, lut, [&](const float* Z, uint64_t ldz, uint64_t cnt, bool more) {
+        launch_syrk_dense_part(Z, ldz, n, cnt, rank, world, blocks, accumulate || more, d.stream);
+    });
+}
 // Finish a GRM held as tiles on the device: optional DiagKtoN, then K (n x n) to the host,
 // extracted in row blocks so the device never needs a second full-size K.
 template <typename T>
@@ -540,7 +586,7 @@ static bool grm_add_bed(Device& d, T* tiles, bool first, const char* path, uint6
             SNPMI_HIP(hipMemcpyAsync(st_dev, st_host + 2 * c0, cnt * 2 * sizeof(T), hipMemcpyHostToDevice, d.stream));
         launch_snp_stats(packed, p.pitch_out, n_out, cnt, count_a1, std_kind, a, b, use_stats, dt, st_dev, lut,
                          d.stream);
-        launch_syrk_packed(packed, p.pitch_out, n_out, cnt, lut, dt, tiles, !(first && !wrote), d.stream);
+        syrk_packed_auto(d, packed, p.pitch_out, n_out, cnt, lut, dt, tiles, !(first && !wrote));
         wrote = true;
         if (has_stats && !use_stats)
             SNPMI_HIP(hipMemcpyAsync(st_host + 2 * c0, st_dev, cnt * 2 * sizeof(T), hipMemcpyDeviceToHost, d.stream));
@@ -590,7 +636,7 @@ static void grm_dense_impl(const T* val, uint64_t rows, uint64_t cols, int order
     SNPMI_REQUIRE(K_out != nullptr || rows == 0, SNPMI_E_ARG, "K_out is NULL");
     Device& d = device();
     const int dt = DT<T>::v;
-    const uint64_t ldz = n_tiles_1d(std::max<uint64_t>(rows, 1)) * kTile;
+    const uint64_t ldz = round_up(std::max<uint64_t>(rows, 1), 256);  // 256-iid panels of the glds SYRK
     T* Z = (T*)d.get(Device::S_DENSE, ldz * std::max<uint64_t>(cols, 1) * sizeof(T));
     if (cols > 0 && rows > 0) {
         if (!order_c) {
@@ -1014,7 +1060,7 @@ int snpmi_dev_syrk_packed(const uint8_t* packed, uint64_t pitch, uint64_t n_iid,
     return guarded([&] {
         SNPMI_REQUIRE(dtype == SNPMI_DT_F32 || dtype == SNPMI_DT_F64, SNPMI_E_ARG, "GRM dtype must be f32/f64");
         SNPMI_REQUIRE(pitch % 64 == 0 && pitch >= ceil_div(n_iid, 4), SNPMI_E_ARG, "pitch must be snpmi_packed_pitch");
-        launch_syrk_packed(packed, pitch, n_iid, n_sid, lut, dtype, K_tiles, accumulate, stream());
+        syrk_packed_auto(device(), packed, pitch, n_iid, n_sid, lut, dtype, K_tiles, accumulate);
     });
 }
 
@@ -1042,7 +1088,8 @@ int snpmi_dev_syrk_packed_part(const uint8_t* packed, uint64_t pitch, uint64_t n
     return guarded([&] {
         SNPMI_REQUIRE(part_world >= 1 && part_rank >= 0 && part_rank < part_world, SNPMI_E_ARG, "bad partition");
         SNPMI_REQUIRE(pitch % 64 == 0 && pitch >= ceil_div(n_iid, 4), SNPMI_E_ARG, "pitch must be snpmi_packed_pitch");
-        launch_syrk_packed_part(packed, pitch, n_iid, n_sid, lut, part_rank, part_world, blocks, accumulate, stream());
+        syrk_packed_part_auto(device(), packed, pitch, n_iid, n_sid, (const float*)lut, part_rank, part_world, blocks,
+                              accumulate);
     });
 }
 

@@ -65,7 +65,7 @@ struct Device {
     int cu_count = 0;
     // grow-only scratch slots
     enum Slot { S_PACKED, S_PACKED2, S_IDX, S_IDX2, S_LUT, S_STATS, S_OUT, S_TILES, S_K, S_DENSE,
-                S_DENSE2, S_RED, S_SESSION, S_PACKED_B, S_NUM };
+                S_DENSE2, S_RED, S_SESSION, S_PACKED_B, S_ZBLK, S_NUM };
     void* buf[S_NUM] = {};
     hipEvent_t staged[2] = {};  // recorded after the H2D that last read pinned slot 0 / 1
     size_t cap[S_NUM] = {};
@@ -116,6 +116,8 @@ void launch_syrk_packed(const uint8_t* packed, uint64_t pitch, uint64_t n_iid, u
 uint64_t grm_part_blocks(uint64_t n, int rank, int world);
 void launch_syrk_packed_part(const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m, const void* lut,
                              int rank, int world, void* blocks, int accumulate, hipStream_t st);
+void launch_syrk_dense_part(const float* Z, uint64_t ldz, uint64_t n, uint64_t m, int rank, int world, void* blocks,
+                            int accumulate, hipStream_t st);
 void launch_syrk_dense(const void* Z, uint64_t ldz, uint64_t n_iid, uint64_t n_sid, int dtype, void* tiles,
                        int accumulate, hipStream_t st);
 

@@ -387,6 +387,40 @@ __global__ __launch_bounds__(256, 4) void k_syrk_ablate(const uint8_t* __restric
 namespace f32w {
 constexpr int BW = 256, BK = 16, LDA = 256;
 
+// write/accumulate a wave's 128x64 of the 256x256 block: into the 128x128 upper-triangle tile
+// store (replicated K), or (LOCAL, cfg5) into the rank's dense 256x256 block at blockIdx.x.
+template <bool LOCAL>
+__device__ __forceinline__ void epilogue(f32x16 (&acc)[4][2], float* __restrict__ tiles, uint64_t n, uint32_t bi,
+                                         uint32_t bj, int accumulate, int lane, int wm, int wn) {
+    float* T;
+    uint64_t ldo;
+    if constexpr (LOCAL) {
+        T = tiles + (uint64_t)blockIdx.x * (BW * BW) + (uint64_t)(wm * 128) * BW + (wn >> 1) * 128;
+        ldo = BW;
+    } else {
+        const uint64_t nt128 = (n + 127) / 128;
+        const uint64_t ti = 2 * (uint64_t)bi + wm, tj = 2 * (uint64_t)bj + (wn >> 1);
+        if (ti > tj || tj >= nt128) return;  // wave-uniform
+        T = tiles + (tj * (tj + 1) / 2 + ti) * (uint64_t)(BM * BM);
+        ldo = BM;
+    }
+#pragma unroll
+    for (int x = 0; x < 4; x++)
+#pragma unroll
+        for (int y = 0; y < 2; y++) {
+            float* bp = T + (32 * x + 4 * (lane >> 5)) * ldo + (wn & 1) * 64 + 32 * y + (lane & 31);
+            if (accumulate) {
+                float old[16];
+#pragma unroll
+                for (int r = 0; r < 16; r++) old[r] = bp[((r & 3) + 8 * (r >> 2)) * ldo];
+#pragma unroll
+                for (int r = 0; r < 16; r++) acc[x][y][r] += old[r];
+            }
+#pragma unroll
+            for (int r = 0; r < 16; r++) bp[((r & 3) + 8 * (r >> 2)) * ldo] = acc[x][y][r];
+        }
+}
+
 // LOCAL (cfg5, K too large to replicate): this rank owns blocks L = blockIdx.x * world + rank
 // of the upper-triangle block list and writes each as a full 256x256 row-major block at
 // tiles + blockIdx.x * 65536 (no cross-rank reduction is needed).
@@ -491,33 +525,98 @@ __global__ __launch_bounds__(512, MINB) void k_syrk256(const uint8_t* __restrict
         }
         __syncthreads();
     }
-    float* T;
-    uint64_t ldo;
-    if constexpr (LOCAL) {
-        T = tiles + (uint64_t)blockIdx.x * (BW * BW) + (uint64_t)(wm * 128) * BW + (wn >> 1) * 128;
-        ldo = BW;
-    } else {
-        const uint64_t nt128 = (n + 127) / 128;
-        const uint64_t ti = 2 * (uint64_t)bi + wm, tj = 2 * (uint64_t)bj + (wn >> 1);
-        if (ti > tj || tj >= nt128) return;  // wave-uniform
-        T = tiles + (tj * (tj + 1) / 2 + ti) * (uint64_t)(BM * BM);
-        ldo = BM;
-    }
+    epilogue<LOCAL>(acc, tiles, n, bi, bj, accumulate, lane, wm, wn);
+}
+
+// dense operand: Z (f32, F order, column k at Z + k*ldz, ldz >= round_up(n, 256), ldz % 4 == 0)
+// streamed global -> LDS by global_load_lds_dwordx4 (no VGPR round trip, no VALU): one
+// wave-instruction moves one 1 KiB SNP row of a 256-iid panel; odd rows are rotated by 32
+// floats through the SOURCE address (the LDS image of a glds is lane-linear) so the two rows a
+// ds_read_b32 of the MFMA operands touches hit disjoint banks.  SNP rows >= kdim are zero-filled
+// by ds_write (wave-uniform branch).
+template <bool LOCAL = false, int BKD = 16, int NBUF = 2>
+__global__ __launch_bounds__(512, 1) void k_syrk256d(const float* __restrict__ Z, uint64_t ldz, uint64_t n,
+                                                    uint64_t kdim, float* __restrict__ tiles, int accumulate,
+                                                    uint32_t part_rank = 0, uint32_t part_world = 1) {
+    static_assert(NBUF == 2 || NBUF == 3, "2 or 3 LDS stages");
+    constexpr int G = 2 * BKD / 8;  // glds per wave per stage (8 waves, one 1 KiB row each)
+    __shared__ __attribute__((aligned(16))) float lds[NBUF][2][BKD * LDA];
+    uint32_t bi, bj;
+    tile_coords(LOCAL ? (uint64_t)blockIdx.x * part_world + part_rank : (uint64_t)blockIdx.x, bi, bj);
+    const uint64_t i0 = (uint64_t)bi * BW, j0 = (uint64_t)bj * BW;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int wm = wave >> 2, wn = wave & 3;
+    const int kr = lane >> 5, c = lane & 31;
+    f32x16 acc[4][2];
 #pragma unroll
     for (int x = 0; x < 4; x++)
 #pragma unroll
-        for (int y = 0; y < 2; y++) {
-            float* bp = T + (32 * x + 4 * (lane >> 5)) * ldo + (wn & 1) * 64 + 32 * y + (lane & 31);
-            if (accumulate) {
-                float old[16];
+        for (int y = 0; y < 2; y++) acc[x][y] = (f32x16){};
+    const uint64_t nst = (kdim + BKD - 1) / BKD;
+    auto issue = [&](uint64_t k0, int buf) {
 #pragma unroll
-                for (int r = 0; r < 16; r++) old[r] = bp[((r & 3) + 8 * (r >> 2)) * ldo];
-#pragma unroll
-                for (int r = 0; r < 16; r++) acc[x][y][r] += old[r];
+        for (int q = 0; q < G; q++) {
+            const int r = wave * G + q;  // 2*BKD rows per stage: 2 panels x BKD SNPs
+            const int panel = r / BKD, k = r % BKD;
+            float* dst = &lds[buf][panel][k * LDA];
+            const uint64_t kk = k0 + k;
+            if (kk < kdim) {
+                const float* src = Z + kk * ldz + (panel ? j0 : i0) + ((4 * lane + 32 * (k & 1)) & (BW - 1));
+                __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                                 (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+            } else {
+                reinterpret_cast<float4*>(dst)[lane] = make_float4(0.f, 0.f, 0.f, 0.f);
             }
-#pragma unroll
-            for (int r = 0; r < 16; r++) bp[((r & 3) + 8 * (r >> 2)) * ldo] = acc[x][y][r];
         }
+    };
+    auto compute = [&](int buf) {
+        const float* As = lds[buf][0];
+        const float* Bs = lds[buf][1];
+#pragma unroll
+        for (int kk = 0; kk < BKD / 2; kk++) {
+            const int row = (2 * kk + kr) * LDA;
+            const int rot = 32 * kr;
+            float a[4], b[2];
+#pragma unroll
+            for (int x = 0; x < 4; x++) a[x] = As[row + ((wm * 128 + 32 * x - rot) & (LDA - 1)) + c];
+#pragma unroll
+            for (int y = 0; y < 2; y++) b[y] = Bs[row + ((wn * 64 + 32 * y - rot) & (LDA - 1)) + c];
+#pragma unroll
+            for (int x = 0; x < 4; x++)
+#pragma unroll
+                for (int y = 0; y < 2; y++)
+                    acc[x][y] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[x], b[y], acc[x][y], 0, 0, 0);
+        }
+    };
+    if constexpr (NBUF == 2) {
+        issue(0, 0);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        for (uint64_t s = 0; s < nst; s++) {
+            const int buf = s & 1;
+            if (s + 1 < nst) issue((s + 1) * BKD, buf ^ 1);
+            compute(buf);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+        }
+    } else {
+        // 3 stages, one raw barrier per stage; a counted vmcnt leaves stage s+1 in flight
+        issue(0, 0);
+        if (nst > 1) issue(BKD, 1);
+        for (uint64_t s = 0; s < nst; s++) {
+            if (s + 1 < nst) {
+                if constexpr (G == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+                else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+            } else {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            if (s + 2 < nst) issue((s + 2) * BKD, (int)((s + 2) % 3));
+            compute((int)(s % 3));
+        }
+    }
+    epilogue<LOCAL>(acc, tiles, n, bi, bj, accumulate, lane, wm, wn);
 }
 }  // namespace f32w
 
@@ -848,6 +947,21 @@ void launch_syrk_packed_part(const uint8_t* packed, uint64_t pitch, uint64_t n, 
     SNPMI_HIP(hipGetLastError());
 }
 
+void launch_syrk_dense_part(const float* Z, uint64_t ldz, uint64_t n, uint64_t m, int rank, int world, void* blocks,
+                            int accumulate, hipStream_t st) {
+    const uint64_t nloc = grm_part_blocks(n, rank, world);
+    if (nloc == 0) return;
+    SNPMI_REQUIRE(nloc < (1ull << 31), SNPMI_E_ARG, "too many GRM blocks for one launch");
+    SNPMI_REQUIRE(ldz % 4 == 0 && ldz >= ceil_div(n, 256) * 256, SNPMI_E_ARG, "dense GRM operand needs ldz >= round_up(n, 256)");
+    if (m == 0) {
+        if (!accumulate) SNPMI_HIP(hipMemsetAsync(blocks, 0, nloc * 256 * 256 * sizeof(float), st));
+        return;
+    }
+    f32w::k_syrk256d<true><<<(unsigned)nloc, 512, 0, st>>>(Z, ldz, n, m, (float*)blocks, accumulate, (uint32_t)rank,
+                                                           (uint32_t)world);
+    SNPMI_HIP(hipGetLastError());
+}
+
 void launch_syrk_dense(const void* Z, uint64_t ldz, uint64_t n, uint64_t m, int dtype, void* tiles, int accumulate,
                        hipStream_t st) {
     const uint64_t nt = n_tiles_upper(n);
@@ -858,9 +972,20 @@ void launch_syrk_dense(const void* Z, uint64_t ldz, uint64_t n, uint64_t m, int 
         if (!accumulate) SNPMI_HIP(hipMemsetAsync(tiles, 0, nt * BM * BM * dtype_size(dtype), st));
         return;
     }
-    if (dtype == SNPMI_DT_F32)
-        f32k::k_syrk<false, 16, 4><<<(unsigned)nt, 256, 0, st>>>(Z, ldz, m, nullptr, (float*)tiles, accumulate);
-    else
+    if (dtype == SNPMI_DT_F32) {
+        const uint64_t nb = ceil_div(n, 256);
+        const unsigned g = (unsigned)(nb * (nb + 1) / 2);
+        const float* Zf = (const float*)Z;
+        float* Tf = (float*)tiles;
+        if (n >= 4096 && ldz >= nb * 256 && g_variant_syrk == 8)
+            f32w::k_syrk256d<false, 32, 2><<<g, 512, 0, st>>>(Zf, ldz, n, m, Tf, accumulate);
+        else if (n >= 4096 && ldz >= nb * 256 && g_variant_syrk == 9)
+            f32w::k_syrk256d<false, 16, 3><<<g, 512, 0, st>>>(Zf, ldz, n, m, Tf, accumulate);
+        else if (n >= 4096 && ldz >= nb * 256 && g_variant_syrk != 5)
+            f32w::k_syrk256d<><<<g, 512, 0, st>>>(Zf, ldz, n, m, Tf, accumulate);
+        else
+            f32k::k_syrk<false, 16, 4><<<(unsigned)nt, 256, 0, st>>>(Z, ldz, m, nullptr, (float*)tiles, accumulate);
+    } else
         f64k::k_syrk<false><<<(unsigned)nt, 256, 0, st>>>(Z, ldz, m, nullptr, (double*)tiles, accumulate);
     SNPMI_HIP(hipGetLastError());
 }

@@ -331,9 +331,11 @@ def syrk_variant(request):
     N.call("snpmi_set_kernel_variant", b"syrk", 0)
 
 
-@pytest.mark.parametrize("n", [1, 127, 128, 129, 255, 256, 257, 383, 600])
+@pytest.mark.parametrize("n", [1, 127, 128, 129, 255, 256, 257, 383, 600, 4096, 4097, 4353])
 def test_grm_tile_edges(n, syrk_variant):
-    """Odd tile coverage: N not a multiple of the 128/256-iid tiles, 1 SNP .. several chunks."""
+    """Odd tile coverage: N not a multiple of the 128/256-iid tiles, 1 SNP .. several chunks.
+    N >= 4096 under variant 0 runs the two-phase path (decode to Z + glds SYRK) over two Z
+    sub-blocks (32 + 5 SNPs: a zero-filled tail stage)."""
     rng = np.random.default_rng(n)
     val = rng.integers(0, 3, size=(n, 37)).astype(np.float64)
     val[rng.random(val.shape) < 0.05] = np.nan
@@ -411,7 +413,7 @@ def test_device_decode_standardize_large_properties(dtype):
     assert np.all(v64[~poly] == 0)
 
 
-@pytest.mark.parametrize("n,world", [(300, 1), (700, 3), (1100, 4)])
+@pytest.mark.parametrize("n,world", [(300, 1), (700, 3), (1100, 4), (4100, 2), (4500, 3)])
 def test_grm_partitioned_blocks_assemble_k(n, world):
     """cfg5 mode: every rank's 256x256 blocks (simulated ranks on one GPU) assemble to K."""
     rng = np.random.default_rng(n)
