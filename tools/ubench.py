@@ -56,14 +56,17 @@ def decode(args):
 
 
 def syrk_dense(args):
-    """decode the block to f32 in HBM (ld = round_up(n,128)) + dense-loader SYRK."""
+    """decode the block to f32/f64 in HBM (ld = round_up(n,256)) + dense-loader SYRK."""
     n, m = args.n, args.m
+    dt = N.DT_F64 if args.dtype == "f64" else N.DT_F32
+    esz = 8 if dt == N.DT_F64 else 4
     pitch = N.lib().snpmi_packed_pitch(n)
     ldz = (n + 255) // 256 * 256
     packed = Dev(N, pitch * m)
     synth(N, packed.p, pitch, n, 0, m, 3, 0.01)
-    lut, st, Z = Dev(N, m * 16), Dev(N, m * 8), Dev(N, m * ldz * 4)
-    tiles = Dev(N, N.lib().snpmi_grm_tile_bytes(n, N.DT_F32))
+    lut, st, Z = Dev(N, m * 4 * esz), Dev(N, m * 2 * esz), Dev(N, m * ldz * esz)
+    N.call("snpmi_dev_memset", Z.p, 0, m * ldz * esz)
+    tiles = Dev(N, N.lib().snpmi_grm_tile_bytes(n, dt))
     ev = Events(N, 4)
     variants = [int(v) for v in args.variants.split(",")]
     ts = {v: [] for v in variants}
@@ -73,24 +76,26 @@ def syrk_dense(args):
         for v in variants:
             N.call("snpmi_set_kernel_variant", b"syrk", v)
             ev.record(0)
-            N.call("snpmi_dev_snp_stats", packed.p, pitch, n, m, 0, N.STD_UNIT, 0.0, 0.0, 0, N.DT_F32, st.p, lut.p)
-            N.call("snpmi_dev_decode", packed.p, pitch, n, m, lut.p, N.DT_F32, 0, Z.p, ldz)
+            N.call("snpmi_dev_snp_stats", packed.p, pitch, n, m, 0, N.STD_UNIT, 0.0, 0.0, 0, dt, st.p, lut.p)
+            N.call("snpmi_dev_decode", packed.p, pitch, n, m, lut.p, dt, 0, Z.p, ldz)
             ev.record(1)
-            N.call("snpmi_dev_syrk_dense", Z.p, ldz, n, m, N.DT_F32, tiles.p, 0)
+            N.call("snpmi_dev_syrk_dense", Z.p, ldz, n, m, dt, tiles.p, 0)
             ev.record(2)
             td.append(ev.ms(0, 1))
             ts[v].append(ev.ms(1, 2))
             if rnd == 0:
-                chk = np.empty(1 << 22, dtype=np.float32)
+                chk = np.empty(1 << 22, dtype=np.float64 if esz == 8 else np.float32)
                 N.call("snpmi_memcpy_d2h", N.ptr(chk), tiles.p, chk.nbytes)
                 ref = chk.copy() if ref is None else ref
                 err = np.abs(chk.astype(np.float64) - ref).max() / max(np.abs(ref).max(), 1)
                 assert err < 1e-5, "variant %d differs: %g" % (v, err)
     d = np.median(td)
+    peak = 78.6 if esz == 8 else 157.3
     for v in variants:
         t = np.median(ts[v])
-        print(json.dumps({"kernel": "decode+syrk_dense_f32", "variant": v, "n": n, "m": m, "decode_ms": d,
+        print(json.dumps({"kernel": "decode+syrk_dense_" + args.dtype, "variant": v, "n": n, "m": m, "decode_ms": d,
                           "syrk_ms": t, "TFLOPs_syrk": n * (n + 1) * m / t / 1e9,
+                          "frac_syrk": n * (n + 1) * m / t / 1e9 / peak,
                           "TFLOPs_total": n * (n + 1) * m / (t + d) / 1e9}))
 
 
