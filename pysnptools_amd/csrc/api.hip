@@ -205,6 +205,16 @@ static void d2h_rows(Device& d, void* dst, size_t dpitch, const void* src, size_
     drain(prev_r0, prev_n, (i - 1) & 1);
 }
 
+// contiguous byte range as rows of 4 MiB (+ a tail) through the pipelined copy above.  (The
+// same bounce for host->device measured no faster than the runtime's pageable H2D: the
+// source pages are already resident, while a D2H into fresh NumPy memory pays page faults
+// that the threaded copy-out spreads over cores.)
+static void d2h_bytes(Device& d, void* dst, const void* src, size_t bytes, int nthreads) {
+    const size_t w = 4u << 20, rows = bytes / w, tail = bytes - rows * w;
+    d2h_rows(d, dst, w, src, w, w, rows, nthreads);
+    if (tail) d2h_rows(d, (uint8_t*)dst + rows * w, tail, (const uint8_t*)src + rows * w, tail, tail, 1, nthreads);
+}
+
 struct BedMap {
     int fd = -1;
     const uint8_t* base = nullptr;
@@ -443,11 +453,12 @@ static void standardize_impl(T* val, uint64_t rows, uint64_t cols, int order_c, 
     const size_t bytes = rows * cols * sizeof(T);
     T* dv = (T*)d.get(Device::S_DENSE, bytes);
     T* ds = (T*)d.get(Device::S_STATS, cols * 2 * sizeof(T));
+    const int nthreads = resolve_threads(0);
     SNPMI_HIP(hipMemcpyAsync(dv, val, bytes, hipMemcpyHostToDevice, d.stream));
     if (use_stats) SNPMI_HIP(hipMemcpyAsync(ds, stats, cols * 2 * sizeof(T), hipMemcpyHostToDevice, d.stream));
     launch_dense_standardize(dv, rows, cols, order_c ? cols : rows, order_c, DT<T>::v,
                              is_beta ? SNPMI_STD_BETA : SNPMI_STD_UNIT, a, b, use_stats, ds, d.stream);
-    if (apply_in_place) SNPMI_HIP(hipMemcpyAsync(val, dv, bytes, hipMemcpyDeviceToHost, d.stream));
+    if (apply_in_place) d2h_bytes(d, val, dv, bytes, nthreads);
     if (!use_stats) SNPMI_HIP(hipMemcpyAsync(stats, ds, cols * 2 * sizeof(T), hipMemcpyDeviceToHost, d.stream));
     SNPMI_HIP(hipStreamSynchronize(d.stream));
 }
@@ -471,7 +482,7 @@ static void subset_impl(const S* val, uint64_t rows, uint64_t cols, uint64_t k, 
     SNPMI_HIP(hipMemcpyAsync(dri, ri, nr * 8, hipMemcpyHostToDevice, d.stream));
     SNPMI_HIP(hipMemcpyAsync(dci, ci, nc * 8, hipMemcpyHostToDevice, d.stream));
     launch_subset(dv, DT<S>::v, rows, cols, k, in_c, dri, nr, dci, nc, out_c, dout, DT<D>::v, d.stream);
-    SNPMI_HIP(hipMemcpyAsync(out, dout, nr * nc * k * sizeof(D), hipMemcpyDeviceToHost, d.stream));
+    d2h_bytes(d, out, dout, nr * nc * k * sizeof(D), resolve_threads(0));
     SNPMI_HIP(hipStreamSynchronize(d.stream));
 }
 
@@ -482,22 +493,23 @@ static void subset_impl(const S* val, uint64_t rows, uint64_t cols, uint64_t k, 
 // MFMA-only (no VALU in its loader): 136.7 TFLOP/s vs 130.9 for the fused LUT-expanding
 // kernel (tools/ubench.py syrk / syrk_dense, N=50k, 10k SNPs).  Sub-blocks keep Z <= 16 GiB.
 static bool use_two_phase(int dt, uint64_t n) {
-    return dt == SNPMI_DT_F32 && n >= 4096 && (g_variant_syrk == 0 || g_variant_syrk == 20);
+    if (g_variant_syrk != 0 && g_variant_syrk != 20) return false;
+    return dt == SNPMI_DT_F32 ? n >= 4096 : n >= 1024;
 }
 
-template <class F>
-static void for_z_blocks(Device& d, const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m, const float* lut,
+template <typename T, class F>
+static void for_z_blocks(Device& d, const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m, const T* lut,
                          F&& syrk) {
     const uint64_t ldz = round_up(n, 256);
-    uint64_t sub = std::min<uint64_t>(m, std::max<uint64_t>(256, (16ull << 30) / (ldz * 4)));
+    uint64_t sub = std::min<uint64_t>(m, std::max<uint64_t>(256, (16ull << 30) / (ldz * sizeof(T))));
     sub = std::min<uint64_t>(m, std::max<uint64_t>(16, sub / 16 * 16));
-    float* Z = (float*)d.get(Device::S_ZBLK, sub * ldz * 4);
-    if (ldz > n)  // pad iids read by the last 256-iid panel: keep them finite (they only feed K(i,j), i or j >= n)
-        SNPMI_HIP(hipMemset2DAsync(Z + n, ldz * 4, 0, (ldz - n) * 4, sub, d.stream));
+    T* Z = (T*)d.get(Device::S_ZBLK, sub * ldz * sizeof(T));
+    if (ldz > n)  // pad iids read by the last panel: keep them finite (they only feed K(i,j), i or j >= n)
+        SNPMI_HIP(hipMemset2DAsync(Z + n, ldz * sizeof(T), 0, (ldz - n) * sizeof(T), sub, d.stream));
     for (uint64_t s0 = 0; s0 < m; s0 += sub) {
         const uint64_t cnt = std::min(sub, m - s0);
-        launch_decode(packed + s0 * pitch, pitch, n, cnt, lut + 4 * s0, SNPMI_DT_F32, 0, Z, ldz, d.stream);
-        syrk(Z, ldz, cnt, s0 > 0);
+        launch_decode(packed + s0 * pitch, pitch, n, cnt, lut + 4 * s0, DT<T>::v, 0, Z, ldz, d.stream);
+        syrk((const T*)Z, ldz, cnt, s0 > 0);
     }
 }
 
@@ -507,9 +519,11 @@ static void syrk_packed_auto(Device& d, const uint8_t* packed, uint64_t pitch, u
         launch_syrk_packed(packed, pitch, n, m, lut, dt, tiles, accumulate, d.stream);
         return;
     }
-    for_z_blocks(d, packed, pitch, n, m, (const float*)lut, [&](const float* Z, uint64_t ldz, uint64_t cnt, bool more) {
-        launch_syrk_dense(Z, ldz, n, cnt, SNPMI_DT_F32, tiles, accumulate || more, d.stream);
-    });
+    auto run = [&](const void* Z, uint64_t ldz, uint64_t cnt, bool more) {
+        launch_syrk_dense(Z, ldz, n, cnt, dt, tiles, accumulate || more, d.stream);
+    };
+    if (dt == SNPMI_DT_F32) for_z_blocks(d, packed, pitch, n, m, (const float*)lut, run);
+    else for_z_blocks(d, packed, pitch, n, m, (const double*)lut, run);
 }
 
 static void syrk_packed_part_auto(Device& d, const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m,

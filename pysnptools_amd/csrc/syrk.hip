@@ -779,6 +779,27 @@ __device__ __forceinline__ void compute_store(const double* As, const double* Bs
     }
 }
 
+// f64 16x16x4 C/D layout: col = lane&15, row = (lane>>4) + 4*r
+__device__ __forceinline__ void epilogue(f64x4 (&acc)[4][4], double* __restrict__ tiles, int accumulate, int lane,
+                                         int wm, int wn) {
+    double* T = tiles + (uint64_t)blockIdx.x * (BM * BM);
+#pragma unroll
+    for (int x = 0; x < 4; x++)
+#pragma unroll
+        for (int y = 0; y < 4; y++) {
+            double* base = T + (wm * 64 + 16 * x + (lane >> 4)) * BM + wn * 64 + 16 * y + (lane & 15);
+            if (accumulate) {
+                double old[4];
+#pragma unroll
+                for (int r = 0; r < 4; r++) old[r] = base[4 * r * BM];
+#pragma unroll
+                for (int r = 0; r < 4; r++) acc[x][y][r] += old[r];
+            }
+#pragma unroll
+            for (int r = 0; r < 4; r++) base[4 * r * BM] = acc[x][y][r];
+        }
+}
+
 // MODE 0: production; 1: bfi select; 2: bfi select interleaved with the MFMAs;
 // 10: compute only (ablation); 11: loader only (ablation)
 template <bool PACKED, int MODE = 0>
@@ -844,23 +865,53 @@ __global__ __launch_bounds__(256, 2) void k_syrk(const void* __restrict__ src, u
         }
         __syncthreads();
     }
-    // epilogue: f64 16x16x4 C/D layout: col = lane&15, row = (lane>>4) + 4*r
-    double* T = tiles + (uint64_t)blockIdx.x * (BM * BM);
+    epilogue(acc, tiles, accumulate, lane, wm, wn);
+}
+
+// Dense f64 operand (F order, ldz >= round_up(n, 128)) streamed global -> LDS with
+// global_load_lds_dwordx4: one wave-instruction = one 128-double (1 KiB) SNP row of a panel,
+// rows padded to LDA (allowed: no instruction crosses a row).  No VALU in the loader.
+__global__ __launch_bounds__(256, 2) void k_syrk_glds(const double* __restrict__ Z, uint64_t ldz, uint64_t kdim,
+                                                      double* __restrict__ tiles, int accumulate) {
+    __shared__ __attribute__((aligned(16))) double lds[2][2][BK * LDA];
+    uint32_t ti, tj;
+    tile_coords(blockIdx.x, ti, tj);
+    const uint64_t i0 = (uint64_t)ti * BM, j0 = (uint64_t)tj * BM;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int wm = wave >> 1, wn = wave & 1;
+    f64x4 acc[4][4];
 #pragma unroll
     for (int x = 0; x < 4; x++)
 #pragma unroll
-        for (int y = 0; y < 4; y++) {
-            double* base = T + (wm * 64 + 16 * x + (lane >> 4)) * BM + wn * 64 + 16 * y + (lane & 15);
-            if (accumulate) {
-                double old[4];
+        for (int y = 0; y < 4; y++) acc[x][y] = (f64x4){};
+    const uint64_t nst = (kdim + BK - 1) / BK;
+    auto issue = [&](uint64_t k0, int buf) {
 #pragma unroll
-                for (int r = 0; r < 4; r++) old[r] = base[4 * r * BM];
-#pragma unroll
-                for (int r = 0; r < 4; r++) acc[x][y][r] += old[r];
+        for (int q = 0; q < 8; q++) {
+            const int r = wave * 8 + q;  // 32 rows per stage: 2 panels x BK
+            const int panel = r >> 4, k = r & (BK - 1);
+            double* dst = &lds[buf][panel][k * LDA];
+            const uint64_t kk = k0 + k;
+            if (kk < kdim) {
+                const double* src = Z + kk * ldz + (panel ? j0 : i0) + 2 * lane;
+                __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                                 (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+            } else {
+                reinterpret_cast<double2*>(dst)[lane] = make_double2(0.0, 0.0);
             }
-#pragma unroll
-            for (int r = 0; r < 4; r++) base[4 * r * BM] = acc[x][y][r];
         }
+    };
+    issue(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (uint64_t s = 0; s < nst; s++) {
+        const int buf = s & 1;
+        if (s + 1 < nst) issue((s + 1) * BK, buf ^ 1);
+        compute(lds[buf][0], lds[buf][1], acc, wm, wn, lane);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
+    epilogue(acc, tiles, accumulate, lane, wm, wn);
 }
 }  // namespace f64k
 
@@ -985,8 +1036,11 @@ void launch_syrk_dense(const void* Z, uint64_t ldz, uint64_t n, uint64_t m, int 
             f32w::k_syrk256d<><<<g, 512, 0, st>>>(Zf, ldz, n, m, Tf, accumulate);
         else
             f32k::k_syrk<false, 16, 4><<<(unsigned)nt, 256, 0, st>>>(Z, ldz, m, nullptr, (float*)tiles, accumulate);
-    } else
+    } else if (g_variant_syrk == 5) {
         f64k::k_syrk<false><<<(unsigned)nt, 256, 0, st>>>(Z, ldz, m, nullptr, (double*)tiles, accumulate);
+    } else {
+        f64k::k_syrk_glds<<<(unsigned)nt, 256, 0, st>>>((const double*)Z, ldz, m, (double*)tiles, accumulate);
+    }
     SNPMI_HIP(hipGetLastError());
 }
 

@@ -85,6 +85,14 @@ def main():
         print(json.dumps({"bench": "file-backed read (Bed[:, :B].read, f32, F)", "n_iid": n, "snps": B,
                           "seconds": t_read, "snps_per_s": B / t_read, "out_GB_per_s": v.val.nbytes / t_read / 1e9}),
               flush=True)
+        # in-memory SnpData.standardize (host array -> GPU -> host, in place)
+        v.standardize(Unit())
+        t0 = time.perf_counter()
+        v.standardize(Unit())
+        t_std = time.perf_counter() - t0
+        print(json.dumps({"bench": "SnpData.standardize(Unit()) in memory, f32", "n_iid": n, "snps": B,
+                          "seconds": t_std, "snps_per_s": B / t_std,
+                          "GB_per_s_each_way": v.val.nbytes / t_std / 1e9}), flush=True)
 
 
 if __name__ == "__main__":
