@@ -711,6 +711,124 @@ __global__ __launch_bounds__(kBlock) void k_synth(uint8_t* __restrict__ packed, 
     }
 }
 
+// Fused stats + decode with the packed column held in LDS (one 1024-thread workgroup per SNP,
+// column <= kLdsColMax bytes, i.e. N <= ~600k): pass 1 streams the column HBM -> LDS once and
+// counts its codes; one lane turns the counts into f64 stats + the LUT exactly as k_snp_stats
+// does; pass 2 decodes from LDS with the k_decode_f store pattern (each wave store = 1 KiB
+// contiguous, non-temporal).  The packed bytes are read from HBM once instead of twice.
+constexpr int kLdsBlock = 1024;
+constexpr uint64_t kLdsColMax = 150 * 1024;
+
+__global__ __launch_bounds__(kLdsBlock) void k_decode_std_lds_f32(const uint8_t* __restrict__ packed, uint64_t pitch,
+                                                                 uint64_t n, int count_a1, int std_kind, double a,
+                                                                 double b, int use_stats, float* __restrict__ stats,
+                                                                 float* __restrict__ lut_out, float* __restrict__ out,
+                                                                 uint64_t ld) {
+    extern __shared__ u32x4_t col[];
+    __shared__ uint32_t red[3][kLdsBlock / kWave];
+    __shared__ float lutsh[4];
+    const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
+    const uint64_t j = blockIdx.x;
+    const u32x4_t* src = reinterpret_cast<const u32x4_t*>(packed + j * pitch);
+    const uint64_t nq = (n + 63) / 64;  // 16-byte words holding the column's codes
+    const bool count = std_kind != SNPMI_STD_NONE && !use_stats;
+    uint32_t c1 = 0, c2 = 0, c3 = 0;
+    for (uint64_t q = threadIdx.x; q < nq; q += kLdsBlock) {
+        const u32x4_t v = __builtin_nontemporal_load(src + q);
+        col[q] = v;
+        if (count) {
+            const uint32_t w4[4] = {v[0], v[1], v[2], v[3]};
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                uint32_t lo = w4[k] & 0x55555555u, hi = (w4[k] >> 1) & 0x55555555u;
+                const uint64_t ib = q * 64 + 16 * k;
+                if (ib + 16 > n) {
+                    const uint64_t valid = n > ib ? n - ib : 0;
+                    const uint32_t mk = ((1u << (2 * valid)) - 1u) & 0x55555555u;  // valid < 16 here
+                    lo &= mk;
+                    hi &= mk;
+                }
+                c3 += __popc(lo & hi);
+                c2 += __popc(hi & ~lo);
+                c1 += __popc(lo & ~hi);
+            }
+        }
+    }
+    if (count) {
+        c1 = wave_sum_u32(c1);
+        c2 = wave_sum_u32(c2);
+        c3 = wave_sum_u32(c3);
+        if (lane == 0) {
+            red[0][wave] = c1;
+            red[1][wave] = c2;
+            red[2][wave] = c3;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        if (std_kind == SNPMI_STD_NONE) {
+            for (int c = 0; c < 4; c++) {
+                const int v = code_value(c, count_a1);
+                lutsh[c] = v < 0 ? __builtin_nanf("") : (float)v;
+            }
+        } else {
+            double mean, sd;
+            if (count) {
+                uint64_t t1 = 0, t2 = 0, t3 = 0;
+                for (int q = 0; q < kLdsBlock / kWave; q++) {
+                    t1 += red[0][q];
+                    t2 += red[1][q];
+                    t3 += red[2][q];
+                }
+                const uint64_t c0 = n - t1 - t2 - t3, chi = count_a1 ? c0 : t3;
+                mean = stats_mean_std((double)(n - t1), (double)(t2 + 2 * chi), (double)(t2 + 4 * chi), &sd);
+                stats[2 * j] = (float)mean;
+                stats[2 * j + 1] = (float)sd;
+            } else {
+                mean = (double)stats[2 * j];
+                sd = (double)stats[2 * j + 1];
+            }
+            const double w = std_kind == SNPMI_STD_BETA ? beta_weight(mean, a, b) : 0.0;
+            const bool zero_col = std_kind == SNPMI_STD_BETA && use_stats && __builtin_isinf(sd);
+            for (int c = 0; c < 4; c++) {
+                const int v = code_value(c, count_a1);
+                double x;
+                if (v < 0 || zero_col) x = 0.0;
+                else if (std_kind == SNPMI_STD_BETA) x = ((double)v - mean) * w;
+                else x = ((double)v - mean) / sd;
+                lutsh[c] = (float)x;
+            }
+        }
+        for (int c = 0; c < 4; c++) lut_out[4 * j + c] = lutsh[c];
+    }
+    __syncthreads();
+    const float l0 = lutsh[0], l1 = lutsh[1], l2 = lutsh[2], l3 = lutsh[3];
+    const uint32_t* cw = reinterpret_cast<const uint32_t*>(col);
+    float* o = out + j * ld;
+    const uint64_t chunks = (n + 1023) / 1024;
+    for (uint64_t c = wave; c < chunks; c += kLdsBlock / kWave) {
+        const uint64_t i0 = c * 1024;
+        const uint32_t wv = (i0 + 16 * (uint64_t)lane < n) ? cw[c * 64 + lane] : 0u;
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const uint32_t srcw = __shfl(wv, r * 16 + (lane >> 2), kWave);
+            const uint32_t byte = (srcw >> (8 * (lane & 3))) & 0xffu;
+            const uint64_t i = i0 + r * 256 + 4 * lane;
+            f32x4_t v;
+            v.x = sel4(l0, l1, l2, l3, byte & 3u);
+            v.y = sel4(l0, l1, l2, l3, (byte >> 2) & 3u);
+            v.z = sel4(l0, l1, l2, l3, (byte >> 4) & 3u);
+            v.w = sel4(l0, l1, l2, l3, byte >> 6);
+            if (i + 4 <= n) {
+                store_nt(reinterpret_cast<f32x4_t*>(o + i), v);
+            } else {
+                for (int t = 0; t < 4; t++)
+                    if (i + t < n) o[i + t] = v[t];
+            }
+        }
+    }
+}
+
 inline unsigned grid_for(uint64_t work, uint64_t per_block, unsigned cap = 65536) {
     uint64_t g = (work + per_block - 1) / per_block;
     if (g < 1) g = 1;
@@ -771,8 +889,17 @@ void launch_decode_std_fused(const uint8_t* packed, uint64_t pitch, uint64_t n, 
                              int std_kind, double a, double b, int use_stats, void* stats, void* lut, void* out,
                              uint64_t ld, hipStream_t st) {
     if (m == 0 || n == 0) return;
-    k_decode_std_col_f32<4><<<(unsigned)m, kBlock, 0, st>>>(packed, pitch, n, count_a1, std_kind, a, b, use_stats,
-                                                            (float*)stats, (float*)lut, (float*)out, ld);
+    const uint64_t col_bytes = ceil_div(n, 64) * 16;
+    if (g_variant_decode != 1 && col_bytes <= kLdsColMax) {
+        SNPMI_HIP(hipFuncSetAttribute((const void*)k_decode_std_lds_f32, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      (int)kLdsColMax));
+        k_decode_std_lds_f32<<<(unsigned)m, kLdsBlock, col_bytes, st>>>(packed, pitch, n, count_a1, std_kind, a, b,
+                                                                        use_stats, (float*)stats, (float*)lut,
+                                                                        (float*)out, ld);
+    } else {
+        k_decode_std_col_f32<4><<<(unsigned)m, kBlock, 0, st>>>(packed, pitch, n, count_a1, std_kind, a, b, use_stats,
+                                                                (float*)stats, (float*)lut, (float*)out, ld);
+    }
     SNPMI_LAUNCH_CHECK();
 }
 

@@ -391,11 +391,12 @@ constexpr int BW = 256, BK = 16, LDA = 256;
 // store (replicated K), or (LOCAL, cfg5) into the rank's dense 256x256 block at blockIdx.x.
 template <bool LOCAL>
 __device__ __forceinline__ void epilogue(f32x16 (&acc)[4][2], float* __restrict__ tiles, uint64_t n, uint32_t bi,
-                                         uint32_t bj, int accumulate, int lane, int wm, int wn) {
+                                         uint32_t bj, int accumulate, int lane, int wm, int wn,
+                                         uint64_t local_block) {
     float* T;
     uint64_t ldo;
     if constexpr (LOCAL) {
-        T = tiles + (uint64_t)blockIdx.x * (BW * BW) + (uint64_t)(wm * 128) * BW + (wn >> 1) * 128;
+        T = tiles + local_block * (BW * BW) + (uint64_t)(wm * 128) * BW + (wn >> 1) * 128;
         ldo = BW;
     } else {
         const uint64_t nt128 = (n + 127) / 128;
@@ -525,7 +526,7 @@ __global__ __launch_bounds__(512, MINB) void k_syrk256(const uint8_t* __restrict
         }
         __syncthreads();
     }
-    epilogue<LOCAL>(acc, tiles, n, bi, bj, accumulate, lane, wm, wn);
+    epilogue<LOCAL>(acc, tiles, n, bi, bj, accumulate, lane, wm, wn, blockIdx.x);
 }
 
 // dense operand: Z (f32, F order, column k at Z + k*ldz, ldz >= round_up(n, 256), ldz % 4 == 0)
@@ -534,15 +535,24 @@ __global__ __launch_bounds__(512, MINB) void k_syrk256(const uint8_t* __restrict
 // floats through the SOURCE address (the LDS image of a glds is lane-linear) so the two rows a
 // ds_read_b32 of the MFMA operands touches hit disjoint banks.  SNP rows >= kdim are zero-filled
 // by ds_write (wave-uniform branch).
-template <bool LOCAL = false, int BKD = 16, int NBUF = 2>
+// XCD remap: the hardware deals consecutive workgroups round-robin over the 8 XCDs (each with
+// its own L2); remapping so that XCD x runs a contiguous range of the block list keeps blocks
+// that share a panel (same column bj, neighbouring bi) on one L2 (bijective for any count).
+__device__ __forceinline__ uint64_t xcd_remap(uint64_t orig, uint64_t nwg) {
+    const uint64_t q = nwg / 8, r = nwg % 8, xcd = orig % 8;
+    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
+}
+
+template <bool LOCAL = false, int BKD = 16, int NBUF = 2, bool XCD = false>
 __global__ __launch_bounds__(512, 1) void k_syrk256d(const float* __restrict__ Z, uint64_t ldz, uint64_t n,
                                                     uint64_t kdim, float* __restrict__ tiles, int accumulate,
                                                     uint32_t part_rank = 0, uint32_t part_world = 1) {
     static_assert(NBUF == 2 || NBUF == 3, "2 or 3 LDS stages");
     constexpr int G = 2 * BKD / 8;  // glds per wave per stage (8 waves, one 1 KiB row each)
     __shared__ __attribute__((aligned(16))) float lds[NBUF][2][BKD * LDA];
+    const uint64_t wg = XCD ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
     uint32_t bi, bj;
-    tile_coords(LOCAL ? (uint64_t)blockIdx.x * part_world + part_rank : (uint64_t)blockIdx.x, bi, bj);
+    tile_coords(LOCAL ? wg * part_world + part_rank : wg, bi, bj);
     const uint64_t i0 = (uint64_t)bi * BW, j0 = (uint64_t)bj * BW;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int wm = wave >> 2, wn = wave & 3;
@@ -616,7 +626,7 @@ __global__ __launch_bounds__(512, 1) void k_syrk256d(const float* __restrict__ Z
             compute((int)(s % 3));
         }
     }
-    epilogue<LOCAL>(acc, tiles, n, bi, bj, accumulate, lane, wm, wn);
+    epilogue<LOCAL>(acc, tiles, n, bi, bj, accumulate, lane, wm, wn, wg);
 }
 }  // namespace f32w
 
@@ -1032,6 +1042,8 @@ void launch_syrk_dense(const void* Z, uint64_t ldz, uint64_t n, uint64_t m, int 
             f32w::k_syrk256d<false, 32, 2><<<g, 512, 0, st>>>(Zf, ldz, n, m, Tf, accumulate);
         else if (n >= 4096 && ldz >= nb * 256 && g_variant_syrk == 9)
             f32w::k_syrk256d<false, 16, 3><<<g, 512, 0, st>>>(Zf, ldz, n, m, Tf, accumulate);
+        else if (n >= 4096 && ldz >= nb * 256 && g_variant_syrk == 21)
+            f32w::k_syrk256d<false, 16, 2, true><<<g, 512, 0, st>>>(Zf, ldz, n, m, Tf, accumulate);
         else if (n >= 4096 && ldz >= nb * 256 && g_variant_syrk != 5)
             f32w::k_syrk256d<><<<g, 512, 0, st>>>(Zf, ldz, n, m, Tf, accumulate);
         else

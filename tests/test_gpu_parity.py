@@ -544,3 +544,41 @@ def test_dev_encode_large(order_c):
     assert bad.value == 0
     bpc = (n + 3) // 4
     assert np.array_equal(out[:, :bpc], O.encode(v))
+
+
+@pytest.mark.parametrize("n", [1, 63, 64, 65, 1023, 1025, 5000, 700_000])
+@pytest.mark.parametrize("kind,use_stats,count_a1", [(N.STD_UNIT, 0, 0), (N.STD_BETA, 0, 1), (N.STD_NONE, 0, 0),
+                                                     (N.STD_UNIT, 1, 0)])
+def test_fused_decode_standardize_equals_two_kernels(n, kind, use_stats, count_a1):
+    """snpmi_dev_decode_standardize (LDS-resident column; > 150 KiB columns fall back to the
+    re-reading kernel, as does decode variant 1) == k_snp_stats + k_decode_f, bit for bit."""
+    m = 3 if n > 100_000 else 37
+    buf, pitch = synth_dev(n, m, 5 + n)
+    ld = (n + 15) // 16 * 16
+    a, b = (1.0, 25.0) if kind == N.STD_BETA else (0.0, 0.0)
+    outs = []
+    for fused, variant in ((False, 0), (True, 0), (True, 1)):
+        N.call("snpmi_set_kernel_variant", b"decode", variant)
+        lut, st, out = Dev(m * 16), Dev(m * 8), Dev(m * ld * 4)
+        if use_stats:
+            stats_in = np.tile(np.array([[0.9, 0.7]], dtype=np.float32), (m, 1))
+            st.put(stats_in)
+        if fused:
+            N.call("snpmi_dev_decode_standardize", buf.p, pitch, n, m, count_a1, kind, a, b, use_stats, N.DT_F32,
+                   st.p, lut.p, out.p, ld)
+        else:
+            N.call("snpmi_dev_snp_stats", buf.p, pitch, n, m, count_a1, kind, a, b, use_stats, N.DT_F32, st.p, lut.p)
+            N.call("snpmi_dev_decode", buf.p, pitch, n, m, lut.p, N.DT_F32, 0, out.p, ld)
+        outs.append((out.get(np.empty((m, ld), dtype=np.float32))[:, :n], lut.get(np.empty((m, 4), dtype=np.float32)),
+                     st.get(np.empty((m, 2), dtype=np.float32))))
+    N.call("snpmi_set_kernel_variant", b"decode", 0)
+    for o in outs[1:]:
+        for q, (x, y) in enumerate(zip(outs[0], o)):
+            if q == 2 and kind == N.STD_NONE:
+                continue  # Identity writes no stats
+            assert np.array_equal(x, y, equal_nan=True)
+    if kind == N.STD_UNIT and not use_stats and n <= 5000:
+        host = buf.get(np.empty((m, pitch), dtype=np.uint8))
+        exp, est = O.decode_standardize(np.ascontiguousarray(host[:, :(n + 3) // 4]).reshape(-1), n, m,
+                                        count_A1=bool(count_a1), dtype=np.float32)
+        assert np.array_equal(outs[1][0].T, exp) and np.array_equal(outs[1][2], est)

@@ -11,7 +11,7 @@ import json
 import os
 import sys
 
-KERNELS = {"k_decode_f<float, 4>": "k_decode_f<float>", "k_decode_f<float": "k_decode_f<float>",
+KERNELS = {"k_decode_std_lds_f32": "k_decode_std_lds_f32", "k_decode_f<float, 4>": "k_decode_f<float>", "k_decode_f<float": "k_decode_f<float>",
            "f32k::k_syrk<true": "f32k::k_syrk<true>", "k_syrk256<1, false>": "f32w::k_syrk256",
            "k_syrk256<1, true>": "f32w::k_syrk256<local>", "k_syrk256d<false": "f32w::k_syrk256d",
            "k_syrk256d<true": "f32w::k_syrk256d<local>", "k_snp_stats<float>": "k_snp_stats<float>"}
