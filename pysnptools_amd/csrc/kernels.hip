@@ -437,6 +437,51 @@ __global__ __launch_bounds__(kBlock) void k_repack(const uint8_t* __restrict__ s
     }
 }
 
+// iid gather with the source column staged in LDS (one 1024-thread workgroup per SNP): the
+// column is read from HBM once with 16-B loads, every output word gathers its 16 codes from
+// LDS (ds_read_u8) through a 32-bit copy of the index list, and the output words are written
+// coalesced.  k_repack above (per-thread global byte gathers, 64-bit indices) is the fallback
+// for columns > 150 KiB.
+__global__ void k_idx_to_u32(const uint64_t* __restrict__ idx, uint64_t n, uint32_t* __restrict__ out) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+        out[i] = (uint32_t)idx[i];
+}
+
+__global__ __launch_bounds__(1024) void k_repack_lds(const uint8_t* __restrict__ src, uint64_t sp, uint64_t nq,
+                                                     const uint32_t* __restrict__ idx, uint64_t n_out,
+                                                     uint8_t* __restrict__ dst, uint64_t dp) {
+    extern __shared__ u32x4_t colq[];
+    const uint64_t j = blockIdx.x;
+    const u32x4_t* s = reinterpret_cast<const u32x4_t*>(src + j * sp);
+    for (uint64_t q = threadIdx.x; q < nq; q += 1024) colq[q] = __builtin_nontemporal_load(s + q);
+    __syncthreads();
+    const uint8_t* cb = reinterpret_cast<const uint8_t*>(colq);
+    uint32_t* o = reinterpret_cast<uint32_t*>(dst + j * dp);
+    const uint64_t nd = (n_out + 15) / 16;
+    for (uint64_t d = threadIdx.x; d < nd; d += 1024) {
+        const uint64_t r0 = 16 * d;
+        uint32_t w = 0;
+        if (r0 + 16 <= n_out) {
+            const u32x4_t* ip = reinterpret_cast<const u32x4_t*>(idx + r0);
+#pragma unroll
+            for (int v = 0; v < 4; v++) {
+                const u32x4_t ii = ip[v];
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const uint32_t i = ii[k];
+                    w |= (uint32_t)((cb[i >> 2] >> (2 * (i & 3))) & 3u) << (2 * (4 * v + k));
+                }
+            }
+        } else {
+            for (int k = 0; r0 + k < n_out; k++) {
+                const uint32_t i = idx[r0 + k];
+                w |= (uint32_t)((cb[i >> 2] >> (2 * (i & 3))) & 3u) << (2 * k);
+            }
+        }
+        o[d] = w;
+    }
+}
+
 // ------------------------------------------------------------------ dense standardize
 template <typename T>
 __device__ __forceinline__ T apply_one(T x, double mean, double sd, int is_beta, double w, bool zero_col) {
@@ -903,13 +948,26 @@ void launch_decode_std_fused(const uint8_t* packed, uint64_t pitch, uint64_t n, 
     SNPMI_LAUNCH_CHECK();
 }
 
-void launch_repack(const uint8_t* src, uint64_t src_pitch, uint64_t, const uint64_t* idx, uint64_t n_out,
-                   uint64_t n_sid, uint8_t* dst, uint64_t dst_pitch, int*, hipStream_t st) {
+void launch_idx_u32(const uint64_t* idx, uint64_t n, uint32_t* out, hipStream_t st) {
+    if (n == 0) return;
+    k_idx_to_u32<<<grid_for(n, kBlock, 4096), kBlock, 0, st>>>(idx, n, out);
+    SNPMI_LAUNCH_CHECK();
+}
+
+void launch_repack(const uint8_t* src, uint64_t src_pitch, uint64_t n_src, const uint64_t* idx, const uint32_t* idx32,
+                   uint64_t n_out, uint64_t n_sid, uint8_t* dst, uint64_t dst_pitch, hipStream_t st) {
     if (n_sid == 0) return;
     SNPMI_HIP(hipMemsetAsync(dst, 0, n_sid * dst_pitch, st));
     if (n_out == 0) return;
-    const unsigned g = grid_for(ceil_div(n_out, 16) * n_sid, kBlock);
-    k_repack<<<g, kBlock, 0, st>>>(src, src_pitch, idx, n_out, n_sid, dst, dst_pitch);
+    const uint64_t nq = ceil_div(ceil_div(n_src, 4), 16);  // 16-B words of a source column
+    if (idx32 != nullptr && nq * 16 <= kLdsColMax && src_pitch % 16 == 0 && n_sid < (1ull << 31)) {
+        SNPMI_HIP(hipFuncSetAttribute((const void*)k_repack_lds, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      (int)kLdsColMax));
+        k_repack_lds<<<(unsigned)n_sid, 1024, nq * 16, st>>>(src, src_pitch, nq, idx32, n_out, dst, dst_pitch);
+    } else {
+        const unsigned g = grid_for(ceil_div(n_out, 16) * n_sid, kBlock);
+        k_repack<<<g, kBlock, 0, st>>>(src, src_pitch, idx, n_out, n_sid, dst, dst_pitch);
+    }
     SNPMI_LAUNCH_CHECK();
 }
 

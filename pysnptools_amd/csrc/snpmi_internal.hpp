@@ -65,7 +65,7 @@ struct Device {
     int cu_count = 0;
     // grow-only scratch slots
     enum Slot { S_PACKED, S_PACKED2, S_IDX, S_IDX2, S_LUT, S_STATS, S_OUT, S_TILES, S_K, S_DENSE,
-                S_DENSE2, S_RED, S_SESSION, S_PACKED_B, S_ZBLK, S_NUM };
+                S_DENSE2, S_RED, S_SESSION, S_PACKED_B, S_ZBLK, S_IDX32, S_NUM };
     void* buf[S_NUM] = {};
     hipEvent_t staged[2] = {};  // recorded after the H2D that last read pinned slot 0 / 1
     size_t cap[S_NUM] = {};
@@ -91,8 +91,9 @@ void launch_decode(const uint8_t* packed, uint64_t pitch, uint64_t n_iid, uint64
 void launch_decode_std_fused(const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m, int count_a1,
                              int std_kind, double a, double b, int use_stats, void* stats, void* lut, void* out,
                              uint64_t ld, hipStream_t st);
-void launch_repack(const uint8_t* src, uint64_t src_pitch, uint64_t n_src, const uint64_t* idx, uint64_t n_out,
-                   uint64_t n_sid, uint8_t* dst, uint64_t dst_pitch, int* err_flag, hipStream_t st);
+void launch_idx_u32(const uint64_t* idx, uint64_t n, uint32_t* out, hipStream_t st);
+void launch_repack(const uint8_t* src, uint64_t src_pitch, uint64_t n_src, const uint64_t* idx, const uint32_t* idx32,
+                   uint64_t n_out, uint64_t n_sid, uint8_t* dst, uint64_t dst_pitch, hipStream_t st);
 void launch_dense_standardize(void* val, uint64_t rows, uint64_t cols, uint64_t ld, int order_c, int dtype,
                               int std_kind, double a, double b, int use_stats, void* stats, hipStream_t st);
 void launch_subset(const void* in, int in_dt, uint64_t rows, uint64_t cols, uint64_t k, int in_order_c,

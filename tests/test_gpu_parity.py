@@ -582,3 +582,24 @@ def test_fused_decode_standardize_equals_two_kernels(n, kind, use_stats, count_a
         exp, est = O.decode_standardize(np.ascontiguousarray(host[:, :(n + 3) // 4]).reshape(-1), n, m,
                                         count_A1=bool(count_a1), dtype=np.float32)
         assert np.array_equal(outs[1][0].T, exp) and np.array_equal(outs[1][2], est)
+
+
+@pytest.mark.parametrize("n,m", [(20_011, 40), (700_003, 3)])
+def test_dev_repack_random_gather(n, m):
+    """snpmi_dev_repack (LDS-staged column; > 150 KiB columns take the global-gather fallback):
+    repacked codes decode to the source codes at the gathered iids, pad bits zero."""
+    buf, pitch = synth_dev(n, m, 17)
+    rng = np.random.default_rng(n)
+    idx = rng.choice(n, size=n // 3, replace=True).astype(np.uint64)
+    n_out = len(idx)
+    pitch_out = N.lib().snpmi_packed_pitch(n_out)
+    didx, dst = Dev(n_out * 8), Dev(pitch_out * m)
+    didx.put(idx)
+    N.call("snpmi_dev_repack", buf.p, pitch, n, didx.p, n_out, m, dst.p, pitch_out)
+    src = buf.get(np.empty((m, pitch), dtype=np.uint8))
+    got = dst.get(np.empty((m, pitch_out), dtype=np.uint8))
+    full = O.decode(np.ascontiguousarray(src[:, :(n + 3) // 4]).reshape(-1), n, m, dtype=np.int8)
+    sub = O.decode(np.ascontiguousarray(got[:, :(n_out + 3) // 4]).reshape(-1), n_out, m, dtype=np.int8)
+    assert np.array_equal(sub, full[idx.astype(np.int64)])
+    if n_out % 4:
+        assert np.all((got[:, n_out // 4] >> (2 * (n_out % 4))) == 0)

@@ -55,6 +55,54 @@ def decode(args):
                           "GBps": nbytes / t / 1e6, "frac_8TBs": nbytes / t / 1e6 / 8000}))
 
 
+def decode_c(args):
+    """C-order decode (k_decode_c): out[i][j], ld = m; the same bytes as the F-order decode."""
+    n, m = args.n, args.m
+    pitch = N.lib().snpmi_packed_pitch(n)
+    packed = Dev(N, pitch * m)
+    synth(N, packed.p, pitch, n, 0, m, 3, 0.01)
+    lut, st, out = Dev(N, m * 16), Dev(N, m * 8), Dev(N, m * n * 4)
+    N.call("snpmi_dev_snp_stats", packed.p, pitch, n, m, 0, N.STD_UNIT, 0.0, 0.0, 0, N.DT_F32, st.p, lut.p)
+    variants = [int(v) for v in args.variants.split(",")]
+    ev = Events(N, 2)
+    res = {v: [] for v in variants}
+    for rnd in range(args.rounds):
+        for v in variants:
+            N.call("snpmi_set_kernel_variant", b"decode", v)
+            ev.record(0)
+            N.call("snpmi_dev_decode", packed.p, pitch, n, m, lut.p, N.DT_F32, 1, out.p, m)
+            ev.record(1)
+            res[v].append(ev.ms(0, 1))
+    N.call("snpmi_set_kernel_variant", b"decode", 0)
+    nbytes = m * ((n + 3) // 4 + 4 * n)
+    for v in variants:
+        t = np.median(res[v])
+        print(json.dumps({"kernel": "decode_c", "variant": v, "n": n, "m": m, "median_ms": t, "GBps": nbytes / t / 1e6,
+                          "frac_8TBs": nbytes / t / 1e6 / 8000}))
+
+
+def repack(args):
+    """iid gather of packed columns (k_repack): every other iid, reversed."""
+    n, m = args.n, args.m
+    pitch = N.lib().snpmi_packed_pitch(n)
+    idx = np.arange(n - 1, -1, -2, dtype=np.uint64)
+    n_out = len(idx)
+    pitch_out = N.lib().snpmi_packed_pitch(n_out)
+    packed, dst, didx = Dev(N, pitch * m), Dev(N, pitch_out * m), Dev(N, n_out * 8)
+    synth(N, packed.p, pitch, n, 0, m, 3, 0.01)
+    N.call("snpmi_memcpy_h2d", didx.p, N.ptr(idx), idx.nbytes)
+    ev = Events(N, 2)
+    ts = []
+    for rnd in range(args.rounds):
+        ev.record(0)
+        N.call("snpmi_dev_repack", packed.p, pitch, n, didx.p, n_out, m, dst.p, pitch_out)
+        ev.record(1)
+        ts.append(ev.ms(0, 1))
+    t = np.median(ts)
+    nbytes = m * ((n + 3) // 4 + (n_out + 3) // 4)
+    print(json.dumps({"kernel": "repack", "n": n, "n_out": n_out, "m": m, "median_ms": t, "GBps": nbytes / t / 1e6}))
+
+
 def syrk_dense(args):
     """decode the block to f32/f64 in HBM (ld = round_up(n,256)) + dense-loader SYRK."""
     n, m = args.n, args.m
@@ -148,4 +196,4 @@ if __name__ == "__main__":
     if a.set_variant:
         k, v = a.set_variant.split("=")
         N.call("snpmi_set_kernel_variant", k.encode(), int(v))
-    {"decode": decode, "syrk": syrk, "syrk_dense": syrk_dense}[a.what](a)
+    {"decode": decode, "decode_c": decode_c, "repack": repack, "syrk": syrk, "syrk_dense": syrk_dense}[a.what](a)
