@@ -374,9 +374,11 @@ static void bed_read_impl(const char* path, uint64_t n_iid, uint64_t n_sid, int 
                 d2h_rows(d, out + c0 * n_out, n_out * sizeof(T), dev_out, ldF * sizeof(T), n_out * sizeof(T), cnt,
                          nthreads);
             } else {
-                T* dev_out = (T*)d.get(Device::S_OUT, cnt * n_out * sizeof(T));
-                launch_decode(packed, p.pitch_out, n_out, cnt, lut, dt, 1, dev_out, cnt, d.stream);
-                d2h_rows(d, out + c0, m_out * sizeof(T), dev_out, cnt * sizeof(T), cnt * sizeof(T), n_out, nthreads);
+                // rows padded to 16 B on the device (k_decode_c_reg vector stores), tight on the host
+                const uint64_t ldc = sizeof(T) < 4 ? cnt : round_up(cnt, 16 / sizeof(T));
+                T* dev_out = (T*)d.get(Device::S_OUT, ldc * n_out * sizeof(T));
+                launch_decode(packed, p.pitch_out, n_out, cnt, lut, dt, 1, dev_out, ldc, d.stream);
+                d2h_rows(d, out + c0, m_out * sizeof(T), dev_out, ldc * sizeof(T), cnt * sizeof(T), n_out, nthreads);
             }
         }
         if (std_kind != SNPMI_STD_NONE && !use_stats)

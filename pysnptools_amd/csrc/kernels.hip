@@ -414,6 +414,71 @@ __global__ __launch_bounds__(kBlock) void k_decode_c(const uint8_t* __restrict__
     }
 }
 
+// C order, register-resident codes: one wave per tile of 256 iids x (64*V) SNPs (V = 16 bytes /
+// sizeof(T): 4 f32 or 2 f64 SNPs per lane).  Each lane loads the 64-byte code segments of its
+// V SNPs (256 iids each) into registers, then walks the 256 rows: per row it extracts V codes
+// and writes one 16-byte vector, so every store instruction of the wave covers 1 KiB of one
+// output row.  No LDS, no barriers.  Needs ld % V == 0 (16-B aligned rows).
+template <typename T, bool ROWMAJOR = false>
+__global__ __launch_bounds__(kBlock) void k_decode_c_reg(const uint8_t* __restrict__ packed, uint64_t pitch,
+                                                         uint64_t n, uint64_t m, const T* __restrict__ lut,
+                                                         T* __restrict__ out, uint64_t ld) {
+    constexpr int V = 16 / sizeof(T);
+    typedef T vec_t __attribute__((ext_vector_type(V)));
+    const int lane = threadIdx.x & (kWave - 1);
+    const uint64_t ti_n = (n + 255) / 256, tj_n = (m + 64 * V - 1) / (64 * V);
+    const uint64_t nwaves = (uint64_t)gridDim.x * (kBlock / kWave);
+    for (uint64_t it = (uint64_t)blockIdx.x * (kBlock / kWave) + threadIdx.x / kWave; it < ti_n * tj_n; it += nwaves) {
+        // ROWMAJOR: consecutive waves take neighbouring SNP ranges of the same 256 rows, so the
+        // stores in flight cover whole output rows (DRAM page locality) instead of 1 KiB pieces
+        // of many rows
+        const uint64_t tj = ROWMAJOR ? it % tj_n : it / ti_n, ti = ROWMAJOR ? it / tj_n : it - tj * ti_n;
+        const uint64_t i0 = ti * 256, jl = tj * 64 * V + (uint64_t)V * lane;
+        uint32_t w[V][16];
+        T l[V][4];
+#pragma unroll
+        for (int v = 0; v < V; v++) {
+            const uint64_t j = jl + v;
+            if (j < m) {
+                const u32x4_t* c = reinterpret_cast<const u32x4_t*>(packed + j * pitch + i0 / 4);
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const u32x4_t x = c[q];  // pitch % 64 == 0: the 64 bytes are inside the column
+                    w[v][4 * q] = x[0], w[v][4 * q + 1] = x[1], w[v][4 * q + 2] = x[2], w[v][4 * q + 3] = x[3];
+                }
+#pragma unroll
+                for (int k = 0; k < 4; k++) l[v][k] = lut[4 * j + k];
+            } else {
+#pragma unroll
+                for (int q = 0; q < 16; q++) w[v][q] = 0;
+#pragma unroll
+                for (int k = 0; k < 4; k++) l[v][k] = (T)0;
+            }
+        }
+        const bool full = jl + V <= m;
+        const uint64_t rows = n - i0 < 256 ? n - i0 : 256;
+#pragma unroll
+        for (int q = 0; q < 16; q++) {
+#pragma unroll
+            for (int e = 0; e < 16; e++) {
+                const uint64_t r = 16 * q + e;
+                if (r < rows) {
+                    vec_t o;
+#pragma unroll
+                    for (int v = 0; v < V; v++) o[v] = sel4(l[v][0], l[v][1], l[v][2], l[v][3], (w[v][q] >> (2 * e)) & 3u);
+                    T* dst = out + (i0 + r) * ld + jl;
+                    if (full) {
+                        store_nt(reinterpret_cast<vec_t*>(dst), o);
+                    } else {
+                        for (int v = 0; v < V; v++)
+                            if (jl + v < m) dst[v] = o[v];
+                    }
+                }
+            }
+        }
+    }
+}
+
 // ------------------------------------------------------------------ iid gather (repack)
 __global__ __launch_bounds__(kBlock) void k_repack(const uint8_t* __restrict__ src, uint64_t sp,
                                                    const uint64_t* __restrict__ idx, uint64_t n_out, uint64_t m,
@@ -918,6 +983,24 @@ void launch_decode(const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m
         else
             k_decode_f<int8_t, 4><<<g, kBlock, 0, st>>>(packed, pitch, n, m, (const int8_t*)lut, (int8_t*)out, ld);
     } else {
+        if (dtype != SNPMI_DT_I8 && g_variant_decode != 2 && ld % (16 / dtype_size(dtype)) == 0 &&
+            reinterpret_cast<uintptr_t>(out) % 16 == 0 && pitch % 64 == 0) {
+            const uint64_t V = 16 / dtype_size(dtype);
+            const uint64_t waves = ceil_div(n, 256) * ceil_div(m, 64 * V);
+            const unsigned g = grid_for(waves, kBlock / kWave, 256 * 16);
+            // tools/ubench.py decode_c: row tiles fastest 5.51 TB/s at 100k x 16384 (row-major order
+            // 4.97, the 64x64 LDS-tile kernel 4.51); all three ~4.4 at 500k x 4096
+            if (dtype == SNPMI_DT_F32 && g_variant_decode == 3)
+                k_decode_c_reg<float, true><<<g, kBlock, 0, st>>>(packed, pitch, n, m, (const float*)lut, (float*)out, ld);
+            else if (dtype == SNPMI_DT_F32)
+                k_decode_c_reg<float, false><<<g, kBlock, 0, st>>>(packed, pitch, n, m, (const float*)lut, (float*)out,
+                                                                   ld);
+            else
+                k_decode_c_reg<double, false><<<g, kBlock, 0, st>>>(packed, pitch, n, m, (const double*)lut,
+                                                                    (double*)out, ld);
+            SNPMI_LAUNCH_CHECK();
+            return;
+        }
         const uint64_t tiles = ceil_div(n, 64) * ceil_div(m, 64);
         const unsigned g = grid_for(tiles, 1, 256 * 8);
         if (dtype == SNPMI_DT_F32)
