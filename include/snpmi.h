@@ -171,6 +171,14 @@ int snpmi_grm_add_bed_f64(const char* path, uint64_t n_iid, uint64_t n_sid, int 
 int snpmi_grm_session_tiles(void** tiles, uint64_t* count);   /* device tiles + element count */
 int snpmi_grm_end(int diag_k_to_n, double* factor, void* K_out);
 int snpmi_diag_k_to_n_f32(float* K, uint64_t n, double* factor);
+/* SNP-side DiagKtoN (standardizer/diag_K_to_N.py:75-95): factor = rows / sum(val^2) (f64
+ * accumulation); val *= sqrt(factor) unless |factor - 1| <= 1e-15.  val is any contiguous
+ * rows x cols array (order does not matter). */
+int snpmi_diag_k_to_n_snps_f32(float* val, uint64_t rows, uint64_t cols, double* factor);
+int snpmi_diag_k_to_n_snps_f64(double* val, uint64_t rows, uint64_t cols, double* factor);
+/* val[i] *= scale for a contiguous host array (DiagKtoNTrained.standardize, diag_K_to_N.py:101-159) */
+int snpmi_scale_f32(float* val, uint64_t count, double scale);
+int snpmi_scale_f64(double* val, uint64_t count, double scale);
 int snpmi_diag_k_to_n_f64(double* K, uint64_t n, double* factor);
 
 /* ---------------------------------------------------------------- device-resident API

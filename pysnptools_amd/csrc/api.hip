@@ -700,6 +700,34 @@ static void diag_k_to_n_impl(T* K, uint64_t n, double* factor) {
     }
 }
 
+// SNP-side DiagKtoN (diag_K_to_N.py:75-95): factor = rows / sum(val^2); val *= sqrt(factor)
+// when |factor - 1| > 1e-15.  scale_only: val *= scale (trained DiagKtoN / kernel rescale).
+template <typename T>
+static void snp_scale_impl(T* val, uint64_t count, double rows, int scale_only, double scale, double* factor) {
+    std::lock_guard<std::recursive_mutex> lk(g_call_mutex);
+    if (count == 0) {
+        if (factor) *factor = rows / 0.0;
+        return;
+    }
+    Device& d = device();
+    T* dv = (T*)d.get(Device::S_DENSE, count * sizeof(T));
+    SNPMI_HIP(hipMemcpyAsync(dv, val, count * sizeof(T), hipMemcpyHostToDevice, d.stream));
+    double s = scale;
+    if (!scale_only) {
+        double* ss = (double*)d.get(Device::S_RED, 64);
+        launch_sumsq(dv, count, DT<T>::v, ss, d.stream);
+        double sum = 0;
+        SNPMI_HIP(hipMemcpyAsync(&sum, ss, 8, hipMemcpyDeviceToHost, d.stream));
+        SNPMI_HIP(hipStreamSynchronize(d.stream));
+        const double f = rows / sum;
+        if (factor) *factor = f;
+        if (!(std::fabs(f - 1.0) > 1e-15)) return;
+        s = std::sqrt(f);
+    }
+    launch_dense_scale(dv, count, DT<T>::v, s, d.stream);
+    d2h_bytes(d, val, dv, count * sizeof(T), resolve_threads(0));
+}
+
 }  // namespace snpmi
 
 // ====================================================================== exported C ABI
@@ -939,6 +967,18 @@ int snpmi_grm_dense_f32(const float* val, uint64_t rows, uint64_t cols, int orde
 int snpmi_grm_dense_f64(const double* val, uint64_t rows, uint64_t cols, int order_c, int std_kind, double a,
                         double b, int use_stats, double* stats, int diag, double* factor, double* K_out) {
     return guarded([&] { grm_dense_impl<double>(val, rows, cols, order_c, std_kind, a, b, use_stats, stats, diag, factor, K_out); });
+}
+int snpmi_diag_k_to_n_snps_f32(float* val, uint64_t rows, uint64_t cols, double* factor) {
+    return guarded([&] { snp_scale_impl<float>(val, rows * cols, (double)rows, 0, 1.0, factor); });
+}
+int snpmi_diag_k_to_n_snps_f64(double* val, uint64_t rows, uint64_t cols, double* factor) {
+    return guarded([&] { snp_scale_impl<double>(val, rows * cols, (double)rows, 0, 1.0, factor); });
+}
+int snpmi_scale_f32(float* val, uint64_t count, double scale) {
+    return guarded([&] { snp_scale_impl<float>(val, count, 0.0, 1, scale, nullptr); });
+}
+int snpmi_scale_f64(double* val, uint64_t count, double scale) {
+    return guarded([&] { snp_scale_impl<double>(val, count, 0.0, 1, scale, nullptr); });
 }
 int snpmi_diag_k_to_n_f32(float* K, uint64_t n, double* factor) {
     return guarded([&] { diag_k_to_n_impl<float>(K, n, factor); });

@@ -771,6 +771,26 @@ __global__ __launch_bounds__(kBlock) void k_scale(T* __restrict__ p, uint64_t co
         p[t] = (T)((double)p[t] * scale);
 }
 
+// sum of squares in f64 (SNP-side DiagKtoN, diag_K_to_N.py:75-95): grid-stride partial sums,
+// one f64 atomic per workgroup
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_sumsq(const T* __restrict__ p, uint64_t count, double* __restrict__ out) {
+    __shared__ double red[kBlock / kWave];
+    double s = 0;
+    for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < count; t += (uint64_t)gridDim.x * blockDim.x) {
+        const double x = (double)p[t];
+        s += x * x;
+    }
+    s = wave_sum_f64(s);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double t = 0;
+        for (int q = 0; q < kBlock / kWave; q++) t += red[q];
+        atomicAdd(out, t);
+    }
+}
+
 // ------------------------------------------------------------------ synthetic genotypes
 __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
     x += 0x9E3779B97F4A7C15ull;
@@ -1142,6 +1162,17 @@ void launch_dense_scale(void* p, uint64_t count, int dtype, double scale, hipStr
         k_scale<float><<<g, kBlock, 0, st>>>((float*)p, count, scale);
     else
         k_scale<double><<<g, kBlock, 0, st>>>((double*)p, count, scale);
+    SNPMI_LAUNCH_CHECK();
+}
+
+void launch_sumsq(const void* p, uint64_t count, int dtype, double* out_dev, hipStream_t st) {
+    SNPMI_HIP(hipMemsetAsync(out_dev, 0, sizeof(double), st));
+    if (count == 0) return;
+    const unsigned g = grid_for(count, kBlock, 1024);
+    if (dtype == SNPMI_DT_F32)
+        k_sumsq<float><<<g, kBlock, 0, st>>>((const float*)p, count, out_dev);
+    else
+        k_sumsq<double><<<g, kBlock, 0, st>>>((const double*)p, count, out_dev);
     SNPMI_LAUNCH_CHECK();
 }
 

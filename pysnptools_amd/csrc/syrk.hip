@@ -628,6 +628,7 @@ __global__ __launch_bounds__(512, 1) void k_syrk256d(const float* __restrict__ Z
     }
     epilogue<LOCAL>(acc, tiles, n, bi, bj, accumulate, lane, wm, wn, wg);
 }
+
 }  // namespace f32w
 
 // ====================================================================== f64
@@ -1044,6 +1045,7 @@ void launch_syrk_dense(const void* Z, uint64_t ldz, uint64_t n, uint64_t m, int 
             f32w::k_syrk256d<false, 16, 3><<<g, 512, 0, st>>>(Zf, ldz, n, m, Tf, accumulate);
         else if (n >= 4096 && ldz >= nb * 256 && g_variant_syrk == 21)
             f32w::k_syrk256d<false, 16, 2, true><<<g, 512, 0, st>>>(Zf, ldz, n, m, Tf, accumulate);
+
         else if (n >= 4096 && ldz >= nb * 256 && g_variant_syrk != 5)
             f32w::k_syrk256d<><<<g, 512, 0, st>>>(Zf, ldz, n, m, Tf, accumulate);
         else

@@ -1,7 +1,9 @@
 """DiagKtoN: scale so that trace(K) = N (reference standardizer/diag_K_to_N.py).
 
-On a kernel the trace and the scale run on the GPU (``snpmi_diag_k_to_n_*``); the fused
-GRM path applies it before K leaves the device (``snpmi_grm_*(..., diag_k_to_n=1)``).
+Every form runs on the GPU: on a kernel the trace and the scale (``snpmi_diag_k_to_n_*``;
+the fused GRM path applies it before K leaves the device), on SNP data the sum of squares and
+the sqrt(factor) scale (``snpmi_diag_k_to_n_snps_*``), and a trained factor through
+``snpmi_scale_*``.  Non-contiguous or non-float inputs are staged through a contiguous copy.
 """
 import warnings
 
@@ -11,20 +13,36 @@ from pysnptools_amd import _native as N
 from pysnptools_amd.standardizer.standardizer import Standardizer
 
 
+def _float_work(val):
+    """(contiguous float32/float64 array to operate on, whether it is a copy)."""
+    if val.dtype in (np.float32, np.float64) and (val.flags["C_CONTIGUOUS"] or val.flags["F_CONTIGUOUS"]):
+        return val, False
+    return np.ascontiguousarray(val, dtype=val.dtype if val.dtype in (np.float32, np.float64) else np.float64), True
+
+
+def _factor_ptr(f):
+    return f.ctypes.data_as(N.ctypes.POINTER(N.ctypes.c_double))
+
+
 def _scale_kernel_inplace(kerneldata):
     """factor = N / trace(K); K *= factor when |factor - 1| > 1e-15 (diag_K_to_N.py:54-64)."""
     val = kerneldata._val
     n = val.shape[0]
-    if val.dtype in (np.float32, np.float64) and val.shape == (n, n) and (val.flags["C_CONTIGUOUS"] or val.flags["F_CONTIGUOUS"]):
-        f = np.zeros(1, dtype=np.float64)
-        fn = "snpmi_diag_k_to_n_" + N.suffix(val.dtype)
-        # trace and scale are layout independent for a square matrix held contiguously
-        N.call(fn, N.ptr(val), n, f.ctypes.data_as(N.ctypes.POINTER(N.ctypes.c_double)))
-        return float(f[0])
-    factor = float(kerneldata.iid_count) / np.diag(val).sum()
-    if abs(factor - 1.0) > 1e-15:
-        kerneldata._val *= factor
-    return factor
+    assert val.shape == (n, n), "DiagKtoN expects a square kernel"
+    work, copied = _float_work(val)
+    f = np.zeros(1, dtype=np.float64)
+    # trace and scale are layout independent for a square matrix held contiguously
+    N.call("snpmi_diag_k_to_n_" + N.suffix(work.dtype), N.ptr(work), n, _factor_ptr(f))
+    if copied:
+        val[...] = work
+    return float(f[0])
+
+
+def _scale_inplace(val, scale):
+    work, copied = _float_work(val)
+    N.call("snpmi_scale_" + N.suffix(work.dtype), N.ptr(work), work.size, float(scale))
+    if copied:
+        val[...] = work
 
 
 class DiagKtoN(Standardizer):
@@ -51,11 +69,19 @@ class DiagKtoN(Standardizer):
         return self._standardize_snps(input, return_trained=return_trained)
 
     def _standardize_snps(self, snps, return_trained=False, force_python_only=False, num_threads=None):
-        val = snps.val if hasattr(snps, "val") else snps
-        squared_sum = float(np.vdot(val.reshape(-1, order="A"), val.reshape(-1, order="A")))
-        factor = float(val.shape[0]) / squared_sum
-        if abs(factor - 1.0) > 1e-15:
-            val *= np.sqrt(factor)
+        """factor = rows / sum(val^2); val *= sqrt(factor) (diag_K_to_N.py:75-95), on the GPU."""
+        if hasattr(snps, "val"):
+            val = snps.val
+        else:
+            warnings.warn("standardizing an nparray instead of a SnpData is deprecated", DeprecationWarning)
+            val = snps
+        work, copied = _float_work(val)
+        f = np.zeros(1, dtype=np.float64)
+        N.call("snpmi_diag_k_to_n_snps_" + N.suffix(work.dtype), N.ptr(work), work.shape[0],
+               int(np.prod(work.shape[1:])), _factor_ptr(f))
+        if copied:
+            val[...] = work
+        factor = float(f[0])
         return (snps, DiagKtoNTrained(factor)) if return_trained else snps
 
 
@@ -76,9 +102,9 @@ class DiagKtoNTrained(Standardizer):
 
         if isinstance(input, KernelReader) and hasattr(input, "val"):
             if not self.is_constant:
-                input._val *= self.factor
+                _scale_inplace(input._val, self.factor)
         else:
             val = input.val if hasattr(input, "val") else input
             if not self.is_constant:
-                val *= np.sqrt(self.factor)
+                _scale_inplace(val, np.sqrt(self.factor))
         return (input, self) if return_trained else input

@@ -603,3 +603,54 @@ def test_dev_repack_random_gather(n, m):
     assert np.array_equal(sub, full[idx.astype(np.int64)])
     if n_out % 4:
         assert np.all((got[:, n_out // 4] >> (2 * (n_out % 4))) == 0)
+
+
+def test_diag_k_to_n_snp_side_and_trained():
+    """test.py:204-218: DiagKtoN on SNP data gives trace(Z Z^T) = N; the trained factor
+    re-applies it; kernel side on a non-contiguous view is staged through a copy."""
+    from pysnptools_amd.standardizer import DiagKtoN, DiagKtoNTrained
+
+    np.random.seed(42)
+    m = np.random.random((100, 1000))
+    ref_factor = 100.0 / m.reshape(-1).dot(m.reshape(-1))
+    with pytest.warns(DeprecationWarning):
+        _, tr = DiagKtoN()._standardize_snps(m, return_trained=True)
+    np.testing.assert_almost_equal(100, np.sum(np.diag(m.dot(m.T))))
+    assert abs(tr.factor - ref_factor) < 1e-12 * ref_factor
+    for dtype in (np.float32, np.float64):
+        d = SnpData(iid=[["a", str(i)] for i in range(100)], sid=["s%d" % j for j in range(1000)],
+                    val=np.random.random((100, 1000)).astype(dtype))
+        v0 = d.val.copy()
+        d.standardize(DiagKtoN())
+        assert abs(np.trace(d.val.astype(np.float64).dot(d.val.T.astype(np.float64))) - 100) < 1e-3
+        again = SnpData(iid=d.iid, sid=d.sid, val=v0)
+        f = 100.0 / float(np.vdot(v0.astype(np.float64), v0.astype(np.float64)))
+        DiagKtoNTrained(f).standardize(again)
+        np.testing.assert_allclose(again.val, d.val, rtol=1e-6 if dtype == np.float32 else 1e-13)
+    K = np.random.random((60, 60))
+    K = K.dot(K.T)
+    kd = KernelData(iid=[["a", str(i)] for i in range(60)], val=K.copy())
+    kd.standardize()
+    np.testing.assert_allclose(np.trace(kd.val), 60, rtol=1e-12)
+
+
+@pytest.mark.parametrize("std,a,b", [(Unit(), 0, 0), (Beta(1, 25), 1, 25)])
+@pytest.mark.parametrize("dtype,tol", [(np.float64, 1e-10), (np.float32, 1e-5)])
+@pytest.mark.parametrize("order", ["F", "C"])
+def test_nancnc_and_reversed_subsets_vs_python_path(std, a, b, dtype, tol, order):
+    """NaNCNCTestCases (test.py:1201-1358) + load_and_standardize (test.py:642-651, 812-862):
+    reversed iid/sid subsets, NaN at [0,0], a constant (SNC) column 1 -> both standardize to 0,
+    and the rest matches the reference's Python path (restated by the oracle)."""
+    b300 = bed("n300")
+    for iids in (None, np.arange(299, 0, -2), np.array([5, 0, 17, 299, 150])):
+        for sids in (None, np.arange(1014, 0, -2), np.array([3, 1, 400])):
+            r = b300 if iids is None else b300[iids, :]
+            r = r if sids is None else r[:, sids]
+            d = r.read(order=order, dtype=dtype)
+            d.val[0, 0] = np.nan
+            d.val[:, 1] = 1.0
+            exp = np.array(d.val, dtype=np.float64, order=order)
+            O.standardize_python(exp, is_beta=isinstance(std, Beta), a=a, b=b)
+            d.standardize(std)
+            assert d.val[0, 0] == 0 and np.all(d.val[:, 1] == 0)
+            rel_close(d.val, exp, tol)
