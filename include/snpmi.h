@@ -168,6 +168,9 @@ int snpmi_grm_add_bed_f64(const char* path, uint64_t n_iid, uint64_t n_sid, int 
                           const uint64_t* iid_idx, uint64_t n_out_iid, const uint64_t* sid_idx,
                           uint64_t n_out_sid, int std_kind, double a, double b, int use_stats,
                           double* stats, int num_threads);
+/* add Z Z^T of an already standardized rows x cols block (F or C order) to the session */
+int snpmi_grm_add_dense_f32(const float* val, uint64_t rows, uint64_t cols, int order_c);
+int snpmi_grm_add_dense_f64(const double* val, uint64_t rows, uint64_t cols, int order_c);
 int snpmi_grm_session_tiles(void** tiles, uint64_t* count);   /* device tiles + element count */
 int snpmi_grm_end(int diag_k_to_n, double* factor, void* K_out);
 int snpmi_diag_k_to_n_f32(float* K, uint64_t n, double* factor);

@@ -728,6 +728,33 @@ static void snp_scale_impl(T* val, uint64_t count, double rows, int scale_only, 
     d2h_bytes(d, val, dv, count * sizeof(T), resolve_threads(0));
 }
 
+// Z Z^T of an already standardized dense block (rows = iids, cols = SNPs, F or C) added to the
+// session's tiles: the generic SnpReader._read_kernel block loop (snpreader.py:651-655) for
+// readers/standardizers the fused BED path does not cover, with K kept in HBM.
+template <typename T>
+static void grm_add_dense_impl(const T* val, uint64_t rows, uint64_t cols, int order_c) {
+    std::lock_guard<std::recursive_mutex> lk(g_call_mutex);
+    SNPMI_REQUIRE(g_session.active, SNPMI_E_ARG, "no GRM session (call snpmi_grm_begin)");
+    SNPMI_REQUIRE(g_session.dtype == DT<T>::v, SNPMI_E_ARG, "dtype differs from snpmi_grm_begin");
+    SNPMI_REQUIRE(rows == g_session.n, SNPMI_E_ARG, "iid count differs from snpmi_grm_begin");
+    SNPMI_REQUIRE(val != nullptr || rows == 0 || cols == 0, SNPMI_E_ARG, "val is NULL");
+    if (rows == 0 || cols == 0) return;
+    Device& d = device();
+    T* tiles = (T*)session_tiles(d);
+    const uint64_t ldz = round_up(rows, 256);
+    T* Z = (T*)d.get(Device::S_DENSE, ldz * cols * sizeof(T));
+    if (!order_c) {
+        SNPMI_HIP(hipMemcpy2DAsync(Z, ldz * sizeof(T), val, rows * sizeof(T), rows * sizeof(T), cols,
+                                   hipMemcpyHostToDevice, d.stream));
+    } else {
+        T* Zc = (T*)d.get(Device::S_DENSE2, rows * cols * sizeof(T));
+        SNPMI_HIP(hipMemcpyAsync(Zc, val, rows * cols * sizeof(T), hipMemcpyHostToDevice, d.stream));
+        launch_transpose_to_f(Zc, rows, cols, DT<T>::v, Z, ldz, d.stream);
+    }
+    launch_syrk_dense(Z, ldz, rows, cols, DT<T>::v, tiles, g_session.wrote ? 1 : 0, d.stream);
+    g_session.wrote = true;
+    SNPMI_HIP(hipStreamSynchronize(d.stream));
+}
 }  // namespace snpmi
 
 // ====================================================================== exported C ABI
@@ -889,6 +916,13 @@ int snpmi_grm_begin(uint64_t n_out_iid, int dtype) {
     }
 SNPMI_GRM_ADD(f32, float, SNPMI_DT_F32)
 SNPMI_GRM_ADD(f64, double, SNPMI_DT_F64)
+
+int snpmi_grm_add_dense_f32(const float* val, uint64_t rows, uint64_t cols, int order_c) {
+    return guarded([&] { grm_add_dense_impl<float>(val, rows, cols, order_c); });
+}
+int snpmi_grm_add_dense_f64(const double* val, uint64_t rows, uint64_t cols, int order_c) {
+    return guarded([&] { grm_add_dense_impl<double>(val, rows, cols, order_c); });
+}
 
 int snpmi_grm_session_tiles(void** tiles, uint64_t* count) {
     return guarded([&] {

@@ -120,28 +120,44 @@ class SnpReader(PstReader):
                 return K, trained, factor
             return (K, trained) if return_trained else K
         K, trained = self._read_kernel_blocks(standardizer, block_size, order, dtype, force_python_only, num_threads)
+        if isinstance(trained, _LazyMerge) and (return_trained or _diag_k_to_n):
+            trained = trained.merge()
         if _diag_k_to_n:
             return K, trained, None
         return (K, trained) if return_trained else K
 
     def _read_kernel_blocks(self, standardizer, block_size, order, dtype, force_python_only, num_threads):
         """The reference's generic loop (snpreader.py:629-668) for readers/standardizers the
-        fused path does not cover; each block's Z Z^T runs on the GPU."""
-        from pysnptools_amd import standardizer as stdizer
-
-        if block_size is None or self.sid_count <= block_size or self.sid_count <= self.iid_count:
-            data, trained = SnpReader._as_snpdata(self, standardizer, force_python_only, "A", dtype, num_threads)
-            K = data._read_kernel(stdizer.Identity(), order=order, dtype=dtype, view_ok=False, num_threads=num_threads)
-            return K, trained
-        K = np.zeros([self.iid_count, self.iid_count], dtype=dtype, order="C" if order == "A" else order)
+        fused path does not cover: each block is read + standardized, then its Z Z^T is added to
+        a K held in HBM (snpmi_grm_begin / add_dense / end) -- no host-side K +=."""
+        n = self.iid_count
+        if dtype not in (np.float32, np.float64):
+            raise ValueError("GRM dtype must be float32 or float64")
+        sfx = N.suffix(dtype)
+        # all at once unless the SNPs outnumber both the block and the iids (snpreader.py:629)
+        whole = block_size is None or self.sid_count <= block_size or self.sid_count <= self.iid_count
+        bs = self.sid_count if whole else block_size
+        K = np.empty((n, n), dtype=dtype)
         trained_list = []
-        logging.info("reading %d SNPs in blocks of %d", self.sid_count, block_size)
-        for start in range(0, self.sid_count, block_size):
-            data, trained = SnpReader._as_snpdata(self[:, start:start + block_size], standardizer, force_python_only,
-                                                  "A", dtype, num_threads)
-            trained_list.append(trained)
-            K += data._read_kernel(stdizer.Identity(), order=order, dtype=dtype, view_ok=False, num_threads=num_threads)
-        return K, standardizer._merge_trained(trained_list)
+        N.call("snpmi_grm_begin", n, N.dt_code(dtype))
+        try:
+            for start in range(0, self.sid_count, max(bs, 1)):
+                reader = self if (start == 0 and bs >= self.sid_count) else self[:, start:start + bs]
+                data, trained = SnpReader._as_snpdata(reader, standardizer, force_python_only, "A", dtype,
+                                                      num_threads)
+                trained_list.append(trained)
+                val = data.val
+                if not (val.flags["C_CONTIGUOUS"] or val.flags["F_CONTIGUOUS"]):
+                    val = np.asfortranarray(val)
+                order_c = 1 if val.flags["C_CONTIGUOUS"] and not val.flags["F_CONTIGUOUS"] else 0
+                N.call("snpmi_grm_add_dense_" + sfx, N.ptr(val), val.shape[0], val.shape[1], order_c)
+        finally:
+            N.call("snpmi_grm_end", 0, None, N.ptr(K))
+        if whole:
+            return (K.T if order == "F" else K), trained_list[0]
+        # merged lazily: the reference merges only when the trained standardizer is asked for
+        # (snpreader.py:666), and e.g. DiagKtoN cannot merge
+        return (K.T if order == "F" else K), _LazyMerge(standardizer, trained_list)
 
     def copyinputs(self, copier):
         raise NotImplementedError
@@ -155,6 +171,14 @@ class SnpReader(PstReader):
     @property
     def val_shape(self):
         return None
+
+
+class _LazyMerge(object):
+    def __init__(self, standardizer, trained_list):
+        self.standardizer, self.trained_list = standardizer, trained_list
+
+    def merge(self):
+        return self.standardizer._merge_trained(self.trained_list)
 
 
 # ---------------------------------------------------------------------- native dispatch

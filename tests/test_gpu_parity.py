@@ -654,3 +654,24 @@ def test_nancnc_and_reversed_subsets_vs_python_path(std, a, b, dtype, tol, order
             d.standardize(std)
             assert d.val[0, 0] == 0 and np.all(d.val[:, 1] == 0)
             rel_close(d.val, exp, tol)
+
+
+@pytest.mark.parametrize("block_size", [None, 100, 1015])
+@pytest.mark.parametrize("order", ["C", "F"])
+def test_generic_block_loop_keeps_k_on_device(block_size, order):
+    """snpreader.py:629-668 for a standardizer the fused path does not cover (SNP-side DiagKtoN):
+    per-block standardize, Z Z^T accumulated in HBM (snpmi_grm_add_dense_*)."""
+    from pysnptools_amd.standardizer import DiagKtoN
+
+    b = bed("n300")
+    K = b.read_kernel(DiagKtoN(), block_size=block_size, order=order, dtype=np.float64).val
+    full = from_i8(g("n300")["val_i8"])
+    full[np.isnan(full)] = 0  # n300 has no missing values; keeps the restatement simple
+    bs = 1015 if block_size is None else block_size
+    ref = np.zeros((300, 300))
+    for s0 in range(0, 1015, bs):
+        z = full[:, s0:s0 + bs].copy()
+        z *= np.sqrt(300.0 / z.reshape(-1).dot(z.reshape(-1)))
+        ref += z.dot(z.T)
+    grm_close(K, ref, 1e-10)
+    assert K.flags[order + "_CONTIGUOUS"]
