@@ -8,9 +8,11 @@ Metric (BASELINE.json): "SNPs/sec standardized (500k x 1M) + GRM GF/s at 1/2/4/8
                (weak scaling: per-GPU work fixed).  A step = one pass over the 1M SNPs.
   roofline   = the decode kernel (k_decode_f<float>), HBM bound: algorithmic bytes per launch =
                block * (ceil(N/4) + 4N) / its mean HIP-event duration, vs 8.0 TB/s.
-  grm        = SnpKernel GRM of configs[3] (50k iid x 500k SNP, Unit, block 10k, f32 MFMA): SNP
-               blocks round-robin over ranks, one RCCL all-reduce of the upper-triangle K tiles.
-               gflops uses N(N+1)M (SYRK work); roofline vs 157.3 TF FP32 MFMA.
+  grm        = SnpKernel GRM of configs[3] (50k iid x 500k SNP, Unit, block 10k, f32): SNP blocks
+               round-robin over ranks, one RCCL all-reduce of the upper-triangle K tiles.  The f32
+               products run on the bf16 MFMA pipe as 6 bf16 products of each value's exact bf16x3
+               split (f32 accuracy, f32 accumulate).  gflops uses N(N+1)M (SYRK work, SURVEY.md
+               §8d); roofline vs 2.5 PF bf16 dense / 6 = 416.7 TF (the f32-MFMA peak is 157.3).
   cpu_baseline = the oracle's C/OpenMP decode + one-pass Unit standardize (the CPU restatement
                of bed-reader's read + standardize_f32) on a sample of the same packed columns,
                rank 0 only; grm.cpu_baseline = NumPy/OpenBLAS Z.dot(Z.T) (snpreader.py:655).
@@ -32,6 +34,10 @@ sys.path.insert(0, ROOT)
 METRIC = "SNPs/sec standardized (500k×1M) + GRM GF/s at 1/2/4/8 GPUs"
 HBM_PEAK_GBS = 8000.0
 MFMA_F32_PEAK_TFLOPS = 157.3
+MFMA_BF16_PEAK_TFLOPS = 2500.0
+# f32 GRM on the bf16 MFMA pipe: each f32 product = 6 bf16 MFMA products of the bf16x3 split
+BF3_PRODUCTS = 6
+BF3_PEAK_TFLOPS = MFMA_BF16_PEAK_TFLOPS / BF3_PRODUCTS
 
 
 def parse():
@@ -321,7 +327,9 @@ def leg_grm(N, args, dist, rccl):
     tr = ctypes.c_double()
     N.call("snpmi_dev_grm_trace", tiles.p, n, N.DT_F32, ctypes.byref(tr))
     flops_full_block = n * (n + 1) * B
-    res = dict(wall=wall, syrk_ms=syrk_ms, allreduce_ms=allreduce_ms, trace=tr.value,
+    nb = (n + 255) // 256
+    exec_ratio = BF3_PRODUCTS * 2 * 256 * 256 * (nb * (nb + 1) // 2) / (n * (n + 1))  # executed bf16 / algorithmic
+    res = dict(wall=wall, syrk_ms=syrk_ms, allreduce_ms=allreduce_ms, trace=tr.value, exec_ratio=exec_ratio,
                mean_tflops=(flops_full_block / (np.mean(syrk_ms) * 1e-3) / 1e12) if syrk_ms else 0.0, nblocks=len(blocks))
     if dist.rank == 0 and not args.skip_cpu and my_m > 0:
         # parity sample (untimed): K rows 0..63 of the GRM of this rank's first 512 SNPs
@@ -495,11 +503,15 @@ def main():
                            "rank(s)%s" % (n, m, args.grm_block, dist.world, ", RCCL all-reduce of K tiles" if rccl else ""),
                "gflops": gf, "snps_per_s": m / r2["wall"], "seconds": r2["wall"], "scaling": "strong",
                "allreduce_ms": r2["allreduce_ms"], "trace_K": r2["trace"],
-               "roofline": {"bound": "mfma", "achieved": r2["mean_tflops"], "peak": MFMA_F32_PEAK_TFLOPS,
-                            "unit": "TFLOP/s", "frac": r2["mean_tflops"] / MFMA_F32_PEAK_TFLOPS,
-                            "traffic": pmc_traffic("f32w::k_syrk256d", "grm", n, args.grm_block),
-                            "kernel": "f32w::k_syrk256d<false,16,2> (time per block includes k_decode_f of the "
-                                      "block into Z, ~0.2%)", "per_launch_flops": n * (n + 1) * args.grm_block}}
+               "roofline": {"bound": "mfma", "achieved": r2["mean_tflops"], "peak": BF3_PEAK_TFLOPS,
+                            "unit": "TFLOP/s", "frac": r2["mean_tflops"] / BF3_PEAK_TFLOPS,
+                            "traffic": pmc_traffic("f32w::k_syrk_bf3", "grm", n, args.grm_block),
+                            "kernel": "f32w::k_syrk_bf3<false,true,1>: f32 GRM as 6 bf16 MFMA products of each "
+                                      "value's exact bf16x3 split, f32 accumulate (v_mfma_f32_32x32x16_bf16); "
+                                      "peak = 2.5 PF bf16 dense / 6; time per block includes k_lut_bf3",
+                            "per_launch_flops": n * (n + 1) * args.grm_block,
+                            "f32_mfma_peak": MFMA_F32_PEAK_TFLOPS,
+                            "mfma_util_executed": r2["mean_tflops"] * r2["exec_ratio"] / MFMA_BF16_PEAK_TFLOPS}}
     grm5 = None
     run5 = args.grm5 == "on" or (args.grm5 == "auto" and dist.world >= 4 and not args.skip_grm)
     if run5:
@@ -512,9 +524,10 @@ def main():
                 "h2d_ms": r3["h2d_ms"], "allgather_ms": r3["allgather_ms"], "syrk_ms": r3["syrk_ms"],
                 "gflops": gf5, "seconds": r3["wall"], "scaling": "strong",
                 "blocks_on_rank0": r3["n_local_blocks"], "K_bytes_per_rank": r3["n_local_blocks"] * 256 * 256 * 4,
-                "roofline": {"bound": "mfma", "achieved": gf5 / 1e3 / dist.world, "peak": MFMA_F32_PEAK_TFLOPS,
-                             "unit": "TFLOP/s per GPU", "frac": gf5 / 1e3 / dist.world / MFMA_F32_PEAK_TFLOPS,
-                             "traffic": None, "kernel": "f32w::k_syrk256d<true,16,2>"},
+                "roofline": {"bound": "mfma", "achieved": gf5 / 1e3 / dist.world, "peak": BF3_PEAK_TFLOPS,
+                             "unit": "TFLOP/s per GPU", "frac": gf5 / 1e3 / dist.world / BF3_PEAK_TFLOPS,
+                             "traffic": None, "kernel": "f32w::k_syrk_bf3<true,true,1> (bf16x3 split, 6 bf16 "
+                                                        "MFMA products, f32 accumulate; wall incl. H2D + all-gather)"},
                 "projected_seconds_1M_snps": r3["wall"] * 1_000_000 / m5}
         if r3.get("parity_sample") is not None:
             grm5["parity"] = grm5_parity(args, m5, *r3["parity_sample"])

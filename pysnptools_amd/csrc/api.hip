@@ -518,8 +518,27 @@ static void for_z_blocks(Device& d, const uint8_t* packed, uint64_t pitch, uint6
     }
 }
 
+// f32 GRM of packed SNPs: default = the bf16 MFMA pipe (k_syrk_bf3: bf16x3 split of each SNP's
+// f32 LUT, six bf16 products per f32 product, f32 accumulate): 309 TFLOP/s at N=50k, 10k SNPs
+// vs 136 for the f32-MFMA two-phase path (variant 20) -- tools/ubench.py syrk.
+// Variants: 30 = plain loader, 31 = + XCD remap, 39 = ablation (no loader); 4/5/20 = f32 MFMA.
+static bool use_bf3(int dt) {
+    return dt == SNPMI_DT_F32 && (g_variant_syrk == 0 || (g_variant_syrk >= 30 && g_variant_syrk < 40));
+}
+
+static const uint32_t* lut_bf3(Device& d, const float* lut, uint64_t m) {
+    uint32_t* l3 = (uint32_t*)d.get(Device::S_LUT3, lut_bf3_entries(m) * 32);
+    launch_lut_bf3(lut, m, l3, d.stream);
+    return l3;
+}
+
 static void syrk_packed_auto(Device& d, const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m,
                              const void* lut, int dt, void* tiles, int accumulate) {
+    if (use_bf3(dt)) {
+        launch_syrk_packed_bf3(packed, pitch, n, m, lut_bf3(d, (const float*)lut, m), (float*)tiles, accumulate,
+                               d.stream);
+        return;
+    }
     if (!use_two_phase(dt, n) || m == 0) {
         launch_syrk_packed(packed, pitch, n, m, lut, dt, tiles, accumulate, d.stream);
         return;
@@ -533,6 +552,11 @@ static void syrk_packed_auto(Device& d, const uint8_t* packed, uint64_t pitch, u
 
 static void syrk_packed_part_auto(Device& d, const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m,
                                   const float* lut, int rank, int world, void* blocks, int accumulate) {
+    if (use_bf3(SNPMI_DT_F32)) {
+        launch_syrk_packed_bf3_part(packed, pitch, n, m, lut_bf3(d, lut, m), rank, world, (float*)blocks, accumulate,
+                                    d.stream);
+        return;
+    }
     if (!use_two_phase(SNPMI_DT_F32, n) || m == 0) {
         launch_syrk_packed_part(packed, pitch, n, m, lut, rank, world, blocks, accumulate, d.stream);
         return;

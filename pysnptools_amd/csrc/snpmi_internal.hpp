@@ -65,7 +65,7 @@ struct Device {
     int cu_count = 0;
     // grow-only scratch slots
     enum Slot { S_PACKED, S_PACKED2, S_IDX, S_IDX2, S_LUT, S_STATS, S_OUT, S_TILES, S_K, S_DENSE,
-                S_DENSE2, S_RED, S_SESSION, S_PACKED_B, S_ZBLK, S_IDX32, S_NUM };
+                S_DENSE2, S_RED, S_SESSION, S_PACKED_B, S_ZBLK, S_IDX32, S_LUT3, S_NUM };
     void* buf[S_NUM] = {};
     hipEvent_t staged[2] = {};  // recorded after the H2D that last read pinned slot 0 / 1
     size_t cap[S_NUM] = {};
@@ -122,5 +122,12 @@ void launch_syrk_dense_part(const float* Z, uint64_t ldz, uint64_t n, uint64_t m
                             int accumulate, hipStream_t st);
 void launch_syrk_dense(const void* Z, uint64_t ldz, uint64_t n_iid, uint64_t n_sid, int dtype, void* tiles,
                        int accumulate, hipStream_t st);
+// f32 GRM on the bf16 MFMA pipe (bf16x3 split, f32 accuracy); lut3 = scratch of 32 B per SNP
+uint64_t lut_bf3_entries(uint64_t m);  // 8 u32 each, zero-padded to a multiple of the SYRK stage
+void launch_lut_bf3(const float* lut, uint64_t m, uint32_t* lut3, hipStream_t st);
+void launch_syrk_packed_bf3(const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m, const uint32_t* lut3,
+                            float* tiles, int accumulate, hipStream_t st);
+void launch_syrk_packed_bf3_part(const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m, const uint32_t* lut3,
+                                 int rank, int world, float* blocks, int accumulate, hipStream_t st);
 
 }  // namespace snpmi

@@ -629,6 +629,277 @@ __global__ __launch_bounds__(512, 1) void k_syrk256d(const float* __restrict__ Z
     epilogue<LOCAL>(acc, tiles, n, bi, bj, accumulate, lane, wm, wn, wg);
 }
 
+// ---------------------------------------------------------------- f32 GRM on the bf16 MFMA pipe
+// The f32 MFMA (32x32x2) runs at 1/16 of the bf16 MFMA rate on gfx950.  Every f32 value of Z
+// is the sum of three bf16 values, EXACTLY: a0 = bf16(a), a1 = bf16(a - a0), a2 = a - a0 - a1
+// (a has 24 significant bits; each bf16 carries 8, and the residuals are exact in f32).  Then
+//   a*b = sum_{p,q} a_p b_q;   the six terms with p + q <= 2 are kept, the dropped ones are
+//   below 2^-23 |a b| -- the rounding level of one f32 multiply -- and every bf16 x bf16
+// product is exact in the f32 accumulator.  So K = sum over 6 bf16 MFMA products (f32 accumulate)
+// carries f32 accuracy at 16/6 = 2.7x the f32-MFMA peak.  The split is per SNP, on its 4-entry
+// LUT (k_lut_bf3), so the loader expands 2-bit codes straight into three bf16 planes with one
+// v_perm_b32 per 2 values per plane -- the standardized Z never exists in HBM.
+//
+// LDS image (per stage): [panel A/B][plane 3][k 16][iid 256, row stride 288 bf16 = 576 B].
+// MFMA operands (v_mfma_f32_32x32x16_bf16: lane l holds A[iid l&31][k 8(l>>5)..+7]) come out of
+// the SNP-major image with ds_read_b64_tr_b16 (4 k-rows x 16 iids per 16-lane group, delivered
+// column-major).  576 B = 16 dwords (mod 64) per k-row puts the 4 rows x 2 groups of a 32-lane
+// half on 64 distinct banks; the loader's two 16-B ds_write_b128 per row piece are ordered by
+// (d >> 2) & 1 so each 8-lane store group covers all 32 write banks.
+//
+// Cheap expansion: the LUT of plane p is byte-planar (word 2p = low bytes of L0..L3, word 2p+1 =
+// high bytes), so the v_perm selector of a value with code c is just (c, c + 4).  With
+// v_j = (w >> 2j) & 0x03030303 (byte q = code of iid 4q + j), one v_perm of (v_j | 0x04040404,
+// v_j) gives the selector of the iid pair (j, 4 + j) and another that of (8 + j, 12 + j).  The
+// LDS rows therefore hold each 16-iid group in the order pi(p) = 4 (p & 3) + (p >> 2) (a 4x4
+// transpose, an involution), on both panels alike; K's rows and columns come out permuted the
+// same way and the epilogue writes element (p, p') to (pi(p), pi(p')).
+constexpr int B3_RS = 288;                     // bf16 per LDS k-row
+constexpr int B3_PLANE = BK * B3_RS;           // bf16 per plane of one panel (BK = 16 SNPs)
+constexpr int B3_STAGE = 2 * 3 * B3_PLANE;     // bf16 per stage (2 panels x 3 planes)
+
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef short i16x4_t __attribute__((ext_vector_type(4)));
+typedef short i16x8_t __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ i16x4_t lds_tr16(const short* p) {
+    return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) i16x4_t*)p);
+}
+
+__device__ __forceinline__ int pi16(int p) { return 4 * (p & 3) + (p >> 2); }
+
+// f32w::epilogue with the pi-permuted rows/columns of k_syrk_bf3
+template <bool LOCAL>
+__device__ __forceinline__ void epilogue_pi(f32x16 (&acc)[4][2], float* __restrict__ tiles, uint64_t n, uint32_t bi,
+                                            uint32_t bj, int accumulate, int lane, int wm, int wn,
+                                            uint64_t local_block) {
+    float* T;
+    uint64_t ldo;
+    if constexpr (LOCAL) {
+        T = tiles + local_block * (BW * BW) + (uint64_t)(wm * 128) * BW + (wn >> 1) * 128;
+        ldo = BW;
+    } else {
+        const uint64_t nt128 = (n + 127) / 128;
+        const uint64_t ti = 2 * (uint64_t)bi + wm, tj = 2 * (uint64_t)bj + (wn >> 1);
+        if (ti > tj || tj >= nt128) return;  // wave-uniform
+        T = tiles + (tj * (tj + 1) / 2 + ti) * (uint64_t)(BM * BM);
+        ldo = BM;
+    }
+    const int hh = lane >> 5, colp = 16 * ((lane >> 4) & 1) + pi16(lane & 15);
+#pragma unroll
+    for (int x = 0; x < 4; x++)
+#pragma unroll
+        for (int y = 0; y < 2; y++) {
+            float* bp = T + (32 * x + hh) * ldo + (wn & 1) * 64 + 32 * y + colp;
+            // accumulator register r sits at row (r&3) + 8(r>>2) + 4hh of the subtile, i.e. at
+            // pi-row 16(r>>3) + 4(r&3) + 2((r>>2)&1) + hh
+            if (accumulate) {
+                float old[16];
+#pragma unroll
+                for (int r = 0; r < 16; r++) old[r] = bp[(16 * (r >> 3) + 4 * (r & 3) + 2 * ((r >> 2) & 1)) * ldo];
+#pragma unroll
+                for (int r = 0; r < 16; r++) acc[x][y][r] += old[r];
+            }
+#pragma unroll
+            for (int r = 0; r < 16; r++) bp[(16 * (r >> 3) + 4 * (r & 3) + 2 * ((r >> 2) & 1)) * ldo] = acc[x][y][r];
+        }
+}
+
+// MODE 0: load stage s+1 -> registers during stage s, expand + ds_write after its MFMAs.
+// MODE 1: codes/LUT of stage s+2 in flight (two register sets); stage s+1's expansion and
+//         ds_writes are issued plane by plane between the MFMA groups of stage s, so the VALU
+//         and LDS stores fill MFMA gaps instead of a store phase with the matrix pipe idle.
+// MODE 9: ablation -- no loader after the prologue (MFMA + transposed LDS reads only).
+struct B3Regs {
+    uint32_t w;
+    uint4 la, lb;  // plane LUT words: (lo0, hi0, lo1, hi1), (lo2, hi2, -, -)
+};
+
+template <bool LOCAL = false, bool XCD = false, int MODE = 0>
+__global__ __launch_bounds__(512, 1) void k_syrk_bf3(const uint8_t* __restrict__ P, uint64_t pitch, uint64_t n,
+                                                     uint64_t kdim, const uint32_t* __restrict__ lut3,
+                                                     float* __restrict__ tiles, int accumulate,
+                                                     uint32_t part_rank = 0, uint32_t part_world = 1) {
+    __shared__ __attribute__((aligned(16))) short lds[2 * B3_STAGE];
+    const uint64_t wg = XCD ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
+    uint32_t bi, bj;
+    tile_coords(LOCAL ? wg * part_world + part_rank : wg, bi, bj);
+    const uint64_t i0 = (uint64_t)bi * BW, j0 = (uint64_t)bj * BW;
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const int wm = wave >> 2, wn = wave & 3;
+    // loader role: panel, SNP row k of the stage, 16-iid group d
+    const int lp = t >> 8, lk = (t >> 4) & 15, ld_ = t & 15;
+    const int hfirst = (ld_ >> 2) & 1;
+    // packed codes of (SNP k0 + lk, iids base + 16 ld_ ..): walked by pointer, clamped to the last
+    // SNP past kdim (its values are zeroed through the LUT: lut3 is zero-padded to a multiple of BK)
+    const uint8_t* wp = P + (lp ? j0 : i0) / 4 + 4 * ld_ + (uint64_t)lk * pitch;
+    const uint8_t* wlast = P + (lp ? j0 : i0) / 4 + 4 * ld_ + (kdim - 1) * pitch;
+    const uint32_t* lp3 = lut3 + 8 * lk;
+    // transposed-read role: lane 4q+p of group g supplies row 8(g>>1)+q, cols 16(g&1)+4p
+    const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
+    const int rd_off = (8 * (g >> 1) + q) * B3_RS + 16 * (g & 1) + 4 * pp;
+
+    f32x16 acc[4][2];
+#pragma unroll
+    for (int x = 0; x < 4; x++)
+#pragma unroll
+        for (int y = 0; y < 2; y++) acc[x][y] = (f32x16){};
+    const uint64_t nst = (kdim + BK - 1) / BK;
+
+    auto load = [&](uint64_t st, B3Regs& r) {
+        const uint8_t* a = wp + st * BK * pitch;
+        r.w = *reinterpret_cast<const uint32_t*>(a <= wlast ? a : wlast);
+        r.la = *reinterpret_cast<const uint4*>(lp3 + 8 * BK * st);
+        r.lb = *reinterpret_cast<const uint4*>(lp3 + 8 * BK * st + 4);
+    };
+    auto make_sel = [&](uint32_t w, uint32_t (&sel)[8]) {
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const uint32_t v = (w >> (2 * j)) & 0x03030303u;  // byte q: code of iid 4q + j
+            const uint32_t o = v | 0x04040404u;
+            sel[2 * j] = __builtin_amdgcn_perm(o, v, 0x05010400u);      // iids (j, 4 + j)
+            sel[2 * j + 1] = __builtin_amdgcn_perm(o, v, 0x07030602u);  // iids (8 + j, 12 + j)
+        }
+    };
+    auto store_plane = [&](short* S, int pl, const B3Regs& r, const uint32_t (&sel)[8]) {
+        const uint32_t lo = pl == 0 ? r.la.x : pl == 1 ? r.la.z : r.lb.x;
+        const uint32_t hi = pl == 0 ? r.la.y : pl == 1 ? r.la.w : r.lb.y;
+        uint4 v0, v1;
+        v0.x = __builtin_amdgcn_perm(hi, lo, sel[0]);
+        v0.y = __builtin_amdgcn_perm(hi, lo, sel[1]);
+        v0.z = __builtin_amdgcn_perm(hi, lo, sel[2]);
+        v0.w = __builtin_amdgcn_perm(hi, lo, sel[3]);
+        v1.x = __builtin_amdgcn_perm(hi, lo, sel[4]);
+        v1.y = __builtin_amdgcn_perm(hi, lo, sel[5]);
+        v1.z = __builtin_amdgcn_perm(hi, lo, sel[6]);
+        v1.w = __builtin_amdgcn_perm(hi, lo, sel[7]);
+        uint4* r4 = reinterpret_cast<uint4*>(S + (lp * 3 + pl) * B3_PLANE + lk * B3_RS + 16 * ld_);
+        if (hfirst) {
+            r4[1] = v1;
+            r4[0] = v0;
+        } else {
+            r4[0] = v0;
+            r4[1] = v1;
+        }
+    };
+    auto store = [&](short* S, const B3Regs& r) {
+        uint32_t sel[8];
+        make_sel(r.w, sel);
+#pragma unroll
+        for (int pl = 0; pl < 3; pl++) store_plane(S, pl, r, sel);
+    };
+    auto frag = [&](const short* S, int panel, int pl, int col) -> bf16x8_t {
+        const short* b = S + (panel * 3 + pl) * B3_PLANE + rd_off + col;
+        const i16x4_t r0 = lds_tr16(b), r1 = lds_tr16(b + 4 * B3_RS);
+        return __builtin_bit_cast(bf16x8_t, (i16x8_t)__builtin_shufflevector(r0, r1, 0, 1, 2, 3, 4, 5, 6, 7));
+    };
+    // the six products (pa, pb), pa + pb <= 2, as 6 groups of 8 MFMAs; hook(gidx) runs after
+    // group gidx (the interleaved loader's slot)
+    auto compute = [&](const short* S, auto&& hook) {
+        bf16x8_t b[3][2];
+#pragma unroll
+        for (int pl = 0; pl < 3; pl++)
+#pragma unroll
+            for (int y = 0; y < 2; y++) b[pl][y] = frag(S, 1, pl, wn * 64 + 32 * y);
+        int gidx = 0;
+#pragma unroll
+        for (int pa = 0; pa < 3; pa++) {
+            bf16x8_t a[4];
+#pragma unroll
+            for (int x = 0; x < 4; x++) a[x] = frag(S, 0, pa, wm * 128 + 32 * x);
+#pragma unroll
+            for (int pb = 0; pb + pa <= 2; pb++) {
+#pragma unroll
+                for (int x = 0; x < 4; x++)
+#pragma unroll
+                    for (int y = 0; y < 2; y++)
+                        acc[x][y] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[x], b[pb][y], acc[x][y], 0, 0, 0);
+                hook(gidx++);
+            }
+        }
+    };
+
+    if constexpr (MODE == 1) {
+        // two register sets used alternately (stage parity): ra holds the codes of stage s+1
+        // while rb receives stage s+2, then the roles swap -- no register copies
+        B3Regs ra, rb;
+        load(0, ra);
+        store(lds, ra);
+        if (nst > 1) load(1, ra);
+        __syncthreads();
+        auto step = [&](uint64_t s, B3Regs& rn, B3Regs& rf) {
+            short* cur = lds + (s & 1) * B3_STAGE;
+            short* nxt = lds + ((s + 1) & 1) * B3_STAGE;
+            const bool more = s + 1 < nst;
+            if (s + 2 < nst) load(s + 2, rf);
+            uint32_t sel[8];
+            compute(cur, [&](int gi) {
+                if (more) {
+                    if (gi == 0) make_sel(rn.w, sel);
+                    else if (gi <= 3) store_plane(nxt, gi - 1, rn, sel);
+                }
+            });
+            __syncthreads();
+        };
+        for (uint64_t s = 0; s < nst; s += 2) {
+            step(s, ra, rb);
+            if (s + 1 < nst) step(s + 1, rb, ra);
+        }
+    } else {
+        B3Regs r;
+        load(0, r);
+        store(lds, r);
+        __syncthreads();
+        for (uint64_t s = 0; s < nst; s++) {
+            short* cur = lds + (s & 1) * B3_STAGE;
+            short* nxt = lds + ((s + 1) & 1) * B3_STAGE;
+            const bool more = s + 1 < nst;
+            if (MODE == 0 && more) load(s + 1, r);
+            compute(MODE == 9 ? lds : cur, [](int) {});
+            if (MODE == 0 && more) store(nxt, r);
+            __syncthreads();
+        }
+    }
+    epilogue_pi<LOCAL>(acc, tiles, n, bi, bj, accumulate, lane, wm, wn, wg);
+}
+
+// per-SNP f32 LUT [m][4] -> bf16x3 split LUT [mpad][8] u32, byte-planar: plane p at word 2p
+// (low bytes of the bf16 of codes 0..3) and 2p+1 (high bytes).  RNE rounding; NaN (Identity
+// LUT) stays NaN.  Entries m .. mpad-1 are zero (the SYRK loader's tail SNPs).
+__device__ __forceinline__ uint32_t bf16_rne(float f) {
+    const uint32_t u = __float_as_uint(f);
+    if ((u & 0x7f800000u) == 0x7f800000u) return (u >> 16) | ((u & 0xffffu) ? 0x40u : 0u);
+    return (u + 0x7fffu + ((u >> 16) & 1u)) >> 16;
+}
+__global__ __launch_bounds__(256) void k_lut_bf3(const float* __restrict__ lut, uint64_t m, uint64_t mpad,
+                                                 uint32_t* __restrict__ lut3) {
+    const uint64_t s = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (s >= mpad) return;
+    uint32_t h[3][4] = {};
+    if (s < m) {
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+            const float v = lut[4 * s + c];
+            const uint32_t a0 = bf16_rne(v);
+            const float r1 = v - __uint_as_float(a0 << 16);
+            const uint32_t a1 = bf16_rne(r1);
+            const float r2 = r1 - __uint_as_float(a1 << 16);
+            h[0][c] = a0;
+            h[1][c] = a1;
+            h[2][c] = bf16_rne(r2);
+        }
+    }
+    uint32_t o[8];
+#pragma unroll
+    for (int p = 0; p < 3; p++) {
+        o[2 * p] = (h[p][0] & 0xff) | ((h[p][1] & 0xff) << 8) | ((h[p][2] & 0xff) << 16) | ((h[p][3] & 0xff) << 24);
+        o[2 * p + 1] = (h[p][0] >> 8) | ((h[p][1] >> 8) << 8) | ((h[p][2] >> 8) << 16) | ((h[p][3] >> 8) << 24);
+    }
+    o[6] = o[7] = 0;
+    reinterpret_cast<uint4*>(lut3 + 8 * s)[0] = make_uint4(o[0], o[1], o[2], o[3]);
+    reinterpret_cast<uint4*>(lut3 + 8 * s)[1] = make_uint4(o[4], o[5], o[6], o[7]);
+}
+
 }  // namespace f32w
 
 // ====================================================================== f64
@@ -1006,6 +1277,51 @@ void launch_syrk_packed_part(const uint8_t* packed, uint64_t pitch, uint64_t n, 
     }
     f32w::k_syrk256<1, true><<<(unsigned)nloc, 512, 0, st>>>(packed, pitch, n, m, (const float*)lut, (float*)blocks,
                                                              accumulate, (uint32_t)rank, (uint32_t)world);
+    SNPMI_HIP(hipGetLastError());
+}
+
+uint64_t lut_bf3_entries(uint64_t m) { return round_up(std::max<uint64_t>(m, 1), f32w::BK); }
+
+void launch_lut_bf3(const float* lut, uint64_t m, uint32_t* lut3, hipStream_t st) {
+    const uint64_t mpad = lut_bf3_entries(m);
+    f32w::k_lut_bf3<<<(unsigned)ceil_div(mpad, 256), 256, 0, st>>>(lut, m, mpad, lut3);
+    SNPMI_HIP(hipGetLastError());
+}
+
+void launch_syrk_packed_bf3(const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m, const uint32_t* lut3,
+                            float* tiles, int accumulate, hipStream_t st) {
+    const uint64_t nb = ceil_div(n, 256), g = nb * (nb + 1) / 2;
+    if (g == 0) return;
+    SNPMI_REQUIRE(g < (1ull << 31), SNPMI_E_ARG, "too many GRM blocks for one launch");
+    SNPMI_REQUIRE(pitch % 64 == 0 && pitch * 4 >= nb * 256, SNPMI_E_ARG, "packed pitch must cover round_up(n, 256) iids");
+    if (m == 0) {
+        if (!accumulate) SNPMI_HIP(hipMemsetAsync(tiles, 0, n_tiles_upper(n) * BM * BM * sizeof(float), st));
+        return;
+    }
+    // MI355X, N=50k, 10k SNPs (tools/ubench.py syrk): 30 = 293.6 TFLOP/s, 31 = 302.4,
+    // default (interleaved loader + XCD remap) = 309.3, 39 (no loader, ablation) = 369.5
+    switch (g_variant_syrk) {
+        case 30: f32w::k_syrk_bf3<><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, lut3, tiles, accumulate); break;
+        case 31: f32w::k_syrk_bf3<false, true><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, lut3, tiles, accumulate); break;
+        case 39: f32w::k_syrk_bf3<false, true, 9><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, lut3, tiles, accumulate); break;
+        default: f32w::k_syrk_bf3<false, true, 1><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, lut3, tiles, accumulate);
+    }
+    SNPMI_HIP(hipGetLastError());
+}
+
+void launch_syrk_packed_bf3_part(const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m, const uint32_t* lut3,
+                                 int rank, int world, float* blocks, int accumulate, hipStream_t st) {
+    const uint64_t nloc = grm_part_blocks(n, rank, world);
+    if (nloc == 0) return;
+    SNPMI_REQUIRE(nloc < (1ull << 31), SNPMI_E_ARG, "too many GRM blocks for one launch");
+    SNPMI_REQUIRE(pitch % 64 == 0 && pitch * 4 >= ceil_div(n, 256) * 256, SNPMI_E_ARG,
+                  "packed pitch must cover round_up(n, 256) iids");
+    if (m == 0) {
+        if (!accumulate) SNPMI_HIP(hipMemsetAsync(blocks, 0, nloc * 256 * 256 * sizeof(float), st));
+        return;
+    }
+    f32w::k_syrk_bf3<true, true, 1><<<(unsigned)nloc, 512, 0, st>>>(packed, pitch, n, m, lut3, blocks, accumulate,
+                                                                    (uint32_t)rank, (uint32_t)world);
     SNPMI_HIP(hipGetLastError());
 }
 

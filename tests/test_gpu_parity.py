@@ -321,11 +321,12 @@ def test_kerneldata_diag_k_to_n():
     assert abs(np.diag(kd.val).sum() - 3) < 1e-7  # kernelreader/test.py:221-229
 
 
-@pytest.fixture(params=[0, 4, 5], ids=["auto", "syrk256", "syrk128"])
+@pytest.fixture(params=[0, 4, 5, 20, 30, 31], ids=["auto", "syrk256", "syrk128", "f32twophase", "bf3plain", "bf3xcd"])
 def syrk_variant(request):
-    """Run a test under each SYRK kernel -- f32: 0 = size-based choice, 4 = 256x256 tiles,
-    5 = 128x128 tiles; f64: 0/4 = interleaved bank-rotated loader, 5 = plain loader --
-    and restore the default afterwards."""
+    """Run a test under each SYRK kernel -- f32: 0 = default (packed: the bf16x3-split kernel on
+    the bf16 MFMA pipe, interleaved loader, XCD remap), 30/31 = its plain-loader forms, 4 = f32
+    MFMA 256x256 fused, 5 = f32 MFMA 128x128, 20 = f32 MFMA two-phase (decode to Z + glds);
+    f64: 0/4 = interleaved bank-rotated loader, 5 = plain loader -- and restore the default."""
     N.call("snpmi_set_kernel_variant", b"syrk", request.param)
     yield request.param
     N.call("snpmi_set_kernel_variant", b"syrk", 0)
@@ -414,7 +415,7 @@ def test_device_decode_standardize_large_properties(dtype):
 
 
 @pytest.mark.parametrize("n,world", [(300, 1), (700, 3), (1100, 4), (4100, 2), (4500, 3)])
-def test_grm_partitioned_blocks_assemble_k(n, world):
+def test_grm_partitioned_blocks_assemble_k(n, world, syrk_variant):
     """cfg5 mode: every rank's 256x256 blocks (simulated ranks on one GPU) assemble to K."""
     rng = np.random.default_rng(n)
     val = rng.integers(0, 3, size=(n, 45)).astype(np.float64)

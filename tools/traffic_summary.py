@@ -2,7 +2,9 @@
 
 Correction (MI355X_MICROARCH.md §HBM): on gfx950 FETCH_SIZE reports half of the bytes of a
 wide coalesced streaming read, so read bytes = 2 * FETCH_SIZE * 1024; WRITE_SIZE is exact for
-16-B-per-lane streaming stores; both counters are in KiB.
+16-B-per-lane streaming stores; both counters are in KiB.  The bf16x3 SYRK (k_syrk_bf3) reads
+4-B-per-lane packed codes (64-B runs) and 16-B LUT rows, an access width the guide leaves
+uncalibrated: its FETCH_SIZE is reported raw (x1), marked "read_scale": 1.
 Usage: python tools/traffic_summary.py <prof_dir> <out.json>
 """
 import collections
@@ -14,7 +16,8 @@ import sys
 KERNELS = {"k_decode_std_lds_f32": "k_decode_std_lds_f32", "k_decode_f<float, 4>": "k_decode_f<float>", "k_decode_f<float": "k_decode_f<float>",
            "f32k::k_syrk<true": "f32k::k_syrk<true>", "k_syrk256<1, false>": "f32w::k_syrk256",
            "k_syrk256<1, true>": "f32w::k_syrk256<local>", "k_syrk256d<false": "f32w::k_syrk256d",
-           "k_syrk256d<true": "f32w::k_syrk256d<local>", "k_snp_stats<float>": "k_snp_stats<float>"}
+           "k_syrk256d<true": "f32w::k_syrk256d<local>", "k_snp_stats<float>": "k_snp_stats<float>",
+           "k_syrk_bf3<false": "f32w::k_syrk_bf3", "k_syrk_bf3<true": "f32w::k_syrk_bf3<local>"}
 
 
 def short(name):
@@ -44,10 +47,12 @@ def main(prof, out):
             fv = sorted(f[k])
             full_w = [x for x in wv if x >= 0.95 * wv[-1]]
             full_f = [x for x in fv if x >= 0.95 * fv[-1]]
-            read_b = 2.0 * sum(full_f) / len(full_f)
+            scale = 1.0 if "bf3" in k else 2.0
+            read_b = scale * sum(full_f) / len(full_f)
             write_b = sum(full_w) / len(full_w)
             res.setdefault(k, {})[leg] = {"read_bytes": read_b, "write_bytes": write_b,
-                                          "traffic_bytes": read_b + write_b, "launches": len(fv)}
+                                          "traffic_bytes": read_b + write_b, "launches": len(fv),
+                                          "read_scale": scale}
     res["_config"] = {"dec": [500000, 8192], "grm": [50000, 10000]}  # tools/profile.sh settings
     res["_source"] = ("rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes (tools/profile.sh); "
                       "read = 2*FETCH_SIZE (gfx950 correction), per full launch")
