@@ -279,10 +279,10 @@ def cpu_baseline_standardize(args, sample, pitch):
 def leg_grm(N, args, dist, rccl):
     n, m, B = args.grm_iid, args.grm_sid, args.grm_block
     pitch = N.lib().snpmi_packed_pitch(n)
-    from pysnptools_amd.shard import rank_blocks, snp_blocks
+    from pysnptools_amd.shard import rank_span_blocks, snp_blocks
 
     blocks = snp_blocks(m, B)
-    mine = rank_blocks(m, B, dist.rank, dist.world)
+    mine = rank_span_blocks(m, B, dist.rank, dist.world)
     my_m = sum(c for _, c in mine)
     packed = Dev(N, max(1, my_m) * pitch)
     off = 0
@@ -330,7 +330,9 @@ def leg_grm(N, args, dist, rccl):
     nb = (n + 255) // 256
     exec_ratio = BF3_PRODUCTS * 2 * 256 * 256 * (nb * (nb + 1) // 2) / (n * (n + 1))  # executed bf16 / algorithmic
     res = dict(wall=wall, syrk_ms=syrk_ms, allreduce_ms=allreduce_ms, trace=tr.value, exec_ratio=exec_ratio,
-               mean_tflops=(flops_full_block / (np.mean(syrk_ms) * 1e-3) / 1e12) if syrk_ms else 0.0, nblocks=len(blocks))
+               # throughput over this rank's launches (the last block of a shard can be partial)
+               mean_tflops=(n * (n + 1) * my_m / (np.sum(syrk_ms) * 1e-3) / 1e12) if syrk_ms else 0.0,
+               nblocks=len(blocks))
     if dist.rank == 0 and not args.skip_cpu and my_m > 0:
         # parity sample (untimed): K rows 0..63 of the GRM of this rank's first 512 SNPs
         cm, rows = min(512, my_m), 64
@@ -344,7 +346,7 @@ def leg_grm(N, args, dist, rccl):
         N.call("snpmi_memcpy_d2h", N.ptr(krows), dout.p, krows.nbytes)
         sample = np.empty((cm, pitch), dtype=np.uint8)
         N.call("snpmi_memcpy_d2h", N.ptr(sample), packed.p, sample.nbytes)
-        res["parity_sample"] = (krows, sample, cm, (blocks[dist.rank][0] if mine else 0))
+        res["parity_sample"] = (krows, sample, cm, (mine[0][0] if mine else 0))
         dri.free()
         dout.free()
     ev.destroy()
@@ -499,8 +501,9 @@ def main():
         r2 = leg_grm(N, args, dist, rccl)
         n, m = args.grm_iid, args.grm_sid
         gf = n * (n + 1) * m / r2["wall"] / 1e9
-        grm = {"workload": "cfg4: %d iid x %d SNP, Unit, block %d, f32 MFMA SYRK, SNP blocks round-robin over %d "
-                           "rank(s)%s" % (n, m, args.grm_block, dist.world, ", RCCL all-reduce of K tiles" if rccl else ""),
+        grm = {"workload": "cfg4: %d iid x %d SNP, Unit, block %d, f32 (bf16x3 MFMA) SYRK, SNPs split into %d equal "
+                           "contiguous shard(s) streamed in blocks%s" % (n, m, args.grm_block, dist.world,
+                                                                         ", RCCL all-reduce of K tiles" if rccl else ""),
                "gflops": gf, "snps_per_s": m / r2["wall"], "seconds": r2["wall"], "scaling": "strong",
                "allreduce_ms": r2["allreduce_ms"], "trace_K": r2["trace"],
                "roofline": {"bound": "mfma", "achieved": r2["mean_tflops"], "peak": BF3_PEAK_TFLOPS,

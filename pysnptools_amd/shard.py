@@ -20,6 +20,16 @@ def rank_blocks(n_sid, block_size, rank, world):
     return snp_blocks(n_sid, block_size)[rank::world]
 
 
+def rank_span_blocks(n_sid, block_size, rank, world):
+    """Balanced plan: rank ``rank`` owns the contiguous SNP range [r*M/p, (r+1)*M/p), streamed
+    in blocks of at most ``block_size`` -- ranks differ by at most one SNP, where round-robin
+    whole blocks leave them a block apart (50 blocks over 8 ranks: 7 vs 6.25 on average)."""
+    assert 0 <= rank < world
+    lo, hi = n_sid * rank // world, n_sid * (rank + 1) // world
+    block_size = max(1, int(block_size))
+    return [(s0, min(block_size, hi - s0)) for s0 in range(lo, hi, block_size)]
+
+
 def merge_order(n_sid, block_size, world):
     """For each global block (in SNP order): (owner rank, index within that rank's list)."""
     out = []

@@ -42,3 +42,19 @@ def test_sharded_grm_equals_single(tmp_path, world):
         K = np.load(tmp_path / ("K%d.npy" % r))
         np.testing.assert_allclose(K, Kref, rtol=1e-10, atol=1e-8)
         np.testing.assert_array_equal(np.load(tmp_path / ("S%d.npy" % r)), sref)
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+def test_rank_span_blocks_cover_once_balanced(world):
+    """bench.py's cfg4 plan: contiguous equal SNP shards, each in blocks <= block_size."""
+    from pysnptools_amd.shard import rank_span_blocks
+
+    m, bs = 500_000, 10_000
+    spans = [rank_span_blocks(m, bs, r, world) for r in range(world)]
+    cover = sorted(s0 + i for sp in spans for s0, c in sp for i in (0, c - 1))
+    assert sum(c for sp in spans for _, c in sp) == m
+    flat = sorted((s0, c) for sp in spans for s0, c in sp)
+    assert flat[0][0] == 0 and all(a[0] + a[1] == b[0] for a, b in zip(flat, flat[1:]))
+    assert all(0 < c <= bs for sp in spans for _, c in sp) and cover[-1] == m - 1
+    per = [sum(c for _, c in sp) for sp in spans]
+    assert max(per) - min(per) <= 1

@@ -110,7 +110,7 @@ def test_snpmemmap_write_bed_streams_gpu_blocks(tmp_path, order, dtype):
         got = np.asarray(out.val[:, s0:s0 + len(cols)])
         np.testing.assert_array_equal(got, ref)
     assert out.val.flags[order + "_CONTIGUOUS"] and out.val.dtype == dtype
-    assert list(out.sid[:2]) == list(b.sid[7:9]) and np.array_equal(out.pos, b.pos[7:407])
+    assert list(out.sid[:2]) == list(b.sid[7:9]) and np.array_equal(out.pos, b.pos[7:407], equal_nan=True)
     # the memmap is a SnpReader: its GRM through the dense path == Z Z^T of the file
     K = out.read_kernel(Unit(), dtype=np.float64).val
     Z = np.array(out.val, dtype=np.float64)
