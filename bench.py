@@ -4,7 +4,7 @@ Metric (BASELINE.json): "SNPs/sec standardized (500k x 1M) + GRM GF/s at 1/2/4/8
 
   value      = SNPs/s standardized, whole job: every rank decodes + Unit-standardizes its own
                synthetic 500k-iid x 1M-SNP BED matrix (the UKBB shape of configs[4]), resident in
-               HBM as packed 2-bit codes, in blocks of 8192 SNPs into an f32 F-order block buffer
+               HBM as packed 2-bit codes, in blocks of 2048 SNPs into an f32 F-order block buffer
                (weak scaling: per-GPU work fixed).  A step = one pass over the 1M SNPs.
   roofline   = the decode kernel (k_decode_f<float>), HBM bound: algorithmic bytes per launch =
                block * (ceil(N/4) + 4N) / its mean HIP-event duration, vs 8.0 TB/s.
@@ -47,7 +47,7 @@ def parse():
     p.add_argument("--warmup", type=int, default=1)
     p.add_argument("--n-iid", type=int, default=500_000)
     p.add_argument("--n-sid", type=int, default=1_000_000)
-    p.add_argument("--block", type=int, default=8192)
+    p.add_argument("--block", type=int, default=2048)
     p.add_argument("--grm-iid", type=int, default=50_000)
     p.add_argument("--grm-sid", type=int, default=500_000)
     p.add_argument("--grm-block", type=int, default=10_000)

@@ -53,7 +53,7 @@ def main(prof, out):
             res.setdefault(k, {})[leg] = {"read_bytes": read_b, "write_bytes": write_b,
                                           "traffic_bytes": read_b + write_b, "launches": len(fv),
                                           "read_scale": scale}
-    res["_config"] = {"dec": [500000, 8192], "grm": [50000, 10000]}  # tools/profile.sh settings
+    res["_config"] = {"dec": [500000, 2048], "grm": [50000, 10000]}  # tools/profile.sh settings
     res["_source"] = ("rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes (tools/profile.sh); "
                       "read = 2*FETCH_SIZE (gfx950 correction), per full launch")
     json.dump(res, open(out, "w"), indent=1)
