@@ -21,7 +21,6 @@ namespace {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef double f64x4 __attribute__((ext_vector_type(4)));
-typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int BM = kTile;  // 128
 
@@ -864,194 +863,6 @@ __global__ __launch_bounds__(512, 1) void k_syrk_bf3(const uint8_t* __restrict__
     epilogue_pi<LOCAL>(acc, tiles, n, bi, bj, accumulate, lane, wm, wn, wg);
 }
 
-// The same computation on v_mfma_f32_16x16x32_bf16 (k = 32 per instruction): the 32-deep
-// reduction holds TWO products of one 16-SNP stage -- k 0..15 from plane PA, 16..31 from plane
-// PB -- so 3 MFMAs per 16x16 subtile cover the six products:
-//   [a0|a1].[b0|b1] = a0b0 + a1b1,  [a0|a1].[b1|b0] = a0b1 + a1b0,  [a0|a2].[b2|b0] = a0b2 + a2b0.
-// Operand lane l holds A[iid l&15][k 8(l>>4)..+7]: 16-lane groups 0,1 read plane PA (k-rows
-// 0-7 / 8-15), groups 2,3 plane PB, each by two ds_read_b64_tr_b16.  A 32-lane half then reads
-// k-rows r and r+8 of the same 16 iids: the loader stores the 16-iid segment d of k-row r at
-// segment d ^ ((r >> 3) & 1), so with the 576-B row stride the 8 rows land on 64 distinct banks.
-// Output subtile 16x16: C/D col = lane&15, row = 4(lane>>4) + reg -> pi rows 4 reg + (lane>>4).
-template <bool LOCAL>
-__device__ __forceinline__ void epilogue_pi16(f32x4 (&acc)[8][4], float* __restrict__ tiles, uint64_t n, uint32_t bi,
-                                              uint32_t bj, int accumulate, int lane, int wm, int wn,
-                                              uint64_t local_block) {
-    float* T;
-    uint64_t ldo;
-    if constexpr (LOCAL) {
-        T = tiles + local_block * (BW * BW) + (uint64_t)(wm * 128) * BW + (wn >> 1) * 128;
-        ldo = BW;
-    } else {
-        const uint64_t nt128 = (n + 127) / 128;
-        const uint64_t ti = 2 * (uint64_t)bi + wm, tj = 2 * (uint64_t)bj + (wn >> 1);
-        if (ti > tj || tj >= nt128) return;  // wave-uniform
-        T = tiles + (tj * (tj + 1) / 2 + ti) * (uint64_t)(BM * BM);
-        ldo = BM;
-    }
-    const int colp = (wn & 1) * 64 + pi16(lane & 15);
-#pragma unroll
-    for (int x = 0; x < 8; x++)
-#pragma unroll
-        for (int y = 0; y < 4; y++) {
-            float* bp = T + (16 * x + (lane >> 4)) * ldo + 16 * y + colp;
-            if (accumulate) {
-                float old[4];
-#pragma unroll
-                for (int r = 0; r < 4; r++) old[r] = bp[4 * r * ldo];
-#pragma unroll
-                for (int r = 0; r < 4; r++) acc[x][y][r] += old[r];
-            }
-#pragma unroll
-            for (int r = 0; r < 4; r++) bp[4 * r * ldo] = acc[x][y][r];
-        }
-}
-
-template <bool LOCAL = false, bool XCD = true, int MODE = 1>
-__global__ __launch_bounds__(512, 1) void k_syrk_bf3m(const uint8_t* __restrict__ P, uint64_t pitch, uint64_t n,
-                                                      uint64_t kdim, const uint32_t* __restrict__ lut3,
-                                                      float* __restrict__ tiles, int accumulate,
-                                                      uint32_t part_rank = 0, uint32_t part_world = 1) {
-    __shared__ __attribute__((aligned(16))) short lds[2 * B3_STAGE];
-    const uint64_t wg = XCD ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
-    uint32_t bi, bj;
-    tile_coords(LOCAL ? wg * part_world + part_rank : wg, bi, bj);
-    const uint64_t i0 = (uint64_t)bi * BW, j0 = (uint64_t)bj * BW;
-    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-    const int wm = wave >> 2, wn = wave & 3;
-    const int lp = t >> 8, lk = (t >> 4) & 15, ld_ = t & 15;
-    const int ps = ld_ ^ ((lk >> 3) & 1);  // physical 16-iid segment of this k-row
-    const int hfirst = (ps >> 2) & 1;
-    const uint8_t* wp = P + (lp ? j0 : i0) / 4 + 4 * ld_ + (uint64_t)lk * pitch;
-    const uint8_t* wlast = P + (lp ? j0 : i0) / 4 + 4 * ld_ + (kdim - 1) * pitch;
-    const uint32_t* lp3 = lut3 + 8 * lk;
-    // transposed reads: group g = lane>>4 (plane PA for g < 2, PB above), k-rows 8(g&1) + 4h + q,
-    // iid columns 4p.. of the subtile's (swizzled) 16-iid segment
-    const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3, godd = g & 1, ghi = g >> 1;
-    const int rd_base = (8 * godd + q) * B3_RS + 4 * pp;
-    const int sw_even = 16 * godd, sw_odd = -16 * godd;  // segment x ^ godd, for x even / odd
-
-    f32x4 acc[8][4];
-#pragma unroll
-    for (int x = 0; x < 8; x++)
-#pragma unroll
-        for (int y = 0; y < 4; y++) acc[x][y] = (f32x4){};
-    const uint64_t nst = (kdim + BK - 1) / BK;
-
-    auto load = [&](uint64_t st, B3Regs& r) {
-        const uint8_t* a = wp + st * BK * pitch;
-        r.w = *reinterpret_cast<const uint32_t*>(a <= wlast ? a : wlast);
-        r.la = *reinterpret_cast<const uint4*>(lp3 + 8 * BK * st);
-        r.lb = *reinterpret_cast<const uint4*>(lp3 + 8 * BK * st + 4);
-    };
-    auto make_sel = [&](uint32_t w, uint32_t (&sel)[8]) {
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            const uint32_t v = (w >> (2 * j)) & 0x03030303u;
-            const uint32_t o = v | 0x04040404u;
-            sel[2 * j] = __builtin_amdgcn_perm(o, v, 0x05010400u);
-            sel[2 * j + 1] = __builtin_amdgcn_perm(o, v, 0x07030602u);
-        }
-    };
-    auto store_plane = [&](short* S, int pl, const B3Regs& r, const uint32_t (&sel)[8]) {
-        const uint32_t lo = pl == 0 ? r.la.x : pl == 1 ? r.la.z : r.lb.x;
-        const uint32_t hi = pl == 0 ? r.la.y : pl == 1 ? r.la.w : r.lb.y;
-        uint4 v0, v1;
-        v0.x = __builtin_amdgcn_perm(hi, lo, sel[0]);
-        v0.y = __builtin_amdgcn_perm(hi, lo, sel[1]);
-        v0.z = __builtin_amdgcn_perm(hi, lo, sel[2]);
-        v0.w = __builtin_amdgcn_perm(hi, lo, sel[3]);
-        v1.x = __builtin_amdgcn_perm(hi, lo, sel[4]);
-        v1.y = __builtin_amdgcn_perm(hi, lo, sel[5]);
-        v1.z = __builtin_amdgcn_perm(hi, lo, sel[6]);
-        v1.w = __builtin_amdgcn_perm(hi, lo, sel[7]);
-        uint4* r4 = reinterpret_cast<uint4*>(S + (lp * 3 + pl) * B3_PLANE + lk * B3_RS + 16 * ps);
-        if (hfirst) {
-            r4[1] = v1;
-            r4[0] = v0;
-        } else {
-            r4[0] = v0;
-            r4[1] = v1;
-        }
-    };
-    auto store = [&](short* S, const B3Regs& r) {
-        uint32_t sel[8];
-        make_sel(r.w, sel);
-#pragma unroll
-        for (int pl = 0; pl < 3; pl++) store_plane(S, pl, r, sel);
-    };
-    // fragment [plane PA | plane PB] of the 16-iid subtile at column c (multiple of 16)
-    auto frag = [&](const short* S, int panel, int PA, int PB, int c) -> bf16x8_t {
-        const int sw = ((c >> 4) & 1) ? sw_odd : sw_even;
-        const short* b = S + panel * 3 * B3_PLANE + (ghi ? PB : PA) * B3_PLANE + rd_base + c + sw;
-        const i16x4_t r0 = lds_tr16(b), r1 = lds_tr16(b + 4 * B3_RS);
-        return __builtin_bit_cast(bf16x8_t, (i16x8_t)__builtin_shufflevector(r0, r1, 0, 1, 2, 3, 4, 5, 6, 7));
-    };
-    auto compute = [&](const short* S, auto&& hook) {
-        bf16x8_t b01[4], b10[4], b20[4];
-#pragma unroll
-        for (int y = 0; y < 4; y++) {
-            const int c = wn * 64 + 16 * y;
-            b01[y] = frag(S, 1, 0, 1, c);
-            b10[y] = frag(S, 1, 1, 0, c);
-            b20[y] = frag(S, 1, 2, 0, c);
-        }
-#pragma unroll
-        for (int x = 0; x < 8; x++) {
-            const int c = wm * 128 + 16 * x;
-            const bf16x8_t a01 = frag(S, 0, 0, 1, c), a02 = frag(S, 0, 0, 2, c);
-#pragma unroll
-            for (int y = 0; y < 4; y++) {
-                acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a01, b01[y], acc[x][y], 0, 0, 0);
-                acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a01, b10[y], acc[x][y], 0, 0, 0);
-                acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a02, b20[y], acc[x][y], 0, 0, 0);
-            }
-            hook(x);
-        }
-    };
-
-    if constexpr (MODE == 1) {
-        B3Regs ra, rb;
-        load(0, ra);
-        store(lds, ra);
-        if (nst > 1) load(1, ra);
-        __syncthreads();
-        auto step = [&](uint64_t s, B3Regs& rn, B3Regs& rf) {
-            short* cur = lds + (s & 1) * B3_STAGE;
-            short* nxt = lds + ((s + 1) & 1) * B3_STAGE;
-            const bool more = s + 1 < nst;
-            if (s + 2 < nst) load(s + 2, rf);
-            uint32_t sel[8];
-            compute(cur, [&](int gi) {
-                if (more) {
-                    if (gi == 0) make_sel(rn.w, sel);
-                    else if (gi == 2 || gi == 4 || gi == 6) store_plane(nxt, gi / 2 - 1, rn, sel);
-                }
-            });
-            __syncthreads();
-        };
-        for (uint64_t s = 0; s < nst; s += 2) {
-            step(s, ra, rb);
-            if (s + 1 < nst) step(s + 1, rb, ra);
-        }
-    } else {
-        B3Regs r;
-        load(0, r);
-        store(lds, r);
-        __syncthreads();
-        for (uint64_t s = 0; s < nst; s++) {
-            short* cur = lds + (s & 1) * B3_STAGE;
-            short* nxt = lds + ((s + 1) & 1) * B3_STAGE;
-            const bool more = s + 1 < nst;
-            if (MODE == 0 && more) load(s + 1, r);
-            compute(MODE == 9 ? lds : cur, [](int) {});
-            if (MODE == 0 && more) store(nxt, r);
-            __syncthreads();
-        }
-    }
-    epilogue_pi16<LOCAL>(acc, tiles, n, bi, bj, accumulate, lane, wm, wn, wg);
-}
-
 // per-SNP f32 LUT [m][4] -> bf16x3 split LUT [mpad][8] u32, byte-planar: plane p at word 2p
 // (low bytes of the bf16 of codes 0..3) and 2p+1 (high bytes).  RNE rounding; NaN (Identity
 // LUT) stays NaN.  Entries m .. mpad-1 are zero (the SYRK loader's tail SNPs).
@@ -1493,9 +1304,6 @@ void launch_syrk_packed_bf3(const uint8_t* packed, uint64_t pitch, uint64_t n, u
         case 30: f32w::k_syrk_bf3<><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, lut3, tiles, accumulate); break;
         case 31: f32w::k_syrk_bf3<false, true><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, lut3, tiles, accumulate); break;
         case 39: f32w::k_syrk_bf3<false, true, 9><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, lut3, tiles, accumulate); break;
-        case 33: f32w::k_syrk_bf3m<false, true, 1><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, lut3, tiles, accumulate); break;
-        case 34: f32w::k_syrk_bf3m<false, true, 0><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, lut3, tiles, accumulate); break;
-        case 38: f32w::k_syrk_bf3m<false, true, 9><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, lut3, tiles, accumulate); break;
         default: f32w::k_syrk_bf3<false, true, 1><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, lut3, tiles, accumulate);
     }
     SNPMI_HIP(hipGetLastError());

@@ -321,7 +321,7 @@ def test_kerneldata_diag_k_to_n():
     assert abs(np.diag(kd.val).sum() - 3) < 1e-7  # kernelreader/test.py:221-229
 
 
-@pytest.fixture(params=[0, 4, 5, 20, 30, 31, 33], ids=["auto", "syrk256", "syrk128", "f32twophase", "bf3plain", "bf3xcd", "bf3m16"])
+@pytest.fixture(params=[0, 4, 5, 20, 30, 31], ids=["auto", "syrk256", "syrk128", "f32twophase", "bf3plain", "bf3xcd"])
 def syrk_variant(request):
     """Run a test under each SYRK kernel -- f32: 0 = default (packed: the bf16x3-split kernel on
     the bf16 MFMA pipe, interleaved loader, XCD remap), 30/31 = its plain-loader forms, 4 = f32
