@@ -22,14 +22,16 @@ def emit(**kw):
     print(json.dumps(kw), flush=True)
 
 
-def gpu_decode_std(N, n, m, seed, miss, kind, a, b, block=8192, reps=2):
+def gpu_decode_std(N, n, m, seed, miss, kind, a, b, block_bytes=4 << 30, reps=2):
+    """Blocks of ~block_bytes of f32 output (>= 2048 SNPs): at small N a fixed SNP count makes
+    short launches whose gaps dominate (cfg2 at 8192-SNP blocks: 70 us per launch)."""
     from bench import Dev, Events, synth
 
     pitch = N.lib().snpmi_packed_pitch(n)
     ld = (n + 15) // 16 * 16
     packed = Dev(N, pitch * m)
     synth(N, packed.p, pitch, n, 0, m, seed, miss)
-    B = min(block, m)
+    B = min(m, max(2048, block_bytes // (4 * ld)))
     lut, st, out = Dev(N, B * 16), Dev(N, B * 8), Dev(N, B * ld * 4)
     ev = Events(N, 2)
     best = None
@@ -49,7 +51,7 @@ def gpu_decode_std(N, n, m, seed, miss, kind, a, b, block=8192, reps=2):
     for d in (packed, lut, st, out):
         d.free()
     ev.destroy()
-    return best, sample
+    return best, sample, B
 
 
 def cpu_decode_std(sample, n, is_beta, a, b, threads, budget=6.0):
@@ -115,9 +117,9 @@ def main():
                 (3, 100_000, 1_000_000, 3, 0.218, N.STD_BETA, 1.0, 25.0, "Beta(1,25)+NaN impute")):
             if cfg not in only:
                 continue
-            t, sample = gpu_decode_std(N, n, m, seed, miss, kind, a, b)
+            t, sample, B = gpu_decode_std(N, n, m, seed, miss, kind, a, b)
             nbytes = m * ((n + 3) // 4 + 4 * n)
-            emit(cfg=cfg, workload="%d iid x %d SNP, %s, f32, HBM-resident packed, 8192-SNP blocks" % (n, m, lab),
+            emit(cfg=cfg, workload="%d iid x %d SNP, %s, f32, HBM-resident packed, %d-SNP blocks" % (n, m, lab, B),
                  backend="1xMI355X", seconds=t, snps_per_s=m / t, GBps=nbytes / t / 1e9, hbm_frac=nbytes / t / 8e12)
             for th in (allt, 1):
                 v, done = cpu_decode_std(sample, n, kind == N.STD_BETA, a, b, th)
