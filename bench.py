@@ -572,6 +572,7 @@ def main():
             "grm5": grm5,
         }
         print(json.dumps(line), flush=True)
+    dist.barrier()  # every rank leaves together (rank 0 ran the CPU baselines alone)
     dist.close()
 
 

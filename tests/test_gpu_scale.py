@@ -87,3 +87,46 @@ def test_config1_10k_x_100k_unit():
 def test_config2_100k_x_1m_beta():
     """BASELINE configs[2]: 100k iid x 1M SNP, Beta(1,25) + NaN impute (21.8% missing, snpgen.py:166)."""
     assert run_config(100_000, 1_000_000, seed=3, miss=0.218, std_kind=N.STD_BETA, a=1.0, b=25.0, samples=4) > 0
+
+
+def test_grm_config4_50k_x_500k():
+    """BASELINE configs[3] at full size: 50k iids x 500k SNPs, Unit, f32 GRM accumulated on the
+    device over 10k-SNP blocks (bf16x3 split on the bf16 MFMA).  K restricted to 96 sampled iids
+    (rows AND columns, incl. iids 0 and n-1) against the f64 oracle over all 500k SNPs -- only
+    those iids are decoded; stats from the code counts of every iid -- max|dK| <= 1e-5 max diag,
+    and the diagonal elementwise within 1e-5."""
+    n, m, B = 50_000, 500_000, 10_000
+    pitch = N.lib().snpmi_packed_pitch(n)
+    packed = Dev(pitch * m)
+    x, cdf = O.maf_table(n)
+    N.call("snpmi_dev_synth_bed", packed.p, pitch, n, 0, m, 4, 0.01, N.ptr(x), N.ptr(cdf), len(x))
+    tiles = Dev(N.lib().snpmi_grm_tile_bytes(n, N.DT_F32))
+    lut, st = Dev(B * 16), Dev(B * 8)
+    for s0 in range(0, m, B):
+        cnt = min(B, m - s0)
+        N.call("snpmi_dev_snp_stats", packed.at(s0 * pitch), pitch, n, cnt, 0, N.STD_UNIT, 0.0, 0.0, 0, N.DT_F32,
+               st.p, lut.p)
+        N.call("snpmi_dev_syrk_packed", packed.at(s0 * pitch), pitch, n, cnt, lut.p, N.DT_F32, tiles.p, int(s0 > 0))
+    rng = np.random.default_rng(4)
+    sample = np.unique(np.concatenate([[0, n - 1], rng.choice(n, size=94, replace=False)])).astype(np.uint64)
+    ns = len(sample)
+    didx, dout = Dev(ns * 8), Dev(ns * ns * 4)
+    N.call("snpmi_memcpy_h2d", didx.p, N.ptr(sample), sample.nbytes)
+    N.call("snpmi_dev_grm_extract", tiles.p, n, N.DT_F32, didx.p, ns, didx.p, ns, 1, 1.0, dout.p)
+    K = np.empty((ns, ns), dtype=np.float32)
+    N.call("snpmi_memcpy_d2h", N.ptr(K), dout.p, K.nbytes)
+    del tiles
+    host = np.empty((m, pitch), dtype=np.uint8)
+    N.call("snpmi_memcpy_d2h", N.ptr(host), packed.p, host.nbytes)
+    del packed
+    body = np.ascontiguousarray(host[:, :(n + 3) // 4]).reshape(-1)
+    del host
+    stats = O.snp_stats(body, n, m)
+    Zs = O.decode(body, n, m, iid_index=sample, dtype=np.float64)
+    O.standardize_native(Zs, use_stats=True, stats=stats)
+    Kref = Zs.dot(Zs.T)
+    scale = np.abs(np.diag(Kref)).max()
+    err = float(np.abs(K.astype(np.float64) - Kref).max() / scale)
+    assert err <= 1e-5, "cfg4 GRM sample vs f64 oracle: %g" % err
+    np.testing.assert_allclose(np.diag(K), np.diag(Kref), rtol=1e-5)
+    assert np.array_equal(K, K.T)
