@@ -20,6 +20,7 @@ Metric (BASELINE.json): "SNPs/sec standardized (500k x 1M) + GRM GF/s at 1/2/4/8
 Run: python bench.py [--gpus N --steps K --warmup W]; N > 1 under torch.distributed.run.
 """
 import argparse
+import contextlib
 import ctypes
 import json
 import os
@@ -66,6 +67,20 @@ def parse():
     return p.parse_args()
 
 
+@contextlib.contextmanager
+def stdout_to_stderr():
+    """RCCL prints a version banner on the C stdout (fd 1) around communicator setup; the bench's
+    stdout must carry only its one JSON line."""
+    sys.stdout.flush()
+    saved = os.dup(1)
+    os.dup2(2, 1)
+    try:
+        yield
+    finally:
+        os.dup2(saved, 1)
+        os.close(saved)
+
+
 class Dist:
     """Control plane for one process per GPU WITHOUT torch: importing torch would load its own
     libamdhip64.so.7 (ROCm 7.0) next to libsnpmi's (ROCm 7.2) -- same SONAME, two runtimes.
@@ -88,7 +103,8 @@ class Dist:
             path = os.path.join(tempfile.gettempdir(), key)
             uid = (ctypes.c_uint8 * 128)()
             if self.rank == 0:
-                N.call("snpmi_rccl_unique_id", uid, 128)
+                with stdout_to_stderr():
+                    N.call("snpmi_rccl_unique_id", uid, 128)
                 with open(path + ".tmp", "wb") as f:
                     f.write(bytes(uid))
                 os.replace(path + ".tmp", path)
@@ -100,7 +116,8 @@ class Dist:
                     time.sleep(0.05)
                 with open(path, "rb") as f:
                     uid = (ctypes.c_uint8 * 128).from_buffer_copy(f.read(128))
-            N.call("snpmi_rccl_init", self.world, self.rank, uid, 128)
+            with stdout_to_stderr():
+                N.call("snpmi_rccl_init", self.world, self.rank, uid, 128)
             self.rccl = True
             self.barrier()
             if self.rank == 0:
@@ -119,7 +136,8 @@ class Dist:
 
     def close(self):
         if self.rccl:
-            self.N.call("snpmi_rccl_destroy")
+            with stdout_to_stderr():
+                self.N.call("snpmi_rccl_destroy")
 
 
 class Dev:

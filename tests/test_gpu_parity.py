@@ -676,3 +676,24 @@ def test_generic_block_loop_keeps_k_on_device(block_size, order):
         ref += z.dot(z.T)
     grm_close(K, ref, 1e-10)
     assert K.flags[order + "_CONTIGUOUS"]
+
+
+def test_grm_count_a1_and_trained(syrk_variant):
+    """count_A1=True flips every genotype (x -> 2 - x, test.py:226-232), so z -> -z and K is
+    unchanged; the oracle built on the count_A1 decode agrees.  A trained standardizer (stats of
+    SNPs 0..599 applied to the same SNPs through use_stats) reproduces the untrained K."""
+    for dtype, tol in ((np.float32, 1e-5), (np.float64, 1e-10)):
+        for std in (Unit(), Beta(1, 25)):
+            k1 = bed("n300", count_A1=True)[:, :600].read_kernel(std, dtype=dtype).val
+            k0 = bed("n300")[:, :600].read_kernel(std, dtype=dtype).val
+            Z = O.decode(body("n300"), 300, 1015, count_A1=True, sid_index=np.arange(600))
+            if isinstance(std, Unit):
+                O.standardize_native(Z)
+            else:
+                O.standardize_native(Z, is_beta=True, a=1.0, b=25.0)
+            ref = Z.dot(Z.T)
+            grm_close(k1, ref, tol)
+            grm_close(k0, ref, tol)
+    _, trained = bed("n300")[:, :600].read(dtype=np.float64).standardize(Unit(), return_trained=True)
+    kt = SnpKernel(bed("n300")[:, :600], trained).read(dtype=np.float32).val
+    grm_close(kt, bed("n300")[:, :600].read_kernel(Unit(), dtype=np.float64).val, 1e-5)
