@@ -729,7 +729,11 @@ __global__ __launch_bounds__(512, 1) void k_syrk_bf3(const uint8_t* __restrict__
     const int wm = wave >> 2, wn = wave & 3;
     // loader role: panel, SNP row k of the stage, 16-iid group d
     const int lp = t >> 8, lk = (t >> 4) & 15, ld_ = t & 15;
-    const int hfirst = (ld_ >> 2) & 1;
+    // the two 16-B halves of a 32-B segment are stored swapped in segments with bit 2 set
+    // (sw = (d >> 2) & 1): the 8 lanes of a ds_write_b128 group then hit 8 distinct 16-B bank
+    // slots.  (Ordering the two stores instead does not work: the compiler reorders them --
+    // PMC showed 8 conflict cycles per ds_write_b128.)  The transposed reads undo the swap.
+    const int sw = (ld_ >> 2) & 1;
     // packed codes of (SNP k0 + lk, iids base + 16 ld_ ..): walked by pointer, clamped to the last
     // SNP past kdim (its values are zeroed through the LUT: lut3 is zero-padded to a multiple of BK)
     const uint8_t* wp = P + (lp ? j0 : i0) / 4 + 4 * ld_ + (uint64_t)lk * pitch;
@@ -738,6 +742,11 @@ __global__ __launch_bounds__(512, 1) void k_syrk_bf3(const uint8_t* __restrict__
     // transposed-read role: lane 4q+p of group g supplies row 8(g>>1)+q, cols 16(g&1)+4p
     const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
     const int rd_off = (8 * (g >> 1) + q) * B3_RS + 16 * (g & 1) + 4 * pp;
+    // segment of a fragment column c (multiple of 32) + 16(g&1): swapped iff bit 2 of c/16 + (g&1)
+    // is set, i.e. for A (c = wm*128 + 32x) iff x >= 2, for B (c = wn*64 + 32y) iff wn is odd;
+    // the lane's 8-byte piece then moves by +-8 bf16 (first / second half)
+    const int dswz = (pp >> 1) ? -8 : 8;
+    const int rd_offB = rd_off + ((wn & 1) ? dswz : 0);
 
     f32x16 acc[4][2];
 #pragma unroll
@@ -774,13 +783,8 @@ __global__ __launch_bounds__(512, 1) void k_syrk_bf3(const uint8_t* __restrict__
         v1.z = __builtin_amdgcn_perm(hi, lo, sel[6]);
         v1.w = __builtin_amdgcn_perm(hi, lo, sel[7]);
         uint4* r4 = reinterpret_cast<uint4*>(S + (lp * 3 + pl) * B3_PLANE + lk * B3_RS + 16 * ld_);
-        if (hfirst) {
-            r4[1] = v1;
-            r4[0] = v0;
-        } else {
-            r4[0] = v0;
-            r4[1] = v1;
-        }
+        r4[sw] = v0;
+        r4[sw ^ 1] = v1;
     };
     auto store = [&](short* S, const B3Regs& r) {
         uint32_t sel[8];
@@ -788,8 +792,8 @@ __global__ __launch_bounds__(512, 1) void k_syrk_bf3(const uint8_t* __restrict__
 #pragma unroll
         for (int pl = 0; pl < 3; pl++) store_plane(S, pl, r, sel);
     };
-    auto frag = [&](const short* S, int panel, int pl, int col) -> bf16x8_t {
-        const short* b = S + (panel * 3 + pl) * B3_PLANE + rd_off + col;
+    auto frag = [&](const short* S, int panel, int pl, int col, int off) -> bf16x8_t {
+        const short* b = S + (panel * 3 + pl) * B3_PLANE + off + col;
         const i16x4_t r0 = lds_tr16(b), r1 = lds_tr16(b + 4 * B3_RS);
         return __builtin_bit_cast(bf16x8_t, (i16x8_t)__builtin_shufflevector(r0, r1, 0, 1, 2, 3, 4, 5, 6, 7));
     };
@@ -800,13 +804,13 @@ __global__ __launch_bounds__(512, 1) void k_syrk_bf3(const uint8_t* __restrict__
 #pragma unroll
         for (int pl = 0; pl < 3; pl++)
 #pragma unroll
-            for (int y = 0; y < 2; y++) b[pl][y] = frag(S, 1, pl, wn * 64 + 32 * y);
+            for (int y = 0; y < 2; y++) b[pl][y] = frag(S, 1, pl, wn * 64 + 32 * y, rd_offB);
         int gidx = 0;
 #pragma unroll
         for (int pa = 0; pa < 3; pa++) {
             bf16x8_t a[4];
 #pragma unroll
-            for (int x = 0; x < 4; x++) a[x] = frag(S, 0, pa, wm * 128 + 32 * x);
+            for (int x = 0; x < 4; x++) a[x] = frag(S, 0, pa, wm * 128 + 32 * x, x >= 2 ? rd_off + dswz : rd_off);
 #pragma unroll
             for (int pb = 0; pb + pa <= 2; pb++) {
 #pragma unroll
@@ -1298,13 +1302,17 @@ void launch_syrk_packed_bf3(const uint8_t* packed, uint64_t pitch, uint64_t n, u
         if (!accumulate) SNPMI_HIP(hipMemsetAsync(tiles, 0, n_tiles_upper(n) * BM * BM * sizeof(float), st));
         return;
     }
-    // MI355X, N=50k, 10k SNPs (tools/ubench.py syrk): 30 = 293.6 TFLOP/s, 31 = 302.4,
-    // default (interleaved loader + XCD remap) = 309.3, 39 (no loader, ablation) = 369.5
+    // MI355X, N=50k, 10k SNPs (tools/ubench.py syrk, one box, profiles/r01g): default (loader
+    // interleaved between the MFMA groups, plain block order) 315.3 TFLOP/s; 30 (expansion
+    // after the MFMAs) 309.2; 31 (+ XCD remap) / 32 (interleaved + XCD remap) 304-307;
+    // 39 (no loader, ablation) 382.5.  A stagger of the loader between the two waves of each
+    // SIMD lost (298).
     switch (g_variant_syrk) {
         case 30: f32w::k_syrk_bf3<><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, lut3, tiles, accumulate); break;
         case 31: f32w::k_syrk_bf3<false, true><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, lut3, tiles, accumulate); break;
+        case 32: f32w::k_syrk_bf3<false, true, 1><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, lut3, tiles, accumulate); break;
         case 39: f32w::k_syrk_bf3<false, true, 9><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, lut3, tiles, accumulate); break;
-        default: f32w::k_syrk_bf3<false, true, 1><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, lut3, tiles, accumulate);
+        default: f32w::k_syrk_bf3<false, false, 1><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, lut3, tiles, accumulate);
     }
     SNPMI_HIP(hipGetLastError());
 }
@@ -1320,8 +1328,8 @@ void launch_syrk_packed_bf3_part(const uint8_t* packed, uint64_t pitch, uint64_t
         if (!accumulate) SNPMI_HIP(hipMemsetAsync(blocks, 0, nloc * 256 * 256 * sizeof(float), st));
         return;
     }
-    f32w::k_syrk_bf3<true, true, 1><<<(unsigned)nloc, 512, 0, st>>>(packed, pitch, n, m, lut3, blocks, accumulate,
-                                                                    (uint32_t)rank, (uint32_t)world);
+    f32w::k_syrk_bf3<true, false, 1><<<(unsigned)nloc, 512, 0, st>>>(packed, pitch, n, m, lut3, blocks, accumulate,
+                                                                     (uint32_t)rank, (uint32_t)world);
     SNPMI_HIP(hipGetLastError());
 }
 
