@@ -824,30 +824,28 @@ __global__ __launch_bounds__(512, 1) void k_syrk_bf3(const uint8_t* __restrict__
     };
 
     if constexpr (MODE == 1) {
-        // two register sets used alternately (stage parity): ra holds the codes of stage s+1
-        // while rb receives stage s+2, then the roles swap -- no register copies
-        B3Regs ra, rb;
-        load(0, ra);
-        store(lds, ra);
-        if (nst > 1) load(1, ra);
+        // one register set: the codes/LUT of stage s+1 are expanded and stored plane by plane
+        // after MFMA groups 0-3 of stage s, and right after the last plane the loads of stage
+        // s+2 are issued into the same registers -- they have MFMA groups 4-5, the barrier and
+        // group 0 of the next stage to arrive
+        B3Regs r;
+        load(0, r);
+        store(lds, r);
+        if (nst > 1) load(1, r);
         __syncthreads();
-        auto step = [&](uint64_t s, B3Regs& rn, B3Regs& rf) {
+        for (uint64_t s = 0; s < nst; s++) {
             short* cur = lds + (s & 1) * B3_STAGE;
             short* nxt = lds + ((s + 1) & 1) * B3_STAGE;
             const bool more = s + 1 < nst;
-            if (s + 2 < nst) load(s + 2, rf);
             uint32_t sel[8];
             compute(cur, [&](int gi) {
                 if (more) {
-                    if (gi == 0) make_sel(rn.w, sel);
-                    else if (gi <= 3) store_plane(nxt, gi - 1, rn, sel);
+                    if (gi == 0) make_sel(r.w, sel);
+                    else if (gi <= 3) store_plane(nxt, gi - 1, r, sel);
+                    if (gi == 3 && s + 2 < nst) load(s + 2, r);
                 }
             });
             __syncthreads();
-        };
-        for (uint64_t s = 0; s < nst; s += 2) {
-            step(s, ra, rb);
-            if (s + 1 < nst) step(s + 1, rb, ra);
         }
     } else {
         B3Regs r;
@@ -1302,11 +1300,10 @@ void launch_syrk_packed_bf3(const uint8_t* packed, uint64_t pitch, uint64_t n, u
         if (!accumulate) SNPMI_HIP(hipMemsetAsync(tiles, 0, n_tiles_upper(n) * BM * BM * sizeof(float), st));
         return;
     }
-    // MI355X, N=50k, 10k SNPs (tools/ubench.py syrk, one box, profiles/r01g): default (loader
-    // interleaved between the MFMA groups, plain block order) 315.3 TFLOP/s; 30 (expansion
-    // after the MFMAs) 309.2; 31 (+ XCD remap) / 32 (interleaved + XCD remap) 304-307;
-    // 39 (no loader, ablation) 382.5.  A stagger of the loader between the two waves of each
-    // SIMD lost (298).
+    // MI355X, N=50k, 10k SNPs (tools/ubench.py syrk, 7 interleaved rounds, profiles/r01g):
+    // default (loader interleaved between the MFMA groups) 302.9 TFLOP/s, + XCD remap (32)
+    // 303.3, expansion after the MFMAs (30) 306.6, + XCD remap (31) 305.3 -- equal within run
+    // noise; 39 (no loader, ablation) 380-382, at a 8% higher clock (PMC GRBM_GUI_ACTIVE).
     switch (g_variant_syrk) {
         case 30: f32w::k_syrk_bf3<><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, lut3, tiles, accumulate); break;
         case 31: f32w::k_syrk_bf3<false, true><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, lut3, tiles, accumulate); break;
