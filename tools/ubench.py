@@ -18,12 +18,13 @@ from bench import Dev, Events, synth  # noqa: E402
 
 def decode(args):
     n, m = args.n, args.m
+    dt, esz = {"f32": (N.DT_F32, 4), "f64": (N.DT_F64, 8)}[args.dtype]
     pitch = N.lib().snpmi_packed_pitch(n)
     ld = (n + 15) // 16 * 16
     packed = Dev(N, pitch * m)
     synth(N, packed.p, pitch, n, 0, m, 3, 0.01)
-    lut, st, out = Dev(N, m * 16), Dev(N, m * 8), Dev(N, m * ld * 4)
-    N.call("snpmi_dev_snp_stats", packed.p, pitch, n, m, 0, N.STD_UNIT, 0.0, 0.0, 0, N.DT_F32, st.p, lut.p)
+    lut, st, out = Dev(N, m * 4 * esz), Dev(N, m * 2 * esz), Dev(N, m * ld * esz)
+    N.call("snpmi_dev_snp_stats", packed.p, pitch, n, m, 0, N.STD_UNIT, 0.0, 0.0, 0, dt, st.p, lut.p)
     variants = [int(v) for v in args.variants.split(",")]
     ev = Events(N, 2)
     res = {v: [] for v in variants}
@@ -33,8 +34,8 @@ def decode(args):
             if v >= 0:
                 N.call("snpmi_set_kernel_variant", b"decode", v)
                 ev.record(0)
-                N.call("snpmi_dev_snp_stats", packed.p, pitch, n, m, 0, N.STD_UNIT, 0.0, 0.0, 0, N.DT_F32, st.p, lut.p)
-                N.call("snpmi_dev_decode", packed.p, pitch, n, m, lut.p, N.DT_F32, 0, out.p, ld)
+                N.call("snpmi_dev_snp_stats", packed.p, pitch, n, m, 0, N.STD_UNIT, 0.0, 0.0, 0, dt, st.p, lut.p)
+                N.call("snpmi_dev_decode", packed.p, pitch, n, m, lut.p, dt, 0, out.p, ld)
                 ev.record(1)
             else:
                 ev.record(0)
@@ -43,15 +44,15 @@ def decode(args):
                 ev.record(1)
             res[v].append(ev.ms(0, 1))
             if rnd == 0:
-                chk = np.empty(4 * ld, dtype=np.float32)
-                N.call("snpmi_memcpy_d2h", N.ptr(chk), ctypes.c_void_p(out.p.value + (m - 4) * ld * 4), chk.nbytes)
+                chk = np.empty(4 * ld, dtype=np.float32 if esz == 4 else np.float64)
+                N.call("snpmi_memcpy_d2h", N.ptr(chk), ctypes.c_void_p(out.p.value + (m - 4) * ld * esz), chk.nbytes)
                 if ref is None:
                     ref = chk.copy()
                 assert np.array_equal(chk, ref), "variant %d output differs" % v
-    nbytes = m * ((n + 3) // 4 + 4 * n)
+    nbytes = m * ((n + 3) // 4 + esz * n)
     for v in variants:
         t = np.median(res[v])
-        print(json.dumps({"kernel": "stats+decode" if v >= 0 else "fused", "variant": v, "median_ms": t, "min_ms": min(res[v]),
+        print(json.dumps({"kernel": "stats+decode" if v >= 0 else "fused", "dtype": args.dtype, "variant": v, "median_ms": t, "min_ms": min(res[v]),
                           "GBps": nbytes / t / 1e6, "frac_8TBs": nbytes / t / 1e6 / 8000}))
 
 
