@@ -254,6 +254,23 @@ def leg_standardize(N, args, dist):
     full_block_bytes = B * ((n + 3) // 4 + 4 * n)
     total_bytes = m * ((n + 3) // 4 + 4 * n)
     achieved_gbs = (total_bytes / nblk) / (dec_mean_ms * 1e-3) / 1e9
+    # measured copy peak (untimed): device-to-device copies of the block buffer's size
+    cbytes = min(B * ld * 4, pitch * m)
+    N.call("snpmi_dev_memcpy_d2d", out.p, packed.p, cbytes)
+    N.call("snpmi_stream_sync")
+    ev.record(0)
+    for _ in range(5):
+        N.call("snpmi_dev_memcpy_d2d", out.p, packed.p, cbytes)
+    ev.record(1)
+    N.call("snpmi_stream_sync")
+    copy_gbs = 2 * 5 * cbytes / (ev.ms(0, 1) * 1e-3) / 1e9
+    # write-only stream (the decode writes 16 B per 1 B it reads): hipMemset fill of the buffer
+    ev.record(0)
+    for _ in range(5):
+        N.call("snpmi_dev_memset", out.p, 0, B * ld * 4)
+    ev.record(1)
+    N.call("snpmi_stream_sync")
+    fill_gbs = 5 * B * ld * 4 / (ev.ms(0, 1) * 1e-3) / 1e9
     sample = gpu_cols = None
     if dist.rank == 0 and not args.skip_cpu:
         # parity sample: the first 512 columns, re-decoded by the same kernels (untimed)
@@ -264,6 +281,7 @@ def leg_standardize(N, args, dist):
         gpu_cols = np.empty((ncols, ld), dtype=np.float32)
         N.call("snpmi_memcpy_d2h", N.ptr(gpu_cols), out.p, gpu_cols.nbytes)
     res = dict(wall=wall, step_ms=step_ms, dec_mean_ms=dec_mean_ms, achieved_gbs=achieved_gbs, fused=fused,
+               copy_gbs=copy_gbs, fill_gbs=fill_gbs,
                full_block_bytes=full_block_bytes, launches=launches, nblk=nblk, pitch=pitch, sample=sample,
                gpu_cols=gpu_cols)
     ev.destroy()
@@ -583,7 +601,9 @@ def main():
                          "kernel": ("k_decode_std_lds_f32 (stats + decode, packed column staged in LDS)"
                                     if r1["fused"] else "k_decode_f<float> (after k_snp_stats)"),
                          "per_launch_bytes": r1["full_block_bytes"],
-                         "mean_launch_ms": r1["dec_mean_ms"]},
+                         "mean_launch_ms": r1["dec_mean_ms"],
+                         "measured_stream_GBps": {"copy_16B_nt (1 read : 1 write)": r1["copy_gbs"],
+                                                  "hipMemset fill (write only)": r1["fill_gbs"]}},
             "cpu_baseline": cpu,
             "parity": parity,
             "grm": grm,

@@ -197,6 +197,8 @@ int snpmi_host_free(void* ptr);
 int snpmi_dev_memset(void* ptr, int value, uint64_t bytes);
 int snpmi_memcpy_h2d(void* dst, const void* src, uint64_t bytes);
 int snpmi_memcpy_d2h(void* dst, const void* src, uint64_t bytes);
+/* device -> device on the library stream (asynchronous; bench.py's measured copy peak) */
+int snpmi_dev_memcpy_d2d(void* dst, const void* src, uint64_t bytes);
 int snpmi_stream_sync(void);
 int snpmi_event_create(void** ev);
 int snpmi_event_destroy(void* ev);

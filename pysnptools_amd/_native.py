@@ -79,6 +79,7 @@ _SIGS = {
     "snpmi_dev_memset": [_vp, _i32, _u64],
     "snpmi_memcpy_h2d": [_vp, _vp, _u64],
     "snpmi_memcpy_d2h": [_vp, _vp, _u64],
+    "snpmi_dev_memcpy_d2d": [_vp, _vp, _u64],
     "snpmi_stream_sync": [],
     "snpmi_event_create": [ctypes.POINTER(ctypes.c_void_p)],
     "snpmi_event_destroy": [_vp],

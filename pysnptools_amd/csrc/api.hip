@@ -1098,6 +1098,16 @@ int snpmi_memcpy_d2h(void* dst, const void* src, uint64_t bytes) {
         SNPMI_HIP(hipStreamSynchronize(stream()));
     });
 }
+int snpmi_dev_memcpy_d2d(void* dst, const void* src, uint64_t bytes) {
+    return guarded([&] {
+        const bool aligned = reinterpret_cast<uintptr_t>(dst) % 16 == 0 && reinterpret_cast<uintptr_t>(src) % 16 == 0;
+        const uint64_t body = aligned ? bytes / 16 * 16 : 0;
+        if (body) launch_copy16(src, dst, body, stream());
+        if (bytes > body)
+            SNPMI_HIP(hipMemcpyAsync((uint8_t*)dst + body, (const uint8_t*)src + body, bytes - body,
+                                     hipMemcpyDeviceToDevice, stream()));
+    });
+}
 int snpmi_stream_sync(void) {
     return guarded([&] { SNPMI_HIP(hipStreamSynchronize(stream())); });
 }

@@ -1176,6 +1176,32 @@ void launch_sumsq(const void* p, uint64_t count, int dtype, double* out_dev, hip
     SNPMI_LAUNCH_CHECK();
 }
 
+// Streaming device copy (16-B loads/stores, 4 in flight per thread, grid-stride): the measured
+// HBM copy peak bench.py reports beside the decode roofline (hipMemcpy D2D's blit kernel
+// reached only 4.9 TB/s on the same box).
+__global__ __launch_bounds__(kBlock) void k_copy16(const u32x4_t* __restrict__ src, u32x4_t* __restrict__ dst,
+                                                   uint64_t n16) {
+    const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+    uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    for (; i + 3 * stride < n16; i += 4 * stride) {
+        const u32x4_t a = __builtin_nontemporal_load(src + i), b = __builtin_nontemporal_load(src + i + stride);
+        const u32x4_t c = __builtin_nontemporal_load(src + i + 2 * stride);
+        const u32x4_t d = __builtin_nontemporal_load(src + i + 3 * stride);
+        __builtin_nontemporal_store(a, dst + i);
+        __builtin_nontemporal_store(b, dst + i + stride);
+        __builtin_nontemporal_store(c, dst + i + 2 * stride);
+        __builtin_nontemporal_store(d, dst + i + 3 * stride);
+    }
+    for (; i < n16; i += stride) __builtin_nontemporal_store(__builtin_nontemporal_load(src + i), dst + i);
+}
+
+void launch_copy16(const void* src, void* dst, uint64_t bytes, hipStream_t st) {
+    const uint64_t n16 = bytes / 16;
+    if (n16 == 0) return;
+    k_copy16<<<grid_for(ceil_div(n16, 4), kBlock, 256 * 8 * 4), kBlock, 0, st>>>((const u32x4_t*)src, (u32x4_t*)dst, n16);
+    SNPMI_LAUNCH_CHECK();
+}
+
 void launch_synth(uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t sid0, uint64_t m, uint64_t seed,
                   double miss_rate, const double* maf_x, const double* maf_cdf, int n_pts, hipStream_t st) {
     if (m == 0) return;

@@ -107,6 +107,7 @@ void launch_grm_trace(const void* tiles, uint64_t n, int dtype, double* trace_de
 void launch_dense_scale(void* p, uint64_t count, int dtype, double scale, hipStream_t st);
 void launch_sumsq(const void* p, uint64_t count, int dtype, double* out_dev, hipStream_t st);
 void launch_dense_trace(const void* K, uint64_t n, int dtype, double* trace_dev, hipStream_t st);
+void launch_copy16(const void* src, void* dst, uint64_t bytes, hipStream_t st);  // 16-B aligned
 void launch_synth(uint8_t* packed, uint64_t pitch, uint64_t n_iid, uint64_t sid0, uint64_t n_sid, uint64_t seed,
                   double miss_rate, const double* maf_x_dev, const double* maf_cdf_dev, int n_pts, hipStream_t st);
 void launch_encode(const void* val, int dtype, int order_c, uint64_t ld, uint64_t n, uint64_t m, int count_a1,
