@@ -290,8 +290,9 @@ def leg_standardize(N, args, dist):
     return res
 
 
-def cpu_baseline_standardize(args, sample, pitch):
-    """Oracle C/OpenMP decode + one-pass Unit standardize on a bounded sample (rank 0)."""
+def cpu_baseline_standardize(args, sample, pitch, timed=True):
+    """Oracle C/OpenMP decode + one-pass Unit standardize on a bounded sample (rank 0); with
+    timed=False (N > 1: the baseline is reported at N = 1 only) one untimed pass for parity."""
     from oracle import oracle as O
 
     n = args.n_iid
@@ -299,6 +300,9 @@ def cpu_baseline_standardize(args, sample, pitch):
     bpc = (n + 3) // 4
     body = np.ascontiguousarray(sample[:, :bpc]).reshape(-1)
     ncols = sample.shape[0]
+    if not timed:
+        ref, _ = O.decode_standardize(body, n, ncols, dtype=np.float32, num_threads=threads)
+        return ref, None
     done, t0 = 0, time.perf_counter()
     while True:
         ref, _ = O.decode_standardize(body, n, ncols, dtype=np.float32, num_threads=threads)
@@ -576,12 +580,12 @@ def main():
         cpu = None
         parity = None
         if not args.skip_cpu and r1["sample"] is not None:
-            ref, cpu = cpu_baseline_standardize(args, r1["sample"], r1["pitch"])
+            ref, cpu = cpu_baseline_standardize(args, r1["sample"], r1["pitch"], timed=dist.world == 1)
             same = np.array_equal(r1["gpu_cols"][:, :args.n_iid].T, ref)
             parity = {"check": "first %d SNP columns x %d iids: GPU stats+decode vs oracle decode+one-pass "
                                "Unit (f32)" % (ref.shape[1], ref.shape[0]), "bit_exact": bool(same)}
             if grm is not None:
-                grm["cpu_baseline"] = cpu_baseline_grm(args)
+                grm["cpu_baseline"] = cpu_baseline_grm(args) if dist.world == 1 else None
                 if r2.get("parity_sample") is not None:
                     grm["parity"] = grm_parity(args, *r2["parity_sample"])
         n = args.n_iid
