@@ -596,13 +596,12 @@ static void grm_finish(Device& d, const T* tiles, uint64_t n, int diag_k_to_n, d
     SNPMI_HIP(hipStreamSynchronize(d.stream));
 }
 
-// Accumulate the SNP columns of one .bed into upper-triangle tiles (first = overwrite).
-// Returns true if anything was written.
-template <typename T>
-static bool grm_add_bed(Device& d, T* tiles, bool first, const char* path, uint64_t n_iid, uint64_t n_sid,
-                        int count_a1, const uint64_t* iid_idx, uint64_t n_out_iid, const uint64_t* sid_idx,
-                        uint64_t n_out_sid, int std_kind, double a, double b, int use_stats, T* stats,
-                        int num_threads) {
+// Stream the SNP columns of one .bed through stats and `syrk(packed, pitch, n, cnt, lut,
+// accumulate)` (first = overwrite).  Returns true if anything was written.
+template <typename T, class Syrk>
+static bool grm_stream_bed(Device& d, bool first, const char* path, uint64_t n_iid, uint64_t n_sid, int count_a1,
+                           const uint64_t* iid_idx, uint64_t n_out_iid, const uint64_t* sid_idx, uint64_t n_out_sid,
+                           int std_kind, double a, double b, int use_stats, T* stats, int num_threads, Syrk&& syrk) {
     BedMap m;
     open_bed(m, path, n_iid, n_sid);
     const uint64_t n_out = iid_idx ? n_out_iid : n_iid;
@@ -629,7 +628,7 @@ static bool grm_add_bed(Device& d, T* tiles, bool first, const char* path, uint6
             SNPMI_HIP(hipMemcpyAsync(st_dev, st_host + 2 * c0, cnt * 2 * sizeof(T), hipMemcpyHostToDevice, d.stream));
         launch_snp_stats(packed, p.pitch_out, n_out, cnt, count_a1, std_kind, a, b, use_stats, dt, st_dev, lut,
                          d.stream);
-        syrk_packed_auto(d, packed, p.pitch_out, n_out, cnt, lut, dt, tiles, !(first && !wrote));
+        syrk(packed, p.pitch_out, n_out, cnt, (const T*)lut, !(first && !wrote));
         wrote = true;
         if (has_stats && !use_stats)
             SNPMI_HIP(hipMemcpyAsync(st_host + 2 * c0, st_dev, cnt * 2 * sizeof(T), hipMemcpyDeviceToHost, d.stream));
@@ -640,6 +639,19 @@ static bool grm_add_bed(Device& d, T* tiles, bool first, const char* path, uint6
         for (uint64_t j = 0; j < m_out; j++) stats[2 * j] = stats[2 * j + 1] = (T)NAN;
     }
     return wrote;
+}
+
+// Accumulate the SNP columns of one .bed into the replicated upper-triangle tiles.
+template <typename T>
+static bool grm_add_bed(Device& d, T* tiles, bool first, const char* path, uint64_t n_iid, uint64_t n_sid,
+                        int count_a1, const uint64_t* iid_idx, uint64_t n_out_iid, const uint64_t* sid_idx,
+                        uint64_t n_out_sid, int std_kind, double a, double b, int use_stats, T* stats,
+                        int num_threads) {
+    return grm_stream_bed<T>(d, first, path, n_iid, n_sid, count_a1, iid_idx, n_out_iid, sid_idx, n_out_sid, std_kind,
+                             a, b, use_stats, stats, num_threads,
+                             [&](const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t cnt, const T* lut, bool acc) {
+                                 syrk_packed_auto(d, packed, pitch, n, cnt, lut, DT<T>::v, tiles, acc);
+                             });
 }
 
 template <typename T>
@@ -1210,6 +1222,36 @@ int snpmi_grm_part_coords(uint64_t n_iid, int part_rank, int part_world, uint64_
         while (j * (j + 1) / 2 > L) j--;
         if (row0) *row0 = (L - j * (j + 1) / 2) * 256;
         if (col0) *col0 = j * 256;
+    });
+}
+
+// cfg5 from a file (K too large to replicate): rank part_rank of part_world streams EVERY SNP of
+// the .bed (stats need all iids of a SNP; each rank computes them itself -- no exchange) and
+// accumulates only its own 256x256 K blocks (snpmi_grm_part_coords) in HBM, then copies them to
+// blocks_out (n_local x 65536 f32, row-major blocks; may be a memory-mapped file).
+int snpmi_grm_part_bed_f32(const char* path, uint64_t n_iid, uint64_t n_sid, int count_a1, const uint64_t* iid_idx,
+                           uint64_t n_out_iid, const uint64_t* sid_idx, uint64_t n_out_sid, int std_kind, double a,
+                           double b, int use_stats, float* stats, int part_rank, int part_world, float* blocks_out,
+                           int num_threads) {
+    return guarded([&] {
+        std::lock_guard<std::recursive_mutex> lk(g_call_mutex);
+        SNPMI_REQUIRE(part_world >= 1 && part_rank >= 0 && part_rank < part_world, SNPMI_E_ARG, "bad rank / world");
+        const uint64_t n_out = iid_idx ? n_out_iid : n_iid;
+        const uint64_t nloc = grm_part_blocks(n_out, part_rank, part_world);
+        SNPMI_REQUIRE(blocks_out != nullptr || nloc == 0, SNPMI_E_ARG, "blocks_out is NULL");
+        Device& d = device();
+        const uint64_t bytes = std::max<uint64_t>(nloc, 1) * 256 * 256 * sizeof(float);
+        float* blocks = (float*)d.get(Device::S_TILES, bytes);
+        const bool wrote = grm_stream_bed<float>(
+            d, true, path, n_iid, n_sid, count_a1, iid_idx, n_out_iid, sid_idx, n_out_sid, std_kind, a, b, use_stats,
+            stats, num_threads,
+            [&](const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t cnt, const float* lut, bool acc) {
+                syrk_packed_part_auto(d, packed, pitch, n, cnt, lut, part_rank, part_world, blocks, acc);
+            });
+        if (!wrote) SNPMI_HIP(hipMemsetAsync(blocks, 0, bytes, d.stream));
+        const size_t bb = 256 * 256 * sizeof(float);  // one block per "row" of the pinned-bounce copy
+        if (nloc) d2h_rows(d, blocks_out, bb, blocks, bb, bb, nloc, resolve_threads(num_threads));
+        SNPMI_HIP(hipStreamSynchronize(d.stream));
     });
 }
 

@@ -117,3 +117,62 @@ def _allreduce_host(N, arr):
     finally:
         N.call("snpmi_dev_free", dev)
     return buf.astype(arr.dtype)
+
+
+def grm_partitioned(reader, standardizer, rank, world, out=None, num_threads=None):
+    """cfg5 GRM of a Bed (or a subset of one) too large to replicate: K is
+    partitioned over ``world`` ranks as the 256x256 blocks of its upper triangle
+    (``snpmi_grm_part_coords``); this rank streams every selected SNP through the fused
+    decode -> standardize -> bf16x3 MFMA SYRK and keeps only its own blocks -- no collective.
+    Stats are computed per rank from all iids (identical on every rank).
+
+    Returns (blocks [n_local, 256, 256] float32 -- ``out`` if given, e.g. an ``np.memmap`` of a
+    file --, coords [n_local, 2] int64 = (row0, col0) of each block, trained standardizer).
+    Entries of a block beyond iid n-1 are padding."""
+    import ctypes
+
+    import numpy as np
+
+    from pysnptools_amd import _native as N
+    from pysnptools_amd.snpreader.bed import Bed
+    from pysnptools_amd.snpreader.snpreader import _resolve, _trained_from
+    from pysnptools_amd.standardizer.standardizer import _std_args
+    from pysnptools_amd.util import get_num_threads
+
+    args = _std_args(standardizer)
+    assert args is not None, "grm_partitioned supports Unit/Beta/UnitTrained/BetaTrained/Identity"
+    kind, a, b, use_stats, _, _ = args
+    base, rows, cols = _resolve(reader)
+    assert isinstance(base, Bed), "grm_partitioned streams a Bed file"
+    base._run_once()
+    sid = reader.sid
+    n = reader.iid_count
+    stats = (np.ascontiguousarray(standardizer.stats_for(sid), dtype=np.float32) if use_stats
+             else np.empty((len(sid), 2), dtype=np.float32))
+    nloc = N.lib().snpmi_grm_part_blocks(n, rank, world)
+    if out is None:
+        out = np.empty((nloc, 256, 256), dtype=np.float32)
+    assert out.shape == (nloc, 256, 256) and out.dtype == np.float32 and out.flags["C_CONTIGUOUS"]
+    ri, ci = N.index_array(rows), N.index_array(cols)
+    N.call("snpmi_grm_part_bed_f32", base.filename.encode(), base.iid_count, base.sid_count,
+           int(bool(base.count_A1)), N.ptr(ri), n, N.ptr(ci), len(sid), kind, a, b, int(use_stats), N.ptr(stats),
+           rank, world, N.ptr(out), get_num_threads(num_threads))
+    coords = np.empty((nloc, 2), dtype=np.int64)
+    r0, c0 = ctypes.c_uint64(), ctypes.c_uint64()
+    for k in range(nloc):
+        N.call("snpmi_grm_part_coords", n, rank, world, k, ctypes.byref(r0), ctypes.byref(c0))
+        coords[k] = (r0.value, c0.value)
+    return out, coords, _trained_from(standardizer, kind, a, b, sid, stats)
+
+
+def assemble_partitioned(parts, n):
+    """Full symmetric n x n K (float32) from every rank's (blocks, coords) -- for sizes that fit."""
+    import numpy as np
+
+    nb = (n + 255) // 256
+    K = np.zeros((nb * 256, nb * 256), dtype=np.float32)
+    for blocks, coords in parts:
+        for blk, (i, j) in zip(blocks, coords):
+            K[i:i + 256, j:j + 256] = blk
+            K[j:j + 256, i:i + 256] = blk.T
+    return K[:n, :n]

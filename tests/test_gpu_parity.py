@@ -697,3 +697,33 @@ def test_grm_count_a1_and_trained(syrk_variant):
     _, trained = bed("n300")[:, :600].read(dtype=np.float64).standardize(Unit(), return_trained=True)
     kt = SnpKernel(bed("n300")[:, :600], trained).read(dtype=np.float32).val
     grm_close(kt, bed("n300")[:, :600].read_kernel(Unit(), dtype=np.float64).val, 1e-5)
+
+
+@pytest.mark.parametrize("name,rows,world,std", [("n300", None, 1, "unit"), ("n300", None, 3, "beta"),
+                                                  ("toydata", slice(None, None, 2), 2, "unit"),
+                                                  ("toydata", slice(None, None, -1), 4, "unit")])
+def test_grm_partitioned_from_file(name, rows, world, std):
+    """cfg5 from a .bed (snpmi_grm_part_bed_f32 / shard.grm_partitioned): every rank's blocks,
+    assembled, == the replicated f32 GRM and the f64 oracle; trained stats == the Bed path's."""
+    from pysnptools_amd.shard import assemble_partitioned, grm_partitioned
+
+    b = bed(name)
+    r = b if rows is None else b[rows, :]
+    stdz = Unit() if std == "unit" else Beta(1, 25)
+    parts, trained = [], None
+    for rank in range(world):
+        blocks, coords, trained = grm_partitioned(r, stdz, rank, world)
+        parts.append((blocks, coords))
+    K = assemble_partitioned(parts, r.iid_count)
+    n, m = SHAPES[name]
+    iid = None if rows is None else np.arange(n)[rows]
+    Z = O.decode(body(name), n, m, iid_index=iid)
+    if std == "unit":
+        O.standardize_native(Z)
+    else:
+        O.standardize_native(Z, is_beta=True, a=1.0, b=25.0)
+    grm_close(K, Z.dot(Z.T), 1e-5)
+    Kr, tr = r.read_kernel(stdz, dtype=np.float32), None
+    np.testing.assert_allclose(K, Kr.val, rtol=0, atol=2e-6 * np.abs(np.diag(Kr.val)).max())
+    _, tr = r.read(dtype=np.float32).standardize(stdz, return_trained=True)
+    np.testing.assert_array_equal(np.asarray(trained.stats), np.asarray(tr.stats))

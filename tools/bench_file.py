@@ -52,6 +52,9 @@ def main():
     ap.add_argument("--read-block", type=int, default=10_000)
     ap.add_argument("--dir", default=tempfile.gettempdir())
     ap.add_argument("--seed", type=int, default=4)
+    ap.add_argument("--part-iid", type=int, default=100_000, help="cfg5 rehearsal: iids of the partitioned leg")
+    ap.add_argument("--part-sid", type=int, default=20_000)
+    ap.add_argument("--part-world", type=int, default=8)
     args = ap.parse_args()
     from pysnptools_amd import _native as N
     from pysnptools_amd.snpreader import Bed
@@ -93,6 +96,26 @@ def main():
         print(json.dumps({"bench": "SnpData.standardize(Unit()) in memory, f32", "n_iid": n, "snps": B,
                           "seconds": t_std, "snps_per_s": B / t_std,
                           "GB_per_s_each_way": v.val.nbytes / t_std / 1e9}), flush=True)
+    # cfg5 rehearsal from a file: K partitioned over W ranks (shard.grm_partitioned); rank 0's
+    # share timed on this GPU (every rank streams the whole file and owns ~1/W of the blocks)
+    from pysnptools_amd.shard import grm_partitioned
+
+    n5, m5, W = args.part_iid, args.part_sid, args.part_world
+    with tempfile.TemporaryDirectory(dir=args.dir) as d:
+        base = os.path.join(d, "cfg5")
+        write_bed(N, base, n5, m5, args.seed + 1)
+        bed = Bed(base + ".bed", count_A1=False)
+        bed.iid, bed.sid
+        grm_partitioned(bed[:, :1000], Unit(), 0, W)  # warm-up (scratch, page cache of the head)
+        t0 = time.perf_counter()
+        blocks, coords, _ = grm_partitioned(bed, Unit(), 0, W)
+        t5 = time.perf_counter() - t0
+        flops = n5 * (n5 + 1) * m5 / W
+        print(json.dumps({"bench": "file-backed partitioned GRM (cfg5 form, shard.grm_partitioned), rank 0 of %d" % W,
+                          "n_iid": n5, "n_sid": m5, "seconds": t5, "blocks_on_rank": len(coords),
+                          "K_GB_on_rank": blocks.nbytes / 1e9, "TFLOPs_end_to_end_per_rank": flops / t5 / 1e12,
+                          "projected_500k_x_1M_s_per_rank": t5 * (500_000 / n5) ** 2 * (1_000_000 / m5)}),
+              flush=True)
 
 
 if __name__ == "__main__":
