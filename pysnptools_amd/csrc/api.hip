@@ -522,8 +522,31 @@ static void for_z_blocks(Device& d, const uint8_t* packed, uint64_t pitch, uint6
 // f32 LUT, six bf16 products per f32 product, f32 accumulate): 309 TFLOP/s at N=50k, 10k SNPs
 // vs 136 for the f32-MFMA two-phase path (variant 20) -- tools/ubench.py syrk.
 // Variants: 30 = plain loader, 31 = + XCD remap, 39 = ablation (no loader); 4/5/20 = f32 MFMA.
+static int g_variant_syrk_split = 0;  // tuning hook: 0 = auto, 1 = off, S = force S slices
+
 static bool use_bf3(int dt) {
     return dt == SNPMI_DT_F32 && (g_variant_syrk == 0 || (g_variant_syrk >= 30 && g_variant_syrk < 40));
+}
+
+// split-K slices for the bf16x3 SYRK when the 256x256-block grid leaves CUs idle in its last
+// round: minimise rounds-per-slice ceil(g*S / CUs) / S, +1% per extra slice (partial sets + the
+// reduce), >= 1024 SNPs per slice.  Measured (tools/ubench.py syrk, m = 20k): N=10k 213 -> 242
+// TFLOP/s at S=4, N=5k 199 -> 217 at S=6 -- the slice counts this model picks.
+static int bf3_split_slices(uint64_t n, uint64_t m, int cus) {
+    if (g_variant_syrk == 35 || g_variant_syrk_split == 1) return 1;
+    if (g_variant_syrk_split > 1) return g_variant_syrk_split;
+    const uint64_t nb = ceil_div(n, 256), g = nb * (nb + 1) / 2, C = (uint64_t)std::max(cus, 1);
+    const double unsplit = (double)ceil_div(g, C);
+    int best = 1;
+    double best_cost = unsplit;
+    for (int S = 2; S <= 8 && m / (uint64_t)S >= 1024; S++) {
+        const double cost = (double)ceil_div(g * S, C) / S * (1.0 + 0.01 * (S - 1));
+        if (cost < best_cost) {
+            best = S;
+            best_cost = cost;
+        }
+    }
+    return best_cost < 0.97 * unsplit ? best : 1;
 }
 
 static const uint32_t* lut_bf3(Device& d, const float* lut, uint64_t m) {
@@ -535,8 +558,14 @@ static const uint32_t* lut_bf3(Device& d, const float* lut, uint64_t m) {
 static void syrk_packed_auto(Device& d, const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m,
                              const void* lut, int dt, void* tiles, int accumulate) {
     if (use_bf3(dt)) {
-        launch_syrk_packed_bf3(packed, pitch, n, m, lut_bf3(d, (const float*)lut, m), (float*)tiles, accumulate,
-                               d.stream);
+        const uint32_t* l3 = lut_bf3(d, (const float*)lut, m);
+        const int S = bf3_split_slices(n, m, d.cu_count);
+        if (S > 1) {
+            float* part = (float*)d.get(Device::S_ZBLK, (uint64_t)S * n_tiles_upper(n) * kTile * kTile * sizeof(float));
+            launch_syrk_packed_bf3_split(packed, pitch, n, m, l3, S, part, (float*)tiles, accumulate, d.stream);
+        } else {
+            launch_syrk_packed_bf3(packed, pitch, n, m, l3, (float*)tiles, accumulate, d.stream);
+        }
         return;
     }
     if (!use_two_phase(dt, n) || m == 0) {
@@ -856,6 +885,7 @@ int snpmi_set_kernel_variant(const char* kernel, int variant) {
         SNPMI_REQUIRE(kernel != nullptr, SNPMI_E_ARG, "kernel name is NULL");
         if (std::strcmp(kernel, "decode") == 0) g_variant_decode = variant;
         else if (std::strcmp(kernel, "syrk") == 0) g_variant_syrk = variant;
+        else if (std::strcmp(kernel, "syrk_split") == 0) g_variant_syrk_split = variant;
         else throw Error(SNPMI_E_ARG, std::string("unknown kernel ") + kernel);
     });
 }

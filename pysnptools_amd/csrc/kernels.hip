@@ -1202,6 +1202,25 @@ void launch_copy16(const void* src, void* dst, uint64_t bytes, hipStream_t st) {
     SNPMI_LAUNCH_CHECK();
 }
 
+// tiles = (accumulate ? tiles : 0) + sum of `slices` partial tile sets (split-K GRM), in order
+__global__ __launch_bounds__(kBlock) void k_tile_reduce(const f32x4_t* __restrict__ part, unsigned slices,
+                                                        uint64_t n4, f32x4_t* __restrict__ tiles, int accumulate) {
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n4; i += (uint64_t)gridDim.x * kBlock) {
+        f32x4_t acc = accumulate ? tiles[i] : (f32x4_t){0.f, 0.f, 0.f, 0.f};
+        for (unsigned s = 0; s < slices; s++) acc += part[s * n4 + i];
+        tiles[i] = acc;
+    }
+}
+
+void launch_tile_reduce(const float* partial, unsigned slices, uint64_t elems, float* tiles, int accumulate,
+                        hipStream_t st) {
+    const uint64_t n4 = elems / 4;  // tile sets are multiples of 128x128 floats
+    if (n4 == 0) return;
+    k_tile_reduce<<<grid_for(n4, kBlock, 256 * 16), kBlock, 0, st>>>((const f32x4_t*)partial, slices, n4,
+                                                                      (f32x4_t*)tiles, accumulate);
+    SNPMI_LAUNCH_CHECK();
+}
+
 void launch_synth(uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t sid0, uint64_t m, uint64_t seed,
                   double miss_rate, const double* maf_x, const double* maf_cdf, int n_pts, hipStream_t st) {
     if (m == 0) return;

@@ -128,6 +128,10 @@ uint64_t lut_bf3_entries(uint64_t m);  // 8 u32 each, zero-padded to a multiple 
 void launch_lut_bf3(const float* lut, uint64_t m, uint32_t* lut3, hipStream_t st);
 void launch_syrk_packed_bf3(const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m, const uint32_t* lut3,
                             float* tiles, int accumulate, hipStream_t st);
+void launch_syrk_packed_bf3_split(const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m, const uint32_t* lut3,
+                                  int slices, float* partial, float* tiles, int accumulate, hipStream_t st);
+void launch_tile_reduce(const float* partial, unsigned slices, uint64_t elems, float* tiles, int accumulate,
+                        hipStream_t st);
 void launch_syrk_packed_bf3_part(const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m, const uint32_t* lut3,
                                  int rank, int world, float* blocks, int accumulate, hipStream_t st);
 

@@ -719,8 +719,16 @@ template <bool LOCAL = false, bool XCD = false, int MODE = 0>
 __global__ __launch_bounds__(512, 1) void k_syrk_bf3(const uint8_t* __restrict__ P, uint64_t pitch, uint64_t n,
                                                      uint64_t kdim, const uint32_t* __restrict__ lut3,
                                                      float* __restrict__ tiles, int accumulate,
-                                                     uint32_t part_rank = 0, uint32_t part_world = 1) {
+                                                     uint32_t part_rank = 0, uint32_t part_world = 1,
+                                                     uint64_t kslice = 0, uint64_t slice_elems = 0) {
     __shared__ __attribute__((aligned(16))) short lds[2 * B3_STAGE];
+    if (gridDim.y > 1) {  // split-K: slice blockIdx.y covers SNPs [y*kslice, +kslice) into its own partial K
+        const uint64_t k0 = (uint64_t)blockIdx.y * kslice;
+        P += k0 * pitch;
+        lut3 += 8 * k0;
+        kdim = min(kslice, kdim - k0);
+        tiles += (uint64_t)blockIdx.y * slice_elems;
+    }
     const uint64_t wg = XCD ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
     uint32_t bi, bj;
     tile_coords(LOCAL ? wg * part_world + part_rank : wg, bi, bj);
@@ -1312,6 +1320,21 @@ void launch_syrk_packed_bf3(const uint8_t* packed, uint64_t pitch, uint64_t n, u
         default: f32w::k_syrk_bf3<false, false, 1><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, lut3, tiles, accumulate);
     }
     SNPMI_HIP(hipGetLastError());
+}
+
+// split-K form for grids too small to fill the chip (N <~ 16k): `slices` partial tile sets in
+// `partial` (each n_tiles_upper(n) * 128^2 floats, overwritten), then a deterministic reduce
+void launch_syrk_packed_bf3_split(const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m, const uint32_t* lut3,
+                                  int slices, float* partial, float* tiles, int accumulate, hipStream_t st) {
+    const uint64_t nb = ceil_div(n, 256), g = nb * (nb + 1) / 2;
+    const uint64_t elems = n_tiles_upper(n) * BM * BM;
+    const uint64_t kslice = round_up(ceil_div(m, (uint64_t)slices), (uint64_t)f32w::BK);
+    const unsigned S = (unsigned)ceil_div(m, kslice);
+    SNPMI_REQUIRE(g < (1ull << 31) && S >= 1, SNPMI_E_ARG, "bad split");
+    f32w::k_syrk_bf3<false, false, 1><<<dim3((unsigned)g, S), 512, 0, st>>>(packed, pitch, n, m, lut3, partial, 0, 0, 1,
+                                                                          kslice, elems);
+    SNPMI_HIP(hipGetLastError());
+    launch_tile_reduce(partial, S, elems, tiles, accumulate, st);
 }
 
 void launch_syrk_packed_bf3_part(const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m, const uint32_t* lut3,

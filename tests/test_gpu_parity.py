@@ -724,6 +724,29 @@ def test_grm_partitioned_from_file(name, rows, world, std):
         O.standardize_native(Z, is_beta=True, a=1.0, b=25.0)
     grm_close(K, Z.dot(Z.T), 1e-5)
     Kr, tr = r.read_kernel(stdz, dtype=np.float32), None
-    np.testing.assert_allclose(K, Kr.val, rtol=0, atol=2e-6 * np.abs(np.diag(Kr.val)).max())
+    np.testing.assert_allclose(K, Kr.val, rtol=0, atol=1e-5 * np.abs(np.diag(Kr.val)).max())  # summation orders differ
     _, tr = r.read(dtype=np.float32).standardize(stdz, return_trained=True)
     np.testing.assert_array_equal(np.asarray(trained.stats), np.asarray(tr.stats))
+
+
+@pytest.mark.parametrize("slices", [2, 3, 8])
+@pytest.mark.parametrize("n", [300, 600, 4100])
+def test_grm_split_k(n, slices):
+    """Split-K bf16x3 SYRK (partial tile sets + ordered reduce; auto below ~16k iids): forced
+    slice counts, ragged SNP tails, accumulate across .bed chunks -- == the f64 oracle."""
+    rng = np.random.default_rng(n + slices)
+    m = 1000 + 37 * slices
+    val = rng.integers(0, 3, size=(n, m)).astype(np.float64)
+    val[rng.random(val.shape) < 0.05] = np.nan
+    d = SnpData(iid=[["a", str(i)] for i in range(n)], sid=["s%d" % j for j in range(m)], val=val)
+    Z = val.copy(order="F")
+    O.standardize_native(Z)
+    ref = Z.dot(Z.T)
+    N.call("snpmi_set_kernel_variant", b"syrk_split", slices)
+    try:
+        with tempfile.TemporaryDirectory() as tmp:
+            b = Bed.write(os.path.join(tmp, "t.bed"), d, count_A1=False)
+            grm_close(b.read_kernel(Unit(), dtype=np.float32).val, ref, 1e-5)
+            grm_close(b.read_kernel(Unit(), dtype=np.float32, block_size=333).val, ref, 1e-5)
+    finally:
+        N.call("snpmi_set_kernel_variant", b"syrk_split", 0)
