@@ -79,6 +79,14 @@ def main():
                           "packed_GB": m * ((n + 3) // 4) / 1e9, "K_GB": n * n * 4 / 1e9,
                           "bed_write_s": t_write, "trace": float(np.trace(K.val))}), flush=True)
         del K
+        # the reference's default dtype (snpreader.py:528 read_kernel(..., dtype=np.float64))
+        t0 = time.perf_counter()
+        K = bed.read_kernel(Unit())
+        t_grm64 = time.perf_counter() - t0
+        print(json.dumps({"bench": "file-backed GRM (Bed.read_kernel, f64 default)", "n_iid": n, "n_sid": m,
+                          "seconds": t_grm64, "TFLOPs_end_to_end": flops / t_grm64 / 1e12, "K_GB": n * n * 8 / 1e9}),
+              flush=True)
+        del K
         B = args.read_block
         sub = bed[:, :B]
         sub.read(dtype=np.float32)
