@@ -831,7 +831,72 @@ __global__ __launch_bounds__(512, 1) void k_syrk_bf3(const uint8_t* __restrict__
         }
     };
 
-    if constexpr (MODE == 1) {
+    if constexpr (MODE == 2) {
+        // MODE 1's loader, with the workgroup barrier moved to the middle of the stage: after
+        // MFMA group 3 (stage s+1's planes are all stored) every wave reads stage s+1's B planes
+        // 0-1 into a second register set during groups 4-5, so the next stage starts after its
+        // 8 A-plane-0 reads instead of 20 transposed LDS reads.  Stage s's own A planes and B
+        // plane 2 are read before its barrier -- after it, its buffer may be overwritten
+        // (stage s+2's stores during stage s+1's groups 1-3).  256 VGPRs per wave at 2 waves
+        // per SIMD: 128 hold the accumulators, so only part of the next stage is prefetched.
+        auto fragB = [&](const short* S, int pl, bf16x8_t (&b)[2]) {
+#pragma unroll
+            for (int y = 0; y < 2; y++) b[y] = frag(S, 1, pl, wn * 64 + 32 * y, rd_offB);
+        };
+        auto fragsA = [&](const short* S, int pa, bf16x8_t (&a)[4]) {
+#pragma unroll
+            for (int x = 0; x < 4; x++) a[x] = frag(S, 0, pa, wm * 128 + 32 * x, x >= 2 ? rd_off + dswz : rd_off);
+        };
+        auto group = [&](const bf16x8_t (&a)[4], const bf16x8_t (&b)[2]) {
+#pragma unroll
+            for (int x = 0; x < 4; x++)
+#pragma unroll
+                for (int y = 0; y < 2; y++)
+                    acc[x][y] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[x], b[y], acc[x][y], 0, 0, 0);
+        };
+        B3Regs r;
+        load(0, r);
+        store(lds, r);
+        if (nst > 1) load(1, r);
+        __syncthreads();
+        bf16x8_t B0s[2], B1s[2], B0t[2], B1t[2];
+        fragB(lds, 0, B0s);
+        fragB(lds, 1, B1s);
+        auto stage = [&](uint64_t s, bf16x8_t (&B0)[2], bf16x8_t (&B1)[2], bf16x8_t (&B0n)[2], bf16x8_t (&B1n)[2]) {
+            const short* cur = lds + (s & 1) * B3_STAGE;
+            short* nxt = lds + ((s + 1) & 1) * B3_STAGE;
+            const bool more = s + 1 < nst;
+            bf16x8_t A0[4], B2[2], A1[4], A2[4];
+            fragsA(cur, 0, A0);
+            fragB(cur, 2, B2);
+            fragsA(cur, 1, A1);
+            uint32_t sel[8];
+            group(A0, B0);
+            if (more) make_sel(r.w, sel);
+            group(A0, B1);
+            if (more) store_plane(nxt, 0, r, sel);
+            group(A0, B2);
+            fragsA(cur, 2, A2);
+            if (more) store_plane(nxt, 1, r, sel);
+            group(A1, B0);
+            if (more) {
+                store_plane(nxt, 2, r, sel);
+                if (s + 2 < nst) load(s + 2, r);
+            }
+            __syncthreads();
+            if (more) {
+                fragB(nxt, 0, B0n);
+                fragB(nxt, 1, B1n);
+            }
+            group(A1, B1);
+            group(A2, B0);
+        };
+        // two stages per trip so the two fragment sets keep fixed registers (no copies)
+        for (uint64_t s = 0; s < nst; s += 2) {
+            stage(s, B0s, B1s, B0t, B1t);
+            if (s + 1 < nst) stage(s + 1, B0t, B1t, B0s, B1s);
+        }
+    } else if constexpr (MODE == 1) {
         // one register set: the codes/LUT of stage s+1 are expanded and stored plane by plane
         // after MFMA groups 0-3 of stage s, and right after the last plane the loads of stage
         // s+2 are issued into the same registers -- they have MFMA groups 4-5, the barrier and
@@ -1309,15 +1374,18 @@ void launch_syrk_packed_bf3(const uint8_t* packed, uint64_t pitch, uint64_t n, u
         return;
     }
     // MI355X, N=50k, 10k SNPs (tools/ubench.py syrk, 7 interleaved rounds, profiles/r01g):
-    // default (loader interleaved between the MFMA groups) 302.9 TFLOP/s, + XCD remap (32)
+    // loader interleaved between the MFMA groups (MODE 1, now 33) 302.9 TFLOP/s, + XCD remap (32)
     // 303.3, expansion after the MFMAs (30) 306.6, + XCD remap (31) 305.3 -- equal within run
     // noise; 39 (no loader, ablation) 380-382, at a 8% higher clock (PMC GRBM_GUI_ACTIVE).
+    // Default MODE 2 (mid-stage barrier, next B planes prefetched into registers): 311.0 vs
+    // 307.1 for MODE 1 at N=50k, 304.1 vs 300.5 at N=30k (profiles/r01i/ubench_syrk_bf3_mode2.jsonl).
     switch (g_variant_syrk) {
         case 30: f32w::k_syrk_bf3<><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, lut3, tiles, accumulate); break;
         case 31: f32w::k_syrk_bf3<false, true><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, lut3, tiles, accumulate); break;
         case 32: f32w::k_syrk_bf3<false, true, 1><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, lut3, tiles, accumulate); break;
+        case 33: f32w::k_syrk_bf3<false, false, 1><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, lut3, tiles, accumulate); break;
         case 39: f32w::k_syrk_bf3<false, true, 9><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, lut3, tiles, accumulate); break;
-        default: f32w::k_syrk_bf3<false, false, 1><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, lut3, tiles, accumulate);
+        default: f32w::k_syrk_bf3<false, false, 2><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, lut3, tiles, accumulate);
     }
     SNPMI_HIP(hipGetLastError());
 }
@@ -1331,7 +1399,7 @@ void launch_syrk_packed_bf3_split(const uint8_t* packed, uint64_t pitch, uint64_
     const uint64_t kslice = round_up(ceil_div(m, (uint64_t)slices), (uint64_t)f32w::BK);
     const unsigned S = (unsigned)ceil_div(m, kslice);
     SNPMI_REQUIRE(g < (1ull << 31) && S >= 1, SNPMI_E_ARG, "bad split");
-    f32w::k_syrk_bf3<false, false, 1><<<dim3((unsigned)g, S), 512, 0, st>>>(packed, pitch, n, m, lut3, partial, 0, 0, 1,
+    f32w::k_syrk_bf3<false, false, 2><<<dim3((unsigned)g, S), 512, 0, st>>>(packed, pitch, n, m, lut3, partial, 0, 0, 1,
                                                                           kslice, elems);
     SNPMI_HIP(hipGetLastError());
     launch_tile_reduce(partial, S, elems, tiles, accumulate, st);
@@ -1348,7 +1416,7 @@ void launch_syrk_packed_bf3_part(const uint8_t* packed, uint64_t pitch, uint64_t
         if (!accumulate) SNPMI_HIP(hipMemsetAsync(blocks, 0, nloc * 256 * 256 * sizeof(float), st));
         return;
     }
-    f32w::k_syrk_bf3<true, false, 1><<<(unsigned)nloc, 512, 0, st>>>(packed, pitch, n, m, lut3, blocks, accumulate,
+    f32w::k_syrk_bf3<true, false, 2><<<(unsigned)nloc, 512, 0, st>>>(packed, pitch, n, m, lut3, blocks, accumulate,
                                                                      (uint32_t)rank, (uint32_t)world);
     SNPMI_HIP(hipGetLastError());
 }
