@@ -1378,7 +1378,9 @@ void launch_syrk_packed_bf3(const uint8_t* packed, uint64_t pitch, uint64_t n, u
     // 303.3, expansion after the MFMAs (30) 306.6, + XCD remap (31) 305.3 -- equal within run
     // noise; 39 (no loader, ablation) 380-382, at a 8% higher clock (PMC GRBM_GUI_ACTIVE).
     // Default MODE 2 (mid-stage barrier, next B planes prefetched into registers): 311.0 vs
-    // 307.1 for MODE 1 at N=50k, 304.1 vs 300.5 at N=30k (profiles/r01i/ubench_syrk_bf3_mode2.jsonl).
+    // 307.1 for MODE 1 at N=50k, 304.1 vs 300.5 at N=30k (profiles/r01i/ubench_syrk_bf3_mode2.jsonl);
+    // SIMD partners staggered by one loader slot (waves 4-7 expand before group 0, runtime
+    // plane index, 3 VGPRs spilled) lost: 296.8 vs 313.5 (ubench_syrk_bf3_stagger.jsonl).
     switch (g_variant_syrk) {
         case 30: f32w::k_syrk_bf3<><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, lut3, tiles, accumulate); break;
         case 31: f32w::k_syrk_bf3<false, true><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, lut3, tiles, accumulate); break;

@@ -5,7 +5,7 @@
 #     on a 1-step decode run and a short GRM run, for HBM traffic per launch.
 # Outputs land in gpurun_out/prof_<tag>/; copy the summaries to profiles/<tag>/.
 set -e
-TAG=${1:-r01h}
+TAG=${1:-r01i}
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
