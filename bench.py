@@ -61,6 +61,7 @@ def parse():
     p.add_argument("--fused", choices=["on", "off"], default="off",
                    help="decode leg: fused stats+decode kernel k_decode_std_lds_f32 (needs a packed column <= "
                         "150 KiB); off = k_snp_stats + k_decode_f, measured faster at 500k iids (2.63 vs 2.40 M SNPs/s)")
+    p.add_argument("--decode-variant", type=int, default=0, help="snpmi_set_kernel_variant('decode', v) (A/B runs)")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--seed", type=int, default=5)
     p.add_argument("--force-rccl", action="store_true", help="build the RCCL communicator even at world size 1")
@@ -206,6 +207,7 @@ def leg_standardize(N, args, dist):
     lut, stats, out = Dev(N, B * 16), Dev(N, B * 8), Dev(N, B * ld * 4)
     ev = Events(N, 2 + 2 * nblk)
     fused = use_fused(args, n)
+    N.call("snpmi_set_kernel_variant", b"decode", args.decode_variant)
 
     def run_block(src, cnt, timed, k):
         if fused:  # stats + decode in one kernel (column staged in LDS, packed bytes read once)

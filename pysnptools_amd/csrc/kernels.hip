@@ -64,52 +64,83 @@ __device__ __forceinline__ double wave_sum_f64(double v) {
 }
 
 // ------------------------------------------------------------------ per-SNP stats + LUT
-// One wave per SNP column; 16-byte loads (64 iids per lane-load).
-template <typename T>
+// W waves per SNP column, 4/W SNPs per 256-thread block; 16-byte loads (64 iids per
+// lane-load), 4 in flight per lane.  W = 1 for short columns; W = 4 for long ones,
+// where one wave per SNP left 2 waves per SIMD streaming 125 KB columns (latency-bound).
+template <typename T, int W>
 __global__ __launch_bounds__(kBlock) void k_snp_stats(const uint8_t* __restrict__ packed, uint64_t pitch,
                                                       uint64_t n, uint64_t m, int count_a1, int std_kind,
                                                       double a, double b, int use_stats, T* __restrict__ stats,
                                                       T* __restrict__ lut) {
-    const int lane = threadIdx.x & (kWave - 1);
-    const uint64_t s = (uint64_t)blockIdx.x * (kBlock / kWave) + (threadIdx.x / kWave);
-    if (s >= m) return;
+    constexpr int kS = kBlock / kWave / W;  // SNPs per block
+    __shared__ uint32_t red[kBlock / kWave][3];
+    const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave, sub = wave % W;
+    const uint64_t s = (uint64_t)blockIdx.x * kS + wave / W;
+    const bool valid = s < m;
+    if (W == 1 && !valid) return;
     if (std_kind == SNPMI_STD_NONE) {
-        if (lane < 4) {
+        if (valid && sub == 0 && lane < 4) {
             int v = code_value(lane, count_a1);
             lut[4 * s + lane] = v < 0 ? lut_missing<T>() : (T)v;
         }
-        return;
+        return;  // block-uniform (std_kind): no barrier below is skipped by part of the block
     }
     double mean, sd;
     if (use_stats) {
+        if (!valid || sub != 0) return;  // block-uniform branch (use_stats); no barrier follows
         mean = (double)stats[2 * s];
         sd = (double)stats[2 * s + 1];
     } else {
-        const uint4* col = reinterpret_cast<const uint4*>(packed + s * pitch);
-        const uint64_t nq = (n + 63) / 64;
         uint32_t c1 = 0, c2 = 0, c3 = 0;
-        for (uint64_t q = lane; q < nq; q += kWave) {
-            uint4 v = col[q];
-            uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+        if (valid) {
+            const uint4* col = reinterpret_cast<const uint4*>(packed + s * pitch);
+            const uint64_t nq = (n + 63) / 64;
+            auto count16 = [&](const uint4& v, uint64_t q) {
+                const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-            for (int k = 0; k < 4; k++) {
-                uint32_t w = w4[k];
-                uint32_t lo = w & 0x55555555u, hi = (w >> 1) & 0x55555555u;
-                uint64_t ib = q * 64 + 16 * k;
-                if (ib + 16 > n) {
-                    uint64_t valid = n > ib ? n - ib : 0;
-                    uint32_t mk = ((1u << (2 * valid)) - 1u) & 0x55555555u;  // valid < 16 here
-                    lo &= mk;
-                    hi &= mk;
+                for (int k = 0; k < 4; k++) {
+                    uint32_t lo = w4[k] & 0x55555555u, hi = (w4[k] >> 1) & 0x55555555u;
+                    const uint64_t ib = q * 64 + 16 * k;
+                    if (ib + 16 > n) {
+                        const uint64_t valid_i = n > ib ? n - ib : 0;
+                        const uint32_t mk = ((1u << (2 * valid_i)) - 1u) & 0x55555555u;  // valid_i < 16 here
+                        lo &= mk;
+                        hi &= mk;
+                    }
+                    c3 += __popc(lo & hi);
+                    c2 += __popc(hi & ~lo);
+                    c1 += __popc(lo & ~hi);
                 }
-                c3 += __popc(lo & hi);
-                c2 += __popc(hi & ~lo);
-                c1 += __popc(lo & ~hi);
+            };
+            constexpr uint64_t step = (uint64_t)W * kWave;
+            uint64_t q = (uint64_t)sub * kWave + lane;
+            for (; q + 3 * step < nq; q += 4 * step) {  // 4 independent loads in flight
+                const uint4 v0 = col[q], v1 = col[q + step], v2 = col[q + 2 * step], v3 = col[q + 3 * step];
+                count16(v0, q);
+                count16(v1, q + step);
+                count16(v2, q + 2 * step);
+                count16(v3, q + 3 * step);
             }
+            for (; q < nq; q += step) count16(col[q], q);
         }
         c1 = wave_sum_u32(c1);
         c2 = wave_sum_u32(c2);
         c3 = wave_sum_u32(c3);
+        if constexpr (W > 1) {
+            if (lane == 0) {
+                red[wave][0] = c1;
+                red[wave][1] = c2;
+                red[wave][2] = c3;
+            }
+            __syncthreads();
+            if (!valid || sub != 0) return;
+#pragma unroll
+            for (int w = 1; w < W; w++) {
+                c1 += red[wave + w][0];
+                c2 += red[wave + w][1];
+                c3 += red[wave + w][2];
+            }
+        }
         uint64_t c0 = n - c1 - c2 - c3;
         uint64_t chi = count_a1 ? c0 : c3;  // count of value 2
         double nobs = (double)(n - c1);
@@ -976,16 +1007,22 @@ int g_variant_decode = 0;  // tuning hook (snpmi_set_kernel_variant); no variant
 void launch_snp_stats(const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m, int count_a1, int std_kind,
                       double a, double b, int use_stats, int dtype, void* stats, void* lut, hipStream_t st) {
     if (m == 0) return;
-    const unsigned g = (unsigned)ceil_div(m, kBlock / kWave);
-    if (dtype == SNPMI_DT_F32)
-        k_snp_stats<float><<<g, kBlock, 0, st>>>(packed, pitch, n, m, count_a1, std_kind, a, b, use_stats,
-                                                  (float*)stats, (float*)lut);
-    else if (dtype == SNPMI_DT_F64)
-        k_snp_stats<double><<<g, kBlock, 0, st>>>(packed, pitch, n, m, count_a1, std_kind, a, b, use_stats,
-                                                   (double*)stats, (double*)lut);
-    else
-        k_snp_stats<int8_t><<<g, kBlock, 0, st>>>(packed, pitch, n, m, count_a1, SNPMI_STD_NONE, a, b, 0,
-                                                   (int8_t*)stats, (int8_t*)lut);
+    // 4 waves per SNP once a column is >= 16 KiB (tools/ubench.py / bench A/B: decode variant 6
+    // forces one wave per SNP)
+    const bool wide = n >= 65536 && g_variant_decode != 6;
+#define SNPMI_STATS(T, W, kind)                                                                                    \
+    k_snp_stats<T, W><<<(unsigned)ceil_div(m, kBlock / kWave / W), kBlock, 0, st>>>(                               \
+        packed, pitch, n, m, count_a1, kind, a, b, dtype == SNPMI_DT_I8 ? 0 : use_stats, (T*)stats, (T*)lut)
+    if (dtype == SNPMI_DT_F32) {
+        if (wide) SNPMI_STATS(float, 4, std_kind);
+        else SNPMI_STATS(float, 1, std_kind);
+    } else if (dtype == SNPMI_DT_F64) {
+        if (wide) SNPMI_STATS(double, 4, std_kind);
+        else SNPMI_STATS(double, 1, std_kind);
+    } else {
+        SNPMI_STATS(int8_t, 1, SNPMI_STD_NONE);
+    }
+#undef SNPMI_STATS
     SNPMI_LAUNCH_CHECK();
 }
 

@@ -56,6 +56,38 @@ def decode(args):
                           "GBps": nbytes / t / 1e6, "frac_8TBs": nbytes / t / 1e6 / 8000}))
 
 
+def stats(args):
+    """k_snp_stats alone, cycling over --m SNPs in blocks of 2048 so each launch reads its codes
+    from HBM (the whole buffer is larger than the 256 MB Infinity Cache); variant 6 = one wave
+    per SNP, 0 = four waves per SNP for columns >= 16 KiB."""
+    n, m, B = args.n, args.m, 2048
+    pitch = N.lib().snpmi_packed_pitch(n)
+    packed = Dev(N, pitch * m)
+    synth(N, packed.p, pitch, n, 0, m, 3, 0.01)
+    lut, st = Dev(N, B * 16), Dev(N, B * 8)
+    variants = [int(v) for v in args.variants.split(",")]
+    ev = Events(N, 2)
+    res = {v: [] for v in variants}
+    nblk = m // B
+    k = 0
+    for rnd in range(args.rounds):
+        for v in variants:
+            N.call("snpmi_set_kernel_variant", b"decode", v)
+            for _ in range(nblk):
+                src = ctypes.c_void_p(packed.p.value + (k % nblk) * B * pitch)
+                k += 1
+                ev.record(0)
+                N.call("snpmi_dev_snp_stats", src, pitch, n, B, 0, N.STD_UNIT, 0.0, 0.0, 0, N.DT_F32, st.p, lut.p)
+                ev.record(1)
+                res[v].append(ev.ms(0, 1))
+    N.call("snpmi_set_kernel_variant", b"decode", 0)
+    nbytes = B * ((n + 3) // 4)
+    for v in variants:
+        t = np.median(res[v])
+        print(json.dumps({"kernel": "snp_stats", "variant": v, "n": n, "block": B, "median_ms": t,
+                          "GBps": nbytes / t / 1e6}))
+
+
 def decode_c(args):
     """C-order decode (k_decode_c): out[i][j], ld = m; the same bytes as the F-order decode."""
     n, m = args.n, args.m
@@ -197,4 +229,4 @@ if __name__ == "__main__":
     if a.set_variant:
         k, v = a.set_variant.split("=")
         N.call("snpmi_set_kernel_variant", k.encode(), int(v))
-    {"decode": decode, "decode_c": decode_c, "repack": repack, "syrk": syrk, "syrk_dense": syrk_dense}[a.what](a)
+    {"decode": decode, "stats": stats, "decode_c": decode_c, "repack": repack, "syrk": syrk, "syrk_dense": syrk_dense}[a.what](a)
