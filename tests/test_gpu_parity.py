@@ -352,6 +352,25 @@ def test_grm_tile_edges(n, syrk_variant):
             grm_close(b.read_kernel(Unit(), dtype=dtype).val, ref, tol)
 
 
+@pytest.mark.parametrize("m", [1, 15, 16, 17, 31, 32, 33, 48, 49])
+def test_grm_stage_counts(m, syrk_variant):
+    """SNP counts around the 16-SNP LDS stage of the SYRK kernels: one stage, an exact multiple,
+    and odd/even stage counts (the bf16x3 kernel runs its stages in pairs, so an odd count ends
+    on a single stage); N = 513 gives diagonal, off-diagonal and 1-iid edge blocks."""
+    n = 513
+    rng = np.random.default_rng(m)
+    val = rng.integers(0, 3, size=(n, m)).astype(np.float64)
+    val[rng.random(val.shape) < 0.05] = np.nan
+    d = SnpData(iid=[["a", str(i)] for i in range(n)], sid=["s%d" % j for j in range(m)], val=val)
+    with tempfile.TemporaryDirectory() as tmp:
+        b = Bed.write(os.path.join(tmp, "t.bed"), d, count_A1=False)
+        for dtype, tol in ((np.float64, 1e-10), (np.float32, 1e-5)):
+            Z = val.astype(dtype).copy(order="F")
+            O.standardize_native(Z)
+            ref = Z.astype(np.float64).dot(Z.astype(np.float64).T)
+            grm_close(b.read_kernel(Unit(), dtype=dtype).val, ref, tol)
+
+
 # ---------------------------------------------------------------------------------- device API
 class Dev:
     """Tiny RAII helper over snpmi_dev_alloc/free."""
