@@ -551,7 +551,7 @@ def main():
                "roofline": {"bound": "mfma", "achieved": r2["mean_tflops"], "peak": BF3_PEAK_TFLOPS,
                             "unit": "TFLOP/s", "frac": r2["mean_tflops"] / BF3_PEAK_TFLOPS,
                             "traffic": pmc_traffic("f32w::k_syrk_bf3", "grm", n, args.grm_block),
-                            "kernel": "f32w::k_syrk_bf3<false,false,2>: f32 GRM as 6 bf16 MFMA products of each "
+                            "kernel": "f32w::k_syrk_bf3<false,false,5>: f32 GRM as 6 bf16 MFMA products of each "
                                       "value's exact bf16x3 split, f32 accumulate (v_mfma_f32_32x32x16_bf16); "
                                       "peak = 2.5 PF bf16 dense / 6; time per block includes k_lut_bf3",
                             "per_launch_flops": n * (n + 1) * args.grm_block,
@@ -571,7 +571,7 @@ def main():
                 "blocks_on_rank0": r3["n_local_blocks"], "K_bytes_per_rank": r3["n_local_blocks"] * 256 * 256 * 4,
                 "roofline": {"bound": "mfma", "achieved": gf5 / 1e3 / dist.world, "peak": BF3_PEAK_TFLOPS,
                              "unit": "TFLOP/s per GPU", "frac": gf5 / 1e3 / dist.world / BF3_PEAK_TFLOPS,
-                             "traffic": None, "kernel": "f32w::k_syrk_bf3<true,false,2> (bf16x3 split, 6 bf16 "
+                             "traffic": None, "kernel": "f32w::k_syrk_bf3<true,false,5> (bf16x3 split, 6 bf16 "
                                                         "MFMA products, f32 accumulate; wall incl. H2D + all-gather)"},
                 "projected_seconds_1M_snps": r3["wall"] * 1_000_000 / m5}
         if r3.get("parity_sample") is not None:

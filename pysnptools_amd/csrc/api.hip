@@ -521,7 +521,9 @@ static void for_z_blocks(Device& d, const uint8_t* packed, uint64_t pitch, uint6
 // f32 GRM of packed SNPs: default = the bf16 MFMA pipe (k_syrk_bf3: bf16x3 split of each SNP's
 // f32 LUT, six bf16 products per f32 product, f32 accumulate): 309 TFLOP/s at N=50k, 10k SNPs
 // vs 136 for the f32-MFMA two-phase path (variant 20) -- tools/ubench.py syrk.
-// Variants: 30 = plain loader, 31 = + XCD remap, 39 = ablation (no loader); 4/5/20 = f32 MFMA.
+// Variants: 30 = plain loader, 31 = + XCD remap, 33 = end-of-stage barrier, 34 = mid-stage
+// barrier without the pinned VALU interleave, 35 = default kernel without split-K, 39 =
+// ablation (no loader); 4/5/20 = f32 MFMA.
 static int g_variant_syrk_split = 0;  // tuning hook: 0 = auto, 1 = off, S = force S slices
 
 static bool use_bf3(int dt) {

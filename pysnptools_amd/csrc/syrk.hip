@@ -831,7 +831,7 @@ __global__ __launch_bounds__(512, 1) void k_syrk_bf3(const uint8_t* __restrict__
         }
     };
 
-    if constexpr (MODE == 2) {
+    if constexpr (MODE == 2 || MODE == 5) {
         // MODE 1's loader, with the workgroup barrier moved to the middle of the stage: after
         // MFMA group 3 (stage s+1's planes are all stored) every wave reads stage s+1's B planes
         // 0-1 into a second register set during groups 4-5, so the next stage starts after its
@@ -862,10 +862,27 @@ __global__ __launch_bounds__(512, 1) void k_syrk_bf3(const uint8_t* __restrict__
         bf16x8_t B0s[2], B1s[2], B0t[2], B1t[2];
         fragB(lds, 0, B0s);
         fragB(lds, 1, B1s);
+        // MODE 5 (default): the hooks run unconditionally (the last stage expands into the idle
+        // buffer, its code loads clamp to the last stage), so each MFMA group and its loader VALU
+        // share one basic block, and the schedule is pinned to one VALU after each MFMA
+        // (sched_group_barrier) instead of the group's 8 MFMAs followed by a VALU burst.
+        // N=50k: 307.2-315.0 vs 303.3-307.1 TFLOP/s for MODE 2; 2 or 3 VALU per MFMA 305-307,
+        // unconditional hooks without the pin 306.1, + the next B reads pinned between the
+        // group 4-5 MFMAs 293.4 (profiles/r01i/ubench_syrk_bf3_interleave.jsonl).
+        constexpr bool kUncond = MODE == 5;
+        auto pin = [&]() {
+            if constexpr (MODE == 5) {
+#pragma unroll
+                for (int i = 0; i < 8; i++) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+                    __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);  // VALU
+                }
+            }
+        };
         auto stage = [&](uint64_t s, bf16x8_t (&B0)[2], bf16x8_t (&B1)[2], bf16x8_t (&B0n)[2], bf16x8_t (&B1n)[2]) {
             const short* cur = lds + (s & 1) * B3_STAGE;
             short* nxt = lds + ((s + 1) & 1) * B3_STAGE;
-            const bool more = s + 1 < nst;
+            const bool more = kUncond || s + 1 < nst;
             bf16x8_t A0[4], B2[2], A1[4], A2[4];
             fragsA(cur, 0, A0);
             fragB(cur, 2, B2);
@@ -873,16 +890,19 @@ __global__ __launch_bounds__(512, 1) void k_syrk_bf3(const uint8_t* __restrict__
             uint32_t sel[8];
             group(A0, B0);
             if (more) make_sel(r.w, sel);
+            pin();
             group(A0, B1);
             if (more) store_plane(nxt, 0, r, sel);
+            pin();
             group(A0, B2);
             fragsA(cur, 2, A2);
             if (more) store_plane(nxt, 1, r, sel);
+            pin();
             group(A1, B0);
-            if (more) {
-                store_plane(nxt, 2, r, sel);
-                if (s + 2 < nst) load(s + 2, r);
-            }
+            if (more) store_plane(nxt, 2, r, sel);
+            pin();
+            if constexpr (kUncond) load(s + 2 < nst ? s + 2 : nst - 1, r);
+            else if (more && s + 2 < nst) load(s + 2, r);
             __syncthreads();
             if (more) {
                 fragB(nxt, 0, B0n);
@@ -1386,8 +1406,9 @@ void launch_syrk_packed_bf3(const uint8_t* packed, uint64_t pitch, uint64_t n, u
         case 31: f32w::k_syrk_bf3<false, true><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, lut3, tiles, accumulate); break;
         case 32: f32w::k_syrk_bf3<false, true, 1><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, lut3, tiles, accumulate); break;
         case 33: f32w::k_syrk_bf3<false, false, 1><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, lut3, tiles, accumulate); break;
+        case 34: f32w::k_syrk_bf3<false, false, 2><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, lut3, tiles, accumulate); break;
         case 39: f32w::k_syrk_bf3<false, true, 9><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, lut3, tiles, accumulate); break;
-        default: f32w::k_syrk_bf3<false, false, 2><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, lut3, tiles, accumulate);
+        default: f32w::k_syrk_bf3<false, false, 5><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, lut3, tiles, accumulate);
     }
     SNPMI_HIP(hipGetLastError());
 }
@@ -1401,7 +1422,7 @@ void launch_syrk_packed_bf3_split(const uint8_t* packed, uint64_t pitch, uint64_
     const uint64_t kslice = round_up(ceil_div(m, (uint64_t)slices), (uint64_t)f32w::BK);
     const unsigned S = (unsigned)ceil_div(m, kslice);
     SNPMI_REQUIRE(g < (1ull << 31) && S >= 1, SNPMI_E_ARG, "bad split");
-    f32w::k_syrk_bf3<false, false, 2><<<dim3((unsigned)g, S), 512, 0, st>>>(packed, pitch, n, m, lut3, partial, 0, 0, 1,
+    f32w::k_syrk_bf3<false, false, 5><<<dim3((unsigned)g, S), 512, 0, st>>>(packed, pitch, n, m, lut3, partial, 0, 0, 1,
                                                                           kslice, elems);
     SNPMI_HIP(hipGetLastError());
     launch_tile_reduce(partial, S, elems, tiles, accumulate, st);
@@ -1418,7 +1439,7 @@ void launch_syrk_packed_bf3_part(const uint8_t* packed, uint64_t pitch, uint64_t
         if (!accumulate) SNPMI_HIP(hipMemsetAsync(blocks, 0, nloc * 256 * 256 * sizeof(float), st));
         return;
     }
-    f32w::k_syrk_bf3<true, false, 2><<<(unsigned)nloc, 512, 0, st>>>(packed, pitch, n, m, lut3, blocks, accumulate,
+    f32w::k_syrk_bf3<true, false, 5><<<(unsigned)nloc, 512, 0, st>>>(packed, pitch, n, m, lut3, blocks, accumulate,
                                                                      (uint32_t)rank, (uint32_t)world);
     SNPMI_HIP(hipGetLastError());
 }

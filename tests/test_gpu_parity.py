@@ -321,11 +321,13 @@ def test_kerneldata_diag_k_to_n():
     assert abs(np.diag(kd.val).sum() - 3) < 1e-7  # kernelreader/test.py:221-229
 
 
-@pytest.fixture(params=[0, 4, 5, 20, 30, 31, 33], ids=["auto", "syrk256", "syrk128", "f32twophase", "bf3plain", "bf3xcd", "bf3mode1"])
+@pytest.fixture(params=[0, 4, 5, 20, 30, 31, 33, 34],
+                ids=["auto", "syrk256", "syrk128", "f32twophase", "bf3plain", "bf3xcd", "bf3mode1", "bf3mode2"])
 def syrk_variant(request):
     """Run a test under each SYRK kernel -- f32: 0 = default (packed: the bf16x3-split kernel on
-    the bf16 MFMA pipe, interleaved loader, mid-stage barrier with the next B planes prefetched),
-    33 = the same loader with an end-of-stage barrier, 30/31 = its plain-loader forms, 4 = f32
+    the bf16 MFMA pipe, interleaved loader pinned one VALU per MFMA, mid-stage barrier with the
+    next B planes prefetched), 34 = without the pin, 33 = end-of-stage barrier, 30/31 = its
+    plain-loader forms, 4 = f32
     MFMA 256x256 fused, 5 = f32 MFMA 128x128, 20 = f32 MFMA two-phase (decode to Z + glds);
     f64: 0/4 = interleaved bank-rotated loader, 5 = plain loader -- and restore the default."""
     N.call("snpmi_set_kernel_variant", b"syrk", request.param)
