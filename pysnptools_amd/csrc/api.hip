@@ -527,15 +527,18 @@ static void for_z_blocks(Device& d, const uint8_t* packed, uint64_t pitch, uint6
 static int g_variant_syrk_split = 0;  // tuning hook: 0 = auto, 1 = off, S = force S slices
 
 static bool use_bf3(int dt) {
-    return dt == SNPMI_DT_F32 && (g_variant_syrk == 0 || (g_variant_syrk >= 30 && g_variant_syrk < 40));
+    return dt == SNPMI_DT_F32 && (g_variant_syrk == 0 || (g_variant_syrk >= 30 && g_variant_syrk < 50));
 }
+// default: the fp16x2 kernel (k_syrk_h2, 3 products) with the bf16x3 kernel as its range
+// fallback; 30-39 force bf16x3 alone
+static bool use_h2() { return g_variant_syrk == 0 || (g_variant_syrk >= 40 && g_variant_syrk < 50); }
 
 // split-K slices for the bf16x3 SYRK when the 256x256-block grid leaves CUs idle in its last
 // round: minimise rounds-per-slice ceil(g*S / CUs) / S, +1% per extra slice (partial sets + the
 // reduce), >= 1024 SNPs per slice.  Measured (tools/ubench.py syrk, m = 20k): N=10k 213 -> 242
 // TFLOP/s at S=4, N=5k 199 -> 217 at S=6 -- the slice counts this model picks.
 static int bf3_split_slices(uint64_t n, uint64_t m, int cus) {
-    if (g_variant_syrk == 35 || g_variant_syrk_split == 1) return 1;
+    if (g_variant_syrk == 35 || g_variant_syrk == 45 || g_variant_syrk_split == 1) return 1;
     if (g_variant_syrk_split > 1) return g_variant_syrk_split;
     const uint64_t nb = ceil_div(n, 256), g = nb * (nb + 1) / 2, C = (uint64_t)std::max(cus, 1);
     const double unsplit = (double)ceil_div(g, C);
@@ -551,22 +554,35 @@ static int bf3_split_slices(uint64_t n, uint64_t m, int cus) {
     return best_cost < 0.97 * unsplit ? best : 1;
 }
 
-static const uint32_t* lut_bf3(Device& d, const float* lut, uint64_t m) {
-    uint32_t* l3 = (uint32_t*)d.get(Device::S_LUT3, lut_bf3_entries(m) * 32);
+// bf16x3 LUT (32 B per SNP); with h2, also the fp16x2 LUT (16 B per SNP) and its range flag,
+// all in one scratch slot
+static const uint32_t* lut_bf3(Device& d, const float* lut, uint64_t m, H2Lut* h2 = nullptr) {
+    const uint64_t e = lut_bf3_entries(m);
+    uint32_t* l3 = (uint32_t*)d.get(Device::S_LUT3, e * 48 + 256);
     launch_lut_bf3(lut, m, l3, d.stream);
+    if (h2) {
+        uint32_t* l2 = l3 + 8 * e;
+        uint32_t* flag = l2 + 4 * e;
+        launch_lut_h2(lut, m, l2, flag, d.stream);
+        h2->lut2 = l2;
+        h2->flag = flag;
+    }
     return l3;
 }
 
 static void syrk_packed_auto(Device& d, const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m,
                              const void* lut, int dt, void* tiles, int accumulate) {
     if (use_bf3(dt)) {
-        const uint32_t* l3 = lut_bf3(d, (const float*)lut, m);
+        H2Lut h2;
+        const bool h = use_h2() && m > 0;
+        const uint32_t* l3 = lut_bf3(d, (const float*)lut, m, h ? &h2 : nullptr);
         const int S = bf3_split_slices(n, m, d.cu_count);
         if (S > 1) {
             float* part = (float*)d.get(Device::S_ZBLK, (uint64_t)S * n_tiles_upper(n) * kTile * kTile * sizeof(float));
-            launch_syrk_packed_bf3_split(packed, pitch, n, m, l3, S, part, (float*)tiles, accumulate, d.stream);
+            launch_syrk_packed_bf3_split(packed, pitch, n, m, l3, S, part, (float*)tiles, accumulate, d.stream,
+                                         h ? &h2 : nullptr);
         } else {
-            launch_syrk_packed_bf3(packed, pitch, n, m, l3, (float*)tiles, accumulate, d.stream);
+            launch_syrk_packed_bf3(packed, pitch, n, m, l3, (float*)tiles, accumulate, d.stream, h ? &h2 : nullptr);
         }
         return;
     }
@@ -584,8 +600,11 @@ static void syrk_packed_auto(Device& d, const uint8_t* packed, uint64_t pitch, u
 static void syrk_packed_part_auto(Device& d, const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m,
                                   const float* lut, int rank, int world, void* blocks, int accumulate) {
     if (use_bf3(SNPMI_DT_F32)) {
-        launch_syrk_packed_bf3_part(packed, pitch, n, m, lut_bf3(d, lut, m), rank, world, (float*)blocks, accumulate,
-                                    d.stream);
+        H2Lut h2;
+        const bool h = use_h2() && m > 0;
+        const uint32_t* l3 = lut_bf3(d, lut, m, h ? &h2 : nullptr);
+        launch_syrk_packed_bf3_part(packed, pitch, n, m, l3, rank, world, (float*)blocks, accumulate, d.stream,
+                                    h ? &h2 : nullptr);
         return;
     }
     if (!use_two_phase(SNPMI_DT_F32, n) || m == 0) {

@@ -126,13 +126,23 @@ void launch_syrk_dense(const void* Z, uint64_t ldz, uint64_t n_iid, uint64_t n_s
 // f32 GRM on the bf16 MFMA pipe (bf16x3 split, f32 accuracy); lut3 = scratch of 32 B per SNP
 uint64_t lut_bf3_entries(uint64_t m);  // 8 u32 each, zero-padded to a multiple of the SYRK stage
 void launch_lut_bf3(const float* lut, uint64_t m, uint32_t* lut3, hipStream_t st);
+// fp16x2 split (3 MFMA products, f32 accuracy while every SNP's LUT fits fp16's range): lut2 =
+// 16 B per SNP (lut_bf3_entries), flag = 1 u32 raised by k_lut_h2 when a SNP does not fit; with
+// h2 given, the SYRK launchers run k_syrk_h2 and the bf16x3 kernel gated on the flag.
+struct H2Lut {
+    const uint32_t* lut2;
+    const uint32_t* flag;
+};
+void launch_lut_h2(const float* lut, uint64_t m, uint32_t* lut2, uint32_t* flag, hipStream_t st);
 void launch_syrk_packed_bf3(const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m, const uint32_t* lut3,
-                            float* tiles, int accumulate, hipStream_t st);
+                            float* tiles, int accumulate, hipStream_t st, const H2Lut* h2 = nullptr);
 void launch_syrk_packed_bf3_split(const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m, const uint32_t* lut3,
-                                  int slices, float* partial, float* tiles, int accumulate, hipStream_t st);
+                                  int slices, float* partial, float* tiles, int accumulate, hipStream_t st,
+                                  const H2Lut* h2 = nullptr);
 void launch_tile_reduce(const float* partial, unsigned slices, uint64_t elems, float* tiles, int accumulate,
                         hipStream_t st);
 void launch_syrk_packed_bf3_part(const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m, const uint32_t* lut3,
-                                 int rank, int world, float* blocks, int accumulate, hipStream_t st);
+                                 int rank, int world, float* blocks, int accumulate, hipStream_t st,
+                                 const H2Lut* h2 = nullptr);
 
 }  // namespace snpmi

@@ -720,8 +720,10 @@ __global__ __launch_bounds__(512, 1) void k_syrk_bf3(const uint8_t* __restrict__
                                                      uint64_t kdim, const uint32_t* __restrict__ lut3,
                                                      float* __restrict__ tiles, int accumulate,
                                                      uint32_t part_rank = 0, uint32_t part_world = 1,
-                                                     uint64_t kslice = 0, uint64_t slice_elems = 0) {
+                                                     uint64_t kslice = 0, uint64_t slice_elems = 0,
+                                                     const uint32_t* __restrict__ gate = nullptr) {
     __shared__ __attribute__((aligned(16))) short lds[2 * B3_STAGE];
+    if (gate && *gate == 0) return;  // fallback of k_syrk_h2: runs only when its range flag is set
     if (gridDim.y > 1) {  // split-K: slice blockIdx.y covers SNPs [y*kslice, +kslice) into its own partial K
         const uint64_t k0 = (uint64_t)blockIdx.y * kslice;
         P += k0 * pitch;
@@ -993,6 +995,195 @@ __global__ __launch_bounds__(256) void k_lut_bf3(const float* __restrict__ lut, 
     o[6] = o[7] = 0;
     reinterpret_cast<uint4*>(lut3 + 8 * s)[0] = make_uint4(o[0], o[1], o[2], o[3]);
     reinterpret_cast<uint4*>(lut3 + 8 * s)[1] = make_uint4(o[4], o[5], o[6], o[7]);
+}
+
+// ---------------------------------------------------------------- f32 GRM as fp16x2 (3 products)
+// fp16 carries 11 significant bits, so two fp16 values hold 22 of an f32's 24: a0 = f16(a),
+// a1 = f16(a - a0) (a - a0 is exact in f32).  The error of a0 + a1 is <= 2^-22 |a| while a1 is
+// normal in fp16, and <= 2^-25 absolute once it is subnormal.  Keeping a0 b0 + a0 b1 + a1 b0
+// (every fp16 x fp16 product exact in the f32 accumulator; the dropped a1 b1 is <= 2^-22 |ab|)
+// costs 3 MFMAs per f32 product instead of bf16x3's 6.  fp16's range is the price: the split
+// is used only when every SNP's largest |LUT value| M_s lies in [2^-2, 2^15) (or is 0 / NaN),
+// which bounds the error of each product by ~2^-21 M_s^2 -- the magnitude of the SNP's largest
+// K contribution -- and keeps a0 finite.  Unit always qualifies: M_s = max(mu, 2 - mu) / sigma
+// >= 1 and <= 2 sqrt(n).  Beta weights can span 2^24 (Beta(1,25) at MAF 0.5 is 1.5e-6): then
+// k_lut_h2 raises *flag and the bf16x3 kernel (gated on the same flag) computes the block.
+//
+// LUT: [mpad][4] u32, byte-planar like k_lut_bf3: word 2p / 2p+1 = low / high bytes of the fp16
+// plane p of codes 0..3.
+__global__ __launch_bounds__(256) void k_lut_h2(const float* __restrict__ lut, uint64_t m, uint64_t mpad,
+                                                uint32_t* __restrict__ lut2, uint32_t* __restrict__ flag) {
+    const uint64_t s = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (s >= mpad) return;
+    uint32_t h[2][4] = {};
+    if (s < m) {
+        float M = 0.f;
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+            const float v = lut[4 * s + c];
+            M = fmaxf(M, fabsf(v));  // NaN entries are ignored (they stay NaN in both planes)
+            const _Float16 a0 = (_Float16)v;
+            const _Float16 a1 = (_Float16)(v - (float)a0);
+            h[0][c] = __builtin_bit_cast(uint16_t, a0);
+            h[1][c] = __builtin_bit_cast(uint16_t, a1);
+        }
+        if (M != 0.f && !(M >= 0.25f && M < 32768.f)) atomicOr(flag, 1u);
+    }
+    uint32_t o[4];
+#pragma unroll
+    for (int p = 0; p < 2; p++) {
+        o[2 * p] = (h[p][0] & 0xff) | ((h[p][1] & 0xff) << 8) | ((h[p][2] & 0xff) << 16) | ((h[p][3] & 0xff) << 24);
+        o[2 * p + 1] = (h[p][0] >> 8) | ((h[p][1] >> 8) << 8) | ((h[p][2] >> 8) << 16) | ((h[p][3] >> 8) << 24);
+    }
+    reinterpret_cast<uint4*>(lut2)[s] = make_uint4(o[0], o[1], o[2], o[3]);
+}
+
+typedef _Float16 f16x8_t __attribute__((ext_vector_type(8)));
+
+// Same block structure, loader roles and LDS image as k_syrk_bf3 (two fp16 planes per panel
+// instead of three bf16 planes); per 16-SNP stage each wave runs 3 groups of 8
+// v_mfma_f32_32x32x16_f16: (A0,B0), (A0,B1), (A1,B0).  Schedule (MODE 0): stage s+1's codes
+// (loaded one stage ahead) are expanded and stored plane by plane beside groups 0-1, the loads
+// of stage s+2 are issued, then one barrier; stage s+1's B fragments are read into a second
+// register set under group 2.  Runs only when *flag == 0 (see k_lut_h2).
+template <bool LOCAL = false, int MODE = 0>
+__global__ __launch_bounds__(512, 1) void k_syrk_h2(const uint8_t* __restrict__ P, uint64_t pitch, uint64_t n,
+                                                    uint64_t kdim, const uint32_t* __restrict__ lut2,
+                                                    const uint32_t* __restrict__ flag, float* __restrict__ tiles,
+                                                    int accumulate, uint32_t part_rank = 0, uint32_t part_world = 1,
+                                                    uint64_t kslice = 0, uint64_t slice_elems = 0) {
+    constexpr int PLANE = B3_PLANE, STAGE = 2 * 2 * PLANE;
+    __shared__ __attribute__((aligned(16))) short lds[2 * STAGE];
+    if (*flag) return;  // a SNP of this block is outside fp16's range: k_syrk_bf3 runs instead
+    if (gridDim.y > 1) {
+        const uint64_t k0 = (uint64_t)blockIdx.y * kslice;
+        P += k0 * pitch;
+        lut2 += 4 * k0;
+        kdim = min(kslice, kdim - k0);
+        tiles += (uint64_t)blockIdx.y * slice_elems;
+    }
+    const uint64_t wg = blockIdx.x;
+    uint32_t bi, bj;
+    tile_coords(LOCAL ? wg * part_world + part_rank : wg, bi, bj);
+    const uint64_t i0 = (uint64_t)bi * BW, j0 = (uint64_t)bj * BW;
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const int wm = wave >> 2, wn = wave & 3;
+    const int lp = t >> 8, lk = (t >> 4) & 15, ld_ = t & 15;
+    const int sw = (ld_ >> 2) & 1;
+    const uint8_t* wp = P + (lp ? j0 : i0) / 4 + 4 * ld_ + (uint64_t)lk * pitch;
+    const uint8_t* wlast = P + (lp ? j0 : i0) / 4 + 4 * ld_ + (kdim - 1) * pitch;
+    const uint32_t* lp2 = lut2 + 4 * lk;
+    const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
+    const int rd_off = (8 * (g >> 1) + q) * B3_RS + 16 * (g & 1) + 4 * pp;
+    const int dswz = (pp >> 1) ? -8 : 8;
+    const int rd_offB = rd_off + ((wn & 1) ? dswz : 0);
+
+    f32x16 acc[4][2];
+#pragma unroll
+    for (int x = 0; x < 4; x++)
+#pragma unroll
+        for (int y = 0; y < 2; y++) acc[x][y] = (f32x16){};
+    const uint64_t nst = (kdim + BK - 1) / BK;
+
+    uint32_t rw;
+    uint4 rl;
+    auto load = [&](uint64_t st) {
+        const uint8_t* a = wp + st * BK * pitch;
+        rw = *reinterpret_cast<const uint32_t*>(a <= wlast ? a : wlast);
+        rl = *reinterpret_cast<const uint4*>(lp2 + 4 * BK * st);
+    };
+    auto make_sel = [&](uint32_t w, uint32_t (&sel)[8]) {
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const uint32_t v = (w >> (2 * j)) & 0x03030303u;
+            const uint32_t o = v | 0x04040404u;
+            sel[2 * j] = __builtin_amdgcn_perm(o, v, 0x05010400u);
+            sel[2 * j + 1] = __builtin_amdgcn_perm(o, v, 0x07030602u);
+        }
+    };
+    auto store_plane = [&](short* S, int pl, const uint32_t (&sel)[8]) {
+        const uint32_t lo = pl == 0 ? rl.x : rl.z;
+        const uint32_t hi = pl == 0 ? rl.y : rl.w;
+        uint4 v0, v1;
+        v0.x = __builtin_amdgcn_perm(hi, lo, sel[0]);
+        v0.y = __builtin_amdgcn_perm(hi, lo, sel[1]);
+        v0.z = __builtin_amdgcn_perm(hi, lo, sel[2]);
+        v0.w = __builtin_amdgcn_perm(hi, lo, sel[3]);
+        v1.x = __builtin_amdgcn_perm(hi, lo, sel[4]);
+        v1.y = __builtin_amdgcn_perm(hi, lo, sel[5]);
+        v1.z = __builtin_amdgcn_perm(hi, lo, sel[6]);
+        v1.w = __builtin_amdgcn_perm(hi, lo, sel[7]);
+        uint4* r4 = reinterpret_cast<uint4*>(S + (lp * 2 + pl) * PLANE + lk * B3_RS + 16 * ld_);
+        r4[sw] = v0;
+        r4[sw ^ 1] = v1;
+    };
+    auto frag = [&](const short* S, int panel, int pl, int col, int off) -> f16x8_t {
+        const short* b = S + (panel * 2 + pl) * PLANE + off + col;
+        const i16x4_t r0 = lds_tr16(b), r1 = lds_tr16(b + 4 * B3_RS);
+        return __builtin_bit_cast(f16x8_t, (i16x8_t)__builtin_shufflevector(r0, r1, 0, 1, 2, 3, 4, 5, 6, 7));
+    };
+    auto fragB = [&](const short* S, int pl, f16x8_t (&b)[2]) {
+#pragma unroll
+        for (int y = 0; y < 2; y++) b[y] = frag(S, 1, pl, wn * 64 + 32 * y, rd_offB);
+    };
+    auto fragsA = [&](const short* S, int pa, f16x8_t (&a)[4]) {
+#pragma unroll
+        for (int x = 0; x < 4; x++) a[x] = frag(S, 0, pa, wm * 128 + 32 * x, x >= 2 ? rd_off + dswz : rd_off);
+    };
+    auto group = [&](const f16x8_t (&a)[4], const f16x8_t (&b)[2]) {
+#pragma unroll
+        for (int x = 0; x < 4; x++)
+#pragma unroll
+            for (int y = 0; y < 2; y++)
+                acc[x][y] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[x], b[y], acc[x][y], 0, 0, 0);
+    };
+    // V VALU after each of a group's 8 MFMAs
+    auto pin = [&](auto v) {
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, decltype(v)::value, 0);
+        }
+    };
+    {
+        load(0);
+        uint32_t sel[8];
+        make_sel(rw, sel);
+        store_plane(lds, 0, sel);
+        store_plane(lds, 1, sel);
+        load(nst > 1 ? 1 : 0);
+    }
+    __syncthreads();
+    f16x8_t B0s[2], B1s[2], B0t[2], B1t[2];
+    fragB(lds, 0, B0s);
+    fragB(lds, 1, B1s);
+    // the loader runs unconditionally (the last stage expands into the idle buffer and its code
+    // loads clamp to the last stage) so each MFMA group and its VALU share one basic block
+    auto stage = [&](uint64_t s, f16x8_t (&B0)[2], f16x8_t (&B1)[2], f16x8_t (&B0n)[2], f16x8_t (&B1n)[2]) {
+        const short* cur = lds + (s & 1) * STAGE;
+        short* nxt = lds + ((s + 1) & 1) * STAGE;
+        f16x8_t A0[4], A1[4];
+        fragsA(cur, 0, A0);
+        fragsA(cur, 1, A1);
+        uint32_t sel[8];
+        group(A0, B0);
+        make_sel(rw, sel);
+        store_plane(nxt, 0, sel);
+        if constexpr (MODE == 0) pin(std::integral_constant<int, 3>{});
+        group(A0, B1);
+        store_plane(nxt, 1, sel);
+        if constexpr (MODE == 0) pin(std::integral_constant<int, 1>{});
+        load(s + 2 < nst ? s + 2 : nst - 1);
+        __syncthreads();
+        fragB(nxt, 0, B0n);
+        fragB(nxt, 1, B1n);
+        group(A1, B0);
+    };
+    for (uint64_t s = 0; s < nst; s += 2) {
+        stage(s, B0s, B1s, B0t, B1t);
+        if (s + 1 < nst) stage(s + 1, B0t, B1t, B0s, B1s);
+    }
+    epilogue_pi<LOCAL>(acc, tiles, n, bi, bj, accumulate, lane, wm, wn, wg);
 }
 
 }  // namespace f32w
@@ -1383,8 +1574,15 @@ void launch_lut_bf3(const float* lut, uint64_t m, uint32_t* lut3, hipStream_t st
     SNPMI_HIP(hipGetLastError());
 }
 
+void launch_lut_h2(const float* lut, uint64_t m, uint32_t* lut2, uint32_t* flag, hipStream_t st) {
+    const uint64_t mpad = lut_bf3_entries(m);
+    SNPMI_HIP(hipMemsetAsync(flag, 0, sizeof(uint32_t), st));
+    f32w::k_lut_h2<<<(unsigned)ceil_div(mpad, 256), 256, 0, st>>>(lut, m, mpad, lut2, flag);
+    SNPMI_HIP(hipGetLastError());
+}
+
 void launch_syrk_packed_bf3(const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m, const uint32_t* lut3,
-                            float* tiles, int accumulate, hipStream_t st) {
+                            float* tiles, int accumulate, hipStream_t st, const H2Lut* h2) {
     const uint64_t nb = ceil_div(n, 256), g = nb * (nb + 1) / 2;
     if (g == 0) return;
     SNPMI_REQUIRE(g < (1ull << 31), SNPMI_E_ARG, "too many GRM blocks for one launch");
@@ -1401,6 +1599,15 @@ void launch_syrk_packed_bf3(const uint8_t* packed, uint64_t pitch, uint64_t n, u
     // 307.1 for MODE 1 at N=50k, 304.1 vs 300.5 at N=30k (profiles/r01i/ubench_syrk_bf3_mode2.jsonl);
     // SIMD partners staggered by one loader slot (waves 4-7 expand before group 0, runtime
     // plane index, 3 VGPRs spilled) lost: 296.8 vs 313.5 (ubench_syrk_bf3_stagger.jsonl).
+    if (h2) {
+        if (g_variant_syrk == 41) f32w::k_syrk_h2<false, 1><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles, accumulate);
+        else f32w::k_syrk_h2<><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles, accumulate);
+        SNPMI_HIP(hipGetLastError());
+        f32w::k_syrk_bf3<false, false, 5><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, lut3, tiles, accumulate, 0, 1, 0, 0,
+                                                                      h2->flag);
+        SNPMI_HIP(hipGetLastError());
+        return;
+    }
     switch (g_variant_syrk) {
         case 30: f32w::k_syrk_bf3<><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, lut3, tiles, accumulate); break;
         case 31: f32w::k_syrk_bf3<false, true><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, lut3, tiles, accumulate); break;
@@ -1416,20 +1623,27 @@ void launch_syrk_packed_bf3(const uint8_t* packed, uint64_t pitch, uint64_t n, u
 // split-K form for grids too small to fill the chip (N <~ 16k): `slices` partial tile sets in
 // `partial` (each n_tiles_upper(n) * 128^2 floats, overwritten), then a deterministic reduce
 void launch_syrk_packed_bf3_split(const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m, const uint32_t* lut3,
-                                  int slices, float* partial, float* tiles, int accumulate, hipStream_t st) {
+                                  int slices, float* partial, float* tiles, int accumulate, hipStream_t st,
+                                  const H2Lut* h2) {
     const uint64_t nb = ceil_div(n, 256), g = nb * (nb + 1) / 2;
     const uint64_t elems = n_tiles_upper(n) * BM * BM;
     const uint64_t kslice = round_up(ceil_div(m, (uint64_t)slices), (uint64_t)f32w::BK);
     const unsigned S = (unsigned)ceil_div(m, kslice);
     SNPMI_REQUIRE(g < (1ull << 31) && S >= 1, SNPMI_E_ARG, "bad split");
+    if (h2) {
+        f32w::k_syrk_h2<><<<dim3((unsigned)g, S), 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, partial, 0, 0, 1,
+                                                                 kslice, elems);
+        SNPMI_HIP(hipGetLastError());
+    }
     f32w::k_syrk_bf3<false, false, 5><<<dim3((unsigned)g, S), 512, 0, st>>>(packed, pitch, n, m, lut3, partial, 0, 0, 1,
-                                                                          kslice, elems);
+                                                                          kslice, elems, h2 ? h2->flag : nullptr);
     SNPMI_HIP(hipGetLastError());
     launch_tile_reduce(partial, S, elems, tiles, accumulate, st);
 }
 
 void launch_syrk_packed_bf3_part(const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m, const uint32_t* lut3,
-                                 int rank, int world, float* blocks, int accumulate, hipStream_t st) {
+                                 int rank, int world, float* blocks, int accumulate, hipStream_t st,
+                                 const H2Lut* h2) {
     const uint64_t nloc = grm_part_blocks(n, rank, world);
     if (nloc == 0) return;
     SNPMI_REQUIRE(nloc < (1ull << 31), SNPMI_E_ARG, "too many GRM blocks for one launch");
@@ -1439,8 +1653,14 @@ void launch_syrk_packed_bf3_part(const uint8_t* packed, uint64_t pitch, uint64_t
         if (!accumulate) SNPMI_HIP(hipMemsetAsync(blocks, 0, nloc * 256 * 256 * sizeof(float), st));
         return;
     }
+    if (h2) {
+        f32w::k_syrk_h2<true><<<(unsigned)nloc, 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, blocks, accumulate,
+                                                               (uint32_t)rank, (uint32_t)world);
+        SNPMI_HIP(hipGetLastError());
+    }
     f32w::k_syrk_bf3<true, false, 5><<<(unsigned)nloc, 512, 0, st>>>(packed, pitch, n, m, lut3, blocks, accumulate,
-                                                                     (uint32_t)rank, (uint32_t)world);
+                                                                     (uint32_t)rank, (uint32_t)world, 0, 0,
+                                                                     h2 ? h2->flag : nullptr);
     SNPMI_HIP(hipGetLastError());
 }
 

@@ -321,13 +321,15 @@ def test_kerneldata_diag_k_to_n():
     assert abs(np.diag(kd.val).sum() - 3) < 1e-7  # kernelreader/test.py:221-229
 
 
-@pytest.fixture(params=[0, 4, 5, 20, 30, 31, 33, 34],
-                ids=["auto", "syrk256", "syrk128", "f32twophase", "bf3plain", "bf3xcd", "bf3mode1", "bf3mode2"])
+@pytest.fixture(params=[0, 41, 36, 4, 5, 20, 30, 31, 33, 34],
+                ids=["auto", "h2nopin", "bf3", "syrk256", "syrk128", "f32twophase", "bf3plain", "bf3xcd", "bf3mode1",
+                     "bf3mode2"])
 def syrk_variant(request):
-    """Run a test under each SYRK kernel -- f32: 0 = default (packed: the bf16x3-split kernel on
-    the bf16 MFMA pipe, interleaved loader pinned one VALU per MFMA, mid-stage barrier with the
-    next B planes prefetched), 34 = without the pin, 33 = end-of-stage barrier, 30/31 = its
-    plain-loader forms, 4 = f32
+    """Run a test under each SYRK kernel -- f32: 0 = default (packed: the fp16x2-split kernel,
+    3 products on the fp16 MFMA pipe, with the bf16x3 kernel as its range fallback), 41 = the
+    fp16x2 kernel without the pinned VALU schedule, 36 = the bf16x3 kernel alone (interleaved
+    loader pinned one VALU per MFMA, mid-stage barrier with the next B planes prefetched), 34 =
+    without the pin, 33 = end-of-stage barrier, 30/31 = its plain-loader forms, 4 = f32
     MFMA 256x256 fused, 5 = f32 MFMA 128x128, 20 = f32 MFMA two-phase (decode to Z + glds);
     f64: 0/4 = interleaved bank-rotated loader, 5 = plain loader -- and restore the default."""
     N.call("snpmi_set_kernel_variant", b"syrk", request.param)
@@ -371,6 +373,39 @@ def test_grm_stage_counts(m, syrk_variant):
             O.standardize_native(Z)
             ref = Z.astype(np.float64).dot(Z.astype(np.float64).T)
             grm_close(b.read_kernel(Unit(), dtype=dtype).val, ref, tol)
+
+
+@pytest.mark.parametrize("case", ["unit", "beta11", "beta125_common", "beta125_mixed", "one_carrier"])
+def test_grm_h2_range_fallback(case, syrk_variant):
+    """The fp16x2 SYRK holds f32 accuracy only while each SNP's largest |LUT value| is in
+    [2^-2, 2^15): Unit and Beta(1,1) blocks stay on it (one_carrier: M_s ~ sqrt(n)); Beta(1,25)
+    over common SNPs (weights ~1e-6, fp16 subnormals) and a block mixing rare and common SNPs
+    must take the bf16x3 fallback -- all checked against the f64 oracle at 1e-5 of the largest
+    diagonal, which the fp16 kernel alone misses by orders of magnitude on the common-SNP block."""
+    rng = np.random.default_rng(7)
+    n, m = 700, 53
+    p = rng.uniform(0.3, 0.5, size=m) if case == "beta125_common" else rng.uniform(0.002, 0.5, size=m)
+    val = (rng.random((n, m)) < p).astype(np.float64) + (rng.random((n, m)) < p)
+    if case == "one_carrier":
+        val[:] = 0
+        val[rng.integers(0, n, size=m), np.arange(m)] = 1
+    val[rng.random(val.shape) < 0.03] = np.nan
+    is_beta, a, b = {"beta11": (True, 1, 1), "beta125_common": (True, 1, 25),
+                     "beta125_mixed": (True, 1, 25)}.get(case, (False, np.nan, np.nan))
+    std = Beta(a, b) if is_beta else Unit()
+    d = SnpData(iid=[["a", str(i)] for i in range(n)], sid=["s%d" % j for j in range(m)], val=val)
+    Z = val.copy(order="F")
+    O.standardize_native(Z, is_beta, a, b)
+    ref = Z.dot(Z.T)
+    with tempfile.TemporaryDirectory() as tmp:
+        bd = Bed.write(os.path.join(tmp, "t.bed"), d, count_A1=False)
+        K = bd.read_kernel(std, dtype=np.float32).val
+        grm_close(K, ref, 1e-5)
+        grm_close(bd.read_kernel(std, dtype=np.float32, block_size=16).val, ref, 1e-5)
+    # f32-level accuracy, not just the 1e-5 bar: ~2^-21 of the largest diagonal for the split
+    # kernels (fp16 subnormal residuals included), f32 MFMA rounding for the others
+    err = np.abs(K.astype(np.float64) - ref).max() / np.abs(np.diag(ref)).max()
+    assert err <= 2e-6, "GRM max|dK|/max diag = %g" % err
 
 
 # ---------------------------------------------------------------------------------- device API
