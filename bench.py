@@ -10,9 +10,10 @@ Metric (BASELINE.json): "SNPs/sec standardized (500k x 1M) + GRM GF/s at 1/2/4/8
                block * (ceil(N/4) + 4N) / its mean HIP-event duration, vs 8.0 TB/s.
   grm        = SnpKernel GRM of configs[3] (50k iid x 500k SNP, Unit, block 10k, f32): SNP blocks
                round-robin over ranks, one RCCL all-reduce of the upper-triangle K tiles.  The f32
-               products run on the bf16 MFMA pipe as 6 bf16 products of each value's exact bf16x3
-               split (f32 accuracy, f32 accumulate).  gflops uses N(N+1)M (SYRK work, SURVEY.md
-               §8d); roofline vs 2.5 PF bf16 dense / 6 = 416.7 TF (the f32-MFMA peak is 157.3).
+               products run on the fp16 MFMA pipe as 3 fp16 products of each value's fp16x2 split
+               (f32-level accuracy, f32 accumulate; bf16x3 = 6 bf16 products when a SNP's LUT is
+               outside fp16's range).  gflops uses N(N+1)M (SYRK work); roofline
+               vs 2.5 PF fp16 dense / 3 = 833.3 TF (the f32-MFMA peak is 157.3).
   cpu_baseline = the oracle's C/OpenMP decode + one-pass Unit standardize (the CPU restatement
                of bed-reader's read + standardize_f32) on a sample of the same packed columns,
                rank 0 only; grm.cpu_baseline = NumPy/OpenBLAS Z.dot(Z.T) (snpreader.py:655).
@@ -36,9 +37,10 @@ METRIC = "SNPs/sec standardized (500k×1M) + GRM GF/s at 1/2/4/8 GPUs"
 HBM_PEAK_GBS = 8000.0
 MFMA_F32_PEAK_TFLOPS = 157.3
 MFMA_BF16_PEAK_TFLOPS = 2500.0
-# f32 GRM on the bf16 MFMA pipe: each f32 product = 6 bf16 MFMA products of the bf16x3 split
-BF3_PRODUCTS = 6
-BF3_PEAK_TFLOPS = MFMA_BF16_PEAK_TFLOPS / BF3_PRODUCTS
+# f32 GRM on the fp16 MFMA pipe (same dense rate as bf16): each f32 product = 3 fp16 MFMA
+# products of the fp16x2 split (k_syrk_h2; Unit LUTs always fit fp16's range)
+SPLIT_PRODUCTS = 3
+SPLIT_PEAK_TFLOPS = MFMA_BF16_PEAK_TFLOPS / SPLIT_PRODUCTS
 
 
 def parse():
@@ -370,7 +372,7 @@ def leg_grm(N, args, dist, rccl):
     N.call("snpmi_dev_grm_trace", tiles.p, n, N.DT_F32, ctypes.byref(tr))
     flops_full_block = n * (n + 1) * B
     nb = (n + 255) // 256
-    exec_ratio = BF3_PRODUCTS * 2 * 256 * 256 * (nb * (nb + 1) // 2) / (n * (n + 1))  # executed bf16 / algorithmic
+    exec_ratio = SPLIT_PRODUCTS * 2 * 256 * 256 * (nb * (nb + 1) // 2) / (n * (n + 1))  # executed bf16 / algorithmic
     res = dict(wall=wall, syrk_ms=syrk_ms, allreduce_ms=allreduce_ms, trace=tr.value, exec_ratio=exec_ratio,
                # throughput over this rank's launches (the last block of a shard can be partial)
                mean_tflops=(n * (n + 1) * my_m / (np.sum(syrk_ms) * 1e-3) / 1e12) if syrk_ms else 0.0,
@@ -543,20 +545,22 @@ def main():
         r2 = leg_grm(N, args, dist, rccl)
         n, m = args.grm_iid, args.grm_sid
         gf = n * (n + 1) * m / r2["wall"] / 1e9
-        grm = {"workload": "cfg4: %d iid x %d SNP, Unit, block %d, f32 (bf16x3 MFMA) SYRK, SNPs split into %d equal "
+        grm = {"workload": "cfg4: %d iid x %d SNP, Unit, block %d, f32 (fp16x2 MFMA) SYRK, SNPs split into %d equal "
                            "contiguous shard(s) streamed in blocks%s" % (n, m, args.grm_block, dist.world,
                                                                          ", RCCL all-reduce of K tiles" if rccl else ""),
                "gflops": gf, "snps_per_s": m / r2["wall"], "seconds": r2["wall"], "scaling": "strong",
                "allreduce_ms": r2["allreduce_ms"], "trace_K": r2["trace"],
-               "roofline": {"bound": "mfma", "achieved": r2["mean_tflops"], "peak": BF3_PEAK_TFLOPS,
-                            "unit": "TFLOP/s", "frac": r2["mean_tflops"] / BF3_PEAK_TFLOPS,
-                            "traffic": pmc_traffic("f32w::k_syrk_bf3", "grm", n, args.grm_block),
-                            "kernel": "f32w::k_syrk_bf3<false,false,5>: f32 GRM as 6 bf16 MFMA products of each "
-                                      "value's exact bf16x3 split, f32 accumulate (v_mfma_f32_32x32x16_bf16); "
-                                      "peak = 2.5 PF bf16 dense / 6; time per block includes k_lut_bf3",
+               "roofline": {"bound": "mfma", "achieved": r2["mean_tflops"], "peak": SPLIT_PEAK_TFLOPS,
+                            "unit": "TFLOP/s", "frac": r2["mean_tflops"] / SPLIT_PEAK_TFLOPS,
+                            "traffic": pmc_traffic("f32w::k_syrk_h2", "grm", n, args.grm_block),
+                            "kernel": "f32w::k_syrk_h2<false,4>: f32 GRM as 3 fp16 MFMA products of each "
+                                      "value's fp16x2 split, f32 accumulate (v_mfma_f32_32x32x16_f16); "
+                                      "peak = 2.5 PF fp16 dense / 3; time per block includes k_lut_bf3, "
+                                      "k_lut_h2 and the range-gated bf16x3 launch (exits at once for Unit)",
                             "per_launch_flops": n * (n + 1) * args.grm_block,
                             "f32_mfma_peak": MFMA_F32_PEAK_TFLOPS,
-                            "mfma_util_executed": r2["mean_tflops"] * r2["exec_ratio"] / MFMA_BF16_PEAK_TFLOPS}}
+                            "mfma_util_executed": r2["mean_tflops"] * r2["exec_ratio"] / MFMA_BF16_PEAK_TFLOPS,
+                            "bf16x3_peak": MFMA_BF16_PEAK_TFLOPS / 6}}
     grm5 = None
     run5 = args.grm5 == "on" or (args.grm5 == "auto" and dist.world >= 4 and not args.skip_grm)
     if run5:
@@ -569,9 +573,9 @@ def main():
                 "h2d_ms": r3["h2d_ms"], "allgather_ms": r3["allgather_ms"], "syrk_ms": r3["syrk_ms"],
                 "gflops": gf5, "seconds": r3["wall"], "scaling": "strong",
                 "blocks_on_rank0": r3["n_local_blocks"], "K_bytes_per_rank": r3["n_local_blocks"] * 256 * 256 * 4,
-                "roofline": {"bound": "mfma", "achieved": gf5 / 1e3 / dist.world, "peak": BF3_PEAK_TFLOPS,
-                             "unit": "TFLOP/s per GPU", "frac": gf5 / 1e3 / dist.world / BF3_PEAK_TFLOPS,
-                             "traffic": None, "kernel": "f32w::k_syrk_bf3<true,false,5> (bf16x3 split, 6 bf16 "
+                "roofline": {"bound": "mfma", "achieved": gf5 / 1e3 / dist.world, "peak": SPLIT_PEAK_TFLOPS,
+                             "unit": "TFLOP/s per GPU", "frac": gf5 / 1e3 / dist.world / SPLIT_PEAK_TFLOPS,
+                             "traffic": None, "kernel": "f32w::k_syrk_h2<true,4> (fp16x2 split, 3 fp16 "
                                                         "MFMA products, f32 accumulate; wall incl. H2D + all-gather)"},
                 "projected_seconds_1M_snps": r3["wall"] * 1_000_000 / m5}
         if r3.get("parity_sample") is not None:

@@ -1046,13 +1046,15 @@ typedef _Float16 f16x8_t __attribute__((ext_vector_type(8)));
 // (loaded one stage ahead) are expanded and stored plane by plane beside groups 0-1, the loads
 // of stage s+2 are issued, then one barrier; stage s+1's B fragments are read into a second
 // register set under group 2.  Runs only when *flag == 0 (see k_lut_h2).
-template <bool LOCAL = false, int MODE = 0>
+template <bool LOCAL = false, int MODE = 4>
 __global__ __launch_bounds__(512, 1) void k_syrk_h2(const uint8_t* __restrict__ P, uint64_t pitch, uint64_t n,
                                                     uint64_t kdim, const uint32_t* __restrict__ lut2,
                                                     const uint32_t* __restrict__ flag, float* __restrict__ tiles,
                                                     int accumulate, uint32_t part_rank = 0, uint32_t part_world = 1,
                                                     uint64_t kslice = 0, uint64_t slice_elems = 0) {
-    constexpr int PLANE = B3_PLANE, STAGE = 2 * 2 * PLANE;
+    // KS = 16-SNP k-steps per LDS stage (MODE 4/5: two, one barrier per 32 SNPs)
+    constexpr int KS = MODE >= 4 ? 2 : 1, SBK = KS * BK;
+    constexpr int PLANE = KS * B3_PLANE, STAGE = 2 * 2 * PLANE;
     __shared__ __attribute__((aligned(16))) short lds[2 * STAGE];
     if (*flag) return;  // a SNP of this block is outside fp16's range: k_syrk_bf3 runs instead
     if (gridDim.y > 1) {
@@ -1083,14 +1085,17 @@ __global__ __launch_bounds__(512, 1) void k_syrk_h2(const uint8_t* __restrict__ 
     for (int x = 0; x < 4; x++)
 #pragma unroll
         for (int y = 0; y < 2; y++) acc[x][y] = (f32x16){};
-    const uint64_t nst = (kdim + BK - 1) / BK;
+    const uint64_t nst = (kdim + SBK - 1) / SBK;
 
-    uint32_t rw;
-    uint4 rl;
+    uint32_t rw[KS];
+    uint4 rl[KS];
     auto load = [&](uint64_t st) {
-        const uint8_t* a = wp + st * BK * pitch;
-        rw = *reinterpret_cast<const uint32_t*>(a <= wlast ? a : wlast);
-        rl = *reinterpret_cast<const uint4*>(lp2 + 4 * BK * st);
+#pragma unroll
+        for (int h = 0; h < KS; h++) {
+            const uint8_t* a = wp + (st * SBK + h * BK) * pitch;
+            rw[h] = *reinterpret_cast<const uint32_t*>(a <= wlast ? a : wlast);
+            rl[h] = *reinterpret_cast<const uint4*>(lp2 + 4 * (SBK * st + h * BK));
+        }
     };
     auto make_sel = [&](uint32_t w, uint32_t (&sel)[8]) {
 #pragma unroll
@@ -1101,9 +1106,9 @@ __global__ __launch_bounds__(512, 1) void k_syrk_h2(const uint8_t* __restrict__ 
             sel[2 * j + 1] = __builtin_amdgcn_perm(o, v, 0x07030602u);
         }
     };
-    auto store_plane = [&](short* S, int pl, const uint32_t (&sel)[8]) {
-        const uint32_t lo = pl == 0 ? rl.x : rl.z;
-        const uint32_t hi = pl == 0 ? rl.y : rl.w;
+    auto store_plane = [&](short* S, int pl, int h, const uint32_t (&sel)[8]) {
+        const uint32_t lo = pl == 0 ? rl[h].x : rl[h].z;
+        const uint32_t hi = pl == 0 ? rl[h].y : rl[h].w;
         uint4 v0, v1;
         v0.x = __builtin_amdgcn_perm(hi, lo, sel[0]);
         v0.y = __builtin_amdgcn_perm(hi, lo, sel[1]);
@@ -1113,22 +1118,22 @@ __global__ __launch_bounds__(512, 1) void k_syrk_h2(const uint8_t* __restrict__ 
         v1.y = __builtin_amdgcn_perm(hi, lo, sel[5]);
         v1.z = __builtin_amdgcn_perm(hi, lo, sel[6]);
         v1.w = __builtin_amdgcn_perm(hi, lo, sel[7]);
-        uint4* r4 = reinterpret_cast<uint4*>(S + (lp * 2 + pl) * PLANE + lk * B3_RS + 16 * ld_);
+        uint4* r4 = reinterpret_cast<uint4*>(S + (lp * 2 + pl) * PLANE + (lk + BK * h) * B3_RS + 16 * ld_);
         r4[sw] = v0;
         r4[sw ^ 1] = v1;
     };
-    auto frag = [&](const short* S, int panel, int pl, int col, int off) -> f16x8_t {
-        const short* b = S + (panel * 2 + pl) * PLANE + off + col;
+    auto frag = [&](const short* S, int panel, int pl, int h, int col, int off) -> f16x8_t {
+        const short* b = S + (panel * 2 + pl) * PLANE + h * BK * B3_RS + off + col;
         const i16x4_t r0 = lds_tr16(b), r1 = lds_tr16(b + 4 * B3_RS);
         return __builtin_bit_cast(f16x8_t, (i16x8_t)__builtin_shufflevector(r0, r1, 0, 1, 2, 3, 4, 5, 6, 7));
     };
-    auto fragB = [&](const short* S, int pl, f16x8_t (&b)[2]) {
+    auto fragB = [&](const short* S, int pl, int h, f16x8_t (&b)[2]) {
 #pragma unroll
-        for (int y = 0; y < 2; y++) b[y] = frag(S, 1, pl, wn * 64 + 32 * y, rd_offB);
+        for (int y = 0; y < 2; y++) b[y] = frag(S, 1, pl, h, wn * 64 + 32 * y, rd_offB);
     };
-    auto fragsA = [&](const short* S, int pa, f16x8_t (&a)[4]) {
+    auto fragsA = [&](const short* S, int pa, int h, f16x8_t (&a)[4]) {
 #pragma unroll
-        for (int x = 0; x < 4; x++) a[x] = frag(S, 0, pa, wm * 128 + 32 * x, x >= 2 ? rd_off + dswz : rd_off);
+        for (int x = 0; x < 4; x++) a[x] = frag(S, 0, pa, h, wm * 128 + 32 * x, x >= 2 ? rd_off + dswz : rd_off);
     };
     auto group = [&](const f16x8_t (&a)[4], const f16x8_t (&b)[2]) {
 #pragma unroll
@@ -1147,41 +1152,86 @@ __global__ __launch_bounds__(512, 1) void k_syrk_h2(const uint8_t* __restrict__ 
     };
     {
         load(0);
-        uint32_t sel[8];
-        make_sel(rw, sel);
-        store_plane(lds, 0, sel);
-        store_plane(lds, 1, sel);
+#pragma unroll
+        for (int h = 0; h < KS; h++) {
+            uint32_t sel[8];
+            make_sel(rw[h], sel);
+            store_plane(lds, 0, h, sel);
+            store_plane(lds, 1, h, sel);
+        }
         load(nst > 1 ? 1 : 0);
     }
     __syncthreads();
     f16x8_t B0s[2], B1s[2], B0t[2], B1t[2];
-    fragB(lds, 0, B0s);
-    fragB(lds, 1, B1s);
-    // the loader runs unconditionally (the last stage expands into the idle buffer and its code
-    // loads clamp to the last stage) so each MFMA group and its VALU share one basic block
-    auto stage = [&](uint64_t s, f16x8_t (&B0)[2], f16x8_t (&B1)[2], f16x8_t (&B0n)[2], f16x8_t (&B1n)[2]) {
+    fragB(lds, 0, 0, B0s);
+    fragB(lds, 1, 0, B1s);
+    // The loader runs unconditionally (the last stage expands into the idle buffer and its code
+    // loads clamp to the last stage) so each MFMA group and its VALU share one basic block.
+    // MODE 2/3: stage s+1's A plane-0 fragments are read after the barrier too (a second A
+    // register set), so the next stage's first group waits on no LDS read; MODE 0/3/5 pin the
+    // loader VALU between the MFMAs, MODE 1/2/4 leave the order to the compiler.
+    constexpr bool kPreA = MODE == 2 || MODE == 3, kPin = MODE == 0 || MODE == 3 || MODE == 5;
+    f16x8_t A0s[4], A0t[4];
+    if constexpr (kPreA) fragsA(lds, 0, 0, A0s);
+    auto stage = [&](uint64_t s, f16x8_t (&B0)[2], f16x8_t (&B1)[2], f16x8_t (&A0)[4], f16x8_t (&B0n)[2],
+                     f16x8_t (&B1n)[2], f16x8_t (&A0n)[4]) {
         const short* cur = lds + (s & 1) * STAGE;
         short* nxt = lds + ((s + 1) & 1) * STAGE;
-        f16x8_t A0[4], A1[4];
-        fragsA(cur, 0, A0);
-        fragsA(cur, 1, A1);
-        uint32_t sel[8];
-        group(A0, B0);
-        make_sel(rw, sel);
-        store_plane(nxt, 0, sel);
-        if constexpr (MODE == 0) pin(std::integral_constant<int, 3>{});
-        group(A0, B1);
-        store_plane(nxt, 1, sel);
-        if constexpr (MODE == 0) pin(std::integral_constant<int, 1>{});
-        load(s + 2 < nst ? s + 2 : nst - 1);
-        __syncthreads();
-        fragB(nxt, 0, B0n);
-        fragB(nxt, 1, B1n);
-        group(A1, B0);
+        if constexpr (KS == 1) {
+            f16x8_t A1[4];
+            if constexpr (!kPreA) fragsA(cur, 0, 0, A0);
+            fragsA(cur, 1, 0, A1);
+            uint32_t sel[8];
+            group(A0, B0);
+            make_sel(rw[0], sel);
+            store_plane(nxt, 0, 0, sel);
+            if constexpr (kPin) pin(std::integral_constant<int, 3>{});
+            group(A0, B1);
+            store_plane(nxt, 1, 0, sel);
+            if constexpr (kPin) pin(std::integral_constant<int, 1>{});
+            load(s + 2 < nst ? s + 2 : nst - 1);
+            __syncthreads();
+            fragB(nxt, 0, 0, B0n);
+            fragB(nxt, 1, 0, B1n);
+            if constexpr (kPreA) fragsA(nxt, 0, 0, A0n);
+            group(A1, B0);
+        } else {
+            // k-step 0 with the prefetched B, k-step 1 read from cur before the barrier (after
+            // it, stage s+1's stores may overwrite cur); the expansion of stage s+1 (2 k-steps
+            // x 2 planes) rides on groups 0-3
+            f16x8_t Ax[4], Ay[4], C0[2], C1[2];
+            fragsA(cur, 0, 0, Ax);
+            fragsA(cur, 1, 0, Ay);
+            uint32_t sel[8];
+            group(Ax, B0);
+            make_sel(rw[0], sel);
+            store_plane(nxt, 0, 0, sel);
+            if constexpr (kPin) pin(std::integral_constant<int, 3>{});
+            group(Ax, B1);
+            store_plane(nxt, 1, 0, sel);
+            fragB(cur, 0, 1, C0);
+            fragB(cur, 1, 1, C1);
+            if constexpr (kPin) pin(std::integral_constant<int, 1>{});
+            fragsA(cur, 0, 1, Ax);
+            group(Ay, B0);
+            make_sel(rw[1], sel);
+            store_plane(nxt, 0, 1, sel);
+            if constexpr (kPin) pin(std::integral_constant<int, 3>{});
+            fragsA(cur, 1, 1, Ay);
+            group(Ax, C0);
+            store_plane(nxt, 1, 1, sel);
+            if constexpr (kPin) pin(std::integral_constant<int, 1>{});
+            group(Ax, C1);
+            load(s + 2 < nst ? s + 2 : nst - 1);
+            __syncthreads();
+            fragB(nxt, 0, 0, B0n);
+            fragB(nxt, 1, 0, B1n);
+            group(Ay, C0);
+        }
     };
     for (uint64_t s = 0; s < nst; s += 2) {
-        stage(s, B0s, B1s, B0t, B1t);
-        if (s + 1 < nst) stage(s + 1, B0t, B1t, B0s, B1s);
+        stage(s, B0s, B1s, A0s, B0t, B1t, A0t);
+        if (s + 1 < nst) stage(s + 1, B0t, B1t, A0t, B0s, B1s, A0s);
     }
     epilogue_pi<LOCAL>(acc, tiles, n, bi, bj, accumulate, lane, wm, wn, wg);
 }
@@ -1566,7 +1616,7 @@ void launch_syrk_packed_part(const uint8_t* packed, uint64_t pitch, uint64_t n, 
     SNPMI_HIP(hipGetLastError());
 }
 
-uint64_t lut_bf3_entries(uint64_t m) { return round_up(std::max<uint64_t>(m, 1), f32w::BK); }
+uint64_t lut_bf3_entries(uint64_t m) { return round_up(std::max<uint64_t>(m, 1), (uint64_t)2 * f32w::BK); }
 
 void launch_lut_bf3(const float* lut, uint64_t m, uint32_t* lut3, hipStream_t st) {
     const uint64_t mpad = lut_bf3_entries(m);
@@ -1600,8 +1650,19 @@ void launch_syrk_packed_bf3(const uint8_t* packed, uint64_t pitch, uint64_t n, u
     // SIMD partners staggered by one loader slot (waves 4-7 expand before group 0, runtime
     // plane index, 3 VGPRs spilled) lost: 296.8 vs 313.5 (ubench_syrk_bf3_stagger.jsonl).
     if (h2) {
-        if (g_variant_syrk == 41) f32w::k_syrk_h2<false, 1><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles, accumulate);
-        else f32w::k_syrk_h2<><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles, accumulate);
+        // MI355X, N=50k, 10k SNPs (tools/ubench.py syrk, profiles/r01j/ubench_syrk_h2_modes.jsonl):
+        // 32-SNP stages, compiler-ordered loader (MODE 4, default) 577 TFLOP/s; 16-SNP stages:
+        // MODE 1 530-554, loader pinned one-three VALU per MFMA (40) 539-545, next A plane-0
+        // prefetched after the barrier (42) 505, + pin (43) 551-564; 32-SNP + pin (46) 564;
+        // bf16x3 (36) 300-313.
+        switch (g_variant_syrk) {
+            case 40: f32w::k_syrk_h2<false, 0><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles, accumulate); break;
+            case 42: f32w::k_syrk_h2<false, 2><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles, accumulate); break;
+            case 43: f32w::k_syrk_h2<false, 3><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles, accumulate); break;
+            case 41: f32w::k_syrk_h2<false, 1><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles, accumulate); break;
+            case 46: f32w::k_syrk_h2<false, 5><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles, accumulate); break;
+            default: f32w::k_syrk_h2<false, 4><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles, accumulate);
+        }
         SNPMI_HIP(hipGetLastError());
         f32w::k_syrk_bf3<false, false, 5><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, lut3, tiles, accumulate, 0, 1, 0, 0,
                                                                       h2->flag);
@@ -1627,7 +1688,7 @@ void launch_syrk_packed_bf3_split(const uint8_t* packed, uint64_t pitch, uint64_
                                   const H2Lut* h2) {
     const uint64_t nb = ceil_div(n, 256), g = nb * (nb + 1) / 2;
     const uint64_t elems = n_tiles_upper(n) * BM * BM;
-    const uint64_t kslice = round_up(ceil_div(m, (uint64_t)slices), (uint64_t)f32w::BK);
+    const uint64_t kslice = round_up(ceil_div(m, (uint64_t)slices), (uint64_t)2 * f32w::BK);
     const unsigned S = (unsigned)ceil_div(m, kslice);
     SNPMI_REQUIRE(g < (1ull << 31) && S >= 1, SNPMI_E_ARG, "bad split");
     if (h2) {

@@ -17,7 +17,8 @@ KERNELS = {"k_decode_std_lds_f32": "k_decode_std_lds_f32", "k_decode_f<float, 4>
            "f32k::k_syrk<true": "f32k::k_syrk<true>", "k_syrk256<1, false>": "f32w::k_syrk256",
            "k_syrk256<1, true>": "f32w::k_syrk256<local>", "k_syrk256d<false": "f32w::k_syrk256d",
            "k_syrk256d<true": "f32w::k_syrk256d<local>", "k_snp_stats<float>": "k_snp_stats<float>",
-           "k_syrk_bf3<false": "f32w::k_syrk_bf3", "k_syrk_bf3<true": "f32w::k_syrk_bf3<local>"}
+           "k_syrk_bf3<false": "f32w::k_syrk_bf3", "k_syrk_bf3<true": "f32w::k_syrk_bf3<local>",
+           "k_syrk_h2<false": "f32w::k_syrk_h2", "k_syrk_h2<true": "f32w::k_syrk_h2<local>"}
 
 
 def short(name):
@@ -47,7 +48,7 @@ def main(prof, out):
             fv = sorted(f[k])
             full_w = [x for x in wv if x >= 0.95 * wv[-1]]
             full_f = [x for x in fv if x >= 0.95 * fv[-1]]
-            scale = 1.0 if "bf3" in k else 2.0
+            scale = 1.0 if ("bf3" in k or "h2" in k) else 2.0
             read_b = scale * sum(full_f) / len(full_f)
             write_b = sum(full_w) / len(full_w)
             res.setdefault(k, {})[leg] = {"read_bytes": read_b, "write_bytes": write_b,
