@@ -734,6 +734,21 @@ static void* session_tiles(Device& d) {
     return d.get(Device::S_SESSION, n_tiles_upper(g_session.n) * kTile * kTile * dtype_size(g_session.dtype));
 }
 
+// dense GRM operand on the device: f32 with n >= 4096 and the default variant takes the fp16x2
+// split kernel (falls back to the f32-MFMA k_syrk256d on the device-side range flag)
+static void syrk_dense_auto(Device& d, const void* Z, uint64_t ldz, uint64_t n, uint64_t m, int dt, void* tiles,
+                            int accumulate) {
+    if (dt == SNPMI_DT_F32 && (g_variant_syrk == 0 || (g_variant_syrk >= 47 && g_variant_syrk <= 49)) && n >= 4096 &&
+        m > 0 && ldz % 256 == 0) {
+        const uint64_t nb = ldz / 256, g = nb * (nb + 1) / 2;
+        uint16_t* planes = (uint16_t*)d.get(Device::S_H2, 4 * ldz * m + 256 + 4 * g);
+        uint32_t* flag = (uint32_t*)(planes + 2 * ldz * m);
+        launch_syrk_dense_h2((const float*)Z, ldz, n, m, planes, flag, flag + 64, (float*)tiles, accumulate, d.stream);
+        return;
+    }
+    launch_syrk_dense(Z, ldz, n, m, dt, tiles, accumulate, d.stream);
+}
+
 template <typename T>
 static void grm_dense_impl(const T* val, uint64_t rows, uint64_t cols, int order_c, int std_kind, double a, double b,
                            int use_stats, T* stats, int diag_k_to_n, double* factor, T* K_out) {
@@ -761,7 +776,7 @@ static void grm_dense_impl(const T* val, uint64_t rows, uint64_t cols, int order
     }
     const uint64_t tile_bytes = n_tiles_upper(rows) * kTile * kTile * sizeof(T);
     T* tiles = (T*)d.get(Device::S_TILES, tile_bytes);
-    if (rows > 0) launch_syrk_dense(Z, ldz, rows, cols, dt, tiles, 0, d.stream);
+    if (rows > 0) syrk_dense_auto(d, Z, ldz, rows, cols, dt, tiles, 0);
     grm_finish(d, tiles, rows, diag_k_to_n, factor, K_out);
 }
 
@@ -837,7 +852,7 @@ static void grm_add_dense_impl(const T* val, uint64_t rows, uint64_t cols, int o
         SNPMI_HIP(hipMemcpyAsync(Zc, val, rows * cols * sizeof(T), hipMemcpyHostToDevice, d.stream));
         launch_transpose_to_f(Zc, rows, cols, DT<T>::v, Z, ldz, d.stream);
     }
-    launch_syrk_dense(Z, ldz, rows, cols, DT<T>::v, tiles, g_session.wrote ? 1 : 0, d.stream);
+    syrk_dense_auto(d, Z, ldz, rows, cols, DT<T>::v, tiles, g_session.wrote ? 1 : 0);
     g_session.wrote = true;
     SNPMI_HIP(hipStreamSynchronize(d.stream));
 }
@@ -1320,7 +1335,7 @@ int snpmi_dev_syrk_dense(const void* Z, uint64_t ldz, uint64_t n_iid, uint64_t n
                          int accumulate) {
     return guarded([&] {
         SNPMI_REQUIRE(dtype == SNPMI_DT_F32 || dtype == SNPMI_DT_F64, SNPMI_E_ARG, "GRM dtype must be f32/f64");
-        launch_syrk_dense(Z, ldz, n_iid, n_sid, dtype, K_tiles, accumulate, stream());
+        syrk_dense_auto(device(), Z, ldz, n_iid, n_sid, dtype, K_tiles, accumulate);
     });
 }
 

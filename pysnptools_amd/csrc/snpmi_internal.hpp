@@ -65,7 +65,7 @@ struct Device {
     int cu_count = 0;
     // grow-only scratch slots
     enum Slot { S_PACKED, S_PACKED2, S_IDX, S_IDX2, S_LUT, S_STATS, S_OUT, S_TILES, S_K, S_DENSE,
-                S_DENSE2, S_RED, S_SESSION, S_PACKED_B, S_ZBLK, S_IDX32, S_LUT3, S_NUM };
+                S_DENSE2, S_RED, S_SESSION, S_PACKED_B, S_ZBLK, S_IDX32, S_LUT3, S_H2, S_NUM };
     void* buf[S_NUM] = {};
     hipEvent_t staged[2] = {};  // recorded after the H2D that last read pinned slot 0 / 1
     size_t cap[S_NUM] = {};
@@ -134,6 +134,11 @@ struct H2Lut {
     const uint32_t* flag;
 };
 void launch_lut_h2(const float* lut, uint64_t m, uint32_t* lut2, uint32_t* flag, hipStream_t st);
+// dense f32 operand (ld = round_up(n, 256), n >= 4096): split into fp16 planes (scratch of
+// 4 * ldz * m bytes) + k_syrk_h2<DENSE> in supertile block order (order: scratch of one u32
+// per 256-iid block), the f32-MFMA k_syrk256d gated on the range flag
+void launch_syrk_dense_h2(const float* Z, uint64_t ldz, uint64_t n, uint64_t m, uint16_t* planes, uint32_t* flag,
+                          uint32_t* order, float* tiles, int accumulate, hipStream_t st);
 void launch_syrk_packed_bf3(const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m, const uint32_t* lut3,
                             float* tiles, int accumulate, hipStream_t st, const H2Lut* h2 = nullptr);
 void launch_syrk_packed_bf3_split(const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m, const uint32_t* lut3,

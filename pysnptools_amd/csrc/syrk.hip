@@ -16,6 +16,9 @@
 //     standardized Z never exists in HBM.  DENSE loader: an F-order float matrix (SnpData).
 #include "snpmi_internal.hpp"
 
+#include <algorithm>
+#include <vector>
+
 namespace snpmi {
 namespace {
 
@@ -546,10 +549,12 @@ __device__ __forceinline__ uint64_t xcd_remap(uint64_t orig, uint64_t nwg) {
 template <bool LOCAL = false, int BKD = 16, int NBUF = 2, bool XCD = false>
 __global__ __launch_bounds__(512, 1) void k_syrk256d(const float* __restrict__ Z, uint64_t ldz, uint64_t n,
                                                     uint64_t kdim, float* __restrict__ tiles, int accumulate,
-                                                    uint32_t part_rank = 0, uint32_t part_world = 1) {
+                                                    uint32_t part_rank = 0, uint32_t part_world = 1,
+                                                    const uint32_t* __restrict__ gate = nullptr) {
     static_assert(NBUF == 2 || NBUF == 3, "2 or 3 LDS stages");
     constexpr int G = 2 * BKD / 8;  // glds per wave per stage (8 waves, one 1 KiB row each)
     __shared__ __attribute__((aligned(16))) float lds[NBUF][2][BKD * LDA];
+    if (gate && *gate == 0) return;  // fallback of the dense fp16x2 kernel (range flag raised)
     const uint64_t wg = XCD ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
     uint32_t bi, bj;
     tile_coords(LOCAL ? wg * part_world + part_rank : wg, bi, bj);
@@ -1038,6 +1043,39 @@ __global__ __launch_bounds__(256) void k_lut_h2(const float* __restrict__ lut, u
     reinterpret_cast<uint4*>(lut2)[s] = make_uint4(o[0], o[1], o[2], o[3]);
 }
 
+// dense f32 block Z ([sid][ldz], F order) -> two fp16 planes for k_syrk_h2<.., DENSE>:
+// planes[(s * 2 + p) * ldz + 16 d + pi(i)] = plane p of Z[s][16 d + i] (the packed loader's
+// in-group order), rows >= n zero; a column whose max |z| is outside [2^-2, 2^15) (and not 0)
+// raises *flag.  One 256-thread block per SNP column.
+__global__ __launch_bounds__(256) void k_split_h2(const float* __restrict__ Z, uint64_t ldz, uint64_t n,
+                                                  uint16_t* __restrict__ planes, uint32_t* __restrict__ flag) {
+    const uint64_t s = blockIdx.x;
+    const float* col = Z + s * ldz;
+    uint16_t* p0 = planes + s * 2 * ldz;
+    uint16_t* p1 = p0 + ldz;
+    float M = 0.f;
+    for (uint64_t r = threadIdx.x; r < ldz; r += 256) {
+        const float v = r < n ? col[r] : 0.f;
+        M = fmaxf(M, fabsf(v));
+        const _Float16 a0 = (_Float16)v;
+        const _Float16 a1 = (_Float16)(v - (float)a0);
+        const uint64_t o = (r & ~15ull) + (uint64_t)pi16((int)(r & 15));
+        p0[o] = __builtin_bit_cast(uint16_t, a0);
+        p1[o] = __builtin_bit_cast(uint16_t, a1);
+    }
+    __shared__ float red[256];
+    red[threadIdx.x] = M;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w) red[threadIdx.x] = fmaxf(red[threadIdx.x], red[threadIdx.x + w]);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        const float m = red[0];
+        if (m != 0.f && !(m >= 0.25f && m < 32768.f)) atomicOr(flag, 1u);
+    }
+}
+
 typedef _Float16 f16x8_t __attribute__((ext_vector_type(8)));
 
 // Same block structure, loader roles and LDS image as k_syrk_bf3 (two fp16 planes per panel
@@ -1046,7 +1084,9 @@ typedef _Float16 f16x8_t __attribute__((ext_vector_type(8)));
 // (loaded one stage ahead) are expanded and stored plane by plane beside groups 0-1, the loads
 // of stage s+2 are issued, then one barrier; stage s+1's B fragments are read into a second
 // register set under group 2.  Runs only when *flag == 0 (see k_lut_h2).
-template <bool LOCAL = false, int MODE = 4>
+// DENSE: the operand is a float block already split by k_split_h2 into two fp16 planes
+// ([sid][plane][ldp], pitch = ldp elements, each 16-iid group pi-permuted), copied verbatim.
+template <bool LOCAL = false, int MODE = 4, bool DENSE = false>
 __global__ __launch_bounds__(512, 1) void k_syrk_h2(const uint8_t* __restrict__ P, uint64_t pitch, uint64_t n,
                                                     uint64_t kdim, const uint32_t* __restrict__ lut2,
                                                     const uint32_t* __restrict__ flag, float* __restrict__ tiles,
@@ -1066,7 +1106,14 @@ __global__ __launch_bounds__(512, 1) void k_syrk_h2(const uint8_t* __restrict__ 
     }
     const uint64_t wg = blockIdx.x;
     uint32_t bi, bj;
-    tile_coords(LOCAL ? wg * part_world + part_rank : wg, bi, bj);
+    if constexpr (DENSE) {
+        // lut2 = block order table (supertile_order): the 256 blocks in flight share 32 panels
+        const uint32_t c = lut2[wg];
+        bi = c & 0xffffu;
+        bj = c >> 16;
+    } else {
+        tile_coords(LOCAL ? wg * part_world + part_rank : wg, bi, bj);
+    }
     const uint64_t i0 = (uint64_t)bi * BW, j0 = (uint64_t)bj * BW;
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
     const int wm = wave >> 2, wn = wave & 3;
@@ -1075,6 +1122,7 @@ __global__ __launch_bounds__(512, 1) void k_syrk_h2(const uint8_t* __restrict__ 
     const uint8_t* wp = P + (lp ? j0 : i0) / 4 + 4 * ld_ + (uint64_t)lk * pitch;
     const uint8_t* wlast = P + (lp ? j0 : i0) / 4 + 4 * ld_ + (kdim - 1) * pitch;
     const uint32_t* lp2 = lut2 + 4 * lk;
+    const uint16_t* dp = reinterpret_cast<const uint16_t*>(P) + (lp ? j0 : i0) + 16 * ld_;  // DENSE
     const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
     const int rd_off = (8 * (g >> 1) + q) * B3_RS + 16 * (g & 1) + 4 * pp;
     const int dswz = (pp >> 1) ? -8 : 8;
@@ -1089,15 +1137,29 @@ __global__ __launch_bounds__(512, 1) void k_syrk_h2(const uint8_t* __restrict__ 
 
     uint32_t rw[KS];
     uint4 rl[KS];
+    uint4 dv[KS][2][2];  // DENSE: [k-step][plane][16-B half]
     auto load = [&](uint64_t st) {
 #pragma unroll
         for (int h = 0; h < KS; h++) {
-            const uint8_t* a = wp + (st * SBK + h * BK) * pitch;
-            rw[h] = *reinterpret_cast<const uint32_t*>(a <= wlast ? a : wlast);
-            rl[h] = *reinterpret_cast<const uint4*>(lp2 + 4 * (SBK * st + h * BK));
+            if constexpr (DENSE) {
+                const uint64_t k = st * SBK + h * BK + lk;
+                const bool ok = k < kdim;
+                const uint4* a = reinterpret_cast<const uint4*>(dp + (ok ? k : kdim - 1) * 2 * pitch);
+                const uint4* b = reinterpret_cast<const uint4*>(dp + ((ok ? k : kdim - 1) * 2 + 1) * pitch);
+                const uint4 z = make_uint4(0, 0, 0, 0);
+                dv[h][0][0] = ok ? a[0] : z;
+                dv[h][0][1] = ok ? a[1] : z;
+                dv[h][1][0] = ok ? b[0] : z;
+                dv[h][1][1] = ok ? b[1] : z;
+            } else {
+                const uint8_t* a = wp + (st * SBK + h * BK) * pitch;
+                rw[h] = *reinterpret_cast<const uint32_t*>(a <= wlast ? a : wlast);
+                rl[h] = *reinterpret_cast<const uint4*>(lp2 + 4 * (SBK * st + h * BK));
+            }
         }
     };
     auto make_sel = [&](uint32_t w, uint32_t (&sel)[8]) {
+        if constexpr (DENSE) return;
 #pragma unroll
         for (int j = 0; j < 4; j++) {
             const uint32_t v = (w >> (2 * j)) & 0x03030303u;
@@ -1107,6 +1169,12 @@ __global__ __launch_bounds__(512, 1) void k_syrk_h2(const uint8_t* __restrict__ 
         }
     };
     auto store_plane = [&](short* S, int pl, int h, const uint32_t (&sel)[8]) {
+        if constexpr (DENSE) {
+            uint4* r4 = reinterpret_cast<uint4*>(S + (lp * 2 + pl) * PLANE + (lk + BK * h) * B3_RS + 16 * ld_);
+            r4[sw] = dv[h][pl][0];
+            r4[sw ^ 1] = dv[h][pl][1];
+            return;
+        }
         const uint32_t lo = pl == 0 ? rl[h].x : rl[h].z;
         const uint32_t hi = pl == 0 ? rl[h].y : rl[h].w;
         uint4 v0, v1;
@@ -1628,6 +1696,58 @@ void launch_lut_h2(const float* lut, uint64_t m, uint32_t* lut2, uint32_t* flag,
     const uint64_t mpad = lut_bf3_entries(m);
     SNPMI_HIP(hipMemsetAsync(flag, 0, sizeof(uint32_t), st));
     f32w::k_lut_h2<<<(unsigned)ceil_div(mpad, 256), 256, 0, st>>>(lut, m, mpad, lut2, flag);
+    SNPMI_HIP(hipGetLastError());
+}
+
+// Upper-triangle 256-iid blocks in supertile order: 16x16-block supertiles (I <= J) in
+// triangular order, blocks (bi <= bj) inside each; entry = bi | bj << 16.  The dense fp16x2
+// SYRK streams 4 B per value per panel, so the ~256 blocks in flight must share panels: in the
+// plain column order they touch ~nb A panels at once, in this order 32.
+static const std::vector<uint32_t>& supertile_order(uint64_t nb) {
+    static std::vector<uint32_t> tab;
+    static uint64_t tab_nb = 0;
+    if (tab_nb != nb) {
+        tab.clear();
+        const uint64_t ns = ceil_div(nb, 16);
+        for (uint64_t J = 0; J < ns; J++)
+            for (uint64_t I = 0; I <= J; I++)
+                for (uint64_t bj = 16 * J; bj < std::min(16 * J + 16, nb); bj++)
+                    for (uint64_t bi = 16 * I; bi < std::min(16 * I + 16, bj + 1); bi++)
+                        tab.push_back((uint32_t)(bi | (bj << 16)));
+        tab_nb = nb;
+    }
+    return tab;
+}
+
+void launch_syrk_dense_h2(const float* Z, uint64_t ldz, uint64_t n, uint64_t m, uint16_t* planes, uint32_t* flag,
+                          uint32_t* order, float* tiles, int accumulate, hipStream_t st) {
+    const uint64_t nb = ceil_div(n, 256), g = nb * (nb + 1) / 2;
+    if (g == 0) return;
+    SNPMI_REQUIRE(g < (1ull << 31) && m < (1ull << 31) && nb < 65536, SNPMI_E_ARG,
+                  "too many GRM blocks / SNPs for one launch");
+    SNPMI_REQUIRE(ldz % 256 == 0 && ldz >= nb * 256, SNPMI_E_ARG, "dense GRM operand needs ldz = round_up(n, 256)");
+    if (m == 0) {
+        if (!accumulate) SNPMI_HIP(hipMemsetAsync(tiles, 0, n_tiles_upper(n) * BM * BM * sizeof(float), st));
+        return;
+    }
+    SNPMI_HIP(hipMemsetAsync(flag, 0, sizeof(uint32_t), st));
+    f32w::k_split_h2<<<(unsigned)m, 256, 0, st>>>(Z, ldz, n, planes, flag);
+    SNPMI_HIP(hipGetLastError());
+    const std::vector<uint32_t>& tab = supertile_order(nb);
+    SNPMI_HIP(hipMemcpyAsync(order, tab.data(), g * sizeof(uint32_t), hipMemcpyHostToDevice, st));
+    // SNP chunks per launch (one supertile's 32 panels at 4096 SNPs = 128 MB, within the 256 MB
+    // Infinity Cache).  Measured N=50k, 10k SNPs (profiles/r01j/ubench_syrk_dense_h2.jsonl):
+    // chunks of 2048 / 4096 / 8192 / all 146-149 ms, plain column block order 150-160 ms, the
+    // f32-MFMA k_syrk256d 185 ms, the packed fp16x2 kernel on the same block 45 ms -- the
+    // dense loader (64 B of planes per thread per k-step through VGPRs) is the limit, not reuse.
+    const uint64_t ch = g_variant_syrk == 47 ? 2048 : g_variant_syrk == 48 ? 8192 : g_variant_syrk == 49 ? m : 4096;
+    for (uint64_t c0 = 0; c0 < m; c0 += ch) {
+        f32w::k_syrk_h2<false, 4, true><<<(unsigned)g, 512, 0, st>>>((const uint8_t*)(planes + c0 * 2 * ldz), ldz, n,
+                                                                      std::min(ch, m - c0), order, flag, tiles,
+                                                                      accumulate || c0 > 0);
+        SNPMI_HIP(hipGetLastError());
+    }
+    f32w::k_syrk256d<><<<(unsigned)g, 512, 0, st>>>(Z, ldz, n, m, tiles, accumulate, 0, 1, flag);
     SNPMI_HIP(hipGetLastError());
 }
 

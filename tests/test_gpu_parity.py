@@ -410,6 +410,31 @@ def test_grm_h2_range_fallback(case, syrk_variant):
     assert err <= 2e-6, "GRM max|dK|/max diag = %g" % err
 
 
+@pytest.mark.parametrize("scale", [1.0, 1e-3, 1e5, "mixed"])
+def test_grm_dense_h2_range(scale, syrk_variant):
+    """SnpData.read_kernel (dense f32 operand, N >= 4096): the fp16x2 split of the block in HBM
+    (k_split_h2 + k_syrk_h2<DENSE>) for columns whose max |z| lies in [2^-2, 2^15), the f32-MFMA
+    kernel on the device-side flag otherwise (scale 1e-3 / 1e5 / one tiny column) -- vs the f64
+    product of the same f32 values, Identity standardizer (values used as given)."""
+    rng = np.random.default_rng(11)
+    n, m = 4200, 45
+    v = rng.standard_normal((n, m)).astype(np.float32)
+    if scale == "mixed":
+        v[:, 7] *= 1e-4
+    else:
+        v *= np.float32(scale)
+    v[rng.random(v.shape) < 0.01] = 0
+    d = SnpData(iid=[["a", str(i)] for i in range(n)], sid=["s%d" % j for j in range(m)], val=v)
+    ref = v.astype(np.float64).dot(v.astype(np.float64).T)
+    K = d.read_kernel(Identity(), dtype=np.float32).val
+    grm_close(K, ref, 1e-5)
+    err = np.abs(K.astype(np.float64) - ref).max() / np.abs(np.diag(ref)).max()
+    assert err <= 2e-6, "GRM max|dK|/max diag = %g" % err
+    Zs = v.astype(np.float64).copy(order="F")
+    O.standardize_native(Zs)
+    grm_close(d.read_kernel(Unit(), dtype=np.float32).val, Zs.dot(Zs.T), 1e-5)
+
+
 # ---------------------------------------------------------------------------------- device API
 class Dev:
     """Tiny RAII helper over snpmi_dev_alloc/free."""
