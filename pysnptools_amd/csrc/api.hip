@@ -738,11 +738,13 @@ static void* session_tiles(Device& d) {
 // split kernel (falls back to the f32-MFMA k_syrk256d on the device-side range flag)
 static void syrk_dense_auto(Device& d, const void* Z, uint64_t ldz, uint64_t n, uint64_t m, int dt, void* tiles,
                             int accumulate) {
-    if (dt == SNPMI_DT_F32 && (g_variant_syrk == 0 || (g_variant_syrk >= 47 && g_variant_syrk <= 49)) && n >= 4096 &&
-        m > 0 && ldz % 256 == 0) {
+    if (dt == SNPMI_DT_F32 && (g_variant_syrk == 0 || g_variant_syrk == 44 || (g_variant_syrk >= 47 && g_variant_syrk <= 49)) &&
+        n >= 4096 && m > 0 && ldz % 256 == 0) {
         const uint64_t nb = ldz / 256, g = nb * (nb + 1) / 2;
-        uint16_t* planes = (uint16_t*)d.get(Device::S_H2, 4 * ldz * m + 256 + 4 * g);
-        uint32_t* flag = (uint32_t*)(planes + 2 * ldz * m);
+        // fp16 planes (4 B per value) or the stage images (round_up(m, 32) x nb x 2 x 9216 B)
+        const uint64_t scratch = std::max(4 * ldz * m, round_up(m, (uint64_t)32) / 16 * nb * 2 * 9216);
+        uint16_t* planes = (uint16_t*)d.get(Device::S_H2, scratch + 256 + 4 * g);
+        uint32_t* flag = (uint32_t*)((uint8_t*)planes + scratch);
         launch_syrk_dense_h2((const float*)Z, ldz, n, m, planes, flag, flag + 64, (float*)tiles, accumulate, d.stream);
         return;
     }

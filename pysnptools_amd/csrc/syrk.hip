@@ -1047,6 +1047,7 @@ __global__ __launch_bounds__(256) void k_lut_h2(const float* __restrict__ lut, u
 // planes[(s * 2 + p) * ldz + 16 d + pi(i)] = plane p of Z[s][16 d + i] (the packed loader's
 // in-group order), rows >= n zero; a column whose max |z| is outside [2^-2, 2^15) (and not 0)
 // raises *flag.  One 256-thread block per SNP column.
+template <bool WRITE = true>
 __global__ __launch_bounds__(256) void k_split_h2(const float* __restrict__ Z, uint64_t ldz, uint64_t n,
                                                   uint16_t* __restrict__ planes, uint32_t* __restrict__ flag) {
     const uint64_t s = blockIdx.x;
@@ -1059,9 +1060,11 @@ __global__ __launch_bounds__(256) void k_split_h2(const float* __restrict__ Z, u
         M = fmaxf(M, fabsf(v));
         const _Float16 a0 = (_Float16)v;
         const _Float16 a1 = (_Float16)(v - (float)a0);
-        const uint64_t o = (r & ~15ull) + (uint64_t)pi16((int)(r & 15));
-        p0[o] = __builtin_bit_cast(uint16_t, a0);
-        p1[o] = __builtin_bit_cast(uint16_t, a1);
+        if constexpr (WRITE) {
+            const uint64_t o = (r & ~15ull) + (uint64_t)pi16((int)(r & 15));
+            p0[o] = __builtin_bit_cast(uint16_t, a0);
+            p1[o] = __builtin_bit_cast(uint16_t, a1);
+        }
     }
     __shared__ float red[256];
     red[threadIdx.x] = M;
@@ -1073,6 +1076,30 @@ __global__ __launch_bounds__(256) void k_split_h2(const float* __restrict__ Z, u
     if (threadIdx.x == 0) {
         const float m = red[0];
         if (m != 0.f && !(m >= 0.25f && m < 32768.f)) atomicOr(flag, 1u);
+    }
+}
+
+// dense f32 block Z ([sid][ldz]) -> the stage images of k_syrk_h2<.., 6, true>: for 16-SNP step
+// t and 256-iid block b, plane p, a [16][288] fp16 tile laid out as the packed loader's LDS rows
+// (pi order in each 16-iid group, 16-B halves swapped in groups with bit 2 set); SNPs >= m and
+// iids >= n are zero.  Grid (nb, steps), one thread per iid.  The range flag comes from
+// k_split_h2<false> (column max only).
+__global__ __launch_bounds__(256) void k_image_h2(const float* __restrict__ Z, uint64_t ldz, uint64_t n, uint64_t m,
+                                                  short* __restrict__ img) {
+    const uint64_t b = blockIdx.x, t = blockIdx.y, nbk = gridDim.x;
+    const int i = threadIdx.x, d = i >> 4, q = pi16(i & 15), sw = (d >> 2) & 1;
+    const int pos = 16 * d + 8 * ((q >> 3) ^ sw) + (q & 7);
+    short* o0 = img + ((t * nbk + b) * 2) * (uint64_t)B3_PLANE + pos;
+    short* o1 = o0 + B3_PLANE;
+    const uint64_t iid = b * 256 + i;
+#pragma unroll 4
+    for (int k = 0; k < 16; k++) {
+        const uint64_t snp = t * 16 + k;
+        const float v = (snp < m && iid < n) ? Z[snp * ldz + iid] : 0.f;
+        const _Float16 a0 = (_Float16)v;
+        const _Float16 a1 = (_Float16)(v - (float)a0);
+        o0[k * B3_RS] = __builtin_bit_cast(short, a0);
+        o1[k * B3_RS] = __builtin_bit_cast(short, a1);
     }
 }
 
@@ -1218,6 +1245,48 @@ __global__ __launch_bounds__(512, 1) void k_syrk_h2(const uint8_t* __restrict__ 
             __builtin_amdgcn_sched_group_barrier(0x002, decltype(v)::value, 0);
         }
     };
+    if constexpr (MODE == 6) {
+        // DENSE stage images (k_image_h2): P = [16-SNP step t][256-iid block b][plane][16 rows x
+        // 288 fp16], exactly the LDS rows the packed loader writes, so a stage is 8 contiguous
+        // 9 KiB pieces moved by LDS-DMA (global_load_lds_dwordx4, 1 KiB per wave-instruction,
+        // 9 per wave) -- no VGPR staging, no ds_write; one barrier per 32 SNPs
+        const uint64_t nbk = (n + 255) / 256;  // = the image grid's x
+        const short* img = reinterpret_cast<const short*>(P);
+        auto issue = [&](uint64_t st, short* S) {
+#pragma unroll
+            for (int j = 0; j < 9; j++) {
+                const int c = wave * 9 + j;  // 72 pieces: [panel][plane][h][piece]
+                const int panel = c / 36, rem = c % 36, pl = rem / 18, h = (rem / 9) & 1, piece = rem % 9;
+                const uint64_t b = panel ? bj : bi;
+                const short* src = img + (((2 * st + h) * nbk + b) * 2 + pl) * (uint64_t)B3_PLANE + piece * 512 + 8 * lane;
+                short* dst = S + (panel * 2 + pl) * PLANE + h * B3_PLANE + piece * 512;
+                __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                                 (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+            }
+        };
+        issue(0, lds);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        for (uint64_t s = 0; s < nst; s++) {
+            const short* cur = lds + (s & 1) * STAGE;
+            if (s + 1 < nst) issue(s + 1, lds + ((s + 1) & 1) * STAGE);
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                f16x8_t A0[4], A1[4], B0[2], B1[2];
+                fragsA(cur, 0, h, A0);
+                fragB(cur, 0, h, B0);
+                fragB(cur, 1, h, B1);
+                fragsA(cur, 1, h, A1);
+                group(A0, B0);
+                group(A0, B1);
+                group(A1, B0);
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+        }
+        epilogue_pi<LOCAL>(acc, tiles, n, bi, bj, accumulate, lane, wm, wn, wg);
+        return;
+    }
     {
         load(0);
 #pragma unroll
@@ -1731,6 +1800,25 @@ void launch_syrk_dense_h2(const float* Z, uint64_t ldz, uint64_t n, uint64_t m, 
         return;
     }
     SNPMI_HIP(hipMemsetAsync(flag, 0, sizeof(uint32_t), st));
+    // Default (0 / 44): the block is rewritten once as stage images (k_image_h2, 4.6 B per value,
+    // ~1 ms per 10k x 50k) that k_syrk_h2<MODE 6> moves into LDS by DMA -- measured N=50k, 10k
+    // SNPs: 60.5 ms in one launch vs 3 x 50 ms for MODE 4's VGPR-staged loader
+    // (profiles/r01k/).  Over 2^20 SNPs (grid.y limit) the chunked MODE 4 path below runs.
+    const uint64_t steps = 2 * ceil_div(m, (uint64_t)32);
+    if ((g_variant_syrk == 0 || g_variant_syrk == 44) && steps < 65536) {
+        f32w::k_split_h2<false><<<(unsigned)m, 256, 0, st>>>(Z, ldz, n, nullptr, flag);
+        SNPMI_HIP(hipGetLastError());
+        f32w::k_image_h2<<<dim3((unsigned)nb, (unsigned)steps), 256, 0, st>>>(Z, ldz, n, m, (short*)planes);
+        SNPMI_HIP(hipGetLastError());
+        const std::vector<uint32_t>& tab = supertile_order(nb);
+        SNPMI_HIP(hipMemcpyAsync(order, tab.data(), g * sizeof(uint32_t), hipMemcpyHostToDevice, st));
+        f32w::k_syrk_h2<false, 6, true><<<(unsigned)g, 512, 0, st>>>((const uint8_t*)planes, ldz, n, m, order, flag,
+                                                                      tiles, accumulate);
+        SNPMI_HIP(hipGetLastError());
+        f32w::k_syrk256d<><<<(unsigned)g, 512, 0, st>>>(Z, ldz, n, m, tiles, accumulate, 0, 1, flag);
+        SNPMI_HIP(hipGetLastError());
+        return;
+    }
     f32w::k_split_h2<<<(unsigned)m, 256, 0, st>>>(Z, ldz, n, planes, flag);
     SNPMI_HIP(hipGetLastError());
     const std::vector<uint32_t>& tab = supertile_order(nb);

@@ -321,14 +321,14 @@ def test_kerneldata_diag_k_to_n():
     assert abs(np.diag(kd.val).sum() - 3) < 1e-7  # kernelreader/test.py:221-229
 
 
-@pytest.fixture(params=[0, 41, 40, 42, 43, 46, 36, 4, 5, 20, 30, 31, 33, 34],
-                ids=["auto", "h2k16", "h2pin", "h2preA", "h2preApin", "h2k32pin", "bf3", "syrk256", "syrk128", "f32twophase", "bf3plain",
+@pytest.fixture(params=[0, 41, 40, 42, 43, 46, 44, 36, 4, 5, 20, 30, 31, 33, 34],
+                ids=["auto", "h2k16", "h2pin", "h2preA", "h2preApin", "h2k32pin", "h2dma", "bf3", "syrk256", "syrk128", "f32twophase", "bf3plain",
                      "bf3xcd", "bf3mode1", "bf3mode2"])
 def syrk_variant(request):
     """Run a test under each SYRK kernel -- f32: 0 = default (packed: the fp16x2-split kernel,
     3 products on the fp16 MFMA pipe, 32-SNP LDS stages, with the bf16x3 kernel as its range
     fallback), 46 = that with the loader VALU pinned between the MFMAs, 41 = 16-SNP stages, 40 =
-    + pin, 42/43 = 16-SNP stages with the next stage's A plane-0 fragments prefetched after the
+    + pin, 44 = dense operand as LDS-DMA stage images (k_image_h2 + MODE 6), 42/43 = 16-SNP stages with the next stage's A plane-0 fragments prefetched after the
     barrier (unpinned / pinned), 36 = the bf16x3 kernel alone (interleaved
     loader pinned one VALU per MFMA, mid-stage barrier with the next B planes prefetched), 34 =
     without the pin, 33 = end-of-stage barrier, 30/31 = its plain-loader forms, 4 = f32
