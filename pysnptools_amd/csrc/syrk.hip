@@ -1772,18 +1772,31 @@ void launch_lut_h2(const float* lut, uint64_t m, uint32_t* lut2, uint32_t* flag,
 // triangular order, blocks (bi <= bj) inside each; entry = bi | bj << 16.  The dense fp16x2
 // SYRK streams 4 B per value per panel, so the ~256 blocks in flight must share panels: in the
 // plain column order they touch ~nb A panels at once, in this order 32.
-static const std::vector<uint32_t>& supertile_order(uint64_t nb) {
-    static std::vector<uint32_t> tab;
-    static uint64_t tab_nb = 0;
-    if (tab_nb != nb) {
+static const std::vector<uint32_t>& supertile_order(uint64_t nb, bool xcd = false) {
+    static std::vector<uint32_t> tabs[2];
+    static uint64_t tab_nb[2] = {0, 0};
+    std::vector<uint32_t>& tab = tabs[xcd];
+    if (tab_nb[xcd] != nb) {
         tab.clear();
         const uint64_t ns = ceil_div(nb, 16);
         for (uint64_t J = 0; J < ns; J++)
-            for (uint64_t I = 0; I <= J; I++)
+            for (uint64_t I = 0; I <= J; I++) {
+                // xcd: workgroup w runs on XCD w % 8, so deal each supertile's blocks out of 8
+                // 4 (bi) x 8 (bj) sub-tiles round-robin -- one XCD's ~32 blocks then touch 12
+                // panels in its own L2 instead of 18
+                std::vector<uint32_t> sub[8];
                 for (uint64_t bj = 16 * J; bj < std::min(16 * J + 16, nb); bj++)
                     for (uint64_t bi = 16 * I; bi < std::min(16 * I + 16, bj + 1); bi++)
-                        tab.push_back((uint32_t)(bi | (bj << 16)));
-        tab_nb = nb;
+                        sub[xcd ? ((bi - 16 * I) / 4 + 4 * ((bj - 16 * J) / 8)) : 0].push_back((uint32_t)(bi | (bj << 16)));
+                size_t pos[8] = {0, 0, 0, 0, 0, 0, 0, 0}, left = 0;
+                for (int x = 0; x < 8; x++) left += sub[x].size();
+                for (int x = 0; left > 0; x = (x + 1) & 7)
+                    if (pos[x] < sub[x].size()) {
+                        tab.push_back(sub[x][pos[x]++]);
+                        left--;
+                    }
+            }
+        tab_nb[xcd] = nb;
     }
     return tab;
 }
@@ -1803,14 +1816,17 @@ void launch_syrk_dense_h2(const float* Z, uint64_t ldz, uint64_t n, uint64_t m, 
     // Default (0 / 44): the block is rewritten once as stage images (k_image_h2, 4.6 B per value,
     // ~1 ms per 10k x 50k) that k_syrk_h2<MODE 6> moves into LDS by DMA -- measured N=50k, 10k
     // SNPs: 60.5 ms in one launch vs 3 x 50 ms for MODE 4's VGPR-staged loader
-    // (profiles/r01k/).  Over 2^20 SNPs (grid.y limit) the chunked MODE 4 path below runs.
+    // (profiles/r01k/).  Variant 0 deals blocks to XCDs by 4x8 sub-tile: within noise of the
+    // plain supertile order, 44 (59.8 / 61.2 vs 60.4 / 60.9 ms in two runs).  A 4-slot, 16-SNP-step DMA ring (3 steps in flight) was tried:
+    // with dwordx3 pieces the LDS image came out wrong (NaN), with dword pieces it was correct
+    // but 272 ms (18 DMA instructions per wave per step).  Over 2^20 SNPs (grid.y limit) the chunked MODE 4 path below runs.
     const uint64_t steps = 2 * ceil_div(m, (uint64_t)32);
     if ((g_variant_syrk == 0 || g_variant_syrk == 44) && steps < 65536) {
         f32w::k_split_h2<false><<<(unsigned)m, 256, 0, st>>>(Z, ldz, n, nullptr, flag);
         SNPMI_HIP(hipGetLastError());
         f32w::k_image_h2<<<dim3((unsigned)nb, (unsigned)steps), 256, 0, st>>>(Z, ldz, n, m, (short*)planes);
         SNPMI_HIP(hipGetLastError());
-        const std::vector<uint32_t>& tab = supertile_order(nb);
+        const std::vector<uint32_t>& tab = supertile_order(nb, g_variant_syrk == 0);
         SNPMI_HIP(hipMemcpyAsync(order, tab.data(), g * sizeof(uint32_t), hipMemcpyHostToDevice, st));
         f32w::k_syrk_h2<false, 6, true><<<(unsigned)g, 512, 0, st>>>((const uint8_t*)planes, ldz, n, m, order, flag,
                                                                       tiles, accumulate);
