@@ -2,30 +2,49 @@
 
 Metric (BASELINE.json): "SNPs/sec standardized (500k x 1M) + GRM GF/s at 1/2/4/8 GPUs".
 
-  value      = SNPs/s standardized, whole job: every rank decodes + Unit-standardizes its own
-               synthetic 500k-iid x 1M-SNP BED matrix (the UKBB shape of configs[4]), resident in
-               HBM as packed 2-bit codes, in blocks of 2048 SNPs into an f32 F-order block buffer
-               (weak scaling: per-GPU work fixed).  A step = one pass over the 1M SNPs.
+  value      = SNPs/s standardized over the metric's fixed 500k-iid x 1M-SNP BED matrix (the UKBB
+               shape of configs[4]), resident in HBM as packed 2-bit codes: rank r of N owns SNPs
+               [r*1M/N, (r+1)*1M/N) and streams them through stats + decode + Unit in blocks of
+               2048 SNPs into an f32 F-order block buffer; no collective on the data path.  STRONG
+               scaling (total work fixed); a step = one pass over the 1M SNPs by all ranks.
+               `weak` (N > 1) = the same ranks each streaming 1M SNPs per step (their shard N times).
   roofline   = the decode kernel (k_decode_f<float>), HBM bound: algorithmic bytes per launch =
                block * (ceil(N/4) + 4N) / its mean HIP-event duration, vs 8.0 TB/s.
-  grm        = SnpKernel GRM of configs[3] (50k iid x 500k SNP, Unit, block 10k, f32): SNP blocks
-               round-robin over ranks, one RCCL all-reduce of the upper-triangle K tiles.  The f32
+  decode_c   = the C-order form (k_decode_c_reg<float>), same bytes, 500k iids.
+  e2e        = packed columns in pinned HOST memory -> H2D on the copy stream -> stats + decode on
+               the compute stream (3-slot ring, events only) -> f32 in HBM: the PCIe-inclusive rate,
+               with the measured H2D peak of the same buffer beside it.  Never `value`.
+  grm        = SnpKernel GRM of configs[3] (50k iid x 500k SNP, Unit, block 10k, f32): contiguous SNP
+               shards per rank, one RCCL all-reduce of the upper-triangle K tiles.  The f32
                products run on the fp16 MFMA pipe as 3 fp16 products of each value's fp16x2 split
                (f32-level accuracy, f32 accumulate; bf16x3 = 6 bf16 products when a SNP's LUT is
                outside fp16's range).  gflops uses N(N+1)M (SYRK work); roofline
                vs 2.5 PF fp16 dense / 3 = 833.3 TF (the f32-MFMA peak is 157.3).
+  grm_f64    = the same GRM in float64 (the reference's default dtype, snpreader.py:528,623) on
+               the f64 MFMA (78.6 TF dense).
+  grm5       = configs[4] shape: 500k iids, K (500 GB f32 upper triangle) partitioned over the 8
+               ranks of the 8-GPU plan as 256x256 blocks; this process computes part `rank` of
+               max(N, 8) for one 8192-SNP block uploaded from pinned host memory inside the timed
+               region (1/N each + RCCL all-gather at N > 1), parity-checked on a diagonal and an
+               off-diagonal block, projected to 1M SNPs.
   cpu_baseline = the oracle's C/OpenMP decode + one-pass Unit standardize (the CPU restatement
                of bed-reader's read + standardize_f32) on a sample of the same packed columns,
-               rank 0 only; grm.cpu_baseline = NumPy/OpenBLAS Z.dot(Z.T) (snpreader.py:655).
+               rank 0 at N = 1 only, at the box's CPU share and at 1 thread; grm.cpu_baseline =
+               NumPy/OpenBLAS Z.dot(Z.T) (snpreader.py:655) with the BLAS pool pinned.
 
-Run: python bench.py [--gpus N --steps K --warmup W]; N > 1 under torch.distributed.run.
+Run: python bench.py [--gpus N --steps K --warmup W].  N > 1 either under torch.distributed.run
+(RANK / WORLD_SIZE / LOCAL_RANK from the environment) or as a plain `python bench.py --gpus N`, which
+spawns the N rank processes itself before anything touches the GPU and relays rank 0's line.
 """
 import argparse
 import contextlib
 import ctypes
 import json
 import os
+import socket
+import subprocess
 import sys
+import tempfile
 import time
 
 import numpy as np
@@ -36,14 +55,16 @@ sys.path.insert(0, ROOT)
 METRIC = "SNPs/sec standardized (500k×1M) + GRM GF/s at 1/2/4/8 GPUs"
 HBM_PEAK_GBS = 8000.0
 MFMA_F32_PEAK_TFLOPS = 157.3
+MFMA_F64_PEAK_TFLOPS = 78.6
 MFMA_BF16_PEAK_TFLOPS = 2500.0
 # f32 GRM on the fp16 MFMA pipe (same dense rate as bf16): each f32 product = 3 fp16 MFMA
 # products of the fp16x2 split (k_syrk_h2; Unit LUTs always fit fp16's range)
 SPLIT_PRODUCTS = 3
 SPLIT_PEAK_TFLOPS = MFMA_BF16_PEAK_TFLOPS / SPLIT_PRODUCTS
+GRM5_PLAN_WORLD = 8  # configs[4] is an 8-GPU plan
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=3)
@@ -55,19 +76,59 @@ def parse():
     p.add_argument("--grm-sid", type=int, default=500_000)
     p.add_argument("--grm-block", type=int, default=10_000)
     p.add_argument("--skip-grm", action="store_true")
-    p.add_argument("--grm5", choices=["auto", "on", "off"], default="auto",
-                   help="cfg5 tile-partitioned GRM leg (auto: when WORLD_SIZE >= 4)")
+    p.add_argument("--grm-f64", choices=["on", "off"], default="on", help="cfg4 GRM in float64 (reference default)")
+    p.add_argument("--grm5", choices=["on", "off"], default="on", help="cfg5 partitioned-K GRM leg")
     p.add_argument("--grm5-iid", type=int, default=500_000)
     p.add_argument("--grm5-sid", type=int, default=8192)
+    p.add_argument("--e2e", choices=["on", "off"], default="on", help="pinned-host -> HBM streaming leg")
+    p.add_argument("--e2e-sid", type=int, default=8192, help="SNPs held in pinned host memory")
+    p.add_argument("--e2e-passes", type=int, default=4)
     p.add_argument("--skip-cpu", action="store_true")
-    p.add_argument("--fused", choices=["on", "off"], default="off",
-                   help="decode leg: fused stats+decode kernel k_decode_std_lds_f32 (needs a packed column <= "
-                        "150 KiB); off = k_snp_stats + k_decode_f, measured faster at 500k iids (2.63 vs 2.40 M SNPs/s)")
     p.add_argument("--decode-variant", type=int, default=0, help="snpmi_set_kernel_variant('decode', v) (A/B runs)")
-    p.add_argument("--cpu-seconds", type=float, default=12.0)
+    p.add_argument("--cpu-seconds", type=float, default=6.0)
     p.add_argument("--seed", type=int, default=5)
     p.add_argument("--force-rccl", action="store_true", help="build the RCCL communicator even at world size 1")
-    return p.parse_args()
+    return p.parse_args(argv)
+
+
+# ---------------------------------------------------------------------------- process launch
+def _free_port():
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(args, argv):
+    """`python bench.py --gpus N` without a launcher: start N rank processes (one per GPU) before
+    this process touches HIP, relay rank 0's stdout, and exit with the worst rank status."""
+    tmp = tempfile.mkdtemp(prefix="snpmi_bench_")
+    port = str(_free_port())
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus), LOCAL_WORLD_SIZE=str(args.gpus),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port, SNPMI_RCCL_ID_FILE=os.path.join(tmp, "rccl.id"))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env,
+                                      stdout=None if r == 0 else sys.stderr))
+    rc = 0
+    try:
+        while procs:
+            for p in list(procs):
+                code = p.poll()
+                if code is None:
+                    continue
+                procs.remove(p)
+                if code != 0:
+                    rc = rc or code
+                    for q in procs:  # one rank failed: the others would wait in a collective forever
+                        q.kill()
+            time.sleep(0.2)
+    finally:
+        for q in procs:
+            q.kill()
+        for f in os.listdir(tmp):
+            os.remove(os.path.join(tmp, f))
+        os.rmdir(tmp)
+    return rc
 
 
 @contextlib.contextmanager
@@ -84,33 +145,53 @@ def stdout_to_stderr():
         os.close(saved)
 
 
+def _id_file():
+    """Node-local path for the ncclUniqueId: given by the spawning parent, else derived from the
+    launcher (parent pid + its start time, so no stale file of an earlier launcher can match)."""
+    path = os.environ.get("SNPMI_RCCL_ID_FILE")
+    if path:
+        return path
+    ppid = os.getppid()
+    try:
+        start = open("/proc/%d/stat" % ppid).read().rsplit(")", 1)[1].split()[19]
+    except OSError:
+        start = "0"
+    key = "snpmi_rccl_%d_%s_%s.id" % (ppid, start, os.environ.get("MASTER_PORT", "0"))
+    return os.path.join(tempfile.gettempdir(), key)
+
+
 class Dist:
     """Control plane for one process per GPU WITHOUT torch: importing torch would load its own
-    libamdhip64.so.7 (ROCm 7.0) next to libsnpmi's (ROCm 7.2) -- same SONAME, two runtimes.
-    torch.distributed.run only launches the processes; the ncclUniqueId is handed from rank 0
-    to the others through a node-local file keyed by the launcher's pid, and barriers /
-    max-over-ranks are RCCL all-reduces of a scalar."""
+    libamdhip64.so.7 (ROCm 7.0) next to libsnpmi's (ROCm 7.2) -- same SONAME, two runtimes.  The
+    ncclUniqueId goes from rank 0 to the others through an O_EXCL node-local file (removed once
+    every rank holds the communicator); barriers / max-over-ranks are RCCL all-reduces."""
 
     def __init__(self, gpus, N, force_rccl=False):
         self.N = N
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
         self.local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-        assert self.world == gpus or self.world == 1, "--gpus must match WORLD_SIZE"
+        if self.world != gpus:
+            raise SystemExit("bench.py: --gpus %d but WORLD_SIZE=%d (one process per GPU)" % (gpus, self.world))
         N.call("snpmi_set_device", self.local_rank)
         self.rccl = False
+        self.n_gpus = 1
+        self._path = None
         if self.world > 1 or force_rccl:
-            import tempfile
-
-            key = "snpmi_rccl_%d_%s.id" % (os.getppid(), os.environ.get("MASTER_PORT", "0"))
-            path = os.path.join(tempfile.gettempdir(), key)
+            path = _id_file()
             uid = (ctypes.c_uint8 * 128)()
             if self.rank == 0:
                 with stdout_to_stderr():
                     N.call("snpmi_rccl_unique_id", uid, 128)
-                with open(path + ".tmp", "wb") as f:
+                tmp = path + ".tmp"
+                fd = os.open(tmp, os.O_WRONLY | os.O_CREAT | os.O_EXCL, 0o600)
+                with os.fdopen(fd, "wb") as f:
                     f.write(bytes(uid))
-                os.replace(path + ".tmp", path)
+                try:
+                    os.link(tmp, path)  # fails if a file of that name exists: never overwrite
+                finally:
+                    os.remove(tmp)
+                self._path = path
             else:
                 t0 = time.time()
                 while not os.path.exists(path):
@@ -123,8 +204,12 @@ class Dist:
                 N.call("snpmi_rccl_init", self.world, self.rank, uid, 128)
             self.rccl = True
             self.barrier()
-            if self.rank == 0:
-                os.remove(path)
+            if self._path:
+                os.remove(self._path)
+                self._path = None
+            cnt = ctypes.c_int()
+            N.call("snpmi_rccl_comm_count", ctypes.byref(cnt))
+            self.n_gpus = cnt.value
 
     def barrier(self):
         if self.rccl:
@@ -138,6 +223,8 @@ class Dist:
         return float(v[0])
 
     def close(self):
+        if self._path and os.path.exists(self._path):
+            os.remove(self._path)
         if self.rccl:
             with stdout_to_stderr():
                 self.N.call("snpmi_rccl_destroy")
@@ -148,6 +235,9 @@ class Dev:
         self.N = N
         self.p = ctypes.c_void_p()
         N.call("snpmi_dev_alloc", ctypes.byref(self.p), int(nbytes))
+
+    def at(self, off):
+        return ctypes.c_void_p(self.p.value + int(off))
 
     def free(self):
         if self.p:
@@ -164,8 +254,11 @@ class Events:
             N.call("snpmi_event_create", ctypes.byref(e))
             self.ev.append(e)
 
-    def record(self, i):
-        self.N.call("snpmi_event_record", self.ev[i])
+    def record(self, i, on_copy=0):
+        if on_copy:
+            self.N.call("snpmi_event_record_on", self.ev[i], 1)
+        else:
+            self.N.call("snpmi_event_record", self.ev[i])
 
     def ms(self, a, b):
         out = ctypes.c_float()
@@ -193,52 +286,49 @@ def synth(N, buf, pitch, n, sid0, m, seed, miss):
     N.call("snpmi_dev_synth_bed", buf, pitch, n, sid0, m, seed, miss, N.ptr(x), N.ptr(cdf), len(x))
 
 
+def cpu_threads():
+    """The CPU share this process may use: OMP_NUM_THREADS (16 per GPU on the box), else the
+    affinity mask.  os.cpu_count() on the box reports the whole machine."""
+    env = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return env or len(os.sched_getaffinity(0))
+
+
+def shard(m, rank, world):
+    return m * rank // world, m * (rank + 1) // world
+
+
 # ---------------------------------------------------------------------------- leg 1: decode + standardize
-def use_fused(args, n):
-    """k_decode_std_lds_f32 holds one packed column in LDS: up to 150 KiB (N <= 614,400)."""
-    if args.fused != "on":
-        return False
-    return ((n + 63) // 64) * 16 <= 150 * 1024
 def leg_standardize(N, args, dist):
-    n, m, B = args.n_iid, args.n_sid, args.block
+    n, B = args.n_iid, args.block
+    lo, hi = shard(args.n_sid, dist.rank, dist.world)
+    m = hi - lo
     pitch = N.lib().snpmi_packed_pitch(n)
     ld = (n + 15) // 16 * 16
-    packed = Dev(N, pitch * m)
-    synth(N, packed.p, pitch, n, dist.rank * m, m, args.seed, 0.01)
+    packed = Dev(N, pitch * max(m, 1))
+    synth(N, packed.p, pitch, n, lo, m, args.seed, 0.01)
     nblk = (m + B - 1) // B
     lut, stats, out = Dev(N, B * 16), Dev(N, B * 8), Dev(N, B * ld * 4)
     ev = Events(N, 2 + 2 * nblk)
-    fused = use_fused(args, n)
     N.call("snpmi_set_kernel_variant", b"decode", args.decode_variant)
 
     def run_block(src, cnt, timed, k):
-        if fused:  # stats + decode in one kernel (column staged in LDS, packed bytes read once)
-            if timed:
-                ev.record(2 + 2 * k)
-            N.call("snpmi_dev_decode_standardize", src, pitch, n, cnt, 0, N.STD_UNIT, 0.0, 0.0, 0, N.DT_F32,
-                   stats.p, lut.p, out.p, ld)
-        else:
-            N.call("snpmi_dev_snp_stats", src, pitch, n, cnt, 0, N.STD_UNIT, 0.0, 0.0, 0, N.DT_F32, stats.p, lut.p)
-            if timed:
-                ev.record(2 + 2 * k)
-            N.call("snpmi_dev_decode", src, pitch, n, cnt, lut.p, N.DT_F32, 0, out.p, ld)
+        N.call("snpmi_dev_snp_stats", src, pitch, n, cnt, 0, N.STD_UNIT, 0.0, 0.0, 0, N.DT_F32, stats.p, lut.p)
+        if timed:
+            ev.record(2 + 2 * k)
+        N.call("snpmi_dev_decode", src, pitch, n, cnt, lut.p, N.DT_F32, 0, out.p, ld)
         if timed:
             ev.record(3 + 2 * k)
 
     def step(timed):
-        dec_ms = 0.0
         if timed:
             ev.record(0)
         for k in range(nblk):
             s0 = k * B
-            cnt = min(B, m - s0)
-            run_block(ctypes.c_void_p(packed.p.value + s0 * pitch), cnt, timed, k)
+            run_block(packed.at(s0 * pitch), min(B, m - s0), timed, k)
         if timed:
             ev.record(1)
         N.call("snpmi_stream_sync")
-        if timed:
-            dec_ms = sum(ev.ms(2 + 2 * k, 3 + 2 * k) for k in range(nblk))
-        return dec_ms
+        return sum(ev.ms(2 + 2 * k, 3 + 2 * k) for k in range(nblk)) if timed else 0.0
 
     for _ in range(args.warmup):
         step(False)
@@ -246,19 +336,28 @@ def leg_standardize(N, args, dist):
     N.call("snpmi_stream_sync")
     t0 = time.perf_counter()
     dec_ms_total = 0.0
-    step_ms = []
     for _ in range(args.steps):
         dec_ms_total += step(True)
-        step_ms.append(ev.ms(0, 1))
     N.call("snpmi_stream_sync")
     dist.barrier()
     wall = dist.max(time.perf_counter() - t0)
+    weak_wall = None
+    if dist.world > 1:
+        # weak figure: every rank streams 1M SNPs per step (its shard `world` times)
+        dist.barrier()
+        t1 = time.perf_counter()
+        for _ in range(args.steps * dist.world):
+            step(False)
+        N.call("snpmi_stream_sync")
+        dist.barrier()
+        weak_wall = dist.max(time.perf_counter() - t1)
     launches = args.steps * nblk
-    dec_mean_ms = dec_ms_total / launches
-    full_block_bytes = B * ((n + 3) // 4 + 4 * n)
-    total_bytes = m * ((n + 3) // 4 + 4 * n)
-    achieved_gbs = (total_bytes / nblk) / (dec_mean_ms * 1e-3) / 1e9
-    # measured copy peak (untimed): device-to-device copies of the block buffer's size
+    dec_mean_ms = dec_ms_total / max(launches, 1)
+    # achieved = bytes of one full block / mean launch time (the last block of a shard is partial:
+    # count bytes over all launches instead)
+    bytes_per_step = m * ((n + 3) // 4 + 4 * n)
+    achieved_gbs = bytes_per_step * args.steps / (dec_ms_total * 1e-3) / 1e9 if dec_ms_total else 0.0
+    # measured stream ceilings (untimed): device-to-device copy and write-only fill of the block buffer
     cbytes = min(B * ld * 4, pitch * m)
     N.call("snpmi_dev_memcpy_d2d", out.p, packed.p, cbytes)
     N.call("snpmi_stream_sync")
@@ -268,7 +367,6 @@ def leg_standardize(N, args, dist):
     ev.record(1)
     N.call("snpmi_stream_sync")
     copy_gbs = 2 * 5 * cbytes / (ev.ms(0, 1) * 1e-3) / 1e9
-    # write-only stream (the decode writes 16 B per 1 B it reads): hipMemset fill of the buffer
     ev.record(0)
     for _ in range(5):
         N.call("snpmi_dev_memset", out.p, 0, B * ld * 4)
@@ -284,58 +382,180 @@ def leg_standardize(N, args, dist):
         run_block(packed.p, ncols, False, 0)
         gpu_cols = np.empty((ncols, ld), dtype=np.float32)
         N.call("snpmi_memcpy_d2h", N.ptr(gpu_cols), out.p, gpu_cols.nbytes)
-    res = dict(wall=wall, step_ms=step_ms, dec_mean_ms=dec_mean_ms, achieved_gbs=achieved_gbs, fused=fused,
-               copy_gbs=copy_gbs, fill_gbs=fill_gbs,
-               full_block_bytes=full_block_bytes, launches=launches, nblk=nblk, pitch=pitch, sample=sample,
-               gpu_cols=gpu_cols)
+    res = dict(wall=wall, weak_wall=weak_wall, dec_mean_ms=dec_mean_ms, achieved_gbs=achieved_gbs,
+               copy_gbs=copy_gbs, fill_gbs=fill_gbs, full_block_bytes=B * ((n + 3) // 4 + 4 * n), launches=launches,
+               nblk=nblk, pitch=pitch, sample=sample, gpu_cols=gpu_cols, m=m)
     ev.destroy()
     for d in (packed, lut, stats, out):
         d.free()
     return res
 
 
-def cpu_baseline_standardize(args, sample, pitch, timed=True):
-    """Oracle C/OpenMP decode + one-pass Unit standardize on a bounded sample (rank 0); with
-    timed=False (N > 1: the baseline is reported at N = 1 only) one untimed pass for parity."""
+def leg_decode_c(N, args):
+    """C-order decode (k_decode_c_reg<float>): rows of 2048 SNPs at 500k iids, 16-B row pitch."""
+    n, B, reps = args.n_iid, args.block, 8
+    pitch = N.lib().snpmi_packed_pitch(n)
+    packed = Dev(N, pitch * B)
+    synth(N, packed.p, pitch, n, 0, B, args.seed, 0.01)
+    lut, stats, out = Dev(N, B * 16), Dev(N, B * 8), Dev(N, B * n * 4)
+    N.call("snpmi_dev_snp_stats", packed.p, pitch, n, B, 0, N.STD_UNIT, 0.0, 0.0, 0, N.DT_F32, stats.p, lut.p)
+    N.call("snpmi_dev_decode", packed.p, pitch, n, B, lut.p, N.DT_F32, 1, out.p, B)
+    ev = Events(N, 2 * reps)
+    N.call("snpmi_stream_sync")
+    for r in range(reps):
+        ev.record(2 * r)
+        N.call("snpmi_dev_decode", packed.p, pitch, n, B, lut.p, N.DT_F32, 1, out.p, B)
+        ev.record(2 * r + 1)
+    N.call("snpmi_stream_sync")
+    ms = float(np.mean([ev.ms(2 * r, 2 * r + 1) for r in range(reps)]))
+    nbytes = B * ((n + 3) // 4 + 4 * n)
+    # parity: C-order rows equal the F-order decode transposed (first 64 iids x all SNPs)
+    rows = np.empty((64, B), dtype=np.float32)
+    N.call("snpmi_memcpy_d2h", N.ptr(rows), out.p, rows.nbytes)
+    ld = (n + 15) // 16 * 16
+    fout = Dev(N, B * ld * 4)
+    N.call("snpmi_dev_decode", packed.p, pitch, n, B, lut.p, N.DT_F32, 0, fout.p, ld)
+    cols = np.empty((B, ld), dtype=np.float32)
+    N.call("snpmi_memcpy_d2h", N.ptr(cols), fout.p, cols.nbytes)
+    same = bool(np.array_equal(rows, cols[:, :64].T))
+    ev.destroy()
+    for d in (packed, lut, stats, out, fout):
+        d.free()
+    gbs = nbytes / (ms * 1e-3) / 1e9
+    return {"workload": "C-order decode of %d SNPs x %d iids (f32, rows of %d SNPs)" % (B, n, B),
+            "kernel": "k_decode_c_reg<float>", "mean_launch_ms": ms, "per_launch_bytes": nbytes,
+            "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS,
+            "parity": {"check": "rows 0..63 == F-order decode transposed", "bit_exact": same}}
+
+
+def leg_e2e(N, args):
+    """Pinned host -> HBM streaming: packed columns of --e2e-sid SNPs sit in page-locked host memory;
+    each 2048-SNP chunk goes H2D on the copy stream into a 3-slot device ring, the compute stream
+    waits on its event and runs stats + decode (f32, F order, into HBM), and the copy stream waits
+    on the compute event of the chunk that last used a slot before overwriting it."""
+    n, B = args.n_iid, args.block
+    m = args.e2e_sid // B * B
+    pitch = N.lib().snpmi_packed_pitch(n)
+    ld = (n + 15) // 16 * 16
+    host = ctypes.c_void_p()
+    N.call("snpmi_host_alloc", ctypes.byref(host), m * pitch)
+    src = Dev(N, m * pitch)
+    synth(N, src.p, pitch, n, 0, m, args.seed + 7, 0.01)
+    N.call("snpmi_memcpy_d2h", host, src.p, m * pitch)
+    ring = [Dev(N, B * pitch) for _ in range(3)]
+    lut, stats, out = Dev(N, B * 16), Dev(N, B * 8), Dev(N, B * ld * 4)
+    nch = m // B
+    total = nch * args.e2e_passes
+    ev = Events(N, 4 + 2 * 3)  # 0..3 timing; 4+s = H2D done (slot s); 7+s = compute done (slot s)
+    h2d_ev = lambda s: 4 + s  # noqa: E731
+    use_ev = lambda s: 7 + s  # noqa: E731
+
+    def stream(timed):
+        if timed:
+            ev.record(0)
+        for c in range(total):
+            s = c % 3
+            hsrc = ctypes.c_void_p(host.value + (c % nch) * B * pitch)
+            if c >= 3:
+                N.call("snpmi_stream_wait_event", ev.ev[use_ev(s)], 1)
+            N.call("snpmi_memcpy_async", ring[s].p, hsrc, B * pitch, 0, 1)
+            ev.record(h2d_ev(s), on_copy=1)
+            N.call("snpmi_stream_wait_event", ev.ev[h2d_ev(s)], 0)
+            N.call("snpmi_dev_snp_stats", ring[s].p, pitch, n, B, 0, N.STD_UNIT, 0.0, 0.0, 0, N.DT_F32, stats.p, lut.p)
+            N.call("snpmi_dev_decode", ring[s].p, pitch, n, B, lut.p, N.DT_F32, 0, out.p, ld)
+            ev.record(use_ev(s))
+        if timed:
+            ev.record(1)
+        N.call("snpmi_stream_sync")
+
+    stream(False)
+    t0 = time.perf_counter()
+    stream(True)
+    wall = time.perf_counter() - t0
+    ev_ms = ev.ms(0, 1)
+    # parity: the last chunk's values == decode of the same columns from HBM
+    last = np.empty((B, ld), dtype=np.float32)
+    N.call("snpmi_memcpy_d2h", N.ptr(last), out.p, last.nbytes)
+    c_last = (total - 1) % nch
+    N.call("snpmi_dev_snp_stats", src.at(c_last * B * pitch), pitch, n, B, 0, N.STD_UNIT, 0.0, 0.0, 0, N.DT_F32,
+           stats.p, lut.p)
+    N.call("snpmi_dev_decode", src.at(c_last * B * pitch), pitch, n, B, lut.p, N.DT_F32, 0, out.p, ld)
+    ref = np.empty_like(last)
+    N.call("snpmi_memcpy_d2h", N.ptr(ref), out.p, ref.nbytes)
+    same = bool(np.array_equal(last[:, :n], ref[:, :n]))
+    # H2D peak of the same pinned buffer on the copy stream (no kernels)
+    ev.record(2, on_copy=1)
+    for p in range(args.e2e_passes):
+        for c in range(nch):
+            N.call("snpmi_memcpy_async", ring[c % 3].p, ctypes.c_void_p(host.value + c * B * pitch), B * pitch, 0, 1)
+    ev.record(3, on_copy=1)
+    N.call("snpmi_stream_sync")
+    peak_gbs = args.e2e_passes * m * pitch / (ev.ms(2, 3) * 1e-3) / 1e9
+    ev.destroy()
+    N.call("snpmi_host_free", host)
+    for d in ring + [src, lut, stats, out]:
+        d.free()
+    snps = total * B
+    pcie_gbs = snps * pitch / (ev_ms * 1e-3) / 1e9
+    return {"workload": "%d SNPs x %d iids streamed %d times from pinned host (packed, %d B/SNP) -> stats + "
+                        "decode + Unit -> f32 F-order in HBM, 2048-SNP chunks, 3-slot ring, copy stream + "
+                        "compute stream" % (m, n, args.e2e_passes, pitch),
+            "snps_per_s": snps / (ev_ms * 1e-3), "seconds": ev_ms * 1e-3, "host_wall_s": wall,
+            "pcie_GBps": pcie_gbs, "h2d_peak_GBps": peak_gbs, "frac_of_h2d_peak": pcie_gbs / peak_gbs,
+            "parity": {"check": "last chunk == decode of the same columns resident in HBM", "bit_exact": same}}
+
+
+def cpu_baseline_standardize(args, sample, timed=True):
+    """Oracle C/OpenMP decode + one-pass Unit standardize on a bounded sample (rank 0), at the
+    box's CPU share and at 1 thread; with timed=False (N > 1) one untimed pass for parity."""
     from oracle import oracle as O
 
     n = args.n_iid
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    threads = cpu_threads()
     bpc = (n + 3) // 4
     body = np.ascontiguousarray(sample[:, :bpc]).reshape(-1)
     ncols = sample.shape[0]
+    ref, _ = O.decode_standardize(body, n, ncols, dtype=np.float32, num_threads=threads)
     if not timed:
-        ref, _ = O.decode_standardize(body, n, ncols, dtype=np.float32, num_threads=threads)
         return ref, None
-    done, t0 = 0, time.perf_counter()
-    while True:
-        ref, _ = O.decode_standardize(body, n, ncols, dtype=np.float32, num_threads=threads)
-        done += ncols
-        el = time.perf_counter() - t0
-        if el >= args.cpu_seconds or done >= 64 * ncols:
-            break
-    return ref, {"value": done / el, "unit": "SNPs/s", "cores": threads, "kind": "port",
-            "sample": "%d reps x %d SNP columns x %d iids (first packed columns of the same synthetic matrix), "
-                      "f32 Unit, oracle/bed_oracle.c oracle_decode_standardize_f32, %.1f s" % (done // ncols, ncols, n, el)}
+
+    def rate(th, budget, max_reps):
+        done, t0 = 0, time.perf_counter()
+        while True:
+            O.decode_standardize(body, n, ncols, dtype=np.float32, num_threads=th)
+            done += ncols
+            el = time.perf_counter() - t0
+            if el >= budget or done >= max_reps * ncols:
+                return done / el, done // ncols, el
+
+    v_all, reps_all, el_all = rate(threads, args.cpu_seconds, 64)
+    v_one, reps_one, el_one = rate(1, args.cpu_seconds / 2, 4)
+    return ref, {"value": v_all, "unit": "SNPs/s", "cores": threads, "kind": "port",
+                 "single_thread_value": v_one,
+                 "sample": "%d reps x %d SNP columns x %d iids (first packed columns of the same synthetic matrix), "
+                           "f32 Unit, oracle/bed_oracle.c oracle_decode_standardize_f32 at %d threads (the box's CPU "
+                           "share; os.cpu_count() = %d is the whole machine), %.1f s; 1 thread: %d reps, %.1f s"
+                           % (reps_all, ncols, n, threads, os.cpu_count() or 0, el_all, reps_one, el_one)}
 
 
-# ---------------------------------------------------------------------------- leg 2: GRM
-def leg_grm(N, args, dist, rccl):
-    n, m, B = args.grm_iid, args.grm_sid, args.grm_block
-    pitch = N.lib().snpmi_packed_pitch(n)
+# ---------------------------------------------------------------------------- leg 2: GRM (cfg4)
+def leg_grm(N, args, dist, dtype):
     from pysnptools_amd.shard import rank_span_blocks, snp_blocks
 
+    n, m, B = args.grm_iid, args.grm_sid, args.grm_block
+    dt, esz = (N.DT_F32, 4) if dtype == "f32" else (N.DT_F64, 8)
+    pitch = N.lib().snpmi_packed_pitch(n)
     blocks = snp_blocks(m, B)
     mine = rank_span_blocks(m, B, dist.rank, dist.world)
     my_m = sum(c for _, c in mine)
     packed = Dev(N, max(1, my_m) * pitch)
     off = 0
     for s0, c in mine:  # generate exactly the global SNP ids this rank owns
-        synth(N, ctypes.c_void_p(packed.p.value + off * pitch), pitch, n, s0, c, args.seed + 100, 0.01)
+        synth(N, packed.at(off * pitch), pitch, n, s0, c, args.seed + 100, 0.01)
         off += c
-    tile_bytes = N.lib().snpmi_grm_tile_bytes(n, N.DT_F32)
+    tile_bytes = N.lib().snpmi_grm_tile_bytes(n, dt)
     tiles = Dev(N, tile_bytes)
-    lut, stats = Dev(N, B * 16), Dev(N, B * 8)
+    lut, stats = Dev(N, B * 4 * esz), Dev(N, B * 2 * esz)
     ev = Events(N, 2 + 2 * max(1, len(mine)) + 2)
 
     def run(timed, limit=None):
@@ -344,17 +564,17 @@ def leg_grm(N, args, dist, rccl):
         if not todo:
             N.call("snpmi_dev_memset", tiles.p, 0, tile_bytes)
         for k, (s0, c) in enumerate(todo):
-            src = ctypes.c_void_p(packed.p.value + off * pitch)
-            N.call("snpmi_dev_snp_stats", src, pitch, n, c, 0, N.STD_UNIT, 0.0, 0.0, 0, N.DT_F32, stats.p, lut.p)
+            src = packed.at(off * pitch)
+            N.call("snpmi_dev_snp_stats", src, pitch, n, c, 0, N.STD_UNIT, 0.0, 0.0, 0, dt, stats.p, lut.p)
             if timed:
                 ev.record(2 + 2 * k)
-            N.call("snpmi_dev_syrk_packed", src, pitch, n, c, lut.p, N.DT_F32, tiles.p, int(k > 0))
+            N.call("snpmi_dev_syrk_packed", src, pitch, n, c, lut.p, dt, tiles.p, int(k > 0))
             if timed:
                 ev.record(3 + 2 * k)
             off += c
-        if rccl and timed:
+        if dist.rccl and timed:
             ev.record(len(ev.ev) - 2)
-            N.call("snpmi_rccl_allreduce_sum", tiles.p, tile_bytes // 4, N.DT_F32)
+            N.call("snpmi_rccl_allreduce_sum", tiles.p, tile_bytes // esz, dt)
             ev.record(len(ev.ev) - 1)
         N.call("snpmi_stream_sync")
 
@@ -365,32 +585,28 @@ def leg_grm(N, args, dist, rccl):
     dist.barrier()
     wall = dist.max(time.perf_counter() - t0)
     syrk_ms = [ev.ms(2 + 2 * k, 3 + 2 * k) for k in range(len(mine))]
-    allreduce_ms = ev.ms(len(ev.ev) - 2, len(ev.ev) - 1) if rccl else 0.0
-    # spot parity at scale: diag(K) == sum over SNPs of z^2 == count of polymorphic SNPs-ish is
-    # not exact; instead check symmetry-free invariant: trace(K) = sum_j n_obs_j (Unit: sum z^2 = n_obs)
+    allreduce_ms = ev.ms(len(ev.ev) - 2, len(ev.ev) - 1) if dist.rccl else 0.0
     tr = ctypes.c_double()
-    N.call("snpmi_dev_grm_trace", tiles.p, n, N.DT_F32, ctypes.byref(tr))
-    flops_full_block = n * (n + 1) * B
+    N.call("snpmi_dev_grm_trace", tiles.p, n, dt, ctypes.byref(tr))
     nb = (n + 255) // 256
-    exec_ratio = SPLIT_PRODUCTS * 2 * 256 * 256 * (nb * (nb + 1) // 2) / (n * (n + 1))  # executed bf16 / algorithmic
+    exec_ratio = SPLIT_PRODUCTS * 2 * 256 * 256 * (nb * (nb + 1) // 2) / (n * (n + 1))  # executed fp16 / algorithmic
     res = dict(wall=wall, syrk_ms=syrk_ms, allreduce_ms=allreduce_ms, trace=tr.value, exec_ratio=exec_ratio,
-               # throughput over this rank's launches (the last block of a shard can be partial)
                mean_tflops=(n * (n + 1) * my_m / (np.sum(syrk_ms) * 1e-3) / 1e12) if syrk_ms else 0.0,
-               nblocks=len(blocks))
+               nblocks=len(blocks), my_m=my_m)
     if dist.rank == 0 and not args.skip_cpu and my_m > 0:
         # parity sample (untimed): K rows 0..63 of the GRM of this rank's first 512 SNPs
         cm, rows = min(512, my_m), 64
-        N.call("snpmi_dev_snp_stats", packed.p, pitch, n, cm, 0, N.STD_UNIT, 0.0, 0.0, 0, N.DT_F32, stats.p, lut.p)
-        N.call("snpmi_dev_syrk_packed", packed.p, pitch, n, cm, lut.p, N.DT_F32, tiles.p, 0)
+        N.call("snpmi_dev_snp_stats", packed.p, pitch, n, cm, 0, N.STD_UNIT, 0.0, 0.0, 0, dt, stats.p, lut.p)
+        N.call("snpmi_dev_syrk_packed", packed.p, pitch, n, cm, lut.p, dt, tiles.p, 0)
         ri = np.arange(rows, dtype=np.uint64)
-        dri, dout = Dev(N, rows * 8), Dev(N, rows * n * 4)
+        dri, dout = Dev(N, rows * 8), Dev(N, rows * n * esz)
         N.call("snpmi_memcpy_h2d", dri.p, N.ptr(ri), ri.nbytes)
-        N.call("snpmi_dev_grm_extract", tiles.p, n, N.DT_F32, dri.p, rows, None, n, 1, 1.0, dout.p)
-        krows = np.empty((rows, n), dtype=np.float32)
+        N.call("snpmi_dev_grm_extract", tiles.p, n, dt, dri.p, rows, None, n, 1, 1.0, dout.p)
+        krows = np.empty((rows, n), dtype=np.float32 if esz == 4 else np.float64)
         N.call("snpmi_memcpy_d2h", N.ptr(krows), dout.p, krows.nbytes)
         sample = np.empty((cm, pitch), dtype=np.uint8)
         N.call("snpmi_memcpy_d2h", N.ptr(sample), packed.p, sample.nbytes)
-        res["parity_sample"] = (krows, sample, cm, (mine[0][0] if mine else 0))
+        res["parity_sample"] = (krows, sample, cm)
         dri.free()
         dout.free()
     ev.destroy()
@@ -399,21 +615,64 @@ def leg_grm(N, args, dist, rccl):
     return res
 
 
+def grm_parity(args, krows, sample, cm, tol):
+    """Oracle (f64, reference one-pass Unit + NumPy Z Z^T) vs the GPU's K rows."""
+    from oracle import oracle as O
+
+    n = args.grm_iid
+    bpc = (n + 3) // 4
+    Z = O.decode(np.ascontiguousarray(sample[:, :bpc]).reshape(-1), n, cm, dtype=np.float64)
+    O.standardize_native(Z)
+    rows = krows.shape[0]
+    ref = Z[:rows].dot(Z.T)
+    scale = np.abs(np.diag(ref[:, :rows])).max()
+    err = float(np.abs(krows.astype(np.float64) - ref).max() / scale)
+    return {"check": "K rows 0..%d over %d SNPs (first of this rank's blocks), %d iids: GPU %s vs oracle f64"
+                     % (rows - 1, cm, n, krows.dtype), "max_abs_err_over_max_diag": err, "pass": err <= tol}
+
+
+def cpu_baseline_grm(dtype):
+    """NumPy Z.dot(Z.T) (OpenBLAS syrk, the reference's snpdata.py:203-206 / snpreader.py:655) with
+    the BLAS pool pinned to the box's CPU share; `cores` = the threads the BLAS pool reports."""
+    from threadpoolctl import threadpool_info, threadpool_limits
+
+    n, b = 10_000, 2048
+    rng = np.random.default_rng(0)
+    Z = rng.standard_normal((n, b)).astype(np.float32 if dtype == "f32" else np.float64)
+    want = cpu_threads()
+    with threadpool_limits(limits=want, user_api="blas"):
+        used = [p.get("num_threads") for p in threadpool_info() if p.get("user_api") == "blas"]
+        Z.dot(Z.T)
+        t0 = time.perf_counter()
+        reps = 0
+        while True:
+            Z.dot(Z.T)
+            reps += 1
+            el = time.perf_counter() - t0
+            if el > 3.0 or reps >= 8:
+                break
+    cores = used[0] if used else want
+    return {"value": reps * n * (n + 1) * b / el / 1e9, "unit": "GF/s", "cores": cores, "kind": "port",
+            "sample": "%d x Z.dot(Z.T), Z = %d x %d %s (NumPy/OpenBLAS, BLAS pool pinned to %d threads), %.1f s"
+                      % (reps, n, b, dtype, cores, el)}
+
+
 # ---------------------------------------------------------------------------- leg 3: cfg5 partitioned GRM
 def leg_grm5(N, args, dist):
-    """configs[4] shape: 500k iids, K (500 GB upper triangle f32)
-    partitioned over ranks as 256x256 blocks.  Per SNP block each rank uploads ITS 1/p of the
-    packed columns from pinned host memory, ncclAllGather rebuilds the packed block on every
-    rank, then stats + the fused SYRK fill only the rank's own K blocks -- no reduction.
-    One timed block of --grm5-sid SNPs (GRM time is linear in M)."""
-    n, p = args.grm5_iid, dist.world
-    m = (args.grm5_sid + p - 1) // p * p
-    ms = m // p
+    """configs[4] shape: 500k iids, K (500 GB f32 upper triangle) partitioned as
+    256x256 blocks over the P = max(N, 8) parts of the 8-GPU plan; this process owns part `rank`.
+    One block of --grm5-sid SNPs: each rank uploads ITS 1/N of the packed block from pinned host
+    memory (at N = 1 the whole block), ncclAllGather rebuilds it at N > 1, then stats + the fp16x2
+    SYRK fill only this part's K blocks -- no reduction.  GRM time is linear in M."""
+    n, world = args.grm5_iid, dist.world
+    P = max(world, GRM5_PLAN_WORLD)
+    m = (args.grm5_sid + world - 1) // world * world
+    ms = m // world
     pitch = N.lib().snpmi_packed_pitch(n)
-    nloc = N.lib().snpmi_grm_part_blocks(n, dist.rank, p)
+    nloc = N.lib().snpmi_grm_part_blocks(n, dist.rank, P)
     packed = Dev(N, pitch * m)
-    mine = packed.p.value + dist.rank * ms * pitch
-    # the rank's shard of the .bed, staged in page-locked memory (untimed, like reading the file)
+    mine = packed.at(dist.rank * ms * pitch)
+    # the rank's share of the .bed, staged in page-locked memory (untimed, like reading the file)
     host = ctypes.c_void_p()
     N.call("snpmi_host_alloc", ctypes.byref(host), ms * pitch)
     synth(N, mine, pitch, n, dist.rank * ms, ms, args.seed + 200, 0.01)
@@ -426,33 +685,41 @@ def leg_grm5(N, args, dist):
     dist.barrier()
     t0 = time.perf_counter()
     ev.record(0)
-    N.call("snpmi_memcpy_h2d", mine, host, ms * pitch)
+    N.call("snpmi_memcpy_async", mine, host, ms * pitch, 0, 0)
     ev.record(1)
     if dist.rccl:
         N.call("snpmi_rccl_allgather", mine, packed.p, ms * pitch)
     ev.record(2)
     N.call("snpmi_dev_snp_stats", packed.p, pitch, n, m, 0, N.STD_UNIT, 0.0, 0.0, 0, N.DT_F32, stats.p, lut.p)
-    N.call("snpmi_dev_syrk_packed_part", packed.p, pitch, n, m, lut.p, dist.rank, p, blocks.p, 0)
+    N.call("snpmi_dev_syrk_packed_part", packed.p, pitch, n, m, lut.p, dist.rank, P, blocks.p, 0)
     ev.record(3)
     N.call("snpmi_stream_sync")
     dist.barrier()
     wall = dist.max(time.perf_counter() - t0)
     res = {"wall": wall, "h2d_ms": ev.ms(0, 1), "allgather_ms": ev.ms(1, 2), "syrk_ms": ev.ms(2, 3),
-           "n_local_blocks": nloc, "m": m}
-    if dist.rank == 0 and not args.skip_cpu and nloc > 0:
-        r0, c0 = ctypes.c_uint64(), ctypes.c_uint64()
-        N.call("snpmi_grm_part_coords", n, 0, p, 0, ctypes.byref(r0), ctypes.byref(c0))
-        blk = np.empty((256, 256), dtype=np.float32)
-        N.call("snpmi_memcpy_d2h", N.ptr(blk), blocks.p, blk.nbytes)
+           "n_local_blocks": nloc, "m": m, "ms": ms, "P": P, "pitch": pitch}
+    if dist.rank == 0 and not args.skip_cpu and nloc > 1:
+        picks = []
+        for b in range(min(nloc, 64)):  # block 0 is diagonal; the first off-diagonal one after it
+            r0, c0 = ctypes.c_uint64(), ctypes.c_uint64()
+            N.call("snpmi_grm_part_coords", n, 0, P, b, ctypes.byref(r0), ctypes.byref(c0))
+            if (b == 0) or (r0.value != c0.value and len(picks) == 1):
+                blk = np.empty((256, 256), dtype=np.float32)
+                N.call("snpmi_memcpy_d2h", N.ptr(blk), blocks.at(b * 256 * 256 * 4), blk.nbytes)
+                picks.append((blk, r0.value, c0.value))
+            if len(picks) == 2:
+                break
         sample = np.empty((m, pitch), dtype=np.uint8)
         N.call("snpmi_memcpy_d2h", N.ptr(sample), packed.p, sample.nbytes)
         # the gathered block must equal the whole block generated in one piece
-        synth(N, packed.p, pitch, n, 0, m, args.seed + 200, 0.01)
-        whole = np.empty_like(sample)
-        N.call("snpmi_memcpy_d2h", N.ptr(whole), packed.p, whole.nbytes)
-        res["gather_exact"] = bool(np.array_equal(sample, whole))
-        del whole
-        res["parity_sample"] = (blk, sample, r0.value, c0.value)
+        whole = Dev(N, pitch * m)
+        synth(N, whole.p, pitch, n, 0, m, args.seed + 200, 0.01)
+        chk = np.empty_like(sample)
+        N.call("snpmi_memcpy_d2h", N.ptr(chk), whole.p, chk.nbytes)
+        whole.free()
+        res["gather_exact"] = bool(np.array_equal(sample, chk))
+        del chk
+        res["parity_sample"] = (picks, sample)
     ev.destroy()
     N.call("snpmi_host_free", host)
     for d in (packed, lut, stats, blocks):
@@ -460,60 +727,31 @@ def leg_grm5(N, args, dist):
     return res
 
 
-def grm5_parity(args, m, blk, sample, row0, col0):
-    """Oracle (f64) for one 256x256 block of the partitioned K: decode only its 512 iids."""
+def grm5_parity(args, m, picks, sample):
+    """Oracle (f64) for 256x256 blocks of the partitioned K: stats over every iid, values decoded
+    only for the blocks' 512 iids."""
     from oracle import oracle as O
 
     n = args.grm5_iid
     bpc = (n + 3) // 4
     body = np.ascontiguousarray(sample[:, :bpc]).reshape(-1)
-    rows = np.arange(row0, min(row0 + 256, n))
-    cols = np.arange(col0, min(col0 + 256, n))
-    # stats use every iid; the block needs only its rows/cols
     full_stats = O.snp_stats(body, n, m)
-    Zr = O.decode(body, n, m, iid_index=rows)
-    Zc = O.decode(body, n, m, iid_index=cols)
-    O.standardize_native(Zr, use_stats=True, stats=full_stats)
-    O.standardize_native(Zc, use_stats=True, stats=full_stats)
-    ref = Zr.dot(Zc.T)
-    scale = max(np.abs(np.diag(ref)).max() if row0 == col0 else np.abs(ref).max(), 1.0)
-    err = float(np.abs(blk[:len(rows), :len(cols)].astype(np.float64) - ref).max() / scale)
-    return {"check": "rank 0 block 0 (rows %d.., cols %d..) over %d SNPs x %d iids: GPU f32 vs oracle f64"
-                     % (row0, col0, m, n), "max_abs_err_over_scale": err, "pass": err <= 1e-5}
-
-
-def cpu_baseline_grm(args):
-    """NumPy Z.dot(Z.T) (OpenBLAS syrk, the reference's snpdata.py:203-206 / snpreader.py:655)."""
-    n, b = 10_000, 2048
-    rng = np.random.default_rng(0)
-    Z = rng.standard_normal((n, b)).astype(np.float32)
-    t0 = time.perf_counter()
-    reps = 0
-    while True:
-        Z.dot(Z.T)
-        reps += 1
-        el = time.perf_counter() - t0
-        if el > 4.0 or reps >= 8:
-            break
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)
-    return {"value": reps * n * (n + 1) * b / el / 1e9, "unit": "GF/s", "cores": threads, "kind": "port",
-            "sample": "%d x Z.dot(Z.T), Z = %d x %d f32 (NumPy/OpenBLAS), %.1f s" % (reps, n, b, el)}
-
-
-def grm_parity(args, krows, sample, cm, sid0):
-    """Oracle (f64, reference one-pass Unit + NumPy Z Z^T) vs the GPU's f32 K rows."""
-    from oracle import oracle as O
-
-    n = args.grm_iid
-    bpc = (n + 3) // 4
-    Z = O.decode(np.ascontiguousarray(sample[:, :bpc]).reshape(-1), n, cm, dtype=np.float64)
-    O.standardize_native(Z)
-    rows = krows.shape[0]
-    ref = Z[:rows].dot(Z.T)
-    scale = np.abs(np.diag(ref[:, :rows])).max()
-    err = float(np.abs(krows.astype(np.float64) - ref).max() / scale)
-    return {"check": "K rows 0..%d over %d SNPs (first of this rank's blocks), %d iids: GPU f32 MFMA vs oracle f64"
-                     % (rows - 1, cm, n), "max_abs_err_over_max_diag": err, "pass": err <= 1e-5}
+    out = []
+    worst = 0.0
+    for blk, row0, col0 in picks:
+        rows = np.arange(row0, min(row0 + 256, n))
+        cols = np.arange(col0, min(col0 + 256, n))
+        Zr = O.decode(body, n, m, iid_index=rows)
+        Zc = O.decode(body, n, m, iid_index=cols)
+        O.standardize_native(Zr, use_stats=True, stats=full_stats)
+        O.standardize_native(Zc, use_stats=True, stats=full_stats)
+        ref = Zr.dot(Zc.T)
+        scale = max(np.abs(np.diag(ref)).max() if row0 == col0 else np.abs(ref).max(), 1.0)
+        err = float(np.abs(blk[:len(rows), :len(cols)].astype(np.float64) - ref).max() / scale)
+        worst = max(worst, err)
+        out.append({"row0": int(row0), "col0": int(col0), "max_abs_err_over_scale": err})
+    return {"check": "part 0 blocks (diagonal + off-diagonal) over %d SNPs x %d iids: GPU f32 (fp16x2 MFMA) vs "
+                     "oracle f64" % (m, n), "blocks": out, "max_abs_err_over_scale": worst, "pass": worst <= 1e-5}
 
 
 def pmc_traffic(kernel, leg, n_iid, block):
@@ -530,93 +768,131 @@ def pmc_traffic(kernel, leg, n_iid, block):
     return None
 
 
-def main():
-    args = parse()
+def grm_entry(args, dist, r, dtype):
+    n, m = args.grm_iid, args.grm_sid
+    gf = n * (n + 1) * m / r["wall"] / 1e9
+    f32 = dtype == "f32"
+    peak = SPLIT_PEAK_TFLOPS if f32 else MFMA_F64_PEAK_TFLOPS
+    roof = {"bound": "mfma", "achieved": r["mean_tflops"], "peak": peak, "unit": "TFLOP/s",
+            "frac": r["mean_tflops"] / peak, "per_launch_flops": n * (n + 1) * args.grm_block}
+    if f32:
+        roof.update({"traffic": pmc_traffic("f32w::k_syrk_h2", "grm", n, args.grm_block),
+                     "kernel": "f32w::k_syrk_h2<false,4>: f32 GRM as 3 fp16 MFMA products of each value's fp16x2 "
+                               "split, f32 accumulate (v_mfma_f32_32x32x16_f16); peak = 2.5 PF fp16 dense / 3; time "
+                               "per block includes k_lut_bf3, k_lut_h2 and the range-gated bf16x3 launch (exits at "
+                               "once for Unit)",
+                     "f32_mfma_peak": MFMA_F32_PEAK_TFLOPS,
+                     "mfma_util_executed": r["mean_tflops"] * r["exec_ratio"] / MFMA_BF16_PEAK_TFLOPS})
+    else:
+        roof.update({"traffic": None,
+                     "kernel": "k_decode_f<double> into Z + f64k::k_syrk_glds (v_mfma_f64_16x16x4_f64, operand rows "
+                               "by global_load_lds); peak = 78.6 TF f64 dense"})
+    return {"workload": "cfg4: %d iid x %d SNP, Unit, block %d, %s SYRK, SNPs split into %d contiguous shard(s) "
+                        "streamed in blocks%s" % (n, m, args.grm_block, "f32 (fp16x2 MFMA)" if f32 else "f64 (f64 MFMA)",
+                                                 dist.world, ", RCCL all-reduce of K tiles" if dist.rccl else ""),
+            "gflops": gf, "snps_per_s": m / r["wall"], "seconds": r["wall"], "scaling": "strong",
+            "allreduce_ms": r["allreduce_ms"], "trace_K": r["trace"], "roofline": roof}
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args, argv))  # before anything touches the GPU
+    if os.environ.get("SNPMI_BENCH_DRYRUN"):
+        # launcher check without a GPU (tests/test_bench_launch.py): report the rank layout and stop
+        world = int(os.environ.get("WORLD_SIZE", "1"))
+        if world != args.gpus:
+            raise SystemExit("bench.py: --gpus %d but WORLD_SIZE=%d (one process per GPU)" % (args.gpus, world))
+        print(json.dumps({k: os.environ.get(k) for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR",
+                                                         "MASTER_PORT", "SNPMI_RCCL_ID_FILE")}), flush=True)
+        return
     from pysnptools_amd import _native as N
 
     dist = Dist(args.gpus, N, args.force_rccl)
-    rccl = dist.rccl
 
     r1 = leg_standardize(N, args, dist)
-    total_snps = args.n_sid * dist.world * args.steps
-    value = total_snps / r1["wall"]
-    grm = None
+    value = args.n_sid * args.steps / r1["wall"]
+    grm = grm64 = grm5 = dec_c = e2e = None
+    if dist.rank == 0:
+        dec_c = leg_decode_c(N, args)
+        if args.e2e == "on":
+            e2e = leg_e2e(N, args)
+    dist.barrier()
     if not args.skip_grm:
-        r2 = leg_grm(N, args, dist, rccl)
-        n, m = args.grm_iid, args.grm_sid
-        gf = n * (n + 1) * m / r2["wall"] / 1e9
-        grm = {"workload": "cfg4: %d iid x %d SNP, Unit, block %d, f32 (fp16x2 MFMA) SYRK, SNPs split into %d equal "
-                           "contiguous shard(s) streamed in blocks%s" % (n, m, args.grm_block, dist.world,
-                                                                         ", RCCL all-reduce of K tiles" if rccl else ""),
-               "gflops": gf, "snps_per_s": m / r2["wall"], "seconds": r2["wall"], "scaling": "strong",
-               "allreduce_ms": r2["allreduce_ms"], "trace_K": r2["trace"],
-               "roofline": {"bound": "mfma", "achieved": r2["mean_tflops"], "peak": SPLIT_PEAK_TFLOPS,
-                            "unit": "TFLOP/s", "frac": r2["mean_tflops"] / SPLIT_PEAK_TFLOPS,
-                            "traffic": pmc_traffic("f32w::k_syrk_h2", "grm", n, args.grm_block),
-                            "kernel": "f32w::k_syrk_h2<false,4>: f32 GRM as 3 fp16 MFMA products of each "
-                                      "value's fp16x2 split, f32 accumulate (v_mfma_f32_32x32x16_f16); "
-                                      "peak = 2.5 PF fp16 dense / 3; time per block includes k_lut_bf3, "
-                                      "k_lut_h2 and the range-gated bf16x3 launch (exits at once for Unit)",
-                            "per_launch_flops": n * (n + 1) * args.grm_block,
-                            "f32_mfma_peak": MFMA_F32_PEAK_TFLOPS,
-                            "mfma_util_executed": r2["mean_tflops"] * r2["exec_ratio"] / MFMA_BF16_PEAK_TFLOPS,
-                            "bf16x3_peak": MFMA_BF16_PEAK_TFLOPS / 6}}
-    grm5 = None
-    run5 = args.grm5 == "on" or (args.grm5 == "auto" and dist.world >= 4 and not args.skip_grm)
-    if run5:
+        r2 = leg_grm(N, args, dist, "f32")
+        grm = grm_entry(args, dist, r2, "f32")
+        if args.grm_f64 == "on":
+            r2d = leg_grm(N, args, dist, "f64")
+            grm64 = grm_entry(args, dist, r2d, "f64")
+    if args.grm5 == "on":
         r3 = leg_grm5(N, args, dist)
-        n5, m5 = args.grm5_iid, r3["m"]
-        gf5 = n5 * (n5 + 1) * m5 / r3["wall"] / 1e9
-        grm5 = {"workload": "cfg5: %d iid x %d SNP (one block of the 1M), Unit, f32 MFMA; each rank uploads 1/%d "
-                            "of the packed block from pinned host, RCCL all-gather, K as 256x256 blocks "
-                            "partitioned over %d rank(s), no reduction" % (n5, m5, dist.world, dist.world),
-                "h2d_ms": r3["h2d_ms"], "allgather_ms": r3["allgather_ms"], "syrk_ms": r3["syrk_ms"],
-                "gflops": gf5, "seconds": r3["wall"], "scaling": "strong",
+        n5, m5, P = args.grm5_iid, r3["m"], r3["P"]
+        flops_part = n5 * (n5 + 1) * m5 / P  # this part's share of the SYRK work
+        syrk_tf = flops_part / (r3["syrk_ms"] * 1e-3) / 1e12
+        grm5 = {"workload": "cfg5: %d iid x %d SNP (one block of the 1M), Unit, f32 (fp16x2 MFMA); K as 256x256 "
+                            "blocks in %d parts (the 8-GPU plan), this process = part %d; the packed block comes "
+                            "from pinned host memory inside the timed region (%d upload(s) of %d SNPs%s), no "
+                            "reduction" % (n5, m5, P, dist.rank, 1, r3["ms"],
+                                           " + RCCL all-gather" if dist.rccl else ""),
+                "h2d_ms": r3["h2d_ms"], "h2d_GBps": r3["ms"] * r3["pitch"] / (r3["h2d_ms"] * 1e-3) / 1e9,
+                "allgather_ms": r3["allgather_ms"], "syrk_ms": r3["syrk_ms"], "syrk_tflops": syrk_tf,
+                "seconds": r3["wall"], "gflops_per_gpu": flops_part / r3["wall"] / 1e9,
+                "snps_per_s": m5 / r3["wall"], "parts": P, "scaling": "strong",
                 "blocks_on_rank0": r3["n_local_blocks"], "K_bytes_per_rank": r3["n_local_blocks"] * 256 * 256 * 4,
-                "roofline": {"bound": "mfma", "achieved": gf5 / 1e3 / dist.world, "peak": SPLIT_PEAK_TFLOPS,
-                             "unit": "TFLOP/s per GPU", "frac": gf5 / 1e3 / dist.world / SPLIT_PEAK_TFLOPS,
-                             "traffic": None, "kernel": "f32w::k_syrk_h2<true,4> (fp16x2 split, 3 fp16 "
-                                                        "MFMA products, f32 accumulate; wall incl. H2D + all-gather)"},
-                "projected_seconds_1M_snps": r3["wall"] * 1_000_000 / m5}
+                "roofline": {"bound": "mfma", "achieved": syrk_tf, "peak": SPLIT_PEAK_TFLOPS, "unit": "TFLOP/s",
+                             "frac": syrk_tf / SPLIT_PEAK_TFLOPS, "traffic": None,
+                             "kernel": "f32w::k_syrk_h2<true,4> (fp16x2 split, 3 fp16 MFMA products, f32 "
+                                       "accumulate), this part's blocks only"},
+                "projected_seconds_1M_snps": r3["wall"] * 1_000_000 / m5,
+                "projected_note": "per process; the 8 parts run concurrently on 8 GPUs, so this is the 8-GPU "
+                                  "job time when N = 8, and N = 1 shows one part's share"}
         if r3.get("parity_sample") is not None:
             grm5["parity"] = grm5_parity(args, m5, *r3["parity_sample"])
             grm5["parity"]["gathered_block_bit_exact"] = r3["gather_exact"]
             grm5["parity"]["pass"] = grm5["parity"]["pass"] and r3["gather_exact"]
     if dist.rank == 0:
-        cpu = None
-        parity = None
+        cpu = parity = None
         if not args.skip_cpu and r1["sample"] is not None:
-            ref, cpu = cpu_baseline_standardize(args, r1["sample"], r1["pitch"], timed=dist.world == 1)
+            ref, cpu = cpu_baseline_standardize(args, r1["sample"], timed=dist.world == 1)
             same = np.array_equal(r1["gpu_cols"][:, :args.n_iid].T, ref)
             parity = {"check": "first %d SNP columns x %d iids: GPU stats+decode vs oracle decode+one-pass "
                                "Unit (f32)" % (ref.shape[1], ref.shape[0]), "bit_exact": bool(same)}
             if grm is not None:
-                grm["cpu_baseline"] = cpu_baseline_grm(args) if dist.world == 1 else None
+                grm["cpu_baseline"] = cpu_baseline_grm("f32") if dist.world == 1 else None
                 if r2.get("parity_sample") is not None:
-                    grm["parity"] = grm_parity(args, *r2["parity_sample"])
+                    grm["parity"] = grm_parity(args, *r2["parity_sample"], tol=1e-5)
+            if grm64 is not None:
+                grm64["cpu_baseline"] = cpu_baseline_grm("f64") if dist.world == 1 else None
+                if r2d.get("parity_sample") is not None:
+                    grm64["parity"] = grm_parity(args, *r2d["parity_sample"], tol=1e-10)
         n = args.n_iid
         line = {
-            "metric": METRIC, "value": value, "unit": "SNPs/s", "n_gpus": dist.world, "steps": args.steps,
+            "metric": METRIC, "value": value, "unit": "SNPs/s", "n_gpus": dist.n_gpus, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": r1["wall"] / args.steps * 1e3, "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-            "config": {"workload": "decode+Unit standardize, %d iid x %d SNP per GPU (packed BED resident in HBM, "
-                                   "SnpGen MAF curve, 1%% missing), block %d SNPs, f32 F-order" % (
-                                       n, args.n_sid, args.block),
-                       "n_iid": n, "n_sid_per_gpu": args.n_sid, "block": args.block,
+            "scaling": "strong", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "config": {"workload": "decode+Unit standardize of the %d iid x %d SNP matrix (packed BED resident in "
+                                   "HBM, SnpGen MAF curve, 1%% missing), SNPs split into %d contiguous shard(s), "
+                                   "block %d SNPs, f32 F-order" % (n, args.n_sid, dist.world, args.block),
+                       "n_iid": n, "n_sid": args.n_sid, "n_sid_per_gpu": r1["m"], "block": args.block,
                        "parallelism": "snp-shard x%d" % dist.world},
+            "weak": ({"value": args.n_sid * args.steps * dist.world / r1["weak_wall"], "unit": "SNPs/s",
+                      "workload": "every rank streams 1M SNPs per step (its shard %d times)" % dist.world}
+                     if r1["weak_wall"] else None),
             "roofline": {"bound": "hbm", "achieved": r1["achieved_gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": r1["achieved_gbs"] / HBM_PEAK_GBS,
-                         "traffic": pmc_traffic("k_decode_std_lds_f32" if r1["fused"] else "k_decode_f<float>", "dec",
-                                                n, args.block),
-                         "kernel": ("k_decode_std_lds_f32 (stats + decode, packed column staged in LDS)"
-                                    if r1["fused"] else "k_decode_f<float> (after k_snp_stats)"),
+                         "traffic": pmc_traffic("k_decode_f<float>", "dec", n, args.block),
+                         "kernel": "k_decode_f<float> (after k_snp_stats)",
                          "per_launch_bytes": r1["full_block_bytes"],
                          "mean_launch_ms": r1["dec_mean_ms"],
                          "measured_stream_GBps": {"copy_16B_nt (1 read : 1 write)": r1["copy_gbs"],
                                                   "hipMemset fill (write only)": r1["fill_gbs"]}},
             "cpu_baseline": cpu,
             "parity": parity,
+            "decode_c": dec_c,
+            "e2e": e2e,
             "grm": grm,
+            "grm_f64": grm64,
             "grm5": grm5,
         }
         print(json.dumps(line), flush=True)

@@ -204,6 +204,16 @@ int snpmi_event_create(void** ev);
 int snpmi_event_destroy(void* ev);
 int snpmi_event_record(void* ev);
 int snpmi_event_elapsed_ms(void* start, void* stop, float* ms);
+/* Streaming: the library keeps TWO streams per device -- compute (every kernel above) and copy
+ * (DMA).  The file-backed entry points pipeline their chunks across them (H2D of chunk c+1 and
+ * D2H of chunk c-1 overlap the kernels of chunk c); these calls let a caller build the same
+ * pipeline over its own pinned buffers (snpmi_host_alloc).  on_copy: 0 = compute, 1 = copy.
+ * kind: 0 = host->device, 1 = device->host, 2 = device->device.  snpmi_stream_sync waits for
+ * both streams. */
+int snpmi_memcpy_async(void* dst, const void* src, uint64_t bytes, int kind, int on_copy);
+int snpmi_event_record_on(void* ev, int on_copy);
+int snpmi_stream_wait_event(void* ev, int on_copy);   /* that stream waits for ev (no host wait) */
+int snpmi_event_sync(void* ev);
 
 /* counter-based synthetic genotypes (SnpGen MAF curve, snpreader/snpgen.py:140-151) */
 int snpmi_dev_synth_bed(uint8_t* packed, uint64_t pitch, uint64_t n_iid, uint64_t sid0, uint64_t n_sid,
@@ -267,6 +277,7 @@ int snpmi_rccl_allgather(const void* send, void* recv, uint64_t bytes_per_rank);
 /* host-value all-reduce (op 0 = sum, 1 = max) of f64 scalars, synchronous; barrier = 1-elem sum */
 int snpmi_rccl_host_allreduce_f64(double* values, uint64_t count, int op);
 int snpmi_rccl_barrier(void);
+int snpmi_rccl_comm_count(int* count);                    /* ncclCommCount: ranks in the communicator */
 int snpmi_rccl_destroy(void);
 
 #ifdef __cplusplus

@@ -85,6 +85,10 @@ _SIGS = {
     "snpmi_event_destroy": [_vp],
     "snpmi_event_record": [_vp],
     "snpmi_event_elapsed_ms": [_vp, _vp, ctypes.POINTER(ctypes.c_float)],
+    "snpmi_memcpy_async": [_vp, _vp, _u64, _i32, _i32],
+    "snpmi_event_record_on": [_vp, _i32],
+    "snpmi_stream_wait_event": [_vp, _i32],
+    "snpmi_event_sync": [_vp],
     "snpmi_dev_synth_bed": [_vp, _u64, _u64, _u64, _u64, _u64, _f64, _vp, _vp, _i32],
     "snpmi_dev_snp_stats": [_vp, _u64, _u64, _u64, _i32, _i32, _f64, _f64, _i32, _i32, _vp, _vp],
     "snpmi_dev_decode": [_vp, _u64, _u64, _u64, _vp, _i32, _i32, _vp, _u64],
@@ -106,6 +110,7 @@ _SIGS = {
     "snpmi_rccl_allgather": [_vp, _vp, _u64],
     "snpmi_rccl_host_allreduce_f64": [_vp, _u64, _i32],
     "snpmi_rccl_barrier": [],
+    "snpmi_rccl_comm_count": [ctypes.POINTER(ctypes.c_int)],
     "snpmi_rccl_destroy": [],
     "snpmi_last_error": [],
 }

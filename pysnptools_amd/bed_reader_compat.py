@@ -72,8 +72,10 @@ class open_bed(object):
         return self._bim_cols
 
     def _prop(self, name, fam, col, conv=None):
+        # given properties are converted to bed-reader's dtypes too (str / float32 / int32)
         if self._props.get(name) is not None:
-            return np.asarray(self._props[name])
+            v = np.asarray(self._props[name])
+            return conv(v) if conv else v.astype(str)
         cols = self._famc() if fam else self._bimc()
         v = cols[col] if cols else np.empty(0, dtype=str)
         return conv(v) if conv else v
@@ -100,7 +102,7 @@ class open_bed(object):
 
     @property
     def bp_position(self):
-        return self._prop("bp_position", False, 3, lambda v: v.astype(np.int32))
+        return self._prop("bp_position", False, 3, lambda v: v.astype(np.float64).astype(np.int32))
 
     @property
     def iid_count(self):

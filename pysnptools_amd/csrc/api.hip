@@ -56,7 +56,10 @@ Device& device() {
         d = new Device();
         d->id = g_cur_dev;
         SNPMI_HIP(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
-        for (auto& e : d->staged) SNPMI_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        SNPMI_HIP(hipStreamCreateWithFlags(&d->copy, hipStreamNonBlocking));
+        for (hipEvent_t* set : {d->staged, d->consumed, d->produced, d->bounce})
+            for (int s = 0; s < 2; s++) SNPMI_HIP(hipEventCreateWithFlags(&set[s], hipEventDisableTiming));
+        SNPMI_HIP(hipEventCreateWithFlags(&d->fence, hipEventDisableTiming));
         hipDeviceProp_t p;
         SNPMI_HIP(hipGetDeviceProperties(&p, g_cur_dev));
         d->cu_count = p.multiProcessorCount;
@@ -88,6 +91,11 @@ void Device::release() {
         if (buf[s]) (void)hipFree(buf[s]);
         buf[s] = nullptr;
         cap[s] = 0;
+    }
+    for (int x = 0; x < 2; x++) {
+        if (order_tab[x]) (void)hipFree(order_tab[x]);
+        order_tab[x] = nullptr;
+        order_nb[x] = 0;
     }
 }
 
@@ -156,21 +164,28 @@ static void parallel_for(uint64_t n, int nthreads, F&& fn, uint64_t grain = 64) 
 }
 
 // Device -> pageable host copy of `rows` rows of `width` bytes (device pitch spitch, host
-// pitch dpitch).  A plain hipMemcpy to pageable memory runs at ~16 GB/s (the runtime's own
-// bounce + a single-threaded copy); here 256 MiB pieces DMA into two pinned bounce buffers
-// while host threads copy the previous piece out, so PCIe and the host copy overlap.
+// pitch dpitch) on the COPY stream, ordered after the compute stream's work so far (or after
+// `after`).  A plain hipMemcpy to pageable memory runs at ~16 GB/s (the runtime's own bounce +
+// a single-threaded copy); here 256 MiB pieces DMA into two pinned bounce buffers while host
+// threads copy the previous piece out, so PCIe and the host copy overlap -- and, because the
+// DMA sits on its own stream, kernels enqueued before this call keep running beside it.
 static void d2h_rows(Device& d, void* dst, size_t dpitch, const void* src, size_t spitch, size_t width, size_t rows,
-                     int nthreads) {
+                     int nthreads, hipEvent_t after = nullptr) {
     if (rows == 0 || width == 0) return;
+    if (!after) {
+        SNPMI_HIP(hipEventRecord(d.fence, d.stream));
+        after = d.fence;
+    }
+    SNPMI_HIP(hipStreamWaitEvent(d.copy, after, 0));
     const size_t total = width * rows;
     if (total < (32u << 20)) {
-        SNPMI_HIP(hipMemcpy2DAsync(dst, dpitch, src, spitch, width, rows, hipMemcpyDeviceToHost, d.stream));
-        SNPMI_HIP(hipStreamSynchronize(d.stream));
+        SNPMI_HIP(hipMemcpy2DAsync(dst, dpitch, src, spitch, width, rows, hipMemcpyDeviceToHost, d.copy));
+        SNPMI_HIP(hipStreamSynchronize(d.copy));
         return;
     }
     const size_t per = std::max<size_t>(1, (256u << 20) / width);
     uint8_t* bounce[2] = {(uint8_t*)pinned(4, per * width), (uint8_t*)pinned(5, per * width)};
-    hipEvent_t* ev = d.staged;  // reuse: no H2D staging is in flight here (callers sync first)
+    hipEvent_t* ev = d.bounce;
     auto drain = [&](size_t r0, size_t nr, int slot) {
         SNPMI_HIP(hipEventSynchronize(ev[slot]));
         const uint8_t* b = bounce[slot];
@@ -196,8 +211,8 @@ static void d2h_rows(Device& d, void* dst, size_t dpitch, const void* src, size_
         const size_t nr = std::min(per, rows - r0);
         const int slot = i & 1;
         SNPMI_HIP(hipMemcpy2DAsync(bounce[slot], width, (const uint8_t*)src + r0 * spitch, spitch, width, nr,
-                                   hipMemcpyDeviceToHost, d.stream));
-        SNPMI_HIP(hipEventRecord(ev[slot], d.stream));
+                                   hipMemcpyDeviceToHost, d.copy));
+        SNPMI_HIP(hipEventRecord(ev[slot], d.copy));
         if (i > 0) drain(prev_r0, prev_n, slot ^ 1);
         prev_r0 = r0;
         prev_n = nr;
@@ -302,21 +317,28 @@ static IidPlan plan_iids(Device& d, const uint64_t* iid_idx, uint64_t n_iid, uin
 
 // Upload SNP chunk [c0, c0+cnt) and return the device packed buffer for the selected iids.
 // Chunks alternate between two pinned host buffers and two device buffers (slot = chunk
-// parity), so the host gathers chunk c+1 from the mmap while the GPU still computes on
-// chunk c: the only wait is for the H2D that last read this pinned slot (two chunks ago).
+// parity).  The H2D runs on the copy stream: it waits only for the kernels that last read
+// this device slot (chunk c-2, event `consumed`), so the upload of chunk c overlaps the
+// kernels of chunk c-1, and the host gathers chunk c+1 from the mmap meanwhile.  The compute
+// stream waits on `staged` before touching the chunk.  Callers record consumed[slot] on the
+// compute stream after the chunk's last kernel (chunk_done).
 static const uint8_t* stage_chunk(Device& d, const BedMap& m, const uint64_t* sid_idx, uint64_t c0, uint64_t cnt,
                                   const IidPlan& p, int nthreads, int slot) {
-    SNPMI_HIP(hipEventSynchronize(d.staged[slot]));
+    SNPMI_HIP(hipEventSynchronize(d.staged[slot]));  // the pinned slot's previous H2D has finished
     uint8_t* host = (uint8_t*)pinned(slot, cnt * p.pitch_in);
     gather_columns(m, sid_idx, c0, cnt, p.pitch_in, host, nthreads);
     uint8_t* dev = (uint8_t*)d.get(slot ? Device::S_PACKED_B : Device::S_PACKED, cnt * p.pitch_in);
-    SNPMI_HIP(hipMemcpyAsync(dev, host, cnt * p.pitch_in, hipMemcpyHostToDevice, d.stream));
-    SNPMI_HIP(hipEventRecord(d.staged[slot], d.stream));
+    SNPMI_HIP(hipStreamWaitEvent(d.copy, d.consumed[slot], 0));
+    SNPMI_HIP(hipMemcpyAsync(dev, host, cnt * p.pitch_in, hipMemcpyHostToDevice, d.copy));
+    SNPMI_HIP(hipEventRecord(d.staged[slot], d.copy));
+    SNPMI_HIP(hipStreamWaitEvent(d.stream, d.staged[slot], 0));
     if (!p.repack) return dev;
     uint8_t* dev2 = (uint8_t*)d.get(Device::S_PACKED2, cnt * p.pitch_out);
     launch_repack(dev, p.pitch_in, p.n_in, p.idx_dev, p.idx32_dev, p.n_out, cnt, dev2, p.pitch_out, d.stream);
     return dev2;
 }
+
+static void chunk_done(Device& d, int slot) { SNPMI_HIP(hipEventRecord(d.consumed[slot], d.stream)); }
 
 template <typename T>
 struct DT;
@@ -358,33 +380,69 @@ static void bed_read_impl(const char* path, uint64_t n_iid, uint64_t n_sid, int 
     const int dt = DT<T>::v;
     const uint64_t ldF = round_up(std::max<uint64_t>(n_out, 1), 16);
     const uint64_t C = chunk_snps(p.pitch_in + p.pitch_out + ldF * sizeof(T));
+    const bool stats_out = std_kind != SNPMI_STD_NONE && !use_stats;
+    // Three-stage pipeline over SNP chunks, two slots each: host gather + H2D (copy stream) of
+    // chunk c, stats + decode of chunk c (compute stream), D2H + host copy-out of chunk c-1 (copy
+    // stream, after `produced`).  PCIe runs both directions at once and the kernels of chunk c
+    // hide under the copy-out of chunk c-1.
+    struct Pending {
+        uint64_t c0 = 0, cnt = 0, ldc = 0;
+        int slot = 0;
+        T* dev_out = nullptr;
+        T* st_dev = nullptr;
+        bool valid = false;
+    } pending;
+    auto drain = [&](const Pending& q) {
+        if (n_out > 0) {
+            if (!order_c)
+                d2h_rows(d, out + q.c0 * n_out, n_out * sizeof(T), q.dev_out, ldF * sizeof(T), n_out * sizeof(T),
+                         q.cnt, nthreads, d.produced[q.slot]);
+            else
+                d2h_rows(d, out + q.c0, m_out * sizeof(T), q.dev_out, q.ldc * sizeof(T), q.cnt * sizeof(T), n_out,
+                         nthreads, d.produced[q.slot]);
+        }
+        if (stats_out) {
+            SNPMI_HIP(hipStreamWaitEvent(d.copy, d.produced[q.slot], 0));
+            SNPMI_HIP(hipMemcpyAsync(stats + 2 * q.c0, q.st_dev, q.cnt * 2 * sizeof(T), hipMemcpyDeviceToHost, d.copy));
+            SNPMI_HIP(hipStreamSynchronize(d.copy));
+        }
+    };
     for (uint64_t c0 = 0, ci = 0; c0 < m_out; c0 += C, ci++) {
         const uint64_t cnt = std::min(C, m_out - c0);
-        const uint8_t* packed = stage_chunk(d, m, sid_idx, c0, cnt, p, nthreads, (int)(ci & 1));
+        const int slot = (int)(ci & 1);
+        const uint8_t* packed = stage_chunk(d, m, sid_idx, c0, cnt, p, nthreads, slot);
         T* lut = (T*)d.get(Device::S_LUT, cnt * 4 * sizeof(T));
-        T* st_dev = (T*)d.get(Device::S_STATS, cnt * 2 * sizeof(T));
+        T* st_dev = (T*)d.get(slot ? Device::S_STATS_B : Device::S_STATS, cnt * 2 * sizeof(T));
         if (std_kind != SNPMI_STD_NONE && use_stats)
             SNPMI_HIP(hipMemcpyAsync(st_dev, stats + 2 * c0, cnt * 2 * sizeof(T), hipMemcpyHostToDevice, d.stream));
         launch_snp_stats(packed, p.pitch_out, n_out, cnt, count_a1, std_kind, a, b, use_stats, dt, st_dev, lut,
                          d.stream);
+        Pending q;
+        q.c0 = c0;
+        q.cnt = cnt;
+        q.slot = slot;
+        q.st_dev = st_dev;
+        q.valid = true;
         if (n_out > 0) {
+            const Device::Slot os = slot ? Device::S_OUT_B : Device::S_OUT;
             if (!order_c) {
-                T* dev_out = (T*)d.get(Device::S_OUT, cnt * ldF * sizeof(T));
-                launch_decode(packed, p.pitch_out, n_out, cnt, lut, dt, 0, dev_out, ldF, d.stream);
-                d2h_rows(d, out + c0 * n_out, n_out * sizeof(T), dev_out, ldF * sizeof(T), n_out * sizeof(T), cnt,
-                         nthreads);
+                q.dev_out = (T*)d.get(os, cnt * ldF * sizeof(T));
+                launch_decode(packed, p.pitch_out, n_out, cnt, lut, dt, 0, q.dev_out, ldF, d.stream);
             } else {
                 // rows padded to 16 B on the device (k_decode_c_reg vector stores), tight on the host
-                const uint64_t ldc = sizeof(T) < 4 ? cnt : round_up(cnt, 16 / sizeof(T));
-                T* dev_out = (T*)d.get(Device::S_OUT, ldc * n_out * sizeof(T));
-                launch_decode(packed, p.pitch_out, n_out, cnt, lut, dt, 1, dev_out, ldc, d.stream);
-                d2h_rows(d, out + c0, m_out * sizeof(T), dev_out, ldc * sizeof(T), cnt * sizeof(T), n_out, nthreads);
+                q.ldc = sizeof(T) < 4 ? cnt : round_up(cnt, 16 / sizeof(T));
+                q.dev_out = (T*)d.get(os, q.ldc * n_out * sizeof(T));
+                launch_decode(packed, p.pitch_out, n_out, cnt, lut, dt, 1, q.dev_out, q.ldc, d.stream);
             }
         }
-        if (std_kind != SNPMI_STD_NONE && !use_stats)
-            SNPMI_HIP(hipMemcpyAsync(stats + 2 * c0, st_dev, cnt * 2 * sizeof(T), hipMemcpyDeviceToHost, d.stream));
-        SNPMI_HIP(hipStreamSynchronize(d.stream));
+        chunk_done(d, slot);
+        SNPMI_HIP(hipEventRecord(d.produced[slot], d.stream));
+        if (pending.valid) drain(pending);
+        pending = q;
     }
+    if (pending.valid) drain(pending);
+    SNPMI_HIP(hipStreamSynchronize(d.stream));
+    SNPMI_HIP(hipStreamSynchronize(d.copy));
 }
 
 // ====================================================================== BED write (to_bed body)
@@ -682,8 +740,10 @@ static bool grm_stream_bed(Device& d, bool first, const char* path, uint64_t n_i
         wrote = true;
         if (has_stats && !use_stats)
             SNPMI_HIP(hipMemcpyAsync(st_host + 2 * c0, st_dev, cnt * 2 * sizeof(T), hipMemcpyDeviceToHost, d.stream));
+        chunk_done(d, (int)(ci & 1));
     }
     SNPMI_HIP(hipStreamSynchronize(d.stream));
+    SNPMI_HIP(hipStreamSynchronize(d.copy));
     if (has_stats && !use_stats) std::memcpy(stats, st_host, m_out * 2 * sizeof(T));
     if (n_out == 0 && std_kind != SNPMI_STD_NONE && !use_stats) {
         for (uint64_t j = 0; j < m_out; j++) stats[2 * j] = stats[2 * j + 1] = (T)NAN;
@@ -734,19 +794,46 @@ static void* session_tiles(Device& d) {
     return d.get(Device::S_SESSION, n_tiles_upper(g_session.n) * kTile * kTile * dtype_size(g_session.dtype));
 }
 
+// supertile block order of the dense fp16x2 SYRK, kept on the device per (nb, xcd); built once
+// (blocking copy from a local vector), callers hold g_call_mutex
+static const uint32_t* dense_order(Device& d, uint64_t nb, bool xcd) {
+    if (d.order_nb[xcd] != nb || !d.order_tab[xcd]) {
+        std::vector<uint32_t> tab;
+        supertile_order(nb, xcd, tab);
+        if (d.order_tab[xcd]) SNPMI_HIP(hipFree(d.order_tab[xcd]));
+        d.order_tab[xcd] = nullptr;
+        d.order_nb[xcd] = 0;
+        if (hipMalloc(&d.order_tab[xcd], tab.size() * sizeof(uint32_t)) != hipSuccess) {
+            (void)hipGetLastError();
+            throw Error(SNPMI_E_NOMEM, "hipMalloc of the block order table failed");
+        }
+        SNPMI_HIP(hipMemcpy(d.order_tab[xcd], tab.data(), tab.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+        d.order_nb[xcd] = nb;
+    }
+    return d.order_tab[xcd];
+}
+
 // dense GRM operand on the device: f32 with n >= 4096 and the default variant takes the fp16x2
-// split kernel (falls back to the f32-MFMA k_syrk256d on the device-side range flag)
+// split kernel in SNP chunks of bounded stage-image scratch (falls back to the f32-MFMA
+// k_syrk256d on the device-side range flag, or when the scratch cannot be allocated)
 static void syrk_dense_auto(Device& d, const void* Z, uint64_t ldz, uint64_t n, uint64_t m, int dt, void* tiles,
                             int accumulate) {
-    if (dt == SNPMI_DT_F32 && (g_variant_syrk == 0 || g_variant_syrk == 44 || (g_variant_syrk >= 47 && g_variant_syrk <= 49)) &&
-        n >= 4096 && m > 0 && ldz % 256 == 0) {
-        const uint64_t nb = ldz / 256, g = nb * (nb + 1) / 2;
-        // fp16 planes (4 B per value) or the stage images (round_up(m, 32) x nb x 2 x 9216 B)
-        const uint64_t scratch = std::max(4 * ldz * m, round_up(m, (uint64_t)32) / 16 * nb * 2 * 9216);
-        uint16_t* planes = (uint16_t*)d.get(Device::S_H2, scratch + 256 + 4 * g);
-        uint32_t* flag = (uint32_t*)((uint8_t*)planes + scratch);
-        launch_syrk_dense_h2((const float*)Z, ldz, n, m, planes, flag, flag + 64, (float*)tiles, accumulate, d.stream);
-        return;
+    if (dt == SNPMI_DT_F32 && g_variant_syrk == 0 && n >= 4096 && m > 0 && ldz % 256 == 0) {
+        const uint64_t nb = ldz / 256;
+        const uint64_t scratch = round_up(dense_h2_scratch_bytes(n, m), 256);
+        uint16_t* img = nullptr;
+        try {
+            img = (uint16_t*)d.get(Device::S_H2, scratch + 256);
+        } catch (const Error& e) {
+            if (e.code != SNPMI_E_NOMEM) throw;
+            img = nullptr;  // HBM is full: the f32-MFMA kernel needs no scratch
+        }
+        if (img) {
+            uint32_t* flag = (uint32_t*)((uint8_t*)img + scratch);
+            launch_syrk_dense_h2((const float*)Z, ldz, n, m, img, flag, dense_order(d, nb, false), (float*)tiles,
+                                 accumulate, d.stream);
+            return;
+        }
     }
     launch_syrk_dense(Z, ldz, n, m, dt, tiles, accumulate, d.stream);
 }
@@ -922,8 +1009,19 @@ int snpmi_set_kernel_variant(const char* kernel, int variant) {
     return guarded([&] {
         SNPMI_REQUIRE(kernel != nullptr, SNPMI_E_ARG, "kernel name is NULL");
         if (std::strcmp(kernel, "decode") == 0) g_variant_decode = variant;
-        else if (std::strcmp(kernel, "syrk") == 0) g_variant_syrk = variant;
+        else if (std::strcmp(kernel, "syrk") == 0) {
+#ifndef SNPMI_UBENCH
+            // the product library ships the default chain and the kernels it falls back to:
+            // 36 = the bf16x3 kernel alone (fp16x2 range fallback), 20 = the f32-MFMA kernels
+            // (dense-operand range fallback), 5 = the 128x128 small-N kernels; every other
+            // variant is an A/B ablation of the ubench build (make -C pysnptools_amd/csrc ubench)
+            SNPMI_REQUIRE(variant == 0 || variant == 5 || variant == 20 || variant == 36, SNPMI_E_ARG,
+                          "syrk variant " + std::to_string(variant) + " exists only in the ubench build");
+#endif
+            g_variant_syrk = variant;
+        }
         else if (std::strcmp(kernel, "syrk_split") == 0) g_variant_syrk_split = variant;
+        else if (std::strcmp(kernel, "dense_chunk") == 0) g_dense_chunk = std::max(variant, 0);
         else throw Error(SNPMI_E_ARG, std::string("unknown kernel ") + kernel);
     });
 }
@@ -974,6 +1072,7 @@ SNPMI_BED_WRITE(i8, int8_t)
 int snpmi_dev_encode(const void* val, int dtype, int order_c, uint64_t ld, uint64_t n_iid, uint64_t n_sid,
                      int count_a1, uint8_t* packed, uint64_t pitch, uint64_t* bad_values) {
     return guarded([&] {
+        std::lock_guard<std::recursive_mutex> lk(g_call_mutex);  // shared scratch slots
         SNPMI_REQUIRE(pitch % 64 == 0 && pitch >= ceil_div(n_iid, 4), SNPMI_E_ARG, "pitch must be a multiple of 64 >= ceil(n/4)");
         SNPMI_REQUIRE(order_c || ld % 16 == 0, SNPMI_E_ARG, "F-order ld must be a multiple of 16");
         SNPMI_REQUIRE(order_c ? ld >= n_sid : ld >= n_iid, SNPMI_E_ARG, "ld too small");
@@ -1189,7 +1288,39 @@ int snpmi_dev_memcpy_d2d(void* dst, const void* src, uint64_t bytes) {
     });
 }
 int snpmi_stream_sync(void) {
-    return guarded([&] { SNPMI_HIP(hipStreamSynchronize(stream())); });
+    return guarded([&] {
+        Device& d = device();
+        SNPMI_HIP(hipStreamSynchronize(d.stream));
+        SNPMI_HIP(hipStreamSynchronize(d.copy));
+    });
+}
+
+// ---------------------------------------------------------------------- copy stream (streaming API)
+static hipStream_t pick_stream(Device& d, int on_copy) { return on_copy ? d.copy : d.stream; }
+
+int snpmi_memcpy_async(void* dst, const void* src, uint64_t bytes, int kind, int on_copy) {
+    return guarded([&] {
+        SNPMI_REQUIRE(kind >= 0 && kind <= 2, SNPMI_E_ARG, "kind must be 0 (H2D), 1 (D2H) or 2 (D2D)");
+        Device& d = device();
+        const hipMemcpyKind k = kind == 0 ? hipMemcpyHostToDevice : kind == 1 ? hipMemcpyDeviceToHost
+                                                                              : hipMemcpyDeviceToDevice;
+        if (bytes) SNPMI_HIP(hipMemcpyAsync(dst, src, bytes, k, pick_stream(d, on_copy)));
+    });
+}
+int snpmi_event_record_on(void* ev, int on_copy) {
+    return guarded([&] {
+        Device& d = device();
+        SNPMI_HIP(hipEventRecord((hipEvent_t)ev, pick_stream(d, on_copy)));
+    });
+}
+int snpmi_stream_wait_event(void* ev, int on_copy) {
+    return guarded([&] {
+        Device& d = device();
+        SNPMI_HIP(hipStreamWaitEvent(pick_stream(d, on_copy), (hipEvent_t)ev, 0));
+    });
+}
+int snpmi_event_sync(void* ev) {
+    return guarded([&] { SNPMI_HIP(hipEventSynchronize((hipEvent_t)ev)); });
 }
 int snpmi_event_create(void** ev) {
     return guarded([&] {
@@ -1213,6 +1344,7 @@ int snpmi_event_elapsed_ms(void* start, void* stop, float* ms) {
 int snpmi_dev_synth_bed(uint8_t* packed, uint64_t pitch, uint64_t n_iid, uint64_t sid0, uint64_t n_sid, uint64_t seed,
                         double miss_rate, const double* maf_x, const double* maf_cdf, int n_pts) {
     return guarded([&] {
+        std::lock_guard<std::recursive_mutex> lk(g_call_mutex);  // shared scratch slots
         SNPMI_REQUIRE(pitch % 4 == 0 && pitch >= ceil_div(n_iid, 4), SNPMI_E_ARG, "bad pitch");
         SNPMI_REQUIRE(n_pts > 0 && n_pts <= 1024, SNPMI_E_ARG, "bad MAF table");
         Device& d = device();
@@ -1257,6 +1389,7 @@ int snpmi_dev_decode_standardize(const uint8_t* packed, uint64_t pitch, uint64_t
 int snpmi_dev_repack(const uint8_t* src, uint64_t src_pitch, uint64_t n_src, const uint64_t* idx, uint64_t n_out,
                      uint64_t n_sid, uint8_t* dst, uint64_t dst_pitch) {
     return guarded([&] {
+        std::lock_guard<std::recursive_mutex> lk(g_call_mutex);  // shared scratch slots
         SNPMI_REQUIRE(dst_pitch % 64 == 0 && dst_pitch >= ceil_div(n_out, 4), SNPMI_E_ARG, "bad dst pitch");
         Device& d = device();
         uint32_t* idx32 = (uint32_t*)d.get(Device::S_IDX32, std::max<uint64_t>(n_out, 1) * 4);
@@ -1268,6 +1401,7 @@ int snpmi_dev_repack(const uint8_t* src, uint64_t src_pitch, uint64_t n_src, con
 int snpmi_dev_syrk_packed(const uint8_t* packed, uint64_t pitch, uint64_t n_iid, uint64_t n_sid, const void* lut,
                           int dtype, void* K_tiles, int accumulate) {
     return guarded([&] {
+        std::lock_guard<std::recursive_mutex> lk(g_call_mutex);  // shared scratch slots
         SNPMI_REQUIRE(dtype == SNPMI_DT_F32 || dtype == SNPMI_DT_F64, SNPMI_E_ARG, "GRM dtype must be f32/f64");
         SNPMI_REQUIRE(pitch % 64 == 0 && pitch >= ceil_div(n_iid, 4), SNPMI_E_ARG, "pitch must be snpmi_packed_pitch");
         syrk_packed_auto(device(), packed, pitch, n_iid, n_sid, lut, dtype, K_tiles, accumulate);
@@ -1326,6 +1460,7 @@ int snpmi_grm_part_bed_f32(const char* path, uint64_t n_iid, uint64_t n_sid, int
 int snpmi_dev_syrk_packed_part(const uint8_t* packed, uint64_t pitch, uint64_t n_iid, uint64_t n_sid, const void* lut,
                                int part_rank, int part_world, void* blocks, int accumulate) {
     return guarded([&] {
+        std::lock_guard<std::recursive_mutex> lk(g_call_mutex);  // shared scratch slots
         SNPMI_REQUIRE(part_world >= 1 && part_rank >= 0 && part_rank < part_world, SNPMI_E_ARG, "bad partition");
         SNPMI_REQUIRE(pitch % 64 == 0 && pitch >= ceil_div(n_iid, 4), SNPMI_E_ARG, "pitch must be snpmi_packed_pitch");
         syrk_packed_part_auto(device(), packed, pitch, n_iid, n_sid, (const float*)lut, part_rank, part_world, blocks,
@@ -1336,6 +1471,7 @@ int snpmi_dev_syrk_packed_part(const uint8_t* packed, uint64_t pitch, uint64_t n
 int snpmi_dev_syrk_dense(const void* Z, uint64_t ldz, uint64_t n_iid, uint64_t n_sid, int dtype, void* K_tiles,
                          int accumulate) {
     return guarded([&] {
+        std::lock_guard<std::recursive_mutex> lk(g_call_mutex);  // shared scratch slots
         SNPMI_REQUIRE(dtype == SNPMI_DT_F32 || dtype == SNPMI_DT_F64, SNPMI_E_ARG, "GRM dtype must be f32/f64");
         syrk_dense_auto(device(), Z, ldz, n_iid, n_sid, dtype, K_tiles, accumulate);
     });
@@ -1350,6 +1486,7 @@ int snpmi_dev_grm_extract(const void* K_tiles, uint64_t n_iid, int dtype, const 
 
 int snpmi_dev_grm_trace(const void* K_tiles, uint64_t n_iid, int dtype, double* trace) {
     return guarded([&] {
+        std::lock_guard<std::recursive_mutex> lk(g_call_mutex);  // shared scratch slots
         Device& d = device();
         double* tr = (double*)d.get(Device::S_RED, 64);
         launch_grm_trace(K_tiles, n_iid, dtype, tr, d.stream);

@@ -3,7 +3,8 @@
 // ncclAllReduce(sum) of the tile buffer produces K on every rank.  In the K-partitioned
 // mode (cfg5) each rank uploads 1/p of a packed SNP block and ncclAllGather rebuilds the
 // whole block on every rank (packed codes are 16x smaller than the f32 values).  The unique id is
-// exchanged by the caller (bench.py uses torch.distributed's gloo store for that).
+// exchanged by the caller (bench.py: rank 0 writes it to an O_EXCL node-local file named by
+// the launcher; the package never imports torch, whose own HIP runtime would load beside ours).
 #include <rccl/rccl.h>
 
 #include "snpmi_internal.hpp"
@@ -76,6 +77,14 @@ int snpmi_rccl_host_allreduce_f64(double* values, uint64_t count, int op) {
 int snpmi_rccl_barrier(void) {
     double one = 1.0;
     return snpmi_rccl_host_allreduce_f64(&one, 1, 0);
+}
+
+int snpmi_rccl_comm_count(int* count) {
+    return guarded([&] {
+        SNPMI_REQUIRE(g_comm != nullptr, SNPMI_E_ARG, "RCCL communicator not initialised");
+        SNPMI_REQUIRE(count != nullptr, SNPMI_E_ARG, "count is NULL");
+        SNPMI_NCCL(ncclCommCount(g_comm, count));
+    });
 }
 
 int snpmi_rccl_destroy(void) {

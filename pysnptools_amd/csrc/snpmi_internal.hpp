@@ -6,6 +6,7 @@
 #include <cstring>
 #include <stdexcept>
 #include <string>
+#include <vector>
 
 #include "../../include/snpmi.h"
 
@@ -61,14 +62,25 @@ inline size_t dtype_size(int dt) { return dt == SNPMI_DT_F64 ? 8 : dt == SNPMI_D
 // ------------------------------------------------------------------ per-device state
 struct Device {
     int id = -1;
-    hipStream_t stream = nullptr;
+    hipStream_t stream = nullptr;  // compute: every kernel
+    hipStream_t copy = nullptr;    // DMA: host<->device copies of streamed chunks, overlapping compute
     int cu_count = 0;
     // grow-only scratch slots
     enum Slot { S_PACKED, S_PACKED2, S_IDX, S_IDX2, S_LUT, S_STATS, S_OUT, S_TILES, S_K, S_DENSE,
-                S_DENSE2, S_RED, S_SESSION, S_PACKED_B, S_ZBLK, S_IDX32, S_LUT3, S_H2, S_NUM };
+                S_DENSE2, S_RED, S_SESSION, S_PACKED_B, S_ZBLK, S_IDX32, S_LUT3, S_H2, S_OUT_B, S_STATS_B,
+                S_NUM };
     void* buf[S_NUM] = {};
-    hipEvent_t staged[2] = {};  // recorded after the H2D that last read pinned slot 0 / 1
+    // chunk pipeline events (slot = chunk parity), all on-device ordering, no host spin:
+    hipEvent_t staged[2] = {};    // copy stream: H2D of pinned slot done (host may refill it)
+    hipEvent_t consumed[2] = {};  // compute stream: kernels done reading device packed slot
+    hipEvent_t produced[2] = {};  // compute stream: output slot written (its D2H may start)
+    hipEvent_t bounce[2] = {};    // copy stream: D2H into pinned bounce slot done
+    hipEvent_t fence = nullptr;   // compute stream: "all work so far", for a copy to wait on
     size_t cap[S_NUM] = {};
+    // upper-triangle 256-iid block order tables of the dense fp16x2 SYRK, built once per
+    // (nb, xcd) and kept on this device (guarded by the device's own mutex)
+    uint32_t* order_tab[2] = {};
+    uint64_t order_nb[2] = {};
     void* get(Slot s, size_t bytes);
     void release();
 };
@@ -83,6 +95,7 @@ void release_pinned();
 // ------------------------------------------------------------------ kernel launchers (kernels.hip)
 extern int g_variant_decode;
 extern int g_variant_syrk;
+extern int g_dense_chunk;
 void launch_snp_stats(const uint8_t* packed, uint64_t pitch, uint64_t n_iid, uint64_t n_sid, int count_a1,
                       int std_kind, double a, double b, int use_stats, int dtype, void* stats, void* lut,
                       hipStream_t st);
@@ -134,11 +147,15 @@ struct H2Lut {
     const uint32_t* flag;
 };
 void launch_lut_h2(const float* lut, uint64_t m, uint32_t* lut2, uint32_t* flag, hipStream_t st);
-// dense f32 operand (ld = round_up(n, 256), n >= 4096): split into fp16 planes (scratch of
-// 4 * ldz * m bytes) + k_syrk_h2<DENSE> in supertile block order (order: scratch of one u32
-// per 256-iid block), the f32-MFMA k_syrk256d gated on the range flag
-void launch_syrk_dense_h2(const float* Z, uint64_t ldz, uint64_t n, uint64_t m, uint16_t* planes, uint32_t* flag,
-                          uint32_t* order, float* tiles, int accumulate, hipStream_t st);
+// dense f32 operand (ld = round_up(n, 256), n >= 4096) on the fp16 MFMA pipe: range check, then
+// per SNP chunk (dense_h2_chunk_snps) LDS stage images (img: dense_h2_scratch_bytes) + the
+// fp16x2 SYRK in supertile block order (order: device table of supertile_order), the f32-MFMA
+// k_syrk256d gated on the range flag
+void supertile_order(uint64_t nb, bool xcd, std::vector<uint32_t>& tab);
+uint64_t dense_h2_chunk_snps(uint64_t n);
+uint64_t dense_h2_scratch_bytes(uint64_t n, uint64_t m);
+void launch_syrk_dense_h2(const float* Z, uint64_t ldz, uint64_t n, uint64_t m, uint16_t* img, uint32_t* flag,
+                          const uint32_t* order, float* tiles, int accumulate, hipStream_t st);
 void launch_syrk_packed_bf3(const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m, const uint32_t* lut3,
                             float* tiles, int accumulate, hipStream_t st, const H2Lut* h2 = nullptr);
 void launch_syrk_packed_bf3_split(const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m, const uint32_t* lut3,

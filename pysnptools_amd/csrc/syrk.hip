@@ -1385,7 +1385,7 @@ struct PRegs {
     double l[4];
 };
 
-__device__ __forceinline__ void load_dense(const double* __restrict__ Z, uint64_t ldz, uint64_t kdim, uint64_t k0,
+[[maybe_unused]] __device__ __forceinline__ void load_dense(const double* __restrict__ Z, uint64_t ldz, uint64_t kdim, uint64_t k0,
                                            uint64_t i0, uint64_t j0, double2 (&ra)[4], double2 (&rb)[4]) {
     const int t = threadIdx.x;
 #pragma unroll
@@ -1405,7 +1405,7 @@ __device__ __forceinline__ void load_dense(const double* __restrict__ Z, uint64_
     }
 }
 
-__device__ __forceinline__ void store_dense(double* As, double* Bs, const double2 (&ra)[4], const double2 (&rb)[4]) {
+[[maybe_unused]] __device__ __forceinline__ void store_dense(double* As, double* Bs, const double2 (&ra)[4], const double2 (&rb)[4]) {
     const int t = threadIdx.x;
 #pragma unroll
     for (int q = 0; q < 4; q++) {
@@ -1689,15 +1689,18 @@ void launch_syrk_packed(const uint8_t* packed, uint64_t pitch, uint64_t n, uint6
         // Kernel choice (tools/ubench.py syrk, MI355X): 256x256 / 8 waves reaches 129 TFLOP/s at
         // N=50k (82%) vs 118 for 128x128 / 4 waves; below ~4k iids the 256 tiles leave CUs idle.
         const uint64_t nb = ceil_div(n, 256);
+        // Reached for f32 only when the product path is forced off the fp16x2/bf16x3 kernels
+        // (variant 20 below N = 4096) or by the ubench build's ablations.
         int v = g_variant_syrk;
-        if (v == 0) v = n >= 4096 ? 4 : 5;
+        if (v == 0 || v == 20) v = n >= 4096 ? 4 : 5;
         switch (v) {
-            case 1: f32k::k_syrk<true, 32, 2><<<(unsigned)nt, 256, 0, st>>>(packed, pitch, m, L, Tt, accumulate); break;
-            case 2: f32k::k_syrk_il<4><<<(unsigned)nt, 256, 0, st>>>(packed, pitch, m, L, Tt, accumulate); break;
-            case 3: f32k::k_syrk_il<3><<<(unsigned)nt, 256, 0, st>>>(packed, pitch, m, L, Tt, accumulate); break;
             case 4:
                 f32w::k_syrk256<1><<<(unsigned)(nb * (nb + 1) / 2), 512, 0, st>>>(packed, pitch, n, m, L, Tt, accumulate);
                 break;
+#ifdef SNPMI_UBENCH
+            case 1: f32k::k_syrk<true, 32, 2><<<(unsigned)nt, 256, 0, st>>>(packed, pitch, m, L, Tt, accumulate); break;
+            case 2: f32k::k_syrk_il<4><<<(unsigned)nt, 256, 0, st>>>(packed, pitch, m, L, Tt, accumulate); break;
+            case 3: f32k::k_syrk_il<3><<<(unsigned)nt, 256, 0, st>>>(packed, pitch, m, L, Tt, accumulate); break;
             case 6:
                 f32w::k_syrk256<1, false, true>
                     <<<(unsigned)(nb * (nb + 1) / 2), 512, 0, st>>>(packed, pitch, n, m, L, Tt, accumulate);
@@ -1712,6 +1715,7 @@ void launch_syrk_packed(const uint8_t* packed, uint64_t pitch, uint64_t n, uint6
             case 13: f32k::k_syrk_il<4, 2><<<(unsigned)nt, 256, 0, st>>>(packed, pitch, m, L, Tt, accumulate); break;
             case 14: f32k::k_syrk_il<4, 3><<<(unsigned)nt, 256, 0, st>>>(packed, pitch, m, L, Tt, accumulate); break;
             case 15: f32k::k_syrk_il<4, 4><<<(unsigned)nt, 256, 0, st>>>(packed, pitch, m, L, Tt, accumulate); break;
+#endif
             default: f32k::k_syrk<true, 16, 4><<<(unsigned)nt, 256, 0, st>>>(packed, pitch, m, L, Tt, accumulate);
         }
     }
@@ -1722,12 +1726,14 @@ void launch_syrk_packed(const uint8_t* packed, uint64_t pitch, uint64_t n, uint6
         // 2 = select interleaved with the MFMAs 56.1, 0 = that + bank-rotated LDS stores 60.5
         // (77% of 78.6); 10 = MFMA-only ablation 71.5.
         switch (g_variant_syrk) {
+#ifdef SNPMI_UBENCH
             case 1: f64k::k_syrk<true, 1><<<(unsigned)nt, 256, 0, st>>>(packed, pitch, m, L, Tt, accumulate); break;
             case 2: f64k::k_syrk<true, 2><<<(unsigned)nt, 256, 0, st>>>(packed, pitch, m, L, Tt, accumulate); break;
             case 3: f64k::k_syrk<true, 3><<<(unsigned)nt, 256, 0, st>>>(packed, pitch, m, L, Tt, accumulate); break;
             case 5: f64k::k_syrk<true, 0><<<(unsigned)nt, 256, 0, st>>>(packed, pitch, m, L, Tt, accumulate); break;
             case 10: f64k::k_syrk<true, 10><<<(unsigned)nt, 256, 0, st>>>(packed, pitch, m, L, Tt, accumulate); break;
             case 11: f64k::k_syrk<true, 11><<<(unsigned)nt, 256, 0, st>>>(packed, pitch, m, L, Tt, accumulate); break;
+#endif
             default: f64k::k_syrk<true, 4><<<(unsigned)nt, 256, 0, st>>>(packed, pitch, m, L, Tt, accumulate);
         }
     }
@@ -1770,39 +1776,55 @@ void launch_lut_h2(const float* lut, uint64_t m, uint32_t* lut2, uint32_t* flag,
 
 // Upper-triangle 256-iid blocks in supertile order: 16x16-block supertiles (I <= J) in
 // triangular order, blocks (bi <= bj) inside each; entry = bi | bj << 16.  The dense fp16x2
-// SYRK streams 4 B per value per panel, so the ~256 blocks in flight must share panels: in the
-// plain column order they touch ~nb A panels at once, in this order 32.
-static const std::vector<uint32_t>& supertile_order(uint64_t nb, bool xcd = false) {
-    static std::vector<uint32_t> tabs[2];
-    static uint64_t tab_nb[2] = {0, 0};
-    std::vector<uint32_t>& tab = tabs[xcd];
-    if (tab_nb[xcd] != nb) {
-        tab.clear();
-        const uint64_t ns = ceil_div(nb, 16);
-        for (uint64_t J = 0; J < ns; J++)
-            for (uint64_t I = 0; I <= J; I++) {
-                // xcd: workgroup w runs on XCD w % 8, so deal each supertile's blocks out of 8
-                // 4 (bi) x 8 (bj) sub-tiles round-robin -- one XCD's ~32 blocks then touch 12
-                // panels in its own L2 instead of 18
-                std::vector<uint32_t> sub[8];
-                for (uint64_t bj = 16 * J; bj < std::min(16 * J + 16, nb); bj++)
-                    for (uint64_t bi = 16 * I; bi < std::min(16 * I + 16, bj + 1); bi++)
-                        sub[xcd ? ((bi - 16 * I) / 4 + 4 * ((bj - 16 * J) / 8)) : 0].push_back((uint32_t)(bi | (bj << 16)));
-                size_t pos[8] = {0, 0, 0, 0, 0, 0, 0, 0}, left = 0;
-                for (int x = 0; x < 8; x++) left += sub[x].size();
-                for (int x = 0; left > 0; x = (x + 1) & 7)
-                    if (pos[x] < sub[x].size()) {
-                        tab.push_back(sub[x][pos[x]++]);
-                        left--;
-                    }
-            }
-        tab_nb[xcd] = nb;
-    }
-    return tab;
+// SYRK streams 4.6 B per value per panel, so the ~256 blocks in flight must share panels: in the
+// plain column order they touch ~nb A panels at once, in this order 32.  xcd: workgroup w
+// runs on XCD w % 8, so each supertile's blocks are dealt out of 8 4 (bi) x 8 (bj) sub-tiles
+// round-robin -- measured within noise of the plain order (ubench variant 45), so the product
+// uses the plain order.  Pure host function; the caller keeps the table on its device.
+void supertile_order(uint64_t nb, bool xcd, std::vector<uint32_t>& tab) {
+    tab.clear();
+    const uint64_t ns = ceil_div(nb, 16);
+    for (uint64_t J = 0; J < ns; J++)
+        for (uint64_t I = 0; I <= J; I++) {
+            std::vector<uint32_t> sub[8];
+            for (uint64_t bj = 16 * J; bj < std::min(16 * J + 16, nb); bj++)
+                for (uint64_t bi = 16 * I; bi < std::min(16 * I + 16, bj + 1); bi++)
+                    sub[xcd ? ((bi - 16 * I) / 4 + 4 * ((bj - 16 * J) / 8)) : 0].push_back((uint32_t)(bi | (bj << 16)));
+            size_t pos[8] = {0, 0, 0, 0, 0, 0, 0, 0}, left = 0;
+            for (int x = 0; x < 8; x++) left += sub[x].size();
+            for (int x = 0; left > 0; x = (x + 1) & 7)
+                if (pos[x] < sub[x].size()) {
+                    tab.push_back(sub[x][pos[x]++]);
+                    left--;
+                }
+        }
 }
 
-void launch_syrk_dense_h2(const float* Z, uint64_t ldz, uint64_t n, uint64_t m, uint16_t* planes, uint32_t* flag,
-                          uint32_t* order, float* tiles, int accumulate, hipStream_t st) {
+int g_dense_chunk = 0;  // tuning / test hook (snpmi_set_kernel_variant "dense_chunk"): force chunk SNPs
+
+uint64_t dense_h2_chunk_snps(uint64_t n) {
+    if (g_dense_chunk > 0) return round_up((uint64_t)g_dense_chunk, 32);
+    // stage-image scratch per 32-SNP stage: nb blocks x 2 steps x 2 planes x 9216 B; chunks of
+    // <= 4 GiB of images (>= 1024 SNPs), and < 2^20 SNPs (k_image_h2's grid.y = 16-SNP steps)
+    const uint64_t nb = ceil_div(n, 256), per32 = nb * 2 * 2 * 9216;
+    uint64_t c = (4ull << 30) / per32 * 32;
+    c = std::max<uint64_t>(c, 1024);
+    return std::min<uint64_t>(c, (1ull << 19));
+}
+
+uint64_t dense_h2_scratch_bytes(uint64_t n, uint64_t m) {
+    const uint64_t nb = ceil_div(n, 256), c = std::min(round_up(std::max<uint64_t>(m, 1), 32), dense_h2_chunk_snps(n));
+    return round_up(c, 32) / 16 * nb * 2 * 9216;
+}
+
+// Dense f32 operand Z ([sid][ldz], ld = round_up(n, 256), n >= 4096) -> K tiles on the fp16 MFMA
+// pipe: the range check (k_split_h2<false>, column max -> flag) runs over the whole block, then
+// per SNP chunk k_image_h2 rewrites the chunk once as stage images (the exact LDS rows of the
+// packed loader, 4.6 B per value) that k_syrk_h2<MODE 6> moves into LDS by DMA; k_syrk256d (the
+// f32 MFMA) computes the block instead when the flag is raised.  order = supertile_order table
+// on the device; img = dense_h2_scratch_bytes(n, m).
+void launch_syrk_dense_h2(const float* Z, uint64_t ldz, uint64_t n, uint64_t m, uint16_t* img, uint32_t* flag,
+                          const uint32_t* order, float* tiles, int accumulate, hipStream_t st) {
     const uint64_t nb = ceil_div(n, 256), g = nb * (nb + 1) / 2;
     if (g == 0) return;
     SNPMI_REQUIRE(g < (1ull << 31) && m < (1ull << 31) && nb < 65536, SNPMI_E_ARG,
@@ -1813,42 +1835,19 @@ void launch_syrk_dense_h2(const float* Z, uint64_t ldz, uint64_t n, uint64_t m, 
         return;
     }
     SNPMI_HIP(hipMemsetAsync(flag, 0, sizeof(uint32_t), st));
-    // Default (0 / 44): the block is rewritten once as stage images (k_image_h2, 4.6 B per value,
-    // ~1 ms per 10k x 50k) that k_syrk_h2<MODE 6> moves into LDS by DMA -- measured N=50k, 10k
-    // SNPs: 60.5 ms in one launch vs 3 x 50 ms for MODE 4's VGPR-staged loader
-    // (profiles/r01k/).  Variant 0 deals blocks to XCDs by 4x8 sub-tile: within noise of the
-    // plain supertile order, 44 (59.8 / 61.2 vs 60.4 / 60.9 ms in two runs).  A 4-slot, 16-SNP-step DMA ring (3 steps in flight) was tried:
-    // with dwordx3 pieces the LDS image came out wrong (NaN), with dword pieces it was correct
-    // but 272 ms (18 DMA instructions per wave per step).  Over 2^20 SNPs (grid.y limit) the chunked MODE 4 path below runs.
-    const uint64_t steps = 2 * ceil_div(m, (uint64_t)32);
-    if ((g_variant_syrk == 0 || g_variant_syrk == 44) && steps < 65536) {
-        f32w::k_split_h2<false><<<(unsigned)m, 256, 0, st>>>(Z, ldz, n, nullptr, flag);
-        SNPMI_HIP(hipGetLastError());
-        f32w::k_image_h2<<<dim3((unsigned)nb, (unsigned)steps), 256, 0, st>>>(Z, ldz, n, m, (short*)planes);
-        SNPMI_HIP(hipGetLastError());
-        const std::vector<uint32_t>& tab = supertile_order(nb, g_variant_syrk == 0);
-        SNPMI_HIP(hipMemcpyAsync(order, tab.data(), g * sizeof(uint32_t), hipMemcpyHostToDevice, st));
-        f32w::k_syrk_h2<false, 6, true><<<(unsigned)g, 512, 0, st>>>((const uint8_t*)planes, ldz, n, m, order, flag,
-                                                                      tiles, accumulate);
-        SNPMI_HIP(hipGetLastError());
-        f32w::k_syrk256d<><<<(unsigned)g, 512, 0, st>>>(Z, ldz, n, m, tiles, accumulate, 0, 1, flag);
-        SNPMI_HIP(hipGetLastError());
-        return;
-    }
-    f32w::k_split_h2<<<(unsigned)m, 256, 0, st>>>(Z, ldz, n, planes, flag);
+    // Measured N=50k, 10k SNPs: 60.5 ms in one launch vs 3 x 50 ms for the VGPR-staged
+    // dense loader (removed: it spilled 160 B/lane) (profiles/r01k/).  A 4-slot, 16-SNP-step
+    // DMA ring (3 steps in flight) was tried: with dwordx3 pieces the LDS image came out wrong
+    // (NaN), with dword pieces it was correct but 272 ms (18 DMA instructions per wave per step).
+    f32w::k_split_h2<false><<<(unsigned)m, 256, 0, st>>>(Z, ldz, n, nullptr, flag);
     SNPMI_HIP(hipGetLastError());
-    const std::vector<uint32_t>& tab = supertile_order(nb);
-    SNPMI_HIP(hipMemcpyAsync(order, tab.data(), g * sizeof(uint32_t), hipMemcpyHostToDevice, st));
-    // SNP chunks per launch (one supertile's 32 panels at 4096 SNPs = 128 MB, within the 256 MB
-    // Infinity Cache).  Measured N=50k, 10k SNPs (profiles/r01j/ubench_syrk_dense_h2.jsonl):
-    // chunks of 2048 / 4096 / 8192 / all 146-149 ms, plain column block order 150-160 ms, the
-    // f32-MFMA k_syrk256d 185 ms, the packed fp16x2 kernel on the same block 45 ms -- the
-    // dense loader (64 B of planes per thread per k-step through VGPRs) is the limit, not reuse.
-    const uint64_t ch = g_variant_syrk == 47 ? 2048 : g_variant_syrk == 48 ? 8192 : g_variant_syrk == 49 ? m : 4096;
-    for (uint64_t c0 = 0; c0 < m; c0 += ch) {
-        f32w::k_syrk_h2<false, 4, true><<<(unsigned)g, 512, 0, st>>>((const uint8_t*)(planes + c0 * 2 * ldz), ldz, n,
-                                                                      std::min(ch, m - c0), order, flag, tiles,
-                                                                      accumulate || c0 > 0);
+    const uint64_t C = dense_h2_chunk_snps(n);
+    for (uint64_t c0 = 0; c0 < m; c0 += C) {
+        const uint64_t cnt = std::min(C, m - c0), steps = 2 * ceil_div(cnt, (uint64_t)32);
+        f32w::k_image_h2<<<dim3((unsigned)nb, (unsigned)steps), 256, 0, st>>>(Z + c0 * ldz, ldz, n, cnt, (short*)img);
+        SNPMI_HIP(hipGetLastError());
+        f32w::k_syrk_h2<false, 6, true><<<(unsigned)g, 512, 0, st>>>((const uint8_t*)img, ldz, n, cnt, order, flag,
+                                                                      tiles, accumulate || c0 > 0);
         SNPMI_HIP(hipGetLastError());
     }
     f32w::k_syrk256d<><<<(unsigned)g, 512, 0, st>>>(Z, ldz, n, m, tiles, accumulate, 0, 1, flag);
@@ -1880,11 +1879,13 @@ void launch_syrk_packed_bf3(const uint8_t* packed, uint64_t pitch, uint64_t n, u
         // prefetched after the barrier (42) 505, + pin (43) 551-564; 32-SNP + pin (46) 564;
         // bf16x3 (36) 300-313.
         switch (g_variant_syrk) {
+#ifdef SNPMI_UBENCH
             case 40: f32w::k_syrk_h2<false, 0><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles, accumulate); break;
             case 42: f32w::k_syrk_h2<false, 2><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles, accumulate); break;
             case 43: f32w::k_syrk_h2<false, 3><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles, accumulate); break;
             case 41: f32w::k_syrk_h2<false, 1><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles, accumulate); break;
             case 46: f32w::k_syrk_h2<false, 5><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles, accumulate); break;
+#endif
             default: f32w::k_syrk_h2<false, 4><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles, accumulate);
         }
         SNPMI_HIP(hipGetLastError());
@@ -1894,12 +1895,14 @@ void launch_syrk_packed_bf3(const uint8_t* packed, uint64_t pitch, uint64_t n, u
         return;
     }
     switch (g_variant_syrk) {
+#ifdef SNPMI_UBENCH
         case 30: f32w::k_syrk_bf3<><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, lut3, tiles, accumulate); break;
         case 31: f32w::k_syrk_bf3<false, true><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, lut3, tiles, accumulate); break;
         case 32: f32w::k_syrk_bf3<false, true, 1><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, lut3, tiles, accumulate); break;
         case 33: f32w::k_syrk_bf3<false, false, 1><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, lut3, tiles, accumulate); break;
         case 34: f32w::k_syrk_bf3<false, false, 2><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, lut3, tiles, accumulate); break;
         case 39: f32w::k_syrk_bf3<false, true, 9><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, lut3, tiles, accumulate); break;
+#endif
         default: f32w::k_syrk_bf3<false, false, 5><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, lut3, tiles, accumulate);
     }
     SNPMI_HIP(hipGetLastError());
@@ -1979,20 +1982,26 @@ void launch_syrk_dense(const void* Z, uint64_t ldz, uint64_t n, uint64_t m, int 
         const unsigned g = (unsigned)(nb * (nb + 1) / 2);
         const float* Zf = (const float*)Z;
         float* Tf = (float*)tiles;
+#ifdef SNPMI_UBENCH
         if (n >= 4096 && ldz >= nb * 256 && g_variant_syrk == 8)
             f32w::k_syrk256d<false, 32, 2><<<g, 512, 0, st>>>(Zf, ldz, n, m, Tf, accumulate);
         else if (n >= 4096 && ldz >= nb * 256 && g_variant_syrk == 9)
             f32w::k_syrk256d<false, 16, 3><<<g, 512, 0, st>>>(Zf, ldz, n, m, Tf, accumulate);
         else if (n >= 4096 && ldz >= nb * 256 && g_variant_syrk == 21)
             f32w::k_syrk256d<false, 16, 2, true><<<g, 512, 0, st>>>(Zf, ldz, n, m, Tf, accumulate);
-
-        else if (n >= 4096 && ldz >= nb * 256 && g_variant_syrk != 5)
+        else
+#endif
+        if (n >= 4096 && ldz >= nb * 256 && g_variant_syrk != 5)
             f32w::k_syrk256d<><<<g, 512, 0, st>>>(Zf, ldz, n, m, Tf, accumulate);
         else
             f32k::k_syrk<false, 16, 4><<<(unsigned)nt, 256, 0, st>>>(Z, ldz, m, nullptr, (float*)tiles, accumulate);
-    } else if (g_variant_syrk == 5) {
+    }
+#ifdef SNPMI_UBENCH
+    else if (g_variant_syrk == 5) {
         f64k::k_syrk<false><<<(unsigned)nt, 256, 0, st>>>(Z, ldz, m, nullptr, (double*)tiles, accumulate);
-    } else {
+    }
+#endif
+    else {
         f64k::k_syrk_glds<<<(unsigned)nt, 256, 0, st>>>((const double*)Z, ldz, m, (double*)tiles, accumulate);
     }
     SNPMI_HIP(hipGetLastError());

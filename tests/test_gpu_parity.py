@@ -321,21 +321,24 @@ def test_kerneldata_diag_k_to_n():
     assert abs(np.diag(kd.val).sum() - 3) < 1e-7  # kernelreader/test.py:221-229
 
 
-@pytest.fixture(params=[0, 41, 40, 42, 43, 46, 44, 36, 4, 5, 20, 30, 31, 33, 34],
-                ids=["auto", "h2k16", "h2pin", "h2preA", "h2preApin", "h2k32pin", "h2dma", "bf3", "syrk256", "syrk128", "f32twophase", "bf3plain",
-                     "bf3xcd", "bf3mode1", "bf3mode2"])
+@pytest.fixture(params=[0, 36, 20, 5], ids=["auto", "bf3", "f32mfma", "small128"])
 def syrk_variant(request):
-    """Run a test under each SYRK kernel -- f32: 0 = default (packed: the fp16x2-split kernel,
-    3 products on the fp16 MFMA pipe, 32-SNP LDS stages, with the bf16x3 kernel as its range
-    fallback), 46 = that with the loader VALU pinned between the MFMAs, 41 = 16-SNP stages, 40 =
-    + pin, 44 = dense operand as LDS-DMA stage images (k_image_h2 + MODE 6), 42/43 = 16-SNP stages with the next stage's A plane-0 fragments prefetched after the
-    barrier (unpinned / pinned), 36 = the bf16x3 kernel alone (interleaved
-    loader pinned one VALU per MFMA, mid-stage barrier with the next B planes prefetched), 34 =
-    without the pin, 33 = end-of-stage barrier, 30/31 = its plain-loader forms, 4 = f32
-    MFMA 256x256 fused, 5 = f32 MFMA 128x128, 20 = f32 MFMA two-phase (decode to Z + glds);
-    f64: 0/4 = interleaved bank-rotated loader, 5 = plain loader -- and restore the default."""
+    """Run a test under each SYRK kernel the product library ships -- f32: 0 = the default chain
+    (packed: the fp16x2-split kernel, 3 products on the fp16 MFMA pipe, with the bf16x3 kernel
+    as its device-side range fallback; dense operand N >= 4096: fp16x2 LDS-DMA stage images,
+    the f32-MFMA k_syrk256d as fallback), 36 = the bf16x3 kernel alone, 20 = the f32-MFMA
+    kernels (two-phase decode to Z + glds SYRK at N >= 4096, the 128x128 kernel below), 5 =
+    the 128x128 small-N kernels; f64: every variant runs the f64 kernels (0 / 20 / 36: the
+    default fused / glds kernels).  The ablation variants live in the ubench build only."""
     N.call("snpmi_set_kernel_variant", b"syrk", request.param)
     yield request.param
+    N.call("snpmi_set_kernel_variant", b"syrk", 0)
+
+
+def test_product_library_refuses_ablation_variants():
+    for v in (4, 30, 41, 44, 49):
+        with pytest.raises(ValueError):
+            N.call("snpmi_set_kernel_variant", b"syrk", v)
     N.call("snpmi_set_kernel_variant", b"syrk", 0)
 
 
@@ -433,6 +436,37 @@ def test_grm_dense_h2_range(scale, syrk_variant):
     Zs = v.astype(np.float64).copy(order="F")
     O.standardize_native(Zs)
     grm_close(d.read_kernel(Unit(), dtype=np.float32).val, Zs.dot(Zs.T), 1e-5)
+
+
+@pytest.mark.parametrize("m_per_block,chunk", [(45, 0), (70, 0), (70, 32)])
+def test_grm_dense_session_blocks_mixed_range(m_per_block, chunk):
+    """The generic block loop at N >= 4096 in f32 (snpmi_grm_add_dense: SnpReader._read_kernel's
+    K += Z_b Z_b^T, snpreader.py:651-655, K kept on the device): several blocks accumulate into
+    one session, one of them scaled out of fp16 range so that block alone takes the f32-MFMA
+    fallback while its neighbours stay on the fp16x2 stage-image kernel; m not a multiple of 32
+    and more than two 32-SNP stages per block -- vs the f64 product of the same values."""
+    rng = np.random.default_rng(m_per_block)
+    n, nblk = 4200, 4
+    blocks = [rng.standard_normal((n, m_per_block)).astype(np.float32) for _ in range(nblk)]
+    blocks[2] *= np.float32(1e-4)  # outside [2^-2, 2^15): this block runs on k_syrk256d
+    ref = np.zeros((n, n))
+    N.call("snpmi_set_kernel_variant", b"dense_chunk", chunk)  # 32: stage images in 32-SNP chunks
+    try:
+        N.call("snpmi_grm_begin", n, N.DT_F32)
+        for k, blk in enumerate(blocks):
+            order_c = k % 2
+            arr = np.ascontiguousarray(blk) if order_c else np.asfortranarray(blk)
+            N.call("snpmi_grm_add_dense_f32", N.ptr(arr), n, m_per_block, order_c)
+            b64 = blk.astype(np.float64)
+            ref += b64.dot(b64.T)
+        K = np.empty((n, n), dtype=np.float32)
+        factor = ctypes.c_double()
+        N.call("snpmi_grm_end", 0, ctypes.byref(factor), N.ptr(K))
+    finally:
+        N.call("snpmi_set_kernel_variant", b"dense_chunk", 0)
+    grm_close(K, ref, 1e-5)
+    err = np.abs(K.astype(np.float64) - ref).max() / np.abs(np.diag(ref)).max()
+    assert err <= 2e-6, "GRM max|dK|/max diag = %g" % err
 
 
 # ---------------------------------------------------------------------------------- device API
