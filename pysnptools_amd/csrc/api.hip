@@ -296,7 +296,7 @@ struct IidPlan {
     uint64_t n_in, n_out, pitch_in, pitch_out;
     bool repack;
     uint64_t* idx_dev = nullptr;
-    uint32_t* idx32_dev = nullptr;  // same indices as 32-bit words (k_repack_lds)
+    RepackPlan plan;                // gather plan of k_repack_lds / k_repack_win
 };
 
 static IidPlan plan_iids(Device& d, const uint64_t* iid_idx, uint64_t n_iid, uint64_t n_out) {
@@ -309,8 +309,9 @@ static IidPlan plan_iids(Device& d, const uint64_t* iid_idx, uint64_t n_iid, uin
     if (p.repack && p.n_out) {
         p.idx_dev = (uint64_t*)d.get(Device::S_IDX, p.n_out * 8);
         SNPMI_HIP(hipMemcpyAsync(p.idx_dev, iid_idx, p.n_out * 8, hipMemcpyHostToDevice, d.stream));
-        p.idx32_dev = (uint32_t*)d.get(Device::S_IDX32, p.n_out * 4);
-        launch_idx_u32(p.idx_dev, p.n_out, p.idx32_dev, d.stream);
+        uint32_t* plan = (uint32_t*)d.get(Device::S_IDX32, repack_plan_entries(p.n_out) * 4);
+        uint32_t* win = (uint32_t*)d.get(Device::S_WIN, repack_win_entries(p.n_out) * 4);
+        p.plan = launch_repack_plan(p.idx_dev, p.n_out, p.n_in, plan, win, d.stream);
     }
     return p;
 }
@@ -334,7 +335,7 @@ static const uint8_t* stage_chunk(Device& d, const BedMap& m, const uint64_t* si
     SNPMI_HIP(hipStreamWaitEvent(d.stream, d.staged[slot], 0));
     if (!p.repack) return dev;
     uint8_t* dev2 = (uint8_t*)d.get(Device::S_PACKED2, cnt * p.pitch_out);
-    launch_repack(dev, p.pitch_in, p.n_in, p.idx_dev, p.idx32_dev, p.n_out, cnt, dev2, p.pitch_out, d.stream);
+    launch_repack(dev, p.pitch_in, p.n_in, p.idx_dev, p.plan, p.n_out, cnt, dev2, p.pitch_out, d.stream);
     return dev2;
 }
 
@@ -1392,9 +1393,10 @@ int snpmi_dev_repack(const uint8_t* src, uint64_t src_pitch, uint64_t n_src, con
         std::lock_guard<std::recursive_mutex> lk(g_call_mutex);  // shared scratch slots
         SNPMI_REQUIRE(dst_pitch % 64 == 0 && dst_pitch >= ceil_div(n_out, 4), SNPMI_E_ARG, "bad dst pitch");
         Device& d = device();
-        uint32_t* idx32 = (uint32_t*)d.get(Device::S_IDX32, std::max<uint64_t>(n_out, 1) * 4);
-        launch_idx_u32(idx, n_out, idx32, d.stream);
-        launch_repack(src, src_pitch, n_src, idx, idx32, n_out, n_sid, dst, dst_pitch, d.stream);
+        uint32_t* plan = (uint32_t*)d.get(Device::S_IDX32, repack_plan_entries(n_out) * 4);
+        uint32_t* win = (uint32_t*)d.get(Device::S_WIN, repack_win_entries(n_out) * 4);
+        const RepackPlan P = launch_repack_plan(idx, n_out, n_src, plan, win, d.stream);
+        launch_repack(src, src_pitch, n_src, idx, P, n_out, n_sid, dst, dst_pitch, d.stream);
     });
 }
 

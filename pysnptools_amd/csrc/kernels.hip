@@ -488,9 +488,11 @@ __global__ __launch_bounds__(kBlock) void k_decode_c_reg(const uint8_t* __restri
         }
         const bool full = jl + V <= m;
         const uint64_t rows = n - i0 < 256 ? n - i0 : 256;
+        // q fully unrolled (w[v][q] stays in registers), e rolled up to 4 (a fully unrolled
+        // 256-row nest made the compiler index w dynamically -- 272 B/lane of scratch)
 #pragma unroll
         for (int q = 0; q < 16; q++) {
-#pragma unroll
+#pragma unroll 4
             for (int e = 0; e < 16; e++) {
                 const uint64_t r = 16 * q + e;
                 if (r < rows) {
@@ -501,6 +503,7 @@ __global__ __launch_bounds__(kBlock) void k_decode_c_reg(const uint8_t* __restri
                     if (full) {
                         store_nt(reinterpret_cast<vec_t*>(dst), o);
                     } else {
+#pragma unroll
                         for (int v = 0; v < V; v++)
                             if (jl + v < m) dst[v] = o[v];
                     }
@@ -533,48 +536,199 @@ __global__ __launch_bounds__(kBlock) void k_repack(const uint8_t* __restrict__ s
     }
 }
 
-// iid gather with the source column staged in LDS (one 1024-thread workgroup per SNP): the
-// column is read from HBM once with 16-B loads, every output word gathers its 16 codes from
-// LDS (ds_read_u8) through a 32-bit copy of the index list, and the output words are written
-// coalesced.  k_repack above (per-thread global byte gathers, 64-bit indices) is the fallback
-// for columns > 150 KiB.
-__global__ void k_idx_to_u32(const uint64_t* __restrict__ idx, uint64_t n, uint32_t* __restrict__ out) {
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
-        out[i] = (uint32_t)idx[i];
+// iid gather with the source columns staged in LDS.  One 1024-thread workgroup walks groups of
+// K SNP columns (K = 4 / 2 / 1 as K columns fit in 150 KiB of LDS), the columns of a group
+// interleaved by dword (LDS dword w*K + c = dword w of column c), so ONE plan entry serves all
+// K columns: a ds_read_b32/b64/b128 returns the dword holding the source code in every column.
+// The plan (k_repack_plan, once per call) is one u32 per output code: LDS byte address << 5 |
+// bit offset of the code in its dword, so a code costs one LDS read + v_bfe + v_lshl_or; output
+// codes past n_out point at a zero dword behind the columns.  The next group's columns are
+// loaded into registers while the current group gathers (global latency under LDS work), and
+// every dword of the destination pitch is written (no separate memset).  k_repack (global
+// gathers) is the fallback for columns over 150 KiB.
+constexpr uint64_t kRepackLds = 150 * 1024;
+// u32x4 of each column of the next group held per thread: ceil(150 KiB / 16 B / K / 1024) for K = 1, 2, 4
+constexpr int kRepackPre[3] = {10, 5, 3};
+
+__host__ __device__ inline int repack_k(uint64_t nq) {
+    const uint64_t bytes = nq * 16;
+    return 4 * bytes + 16 <= kRepackLds ? 4 : 2 * bytes + 16 <= kRepackLds ? 2 : 1;
 }
 
-__global__ __launch_bounds__(1024) void k_repack_lds(const uint8_t* __restrict__ src, uint64_t sp, uint64_t nq,
-                                                     const uint32_t* __restrict__ idx, uint64_t n_out,
-                                                     uint8_t* __restrict__ dst, uint64_t dp) {
-    extern __shared__ u32x4_t colq[];
-    const uint64_t j = blockIdx.x;
-    const u32x4_t* s = reinterpret_cast<const u32x4_t*>(src + j * sp);
-    for (uint64_t q = threadIdx.x; q < nq; q += 1024) colq[q] = __builtin_nontemporal_load(s + q);
-    __syncthreads();
-    const uint8_t* cb = reinterpret_cast<const uint8_t*>(colq);
-    uint32_t* o = reinterpret_cast<uint32_t*>(dst + j * dp);
-    const uint64_t nd = (n_out + 15) / 16;
-    for (uint64_t d = threadIdx.x; d < nd; d += 1024) {
-        const uint64_t r0 = 16 * d;
-        uint32_t w = 0;
-        if (r0 + 16 <= n_out) {
-            const u32x4_t* ip = reinterpret_cast<const u32x4_t*>(idx + r0);
+constexpr uint64_t kRepackChunk = 8192;  // default output codes per windowed workgroup (512 words)
+
+// win == nullptr: absolute LDS addresses (whole columns, zero dword behind them at u32x4 nq);
+// else per kRepackChunk-code output chunk c the source window starts at u32x4 win[c] and the zero
+// dword sits behind the widest window (u32x4 zq)
+__global__ void k_repack_plan(const uint64_t* __restrict__ idx, uint64_t n_out, uint64_t n_pad, uint64_t zq, int K,
+                              const uint32_t* __restrict__ win, uint64_t chunk, uint32_t* __restrict__ plan) {
+    for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n_pad; r += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t i = r < n_out ? idx[r] : 0;
+        const uint64_t base = win ? 4ull * win[r / chunk] : 0;
+        const uint64_t w = r < n_out ? (i >> 4) - base : 4 * zq;
+        plan[r] = (uint32_t)(((w * K * 4) << 5) | ((i & 15) << 1));
+    }
+}
+
+// source window of each kRepackChunk-code output chunk: lohi[2c] = min, lohi[2c+1] = max of its
+// source iids (u32 atomics; lohi preset to {~0, 0} per chunk), 2048 codes per workgroup
+__global__ __launch_bounds__(256) void k_repack_window(const uint64_t* __restrict__ idx, uint64_t n_out,
+                                                       uint64_t chunk, uint32_t* __restrict__ lohi) {
+    const uint64_t r0 = (uint64_t)blockIdx.x * 2048;
+    uint32_t lo = ~0u, hi = 0;
+    for (uint64_t r = r0 + threadIdx.x; r < min(r0 + 2048, n_out); r += 256) {
+        const uint32_t i = (uint32_t)idx[r];
+        lo = min(lo, i);
+        hi = max(hi, i);
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        lo = min(lo, (uint32_t)__shfl_xor((int)lo, o));
+        hi = max(hi, (uint32_t)__shfl_xor((int)hi, o));
+    }
+    if ((threadIdx.x & 63) == 0 && r0 < n_out) {
+        const uint64_t c = r0 / chunk;
+        atomicMin(lohi + 2 * c, lo);
+        atomicMax(lohi + 2 * c + 1, hi);
+    }
+}
+
+// Windowed gather for index lists with locality (sorted, reversed, strided subsets -- what
+// intersect_apply produces when the iid orders agree): a 256-thread workgroup (chunk c, group g)
+// stages only the source window of output chunk c (512 words) for K columns, K x window <= 40
+// KiB so four workgroups share a CU and one's loads overlap the others' gathers; sources are read
+// once and each plan entry serves K columns.
+template <int K>
+__global__ __launch_bounds__(256) void k_repack_win(const uint8_t* __restrict__ src, uint64_t sp, uint64_t nq,
+                                                    uint64_t zq, uint64_t nchunks, uint64_t chunk_words, uint64_t m,
+                                                    const uint32_t* __restrict__ win,
+                                                    const uint32_t* __restrict__ plan, uint64_t n_out,
+                                                    uint8_t* __restrict__ dst, uint64_t dp) {
+    extern __shared__ u32x4_t colw[];
+    typedef uint32_t vk_t __attribute__((ext_vector_type(K)));
+    const int t = threadIdx.x;
+    const uint64_t c = blockIdx.x % nchunks, g = blockIdx.x / nchunks;
+    const uint64_t lo4 = win[c], n4 = min(zq, nq - lo4);
+    uint32_t* l = reinterpret_cast<uint32_t*>(colw);
+    for (uint64_t q = t; q < n4; q += 256) {
+        u32x4_t v[K];
 #pragma unroll
-            for (int v = 0; v < 4; v++) {
-                const u32x4_t ii = ip[v];
-#pragma unroll
-                for (int k = 0; k < 4; k++) {
-                    const uint32_t i = ii[k];
-                    w |= (uint32_t)((cb[i >> 2] >> (2 * (i & 3))) & 3u) << (2 * (4 * v + k));
-                }
-            }
+        for (int cc = 0; cc < K; cc++) {
+            const uint64_t j = g * K + cc;
+            v[cc] = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(src + (j < m ? j : m - 1) * sp) + lo4 + q);
+        }
+        if constexpr (K == 1) {
+            colw[q] = v[0];
         } else {
-            for (int k = 0; r0 + k < n_out; k++) {
-                const uint32_t i = idx[r0 + k];
-                w |= (uint32_t)((cb[i >> 2] >> (2 * (i & 3))) & 3u) << (2 * k);
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+                vk_t x;
+#pragma unroll
+                for (int cc = 0; cc < K; cc++) x[cc] = v[cc][e];
+                *reinterpret_cast<vk_t*>(l + (4 * q + e) * K) = x;
             }
         }
-        o[d] = w;
+    }
+    if (t < K) l[4 * zq * K + t] = 0;
+    __syncthreads();
+    const uint64_t nd = (n_out + 15) / 16, ndp = dp / 4;
+    const uint64_t d0 = c * chunk_words, d1 = c + 1 == nchunks ? ndp : min(d0 + chunk_words, ndp);
+    const uint8_t* lb = reinterpret_cast<const uint8_t*>(colw);
+    for (uint64_t d = d0 + t; d < d1; d += 256) {
+        vk_t w = {};
+        if (d < nd) {
+            const u32x4_t* pp = reinterpret_cast<const u32x4_t*>(plan + 16 * d);
+#pragma unroll
+            for (int v = 0; v < 4; v++) {
+                const u32x4_t e4 = pp[v];
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const uint32_t e = e4[k];
+                    const vk_t x = *reinterpret_cast<const vk_t*>(lb + (e >> 5));
+#pragma unroll
+                    for (int cc = 0; cc < K; cc++) w[cc] |= __builtin_amdgcn_ubfe(x[cc], e & 31u, 2) << (2 * (4 * v + k));
+                }
+            }
+        }
+#pragma unroll
+        for (int cc = 0; cc < K; cc++)
+            if (g * K + cc < m) reinterpret_cast<uint32_t*>(dst + (g * K + cc) * dp)[d] = w[cc];
+    }
+}
+
+template <int K>
+__global__ __launch_bounds__(1024) void k_repack_lds(const uint8_t* __restrict__ src, uint64_t sp, uint64_t nq,
+                                                     uint64_t m, const uint32_t* __restrict__ plan, uint64_t n_out,
+                                                     uint8_t* __restrict__ dst, uint64_t dp) {
+    extern __shared__ u32x4_t colq[];  // K * nq u32x4 + one zero u32x4
+    typedef uint32_t vk_t __attribute__((ext_vector_type(K)));
+    const int t = threadIdx.x;
+    const uint64_t ng = (m + K - 1) / K;
+    const uint64_t nd = (n_out + 15) / 16, ndp = dp / 4;
+    constexpr int PRE = kRepackPre[K >> 1];  // u32x4 per column per thread held in registers
+    u32x4_t pre[K][PRE];
+    auto fetch = [&](uint64_t g) {
+#pragma unroll
+        for (int c = 0; c < K; c++) {
+            const uint64_t j = g * K + c;
+            const u32x4_t* s = reinterpret_cast<const u32x4_t*>(src + (j < m ? j : m - 1) * sp);
+#pragma unroll
+            for (int u = 0; u < PRE; u++) {
+                const uint64_t q = (uint64_t)t + 1024u * u;
+                pre[c][u] = q < nq ? __builtin_nontemporal_load(s + q) : (u32x4_t){0, 0, 0, 0};
+            }
+        }
+    };
+    auto park = [&]() {
+        uint32_t* l = reinterpret_cast<uint32_t*>(colq);
+#pragma unroll
+        for (int u = 0; u < PRE; u++) {
+            const uint64_t q = (uint64_t)t + 1024u * u;
+            if (q < nq) {
+                if constexpr (K == 1) {
+                    colq[q] = pre[0][u];
+                } else {
+#pragma unroll
+                    for (int e = 0; e < 4; e++) {  // dword 4q+e of every column: one K-dword store
+                        vk_t v;
+#pragma unroll
+                        for (int c = 0; c < K; c++) v[c] = pre[c][u][e];
+                        *reinterpret_cast<vk_t*>(l + (4 * q + e) * K) = v;
+                    }
+                }
+            }
+        }
+        if (t < K) l[4 * nq * K + t] = 0;
+    };
+    uint64_t g = blockIdx.x;
+    if (g >= ng) return;
+    fetch(g);
+    for (; g < ng; g += gridDim.x) {
+        __syncthreads();  // the previous group's gather is done with LDS
+        park();
+        __syncthreads();
+        if (g + gridDim.x < ng) fetch(g + gridDim.x);  // in flight during this group's gather
+        const uint8_t* lb = reinterpret_cast<const uint8_t*>(colq);
+        for (uint64_t d = t; d < ndp; d += 1024) {
+            vk_t w = {};
+            if (d < nd) {
+                const u32x4_t* pp = reinterpret_cast<const u32x4_t*>(plan + 16 * d);
+#pragma unroll
+                for (int v = 0; v < 4; v++) {
+                    const u32x4_t e4 = pp[v];
+#pragma unroll
+                    for (int k = 0; k < 4; k++) {
+                        const uint32_t e = e4[k];
+                        const vk_t x = *reinterpret_cast<const vk_t*>(lb + (e >> 5));
+#pragma unroll
+                        for (int c = 0; c < K; c++)
+                            w[c] |= __builtin_amdgcn_ubfe(x[c], e & 31u, 2) << (2 * (4 * v + k));
+                    }
+                }
+            }
+#pragma unroll
+            for (int c = 0; c < K; c++)
+                if (g * K + c < m) reinterpret_cast<uint32_t*>(dst + (g * K + c) * dp)[d] = w[c];
+        }
     }
 }
 
@@ -1088,23 +1242,107 @@ void launch_decode_std_fused(const uint8_t* packed, uint64_t pitch, uint64_t n, 
     SNPMI_LAUNCH_CHECK();
 }
 
-void launch_idx_u32(const uint64_t* idx, uint64_t n, uint32_t* out, hipStream_t st) {
-    if (n == 0) return;
-    k_idx_to_u32<<<grid_for(n, kBlock, 4096), kBlock, 0, st>>>(idx, n, out);
+uint64_t repack_plan_entries(uint64_t n_out) { return round_up(std::max<uint64_t>(n_out, 1), 16); }
+uint64_t repack_win_entries(uint64_t n_out) { return 3 * ceil_div(std::max<uint64_t>(n_out, 1), 4096) + 64; }
+
+// Build the gather plan for one index list (once per call).  Narrow per-chunk source windows
+// (the widest <= half a column and fitting K >= 1 columns in 40 KiB) select the windowed kernel;
+// the choice needs the windows on the host, so this synchronises the stream once.
+RepackPlan launch_repack_plan(const uint64_t* idx, uint64_t n_out, uint64_t n_src, uint32_t* plan, uint32_t* win,
+                              hipStream_t st) {
+    RepackPlan P;
+    const uint64_t nq = ceil_div(ceil_div(n_src, 4), 16), n_pad = repack_plan_entries(n_out);
+    if (n_out == 0) return P;
+    // tuning hook (decode variants 9-11): chunk of 16384 / 4096 codes, or two columns per group;
+    // measured 500k -> 250k x 8192 SNPs (rev2 / sorted half): 16384 0.402 ms, 8192 0.386, 32768
+    // 0.468, K = 2 0.518 (profiles/r02e/ubench_repack_win.jsonl)
+    const uint64_t chunk = g_variant_decode == 9 ? 16384 : g_variant_decode == 10 ? 4096 : kRepackChunk;
+    const uint64_t nchunks = ceil_div(n_out, chunk);
+    if (win != nullptr && nchunks > 1 && g_variant_decode != 8) {
+        uint32_t* lohi = win + nchunks;
+        std::vector<uint32_t> h(2 * nchunks);
+        for (uint64_t c = 0; c < nchunks; c++) h[2 * c] = ~0u, h[2 * c + 1] = 0;
+        SNPMI_HIP(hipMemcpyAsync(lohi, h.data(), h.size() * 4, hipMemcpyHostToDevice, st));
+        k_repack_window<<<(unsigned)ceil_div(n_out, 2048), 256, 0, st>>>(idx, n_out, chunk, lohi);
+        SNPMI_LAUNCH_CHECK();
+        SNPMI_HIP(hipMemcpyAsync(h.data(), lohi, h.size() * 4, hipMemcpyDeviceToHost, st));
+        SNPMI_HIP(hipStreamSynchronize(st));
+        std::vector<uint32_t> lo4(nchunks);
+        uint64_t w = 0;
+        for (uint64_t c = 0; c < nchunks; c++) {
+            lo4[c] = h[2 * c] >> 6;
+            w = std::max<uint64_t>(w, (h[2 * c + 1] >> 6) - lo4[c] + 1);
+        }
+        const uint64_t budget = 40 * 1024 - 16;  // >= four workgroups per CU
+        int K = 4 * w * 16 <= budget ? 4 : 2 * w * 16 <= budget ? 2 : w * 16 <= budget ? 1 : 0;
+        if (g_variant_decode == 11 && K == 4) K = 2;
+        if (K > 0 && 2 * w <= nq) {
+            SNPMI_HIP(hipMemcpyAsync(win, lo4.data(), nchunks * 4, hipMemcpyHostToDevice, st));
+            k_repack_plan<<<grid_for(n_pad, kBlock, 4096), kBlock, 0, st>>>(idx, n_out, n_pad, w, K, win, chunk, plan);
+            SNPMI_LAUNCH_CHECK();
+            SNPMI_HIP(hipStreamSynchronize(st));  // lo4 is a local vector
+            P.plan = plan;
+            P.win = win;
+            P.K = K;
+            P.zq = w;
+            P.nchunks = nchunks;
+            P.chunk_words = chunk / 16;
+            return P;
+        }
+    }
+    if (nq * 16 + 16 > kRepackLds) return P;  // k_repack (global gathers) reads idx directly
+    const int K = repack_k(nq);
+    k_repack_plan<<<grid_for(n_pad, kBlock, 4096), kBlock, 0, st>>>(idx, n_out, n_pad, nq, K, nullptr, 1, plan);
     SNPMI_LAUNCH_CHECK();
+    P.plan = plan;
+    P.K = K;
+    P.zq = nq;
+    return P;
 }
 
-void launch_repack(const uint8_t* src, uint64_t src_pitch, uint64_t n_src, const uint64_t* idx, const uint32_t* idx32,
+void launch_repack(const uint8_t* src, uint64_t src_pitch, uint64_t n_src, const uint64_t* idx, const RepackPlan& P,
                    uint64_t n_out, uint64_t n_sid, uint8_t* dst, uint64_t dst_pitch, hipStream_t st) {
     if (n_sid == 0) return;
-    SNPMI_HIP(hipMemsetAsync(dst, 0, n_sid * dst_pitch, st));
-    if (n_out == 0) return;
     const uint64_t nq = ceil_div(ceil_div(n_src, 4), 16);  // 16-B words of a source column
-    if (idx32 != nullptr && nq * 16 <= kLdsColMax && src_pitch % 16 == 0 && n_sid < (1ull << 31)) {
-        SNPMI_HIP(hipFuncSetAttribute((const void*)k_repack_lds, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                      (int)kLdsColMax));
-        k_repack_lds<<<(unsigned)n_sid, 1024, nq * 16, st>>>(src, src_pitch, nq, idx32, n_out, dst, dst_pitch);
+    const bool fits = src_pitch % 16 == 0 && dst_pitch % 4 == 0 && n_sid < (1ull << 31);
+    if (P.plan != nullptr && P.win != nullptr && fits) {
+        const uint64_t ng = ceil_div(n_sid, (uint64_t)P.K);
+        SNPMI_REQUIRE(ng * P.nchunks < (1ull << 31), SNPMI_E_ARG, "too many repack workgroups");
+        const size_t lds = (size_t)(P.K * P.zq + 1) * 16;
+#define SNPMI_REPACK_WIN(KK)                                                                                       \
+    k_repack_win<KK><<<(unsigned)(ng * P.nchunks), 256, lds, st>>>(src, src_pitch, nq, P.zq, P.nchunks,             \
+                                                                  P.chunk_words, n_sid,                             \
+                                                                   P.win, P.plan, n_out, dst, dst_pitch)
+        if (P.K == 4) {
+            SNPMI_REPACK_WIN(4);
+        } else if (P.K == 2) {
+            SNPMI_REPACK_WIN(2);
+        } else {
+            SNPMI_REPACK_WIN(1);
+        }
+#undef SNPMI_REPACK_WIN
+    } else if (P.plan != nullptr && nq * 16 + 16 <= kRepackLds && fits) {
+        const int K = P.K;
+        SNPMI_REQUIRE(nq <= (uint64_t)kRepackPre[K >> 1] * 1024, SNPMI_E_ARG, "repack staging exceeds its registers");
+        const uint64_t ng = ceil_div(n_sid, (uint64_t)K);
+        // one workgroup per CU (LDS), each walking several groups so the next one's loads overlap
+        const unsigned grid = (unsigned)std::min<uint64_t>(ng, 256 * 2);
+        const size_t lds = (size_t)(K * nq + 1) * 16;
+#define SNPMI_REPACK(KK)                                                                                            \
+    SNPMI_HIP(hipFuncSetAttribute((const void*)k_repack_lds<KK>, hipFuncAttributeMaxDynamicSharedMemorySize,      \
+                                  (int)kRepackLds));                                                                \
+    k_repack_lds<KK><<<grid, 1024, lds, st>>>(src, src_pitch, nq, n_sid, P.plan, n_out, dst, dst_pitch)
+        if (K == 4) {
+            SNPMI_REPACK(4);
+        } else if (K == 2) {
+            SNPMI_REPACK(2);
+        } else {
+            SNPMI_REPACK(1);
+        }
+#undef SNPMI_REPACK
     } else {
+        SNPMI_HIP(hipMemsetAsync(dst, 0, n_sid * dst_pitch, st));
+        if (n_out == 0) return;
         const unsigned g = grid_for(ceil_div(n_out, 16) * n_sid, kBlock);
         k_repack<<<g, kBlock, 0, st>>>(src, src_pitch, idx, n_out, n_sid, dst, dst_pitch);
     }

@@ -68,7 +68,7 @@ struct Device {
     // grow-only scratch slots
     enum Slot { S_PACKED, S_PACKED2, S_IDX, S_IDX2, S_LUT, S_STATS, S_OUT, S_TILES, S_K, S_DENSE,
                 S_DENSE2, S_RED, S_SESSION, S_PACKED_B, S_ZBLK, S_IDX32, S_LUT3, S_H2, S_OUT_B, S_STATS_B,
-                S_NUM };
+                S_WIN, S_NUM };
     void* buf[S_NUM] = {};
     // chunk pipeline events (slot = chunk parity), all on-device ordering, no host spin:
     hipEvent_t staged[2] = {};    // copy stream: H2D of pinned slot done (host may refill it)
@@ -104,8 +104,21 @@ void launch_decode(const uint8_t* packed, uint64_t pitch, uint64_t n_iid, uint64
 void launch_decode_std_fused(const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m, int count_a1,
                              int std_kind, double a, double b, int use_stats, void* stats, void* lut, void* out,
                              uint64_t ld, hipStream_t st);
-void launch_idx_u32(const uint64_t* idx, uint64_t n, uint32_t* out, hipStream_t st);
-void launch_repack(const uint8_t* src, uint64_t src_pitch, uint64_t n_src, const uint64_t* idx, const uint32_t* idx32,
+// iid gather: plan = repack_plan_entries(n_out) u32 and win = repack_win_entries(n_out) u32 of
+// scratch, built once per index list (launch_repack_plan, which may synchronise the stream once)
+struct RepackPlan {
+    const uint32_t* plan = nullptr;  // nullptr: global-gather fallback (reads idx)
+    const uint32_t* win = nullptr;   // per-chunk source windows (windowed kernel) or nullptr
+    int K = 1;                       // columns per workgroup
+    uint64_t zq = 0;                 // u32x4 per staged column (window or whole column)
+    uint64_t nchunks = 1;
+    uint64_t chunk_words = 0;        // output words per windowed workgroup
+};
+uint64_t repack_plan_entries(uint64_t n_out);
+uint64_t repack_win_entries(uint64_t n_out);
+RepackPlan launch_repack_plan(const uint64_t* idx, uint64_t n_out, uint64_t n_src, uint32_t* plan, uint32_t* win,
+                              hipStream_t st);
+void launch_repack(const uint8_t* src, uint64_t src_pitch, uint64_t n_src, const uint64_t* idx, const RepackPlan& plan,
                    uint64_t n_out, uint64_t n_sid, uint8_t* dst, uint64_t dst_pitch, hipStream_t st);
 void launch_dense_standardize(void* val, uint64_t rows, uint64_t cols, uint64_t ld, int order_c, int dtype,
                               int std_kind, double a, double b, int use_stats, void* stats, hipStream_t st);

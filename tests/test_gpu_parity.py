@@ -703,16 +703,25 @@ def test_fused_decode_standardize_equals_two_kernels(n, kind, use_stats, count_a
         assert np.array_equal(outs[1][0].T, exp) and np.array_equal(outs[1][2], est)
 
 
-@pytest.mark.parametrize("n,m", [(20_011, 40), (700_003, 3)])
-def test_dev_repack_random_gather(n, m):
-    """snpmi_dev_repack (LDS-staged column; > 150 KiB columns take the global-gather fallback):
-    repacked codes decode to the source codes at the gathered iids, pad bits zero."""
+@pytest.mark.parametrize("n,m", [(20_011, 40), (100_003, 2050), (250_001, 1501), (500_000, 1100), (700_003, 3)])
+@pytest.mark.parametrize("kind", ["random", "reversed_stride2", "sorted"])
+def test_dev_repack_random_gather(n, m, kind):
+    """snpmi_dev_repack: columns staged in LDS in groups of K = 4 / 2 / 1 (by column size; more
+    groups than workgroups, so the register prefetch of the next group runs), > 150 KiB columns
+    on the global-gather fallback -- repacked codes decode to the source codes at the gathered
+    iids, and every pad bit and pad byte of the destination pitch is zero."""
     buf, pitch = synth_dev(n, m, 17)
     rng = np.random.default_rng(n)
-    idx = rng.choice(n, size=n // 3, replace=True).astype(np.uint64)
+    if kind == "random":
+        idx = rng.choice(n, size=n // 3, replace=True).astype(np.uint64)
+    elif kind == "reversed_stride2":
+        idx = np.arange(n - 1, -1, -2, dtype=np.uint64)
+    else:
+        idx = np.sort(rng.choice(n, size=n // 2 + 7, replace=False)).astype(np.uint64)
     n_out = len(idx)
     pitch_out = N.lib().snpmi_packed_pitch(n_out)
     didx, dst = Dev(n_out * 8), Dev(pitch_out * m)
+    N.call("snpmi_dev_memset", dst.p, 0xA5, pitch_out * m)  # the kernel must write the pad itself
     didx.put(idx)
     N.call("snpmi_dev_repack", buf.p, pitch, n, didx.p, n_out, m, dst.p, pitch_out)
     src = buf.get(np.empty((m, pitch), dtype=np.uint8))
@@ -722,6 +731,7 @@ def test_dev_repack_random_gather(n, m):
     assert np.array_equal(sub, full[idx.astype(np.int64)])
     if n_out % 4:
         assert np.all((got[:, n_out // 4] >> (2 * (n_out % 4))) == 0)
+    assert np.all(got[:, (n_out + 3) // 4:] == 0)
 
 
 def test_diag_k_to_n_snp_side_and_trained():

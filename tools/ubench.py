@@ -115,25 +115,40 @@ def decode_c(args):
 
 
 def repack(args):
-    """iid gather of packed columns (k_repack): every other iid, reversed."""
+    """iid gather of packed columns (k_repack_lds): --index rev2 (every other iid, reversed; the
+    round-1 figure), random (n/2 draws with replacement) or sorted (a random half, in order)."""
     n, m = args.n, args.m
     pitch = N.lib().snpmi_packed_pitch(n)
-    idx = np.arange(n - 1, -1, -2, dtype=np.uint64)
+    rng = np.random.default_rng(0)
+    if args.index == "random":
+        idx = rng.choice(n, size=n // 2, replace=True).astype(np.uint64)
+    elif args.index == "sorted":
+        idx = np.sort(rng.choice(n, size=n // 2, replace=False)).astype(np.uint64)
+    else:
+        idx = np.arange(n - 1, -1, -2, dtype=np.uint64)
     n_out = len(idx)
     pitch_out = N.lib().snpmi_packed_pitch(n_out)
     packed, dst, didx = Dev(N, pitch * m), Dev(N, pitch_out * m), Dev(N, n_out * 8)
     synth(N, packed.p, pitch, n, 0, m, 3, 0.01)
     N.call("snpmi_memcpy_h2d", didx.p, N.ptr(idx), idx.nbytes)
     ev = Events(N, 2)
-    ts = []
+    variants = [int(v) for v in args.variants.split(",")]
+    ts = {v: [] for v in variants}
     for rnd in range(args.rounds):
-        ev.record(0)
-        N.call("snpmi_dev_repack", packed.p, pitch, n, didx.p, n_out, m, dst.p, pitch_out)
-        ev.record(1)
-        ts.append(ev.ms(0, 1))
-    t = np.median(ts)
+        for v in variants:
+            N.call("snpmi_set_kernel_variant", b"decode", v)
+            ev.record(0)
+            N.call("snpmi_dev_repack", packed.p, pitch, n, didx.p, n_out, m, dst.p, pitch_out)
+            ev.record(1)
+            ts[v].append(ev.ms(0, 1))
+    N.call("snpmi_set_kernel_variant", b"decode", 0)
     nbytes = m * ((n + 3) // 4 + (n_out + 3) // 4)
-    print(json.dumps({"kernel": "repack", "n": n, "n_out": n_out, "m": m, "median_ms": t, "GBps": nbytes / t / 1e6}))
+    for v in variants:
+        t = np.median(ts[v])
+        print(json.dumps({"kernel": "repack", "variant": v, "index": args.index, "n": n, "n_out": n_out, "m": m,
+                          "median_ms": t, "GBps": nbytes / t / 1e6, "frac_8TBs": nbytes / t / 1e6 / 8000,
+                          "note": "time = plan (+ window scan, one host sync) + gather; decode variant 8 = no "
+                                  "windowed kernel"}))
 
 
 def syrk_dense(args):
@@ -223,6 +238,7 @@ if __name__ == "__main__":
     p.add_argument("--m", type=int, default=8192)
     p.add_argument("--rounds", type=int, default=7)
     p.add_argument("--dtype", default="f32")
+    p.add_argument("--index", default="rev2", choices=["rev2", "random", "sorted"])
     p.add_argument("--variants", default="0,1,2,3,4,5,6")
     p.add_argument("--set-variant", default=None, help="kernel=variant applied once before the run")
     a = p.parse_args()
