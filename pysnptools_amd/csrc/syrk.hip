@@ -1373,6 +1373,415 @@ __global__ __launch_bounds__(512, 1) void k_syrk_h2(const uint8_t* __restrict__ 
     epilogue_pi<LOCAL>(acc, tiles, n, bi, bj, accumulate, lane, wm, wn, wg);
 }
 
+// ---------------------------------------------------------------- fp16x2 on v_mfma_f32_16x16x32_f16
+// Same products (A0 B0 + A0 B1 + A1 B0), loader and LDS image as k_syrk_h2 MODE 4, but every MFMA
+// is 16x16x32 instead of 32x32x16: the same cycles per FLOP and the same LDS bytes per FLOP
+// (a wave's 128x64 tile is 8 x 4 16x16 tiles; per 32-SNP stage 8 A + 8 A' + 4 B + 4 B' fragments
+// of 8 fp16 = 48 transposed reads, 96 MFMAs), and MI355X holds a higher clock on the 16x16 shape
+// under load (MI355X_MICROARCH.md, DVFS item 7: 1.12-1.15x FLOP/s with LDS-fed operands).
+// 16x16x32 operand: lane l holds row l%16, k 8(l/16)..+7, so a 32-lane half reads rows 8 apart
+// in the same 16 columns; with the 576-B row stride those rows share banks, so rows with bit 3
+// set hold each 16-iid group d in 32-B unit d ^ 1 (the loader stores through the same map; its
+// 8-lane ds_write_b128 groups keep their 8 distinct bank slots).
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// wave tile (8 x 4 16x16 tiles): accumulator j of lane l is LDS-order row 4(l>>4)+j, column
+// l&15 of its tile, i.e. iid row 16x + pi(4(l>>4)+j) = 16x + 4j + (l>>4), column 16y + pi(l&15)
+template <bool LOCAL>
+__device__ __forceinline__ void epilogue_h2x(f32x4 (&acc)[8][4], float* __restrict__ tiles, uint64_t n, uint32_t bi,
+                                             uint32_t bj, int accumulate, int lane, int wm, int wn,
+                                             uint64_t local_block) {
+    float* T;
+    uint64_t ldo;
+    if constexpr (LOCAL) {
+        T = tiles + local_block * (BW * BW) + (uint64_t)(wm * 128) * BW + (wn >> 1) * 128;
+        ldo = BW;
+    } else {
+        const uint64_t nt128 = (n + 127) / 128;
+        const uint64_t ti = 2 * (uint64_t)bi + wm, tj = 2 * (uint64_t)bj + (wn >> 1);
+        if (ti > tj || tj >= nt128) return;  // wave-uniform
+        T = tiles + (tj * (tj + 1) / 2 + ti) * (uint64_t)(BM * BM);
+        ldo = BM;
+    }
+    const int r = lane >> 4, colp = pi16(lane & 15);
+#pragma unroll
+    for (int x = 0; x < 8; x++)
+#pragma unroll
+        for (int y = 0; y < 4; y++) {
+            float* bp = T + (16 * x + r) * ldo + (wn & 1) * 64 + 16 * y + colp;
+            if (accumulate) {
+                float old[4];
+#pragma unroll
+                for (int j = 0; j < 4; j++) old[j] = bp[4 * j * ldo];
+#pragma unroll
+                for (int j = 0; j < 4; j++) acc[x][y][j] += old[j];
+            }
+#pragma unroll
+            for (int j = 0; j < 4; j++) bp[4 * j * ldo] = acc[x][y][j];
+        }
+}
+
+// MODE bit 0: waves 4-7 at s_setprio 1 for the whole loop (the arbitration loser of each SIMD
+// pair, MI355X_MICROARCH.md "Two waves per SIMD" item 4); bit 1: pin the interleave -- after
+// each MFMA one DS instruction and (in loader iterations) two VALU
+template <bool LOCAL = false, int MODE = 0>
+__global__ __launch_bounds__(512, 1) void k_syrk_h2x(const uint8_t* __restrict__ P, uint64_t pitch, uint64_t n,
+                                                     uint64_t kdim, const uint32_t* __restrict__ lut2,
+                                                     const uint32_t* __restrict__ flag, float* __restrict__ tiles,
+                                                     int accumulate, uint32_t part_rank = 0, uint32_t part_world = 1,
+                                                     uint64_t kslice = 0, uint64_t slice_elems = 0) {
+    constexpr int KS = 2, SBK = KS * BK;                 // 32 SNPs per LDS stage
+    constexpr int PLANE = KS * B3_PLANE, STAGE = 2 * 2 * PLANE;
+    __shared__ __attribute__((aligned(16))) short lds[2 * STAGE];
+    if (*flag) return;  // a SNP of this block is outside fp16's range: k_syrk_bf3 runs instead
+    if (gridDim.y > 1) {
+        const uint64_t k0 = (uint64_t)blockIdx.y * kslice;
+        P += k0 * pitch;
+        lut2 += 4 * k0;
+        kdim = min(kslice, kdim - k0);
+        tiles += (uint64_t)blockIdx.y * slice_elems;
+    }
+    const uint64_t wg = blockIdx.x;
+    uint32_t bi, bj;
+    tile_coords(LOCAL ? wg * part_world + part_rank : wg, bi, bj);
+    const uint64_t i0 = (uint64_t)bi * BW, j0 = (uint64_t)bj * BW;
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const int wm = wave >> 2, wn = wave & 3;
+    // loader role: panel lp, rows lk and lk + 16 of the stage, 16-iid group ld_ (stored in unit
+    // ld_ ^ xr, 16-B halves swapped by sw)
+    const int lp = t >> 8, lk = (t >> 4) & 15, ld_ = t & 15;
+    const int sw = (ld_ >> 2) & 1, xr = (lk >> 3) & 1;
+    const uint8_t* wp = P + (lp ? j0 : i0) / 4 + 4 * ld_ + (uint64_t)lk * pitch;
+    const uint8_t* wlast = P + (lp ? j0 : i0) / 4 + 4 * ld_ + (kdim - 1) * pitch;
+    const uint32_t* lp2 = lut2 + 4 * lk;
+    // transposed-read role: lane 4q+p of group g reads rows 8g+q (and +4), logical columns
+    // 16d + 4p of group d, i.e. physical unit d ^ (g & 1), half (p >> 1) ^ sw(d)
+    const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3, g1 = g & 1;
+    const int rowoff = (8 * g + q) * B3_RS + 4 * (pp & 1);
+    // A: d = 8 wm + x -> unit offset 16 (x ^ g1), half (p >> 1) ^ (x >> 2); B: d = 4 wn + y ->
+    // 16 (y ^ g1), half (p >> 1) ^ (wn & 1)
+    const int parA[2] = {16 * g1, -16 * g1};  // 16 (x ^ g1) - 16 x for even / odd x
+    const int hA[2] = {8 * (pp >> 1), 8 * ((pp >> 1) ^ 1)};
+    const int offA = rowoff + 128 * wm;
+    const int offB = rowoff + 64 * wn + 8 * ((pp >> 1) ^ (wn & 1));
+
+    f32x4 acc[8][4];
+#pragma unroll
+    for (int x = 0; x < 8; x++)
+#pragma unroll
+        for (int y = 0; y < 4; y++) acc[x][y] = (f32x4){};
+    const uint64_t nst = (kdim + SBK - 1) / SBK;
+
+    uint32_t rw[KS];
+    uint4 rl[KS];
+    auto load = [&](uint64_t st) {
+#pragma unroll
+        for (int h = 0; h < KS; h++) {
+            const uint8_t* a = wp + (st * SBK + h * BK) * pitch;
+            rw[h] = *reinterpret_cast<const uint32_t*>(a <= wlast ? a : wlast);
+            rl[h] = *reinterpret_cast<const uint4*>(lp2 + 4 * (SBK * st + h * BK));
+        }
+    };
+    auto make_sel = [&](uint32_t w, uint32_t (&sel)[8]) {
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const uint32_t v = (w >> (2 * j)) & 0x03030303u;
+            const uint32_t o = v | 0x04040404u;
+            sel[2 * j] = __builtin_amdgcn_perm(o, v, 0x05010400u);
+            sel[2 * j + 1] = __builtin_amdgcn_perm(o, v, 0x07030602u);
+        }
+    };
+    auto store_plane = [&](short* S, int pl, int h, const uint32_t (&sel)[8]) {
+        const uint32_t lo = pl == 0 ? rl[h].x : rl[h].z;
+        const uint32_t hi = pl == 0 ? rl[h].y : rl[h].w;
+        uint4 v0, v1;
+        v0.x = __builtin_amdgcn_perm(hi, lo, sel[0]);
+        v0.y = __builtin_amdgcn_perm(hi, lo, sel[1]);
+        v0.z = __builtin_amdgcn_perm(hi, lo, sel[2]);
+        v0.w = __builtin_amdgcn_perm(hi, lo, sel[3]);
+        v1.x = __builtin_amdgcn_perm(hi, lo, sel[4]);
+        v1.y = __builtin_amdgcn_perm(hi, lo, sel[5]);
+        v1.z = __builtin_amdgcn_perm(hi, lo, sel[6]);
+        v1.w = __builtin_amdgcn_perm(hi, lo, sel[7]);
+        uint4* r4 = reinterpret_cast<uint4*>(S + (lp * 2 + pl) * PLANE + (lk + BK * h) * B3_RS + 16 * (ld_ ^ xr));
+        r4[sw] = v0;
+        r4[sw ^ 1] = v1;
+    };
+    auto frag = [&](const short* S, int panel, int pl, int off) -> f16x8_t {
+        const short* b = S + (panel * 2 + pl) * PLANE + off;
+        const i16x4_t r0 = lds_tr16(b), r1 = lds_tr16(b + 4 * B3_RS);
+        return __builtin_bit_cast(f16x8_t, (i16x8_t)__builtin_shufflevector(r0, r1, 0, 1, 2, 3, 4, 5, 6, 7));
+    };
+    {
+        load(0);
+#pragma unroll
+        for (int h = 0; h < KS; h++) {
+            uint32_t sel[8];
+            make_sel(rw[h], sel);
+            store_plane(lds, 0, h, sel);
+            store_plane(lds, 1, h, sel);
+        }
+        load(nst > 1 ? 1 : 0);
+    }
+    __syncthreads();
+    if constexpr (MODE & 1) {
+        if (__builtin_amdgcn_readfirstlane(t) >= 256) __builtin_amdgcn_s_setprio(1);
+    }
+    for (uint64_t s = 0; s < nst; s++) {
+        const short* cur = lds + (s & 1) * STAGE;
+        short* nxt = lds + ((s + 1) & 1) * STAGE;
+        f16x8_t B0[4], B1[4];
+#pragma unroll
+        for (int y = 0; y < 4; y++) {
+            B0[y] = frag(cur, 1, 0, offB + 16 * y + parA[y & 1]);
+            B1[y] = frag(cur, 1, 1, offB + 16 * y + parA[y & 1]);
+        }
+        uint32_t sel[8];
+#pragma unroll
+        for (int x = 0; x < 8; x++) {
+            const int oa = offA + 16 * x + parA[x & 1] + hA[x >> 2];
+            const f16x8_t A0 = frag(cur, 0, 0, oa), A1 = frag(cur, 0, 1, oa);
+#pragma unroll
+            for (int y = 0; y < 4; y++) {
+                acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A0, B0[y], acc[x][y], 0, 0, 0);
+                acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A0, B1[y], acc[x][y], 0, 0, 0);
+                acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A1, B0[y], acc[x][y], 0, 0, 0);
+            }
+            // stage s+1's expansion rides on x = 1, 2, 4, 5; stage s+2's loads after it
+            if (x == 1) {
+                make_sel(rw[0], sel);
+                store_plane(nxt, 0, 0, sel);
+            } else if (x == 2) {
+                store_plane(nxt, 1, 0, sel);
+            } else if (x == 4) {
+                make_sel(rw[1], sel);
+                store_plane(nxt, 0, 1, sel);
+            } else if (x == 5) {
+                store_plane(nxt, 1, 1, sel);
+            } else if (x == 6) {
+                load(s + 2 < nst ? s + 2 : nst - 1);
+            }
+            if constexpr ((MODE & 2) != 0) {
+                const bool ld = x == 1 || x == 2 || x == 4 || x == 5;
+#pragma unroll
+                for (int i = 0; i < 12; i++) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+                    __builtin_amdgcn_sched_group_barrier(0x100 | 0x200, 1, 0);  // DS read / write
+                    if (ld) __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);  // VALU
+                }
+            }
+        }
+        __syncthreads();
+    }
+    epilogue_h2x<LOCAL>(acc, tiles, n, bi, bj, accumulate, lane, wm, wn, wg);
+}
+
+// k_syrk_h2q: the 16x16x32 fp16x2 SYRK with ONE wave per SIMD (4 waves, 512 registers each),
+// each wave a 128x128 quarter of the 256x256 block (8 x 8 16x16 tiles, 256 accumulators): a
+// third fewer transposed LDS reads per MFMA than the 8-wave form (32 fragments per 192 MFMAs).
+// One barrier per 32-SNP stage, placed mid-stage: before it every wave has read ALL of its
+// stage-s operands from LDS (A rows 4-7 are read beside the MFMAs of rows 0-3) and stored stage
+// s+1's planes; after it the MFMAs of rows 4-7 run beside the reads of stage s+1's B0 and A rows
+// 0-3 (published by the barrier) into free registers, and the loader may already overwrite the
+// stage-s buffer in the next stage.  B1 of a stage is read at its start and first used by the
+// third MFMA group of row 0.
+// PREB: stage s+1's B0 is read in phase B into a second register set (else B0 and B1 are read at
+// the start of each stage, the MFMAs of row 0 ordered by column block so the first waits on one)
+template <bool LOCAL = false, bool PREB = true>
+__global__ __launch_bounds__(256, 1) void k_syrk_h2q(const uint8_t* __restrict__ P, uint64_t pitch, uint64_t n,
+                                                     uint64_t kdim, const uint32_t* __restrict__ lut2,
+                                                     const uint32_t* __restrict__ flag, float* __restrict__ tiles,
+                                                     int accumulate, uint32_t part_rank = 0, uint32_t part_world = 1,
+                                                     uint64_t kslice = 0, uint64_t slice_elems = 0) {
+    constexpr int SBK = 2 * BK;  // 32 SNPs per LDS stage
+    constexpr int PLANE = 2 * B3_PLANE, STAGE = 2 * 2 * PLANE;
+    __shared__ __attribute__((aligned(16))) short lds[2 * STAGE];
+    if (*flag) return;  // a SNP of this block is outside fp16's range: k_syrk_bf3 runs instead
+    if (gridDim.y > 1) {
+        const uint64_t k0 = (uint64_t)blockIdx.y * kslice;
+        P += k0 * pitch;
+        lut2 += 4 * k0;
+        kdim = min(kslice, kdim - k0);
+        tiles += (uint64_t)blockIdx.y * slice_elems;
+    }
+    const uint64_t wg = blockIdx.x;
+    uint32_t bi, bj;
+    tile_coords(LOCAL ? wg * part_world + part_rank : wg, bi, bj);
+    const uint64_t i0 = (uint64_t)bi * BW, j0 = (uint64_t)bj * BW;
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const int wm = wave >> 1, wn = wave & 1;
+    // loader role: panel lp, rows lk + 8h (h = 0..3) of the stage, 16-iid group ld_; row lk + 8h
+    // stores group ld_ in unit ld_ ^ (h & 1), its 16-B halves swapped by sw
+    const int lp = t >> 7, lk = (t >> 4) & 7, ld_ = t & 15;
+    const int sw = (ld_ >> 2) & 1;
+    const uint8_t* wp = P + (lp ? j0 : i0) / 4 + 4 * ld_ + (uint64_t)lk * pitch;
+    const uint8_t* wlast = P + (lp ? j0 : i0) / 4 + 4 * ld_ + (kdim - 1) * pitch;
+    const uint32_t* lp2 = lut2 + 4 * lk;
+    const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3, g1 = g & 1;
+    const int rowoff = (8 * g + q) * B3_RS + 4 * (pp & 1);
+    const int par[2] = {16 * g1, -16 * g1};                       // 16 (x ^ g1) - 16 x, x even / odd
+    const int hf[2] = {8 * (pp >> 1), 8 * ((pp >> 1) ^ 1)};      // half of columns 16x.. for x < 4 / >= 4
+    const int offA = rowoff + 128 * wm, offB = rowoff + 128 * wn;
+
+    f32x4 acc[8][8];
+#pragma unroll
+    for (int x = 0; x < 8; x++)
+#pragma unroll
+        for (int y = 0; y < 8; y++) acc[x][y] = (f32x4){};
+    const uint64_t nst = (kdim + SBK - 1) / SBK;
+
+    uint32_t rw[4];
+    uint4 rl[4];
+    auto load = [&](uint64_t st) {
+#pragma unroll
+        for (int h = 0; h < 4; h++) {
+            const uint8_t* a = wp + (st * SBK + 8 * h) * pitch;
+            rw[h] = *reinterpret_cast<const uint32_t*>(a <= wlast ? a : wlast);
+            rl[h] = *reinterpret_cast<const uint4*>(lp2 + 4 * (SBK * st + 8 * h));
+        }
+    };
+    auto make_sel = [&](uint32_t w, uint32_t (&sel)[8]) {
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const uint32_t v = (w >> (2 * j)) & 0x03030303u;
+            const uint32_t o = v | 0x04040404u;
+            sel[2 * j] = __builtin_amdgcn_perm(o, v, 0x05010400u);
+            sel[2 * j + 1] = __builtin_amdgcn_perm(o, v, 0x07030602u);
+        }
+    };
+    auto store_plane = [&](short* S, int pl, int h, const uint32_t (&sel)[8]) {
+        const uint32_t lo = pl == 0 ? rl[h].x : rl[h].z;
+        const uint32_t hi = pl == 0 ? rl[h].y : rl[h].w;
+        uint4 v0, v1;
+        v0.x = __builtin_amdgcn_perm(hi, lo, sel[0]);
+        v0.y = __builtin_amdgcn_perm(hi, lo, sel[1]);
+        v0.z = __builtin_amdgcn_perm(hi, lo, sel[2]);
+        v0.w = __builtin_amdgcn_perm(hi, lo, sel[3]);
+        v1.x = __builtin_amdgcn_perm(hi, lo, sel[4]);
+        v1.y = __builtin_amdgcn_perm(hi, lo, sel[5]);
+        v1.z = __builtin_amdgcn_perm(hi, lo, sel[6]);
+        v1.w = __builtin_amdgcn_perm(hi, lo, sel[7]);
+        uint4* r4 = reinterpret_cast<uint4*>(S + (lp * 2 + pl) * PLANE + (lk + 8 * h) * B3_RS + 16 * (ld_ ^ (h & 1)));
+        r4[sw] = v0;
+        r4[sw ^ 1] = v1;
+    };
+    auto frag = [&](const short* S, int panel, int pl, int off) -> f16x8_t {
+        const short* b = S + (panel * 2 + pl) * PLANE + off;
+        const i16x4_t r0 = lds_tr16(b), r1 = lds_tr16(b + 4 * B3_RS);
+        return __builtin_bit_cast(f16x8_t, (i16x8_t)__builtin_shufflevector(r0, r1, 0, 1, 2, 3, 4, 5, 6, 7));
+    };
+    auto oA = [&](int x) { return offA + 16 * x + par[x & 1] + hf[x >> 2]; };
+    auto oB = [&](int y) { return offB + 16 * y + par[y & 1] + hf[y >> 2]; };
+    f16x8_t A0[8], A1[8], Bc0[8], Bn0[8], B1[8];
+    auto rows = [&](int x, const f16x8_t (&B0)[8]) {
+        if constexpr (PREB) {
+#pragma unroll
+            for (int y = 0; y < 8; y++) acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A0[x], B0[y], acc[x][y], 0, 0, 0);
+#pragma unroll
+            for (int y = 0; y < 8; y++) acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A1[x], B0[y], acc[x][y], 0, 0, 0);
+#pragma unroll
+            for (int y = 0; y < 8; y++) acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A0[x], B1[y], acc[x][y], 0, 0, 0);
+        } else {
+#pragma unroll
+            for (int y = 0; y < 8; y++) {
+                acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A0[x], B0[y], acc[x][y], 0, 0, 0);
+                acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A1[x], B0[y], acc[x][y], 0, 0, 0);
+                acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A0[x], B1[y], acc[x][y], 0, 0, 0);
+            }
+        }
+    };
+    {
+        load(0);
+#pragma unroll
+        for (int h = 0; h < 4; h++) {
+            uint32_t sel[8];
+            make_sel(rw[h], sel);
+            store_plane(lds, 0, h, sel);
+            store_plane(lds, 1, h, sel);
+        }
+        load(nst > 1 ? 1 : 0);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int y = 0; y < 8; y++)
+        if constexpr (PREB) Bc0[y] = frag(lds, 1, 0, oB(y));
+#pragma unroll
+    for (int x = 0; x < 4; x++) {
+        A0[x] = frag(lds, 0, 0, oA(x));
+        A1[x] = frag(lds, 0, 1, oA(x));
+    }
+    auto stage = [&](uint64_t s, f16x8_t (&B0)[8], f16x8_t (&B0n)[8]) {
+        const short* cur = lds + (s & 1) * STAGE;
+        short* nxt = lds + ((s + 1) & 1) * STAGE;
+#pragma unroll
+        for (int y = 0; y < 8; y++) {
+            if constexpr (!PREB) B0[y] = frag(cur, 1, 0, oB(y));
+            B1[y] = frag(cur, 1, 1, oB(y));
+        }
+        // phase A: rows 0-3; rows 4-7 read from cur and stage s+1 stored into nxt beside them
+#pragma unroll
+        for (int x = 0; x < 4; x++) {
+            A0[x + 4] = frag(cur, 0, 0, oA(x + 4));
+            A1[x + 4] = frag(cur, 0, 1, oA(x + 4));
+            uint32_t sel[8];
+            make_sel(rw[x], sel);
+            store_plane(nxt, 0, x, sel);
+            store_plane(nxt, 1, x, sel);
+            rows(x, B0);
+        }
+        __syncthreads();  // stage s+1 published; every wave is done reading cur
+        load(s + 2 < nst ? s + 2 : nst - 1);
+        // phase B: rows 4-7 beside the reads of stage s+1's B0 and rows 0-3
+#pragma unroll
+        for (int x = 4; x < 8; x++) {
+            if constexpr (PREB) {
+                B0n[2 * (x - 4)] = frag(nxt, 1, 0, oB(2 * (x - 4)));
+                B0n[2 * (x - 4) + 1] = frag(nxt, 1, 0, oB(2 * (x - 4) + 1));
+            }
+            rows(x, B0);
+            A0[x - 4] = frag(nxt, 0, 0, oA(x - 4));
+            A1[x - 4] = frag(nxt, 0, 1, oA(x - 4));
+        }
+    };
+    if constexpr (PREB) {
+        for (uint64_t s = 0; s < nst; s += 2) {
+            stage(s, Bc0, Bn0);
+            if (s + 1 < nst) stage(s + 1, Bn0, Bc0);
+        }
+    } else {
+        for (uint64_t s = 0; s < nst; s++) stage(s, Bc0, Bc0);
+    }
+    // epilogue: the wave's 128x128 quarter is one whole 128-tile (2bi + wm, 2bj + wn)
+    float* T;
+    uint64_t ldo;
+    if constexpr (LOCAL) {
+        T = tiles + wg * (BW * BW) + (uint64_t)(wm * 128) * BW + wn * 128;
+        ldo = BW;
+    } else {
+        const uint64_t nt128 = (n + 127) / 128;
+        const uint64_t ti = 2 * (uint64_t)bi + wm, tj = 2 * (uint64_t)bj + wn;
+        if (ti > tj || tj >= nt128) return;  // wave-uniform
+        T = tiles + (tj * (tj + 1) / 2 + ti) * (uint64_t)(BM * BM);
+        ldo = BM;
+    }
+    const int r = lane >> 4, colp = pi16(lane & 15);
+#pragma unroll
+    for (int x = 0; x < 8; x++)
+#pragma unroll
+        for (int y = 0; y < 8; y++) {
+            float* bp = T + (16 * x + r) * ldo + 16 * y + colp;
+            if (accumulate) {
+                float old[4];
+#pragma unroll
+                for (int j = 0; j < 4; j++) old[j] = bp[4 * j * ldo];
+#pragma unroll
+                for (int j = 0; j < 4; j++) acc[x][y][j] += old[j];
+            }
+#pragma unroll
+            for (int j = 0; j < 4; j++) bp[4 * j * ldo] = acc[x][y][j];
+        }
+}
+
 }  // namespace f32w
 
 // ====================================================================== f64
@@ -1880,6 +2289,16 @@ void launch_syrk_packed_bf3(const uint8_t* packed, uint64_t pitch, uint64_t n, u
         // bf16x3 (36) 300-313.
         switch (g_variant_syrk) {
 #ifdef SNPMI_UBENCH
+            // measured N=50k, 10k SNPs (profiles/r02l/): 16x16x32 MFMA runs at 2.32-2.35 GHz vs
+            // 2.06 for 32x32x16, but MFMA busy falls to 0.64-0.66 (8 waves; the 16x16 MFMA holds
+            // vector issue for 8 of its 16 cycles, so the loader's VALU + LDS issue no longer fits
+            // the gaps) and 0.60 (4 waves, 128x128 per wave): 526-539 / 496 vs 552-585 TFLOP/s
+            case 50: f32w::k_syrk_h2x<false><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles, accumulate); break;
+            case 51: f32w::k_syrk_h2x<false, 1><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles, accumulate); break;
+            case 52: f32w::k_syrk_h2x<false, 2><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles, accumulate); break;
+            case 53: f32w::k_syrk_h2x<false, 3><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles, accumulate); break;
+            case 54: f32w::k_syrk_h2q<false><<<(unsigned)g, 256, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles, accumulate); break;
+            case 55: f32w::k_syrk_h2q<false, false><<<(unsigned)g, 256, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles, accumulate); break;
             case 40: f32w::k_syrk_h2<false, 0><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles, accumulate); break;
             case 42: f32w::k_syrk_h2<false, 2><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles, accumulate); break;
             case 43: f32w::k_syrk_h2<false, 3><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles, accumulate); break;
