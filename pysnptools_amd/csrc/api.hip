@@ -584,6 +584,7 @@ static void for_z_blocks(Device& d, const uint8_t* packed, uint64_t pitch, uint6
 // barrier without the pinned VALU interleave, 35 = default kernel without split-K, 39 =
 // ablation (no loader); 4/5/20 = f32 MFMA.
 static int g_variant_syrk_split = 0;  // tuning hook: 0 = auto, 1 = off, S = force S slices
+static int g_dense_codes = 1;         // tuning / test hook: 0 = dense operands never re-encoded
 
 static bool use_bf3(int dt) {
     return dt == SNPMI_DT_F32 && (g_variant_syrk == 0 || (g_variant_syrk >= 30 && g_variant_syrk <= 59));
@@ -817,8 +818,27 @@ static const uint32_t* dense_order(Device& d, uint64_t nb, bool xcd) {
 // dense GRM operand on the device: f32 with n >= 4096 and the default variant takes the fp16x2
 // split kernel in SNP chunks of bounded stage-image scratch (falls back to the f32-MFMA
 // k_syrk256d on the device-side range flag, or when the scratch cannot be allocated)
+static void syrk_packed_auto(Device& d, const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m,
+                             const void* lut, int dt, void* tiles, int accumulate);
+
 static void syrk_dense_auto(Device& d, const void* Z, uint64_t ldz, uint64_t n, uint64_t m, int dt, void* tiles,
                             int accumulate) {
+    if (dt == SNPMI_DT_F32 && g_variant_syrk == 0 && m > 0 && g_dense_codes) {
+        // genotype-valued columns (<= 4 distinct values each, e.g. a standardized SnpData): exact
+        // re-encoding as codes + LUT, then the packed fp16x2 SYRK; one host sync for the flag
+        const uint64_t pitch = packed_pitch(n);
+        uint8_t* packed = (uint8_t*)d.get(Device::S_DPACK, m * pitch);
+        float* lut = (float*)d.get(Device::S_DLUT, m * 16 + 256);
+        unsigned int* flag = (unsigned int*)(lut + 4 * m);
+        launch_dense_codes((const float*)Z, ldz, n, m, packed, pitch, lut, flag, d.stream);
+        unsigned int f = 1;
+        SNPMI_HIP(hipMemcpyAsync(&f, flag, sizeof(f), hipMemcpyDeviceToHost, d.stream));
+        SNPMI_HIP(hipStreamSynchronize(d.stream));
+        if (f == 0) {
+            syrk_packed_auto(d, packed, pitch, n, m, lut, dt, tiles, accumulate);
+            return;
+        }
+    }
     if (dt == SNPMI_DT_F32 && g_variant_syrk == 0 && n >= 4096 && m > 0 && ldz % 256 == 0) {
         const uint64_t nb = ldz / 256;
         const uint64_t scratch = round_up(dense_h2_scratch_bytes(n, m), 256);
@@ -1023,6 +1043,7 @@ int snpmi_set_kernel_variant(const char* kernel, int variant) {
         }
         else if (std::strcmp(kernel, "syrk_split") == 0) g_variant_syrk_split = variant;
         else if (std::strcmp(kernel, "dense_chunk") == 0) g_dense_chunk = std::max(variant, 0);
+        else if (std::strcmp(kernel, "dense_codes") == 0) g_dense_codes = variant;
         else throw Error(SNPMI_E_ARG, std::string("unknown kernel ") + kernel);
     });
 }

@@ -68,7 +68,7 @@ struct Device {
     // grow-only scratch slots
     enum Slot { S_PACKED, S_PACKED2, S_IDX, S_IDX2, S_LUT, S_STATS, S_OUT, S_TILES, S_K, S_DENSE,
                 S_DENSE2, S_RED, S_SESSION, S_PACKED_B, S_ZBLK, S_IDX32, S_LUT3, S_H2, S_OUT_B, S_STATS_B,
-                S_WIN, S_NUM };
+                S_WIN, S_DPACK, S_DLUT, S_NUM };
     void* buf[S_NUM] = {};
     // chunk pipeline events (slot = chunk parity), all on-device ordering, no host spin:
     hipEvent_t staged[2] = {};    // copy stream: H2D of pinned slot done (host may refill it)
@@ -120,6 +120,10 @@ RepackPlan launch_repack_plan(const uint64_t* idx, uint64_t n_out, uint64_t n_sr
                               hipStream_t st);
 void launch_repack(const uint8_t* src, uint64_t src_pitch, uint64_t n_src, const uint64_t* idx, const RepackPlan& plan,
                    uint64_t n_out, uint64_t n_sid, uint8_t* dst, uint64_t dst_pitch, hipStream_t st);
+// dense f32 columns with <= 4 distinct values -> 2-bit codes + f32 LUT [m][4] (exact); *flag = 1
+// if any column has more (then packed/lut are incomplete)
+void launch_dense_codes(const float* Z, uint64_t ldz, uint64_t n, uint64_t m, uint8_t* packed, uint64_t pitch,
+                        float* lut, unsigned int* flag, hipStream_t st);
 void launch_dense_standardize(void* val, uint64_t rows, uint64_t cols, uint64_t ld, int order_c, int dtype,
                               int std_kind, double a, double b, int use_stats, void* stats, hipStream_t st);
 void launch_subset(const void* in, int in_dt, uint64_t rows, uint64_t cols, uint64_t k, int in_order_c,

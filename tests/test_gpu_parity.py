@@ -469,6 +469,39 @@ def test_grm_dense_session_blocks_mixed_range(m_per_block, chunk):
     assert err <= 2e-6, "GRM max|dK|/max diag = %g" % err
 
 
+@pytest.mark.parametrize("n", [300, 4200])
+@pytest.mark.parametrize("codes", [1, 0])
+def test_grm_dense_genotype_columns_reencoded(n, codes):
+    """A dense f32 operand whose columns take <= 4 distinct values (a standardized SnpData) is
+    re-encoded exactly as 2-bit codes + per-SNP LUT and runs on the packed fp16x2 SYRK (codes=1);
+    codes=0 forces the dense kernels.  Columns include -0.0 / +0.0 (distinct bit patterns), a
+    NaN-free imputed column, a constant column and a 4-valued column -- vs the f64 product of the
+    same f32 values."""
+    rng = np.random.default_rng(n)
+    m = 70
+    g = (rng.random((n, m)) < 0.3).astype(np.float64) + (rng.random((n, m)) < 0.3)
+    g[rng.random(g.shape) < 0.02] = np.nan
+    Z = g.copy(order="F")
+    O.standardize_native(Z)
+    v = Z.astype(np.float32)
+    v[:, 3] = 0.0
+    v[::2, 3] = -0.0
+    v[:, 5] = 2.5
+    v[:, 7] = np.array([1.5, -2.0, 0.25, 7.0], dtype=np.float32)[rng.integers(0, 4, n)]
+    ref = v.astype(np.float64).dot(v.astype(np.float64).T)
+    N.call("snpmi_set_kernel_variant", b"dense_codes", codes)
+    try:
+        K = np.empty((n, n), dtype=np.float32)
+        st = np.empty((m, 2), dtype=np.float32)
+        vf = np.asfortranarray(v)
+        N.call("snpmi_grm_dense_f32", N.ptr(vf), n, m, 0, N.STD_NONE, 0.0, 0.0, 0, N.ptr(st), 0, None, N.ptr(K))
+    finally:
+        N.call("snpmi_set_kernel_variant", b"dense_codes", 1)
+    grm_close(K, ref, 1e-5)
+    err = np.abs(K.astype(np.float64) - ref).max() / np.abs(np.diag(ref)).max()
+    assert err <= 2e-6, "GRM max|dK|/max diag = %g" % err
+
+
 # ---------------------------------------------------------------------------------- device API
 class Dev:
     """Tiny RAII helper over snpmi_dev_alloc/free."""

@@ -1,5 +1,8 @@
 """A/B microbenchmarks of single kernels (interleaved rounds in ONE process, HIP events).
 
+Ablation variants (snpmi_set_kernel_variant numbers the product library refuses) need the ubench
+build: `make -C pysnptools_amd/csrc ubench` and SNPMI_LIB=tools/libsnpmi_ubench.so.
+
   python tools/ubench.py decode [--n 500000 --m 8192 --variants 0,1,2,3,4,5,6]
   python tools/ubench.py syrk   [--n 50000 --m 10000]
 """
@@ -170,7 +173,9 @@ def syrk_dense(args):
     ref = None
     for rnd in range(args.rounds):
         for v in variants:
-            N.call("snpmi_set_kernel_variant", b"syrk", v)
+            # v < 0: default kernels with the genotype re-encoding off (dense stage-image path)
+            N.call("snpmi_set_kernel_variant", b"syrk", max(v, 0))
+            N.call("snpmi_set_kernel_variant", b"dense_codes", 0 if v < 0 else 1)
             ev.record(0)
             N.call("snpmi_dev_snp_stats", packed.p, pitch, n, m, 0, N.STD_UNIT, 0.0, 0.0, 0, dt, st.p, lut.p)
             N.call("snpmi_dev_decode", packed.p, pitch, n, m, lut.p, dt, 0, Z.p, ldz)
