@@ -29,6 +29,19 @@
  *     with SNPMI_E_HIP.
  *   - K outputs are n_out x n_out, symmetric; order_c selects the layout of non-square
  *     subsets produced by snpmi_kernel_subset_*.
+ *
+ * Deliberate semantics where the reference's two paths differ (the reference calls bed-reader's
+ * native standardize by default, standardizer.py:114,120, but none of its fixtures pins the
+ * native behaviour below; these follow the reference's Python path, standardizer.py:136-211,
+ * which its goldens do pin -- "parity unpinned" against bed-reader itself):
+ *   - a SNP with no observed value (n = 0) trains NaN stats and standardizes to an all-zero
+ *     column; bed-reader's native code would raise NoIndividuals.
+ *   - Beta with a trained/given mean outside [0, 2]: maf = mean/2 (folded to <= 0.5) leaves
+ *     [0, 1] and the weight is 0 -- scipy.stats.beta.pdf's value there -- so the column
+ *     standardizes to zeros; bed-reader would raise IllegalSnpMean.
+ *   - f32 stats and LUTs are computed in f64 and rounded once (the one-pass formula in f32
+ *     arithmetic misses the reference Python path by 1.47e-5 on N300); bed-reader's f32 native
+ *     path has no fixture.  The claim is "matches the reference Python path", not bed-reader.
  */
 #ifndef SNPMI_H
 #define SNPMI_H

@@ -91,7 +91,8 @@ def test_config2_100k_x_1m_beta():
 
 def test_grm_config4_50k_x_500k():
     """BASELINE configs[3] at full size: 50k iids x 500k SNPs, Unit, f32 GRM accumulated on the
-    device over 10k-SNP blocks (bf16x3 split on the bf16 MFMA).  K restricted to 96 sampled iids
+    device over 10k-SNP blocks (fp16x2 split on the fp16 MFMA, bf16x3 as its range fallback).  K
+    restricted to 96 sampled iids
     (rows AND columns, incl. iids 0 and n-1) against the f64 oracle over all 500k SNPs -- only
     those iids are decoded; stats from the code counts of every iid -- max|dK| <= 1e-5 max diag,
     and the diagonal elementwise within 1e-5."""
