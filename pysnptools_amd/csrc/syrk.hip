@@ -1366,6 +1366,13 @@ __global__ __launch_bounds__(512, 1) void k_syrk_h2(const uint8_t* __restrict__ 
             group(Ay, C0);
         }
     };
+    // MODE 7 / 8: static priority for the second- / first-dispatched half of the waves (the
+    // arbitration loser of each SIMD pair; MI355X_MICROARCH.md "Two waves per SIMD" item 4)
+    if constexpr (MODE == 7) {
+        if (__builtin_amdgcn_readfirstlane(t) >= 256) __builtin_amdgcn_s_setprio(1);
+    } else if constexpr (MODE == 8) {
+        if (__builtin_amdgcn_readfirstlane(t) < 256) __builtin_amdgcn_s_setprio(1);
+    }
     for (uint64_t s = 0; s < nst; s += 2) {
         stage(s, B0s, B1s, A0s, B0t, B1t, A0t);
         if (s + 1 < nst) stage(s + 1, B0t, B1t, A0t, B0s, B1s, A0s);
@@ -2304,6 +2311,8 @@ void launch_syrk_packed_bf3(const uint8_t* packed, uint64_t pitch, uint64_t n, u
             case 43: f32w::k_syrk_h2<false, 3><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles, accumulate); break;
             case 41: f32w::k_syrk_h2<false, 1><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles, accumulate); break;
             case 46: f32w::k_syrk_h2<false, 5><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles, accumulate); break;
+            case 47: f32w::k_syrk_h2<false, 7><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles, accumulate); break;
+            case 48: f32w::k_syrk_h2<false, 8><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles, accumulate); break;
 #endif
             default: f32w::k_syrk_h2<false, 4><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles, accumulate);
         }
