@@ -29,6 +29,13 @@
  *     with SNPMI_E_HIP.
  *   - K outputs are n_out x n_out, symmetric; order_c selects the layout of non-square
  *     subsets produced by snpmi_kernel_subset_*.
+ *   - Value and K buffers (`out`, `val`, `K_out`, `K`, subset in/out) may be HOST memory or
+ *     DEVICE memory of the current device (snpmi_dev_alloc / hipMalloc; HIP unified
+ *     addressing tells them apart).  Device buffers are computed on in place or written
+ *     directly, with no host staging: this is the array-module seam of the reference
+ *     (util/__init__.py:652-730, ARRAY_MODULE=cupy keeps SnpData/KernelData values on the GPU),
+ *     used by pysnptools_amd.hbm.  Stats and index arrays are always host memory.  A device
+ *     buffer of another device fails with SNPMI_E_ARG.
  *
  * Deliberate semantics where the reference's two paths differ (the reference calls bed-reader's
  * native standardize by default, standardizer.py:114,120, but none of its fixtures pins the

@@ -184,9 +184,13 @@ def device_count():
 
 
 def ptr(a):
-    """Raw data pointer of a NumPy array (None for None)."""
+    """Raw data pointer of a NumPy array or an HbmArray (device address; the C ABI takes host or
+    device buffers), None for None."""
     if a is None:
         return None
+    dev = getattr(a, "snpmi_ptr", None)
+    if dev is not None:
+        return dev
     return ctypes.c_void_p(a.ctypes.data)
 
 

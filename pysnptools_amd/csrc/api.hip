@@ -341,6 +341,25 @@ static const uint8_t* stage_chunk(Device& d, const BedMap& m, const uint64_t* si
 
 static void chunk_done(Device& d, int slot) { SNPMI_HIP(hipEventRecord(d.consumed[slot], d.stream)); }
 
+// Value / K buffers may be HOST or DEVICE memory (unified virtual addressing): a pointer into a
+// snpmi_dev_alloc / hipMalloc allocation of the current device is computed on in place or
+// written directly, without the host staging -- the device-resident SnpData / KernelData of
+// pysnptools_amd.hbm (the reference's array-module seam, util/__init__.py:652-730).  Stats
+// arrays stay host memory.
+static bool is_device_ptr(Device& d, const void* p) {
+    if (!p) return false;
+    hipPointerAttribute_t at;
+    if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+        (void)hipGetLastError();  // pageable host memory is unknown to HIP
+        return false;
+    }
+    if (at.type != hipMemoryTypeDevice) return false;
+    SNPMI_REQUIRE(at.device == d.id, SNPMI_E_ARG,
+                  "device buffer belongs to device " + std::to_string(at.device) + ", the call runs on device " +
+                      std::to_string(d.id));
+    return true;
+}
+
 template <typename T>
 struct DT;
 template <>
@@ -379,6 +398,12 @@ static void bed_read_impl(const char* path, uint64_t n_iid, uint64_t n_sid, int 
     const int nthreads = resolve_threads(num_threads);
     IidPlan p = plan_iids(d, iid_idx, n_iid, n_out);
     const int dt = DT<T>::v;
+    const bool dev_out = is_device_ptr(d, out);
+    // device output: decode straight into it when its columns (F) meet the 16-B vector-store
+    // alignment of k_decode_f, else through the block buffer + a device-to-device copy; C order
+    // always straight (k_decode_c_reg checks alignment itself, k_decode_c has none)
+    const bool direct = dev_out && (order_c || (reinterpret_cast<uintptr_t>(out) % 16 == 0 &&
+                                                (n_out * sizeof(T)) % 16 == 0));
     const uint64_t ldF = round_up(std::max<uint64_t>(n_out, 1), 16);
     const uint64_t C = chunk_snps(p.pitch_in + p.pitch_out + ldF * sizeof(T));
     const bool stats_out = std_kind != SNPMI_STD_NONE && !use_stats;
@@ -394,7 +419,12 @@ static void bed_read_impl(const char* path, uint64_t n_iid, uint64_t n_sid, int 
         bool valid = false;
     } pending;
     auto drain = [&](const Pending& q) {
-        if (n_out > 0) {
+        if (n_out > 0 && dev_out && !direct) {
+            SNPMI_HIP(hipStreamWaitEvent(d.copy, d.produced[q.slot], 0));
+            SNPMI_HIP(hipMemcpy2DAsync(out + q.c0 * n_out, n_out * sizeof(T), q.dev_out, ldF * sizeof(T),
+                                       n_out * sizeof(T), q.cnt, hipMemcpyDeviceToDevice, d.copy));
+            SNPMI_HIP(hipStreamSynchronize(d.copy));  // the block buffer slot is reused two chunks on
+        } else if (n_out > 0 && !dev_out) {
             if (!order_c)
                 d2h_rows(d, out + q.c0 * n_out, n_out * sizeof(T), q.dev_out, ldF * sizeof(T), n_out * sizeof(T),
                          q.cnt, nthreads, d.produced[q.slot]);
@@ -424,7 +454,10 @@ static void bed_read_impl(const char* path, uint64_t n_iid, uint64_t n_sid, int 
         q.slot = slot;
         q.st_dev = st_dev;
         q.valid = true;
-        if (n_out > 0) {
+        if (n_out > 0 && direct) {
+            if (!order_c) launch_decode(packed, p.pitch_out, n_out, cnt, lut, dt, 0, out + c0 * n_out, n_out, d.stream);
+            else launch_decode(packed, p.pitch_out, n_out, cnt, lut, dt, 1, out + c0, m_out, d.stream);
+        } else if (n_out > 0) {
             const Device::Slot os = slot ? Device::S_OUT_B : Device::S_OUT;
             if (!order_c) {
                 q.dev_out = (T*)d.get(os, cnt * ldF * sizeof(T));
@@ -484,11 +517,11 @@ static void bed_write_impl(const char* path, const T* val, uint64_t n, uint64_t 
             SNPMI_HIP(hipMemsetAsync(bad_dev, 0, sizeof(unsigned int), d.stream));
             if (!order_c) {
                 SNPMI_HIP(hipMemcpy2DAsync(dev_val, ldF * sizeof(T), val + c0 * n, n * sizeof(T), n * sizeof(T), cnt,
-                                           hipMemcpyHostToDevice, d.stream));
+                                           hipMemcpyDefault, d.stream));  // host or device values
                 launch_encode(dev_val, dt, 0, ldF, n, cnt, count_a1, dev_packed, pitch, bad_dev, d.stream);
             } else {
                 SNPMI_HIP(hipMemcpy2DAsync(dev_val, cnt * sizeof(T), val + c0, m * sizeof(T), cnt * sizeof(T), n,
-                                           hipMemcpyHostToDevice, d.stream));
+                                           hipMemcpyDefault, d.stream));
                 launch_encode(dev_val, dt, 1, cnt, n, cnt, count_a1, dev_packed, pitch, bad_dev, d.stream);
             }
             unsigned int bad = 0;
@@ -515,14 +548,17 @@ static void standardize_impl(T* val, uint64_t rows, uint64_t cols, int order_c, 
     if (cols == 0) return;
     Device& d = device();
     const size_t bytes = rows * cols * sizeof(T);
-    T* dv = (T*)d.get(Device::S_DENSE, bytes);
+    const bool dev = is_device_ptr(d, val);
+    // a device val is standardized in place (a scratch copy when only the stats are wanted)
+    T* dv = dev && apply_in_place ? val : (T*)d.get(Device::S_DENSE, bytes);
     T* ds = (T*)d.get(Device::S_STATS, cols * 2 * sizeof(T));
     const int nthreads = resolve_threads(0);
-    SNPMI_HIP(hipMemcpyAsync(dv, val, bytes, hipMemcpyHostToDevice, d.stream));
+    if (dv != val) SNPMI_HIP(hipMemcpyAsync(dv, val, bytes, dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice,
+                                           d.stream));
     if (use_stats) SNPMI_HIP(hipMemcpyAsync(ds, stats, cols * 2 * sizeof(T), hipMemcpyHostToDevice, d.stream));
     launch_dense_standardize(dv, rows, cols, order_c ? cols : rows, order_c, DT<T>::v,
                              is_beta ? SNPMI_STD_BETA : SNPMI_STD_UNIT, a, b, use_stats, ds, d.stream);
-    if (apply_in_place) d2h_bytes(d, val, dv, bytes, nthreads);
+    if (apply_in_place && !dev) d2h_bytes(d, val, dv, bytes, nthreads);
     if (!use_stats) SNPMI_HIP(hipMemcpyAsync(stats, ds, cols * 2 * sizeof(T), hipMemcpyDeviceToHost, d.stream));
     SNPMI_HIP(hipStreamSynchronize(d.stream));
 }
@@ -538,15 +574,16 @@ static void subset_impl(const S* val, uint64_t rows, uint64_t cols, uint64_t k, 
     if (nr * nc == 0) return;
     Device& d = device();
     const size_t in_bytes = rows * cols * k * sizeof(S);
-    S* dv = (S*)d.get(Device::S_DENSE, in_bytes);
+    const bool dev_in = is_device_ptr(d, val), dev_out = is_device_ptr(d, out);
+    const S* dv = dev_in ? val : (const S*)d.get(Device::S_DENSE, in_bytes);
     uint64_t* dri = (uint64_t*)d.get(Device::S_IDX, nr * 8);
     uint64_t* dci = (uint64_t*)d.get(Device::S_IDX2, nc * 8);
-    D* dout = (D*)d.get(Device::S_OUT, nr * nc * k * sizeof(D));
-    SNPMI_HIP(hipMemcpyAsync(dv, val, in_bytes, hipMemcpyHostToDevice, d.stream));
+    D* dout = dev_out ? out : (D*)d.get(Device::S_OUT, nr * nc * k * sizeof(D));
+    if (!dev_in) SNPMI_HIP(hipMemcpyAsync((S*)dv, val, in_bytes, hipMemcpyHostToDevice, d.stream));
     SNPMI_HIP(hipMemcpyAsync(dri, ri, nr * 8, hipMemcpyHostToDevice, d.stream));
     SNPMI_HIP(hipMemcpyAsync(dci, ci, nc * 8, hipMemcpyHostToDevice, d.stream));
     launch_subset(dv, DT<S>::v, rows, cols, k, in_c, dri, nr, dci, nc, out_c, dout, DT<D>::v, d.stream);
-    d2h_bytes(d, out, dout, nr * nc * k * sizeof(D), resolve_threads(0));
+    if (!dev_out) d2h_bytes(d, out, dout, nr * nc * k * sizeof(D), resolve_threads(0));
     SNPMI_HIP(hipStreamSynchronize(d.stream));
 }
 
@@ -691,17 +728,19 @@ static void grm_finish(Device& d, const T* tiles, uint64_t n, int diag_k_to_n, d
         if (std::fabs(f - 1.0) > 1e-15) scale = f;  // diag_K_to_N.py:56-59
     }
     if (n == 0) return;
-    const uint64_t rows_per = std::max<uint64_t>(1, std::min<uint64_t>(n, (1ull << 30) / (n * sizeof(T))));
+    const bool dev = is_device_ptr(d, K_out);
+    const uint64_t rows_per = dev ? n : std::max<uint64_t>(1, std::min<uint64_t>(n, (1ull << 30) / (n * sizeof(T))));
     std::vector<uint64_t> ri(rows_per);
     uint64_t* dri = (uint64_t*)d.get(Device::S_IDX2, rows_per * 8);
     for (uint64_t r0 = 0; r0 < n; r0 += rows_per) {
         const uint64_t nr = std::min(rows_per, n - r0);
         for (uint64_t r = 0; r < nr; r++) ri[r] = r0 + r;
-        T* dk = (T*)d.get(Device::S_K, nr * n * sizeof(T));
+        // a device K_out is written in one extraction launch, no host copy
+        T* dk = dev ? K_out : (T*)d.get(Device::S_K, nr * n * sizeof(T));
         SNPMI_HIP(hipStreamSynchronize(d.stream));  // ri reused across blocks
         SNPMI_HIP(hipMemcpyAsync(dri, ri.data(), nr * 8, hipMemcpyHostToDevice, d.stream));
         launch_grm_extract(tiles, n, DT<T>::v, dri, nr, nullptr, n, 1, scale, dk, d.stream);
-        d2h_rows(d, K_out + r0 * n, n * sizeof(T), dk, n * sizeof(T), n * sizeof(T), nr, resolve_threads(0));
+        if (!dev) d2h_rows(d, K_out + r0 * n, n * sizeof(T), dk, n * sizeof(T), n * sizeof(T), nr, resolve_threads(0));
     }
     SNPMI_HIP(hipStreamSynchronize(d.stream));
 }
@@ -871,7 +910,9 @@ static void grm_dense_impl(const T* val, uint64_t rows, uint64_t cols, int order
     if (cols > 0 && rows > 0) {
         if (!order_c) {
             SNPMI_HIP(hipMemcpy2DAsync(Z, ldz * sizeof(T), val, rows * sizeof(T), rows * sizeof(T), cols,
-                                       hipMemcpyHostToDevice, d.stream));
+                                       hipMemcpyDefault, d.stream));  // host or device val
+        } else if (is_device_ptr(d, val)) {
+            launch_transpose_to_f(val, rows, cols, dt, Z, ldz, d.stream);
         } else {
             T* Zc = (T*)d.get(Device::S_DENSE2, rows * cols * sizeof(T));
             SNPMI_HIP(hipMemcpyAsync(Zc, val, rows * cols * sizeof(T), hipMemcpyHostToDevice, d.stream));
@@ -895,9 +936,10 @@ static void diag_k_to_n_impl(T* K, uint64_t n, double* factor) {
     std::lock_guard<std::recursive_mutex> lk(g_call_mutex);
     if (n == 0) return;
     Device& d = device();
-    T* dk = (T*)d.get(Device::S_K, n * n * sizeof(T));
+    const bool dev = is_device_ptr(d, K);  // device K: traced and scaled in place
+    T* dk = dev ? K : (T*)d.get(Device::S_K, n * n * sizeof(T));
     double* tr = (double*)d.get(Device::S_RED, 64);
-    SNPMI_HIP(hipMemcpyAsync(dk, K, n * n * sizeof(T), hipMemcpyHostToDevice, d.stream));
+    if (!dev) SNPMI_HIP(hipMemcpyAsync(dk, K, n * n * sizeof(T), hipMemcpyHostToDevice, d.stream));
     launch_dense_trace(dk, n, DT<T>::v, tr, d.stream);
     double trace = 0;
     SNPMI_HIP(hipMemcpyAsync(&trace, tr, 8, hipMemcpyDeviceToHost, d.stream));
@@ -906,7 +948,7 @@ static void diag_k_to_n_impl(T* K, uint64_t n, double* factor) {
     if (factor) *factor = f;
     if (std::fabs(f - 1.0) > 1e-15) {
         launch_dense_scale(dk, n * n, DT<T>::v, f, d.stream);
-        SNPMI_HIP(hipMemcpyAsync(K, dk, n * n * sizeof(T), hipMemcpyDeviceToHost, d.stream));
+        if (!dev) SNPMI_HIP(hipMemcpyAsync(K, dk, n * n * sizeof(T), hipMemcpyDeviceToHost, d.stream));
         SNPMI_HIP(hipStreamSynchronize(d.stream));
     }
 }
@@ -921,8 +963,9 @@ static void snp_scale_impl(T* val, uint64_t count, double rows, int scale_only, 
         return;
     }
     Device& d = device();
-    T* dv = (T*)d.get(Device::S_DENSE, count * sizeof(T));
-    SNPMI_HIP(hipMemcpyAsync(dv, val, count * sizeof(T), hipMemcpyHostToDevice, d.stream));
+    const bool dev = is_device_ptr(d, val);  // device val: scaled in place
+    T* dv = dev ? val : (T*)d.get(Device::S_DENSE, count * sizeof(T));
+    if (!dev) SNPMI_HIP(hipMemcpyAsync(dv, val, count * sizeof(T), hipMemcpyHostToDevice, d.stream));
     double s = scale;
     if (!scale_only) {
         double* ss = (double*)d.get(Device::S_RED, 64);
@@ -936,7 +979,8 @@ static void snp_scale_impl(T* val, uint64_t count, double rows, int scale_only, 
         s = std::sqrt(f);
     }
     launch_dense_scale(dv, count, DT<T>::v, s, d.stream);
-    d2h_bytes(d, val, dv, count * sizeof(T), resolve_threads(0));
+    if (dev) SNPMI_HIP(hipStreamSynchronize(d.stream));
+    else d2h_bytes(d, val, dv, count * sizeof(T), resolve_threads(0));
 }
 
 // Z Z^T of an already standardized dense block (rows = iids, cols = SNPs, F or C) added to the
@@ -956,7 +1000,9 @@ static void grm_add_dense_impl(const T* val, uint64_t rows, uint64_t cols, int o
     T* Z = (T*)d.get(Device::S_DENSE, ldz * cols * sizeof(T));
     if (!order_c) {
         SNPMI_HIP(hipMemcpy2DAsync(Z, ldz * sizeof(T), val, rows * sizeof(T), rows * sizeof(T), cols,
-                                   hipMemcpyHostToDevice, d.stream));
+                                   hipMemcpyDefault, d.stream));  // host or device val
+    } else if (is_device_ptr(d, val)) {
+        launch_transpose_to_f(val, rows, cols, DT<T>::v, Z, ldz, d.stream);
     } else {
         T* Zc = (T*)d.get(Device::S_DENSE2, rows * cols * sizeof(T));
         SNPMI_HIP(hipMemcpyAsync(Zc, val, rows * cols * sizeof(T), hipMemcpyHostToDevice, d.stream));

@@ -21,7 +21,8 @@ class KernelData(KernelReader, PstData):
         empty = lambda count: np.empty([count, 0], dtype="str")
         self._row_property = PstData._fixup_input(None, count=len(self._row), empty_creator=empty, dtype="str")
         self._col_property = PstData._fixup_input(None, count=len(self._col), empty_creator=empty, dtype="str")
-        self._val = PstData._fixup_input_val(val, row_count=len(self._row), col_count=len(self._col))
+        self._val = PstData._fixup_input_val(val, row_count=len(self._row), col_count=len(self._col), xp=xp)
+        self._xp = xp
         self._assert_iid0_iid1(check_val=True)
         self._name = name or parent_string or ""
         self._std_string_list = []
@@ -32,7 +33,8 @@ class KernelData(KernelReader, PstData):
 
     @val.setter
     def val(self, new_value):
-        self._val = PstData._fixup_input_val(new_value, row_count=len(self._row), col_count=len(self._col))
+        self._val = PstData._fixup_input_val(new_value, row_count=len(self._row), col_count=len(self._col),
+                                             xp=self._xp)
         self._assert_iid0_iid1(check_val=True)
 
     def allclose(self, value, equal_nan=True):

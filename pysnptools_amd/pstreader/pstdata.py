@@ -12,7 +12,7 @@ class PstData(PstReader):
     """A PstReader whose values are already in memory."""
 
     def __init__(self, row, col, val, row_property=None, col_property=None, name=None, parent_string=None,
-                 copyinputs_function=None):
+                 copyinputs_function=None, xp=None):
         super(PstData, self).__init__()
         self._val = None
         self._row = PstData._fixup_input(row)
@@ -21,7 +21,8 @@ class PstData(PstReader):
             self._col = self._row
         self._row_property = PstData._fixup_input(row_property, count=len(self._row))
         self._col_property = PstData._fixup_input(col_property, count=len(self._col))
-        self._val = PstData._fixup_input_val(val, row_count=len(self._row), col_count=len(self._col))
+        self._val = PstData._fixup_input_val(val, row_count=len(self._row), col_count=len(self._col), xp=xp)
+        self._xp = xp
         self._name = name or parent_string or ""
 
     @staticmethod
@@ -35,7 +36,23 @@ class PstData(PstReader):
 
     @staticmethod
     def _fixup_input_val(input, row_count, col_count, empty_creator=None, _require_float32_64=True, xp=None):
-        if input is None:
+        """pstdata.py:139-152.  With xp = hbm a host val is copied into HBM (float32/float64 kept,
+        anything else as float64); an HbmArray stays in HBM whatever xp is."""
+        from pysnptools_amd import hbm
+        from pysnptools_amd.util import array_module
+
+        xp = array_module(xp)
+        if isinstance(input, hbm.HbmArray):
+            if _require_float32_64 and input.dtype not in (np.float32, np.float64):
+                input = input.astype(np.float64)
+        elif xp is hbm and input is not None:
+            host = np.asarray(input)
+            if _require_float32_64 and host.dtype not in (np.float32, np.float64):
+                host = host.astype(np.float64)
+            input = hbm.asarray(host)
+        if isinstance(input, hbm.HbmArray):
+            pass
+        elif input is None:
             assert row_count == 0 or col_count == 0, "If val is None, either row_count or col_count must be 0"
             input = np.empty([row_count, col_count], dtype=np.float64)
         elif not isinstance(input, np.ndarray):
@@ -74,7 +91,8 @@ class PstData(PstReader):
 
     @val.setter
     def val(self, new_value):
-        self._val = PstData._fixup_input_val(new_value, row_count=len(self._row), col_count=len(self._col))
+        self._val = PstData._fixup_input_val(new_value, row_count=len(self._row), col_count=len(self._col),
+                                             xp=getattr(self, "_xp", None))
 
     @property
     def val_shape(self):

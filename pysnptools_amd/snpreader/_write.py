@@ -19,8 +19,10 @@ def _fmt(x):
 def write_bed_body(filename, val, count_A1):
     """Genotype half of bed-reader's to_bed: values -> .bed on the GPU (snpmi_bed_write_*)."""
     from pysnptools_amd import _native as N
+    from pysnptools_amd import hbm
 
-    val = np.asarray(val)
+    if not isinstance(val, hbm.HbmArray):  # device values are encoded where they are
+        val = np.asarray(val)
     if val.dtype not in (np.float32, np.float64, np.int8):
         val = val.astype(np.float64)
     if not (val.flags["C_CONTIGUOUS"] or val.flags["F_CONTIGUOUS"]):

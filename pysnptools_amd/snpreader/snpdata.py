@@ -20,7 +20,8 @@ class SnpData(PstData, SnpReader):
         self._col_property = PstData._fixup_input(pos, count=len(self._col),
                                                   empty_creator=lambda count: np.full([count, 3], np.nan))
         self._val = PstData._fixup_input_val(val, row_count=len(self._row), col_count=len(self._col),
-                                             _require_float32_64=_require_float32_64)
+                                             _require_float32_64=_require_float32_64, xp=xp)
+        self._xp = xp
         self._assert_iid_sid_pos()
         self._name = name or parent_string or ""
         self._std_string_list = []
@@ -37,7 +38,8 @@ class SnpData(PstData, SnpReader):
 
     @val.setter
     def val(self, new_value):
-        self._val = PstData._fixup_input_val(new_value, row_count=len(self._row), col_count=len(self._col))
+        self._val = PstData._fixup_input_val(new_value, row_count=len(self._row), col_count=len(self._col),
+                                             xp=self._xp)
         self._assert_iid_sid_pos()
 
     def allclose(self, value, equal_nan=True):

@@ -4,6 +4,7 @@ Mirrors ``pysnptools.util`` (reference util/__init__.py) for the functions the B
 path uses.  ``sub_matrix`` runs as a HIP gather kernel (libsnpmi ``snpmi_subset_*``,
 replacing bed-reader's ``subset_*``, util/__init__.py:341-375).
 """
+import logging
 import os
 from types import ModuleType
 
@@ -23,24 +24,59 @@ def get_num_threads(num_threads=None):
     return os.cpu_count() or 1
 
 
+_warn_array_module_once = False
+
+
 def array_module(xp=None):
-    """The array module of the host API.  Values handed to and from the API are NumPy
-    arrays; device residency is managed inside libsnpmi (the reference's optional CuPy
-    seam, util/__init__.py:652-695, has no counterpart: the GPU path is always on)."""
+    """The array module that holds ``val`` of SnpData / KernelData (util/__init__.py:652-695):
+    the argument, else the ARRAY_MODULE environment variable, else numpy.  ``'hbm'`` selects
+    :mod:`pysnptools_amd.hbm` (values resident in the GPU's HBM; the compute is on the GPU either
+    way).  ``'cupy'`` imports CuPy if it is installed, else falls back to numpy with one warning,
+    as the reference does."""
     xp = xp or os.environ.get("ARRAY_MODULE", "numpy")
     if isinstance(xp, ModuleType):
         return xp
-    if xp in ("numpy", "cupy"):
+    if xp == "numpy":
         return np
+    if xp == "hbm":
+        from pysnptools_amd import hbm
+
+        return hbm
+    if xp == "cupy":
+        try:
+            import cupy as cp
+
+            return cp
+        except ModuleNotFoundError as e:
+            global _warn_array_module_once
+            if not _warn_array_module_once:
+                logging.warning("Using numpy. (%s)" % e)
+                _warn_array_module_once = True
+            return np
     raise ValueError("Don't know ARRAY_MODULE '%s'" % xp)
 
 
 def asnumpy(a):
-    return np.asarray(a)
+    """A NumPy array of ``a`` (device arrays are copied to the host; util/__init__.py:698-713)."""
+    if isinstance(a, np.ndarray):
+        return a
+    return a.get()
 
 
 def get_array_module(a):
+    """The array module of ``a`` (util/__init__.py:716-730)."""
+    from pysnptools_amd import hbm
+
+    if isinstance(a, hbm.HbmArray):
+        return hbm
     return np
+
+
+def _on_device(*arrays):
+    """True when values should live in HBM: any of ``arrays`` already does, or ARRAY_MODULE=hbm."""
+    from pysnptools_amd import hbm
+
+    return any(isinstance(a, hbm.HbmArray) for a in arrays) or array_module() is hbm
 
 
 def sub_matrix(val, row_index_list, col_index_list, order="A", dtype=np.float64, num_threads=None):
@@ -60,6 +96,9 @@ def sub_matrix(val, row_index_list, col_index_list, order="A", dtype=np.float64,
     ri = N.index_array(row_index_list)
     ci = N.index_array(col_index_list)
     shape = (len(ri), len(ci)) if val.ndim == 2 else (len(ri), len(ci), k)
+    from pysnptools_amd import hbm
+
+    dev = isinstance(val, hbm.HbmArray)  # a device input gives a device output (no host copy)
     if val.dtype == np.float64:
         fn, work = "snpmi_subset_f64_f64", np.float64
     elif val.dtype == np.float32:
@@ -68,7 +107,7 @@ def sub_matrix(val, row_index_list, col_index_list, order="A", dtype=np.float64,
         raise Exception("input dtype '%s' not known, only float64 and float32" % val.dtype)
     if dtype not in (np.float32, np.float64):
         raise Exception("dtype '%s' not known, only float64 and float32" % dtype)
-    out = np.empty(shape, dtype=work, order=eff)
+    out = hbm.empty(shape, dtype=work, order=eff) if dev else np.empty(shape, dtype=work, order=eff)
     if out.size:
         in_c = 1 if val.flags["C_CONTIGUOUS"] else 0
         N.call(fn, N.ptr(val), rows, cols, k, in_c, N.ptr(ri), len(ri), N.ptr(ci), len(ci),

@@ -150,3 +150,34 @@ def test_grm_partition_covers_upper_triangle_once(n, world):
             assert r0.value <= c0.value and c0.value < nb * 256
             seen.add((r0.value, c0.value))
     assert len(seen) == total
+
+
+def test_array_module_seam():
+    """util/__init__.py:652-730: numpy default, 'hbm' = the device module, 'cupy' falls back to
+    numpy when CuPy is absent (it is, in this image), unknown names raise."""
+    import types
+
+    from pysnptools_amd import _native as N
+    from pysnptools_amd import hbm
+    from pysnptools_amd.util import array_module, asnumpy, get_array_module
+
+    assert array_module() is np and array_module("numpy") is np and array_module(np) is np
+    assert array_module("hbm") is hbm and hbm.ndarray is hbm.HbmArray
+    assert array_module("cupy") is np
+    with pytest.raises(ValueError):
+        array_module("tensorflow")
+    a = np.arange(6.0).reshape(2, 3)
+    assert asnumpy(a) is a and get_array_module(a) is np
+    # the ctypes binding passes a device buffer's own address, a NumPy array's data pointer
+    fake = types.SimpleNamespace(snpmi_ptr=N.ctypes.c_void_p(0x1234))
+    assert N.ptr(fake).value == 0x1234 and N.ptr(a).value == a.ctypes.data
+
+
+def test_array_module_env(monkeypatch):
+    from pysnptools_amd import hbm
+    from pysnptools_amd.util import _on_device, array_module
+
+    monkeypatch.setenv("ARRAY_MODULE", "hbm")
+    assert array_module() is hbm and _on_device()
+    monkeypatch.setenv("ARRAY_MODULE", "numpy")
+    assert not _on_device(None, np.zeros(2))
