@@ -624,11 +624,11 @@ static int g_variant_syrk_split = 0;  // tuning hook: 0 = auto, 1 = off, S = for
 static int g_dense_codes = 1;         // tuning / test hook: 0 = dense operands never re-encoded
 
 static bool use_bf3(int dt) {
-    return dt == SNPMI_DT_F32 && (g_variant_syrk == 0 || (g_variant_syrk >= 30 && g_variant_syrk <= 59));
+    return dt == SNPMI_DT_F32 && (g_variant_syrk == 0 || (g_variant_syrk >= 30 && g_variant_syrk <= 69));
 }
 // default: the fp16x2 kernel (k_syrk_h2, 3 products) with the bf16x3 kernel as its range
 // fallback; 30-39 force bf16x3 alone
-static bool use_h2() { return g_variant_syrk == 0 || (g_variant_syrk >= 40 && g_variant_syrk <= 59); }
+static bool use_h2() { return g_variant_syrk == 0 || (g_variant_syrk >= 40 && g_variant_syrk <= 69); }
 
 // split-K slices for the bf16x3 SYRK when the 256x256-block grid leaves CUs idle in its last
 // round: minimise rounds-per-slice ceil(g*S / CUs) / S, +1% per extra slice (partial sets + the

@@ -1120,7 +1120,10 @@ __global__ __launch_bounds__(512, 1) void k_syrk_h2(const uint8_t* __restrict__ 
                                                     int accumulate, uint32_t part_rank = 0, uint32_t part_world = 1,
                                                     uint64_t kslice = 0, uint64_t slice_elems = 0) {
     // KS = 16-SNP k-steps per LDS stage (MODE 4/5: two, one barrier per 32 SNPs)
+    // MODE 10 = MODE 4 with the loader's registers double-buffered: stage s+2's codes/LUT are
+    // loaded at the START of stage s (a whole stage to arrive instead of one MFMA group)
     constexpr int KS = MODE >= 4 ? 2 : 1, SBK = KS * BK;
+    constexpr bool kLd2 = MODE == 10;
     constexpr int PLANE = KS * B3_PLANE, STAGE = 2 * 2 * PLANE;
     __shared__ __attribute__((aligned(16))) short lds[2 * STAGE];
     if (*flag) return;  // a SNP of this block is outside fp16's range: k_syrk_bf3 runs instead
@@ -1162,9 +1165,17 @@ __global__ __launch_bounds__(512, 1) void k_syrk_h2(const uint8_t* __restrict__ 
         for (int y = 0; y < 2; y++) acc[x][y] = (f32x16){};
     const uint64_t nst = (kdim + SBK - 1) / SBK;
 
-    uint32_t rw[KS];
-    uint4 rl[KS];
+    uint32_t rw[KS], rw2[KS];
+    uint4 rl[KS], rl2[KS];
     uint4 dv[KS][2][2];  // DENSE: [k-step][plane][16-B half]
+    auto load2 = [&](uint64_t st) {
+#pragma unroll
+        for (int h = 0; h < KS; h++) {
+            const uint8_t* a = wp + (st * SBK + h * BK) * pitch;
+            rw2[h] = *reinterpret_cast<const uint32_t*>(a <= wlast ? a : wlast);
+            rl2[h] = *reinterpret_cast<const uint4*>(lp2 + 4 * (SBK * st + h * BK));
+        }
+    };
     auto load = [&](uint64_t st) {
 #pragma unroll
         for (int h = 0; h < KS; h++) {
@@ -1339,6 +1350,7 @@ __global__ __launch_bounds__(512, 1) void k_syrk_h2(const uint8_t* __restrict__ 
             f16x8_t Ax[4], Ay[4], C0[2], C1[2];
             fragsA(cur, 0, 0, Ax);
             fragsA(cur, 1, 0, Ay);
+            if constexpr (kLd2) load2(s + 2 < nst ? s + 2 : nst - 1);
             uint32_t sel[8];
             group(Ax, B0);
             make_sel(rw[0], sel);
@@ -1359,7 +1371,15 @@ __global__ __launch_bounds__(512, 1) void k_syrk_h2(const uint8_t* __restrict__ 
             store_plane(nxt, 1, 1, sel);
             if constexpr (kPin) pin(std::integral_constant<int, 1>{});
             group(Ax, C1);
-            load(s + 2 < nst ? s + 2 : nst - 1);
+            if constexpr (kLd2) {
+#pragma unroll
+                for (int h = 0; h < KS; h++) {
+                    rw[h] = rw2[h];
+                    rl[h] = rl2[h];
+                }
+            } else {
+                load(s + 2 < nst ? s + 2 : nst - 1);
+            }
             __syncthreads();
             fragB(nxt, 0, 0, B0n);
             fragB(nxt, 1, 0, B1n);
@@ -1786,6 +1806,215 @@ __global__ __launch_bounds__(256, 1) void k_syrk_h2q(const uint8_t* __restrict__
             }
 #pragma unroll
             for (int j = 0; j < 4; j++) bp[4 * j * ldo] = acc[x][y][j];
+        }
+}
+
+// k_syrk_h2w: the 32x32x16 fp16x2 SYRK with ONE wave per SIMD (4 waves, up to 512 registers each):
+// each wave a 128x128 quarter of the 256x256 block (4 x 4 32x32 tiles, 256 accumulators), so a
+// 16-SNP k-step is 16 fragments (A and B, 2 planes x 4) for 48 MFMAs -- two thirds of the 8-wave
+// form's transposed LDS reads per MFMA, and the 32-cycle MFMA leaves room for the loader's VALU
+// and LDS issue that the 16x16x32 form (k_syrk_h2q) could not hide.  Same LDS image as k_syrk_h2
+// (32-SNP stages, rows lk + 8u written by 256 threads, 16-B halves swapped per bank group).
+// Per stage: k-step 1's fragments are read while k-step 0 computes; stage s+1's rows are expanded
+// and stored beside both k-steps; the barrier sits after k-step 1's first half, so the second half
+// covers the reads of stage s+1's k-step 0 (a second fragment set).
+// PIN bit 0: sched_group_barrier pins the interleave (1 MFMA, then up to 2-4 VALU / 1 DS read /
+// 1 DS write); bit 1: loader registers double-buffered by stage parity, stage s+2's codes/LUT
+// loaded at the START of stage s (a whole stage to arrive); bit 2: a scheduling barrier keeps
+// k-step 1's fragment reads at the top of the stage.
+template <bool LOCAL = false, int PIN = 0>
+__global__ __launch_bounds__(256, 1) void k_syrk_h2w(const uint8_t* __restrict__ P, uint64_t pitch, uint64_t n,
+                                                     uint64_t kdim, const uint32_t* __restrict__ lut2,
+                                                     const uint32_t* __restrict__ flag, float* __restrict__ tiles,
+                                                     int accumulate, uint32_t part_rank = 0, uint32_t part_world = 1,
+                                                     uint64_t kslice = 0, uint64_t slice_elems = 0) {
+    constexpr int SBK = 2 * BK;  // 32 SNPs per LDS stage
+    constexpr int PLANE = 2 * B3_PLANE, STAGE = 2 * 2 * PLANE;
+    __shared__ __attribute__((aligned(16))) short lds[2 * STAGE];
+    if (*flag) return;  // a SNP of this block is outside fp16's range: k_syrk_bf3 runs instead
+    if (gridDim.y > 1) {
+        const uint64_t k0 = (uint64_t)blockIdx.y * kslice;
+        P += k0 * pitch;
+        lut2 += 4 * k0;
+        kdim = min(kslice, kdim - k0);
+        tiles += (uint64_t)blockIdx.y * slice_elems;
+    }
+    const uint64_t wg = blockIdx.x;
+    uint32_t bi, bj;
+    tile_coords(LOCAL ? wg * part_world + part_rank : wg, bi, bj);
+    const uint64_t i0 = (uint64_t)bi * BW, j0 = (uint64_t)bj * BW;
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const int wm = wave >> 1, wn = wave & 1;
+    // loader: panel lp, stage rows lk + 8u (u = 0..3), 16-iid group ld_
+    const int lp = t >> 7, lk = (t >> 4) & 7, ld_ = t & 15;
+    const int sw = (ld_ >> 2) & 1;
+    const uint8_t* wp = P + (lp ? j0 : i0) / 4 + 4 * ld_ + (uint64_t)lk * pitch;
+    const uint8_t* wlast = P + (lp ? j0 : i0) / 4 + 4 * ld_ + (kdim - 1) * pitch;
+    const uint32_t* lp2 = lut2 + 4 * lk;
+    const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
+    const int rd_off = (8 * (g >> 1) + q) * B3_RS + 16 * (g & 1) + 4 * pp;
+    const int dswz = (pp >> 1) ? -8 : 8;
+
+    f32x16 acc[4][4];
+#pragma unroll
+    for (int x = 0; x < 4; x++)
+#pragma unroll
+        for (int y = 0; y < 4; y++) acc[x][y] = (f32x16){};
+    const uint64_t nst = (kdim + SBK - 1) / SBK;
+
+    struct LdRegs {
+        uint32_t w[4];
+        uint4 l[4];
+    };
+    auto load = [&](uint64_t st, LdRegs& r) {
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const uint8_t* a = wp + (st * SBK + 8 * u) * pitch;
+            r.w[u] = *reinterpret_cast<const uint32_t*>(a <= wlast ? a : wlast);
+            r.l[u] = *reinterpret_cast<const uint4*>(lp2 + 4 * (SBK * st + 8 * u));
+        }
+    };
+    auto make_sel = [&](uint32_t w, uint32_t (&sel)[8]) {
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const uint32_t v = (w >> (2 * j)) & 0x03030303u;
+            const uint32_t o = v | 0x04040404u;
+            sel[2 * j] = __builtin_amdgcn_perm(o, v, 0x05010400u);
+            sel[2 * j + 1] = __builtin_amdgcn_perm(o, v, 0x07030602u);
+        }
+    };
+    auto store_plane = [&](short* S, int pl, int u, const LdRegs& r, const uint32_t (&sel)[8]) {
+        const uint32_t lo = pl == 0 ? r.l[u].x : r.l[u].z;
+        const uint32_t hi = pl == 0 ? r.l[u].y : r.l[u].w;
+        uint4 v0, v1;
+        v0.x = __builtin_amdgcn_perm(hi, lo, sel[0]);
+        v0.y = __builtin_amdgcn_perm(hi, lo, sel[1]);
+        v0.z = __builtin_amdgcn_perm(hi, lo, sel[2]);
+        v0.w = __builtin_amdgcn_perm(hi, lo, sel[3]);
+        v1.x = __builtin_amdgcn_perm(hi, lo, sel[4]);
+        v1.y = __builtin_amdgcn_perm(hi, lo, sel[5]);
+        v1.z = __builtin_amdgcn_perm(hi, lo, sel[6]);
+        v1.w = __builtin_amdgcn_perm(hi, lo, sel[7]);
+        uint4* r4 = reinterpret_cast<uint4*>(S + (lp * 2 + pl) * PLANE + (lk + 8 * u) * B3_RS + 16 * ld_);
+        r4[sw] = v0;
+        r4[sw ^ 1] = v1;
+    };
+    auto expand = [&](short* S, int u, const LdRegs& r) {
+        uint32_t sel[8];
+        make_sel(r.w[u], sel);
+        store_plane(S, 0, u, r, sel);
+        store_plane(S, 1, u, r, sel);
+    };
+    auto frag = [&](const short* S, int panel, int pl, int h, int col, int off) -> f16x8_t {
+        const short* b = S + (panel * 2 + pl) * PLANE + h * BK * B3_RS + off + col;
+        const i16x4_t r0 = lds_tr16(b), r1 = lds_tr16(b + 4 * B3_RS);
+        return __builtin_bit_cast(f16x8_t, (i16x8_t)__builtin_shufflevector(r0, r1, 0, 1, 2, 3, 4, 5, 6, 7));
+    };
+    struct Frags {
+        f16x8_t a0[4], a1[4], b0[4], b1[4];
+    };
+    auto read = [&](const short* S, int h, Frags& F) {
+#pragma unroll
+        for (int x = 0; x < 4; x++) {
+            const int off = x >= 2 ? rd_off + dswz : rd_off;
+            F.a0[x] = frag(S, 0, 0, h, wm * 128 + 32 * x, off);
+            F.b0[x] = frag(S, 1, 0, h, wn * 128 + 32 * x, off);
+            F.a1[x] = frag(S, 0, 1, h, wm * 128 + 32 * x, off);
+            F.b1[x] = frag(S, 1, 1, h, wn * 128 + 32 * x, off);
+        }
+    };
+    auto pin = [&](auto n_other) {
+        if constexpr (PIN & 1) {
+#pragma unroll
+            for (int i = 0; i < 12; i++) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                           // MFMA
+                __builtin_amdgcn_sched_group_barrier(0x002, decltype(n_other)::value, 0);  // VALU
+                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);        // DS read
+                __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);        // DS write
+            }
+        }
+    };
+    // rows x0..x1-1 of a k-step: 3 products per 32x32 tile
+    auto rows = [&](const Frags& F, int x0, int x1) {
+#pragma unroll
+        for (int x = x0; x < x1; x++)
+#pragma unroll
+            for (int y = 0; y < 4; y++) {
+                acc[x][y] = __builtin_amdgcn_mfma_f32_32x32x16_f16(F.a0[x], F.b0[y], acc[x][y], 0, 0, 0);
+                acc[x][y] = __builtin_amdgcn_mfma_f32_32x32x16_f16(F.a0[x], F.b1[y], acc[x][y], 0, 0, 0);
+                acc[x][y] = __builtin_amdgcn_mfma_f32_32x32x16_f16(F.a1[x], F.b0[y], acc[x][y], 0, 0, 0);
+            }
+    };
+    LdRegs Ra, Rb;
+    load(0, Ra);
+#pragma unroll
+    for (int u = 0; u < 4; u++) expand(lds, u, Ra);
+    load(nst > 1 ? 1 : 0, Rb);
+    __syncthreads();
+    Frags F0, Fk;  // k-step 0 / k-step 1 fragments; F0 is refilled with stage s+1's k-step 0 once
+                   // stage s's k-step 0 is done
+    read(lds, 0, F0);
+    // the loader runs unconditionally (the last stage expands into the idle buffer, its code loads
+    // clamp to the last SNP) so the MFMAs and their VALU share basic blocks
+    // R holds stage s+1's codes/LUT (expanded during stage s); Rn receives stage s+2's
+    auto stage = [&](uint64_t s, LdRegs& R, LdRegs& Rn) {
+        const short* cur = lds + (s & 1) * STAGE;
+        short* nxt = lds + ((s + 1) & 1) * STAGE;
+        const uint64_t s2 = s + 2 < nst ? s + 2 : nst - 1;
+        read(cur, 1, Fk);
+        if constexpr (PIN & 4) __builtin_amdgcn_sched_barrier(0);
+        if constexpr (PIN & 2) load(s2, Rn);
+        rows(F0, 0, 2);
+        expand(nxt, 0, R);
+        pin(std::integral_constant<int, 2>{});
+        rows(F0, 2, 4);
+        expand(nxt, 1, R);
+        pin(std::integral_constant<int, 2>{});
+        rows(Fk, 0, 2);
+        expand(nxt, 2, R);
+        expand(nxt, 3, R);
+        pin(std::integral_constant<int, 4>{});
+        if constexpr (!(PIN & 2)) load(s2, R);
+        __syncthreads();  // stage s+1 published; every wave is done reading cur
+        read(nxt, 0, F0);
+        rows(Fk, 2, 4);
+    };
+    if constexpr (PIN & 2) {
+        for (uint64_t s = 0; s < nst; s += 2) {
+            stage(s, Rb, Ra);
+            if (s + 1 < nst) stage(s + 1, Ra, Rb);
+        }
+    } else {
+        for (uint64_t s = 0; s < nst; s++) stage(s, Rb, Rb);
+    }
+    // epilogue: the wave's 128x128 quarter is one whole 128-tile (2bi + wm, 2bj + wn)
+    float* T;
+    uint64_t ldo;
+    if constexpr (LOCAL) {
+        T = tiles + wg * (BW * BW) + (uint64_t)(wm * 128) * BW + wn * 128;
+        ldo = BW;
+    } else {
+        const uint64_t nt128 = (n + 127) / 128;
+        const uint64_t ti = 2 * (uint64_t)bi + wm, tj = 2 * (uint64_t)bj + wn;
+        if (ti > tj || tj >= nt128) return;  // wave-uniform
+        T = tiles + (tj * (tj + 1) / 2 + ti) * (uint64_t)(BM * BM);
+        ldo = BM;
+    }
+    const int hh = lane >> 5, colp = 16 * ((lane >> 4) & 1) + pi16(lane & 15);
+#pragma unroll
+    for (int x = 0; x < 4; x++)
+#pragma unroll
+        for (int y = 0; y < 4; y++) {
+            float* bp = T + (32 * x + hh) * ldo + 32 * y + colp;
+            if (accumulate) {
+                float old[16];
+#pragma unroll
+                for (int r = 0; r < 16; r++) old[r] = bp[(16 * (r >> 3) + 4 * (r & 3) + 2 * ((r >> 2) & 1)) * ldo];
+#pragma unroll
+                for (int r = 0; r < 16; r++) acc[x][y][r] += old[r];
+            }
+#pragma unroll
+            for (int r = 0; r < 16; r++) bp[(16 * (r >> 3) + 4 * (r & 3) + 2 * ((r >> 2) & 1)) * ldo] = acc[x][y][r];
         }
 }
 
@@ -2306,6 +2535,12 @@ void launch_syrk_packed_bf3(const uint8_t* packed, uint64_t pitch, uint64_t n, u
             case 53: f32w::k_syrk_h2x<false, 3><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles, accumulate); break;
             case 54: f32w::k_syrk_h2q<false><<<(unsigned)g, 256, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles, accumulate); break;
             case 55: f32w::k_syrk_h2q<false, false><<<(unsigned)g, 256, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles, accumulate); break;
+            case 56: f32w::k_syrk_h2w<false><<<(unsigned)g, 256, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles, accumulate); break;
+            case 57: f32w::k_syrk_h2w<false, 1><<<(unsigned)g, 256, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles, accumulate); break;
+            case 58: f32w::k_syrk_h2w<false, 3><<<(unsigned)g, 256, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles, accumulate); break;
+            case 59: f32w::k_syrk_h2w<false, 7><<<(unsigned)g, 256, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles, accumulate); break;
+            case 60: f32w::k_syrk_h2w<false, 2><<<(unsigned)g, 256, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles, accumulate); break;
+            case 61: f32w::k_syrk_h2w<false, 5><<<(unsigned)g, 256, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles, accumulate); break;
             case 40: f32w::k_syrk_h2<false, 0><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles, accumulate); break;
             case 42: f32w::k_syrk_h2<false, 2><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles, accumulate); break;
             case 43: f32w::k_syrk_h2<false, 3><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles, accumulate); break;
@@ -2313,6 +2548,7 @@ void launch_syrk_packed_bf3(const uint8_t* packed, uint64_t pitch, uint64_t n, u
             case 46: f32w::k_syrk_h2<false, 5><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles, accumulate); break;
             case 47: f32w::k_syrk_h2<false, 7><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles, accumulate); break;
             case 48: f32w::k_syrk_h2<false, 8><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles, accumulate); break;
+            case 62: f32w::k_syrk_h2<false, 10><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles, accumulate); break;
 #endif
             default: f32w::k_syrk_h2<false, 4><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles, accumulate);
         }

@@ -220,10 +220,11 @@ def syrk(args):
         for v in variants:
             N.call("snpmi_set_kernel_variant", b"syrk", v)
             ev.record(0)
-            N.call("snpmi_dev_syrk_packed", packed.p, pitch, n, m, lut.p, dt, tiles.p, 0)
+            N.call("snpmi_dev_syrk_packed", packed.p, pitch, n, m, lut.p, dt, tiles.p, int(args.acc and rnd > 0))
             ev.record(1)
             ts[v].append(ev.ms(0, 1))
             if rnd == 0:
+                N.call("snpmi_stream_sync")
                 chk = np.empty(min(nt_bytes // esz, 1 << 22), dtype=np.float64 if esz == 8 else np.float32)
                 N.call("snpmi_memcpy_d2h", N.ptr(chk), tiles.p, chk.nbytes)
                 if ref is None:
@@ -232,7 +233,8 @@ def syrk(args):
                 assert v in (10, 11, 12, 13, 14, 15, 39) or err < 1e-5, "variant %d differs: %g" % (v, err)
     for v in variants:
         t = np.median(ts[v])
-        print(json.dumps({"kernel": "syrk_" + args.dtype, "variant": v, "n": n, "m": m, "median_ms": t,
+        print(json.dumps({"kernel": "syrk_" + args.dtype, "variant": v, "n": n, "m": m, "accumulate": args.acc,
+                          "median_ms": t,
                           "TFLOPs": n * (n + 1) * m / t / 1e9, "frac": n * (n + 1) * m / t / 1e9 / peak}))
 
 
@@ -245,6 +247,7 @@ if __name__ == "__main__":
     p.add_argument("--dtype", default="f32")
     p.add_argument("--index", default="rev2", choices=["rev2", "random", "sorted"])
     p.add_argument("--variants", default="0,1,2,3,4,5,6")
+    p.add_argument("--acc", type=int, default=0, help="syrk: accumulate into the tiles (rounds after the first)")
     p.add_argument("--set-variant", default=None, help="kernel=variant applied once before the run")
     a = p.parse_args()
     if a.set_variant:
