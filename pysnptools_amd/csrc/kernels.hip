@@ -191,13 +191,16 @@ __device__ __forceinline__ void store_nt(V* p, const V& v) {
 // ORD (ubench-only A/B of the item order; 0 ships): 1 = each XCD takes a contiguous slice of
 // every grid pass, 2 = items column-interleaved (a wave's U items in U different columns),
 // 3 = store-only ablation (no code loads)
-template <typename T, int U, int ORD = 0>
+// CS > 0: columns visited in stride-CS order (logical column l -> (l mod R) CS + l div R, R =
+// ceil(m / CS)), so the columns in flight at once sit CS columns apart in the output
+template <typename T, int U, int ORD = 0, int CS = 0>
 __global__ __launch_bounds__(kBlock) void k_decode_f(const uint8_t* __restrict__ packed, uint64_t pitch, uint64_t n,
                                                      uint64_t m, const T* __restrict__ lut, T* __restrict__ out,
                                                      uint64_t ld) {
     const int lane = threadIdx.x & (kWave - 1);
     const uint64_t chunks = (n + 1023) / 1024;
-    const uint64_t total = chunks * m;
+    const uint64_t R = CS ? (m + CS - 1) / CS : m;
+    const uint64_t total = chunks * (CS ? R * CS : m);
     const uint64_t groups = (total + U - 1) / U;
     const uint64_t nwaves = (uint64_t)gridDim.x * (kBlock / kWave);
     uint64_t lb = blockIdx.x;
@@ -205,6 +208,7 @@ __global__ __launch_bounds__(kBlock) void k_decode_f(const uint8_t* __restrict__
     for (uint64_t gi = lb * (kBlock / kWave) + threadIdx.x / kWave; gi < groups; gi += nwaves) {
         uint32_t w[U];
         uint64_t jv[U], cv[U];
+        bool val[U];
 #pragma unroll
         for (int u = 0; u < U; u++) {
             const uint64_t it = gi * U + u;
@@ -213,14 +217,16 @@ __global__ __launch_bounds__(kBlock) void k_decode_f(const uint8_t* __restrict__
                 c = it / m;
                 j = it - c * m;
             }
+            if constexpr (CS > 0) j = (j % R) * CS + j / R;
             jv[u] = j;
             cv[u] = c;
-            const bool ok = ORD != 3 && it < total && (c * 1024 + 16 * (uint64_t)lane < n);
+            val[u] = it < total && j < m;  // wave-uniform
+            const bool ok = ORD != 3 && val[u] && (c * 1024 + 16 * (uint64_t)lane < n);
             w[u] = ok ? reinterpret_cast<const uint32_t*>(packed + j * pitch)[c * 64 + lane] : (uint32_t)lane * 0x9E3779B9u;
         }
 #pragma unroll
         for (int u = 0; u < U; u++) {
-            if (gi * U + u >= total) break;
+            if (!val[u]) continue;
             const uint64_t j = jv[u], i0 = cv[u] * 1024;
             const T l0 = lut[4 * j], l1 = lut[4 * j + 1], l2 = lut[4 * j + 2], l3 = lut[4 * j + 3];
             T* o = out + j * ld + i0;
@@ -1302,6 +1308,18 @@ void launch_decode(const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m
         const uint64_t waves = ceil_div(ceil_div(n, 1024) * m, 4);
         const unsigned g = grid_for(waves, kBlock / kWave, 256 * 16 * 8);
 #ifdef SNPMI_UBENCH
+        if (dtype == SNPMI_DT_F32 && g_variant_decode >= 24 && g_variant_decode <= 27) {
+            // columns in stride-S order (S = 8 / 16 / 32 / 64) on the XCD-sliced item order
+            const unsigned g8 = (unsigned)round_up(g, 8);
+            const float* L = (const float*)lut;
+            float* O = (float*)out;
+            if (g_variant_decode == 24) k_decode_f<float, 4, 1, 8><<<g8, kBlock, 0, st>>>(packed, pitch, n, m, L, O, ld);
+            else if (g_variant_decode == 25) k_decode_f<float, 4, 1, 16><<<g8, kBlock, 0, st>>>(packed, pitch, n, m, L, O, ld);
+            else if (g_variant_decode == 26) k_decode_f<float, 4, 1, 32><<<g8, kBlock, 0, st>>>(packed, pitch, n, m, L, O, ld);
+            else k_decode_f<float, 4, 1, 64><<<g8, kBlock, 0, st>>>(packed, pitch, n, m, L, O, ld);
+            SNPMI_LAUNCH_CHECK();
+            return;
+        }
         if (dtype == SNPMI_DT_F32 && g_variant_decode >= 20 && g_variant_decode <= 23) {
             // A/B of the item order: 20 = plain grid order, 22 = column-interleaved items,
             // 23 = store-only ablation (21 = the shipped XCD-sliced order)
