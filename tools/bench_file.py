@@ -79,6 +79,36 @@ def main():
                           "packed_GB": m * ((n + 3) // 4) / 1e9, "K_GB": n * n * 4 / 1e9,
                           "bed_write_s": t_write, "trace": float(np.trace(K.val))}), flush=True)
         del K
+        # the same with K left in HBM (ARRAY_MODULE=hbm: no 10 GB copy-out, util/__init__.py:652-730 seam)
+        os.environ["ARRAY_MODULE"] = "hbm"
+        bed[:, :2000].read_kernel(Unit(), dtype=np.float32)
+        t0 = time.perf_counter()
+        Kd = bed.read_kernel(Unit(), dtype=np.float32)
+        t_grm_d = time.perf_counter() - t0
+        kd = Kd.val[17, 17]
+        print(json.dumps({"bench": "file-backed GRM (Bed.read_kernel, f32), K resident in HBM (ARRAY_MODULE=hbm)",
+                          "n_iid": n, "n_sid": m, "seconds": t_grm_d, "TFLOPs_end_to_end": flops / t_grm_d / 1e12,
+                          "K_GB": n * n * 4 / 1e9, "K17_17": float(kd)}), flush=True)
+        t0 = time.perf_counter()
+        Kd.standardize()  # DiagKtoN in place in HBM
+        t_diag = time.perf_counter() - t0
+        print(json.dumps({"bench": "KernelData.standardize(DiagKtoN()) on the HBM-resident K", "n_iid": n,
+                          "seconds": t_diag, "GB_per_s": 2 * n * n * 4 / t_diag / 1e9}), flush=True)
+        del Kd
+        B = args.read_block
+        bed[:, :B].read(dtype=np.float32)
+        t0 = time.perf_counter()
+        vd = bed[:, :B].read(dtype=np.float32)
+        t_read_d = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        vd.standardize(Unit())
+        t_std_d = time.perf_counter() - t0
+        print(json.dumps({"bench": "file-backed read into HBM (Bed[:, :B].read, f32, F, ARRAY_MODULE=hbm) + "
+                                   "standardize in place", "n_iid": n, "snps": B, "read_seconds": t_read_d,
+                          "read_snps_per_s": B / t_read_d, "packed_GB_per_s": B * ((n + 3) // 4) / t_read_d / 1e9,
+                          "standardize_seconds": t_std_d}), flush=True)
+        del vd
+        os.environ.pop("ARRAY_MODULE")
         # the reference's default dtype (snpreader.py:528 read_kernel(..., dtype=np.float64))
         t0 = time.perf_counter()
         K = bed.read_kernel(Unit())
