@@ -182,3 +182,25 @@ def test_write_from_device_values():
     with tempfile.TemporaryDirectory() as tmp:
         b = Bed.write(os.path.join(tmp, "w.bed"), d, count_A1=False)
         assert np.array_equal(b.read().val, v, equal_nan=True)
+
+
+def test_distributed_bed_and_subsets_in_hbm(hbm_env):
+    """DistributedBed GRM (one GPU session over the 44 pieces) and SnpKernel subsets with K in HBM
+    equal the host API (snpkernel.py:78-99; the subset of a device K is gathered on the device)."""
+    import pysnptools_amd.util as U
+    from pysnptools_amd.snpreader import DistributedBed
+
+    dist = DistributedBed(os.path.join(DATA, "distributed_bed_test1"))
+    Kd = dist.read_kernel(Unit(), dtype=np.float64).val
+    assert isinstance(Kd, hbm.HbmArray)
+    sub = SnpKernel(bed("toydata"), Unit())[::2, ::3].read(dtype=np.float32).val
+    assert isinstance(sub, hbm.HbmArray) and sub.shape == (250, 167)
+    os.environ["ARRAY_MODULE"] = "numpy"
+    try:
+        Kh = dist.read_kernel(Unit(), dtype=np.float64).val
+        subh = SnpKernel(bed("toydata"), Unit())[::2, ::3].read(dtype=np.float32).val
+    finally:
+        os.environ["ARRAY_MODULE"] = "hbm"
+    assert isinstance(Kh, np.ndarray) and np.array_equal(Kd.get(), Kh)
+    assert np.array_equal(U.asnumpy(sub), subh)
+    np.testing.assert_allclose(Kh, g("dist_x")["K_unit"], rtol=1e-10, atol=1e-8)
