@@ -137,13 +137,21 @@ def repack(args):
     ev = Events(N, 2)
     variants = [int(v) for v in args.variants.split(",")]
     ts = {v: [] for v in variants}
+    ref = None
     for rnd in range(args.rounds):
         for v in variants:
             N.call("snpmi_set_kernel_variant", b"decode", v)
+            N.call("snpmi_dev_memset", dst.p, 0xA5, pitch_out * m)
             ev.record(0)
             N.call("snpmi_dev_repack", packed.p, pitch, n, didx.p, n_out, m, dst.p, pitch_out)
             ev.record(1)
             ts[v].append(ev.ms(0, 1))
+            if rnd == 0:  # every variant must produce the same bytes
+                got = np.empty((m, pitch_out), dtype=np.uint8)
+                N.call("snpmi_memcpy_d2h", N.ptr(got), dst.p, got.nbytes)
+                if ref is None:
+                    ref = got
+                assert np.array_equal(got[:, :(n_out + 3) // 4], ref[:, :(n_out + 3) // 4]), "variant %d differs" % v
     N.call("snpmi_set_kernel_variant", b"decode", 0)
     nbytes = m * ((n + 3) // 4 + (n_out + 3) // 4)
     for v in variants:
