@@ -1122,7 +1122,9 @@ __global__ __launch_bounds__(512, 1) void k_syrk_h2(const uint8_t* __restrict__ 
     // KS = 16-SNP k-steps per LDS stage (MODE 4/5: two, one barrier per 32 SNPs)
     // MODE 10 = MODE 4 with the loader's registers double-buffered: stage s+2's codes/LUT are
     // loaded at the START of stage s (a whole stage to arrive instead of one MFMA group)
+    // MODE 11: ablation of MODE 4 -- no loader after the prologue (same LDS reads, MFMAs, barriers)
     constexpr int KS = MODE >= 4 ? 2 : 1, SBK = KS * BK;
+    constexpr bool kNoLd = MODE == 11;
     constexpr bool kLd2 = MODE == 10;
     constexpr int PLANE = KS * B3_PLANE, STAGE = 2 * 2 * PLANE;
     __shared__ __attribute__((aligned(16))) short lds[2 * STAGE];
@@ -1353,22 +1355,26 @@ __global__ __launch_bounds__(512, 1) void k_syrk_h2(const uint8_t* __restrict__ 
             if constexpr (kLd2) load2(s + 2 < nst ? s + 2 : nst - 1);
             uint32_t sel[8];
             group(Ax, B0);
-            make_sel(rw[0], sel);
-            store_plane(nxt, 0, 0, sel);
+            if constexpr (!kNoLd) {
+                make_sel(rw[0], sel);
+                store_plane(nxt, 0, 0, sel);
+            }
             if constexpr (kPin) pin(std::integral_constant<int, 3>{});
             group(Ax, B1);
-            store_plane(nxt, 1, 0, sel);
+            if constexpr (!kNoLd) store_plane(nxt, 1, 0, sel);
             fragB(cur, 0, 1, C0);
             fragB(cur, 1, 1, C1);
             if constexpr (kPin) pin(std::integral_constant<int, 1>{});
             fragsA(cur, 0, 1, Ax);
             group(Ay, B0);
-            make_sel(rw[1], sel);
-            store_plane(nxt, 0, 1, sel);
+            if constexpr (!kNoLd) {
+                make_sel(rw[1], sel);
+                store_plane(nxt, 0, 1, sel);
+            }
             if constexpr (kPin) pin(std::integral_constant<int, 3>{});
             fragsA(cur, 1, 1, Ay);
             group(Ax, C0);
-            store_plane(nxt, 1, 1, sel);
+            if constexpr (!kNoLd) store_plane(nxt, 1, 1, sel);
             if constexpr (kPin) pin(std::integral_constant<int, 1>{});
             group(Ax, C1);
             if constexpr (kLd2) {
@@ -1377,7 +1383,7 @@ __global__ __launch_bounds__(512, 1) void k_syrk_h2(const uint8_t* __restrict__ 
                     rw[h] = rw2[h];
                     rl[h] = rl2[h];
                 }
-            } else {
+            } else if constexpr (!kNoLd) {
                 load(s + 2 < nst ? s + 2 : nst - 1);
             }
             __syncthreads();
@@ -2549,6 +2555,7 @@ void launch_syrk_packed_bf3(const uint8_t* packed, uint64_t pitch, uint64_t n, u
             case 47: f32w::k_syrk_h2<false, 7><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles, accumulate); break;
             case 48: f32w::k_syrk_h2<false, 8><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles, accumulate); break;
             case 62: f32w::k_syrk_h2<false, 10><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles, accumulate); break;
+            case 63: f32w::k_syrk_h2<false, 11><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles, accumulate); break;
 #endif
             default: f32w::k_syrk_h2<false, 4><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles, accumulate);
         }
