@@ -102,6 +102,7 @@ def decode_c(args):
     variants = [int(v) for v in args.variants.split(",")]
     ev = Events(N, 2)
     res = {v: [] for v in variants}
+    ref = None
     for rnd in range(args.rounds):
         for v in variants:
             N.call("snpmi_set_kernel_variant", b"decode", v)
@@ -109,6 +110,13 @@ def decode_c(args):
             N.call("snpmi_dev_decode", packed.p, pitch, n, m, lut.p, N.DT_F32, 1, out.p, m)
             ev.record(1)
             res[v].append(ev.ms(0, 1))
+            if rnd == 0:  # every variant must write the same values (first and last 64 rows)
+                got = np.empty((128, m), dtype=np.float32)
+                N.call("snpmi_memcpy_d2h", N.ptr(got[:64]), out.p, 64 * m * 4)
+                N.call("snpmi_memcpy_d2h", N.ptr(got[64:]), out.at((n - 64) * m * 4), 64 * m * 4)
+                if ref is None:
+                    ref = got
+                assert np.array_equal(got, ref), "variant %d differs" % v
     N.call("snpmi_set_kernel_variant", b"decode", 0)
     nbytes = m * ((n + 3) // 4 + 4 * n)
     for v in variants:
