@@ -594,7 +594,7 @@ static void subset_impl(const S* val, uint64_t rows, uint64_t cols, uint64_t k, 
 // MFMA-only (no VALU in its loader): 136.7 TFLOP/s vs 130.9 for the fused LUT-expanding
 // kernel (tools/ubench.py syrk / syrk_dense, N=50k, 10k SNPs).  Sub-blocks keep Z <= 16 GiB.
 static bool use_two_phase(int dt, uint64_t n) {
-    if (g_variant_syrk != 0 && g_variant_syrk != 20) return false;
+    if (g_variant_syrk != 0 && g_variant_syrk != 20 && g_variant_syrk != 71) return false;
     return dt == SNPMI_DT_F32 ? n >= 4096 : n >= 1024;
 }
 
@@ -667,8 +667,37 @@ static const uint32_t* lut_bf3(Device& d, const float* lut, uint64_t m, H2Lut* h
     return l3;
 }
 
+// f64 GRM of packed SNPs: default = the int8 MFMA residue path (syrk_crt.hip; variant 70 forces
+// it), 71 = the f64 MFMA two-phase path (decode to a dense f64 block, then k_syrk_glds).
+static bool use_crt(int dt) {
+    return dt == SNPMI_DT_F64 && (g_variant_syrk == 0 || g_variant_syrk == 70 || g_variant_syrk == 72);
+}
+
+static void syrk_packed_crt(Device& d, const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m,
+                            const double* lut, double* tiles, int accumulate) {
+    const uint64_t nb = ceil_div(n, 256), blocks = nb * (nb + 1) / 2;
+    // residue scratch: 18 bytes per element of the 256-blocks, at most 4 GiB (then chunked)
+    const uint64_t res_bytes = std::min<uint64_t>(blocks * 18ull * 65536, 4ull << 30);
+    uint8_t* res = (uint8_t*)d.get(Device::S_ZBLK, res_bytes);
+    const uint64_t step = crt_max_snps();
+    void* ws = d.get(Device::S_LUT3, crt_lut_bytes(std::min(m, step)));
+    for (uint64_t s0 = 0; s0 < m; s0 += step) {
+        const uint64_t cnt = std::min(step, m - s0);
+        const int acc = accumulate || s0 > 0;
+        launch_syrk_packed_crt(packed + s0 * pitch, pitch, n, cnt, lut + 4 * s0, tiles, acc, ws, res, res_bytes,
+                               d.stream);
+        // NaN/Inf in this chunk's LUT: the f64 MFMA kernel computes it (gated on the device flag)
+        launch_syrk_packed_f64_gated(packed + s0 * pitch, pitch, n, cnt, lut + 4 * s0, tiles, acc,
+                                     (const int*)ws + 1, d.stream);
+    }
+}
+
 static void syrk_packed_auto(Device& d, const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m,
                              const void* lut, int dt, void* tiles, int accumulate) {
+    if (use_crt(dt) && m > 0 && n > 0) {
+        syrk_packed_crt(d, packed, pitch, n, m, (const double*)lut, (double*)tiles, accumulate);
+        return;
+    }
     if (use_bf3(dt)) {
         H2Lut h2;
         const bool h = use_h2() && m > 0;
@@ -1080,9 +1109,10 @@ int snpmi_set_kernel_variant(const char* kernel, int variant) {
 #ifndef SNPMI_UBENCH
             // the product library ships the default chain and the kernels it falls back to:
             // 36 = the bf16x3 kernel alone (fp16x2 range fallback), 20 = the f32-MFMA kernels
-            // (dense-operand range fallback), 5 = the 128x128 small-N kernels; every other
-            // variant is an A/B ablation of the ubench build (make -C pysnptools_amd/csrc ubench)
-            SNPMI_REQUIRE(variant == 0 || variant == 5 || variant == 20 || variant == 36, SNPMI_E_ARG,
+            // (dense-operand range fallback), 5 = the 128x128 small-N kernels, 71 = f64 GRMs on the
+            // f64 MFMA (the CRT path's non-finite fallback); every other variant is an A/B
+            // ablation of the ubench build (make -C pysnptools_amd/csrc ubench)
+            SNPMI_REQUIRE(variant == 0 || variant == 5 || variant == 20 || variant == 36 || variant == 71, SNPMI_E_ARG,
                           "syrk variant " + std::to_string(variant) + " exists only in the ubench build");
 #endif
             g_variant_syrk = variant;

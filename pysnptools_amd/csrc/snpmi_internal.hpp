@@ -180,6 +180,18 @@ void launch_syrk_packed_bf3_split(const uint8_t* packed, uint64_t pitch, uint64_
                                   const H2Lut* h2 = nullptr);
 void launch_tile_reduce(const float* partial, unsigned slices, uint64_t elems, float* tiles, int accumulate,
                         hipStream_t st);
+// f64 GRM of packed SNPs on the int8 MFMA pipe (syrk_crt.hip): residues modulo 18 moduli, CRT
+// back to f64.  ws_lut = crt_lut_bytes(m) of scratch (its first int pair: block exponent and the
+// non-finite flag), res = residue scratch (>= 18 * 64 KiB; more = fewer launches); m <= crt_max_snps()
+uint64_t crt_max_snps();
+uint64_t crt_lut_bytes(uint64_t m);
+int crt_fraction_bits(uint64_t m);
+void launch_syrk_packed_crt(const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m, const double* lut,
+                            double* tiles, int accumulate, void* ws_lut, uint8_t* res, uint64_t res_bytes,
+                            hipStream_t st);
+// the f64-MFMA packed SYRK, run only when the device word *gate is non-zero (the CRT path's flag)
+void launch_syrk_packed_f64_gated(const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m, const double* lut,
+                                  double* tiles, int accumulate, const int* gate, hipStream_t st);
 void launch_syrk_packed_bf3_part(const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m, const uint32_t* lut3,
                                  int rank, int world, float* blocks, int accumulate, hipStream_t st,
                                  const H2Lut* h2 = nullptr);

@@ -2211,8 +2211,9 @@ __device__ __forceinline__ void epilogue(f64x4 (&acc)[4][4], double* __restrict_
 template <bool PACKED, int MODE = 0>
 __global__ __launch_bounds__(256, 2) void k_syrk(const void* __restrict__ src, uint64_t ld, uint64_t kdim,
                                                  const double* __restrict__ lut, double* __restrict__ tiles,
-                                                 int accumulate) {
+                                                 int accumulate, const int* __restrict__ gate = nullptr) {
     __shared__ __attribute__((aligned(16))) double lds[2][2][BK * LDA];
+    if (gate && *gate == 0) return;  // fallback of the CRT path: runs only when its flag is set
     uint32_t ti, tj;
     tile_coords(blockIdx.x, ti, tj);
     const uint64_t i0 = (uint64_t)ti * BM, j0 = (uint64_t)tj * BM;
@@ -2388,6 +2389,15 @@ void launch_syrk_packed(const uint8_t* packed, uint64_t pitch, uint64_t n, uint6
             default: f64k::k_syrk<true, 4><<<(unsigned)nt, 256, 0, st>>>(packed, pitch, m, L, Tt, accumulate);
         }
     }
+    SNPMI_HIP(hipGetLastError());
+}
+
+void launch_syrk_packed_f64_gated(const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m, const double* lut,
+                                  double* tiles, int accumulate, const int* gate, hipStream_t st) {
+    const uint64_t nt = n_tiles_upper(n);
+    if (nt == 0 || m == 0) return;
+    SNPMI_REQUIRE(nt < (1ull << 31), SNPMI_E_ARG, "too many GRM tiles for one launch");
+    f64k::k_syrk<true, 4><<<(unsigned)nt, 256, 0, st>>>(packed, pitch, m, lut, tiles, accumulate, gate);
     SNPMI_HIP(hipGetLastError());
 }
 

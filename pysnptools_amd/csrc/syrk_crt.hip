@@ -1,0 +1,362 @@
+// f64 GRM of packed SNPs on the int8 MFMA pipe: exact integer products in a residue number system.
+//
+// Reference: SnpReader._read_kernel (snpreader.py:637-668) accumulates K = sum_b Z_b Z_b^T in
+// float64 (the reference's default dtype).  gfx950's f64 MFMA peaks at 78.6 TFLOP/s; its int8
+// MFMA at ~5 POP/s.  Per launch (one SNP block, m SNPs):
+//   1. every LUT value a (standardized value of a SNP for one of its 4 codes) becomes the integer
+//      q = rint(a * 2^(F - e)), |q| <= 2^F, with e = the block's exponent (max |a| <= 2^e); the
+//      quantisation error is <= 2^(e - F - 1), i.e. 2^-(F+1) of the block's largest value;
+//   2. K_int = sum_s q_is q_js is an exact integer with |K_int| <= m 2^2F < P/2, P = product of
+//      R pairwise-coprime moduli p <= 128; for each modulus the int8 MFMA computes
+//      sum_s rho(q_is) rho(q_js) with rho = q mod p in (-p/2, p/2] (|rho| <= 64, exact int32
+//      accumulation for m < 2^19) and the epilogue keeps it mod p (one byte per K element);
+//   3. k_crt rebuilds K_int from its R residues (Garner's mixed-radix digits, exact), converts to
+//      f64 (Horner, one rounding per step) and adds K_int 2^(2(e - F)) to the f64 K tiles.
+// R = 18 moduli (P ~ 2^119.5): F = floor((log2 P - 1 - log2 m) / 2) = 52 at m = 10k, so every
+// value keeps all of its bits down to 2^-53 of the block's largest -- the f64 product K's own
+// rounding level.  A block whose LUT holds NaN/Inf raises a flag on the device and the f64 MFMA
+// kernel (gated on the flag) computes it instead.
+#include "snpmi_internal.hpp"
+
+#include <cmath>
+
+namespace snpmi {
+namespace {
+
+constexpr int kR = 18;
+// pairwise coprime: 2^7, 127, 5^3, 11^2, 7*17, 3^2*13, then primes
+constexpr int mod_of(int i) {
+    constexpr int m[kR] = {128, 127, 125, 121, 119, 117, 113, 109, 107, 103, 101, 97, 89, 83, 79, 73, 71, 67};
+    return m[i];
+}
+__constant__ int kMod[kR] = {128, 127, 125, 121, 119, 117, 113, 109, 107, 103, 101, 97, 89, 83, 79, 73, 71, 67};
+
+constexpr int BW = 256;    // block edge (iids)
+constexpr int SK = 128;    // SNPs per LDS stage (four 32-deep MFMA k-steps): 147 KiB of LDS, double-buffered
+constexpr int RS = 288;    // LDS bytes per SNP row (256 iids + 32: the 8 rows of a transposed read hit distinct banks)
+
+typedef int v2i __attribute__((ext_vector_type(2)));
+typedef int v4i __attribute__((ext_vector_type(4)));
+typedef int v16i __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ void tile_coords(uint64_t L, uint32_t& ti, uint32_t& tj) {
+    uint64_t j = (uint64_t)((sqrt(8.0 * (double)L + 1.0) - 1.0) * 0.5);
+    while ((j + 1) * (j + 2) / 2 <= L) j++;
+    while (j * (j + 1) / 2 > L) j--;
+    tj = (uint32_t)j;
+    ti = (uint32_t)(L - j * (j + 1) / 2);
+}
+
+__device__ __forceinline__ int pi16(int p) { return 4 * (p & 3) + (p >> 2); }
+
+// ---------------------------------------------------------------- block exponent + range flag
+// ctl[0] = e (max |a| <= 2^e, 0 for an all-zero block), ctl[1] = 1 if any LUT value is NaN/Inf
+__global__ __launch_bounds__(1024) void k_crt_exp(const double* __restrict__ lut, uint64_t cnt, int* __restrict__ ctl) {
+    double M = 0.0;
+    int bad = 0;
+    for (uint64_t i = threadIdx.x; i < cnt; i += 1024) {
+        const double v = lut[i];
+        if (!isfinite(v)) bad = 1;
+        else M = fmax(M, fabs(v));
+    }
+    __shared__ double red[1024];
+    __shared__ int rb[1024];
+    red[threadIdx.x] = M;
+    rb[threadIdx.x] = bad;
+    __syncthreads();
+    for (int w = 512; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w) {
+            red[threadIdx.x] = fmax(red[threadIdx.x], red[threadIdx.x + w]);
+            rb[threadIdx.x] |= rb[threadIdx.x + w];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        int e = 0;
+        if (red[0] > 0.0) frexp(red[0], &e);  // red = f 2^e, f in [0.5, 1)
+        ctl[0] = e;
+        ctl[1] = rb[0];
+    }
+}
+
+// residue LUT: lutr[r * mpad + s] byte c = rho_r(q_s[c]) (int8), zero for s >= m
+__global__ __launch_bounds__(256) void k_crt_lut(const double* __restrict__ lut, uint64_t m, uint64_t mpad, int F,
+                                                 const int* __restrict__ ctl, uint32_t* __restrict__ lutr) {
+    const uint64_t s = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (s >= mpad) return;
+    const int e = ctl[0];
+    long long q[4];
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+        const double a = s < m && !ctl[1] ? lut[4 * s + c] : 0.0;
+        q[c] = (long long)rint(ldexp(a, F - e));
+    }
+#pragma unroll
+    for (int r = 0; r < kR; r++) {
+        const long long p = kMod[r];
+        uint32_t w = 0;
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+            long long x = q[c] % p;
+            if (x < 0) x += p;
+            if (x >= (p + 1) / 2) x -= p;  // (-p/2, p/2]: [-64, 63] for 128, +-(p-1)/2 otherwise
+            w |= ((uint32_t)x & 0xffu) << (8 * c);
+        }
+        lutr[(uint64_t)r * mpad + s] = w;
+    }
+}
+
+__device__ __forceinline__ v2i lds_tr8(const uint8_t* p) {
+    return __builtin_amdgcn_ds_read_tr8_b64_v2i32((__attribute__((address_space(3))) v2i*)p);
+}
+
+// ---------------------------------------------------------------- residue SYRK
+// grid (blocks of this chunk, R): block (bi, bj) = upper-triangle 256-block b0 + blockIdx.x,
+// modulus kMod[blockIdx.y].  8 waves (2 x 4), each 128 x 64 = 4 x 2 v_mfma_i32_32x32x32_i8 tiles.
+// LDS: per stage and panel SKT SNP rows x 256 iids of int8 residues ([k][iid], RS-byte rows, the
+// 16 iids of a group in pi16 order as the loader's byte permutes leave them), double-buffered.
+// Loader: thread (panel lp, 16-iid group d, row block kq) expands SKT/16 consecutive SNP rows
+// per stage: one code dword per row, 16-B LUT loads, 4 v_perm per row.  MFMA operand
+// (32x32x32 i8): lane l holds row l&31, k = 16(l>>5) + j (j < 16), read as two
+// ds_read_b64_tr_b8 of 8 SNP rows: within a 16-lane group, lane 2j+p addresses row j, bytes
+// 8p..8p+7 and receives column (its group-lane index) of the 8 rows (tools/probe/tr8_probe.hip).
+// Per 32-SNP k-step: the next k-step's fragments are read under this one's 8 MFMAs, and a
+// share of the next stage's rows is expanded and stored; one barrier per stage.
+// Epilogue: residue of each int32 sum, one byte per element, written as a dense 256 x 256 block
+// (true iid order) at res + (blockIdx.y * nblk + blockIdx.x) * 65536.
+template <int SKT>
+__global__ __launch_bounds__(512, 1) void k_syrk_i8r(const uint8_t* __restrict__ P, uint64_t pitch, uint64_t kdim,
+                                                     uint64_t mpad, const uint32_t* __restrict__ lutr,
+                                                     const int* __restrict__ ctl, uint64_t b0, uint64_t nblk,
+                                                     uint8_t* __restrict__ res) {
+    constexpr int KS = SKT / 32, RPT = SKT / 16, PNL = SKT * RS, STG = 2 * PNL;
+    __shared__ __attribute__((aligned(16))) uint8_t lds[2 * STG];
+    if (ctl[1]) return;  // non-finite LUT: the f64 MFMA kernel runs instead
+    const int r = blockIdx.y;
+    const uint32_t* lr = lutr + (uint64_t)r * mpad;
+    uint32_t bi, bj;
+    tile_coords(b0 + blockIdx.x, bi, bj);
+    const uint64_t i0 = (uint64_t)bi * BW, j0 = (uint64_t)bj * BW;
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const int wm = wave >> 2, wn = wave & 3;
+    // loader role: panel lp, rows RPT kq .. RPT kq + RPT-1 of the stage, 16-iid group d
+    const int lp = t >> 8, kq = (t >> 4) & 15, d = t & 15;
+    const uint8_t* wp = P + (lp ? j0 : i0) / 4 + 4 * d + (uint64_t)(RPT * kq) * pitch;
+    const uint8_t* wlast = P + (lp ? j0 : i0) / 4 + 4 * d + (kdim - 1) * pitch;
+    const uint32_t* lq = lr + RPT * kq;
+    // transposed-read role: group g = lane>>4 covers k half h = g>>1 and columns 16(g&1)..+15
+    const int g = lane >> 4, jj = (lane & 15) >> 1, pp = lane & 1;
+    const int rd = (16 * (g >> 1) + jj) * RS + 16 * (g & 1) + 8 * pp;
+
+    v16i acc[4][2];
+#pragma unroll
+    for (int x = 0; x < 4; x++)
+#pragma unroll
+        for (int y = 0; y < 2; y++) acc[x][y] = (v16i){};
+    const uint64_t nst = (kdim + SKT - 1) / SKT;
+
+    uint32_t cw[RPT];
+    uint4 cl[RPT / 4];
+    auto load = [&](uint64_t st) {
+#pragma unroll
+        for (int h = 0; h < RPT; h++) {
+            const uint8_t* a = wp + (st * SKT + h) * pitch;
+            cw[h] = *reinterpret_cast<const uint32_t*>(a <= wlast ? a : wlast);
+        }
+#pragma unroll
+        for (int u = 0; u < RPT / 4; u++)  // lutr is zero-padded to mpad >= nst * SKT
+            cl[u] = *reinterpret_cast<const uint4*>(lq + SKT * st + 4 * u);
+    };
+    auto store = [&](uint8_t* S, int h0, int h1) {
+#pragma unroll
+        for (int h = h0; h < h1; h++) {
+            const uint4 c4 = cl[h >> 2];
+            const uint32_t L = (h & 3) == 0 ? c4.x : (h & 3) == 1 ? c4.y : (h & 3) == 2 ? c4.z : c4.w;
+            uint4 o;
+            o.x = __builtin_amdgcn_perm(L, L, cw[h] & 0x03030303u);
+            o.y = __builtin_amdgcn_perm(L, L, (cw[h] >> 2) & 0x03030303u);
+            o.z = __builtin_amdgcn_perm(L, L, (cw[h] >> 4) & 0x03030303u);
+            o.w = __builtin_amdgcn_perm(L, L, (cw[h] >> 6) & 0x03030303u);
+            *reinterpret_cast<uint4*>(S + lp * PNL + (RPT * kq + h) * RS + 16 * d) = o;
+        }
+    };
+    auto frag = [&](const uint8_t* S, int panel, int ks, int col) -> v4i {
+        const uint8_t* b = S + panel * PNL + 32 * ks * RS + rd + col;
+        const v2i x = lds_tr8(b), y = lds_tr8(b + 8 * RS);
+        return (v4i){x.x, x.y, y.x, y.y};
+    };
+    auto frags = [&](const uint8_t* S, int ks, v4i (&A)[4], v4i (&B)[2]) {
+#pragma unroll
+        for (int x = 0; x < 4; x++) A[x] = frag(S, 0, ks, wm * 128 + 32 * x);
+#pragma unroll
+        for (int y = 0; y < 2; y++) B[y] = frag(S, 1, ks, wn * 64 + 32 * y);
+    };
+
+    load(0);
+    store(lds, 0, RPT);
+    load(nst > 1 ? 1 : 0);
+    __syncthreads();
+    for (uint64_t s = 0; s < nst; s++) {
+        const uint8_t* cur = lds + (s & 1) * STG;
+        uint8_t* nxt = lds + ((s + 1) & 1) * STG;
+        const bool more = s + 1 < nst;
+        v4i a[2][4], b[2][2];
+        frags(cur, 0, a[0], b[0]);
+#pragma unroll
+        for (int ks = 0; ks < KS; ks++) {
+            if (ks + 1 < KS) frags(cur, ks + 1, a[(ks + 1) & 1], b[(ks + 1) & 1]);
+#pragma unroll
+            for (int x = 0; x < 4; x++)
+#pragma unroll
+                for (int y = 0; y < 2; y++)
+                    acc[x][y] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[ks & 1][x], b[ks & 1][y], acc[x][y], 0, 0, 0);
+            if (more) store(nxt, ks * RPT / KS, (ks + 1) * RPT / KS);
+        }
+        if (more) load(s + 2 < nst ? s + 2 : nst - 1);
+        __syncthreads();
+    }
+    // epilogue: acc mod p -> [0, p), one byte per element at its true (row, col) in the block
+    const int p = kMod[r];
+    const double invp = 1.0 / (double)p;
+    uint8_t* O = res + ((uint64_t)r * nblk + blockIdx.x) * (BW * BW);
+    const int hh = lane >> 5, colp = 16 * ((lane >> 4) & 1) + pi16(lane & 15);
+#pragma unroll
+    for (int x = 0; x < 4; x++)
+#pragma unroll
+        for (int y = 0; y < 2; y++) {
+            uint8_t* bp = O + (wm * 128 + 32 * x + hh) * BW + wn * 64 + 32 * y + colp;
+#pragma unroll
+            for (int q = 0; q < 16; q++) {
+                const int v = acc[x][y][q];
+                int rr = v - p * (int)floor((double)v * invp);
+                rr += rr < 0 ? p : 0;
+                rr -= rr >= p ? p : 0;
+                bp[(16 * (q >> 3) + 4 * (q & 3) + 2 * ((q >> 2) & 1)) * BW] = (uint8_t)rr;
+            }
+        }
+}
+
+// ---------------------------------------------------------------- reconstruction
+// one thread per element of the chunk's 256-blocks; residues of the R planes -> K_int (Garner,
+// exact: all digit arithmetic is on integers < 2^24 held in f32) -> f64 -> K tiles.
+template <int I>
+struct Garner {
+    // y = (sum_{j<I} v_j W_j) mod p_I by Horner over the digits, W_j = prod_{k<j} p_k
+    __device__ static __forceinline__ float prefix_mod(const float (&v)[kR]) {
+        constexpr float p = (float)mod_of(I), ip = 1.0f / (float)mod_of(I);
+        float y = v[I - 1];
+#pragma unroll
+        for (int j = I - 2; j >= 0; j--) {
+            y = fmaf(y, (float)mod_of(j), v[j]);       // |y| < 2^15, exact
+            y = fmaf(-p, rintf(y * ip), y);         // y mod p in [-p/2, p/2]
+        }
+        return y;
+    }
+};
+
+// inverse of W_i = prod_{j<i} p_j modulo p_i (host-computed, passed by value)
+struct CrtConst {
+    float inv[kR];
+};
+
+__global__ __launch_bounds__(256) void k_crt(const uint8_t* __restrict__ res, uint64_t b0, uint64_t nblk, uint64_t n,
+                                             const int* __restrict__ ctl, int F, CrtConst cc, double* __restrict__ tiles,
+                                             int accumulate) {
+    if (ctl[1]) return;
+    const uint64_t blk = blockIdx.x >> 8;  // 256 threads x 256 rows per 256-block
+    const int row = blockIdx.x & 255, col = threadIdx.x;
+    uint32_t bi, bj;
+    tile_coords(b0 + blk, bi, bj);
+    const uint64_t ti = 2 * (uint64_t)bi + (row >> 7), tj = 2 * (uint64_t)bj + (col >> 7);
+    const uint64_t nt128 = (n + 127) / 128;
+    if (ti > tj || tj >= nt128) return;
+    const uint64_t e_off = (blk * BW + row) * BW + col;
+    float v[kR];
+    {
+        const int r0 = res[e_off];
+        v[0] = (float)(r0 >= 64 ? r0 - 128 : r0);
+    }
+#define SNPMI_CRT_DIGIT(I)                                                                   \
+    if constexpr (I < kR) {                                                                  \
+        constexpr float p = (float)mod_of(I), ip = 1.0f / (float)mod_of(I);                     \
+        const float ri = (float)res[(uint64_t)(I) * nblk * (BW * BW) + e_off];               \
+        float y = Garner<I>::prefix_mod(v);                                                  \
+        y = (ri - y) * cc.inv[I];                                  /* |.| < 2^15: exact */   \
+        v[I] = fmaf(-p, rintf(y * ip), y);                         /* odd p: no ties */      \
+    }
+    SNPMI_CRT_DIGIT(1) SNPMI_CRT_DIGIT(2) SNPMI_CRT_DIGIT(3) SNPMI_CRT_DIGIT(4) SNPMI_CRT_DIGIT(5)
+    SNPMI_CRT_DIGIT(6) SNPMI_CRT_DIGIT(7) SNPMI_CRT_DIGIT(8) SNPMI_CRT_DIGIT(9) SNPMI_CRT_DIGIT(10)
+    SNPMI_CRT_DIGIT(11) SNPMI_CRT_DIGIT(12) SNPMI_CRT_DIGIT(13) SNPMI_CRT_DIGIT(14) SNPMI_CRT_DIGIT(15)
+    SNPMI_CRT_DIGIT(16) SNPMI_CRT_DIGIT(17)
+#undef SNPMI_CRT_DIGIT
+    double X = (double)v[kR - 1];
+#pragma unroll
+    for (int i = kR - 2; i >= 0; i--) X = fma(X, (double)mod_of(i), (double)v[i]);
+    const double k = ldexp(X, 2 * (ctl[0] - F));
+    double* T = tiles + (tj * (tj + 1) / 2 + ti) * (uint64_t)(128 * 128) + (row & 127) * 128 + (col & 127);
+    *T = accumulate ? *T + k : k;
+}
+
+}  // namespace
+
+// --------------------------------------------------------------------------- host side
+static double log2_modulus_product() {
+    double s = 0;
+    for (int i = 0; i < kR; i++) s += std::log2((double)mod_of(i));
+    return s;
+}
+
+static CrtConst crt_constants() {
+    CrtConst c{};
+    c.inv[0] = 1.0f;
+    for (int i = 1; i < kR; i++) {
+        const long p = mod_of(i);
+        long w = 1;
+        for (int j = 0; j < i; j++) w = w * (mod_of(j) % p) % p;
+        long inv = 1;
+        while ((w * inv) % p != 1) inv++;
+        c.inv[i] = (float)inv;
+    }
+    return c;
+}
+
+// largest F with 2 m 2^2F < P (|K_int| <= m 2^2F must sit inside (-P/2, P/2))
+int crt_fraction_bits(uint64_t m) {
+    const double f = (log2_modulus_product() - 1.0 - std::log2((double)std::max<uint64_t>(m, 1)) - 1e-9) / 2.0;
+    return std::min(52, (int)std::floor(f));
+}
+
+uint64_t crt_max_snps() { return 1ull << 16; }  // keeps F >= 50 and the int32 sums exact
+
+uint64_t crt_lut_bytes(uint64_t m) { return (uint64_t)kR * round_up(std::max<uint64_t>(m, 1), SK) * 4 + 256; }
+
+// K_tiles (+)= Z Z^T for packed codes + f64 LUT; ws_lut: crt_lut_bytes(m); res: res_bytes of
+// scratch (>= kR * 65536); gate: device u32 set when the block must run on the f64 MFMA instead
+void launch_syrk_packed_crt(const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m, const double* lut,
+                            double* tiles, int accumulate, void* ws_lut, uint8_t* res, uint64_t res_bytes,
+                            hipStream_t st) {
+    SNPMI_REQUIRE(m > 0 && m <= crt_max_snps(), SNPMI_E_ARG, "crt SYRK: SNP count per launch out of range");
+    const uint64_t nb = ceil_div(n, BW), total = nb * (nb + 1) / 2;
+    const uint64_t mpad = round_up(m, SK);
+    int* ctl = (int*)ws_lut;
+    uint32_t* lutr = (uint32_t*)((uint8_t*)ws_lut + 256);
+    const int F = crt_fraction_bits(m);
+    k_crt_exp<<<1, 1024, 0, st>>>(lut, 4 * m, ctl);
+    k_crt_lut<<<(unsigned)ceil_div(mpad, 256), 256, 0, st>>>(lut, m, mpad, F, ctl, lutr);
+    const uint64_t per = std::max<uint64_t>(1, res_bytes / ((uint64_t)kR * BW * BW));
+    static const CrtConst cc = crt_constants();
+    for (uint64_t b0 = 0; b0 < total; b0 += per) {
+        const uint64_t cnt = std::min(per, total - b0);
+        SNPMI_REQUIRE(cnt < (1ull << 23), SNPMI_E_ARG, "crt SYRK: chunk too large");
+#ifdef SNPMI_UBENCH
+        if (g_variant_syrk == 72)  // 64-SNP stages (73.7 KiB of LDS)
+            k_syrk_i8r<64><<<dim3((unsigned)cnt, kR), 512, 0, st>>>(packed, pitch, m, mpad, lutr, ctl, b0, cnt, res);
+        else
+#endif
+        k_syrk_i8r<SK><<<dim3((unsigned)cnt, kR), 512, 0, st>>>(packed, pitch, m, mpad, lutr, ctl, b0, cnt, res);
+        k_crt<<<(unsigned)(cnt * 256), 256, 0, st>>>(res, b0, cnt, n, ctl, F, cc, tiles, accumulate);
+    }
+    SNPMI_HIP(hipGetLastError());
+}
+
+}  // namespace snpmi

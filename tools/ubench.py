@@ -230,6 +230,7 @@ def syrk(args):
     ev = Events(N, 2)
     variants = [int(v) for v in args.variants.split(",")]
     ts = {v: [] for v in variants}
+    errs = {}
     ref = None
     nt_bytes = N.lib().snpmi_grm_tile_bytes(n, dt)
     for rnd in range(args.rounds):
@@ -246,11 +247,12 @@ def syrk(args):
                 if ref is None:
                     ref = chk.copy()
                 err = np.abs(chk.astype(np.float64) - ref).max() / max(np.abs(ref).max(), 1)
+                errs[v] = float(err)
                 assert v in (10, 11, 12, 13, 14, 15, 39, 63) or err < 1e-5, "variant %d differs: %g" % (v, err)
     for v in variants:
         t = np.median(ts[v])
         print(json.dumps({"kernel": "syrk_" + args.dtype, "variant": v, "n": n, "m": m, "accumulate": args.acc,
-                          "median_ms": t,
+                          "median_ms": t, "err_vs_first": errs.get(v),
                           "TFLOPs": n * (n + 1) * m / t / 1e9, "frac": n * (n + 1) * m / t / 1e9 / peak}))
 
 
