@@ -21,7 +21,11 @@ Metric (BASELINE.json): "SNPs/sec standardized (500k x 1M) + GRM GF/s at 1/2/4/8
                outside fp16's range).  gflops uses N(N+1)M (SYRK work); roofline
                vs 2.5 PF fp16 dense / 3 = 833.3 TF (the f32-MFMA peak is 157.3).
   grm_f64    = the same GRM in float64 (the reference's default dtype, snpreader.py:528,623) on
-               the f64 MFMA (78.6 TF dense).
+               the int8 MFMA: each block's LUT quantised to 51-52-bit integers, K_int computed
+               exactly modulo 15 coprime moduli <= 256 (one int8 SYRK each), rebuilt by CRT and
+               added to the f64 K (syrk_crt.hip).  roofline vs the int8 dense peak (2 x bf16 =
+               5.0 POP/s) on the executed ops; f64_equiv_tflops = N(N+1)M / time, beside the f64
+               MFMA's 78.6 TF dense peak.
   grm5       = configs[4] shape: 500k iids, K (500 GB f32 upper triangle) partitioned over the 8
                ranks of the 8-GPU plan as 256x256 blocks; this process computes part `rank` of
                max(N, 8) for one 8192-SNP block uploaded from pinned host memory inside the timed
@@ -61,6 +65,9 @@ MFMA_BF16_PEAK_TFLOPS = 2500.0
 # products of the fp16x2 split (k_syrk_h2; Unit LUTs always fit fp16's range)
 SPLIT_PRODUCTS = 3
 SPLIT_PEAK_TFLOPS = MFMA_BF16_PEAK_TFLOPS / SPLIT_PRODUCTS
+# f64 GRM on the int8 MFMA pipe (i8 = 2x the bf16 rate): one int8 SYRK per modulus
+MFMA_I8_PEAK_TOPS = 2 * MFMA_BF16_PEAK_TFLOPS
+CRT_MODULI = 15  # kR, pysnptools_amd/csrc/syrk_crt.hip
 GRM5_PLAN_WORLD = 8  # configs[4] is an 8-GPU plan
 
 
@@ -784,11 +791,20 @@ def grm_entry(args, dist, r, dtype):
                      "f32_mfma_peak": MFMA_F32_PEAK_TFLOPS,
                      "mfma_util_executed": r["mean_tflops"] * r["exec_ratio"] / MFMA_BF16_PEAK_TFLOPS})
     else:
-        roof.update({"traffic": None,
-                     "kernel": "k_decode_f<double> into Z + f64k::k_syrk_glds (v_mfma_f64_16x16x4_f64, operand rows "
-                               "by global_load_lds); peak = 78.6 TF f64 dense"})
+        nb = (n + 255) // 256
+        ops = CRT_MODULI * 2 * 256 * 256 * (nb * (nb + 1) // 2) * args.grm_block  # executed int8 ops per launch
+        launch_s = (np.mean(r["syrk_ms"]) * 1e-3) if r["syrk_ms"] else float("nan")
+        achieved = ops / launch_s / 1e12
+        roof = {"bound": "mfma", "achieved": achieved, "peak": MFMA_I8_PEAK_TOPS, "unit": "TOP/s",
+                "frac": achieved / MFMA_I8_PEAK_TOPS, "per_launch_ops": ops, "traffic": None,
+                "f64_equiv_tflops": r["mean_tflops"], "f64_mfma_peak": MFMA_F64_PEAK_TFLOPS,
+                "vs_f64_mfma_peak": r["mean_tflops"] / MFMA_F64_PEAK_TFLOPS,
+                "kernel": "k_syrk_i8r (v_mfma_i32_32x32x32_i8; grid = 256-blocks of a tile chunk x 15 moduli) + k_crt "
+                          "(Garner) + k_crt_exp/k_crt_lut; achieved = executed int8 ops (15 moduli x full "
+                          "256-blocks) / the whole per-block time"}
     return {"workload": "cfg4: %d iid x %d SNP, Unit, block %d, %s SYRK, SNPs split into %d contiguous shard(s) "
-                        "streamed in blocks%s" % (n, m, args.grm_block, "f32 (fp16x2 MFMA)" if f32 else "f64 (f64 MFMA)",
+                        "streamed in blocks%s" % (n, m, args.grm_block, "f32 (fp16x2 MFMA)" if f32 else
+                                                 "f64 (int8 MFMA residues + CRT)",
                                                  dist.world, ", RCCL all-reduce of K tiles" if dist.rccl else ""),
             "gflops": gf, "snps_per_s": m / r["wall"], "seconds": r["wall"], "scaling": "strong",
             "allreduce_ms": r["allreduce_ms"], "trace_K": r["trace"], "roofline": roof}

@@ -676,8 +676,8 @@ static bool use_crt(int dt) {
 static void syrk_packed_crt(Device& d, const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m,
                             const double* lut, double* tiles, int accumulate) {
     const uint64_t nb = ceil_div(n, 256), blocks = nb * (nb + 1) / 2;
-    // residue scratch: 18 bytes per element of the 256-blocks, at most 4 GiB (then chunked)
-    const uint64_t res_bytes = std::min<uint64_t>(blocks * 18ull * 65536, 4ull << 30);
+    // residue scratch: one byte per modulus and element of the 256-blocks, at most 4 GiB (then chunked)
+    const uint64_t res_bytes = std::min<uint64_t>(blocks * (uint64_t)crt_moduli() * 65536, 4ull << 30);
     uint8_t* res = (uint8_t*)d.get(Device::S_ZBLK, res_bytes);
     const uint64_t step = crt_max_snps();
     void* ws = d.get(Device::S_LUT3, crt_lut_bytes(std::min(m, step)));

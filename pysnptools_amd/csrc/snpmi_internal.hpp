@@ -180,9 +180,11 @@ void launch_syrk_packed_bf3_split(const uint8_t* packed, uint64_t pitch, uint64_
                                   const H2Lut* h2 = nullptr);
 void launch_tile_reduce(const float* partial, unsigned slices, uint64_t elems, float* tiles, int accumulate,
                         hipStream_t st);
-// f64 GRM of packed SNPs on the int8 MFMA pipe (syrk_crt.hip): residues modulo 18 moduli, CRT
-// back to f64.  ws_lut = crt_lut_bytes(m) of scratch (its first int pair: block exponent and the
-// non-finite flag), res = residue scratch (>= 18 * 64 KiB; more = fewer launches); m <= crt_max_snps()
+// f64 GRM of packed SNPs on the int8 MFMA pipe (syrk_crt.hip): residues modulo crt_moduli()
+// moduli, CRT back to f64.  ws_lut = crt_lut_bytes(m) of scratch (its first int pair: block
+// exponent and the non-finite flag), res = residue scratch (>= crt_moduli() * 64 KiB; more =
+// fewer launches); m <= crt_max_snps()
+int crt_moduli();
 uint64_t crt_max_snps();
 uint64_t crt_lut_bytes(uint64_t m);
 int crt_fraction_bits(uint64_t m);

@@ -7,15 +7,15 @@
 //      q = rint(a * 2^(F - e)), |q| <= 2^F, with e = the block's exponent (max |a| <= 2^e); the
 //      quantisation error is <= 2^(e - F - 1), i.e. 2^-(F+1) of the block's largest value;
 //   2. K_int = sum_s q_is q_js is an exact integer with |K_int| <= m 2^2F < P/2, P = product of
-//      R pairwise-coprime moduli p <= 128; for each modulus the int8 MFMA computes
-//      sum_s rho(q_is) rho(q_js) with rho = q mod p in (-p/2, p/2] (|rho| <= 64, exact int32
-//      accumulation for m < 2^19) and the epilogue keeps it mod p (one byte per K element);
+//      R pairwise-coprime moduli p <= 256; for each modulus the int8 MFMA computes
+//      sum_s rho(q_is) rho(q_js) with rho = q mod p in [-p/2, p/2) (|rho| <= 128, exact int32
+//      accumulation for m <= 2^17) and the epilogue keeps it mod p (one byte per K element);
 //   3. k_crt rebuilds K_int from its R residues (Garner's mixed-radix digits, exact), converts to
 //      f64 (Horner, one rounding per step) and adds K_int 2^(2(e - F)) to the f64 K tiles.
-// R = 18 moduli (P ~ 2^119.5): F = floor((log2 P - 1 - log2 m) / 2) = 52 at m = 10k, so every
-// value keeps all of its bits down to 2^-53 of the block's largest -- the f64 product K's own
-// rounding level.  A block whose LUT holds NaN/Inf raises a flag on the device and the f64 MFMA
-// kernel (gated on the flag) computes it instead.
+// R = 15 moduli (P ~ 2^117.8): F = floor((log2 P - 1 - log2 m) / 2) = 51 at m = 10k, so every
+// value keeps its bits down to 2^-52 of the block's largest -- the f64 product K's own rounding
+// level.  A block whose LUT holds NaN/Inf raises a flag on the device and the f64 MFMA kernel
+// (gated on the flag) computes it instead.
 #include "snpmi_internal.hpp"
 
 #include <cmath>
@@ -23,13 +23,14 @@
 namespace snpmi {
 namespace {
 
-constexpr int kR = 18;
-// pairwise coprime: 2^7, 127, 5^3, 11^2, 7*17, 3^2*13, then primes
+constexpr int kR = 15;
+// pairwise coprime, <= 256 (symmetric residues fit int8): 2^8, 3*5*17, 11*23, 251, 13*19, 241, 239,
+// 233, 229, 227, 223, 7*31, 211, 199, 197 -- P ~ 2^117.8
 constexpr int mod_of(int i) {
-    constexpr int m[kR] = {128, 127, 125, 121, 119, 117, 113, 109, 107, 103, 101, 97, 89, 83, 79, 73, 71, 67};
+    constexpr int m[kR] = {256, 255, 253, 251, 247, 241, 239, 233, 229, 227, 223, 217, 211, 199, 197};
     return m[i];
 }
-__constant__ int kMod[kR] = {128, 127, 125, 121, 119, 117, 113, 109, 107, 103, 101, 97, 89, 83, 79, 73, 71, 67};
+__constant__ int kMod[kR] = {256, 255, 253, 251, 247, 241, 239, 233, 229, 227, 223, 217, 211, 199, 197};
 
 constexpr int BW = 256;    // block edge (iids)
 constexpr int SK = 128;    // SNPs per LDS stage (four 32-deep MFMA k-steps): 147 KiB of LDS, double-buffered
@@ -99,7 +100,7 @@ __global__ __launch_bounds__(256) void k_crt_lut(const double* __restrict__ lut,
         for (int c = 0; c < 4; c++) {
             long long x = q[c] % p;
             if (x < 0) x += p;
-            if (x >= (p + 1) / 2) x -= p;  // (-p/2, p/2]: [-64, 63] for 128, +-(p-1)/2 otherwise
+            if (x >= (p + 1) / 2) x -= p;  // [-128, 127] for 256, +-(p-1)/2 otherwise
             w |= ((uint32_t)x & 0xffu) << (8 * c);
         }
         lutr[(uint64_t)r * mpad + s] = w;
@@ -237,20 +238,32 @@ __global__ __launch_bounds__(512, 1) void k_syrk_i8r(const uint8_t* __restrict__
 }
 
 // ---------------------------------------------------------------- reconstruction
-// one thread per element of the chunk's 256-blocks; residues of the R planes -> K_int (Garner,
-// exact: all digit arithmetic is on integers < 2^24 held in f32) -> f64 -> K tiles.
+// two elements per thread (packed f32 math: v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32); the
+// residues of the R planes -> K_int (Garner, exact: all digit arithmetic is on integers < 2^24
+// held in f32) -> f64 -> K tiles.
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+// y - p round(y / p): round by the 1.5 * 2^23 magic constant (|y / p| < 2^22), exact for the
+// integers here; for odd p the result is the canonical residue in [-(p-1)/2, (p-1)/2] (no ties:
+// y / p is at least 1/(2p) from a half-integer and the f32 quotient errs by < 2^-8 of that)
+template <int I>
+__device__ __forceinline__ f2 mod_sym(f2 y) {
+    constexpr float p = (float)mod_of(I), ip = 1.0f / (float)mod_of(I), M = 12582912.0f;
+    const f2 t = (y * ip + M) - M;
+    return __builtin_elementwise_fma((f2)(-p), t, y);
+}
+
 template <int I>
 struct Garner {
     // y = (sum_{j<I} v_j W_j) mod p_I by Horner over the digits, W_j = prod_{k<j} p_k
-    __device__ static __forceinline__ float prefix_mod(const float (&v)[kR]) {
-        constexpr float p = (float)mod_of(I), ip = 1.0f / (float)mod_of(I);
-        float y = v[I - 1];
-#pragma unroll
-        for (int j = I - 2; j >= 0; j--) {
-            y = fmaf(y, (float)mod_of(j), v[j]);       // |y| < 2^15, exact
-            y = fmaf(-p, rintf(y * ip), y);         // y mod p in [-p/2, p/2]
+    template <int J>
+    __device__ static __forceinline__ f2 horner(const f2 (&v)[kR], f2 y) {
+        if constexpr (J < 0) {
+            return y;
+        } else {
+            y = __builtin_elementwise_fma(y, (f2)((float)mod_of(J)), v[J]);  // |y| < 2^16, exact
+            return horner<J - 1>(v, mod_sym<I>(y));
         }
-        return y;
     }
 };
 
@@ -259,42 +272,54 @@ struct CrtConst {
     float inv[kR];
 };
 
+template <int I>
+__device__ __forceinline__ void digits(f2 (&v)[kR], const uint8_t* __restrict__ res, uint64_t plane, uint64_t e_off,
+                                       const CrtConst& cc) {
+    if constexpr (I < kR) {
+        const uint32_t x = *reinterpret_cast<const uint16_t*>(res + (uint64_t)I * plane + e_off);
+        const f2 ri = {(float)(x & 0xffu), (float)(x >> 8)};
+        const f2 y = Garner<I>::template horner<I - 2>(v, v[I - 1]);
+        v[I] = mod_sym<I>((ri - y) * cc.inv[I]);  // |.| < 2^17: exact
+        digits<I + 1>(v, res, plane, e_off, cc);
+    }
+}
+
+// grid: 128 workgroups per 256-block (two rows each), 256 threads = 2 rows x 128 column pairs
 __global__ __launch_bounds__(256) void k_crt(const uint8_t* __restrict__ res, uint64_t b0, uint64_t nblk, uint64_t n,
                                              const int* __restrict__ ctl, int F, CrtConst cc, double* __restrict__ tiles,
                                              int accumulate) {
     if (ctl[1]) return;
-    const uint64_t blk = blockIdx.x >> 8;  // 256 threads x 256 rows per 256-block
-    const int row = blockIdx.x & 255, col = threadIdx.x;
+    const uint64_t blk = blockIdx.x >> 7;
+    const int row = 2 * (blockIdx.x & 127) + (threadIdx.x >> 7), col = 2 * (threadIdx.x & 127);
     uint32_t bi, bj;
     tile_coords(b0 + blk, bi, bj);
     const uint64_t ti = 2 * (uint64_t)bi + (row >> 7), tj = 2 * (uint64_t)bj + (col >> 7);
     const uint64_t nt128 = (n + 127) / 128;
     if (ti > tj || tj >= nt128) return;
-    const uint64_t e_off = (blk * BW + row) * BW + col;
-    float v[kR];
+    const uint64_t e_off = (blk * BW + row) * BW + col, plane = nblk * (BW * BW);
+    f2 v[kR];
     {
-        const int r0 = res[e_off];
-        v[0] = (float)(r0 >= 64 ? r0 - 128 : r0);
+        const uint32_t x = *reinterpret_cast<const uint16_t*>(res + e_off);
+        const int r0 = x & 0xff, r1 = x >> 8;  // modulus 256: symmetric digit in [-128, 127]
+        v[0] = (f2){(float)(r0 >= 128 ? r0 - 256 : r0), (float)(r1 >= 128 ? r1 - 256 : r1)};
     }
-#define SNPMI_CRT_DIGIT(I)                                                                   \
-    if constexpr (I < kR) {                                                                  \
-        constexpr float p = (float)mod_of(I), ip = 1.0f / (float)mod_of(I);                     \
-        const float ri = (float)res[(uint64_t)(I) * nblk * (BW * BW) + e_off];               \
-        float y = Garner<I>::prefix_mod(v);                                                  \
-        y = (ri - y) * cc.inv[I];                                  /* |.| < 2^15: exact */   \
-        v[I] = fmaf(-p, rintf(y * ip), y);                         /* odd p: no ties */      \
-    }
-    SNPMI_CRT_DIGIT(1) SNPMI_CRT_DIGIT(2) SNPMI_CRT_DIGIT(3) SNPMI_CRT_DIGIT(4) SNPMI_CRT_DIGIT(5)
-    SNPMI_CRT_DIGIT(6) SNPMI_CRT_DIGIT(7) SNPMI_CRT_DIGIT(8) SNPMI_CRT_DIGIT(9) SNPMI_CRT_DIGIT(10)
-    SNPMI_CRT_DIGIT(11) SNPMI_CRT_DIGIT(12) SNPMI_CRT_DIGIT(13) SNPMI_CRT_DIGIT(14) SNPMI_CRT_DIGIT(15)
-    SNPMI_CRT_DIGIT(16) SNPMI_CRT_DIGIT(17)
-#undef SNPMI_CRT_DIGIT
-    double X = (double)v[kR - 1];
+    digits<1>(v, res, plane, e_off, cc);
+    double X0 = (double)v[kR - 1].x, X1 = (double)v[kR - 1].y;
 #pragma unroll
-    for (int i = kR - 2; i >= 0; i--) X = fma(X, (double)mod_of(i), (double)v[i]);
-    const double k = ldexp(X, 2 * (ctl[0] - F));
-    double* T = tiles + (tj * (tj + 1) / 2 + ti) * (uint64_t)(128 * 128) + (row & 127) * 128 + (col & 127);
-    *T = accumulate ? *T + k : k;
+    for (int i = kR - 2; i >= 0; i--) {
+        X0 = fma(X0, (double)mod_of(i), (double)v[i].x);
+        X1 = fma(X1, (double)mod_of(i), (double)v[i].y);
+    }
+    const int sh = 2 * (ctl[0] - F);
+    double2* T = reinterpret_cast<double2*>(tiles + (tj * (tj + 1) / 2 + ti) * (uint64_t)(128 * 128) +
+                                            (row & 127) * 128 + (col & 127));
+    double2 k = make_double2(ldexp(X0, sh), ldexp(X1, sh));
+    if (accumulate) {
+        const double2 o = *T;
+        k.x += o.x;
+        k.y += o.y;
+    }
+    *T = k;
 }
 
 }  // namespace
@@ -327,6 +352,7 @@ int crt_fraction_bits(uint64_t m) {
 }
 
 uint64_t crt_max_snps() { return 1ull << 16; }  // keeps F >= 50 and the int32 sums exact
+int crt_moduli() { return kR; }
 
 uint64_t crt_lut_bytes(uint64_t m) { return (uint64_t)kR * round_up(std::max<uint64_t>(m, 1), SK) * 4 + 256; }
 
@@ -354,7 +380,7 @@ void launch_syrk_packed_crt(const uint8_t* packed, uint64_t pitch, uint64_t n, u
         else
 #endif
         k_syrk_i8r<SK><<<dim3((unsigned)cnt, kR), 512, 0, st>>>(packed, pitch, m, mpad, lutr, ctl, b0, cnt, res);
-        k_crt<<<(unsigned)(cnt * 256), 256, 0, st>>>(res, b0, cnt, n, ctl, F, cc, tiles, accumulate);
+        k_crt<<<(unsigned)(cnt * 128), 256, 0, st>>>(res, b0, cnt, n, ctl, F, cc, tiles, accumulate);
     }
     SNPMI_HIP(hipGetLastError());
 }
