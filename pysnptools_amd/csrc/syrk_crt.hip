@@ -140,10 +140,12 @@ __global__ __launch_bounds__(512, 1) void k_syrk_i8r(const uint8_t* __restrict__
     const uint64_t i0 = (uint64_t)bi * BW, j0 = (uint64_t)bj * BW;
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
     const int wm = wave >> 2, wn = wave & 3;
-    // loader role: panel lp, rows RPT kq .. RPT kq + RPT-1 of the stage, 16-iid group d
-    const int lp = t >> 8, kq = (t >> 4) & 15, d = t & 15;
-    const uint8_t* wp = P + (lp ? j0 : i0) / 4 + 4 * d + (uint64_t)(RPT * kq) * pitch;
-    const uint8_t* wlast = P + (lp ? j0 : i0) / 4 + 4 * d + (kdim - 1) * pitch;
+    // loader role: panel lp (wave-uniform), rows RPT kq .. RPT kq + RPT-1 of the stage, 16-iid
+    // group d.  Code loads: wave-uniform 64-bit base + 32-bit per-lane offset, the row clamped to
+    // the block's last SNP (its LUT words are zero past kdim: lutr is zero-padded to mpad)
+    const int lp = __builtin_amdgcn_readfirstlane(t >> 8), kq = (t >> 4) & 15, d = t & 15;
+    const uint8_t* pbase = P + (lp ? j0 : i0) / 4;
+    const uint32_t pit = (uint32_t)pitch;
     const uint32_t* lq = lr + RPT * kq;
     // transposed-read role: group g = lane>>4 covers k half h = g>>1 and columns 16(g&1)..+15
     const int g = lane >> 4, jj = (lane & 15) >> 1, pp = lane & 1;
@@ -159,10 +161,12 @@ __global__ __launch_bounds__(512, 1) void k_syrk_i8r(const uint8_t* __restrict__
     uint32_t cw[RPT];
     uint4 cl[RPT / 4];
     auto load = [&](uint64_t st) {
+        const uint8_t* sb = pbase + st * SKT * pitch;
+        const uint32_t lim = (uint32_t)(kdim - 1 - st * SKT);  // st < nst: >= 0
 #pragma unroll
         for (int h = 0; h < RPT; h++) {
-            const uint8_t* a = wp + (st * SKT + h) * pitch;
-            cw[h] = *reinterpret_cast<const uint32_t*>(a <= wlast ? a : wlast);
+            const uint32_t row = min((uint32_t)(RPT * kq + h), lim);
+            cw[h] = *reinterpret_cast<const uint32_t*>(sb + (row * pit + 4 * d));
         }
 #pragma unroll
         for (int u = 0; u < RPT / 4; u++)  // lutr is zero-padded to mpad >= nst * SKT
@@ -200,9 +204,10 @@ __global__ __launch_bounds__(512, 1) void k_syrk_i8r(const uint8_t* __restrict__
     for (uint64_t s = 0; s < nst; s++) {
         const uint8_t* cur = lds + (s & 1) * STG;
         uint8_t* nxt = lds + ((s + 1) & 1) * STG;
-        const bool more = s + 1 < nst;
         v4i a[2][4], b[2][2];
         frags(cur, 0, a[0], b[0]);
+        // the loader runs unconditionally (the last stage expands into the idle buffer, its code
+        // loads clamp to the last stage) so each k-step's MFMAs and loader VALU share a basic block
 #pragma unroll
         for (int ks = 0; ks < KS; ks++) {
             if (ks + 1 < KS) frags(cur, ks + 1, a[(ks + 1) & 1], b[(ks + 1) & 1]);
@@ -211,9 +216,9 @@ __global__ __launch_bounds__(512, 1) void k_syrk_i8r(const uint8_t* __restrict__
 #pragma unroll
                 for (int y = 0; y < 2; y++)
                     acc[x][y] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[ks & 1][x], b[ks & 1][y], acc[x][y], 0, 0, 0);
-            if (more) store(nxt, ks * RPT / KS, (ks + 1) * RPT / KS);
+            store(nxt, ks * RPT / KS, (ks + 1) * RPT / KS);
         }
-        if (more) load(s + 2 < nst ? s + 2 : nst - 1);
+        load(s + 2 < nst ? s + 2 : nst - 1);
         __syncthreads();
     }
     // epilogue: acc mod p -> [0, p), one byte per element at its true (row, col) in the block
