@@ -278,53 +278,63 @@ struct CrtConst {
 };
 
 template <int I>
-__device__ __forceinline__ void digits(f2 (&v)[kR], const uint8_t* __restrict__ res, uint64_t plane, uint64_t e_off,
-                                       const CrtConst& cc) {
+__device__ __forceinline__ void digits(f2 (&v)[2][kR], const uint8_t* __restrict__ res, uint64_t plane,
+                                       uint64_t e_off, const CrtConst& cc) {
     if constexpr (I < kR) {
-        const uint32_t x = *reinterpret_cast<const uint16_t*>(res + (uint64_t)I * plane + e_off);
-        const f2 ri = {(float)(x & 0xffu), (float)(x >> 8)};
-        const f2 y = Garner<I>::template horner<I - 2>(v, v[I - 1]);
-        v[I] = mod_sym<I>((ri - y) * cc.inv[I]);  // |.| < 2^17: exact
+        const uint32_t x = *reinterpret_cast<const uint32_t*>(res + (uint64_t)I * plane + e_off);
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            const f2 ri = {(float)((x >> (16 * h)) & 0xffu), (float)((x >> (16 * h + 8)) & 0xffu)};
+            const f2 y = Garner<I>::template horner<I - 2>(v[h], v[h][I - 1]);
+            v[h][I] = mod_sym<I>((ri - y) * cc.inv[I]);  // |.| < 2^17: exact
+        }
         digits<I + 1>(v, res, plane, e_off, cc);
     }
 }
 
-// grid: 128 workgroups per 256-block (two rows each), 256 threads = 2 rows x 128 column pairs
+// grid: 64 workgroups per 256-block (four rows each), 256 threads = 4 rows x 64 column quads;
+// one 4-B load per residue plane and thread, two independent packed-f32 Garner chains
 __global__ __launch_bounds__(256) void k_crt(const uint8_t* __restrict__ res, uint64_t b0, uint64_t nblk, uint64_t n,
                                              const int* __restrict__ ctl, int F, CrtConst cc, double* __restrict__ tiles,
                                              int accumulate) {
     if (ctl[1]) return;
-    const uint64_t blk = blockIdx.x >> 7;
-    const int row = 2 * (blockIdx.x & 127) + (threadIdx.x >> 7), col = 2 * (threadIdx.x & 127);
+    const uint64_t blk = blockIdx.x >> 6;
+    const int row = 4 * (blockIdx.x & 63) + (threadIdx.x >> 6), col = 4 * (threadIdx.x & 63);
     uint32_t bi, bj;
     tile_coords(b0 + blk, bi, bj);
     const uint64_t ti = 2 * (uint64_t)bi + (row >> 7), tj = 2 * (uint64_t)bj + (col >> 7);
     const uint64_t nt128 = (n + 127) / 128;
     if (ti > tj || tj >= nt128) return;
     const uint64_t e_off = (blk * BW + row) * BW + col, plane = nblk * (BW * BW);
-    f2 v[kR];
+    f2 v[2][kR];
     {
-        const uint32_t x = *reinterpret_cast<const uint16_t*>(res + e_off);
-        const int r0 = x & 0xff, r1 = x >> 8;  // modulus 256: symmetric digit in [-128, 127]
-        v[0] = (f2){(float)(r0 >= 128 ? r0 - 256 : r0), (float)(r1 >= 128 ? r1 - 256 : r1)};
+        const uint32_t x = *reinterpret_cast<const uint32_t*>(res + e_off);
+#pragma unroll
+        for (int h = 0; h < 2; h++) {  // modulus 256: symmetric digit in [-128, 127]
+            const int r0 = (x >> (16 * h)) & 0xff, r1 = (x >> (16 * h + 8)) & 0xff;
+            v[h][0] = (f2){(float)(r0 >= 128 ? r0 - 256 : r0), (float)(r1 >= 128 ? r1 - 256 : r1)};
+        }
     }
     digits<1>(v, res, plane, e_off, cc);
-    double X0 = (double)v[kR - 1].x, X1 = (double)v[kR - 1].y;
-#pragma unroll
-    for (int i = kR - 2; i >= 0; i--) {
-        X0 = fma(X0, (double)mod_of(i), (double)v[i].x);
-        X1 = fma(X1, (double)mod_of(i), (double)v[i].y);
-    }
     const int sh = 2 * (ctl[0] - F);
     double2* T = reinterpret_cast<double2*>(tiles + (tj * (tj + 1) / 2 + ti) * (uint64_t)(128 * 128) +
                                             (row & 127) * 128 + (col & 127));
-    double2 k = make_double2(ldexp(X0, sh), ldexp(X1, sh));
-    if (accumulate) {
-        const double2 o = *T;
-        k.x += o.x;
-        k.y += o.y;
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+        double X0 = (double)v[h][kR - 1].x, X1 = (double)v[h][kR - 1].y;
+#pragma unroll
+        for (int i = kR - 2; i >= 0; i--) {
+            X0 = fma(X0, (double)mod_of(i), (double)v[h][i].x);
+            X1 = fma(X1, (double)mod_of(i), (double)v[h][i].y);
+        }
+        double2 k = make_double2(ldexp(X0, sh), ldexp(X1, sh));
+        if (accumulate) {
+            const double2 o = T[h];
+            k.x += o.x;
+            k.y += o.y;
+        }
+        T[h] = k;
     }
-    *T = k;
 }
 
 }  // namespace
@@ -385,7 +395,7 @@ void launch_syrk_packed_crt(const uint8_t* packed, uint64_t pitch, uint64_t n, u
         else
 #endif
         k_syrk_i8r<SK><<<dim3((unsigned)cnt, kR), 512, 0, st>>>(packed, pitch, m, mpad, lutr, ctl, b0, cnt, res);
-        k_crt<<<(unsigned)(cnt * 128), 256, 0, st>>>(res, b0, cnt, n, ctl, F, cc, tiles, accumulate);
+        k_crt<<<(unsigned)(cnt * 64), 256, 0, st>>>(res, b0, cnt, n, ctl, F, cc, tiles, accumulate);
     }
     SNPMI_HIP(hipGetLastError());
 }
