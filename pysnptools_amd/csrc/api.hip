@@ -670,7 +670,7 @@ static const uint32_t* lut_bf3(Device& d, const float* lut, uint64_t m, H2Lut* h
 // f64 GRM of packed SNPs: default = the int8 MFMA residue path (syrk_crt.hip; variant 70 forces
 // it), 71 = the f64 MFMA two-phase path (decode to a dense f64 block, then k_syrk_glds).
 static bool use_crt(int dt) {
-    return dt == SNPMI_DT_F64 && (g_variant_syrk == 0 || g_variant_syrk == 70 || g_variant_syrk == 72);
+    return dt == SNPMI_DT_F64 && (g_variant_syrk == 0 || (g_variant_syrk >= 70 && g_variant_syrk != 71 && g_variant_syrk <= 79));
 }
 
 static void syrk_packed_crt(Device& d, const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m,

@@ -125,7 +125,12 @@ __device__ __forceinline__ v2i lds_tr8(const uint8_t* p) {
 // share of the next stage's rows is expanded and stored; one barrier per stage.
 // Epilogue: residue of each int32 sum, one byte per element, written as a dense 256 x 256 block
 // (true iid order) at res + (blockIdx.y * nblk + blockIdx.x) * 65536.
-template <int SKT>
+// ABL (ubench ablations, wrong results): 1 = no loader after the prologue, 2 = fragments read once
+// per stage (k-step 0) and reused by all four k-steps.
+// LDM 1: row-per-wave loader -- wave w expands rows 32(w&3)..+31 of panel w>>2, lane L the 4 iids
+// of LDS dword L (one code dword per lane, one v_perm), stored by ds_write_addtid_b32 (address =
+// M0 + 4 lane: 2 cycles per 256-B row vs 13 per ds_write_b128); the row's LUT word is uniform.
+template <int SKT, int ABL = 0, int LDM = 0>
 __global__ __launch_bounds__(512, 1) void k_syrk_i8r(const uint8_t* __restrict__ P, uint64_t pitch, uint64_t kdim,
                                                      uint64_t mpad, const uint32_t* __restrict__ lutr,
                                                      const int* __restrict__ ctl, uint64_t b0, uint64_t nblk,
@@ -197,9 +202,46 @@ __global__ __launch_bounds__(512, 1) void k_syrk_i8r(const uint8_t* __restrict__
         for (int y = 0; y < 2; y++) B[y] = frag(S, 1, ks, wn * 64 + 32 * y);
     };
 
-    load(0);
-    store(lds, 0, RPT);
-    load(nst > 1 ? 1 : 0);
+    // LDM 1 state
+    constexpr int RPW = SKT / 4;  // rows per wave per stage (2 panels x SKT rows / 8 waves)
+    const int wq = __builtin_amdgcn_readfirstlane(wave & 3), lpw = __builtin_amdgcn_readfirstlane(wave >> 2);
+    const uint8_t* pbu = P + (lpw ? j0 : i0) / 4;  // wave-uniform
+    const uint32_t loff = 4 * (lane >> 2), sh1 = 2 * (lane & 3);
+    uint32_t cwa[LDM == 1 ? RPW : 1], lutv = 0;
+    auto load1 = [&](uint64_t st) {
+        // 32-bit row numbers (kdim <= crt_max_snps()): gfx950 has no 64-bit scalar compare; the
+        // code loads are raw buffer loads off a wave-uniform stage base, row offset in SGPR
+        // (clamped to the block's last SNP), lane offset in VGPR
+        const uint32_t r0 = (uint32_t)st * SKT + RPW * wq, lim = (uint32_t)kdim - 1 - (uint32_t)st * SKT;
+        lutv = lr[r0 + (lane & (RPW - 1))];  // lane i < RPW: LUT word of row i (zero-padded to mpad)
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<uint8_t*>(pbu + st * SKT * pitch), (short)0, (int)0x7ffffff0, 0x00020000);
+#pragma unroll
+        for (int i = 0; i < RPW; i++) {
+            const uint32_t row = min((uint32_t)(RPW * wq + i), lim);
+            cwa[i] = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)loff, (int)(row * (uint32_t)pitch), 0);
+        }
+    };
+    auto store1 = [&](uint8_t* S, int i0_, int i1_) {
+        const uint32_t base = (uint32_t)(uintptr_t)(S + lpw * PNL + RPW * wq * RS);
+#pragma unroll
+        for (int i = i0_; i < i1_; i++) {
+            const uint32_t L = __builtin_amdgcn_readlane(lutv, i);
+            const uint32_t v = __builtin_amdgcn_perm(L, L, (cwa[i] >> sh1) & 0x03030303u);
+            asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tds_write_addtid_b32 %1" ::"s"(base + i * RS), "v"(v)
+                         : "memory", "m0");
+        }
+    };
+
+    if constexpr (LDM == 1) {
+        load1(0);
+        store1(lds, 0, RPW);
+        load1(nst > 1 ? 1 : 0);
+    } else {
+        load(0);
+        store(lds, 0, RPT);
+        load(nst > 1 ? 1 : 0);
+    }
     __syncthreads();
     for (uint64_t s = 0; s < nst; s++) {
         const uint8_t* cur = lds + (s & 1) * STG;
@@ -210,15 +252,30 @@ __global__ __launch_bounds__(512, 1) void k_syrk_i8r(const uint8_t* __restrict__
         // loads clamp to the last stage) so each k-step's MFMAs and loader VALU share a basic block
 #pragma unroll
         for (int ks = 0; ks < KS; ks++) {
-            if (ks + 1 < KS) frags(cur, ks + 1, a[(ks + 1) & 1], b[(ks + 1) & 1]);
+            if constexpr (ABL == 2) {
+                if (ks + 1 < KS) {
+#pragma unroll
+                    for (int x = 0; x < 4; x++) a[(ks + 1) & 1][x] = a[ks & 1][x];
+#pragma unroll
+                    for (int y = 0; y < 2; y++) b[(ks + 1) & 1][y] = b[ks & 1][y];
+                }
+            } else if (ks + 1 < KS) {
+                frags(cur, ks + 1, a[(ks + 1) & 1], b[(ks + 1) & 1]);
+            }
 #pragma unroll
             for (int x = 0; x < 4; x++)
 #pragma unroll
                 for (int y = 0; y < 2; y++)
                     acc[x][y] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[ks & 1][x], b[ks & 1][y], acc[x][y], 0, 0, 0);
-            store(nxt, ks * RPT / KS, (ks + 1) * RPT / KS);
+            if constexpr (ABL != 1) {
+                if constexpr (LDM == 1) store1(nxt, ks * RPW / KS, (ks + 1) * RPW / KS);
+                else store(nxt, ks * RPT / KS, (ks + 1) * RPT / KS);
+            }
         }
-        load(s + 2 < nst ? s + 2 : nst - 1);
+        if constexpr (ABL != 1) {
+            if constexpr (LDM == 1) load1(s + 2 < nst ? s + 2 : nst - 1);
+            else load(s + 2 < nst ? s + 2 : nst - 1);
+        }
         __syncthreads();
     }
     // epilogue: acc mod p -> [0, p), one byte per element at its true (row, col) in the block
@@ -392,6 +449,14 @@ void launch_syrk_packed_crt(const uint8_t* packed, uint64_t pitch, uint64_t n, u
 #ifdef SNPMI_UBENCH
         if (g_variant_syrk == 72)  // 64-SNP stages (73.7 KiB of LDS)
             k_syrk_i8r<64><<<dim3((unsigned)cnt, kR), 512, 0, st>>>(packed, pitch, m, mpad, lutr, ctl, b0, cnt, res);
+        else if (g_variant_syrk == 73)  // ablation: no loader
+            k_syrk_i8r<SK, 1><<<dim3((unsigned)cnt, kR), 512, 0, st>>>(packed, pitch, m, mpad, lutr, ctl, b0, cnt, res);
+        else if (g_variant_syrk == 75)  // row-per-wave loader, ds_write_addtid_b32
+            k_syrk_i8r<SK, 0, 1><<<dim3((unsigned)cnt, kR), 512, 0, st>>>(packed, pitch, m, mpad, lutr, ctl, b0, cnt, res);
+        else if (g_variant_syrk == 76)  // same, 64-SNP stages
+            k_syrk_i8r<64, 0, 1><<<dim3((unsigned)cnt, kR), 512, 0, st>>>(packed, pitch, m, mpad, lutr, ctl, b0, cnt, res);
+        else if (g_variant_syrk == 74)  // ablation: fragments read once per stage
+            k_syrk_i8r<SK, 2><<<dim3((unsigned)cnt, kR), 512, 0, st>>>(packed, pitch, m, mpad, lutr, ctl, b0, cnt, res);
         else
 #endif
         k_syrk_i8r<SK><<<dim3((unsigned)cnt, kR), 512, 0, st>>>(packed, pitch, m, mpad, lutr, ctl, b0, cnt, res);
