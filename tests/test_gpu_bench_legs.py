@@ -60,3 +60,29 @@ def test_grm_leg_partial_traces_sum_to_whole(world, dtype):
     assert abs(total - whole["trace"]) <= tol * abs(whole["trace"]), (total, whole["trace"])
     # trace(K) of Unit-standardized SNPs = the observed entries of the polymorphic SNPs <= N * M
     assert 0 < whole["trace"] <= args.grm_iid * args.grm_sid * (1 + 1e-5)
+
+
+def test_bench_with_rccl_communicator_world1():
+    """The whole bench (every leg, parity checks, JSON line) with an RCCL communicator at world size
+    1 (--force-rccl): the collective calls of the N > 1 plan run with their real buffers and sizes
+    -- the in-place all-reduce of the K tiles (f32 and f64), the packed-block all-gather of the
+    partitioned GRM, the RCCL barrier and max-over-ranks -- and the line keeps its schema."""
+    import json
+    import subprocess
+
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--force-rccl", "--steps", "1", "--warmup", "0",
+           "--n-iid", "4099", "--n-sid", "6000", "--grm-iid", "5000", "--grm-sid", "12000", "--grm-block", "5000",
+           "--grm5-iid", "20000", "--grm5-sid", "2048", "--e2e-sid", "4096", "--e2e-passes", "1",
+           "--cpu-seconds", "0.2"]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=110)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, out.stdout  # stdout carries the JSON line only (RCCL banners go to stderr)
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 1 and d["value"] > 0 and d["parity"]["bit_exact"]
+    for k in ("grm", "grm_f64"):
+        assert d[k]["parity"]["pass"], d[k]["parity"]
+        assert d[k]["allreduce_ms"] > 0
+    assert d["grm5"]["parity"]["pass"] and d["grm5"]["parity"]["gathered_block_bit_exact"]
+    assert d["grm5"]["allgather_ms"] > 0
+    assert "+ RCCL all-gather" in d["grm5"]["workload"]
