@@ -67,7 +67,7 @@ SPLIT_PRODUCTS = 3
 SPLIT_PEAK_TFLOPS = MFMA_BF16_PEAK_TFLOPS / SPLIT_PRODUCTS
 # f64 GRM on the int8 MFMA pipe (i8 = 2x the bf16 rate): one int8 SYRK per modulus
 MFMA_I8_PEAK_TOPS = 2 * MFMA_BF16_PEAK_TFLOPS
-CRT_MODULI = 15  # kR, pysnptools_amd/csrc/syrk_crt.hip
+CRT_MODULI = 15  # kR, pysnptools_amd/csrc/syrk_crt.hip: the most a block can need (R per block, on the device)
 GRM5_PLAN_WORLD = 8  # configs[4] is an 8-GPU plan
 
 
@@ -586,11 +586,18 @@ def leg_grm(N, args, dist, dtype):
         N.call("snpmi_stream_sync")
 
     run(False, limit=1)  # warm-up: one block
+    sum_r, nlaunch = ctypes.c_uint64(), ctypes.c_uint64()
+    if dtype == "f64":
+        N.call("snpmi_crt_moduli_stats", ctypes.byref(sum_r), ctypes.byref(nlaunch), 1)
     dist.barrier()
     t0 = time.perf_counter()
     run(True)
     dist.barrier()
     wall = dist.max(time.perf_counter() - t0)
+    crt_moduli = None
+    if dtype == "f64":  # moduli the timed blocks ran with (chosen per block on the device)
+        N.call("snpmi_crt_moduli_stats", ctypes.byref(sum_r), ctypes.byref(nlaunch), 1)
+        crt_moduli = sum_r.value / max(nlaunch.value, 1)
     syrk_ms = [ev.ms(2 + 2 * k, 3 + 2 * k) for k in range(len(mine))]
     allreduce_ms = ev.ms(len(ev.ev) - 2, len(ev.ev) - 1) if dist.rccl else 0.0
     tr = ctypes.c_double()
@@ -599,7 +606,7 @@ def leg_grm(N, args, dist, dtype):
     exec_ratio = SPLIT_PRODUCTS * 2 * 256 * 256 * (nb * (nb + 1) // 2) / (n * (n + 1))  # executed fp16 / algorithmic
     res = dict(wall=wall, syrk_ms=syrk_ms, allreduce_ms=allreduce_ms, trace=tr.value, exec_ratio=exec_ratio,
                mean_tflops=(n * (n + 1) * my_m / (np.sum(syrk_ms) * 1e-3) / 1e12) if syrk_ms else 0.0,
-               nblocks=len(blocks), my_m=my_m)
+               nblocks=len(blocks), my_m=my_m, crt_moduli=crt_moduli)
     if dist.rank == 0 and not args.skip_cpu and my_m > 0:
         # parity sample (untimed): K rows 0..63 of the GRM of this rank's first 512 SNPs
         cm, rows = min(512, my_m), 64
@@ -792,16 +799,19 @@ def grm_entry(args, dist, r, dtype):
                      "mfma_util_executed": r["mean_tflops"] * r["exec_ratio"] / MFMA_BF16_PEAK_TFLOPS})
     else:
         nb = (n + 255) // 256
-        ops = CRT_MODULI * 2 * 256 * 256 * (nb * (nb + 1) // 2) * args.grm_block  # executed int8 ops per launch
+        R = r["crt_moduli"] or CRT_MODULI
+        ops = R * 2 * 256 * 256 * (nb * (nb + 1) // 2) * args.grm_block  # executed int8 ops per launch
         launch_s = (np.mean(r["syrk_ms"]) * 1e-3) if r["syrk_ms"] else float("nan")
         achieved = ops / launch_s / 1e12
         roof = {"bound": "mfma", "achieved": achieved, "peak": MFMA_I8_PEAK_TOPS, "unit": "TOP/s",
                 "frac": achieved / MFMA_I8_PEAK_TOPS, "per_launch_ops": ops, "traffic": None,
                 "f64_equiv_tflops": r["mean_tflops"], "f64_mfma_peak": MFMA_F64_PEAK_TFLOPS,
                 "vs_f64_mfma_peak": r["mean_tflops"] / MFMA_F64_PEAK_TFLOPS,
-                "kernel": "k_syrk_i8r (v_mfma_i32_32x32x32_i8; grid = 256-blocks of a tile chunk x 15 moduli) + k_crt "
-                          "(Garner) + k_crt_exp/k_crt_lut; achieved = executed int8 ops (15 moduli x full "
-                          "256-blocks) / the whole per-block time"}
+                "moduli_per_block": R, "moduli_max": CRT_MODULI,
+                "kernel": "k_syrk_i8r (v_mfma_i32_32x32x32_i8; grid = 256-blocks of a tile chunk x 15 moduli, those "
+                          "past the block's R exit at once) + k_crt (Garner over R digits) + k_crt_exp/k_crt_lut/"
+                          "k_crt_bound/k_crt_r; achieved = executed int8 ops (R moduli x full 256-blocks) / the whole "
+                          "per-block time"}
     return {"workload": "cfg4: %d iid x %d SNP, Unit, block %d, %s SYRK, SNPs split into %d contiguous shard(s) "
                         "streamed in blocks%s" % (n, m, args.grm_block, "f32 (fp16x2 MFMA)" if f32 else
                                                  "f64 (int8 MFMA residues + CRT)",

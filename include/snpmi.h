@@ -286,6 +286,10 @@ int snpmi_dev_syrk_dense(const void* Z, uint64_t ldz, uint64_t n_iid, uint64_t n
 int snpmi_dev_grm_extract(const void* K_tiles, uint64_t n_iid, int dtype, const uint64_t* ri, uint64_t nr,
                           const uint64_t* ci, uint64_t nc, int order_c, double scale, void* out);
 int snpmi_dev_grm_trace(const void* K_tiles, uint64_t n_iid, int dtype, double* trace);
+/* float64 GRMs run on the int8 MFMA as residues modulo the first R of 15 coprime moduli, R chosen
+ * per SNP block on the device from the block's own bound max_i sum_s q_is^2:
+ * sum of R and number of such blocks on this device since the last reset (synchronous). */
+int snpmi_crt_moduli_stats(uint64_t* sum_r, uint64_t* launches, int reset);
 
 /* ---------------------------------------------------------------- RCCL (one process per GPU) */
 int snpmi_rccl_unique_id(uint8_t* id, uint64_t id_len);   /* id_len >= 128 */

@@ -21,6 +21,7 @@ _i32 = ctypes.c_int
 _f64 = ctypes.c_double
 _cp = ctypes.c_char_p
 _dp = ctypes.POINTER(ctypes.c_double)
+_u64p = ctypes.POINTER(ctypes.c_uint64)
 
 # name -> argtypes (restype int unless listed in _RESTYPES)
 _SIGS = {
@@ -104,6 +105,7 @@ _SIGS = {
     "snpmi_dev_syrk_dense": [_vp, _u64, _u64, _u64, _i32, _vp, _i32],
     "snpmi_dev_grm_extract": [_vp, _u64, _i32, _vp, _u64, _vp, _u64, _i32, _f64, _vp],
     "snpmi_dev_grm_trace": [_vp, _u64, _i32, _dp],
+    "snpmi_crt_moduli_stats": [_u64p, _u64p, _i32],
     "snpmi_rccl_unique_id": [_vp, _u64],
     "snpmi_rccl_init": [_i32, _i32, _vp, _u64],
     "snpmi_rccl_allreduce_sum": [_vp, _u64, _i32],

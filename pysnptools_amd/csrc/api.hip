@@ -673,6 +673,14 @@ static bool use_crt(int dt) {
     return dt == SNPMI_DT_F64 && (g_variant_syrk == 0 || (g_variant_syrk >= 70 && g_variant_syrk != 71 && g_variant_syrk <= 79));
 }
 
+// per-device record of the CRT path's moduli counts: [0] = sum of R, [1] = launches
+static unsigned long long* crt_record(Device& d) {
+    const bool fresh = d.cap[Device::S_CRTREC] == 0;
+    auto* rec = (unsigned long long*)d.get(Device::S_CRTREC, 16);
+    if (fresh) SNPMI_HIP(hipMemsetAsync(rec, 0, 16, d.stream));
+    return rec;
+}
+
 static void syrk_packed_crt(Device& d, const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m,
                             const double* lut, double* tiles, int accumulate) {
     const uint64_t nb = ceil_div(n, 256), blocks = nb * (nb + 1) / 2;
@@ -680,12 +688,13 @@ static void syrk_packed_crt(Device& d, const uint8_t* packed, uint64_t pitch, ui
     const uint64_t res_bytes = std::min<uint64_t>(blocks * (uint64_t)crt_moduli() * 65536, 4ull << 30);
     uint8_t* res = (uint8_t*)d.get(Device::S_ZBLK, res_bytes);
     const uint64_t step = crt_max_snps();
-    void* ws = d.get(Device::S_LUT3, crt_lut_bytes(std::min(m, step)));
+    void* ws = d.get(Device::S_LUT3, crt_lut_bytes(std::min(m, step), n));
+    unsigned long long* rec = crt_record(d);
     for (uint64_t s0 = 0; s0 < m; s0 += step) {
         const uint64_t cnt = std::min(step, m - s0);
         const int acc = accumulate || s0 > 0;
         launch_syrk_packed_crt(packed + s0 * pitch, pitch, n, cnt, lut + 4 * s0, tiles, acc, ws, res, res_bytes,
-                               d.stream);
+                               rec, d.stream);
         // NaN/Inf in this chunk's LUT: the f64 MFMA kernel computes it (gated on the device flag)
         launch_syrk_packed_f64_gated(packed + s0 * pitch, pitch, n, cnt, lut + 4 * s0, tiles, acc,
                                      (const int*)ws + 1, d.stream);
@@ -1580,6 +1589,21 @@ int snpmi_dev_grm_extract(const void* K_tiles, uint64_t n_iid, int dtype, const 
                           const uint64_t* ci, uint64_t nc, int order_c, double scale, void* out) {
     return guarded([&] {
         launch_grm_extract(K_tiles, n_iid, dtype, ri, nr, ci, nc, order_c, scale, out, stream());
+    });
+}
+
+int snpmi_crt_moduli_stats(uint64_t* sum_r, uint64_t* launches, int reset) {
+    return guarded([&] {
+        std::lock_guard<std::recursive_mutex> lk(g_call_mutex);
+        SNPMI_REQUIRE(sum_r != nullptr && launches != nullptr, SNPMI_E_ARG, "NULL output");
+        Device& d = device();
+        unsigned long long h[2] = {0, 0};
+        unsigned long long* rec = crt_record(d);
+        SNPMI_HIP(hipMemcpyAsync(h, rec, sizeof(h), hipMemcpyDeviceToHost, d.stream));
+        if (reset) SNPMI_HIP(hipMemsetAsync(rec, 0, sizeof(h), d.stream));
+        SNPMI_HIP(hipStreamSynchronize(d.stream));
+        *sum_r = h[0];
+        *launches = h[1];
     });
 }
 

@@ -68,7 +68,7 @@ struct Device {
     // grow-only scratch slots
     enum Slot { S_PACKED, S_PACKED2, S_IDX, S_IDX2, S_LUT, S_STATS, S_OUT, S_TILES, S_K, S_DENSE,
                 S_DENSE2, S_RED, S_SESSION, S_PACKED_B, S_ZBLK, S_IDX32, S_LUT3, S_H2, S_OUT_B, S_STATS_B,
-                S_WIN, S_DPACK, S_DLUT, S_NUM };
+                S_WIN, S_DPACK, S_DLUT, S_CRTREC, S_NUM };
     void* buf[S_NUM] = {};
     // chunk pipeline events (slot = chunk parity), all on-device ordering, no host spin:
     hipEvent_t staged[2] = {};    // copy stream: H2D of pinned slot done (host may refill it)
@@ -181,16 +181,17 @@ void launch_syrk_packed_bf3_split(const uint8_t* packed, uint64_t pitch, uint64_
 void launch_tile_reduce(const float* partial, unsigned slices, uint64_t elems, float* tiles, int accumulate,
                         hipStream_t st);
 // f64 GRM of packed SNPs on the int8 MFMA pipe (syrk_crt.hip): residues modulo crt_moduli()
-// moduli, CRT back to f64.  ws_lut = crt_lut_bytes(m) of scratch (its first int pair: block
-// exponent and the non-finite flag), res = residue scratch (>= crt_moduli() * 64 KiB; more =
-// fewer launches); m <= crt_max_snps()
+// moduli, CRT back to f64.  ws_lut = crt_lut_bytes(m, n) of scratch (its first ints: block
+// exponent, the non-finite flag, the moduli count R this block needs), res = residue scratch
+// (>= crt_moduli() * 64 KiB; more = fewer launches); m <= crt_max_snps(); rec (device, may be
+// NULL): rec[0] += R, rec[1] += 1 per launch
 int crt_moduli();
 uint64_t crt_max_snps();
-uint64_t crt_lut_bytes(uint64_t m);
+uint64_t crt_lut_bytes(uint64_t m, uint64_t n);
 int crt_fraction_bits(uint64_t m);
 void launch_syrk_packed_crt(const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m, const double* lut,
                             double* tiles, int accumulate, void* ws_lut, uint8_t* res, uint64_t res_bytes,
-                            hipStream_t st);
+                            unsigned long long* rec, hipStream_t st);
 // the f64-MFMA packed SYRK, run only when the device word *gate is non-zero (the CRT path's flag)
 void launch_syrk_packed_f64_gated(const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m, const double* lut,
                                   double* tiles, int accumulate, const int* gate, hipStream_t st);

@@ -12,9 +12,13 @@
 //      accumulation for m <= 2^17) and the epilogue keeps it mod p (one byte per K element);
 //   3. k_crt rebuilds K_int from its R residues (Garner's mixed-radix digits, exact), converts to
 //      f64 (Horner, one rounding per step) and adds K_int 2^(2(e - F)) to the f64 K tiles.
-// R = 15 moduli (P ~ 2^117.8): F = floor((log2 P - 1 - log2 m) / 2) = 51 at m = 10k, so every
+// kR = 15 moduli (P ~ 2^117.8): F = floor((log2 P - 1 - log2 m) / 2) = 51 at m = 10k, so every
 // value keeps its bits down to 2^-52 of the block's largest -- the f64 product K's own rounding
-// level.  A block whose LUT holds NaN/Inf raises a flag on the device and the f64 MFMA kernel
+// level.  That F is fixed by the worst case |K_int| <= m 2^2F; the block's actual bound is
+// |K_int,ij| <= sqrt(K_int,ii K_int,jj) <= max_i sum_s q_is^2 (Cauchy-Schwarz), which k_crt_bound
+// computes per iid on the device (rare-variant LUT values set e, so typical blocks sit 10-13 bits
+// below the worst case), and only the first R <= kR moduli with P_R > 2 max_i sum_s q_is^2 run
+// (the SYRK workgroups of moduli >= R exit at once, k_crt's Garner stops at R).  A block whose LUT holds NaN/Inf raises a flag on the device and the f64 MFMA kernel
 // (gated on the flag) computes it instead.
 #include "snpmi_internal.hpp"
 
@@ -81,8 +85,10 @@ __global__ __launch_bounds__(1024) void k_crt_exp(const double* __restrict__ lut
 }
 
 // residue LUT: lutr[r * mpad + s] byte c = rho_r(q_s[c]) (int8), zero for s >= m
+// qsq[4 s + c] = q_s[c]^2 in f64 (the bound table of k_crt_bound; 0 for s >= m)
 __global__ __launch_bounds__(256) void k_crt_lut(const double* __restrict__ lut, uint64_t m, uint64_t mpad, int F,
-                                                 const int* __restrict__ ctl, uint32_t* __restrict__ lutr) {
+                                                 const int* __restrict__ ctl, uint32_t* __restrict__ lutr,
+                                                 double* __restrict__ qsq) {
     const uint64_t s = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (s >= mpad) return;
     const int e = ctl[0];
@@ -91,6 +97,7 @@ __global__ __launch_bounds__(256) void k_crt_lut(const double* __restrict__ lut,
     for (int c = 0; c < 4; c++) {
         const double a = s < m && !ctl[1] ? lut[4 * s + c] : 0.0;
         q[c] = (long long)rint(ldexp(a, F - e));
+        qsq[4 * s + c] = (double)q[c] * (double)q[c];
     }
 #pragma unroll
     for (int r = 0; r < kR; r++) {
@@ -104,6 +111,65 @@ __global__ __launch_bounds__(256) void k_crt_lut(const double* __restrict__ lut,
             w |= ((uint32_t)x & 0xffu) << (8 * c);
         }
         lutr[(uint64_t)r * mpad + s] = w;
+    }
+}
+
+// ---------------------------------------------------------------- per-block modulus count
+// S[i] += sum_s q_is^2 over a slice of kBoundSlice SNPs: thread = 16 iids (one code dword per SNP,
+// the SNP's 4 table values are wave-uniform), one f64 atomic add per iid and slice.  f64 sums of
+// integers <= 2^104: relative error <= kBoundSlice 2^-53 per slice, covered by k_crt_r's margin.
+constexpr int kBoundSlice = 256;
+__global__ __launch_bounds__(256) void k_crt_bound(const uint8_t* __restrict__ P, uint64_t pitch, uint64_t n,
+                                                   uint64_t m, const double* __restrict__ qsq,
+                                                   const int* __restrict__ ctl, double* __restrict__ S) {
+    if (ctl[1]) return;
+    const uint64_t w = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (w >= (n + 15) / 16) return;
+    const uint64_t s0 = (uint64_t)blockIdx.y * kBoundSlice, s1 = min(m, s0 + kBoundSlice);
+    double acc[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) acc[k] = 0.0;
+    for (uint64_t s = s0; s < s1; s++) {
+        const uint32_t x = *reinterpret_cast<const uint32_t*>(P + s * pitch + 4 * w);
+        const double t0 = qsq[4 * s], t1 = qsq[4 * s + 1], t2 = qsq[4 * s + 2], t3 = qsq[4 * s + 3];
+#pragma unroll
+        for (int k = 0; k < 16; k++) {
+            const uint32_t c = (x >> (2 * k)) & 3u;
+            acc[k] += c & 2u ? (c & 1u ? t3 : t2) : (c & 1u ? t1 : t0);
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 16; k++)
+        if (16 * w + k < n) atomicAdd(S + 16 * w + k, acc[k]);
+}
+
+// ctl[2] = R: the fewest moduli with P_R > 2 max_i S[i] (1 + 2^-20); plog[r] = log2 P_{r+1} (host)
+struct CrtLog {
+    double plog[kR];
+};
+__global__ __launch_bounds__(1024) void k_crt_r(const double* __restrict__ S, uint64_t n, CrtLog L,
+                                               int* __restrict__ ctl, unsigned long long* __restrict__ rec) {
+    double M = 0.0;
+    for (uint64_t i = threadIdx.x; i < n; i += 1024) M = fmax(M, S[i]);
+    __shared__ double red[1024];
+    red[threadIdx.x] = M;
+    __syncthreads();
+    for (int w = 512; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w) red[threadIdx.x] = fmax(red[threadIdx.x], red[threadIdx.x + w]);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        int R = kR;
+        if (!ctl[1]) {
+            const double need = red[0] > 0.0 ? log2(red[0] * (1.0 + 0x1p-20)) + 1.0 : 0.0;
+            R = 1;
+            while (R < kR && L.plog[R - 1] <= need) R++;
+        }
+        ctl[2] = R;
+        if (rec) {
+            atomicAdd(rec, (unsigned long long)R);
+            atomicAdd(rec + 1, 1ull);
+        }
     }
 }
 
@@ -139,6 +205,7 @@ __global__ __launch_bounds__(512, 1) void k_syrk_i8r(const uint8_t* __restrict__
     __shared__ __attribute__((aligned(16))) uint8_t lds[2 * STG];
     if (ctl[1]) return;  // non-finite LUT: the f64 MFMA kernel runs instead
     const int r = blockIdx.y;
+    if (r >= ctl[2]) return;  // K_int fits the first ctl[2] moduli
     const uint32_t* lr = lutr + (uint64_t)r * mpad;
     uint32_t bi, bj;
     tile_coords(b0 + blockIdx.x, bi, bj);
@@ -334,18 +401,24 @@ struct CrtConst {
     float inv[kR];
 };
 
+// digits I >= R are zero: K_int is the balanced mixed-radix number of the first R digits
 template <int I>
 __device__ __forceinline__ void digits(f2 (&v)[2][kR], const uint8_t* __restrict__ res, uint64_t plane,
-                                       uint64_t e_off, const CrtConst& cc) {
+                                       uint64_t e_off, const CrtConst& cc, int R) {
     if constexpr (I < kR) {
-        const uint32_t x = *reinterpret_cast<const uint32_t*>(res + (uint64_t)I * plane + e_off);
+        if (I < R) {
+            const uint32_t x = *reinterpret_cast<const uint32_t*>(res + (uint64_t)I * plane + e_off);
 #pragma unroll
-        for (int h = 0; h < 2; h++) {
-            const f2 ri = {(float)((x >> (16 * h)) & 0xffu), (float)((x >> (16 * h + 8)) & 0xffu)};
-            const f2 y = Garner<I>::template horner<I - 2>(v[h], v[h][I - 1]);
-            v[h][I] = mod_sym<I>((ri - y) * cc.inv[I]);  // |.| < 2^17: exact
+            for (int h = 0; h < 2; h++) {
+                const f2 ri = {(float)((x >> (16 * h)) & 0xffu), (float)((x >> (16 * h + 8)) & 0xffu)};
+                const f2 y = Garner<I>::template horner<I - 2>(v[h], v[h][I - 1]);
+                v[h][I] = mod_sym<I>((ri - y) * cc.inv[I]);  // |.| < 2^17: exact
+            }
+        } else {
+#pragma unroll
+            for (int h = 0; h < 2; h++) v[h][I] = (f2){0.0f, 0.0f};
         }
-        digits<I + 1>(v, res, plane, e_off, cc);
+        digits<I + 1>(v, res, plane, e_off, cc, R);
     }
 }
 
@@ -372,7 +445,7 @@ __global__ __launch_bounds__(256) void k_crt(const uint8_t* __restrict__ res, ui
             v[h][0] = (f2){(float)(r0 >= 128 ? r0 - 256 : r0), (float)(r1 >= 128 ? r1 - 256 : r1)};
         }
     }
-    digits<1>(v, res, plane, e_off, cc);
+    digits<1>(v, res, plane, e_off, cc, ctl[2]);
     const int sh = 2 * (ctl[0] - F);
     double2* T = reinterpret_cast<double2*>(tiles + (tj * (tj + 1) / 2 + ti) * (uint64_t)(128 * 128) +
                                             (row & 127) * 128 + (col & 127));
@@ -426,21 +499,39 @@ int crt_fraction_bits(uint64_t m) {
 uint64_t crt_max_snps() { return 1ull << 16; }  // keeps F >= 50 and the int32 sums exact
 int crt_moduli() { return kR; }
 
-uint64_t crt_lut_bytes(uint64_t m) { return (uint64_t)kR * round_up(std::max<uint64_t>(m, 1), SK) * 4 + 256; }
+// ctl (256 B) | residue LUT (kR x mpad u32) | bound table (4 x mpad f64) | per-iid bound sums (n f64)
+uint64_t crt_lut_bytes(uint64_t m, uint64_t n) {
+    const uint64_t mpad = round_up(std::max<uint64_t>(m, 1), SK);
+    return 256 + (uint64_t)kR * mpad * 4 + mpad * 32 + round_up(std::max<uint64_t>(n, 1), 2) * 8;
+}
+
+static CrtLog crt_logs() {
+    CrtLog L{};
+    double s = 0;
+    for (int i = 0; i < kR; i++) L.plog[i] = (s += std::log2((double)mod_of(i)));
+    return L;
+}
 
 // K_tiles (+)= Z Z^T for packed codes + f64 LUT; ws_lut: crt_lut_bytes(m); res: res_bytes of
 // scratch (>= kR * 65536); gate: device u32 set when the block must run on the f64 MFMA instead
 void launch_syrk_packed_crt(const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m, const double* lut,
                             double* tiles, int accumulate, void* ws_lut, uint8_t* res, uint64_t res_bytes,
-                            hipStream_t st) {
+                            unsigned long long* rec, hipStream_t st) {
     SNPMI_REQUIRE(m > 0 && m <= crt_max_snps(), SNPMI_E_ARG, "crt SYRK: SNP count per launch out of range");
     const uint64_t nb = ceil_div(n, BW), total = nb * (nb + 1) / 2;
     const uint64_t mpad = round_up(m, SK);
     int* ctl = (int*)ws_lut;
     uint32_t* lutr = (uint32_t*)((uint8_t*)ws_lut + 256);
+    double* qsq = (double*)(lutr + (uint64_t)kR * mpad);
+    double* S = qsq + 4 * mpad;
     const int F = crt_fraction_bits(m);
     k_crt_exp<<<1, 1024, 0, st>>>(lut, 4 * m, ctl);
-    k_crt_lut<<<(unsigned)ceil_div(mpad, 256), 256, 0, st>>>(lut, m, mpad, F, ctl, lutr);
+    k_crt_lut<<<(unsigned)ceil_div(mpad, 256), 256, 0, st>>>(lut, m, mpad, F, ctl, lutr, qsq);
+    SNPMI_HIP(hipMemsetAsync(S, 0, n * sizeof(double), st));
+    k_crt_bound<<<dim3((unsigned)ceil_div(ceil_div(n, 16), 256), (unsigned)ceil_div(m, kBoundSlice)), 256, 0, st>>>(
+        packed, pitch, n, m, qsq, ctl, S);
+    static const CrtLog logs = crt_logs();
+    k_crt_r<<<1, 1024, 0, st>>>(S, n, logs, ctl, rec);
     const uint64_t per = std::max<uint64_t>(1, res_bytes / ((uint64_t)kR * BW * BW));
     static const CrtConst cc = crt_constants();
     for (uint64_t b0 = 0; b0 < total; b0 += per) {
