@@ -22,7 +22,8 @@ Metric (BASELINE.json): "SNPs/sec standardized (500k x 1M) + GRM GF/s at 1/2/4/8
                vs 2.5 PF fp16 dense / 3 = 833.3 TF (the f32-MFMA peak is 157.3).
   grm_f64    = the same GRM in float64 (the reference's default dtype, snpreader.py:528,623) on
                the int8 MFMA: each block's LUT quantised to 51-52-bit integers, K_int computed
-               exactly modulo 15 coprime moduli <= 256 (one int8 SYRK each), rebuilt by CRT and
+               exactly modulo the first R of 15 coprime moduli <= 256 (one int8 SYRK each; R per
+               block from the block's bound max_i sum_s q_is^2, on the device), rebuilt by CRT and
                added to the f64 K (syrk_crt.hip).  roofline vs the int8 dense peak (2 x bf16 =
                5.0 POP/s) on the executed ops; f64_equiv_tflops = N(N+1)M / time, beside the f64
                MFMA's 78.6 TF dense peak.
