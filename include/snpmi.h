@@ -275,7 +275,8 @@ int snpmi_dev_syrk_packed_part(const uint8_t* packed, uint64_t pitch, uint64_t n
 /* cfg5 from a .bed file (SnpReader._read_kernel, snpreader.py:623-668, with K partitioned as
  * above): this rank streams every selected SNP, standardizes it with stats over all selected
  * iids (stats in/out as snpmi_grm_bed_f32), accumulates only its own blocks and writes them to
- * blocks_out[snpmi_grm_part_blocks][256][256] (rows/cols past n are padding). */
+ * blocks_out[snpmi_grm_part_blocks][256][256] (rows/cols past n are padding).  blocks_out may be
+ * host memory (copied out at the end) or device memory (accumulated in place: K stays in HBM). */
 int snpmi_grm_part_bed_f32(const char* path, uint64_t n_iid, uint64_t n_sid, int count_a1,
                            const uint64_t* iid_idx, uint64_t n_out_iid, const uint64_t* sid_idx, uint64_t n_out_sid,
                            int std_kind, double a, double b, int use_stats, float* stats, int part_rank,

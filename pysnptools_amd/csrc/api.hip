@@ -1551,16 +1551,19 @@ int snpmi_grm_part_bed_f32(const char* path, uint64_t n_iid, uint64_t n_sid, int
         SNPMI_REQUIRE(blocks_out != nullptr || nloc == 0, SNPMI_E_ARG, "blocks_out is NULL");
         Device& d = device();
         const uint64_t bytes = std::max<uint64_t>(nloc, 1) * 256 * 256 * sizeof(float);
-        float* blocks = (float*)d.get(Device::S_TILES, bytes);
+        // blocks_out in device memory: the SYRK accumulates into it directly (K stays in HBM, no
+        // scratch, no copy-out); host memory: scratch tiles + a pinned-bounce copy at the end
+        const bool dev_out = nloc && is_device_ptr(d, blocks_out);
+        float* blocks = dev_out ? blocks_out : (float*)d.get(Device::S_TILES, bytes);
         const bool wrote = grm_stream_bed<float>(
             d, true, path, n_iid, n_sid, count_a1, iid_idx, n_out_iid, sid_idx, n_out_sid, std_kind, a, b, use_stats,
             stats, num_threads,
             [&](const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t cnt, const float* lut, bool acc) {
                 syrk_packed_part_auto(d, packed, pitch, n, cnt, lut, part_rank, part_world, blocks, acc);
             });
-        if (!wrote) SNPMI_HIP(hipMemsetAsync(blocks, 0, bytes, d.stream));
+        if (!wrote) SNPMI_HIP(hipMemsetAsync(blocks, 0, dev_out ? nloc * 256 * 256 * sizeof(float) : bytes, d.stream));
         const size_t bb = 256 * 256 * sizeof(float);  // one block per "row" of the pinned-bounce copy
-        if (nloc) d2h_rows(d, blocks_out, bb, blocks, bb, bb, nloc, resolve_threads(num_threads));
+        if (nloc && !dev_out) d2h_rows(d, blocks_out, bb, blocks, bb, bb, nloc, resolve_threads(num_threads));
         SNPMI_HIP(hipStreamSynchronize(d.stream));
     });
 }

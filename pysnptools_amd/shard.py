@@ -127,8 +127,9 @@ def grm_partitioned(reader, standardizer, rank, world, out=None, num_threads=Non
     Stats are computed per rank from all iids (identical on every rank).
 
     Returns (blocks [n_local, 256, 256] float32 -- ``out`` if given, e.g. an ``np.memmap`` of a
-    file --, coords [n_local, 2] int64 = (row0, col0) of each block, trained standardizer).
-    Entries of a block beyond iid n-1 are padding."""
+    file, or ``"hbm"`` / an ``hbm.HbmArray`` to keep the blocks in device memory (accumulated in
+    place, no copy-out) --, coords [n_local, 2] int64 = (row0, col0) of each block, trained
+    standardizer).  Entries of a block beyond iid n-1 are padding."""
     import ctypes
 
     import numpy as np
@@ -150,9 +151,14 @@ def grm_partitioned(reader, standardizer, rank, world, out=None, num_threads=Non
     stats = (np.ascontiguousarray(standardizer.stats_for(sid), dtype=np.float32) if use_stats
              else np.empty((len(sid), 2), dtype=np.float32))
     nloc = N.lib().snpmi_grm_part_blocks(n, rank, world)
-    if out is None:
+    if isinstance(out, str) and out == "hbm":
+        from pysnptools_amd import hbm
+
+        out = hbm.empty((nloc, 256, 256), dtype=np.float32, order="C")
+    elif out is None:
         out = np.empty((nloc, 256, 256), dtype=np.float32)
-    assert out.shape == (nloc, 256, 256) and out.dtype == np.float32 and out.flags["C_CONTIGUOUS"]
+    assert tuple(out.shape) == (nloc, 256, 256) and np.dtype(out.dtype) == np.float32
+    assert getattr(out, "order", None) == "C" if hasattr(out, "snpmi_ptr") else out.flags["C_CONTIGUOUS"]
     ri, ci = N.index_array(rows), N.index_array(cols)
     N.call("snpmi_grm_part_bed_f32", base.filename.encode(), base.iid_count, base.sid_count,
            int(bool(base.count_A1)), N.ptr(ri), n, N.ptr(ci), len(sid), kind, a, b, int(use_stats), N.ptr(stats),

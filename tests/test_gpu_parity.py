@@ -874,6 +874,9 @@ def test_grm_partitioned_from_file(name, rows, world, std):
     parts, trained = [], None
     for rank in range(world):
         blocks, coords, trained = grm_partitioned(r, stdz, rank, world)
+        # blocks kept in HBM (accumulated in place, no copy-out) == the host copy, bit for bit
+        hb, hcoords, _ = grm_partitioned(r, stdz, rank, world, out="hbm")
+        assert np.array_equal(hb.get(), blocks) and np.array_equal(hcoords, coords)
         parts.append((blocks, coords))
     K = assemble_partitioned(parts, r.iid_count)
     n, m = SHAPES[name]
