@@ -670,6 +670,124 @@ __global__ __launch_bounds__(256) void k_repack_win(const uint8_t* __restrict__ 
     }
 }
 
+// Lane-interleaved form of k_repack_win (the default windowed gather): a wave owns 1024-code
+// output segments; at step k lane t gathers code 64k + t, so the 64 lanes of one LDS read fetch
+// neighbouring source codes (same or consecutive u32x4: broadcast, no bank conflict, where the
+// dword-per-lane form had lanes 16 codes apart = 2-way conflicts), and each lane packs its 16
+// codes into one dword.  A 16x16 transpose of 2-bit pairs inside each 16-lane row (4 butterfly
+// stages, DPP + v_alignbit + v_bfi) turns those into output dwords: lane 16q + i holds dword
+// 4i + q of the segment, so one store per column still covers 256 contiguous bytes.  The plan is
+// u16 (window dword << 4 | code in dword), stored per lane (entry [segment][lane][k]) so a lane
+// reads its 2 segments' 32 entries as four 16-B loads issued before the window loads.
+__device__ __forceinline__ uint32_t dpp_xor(uint32_t v, int s) {
+    // partner lane i ^ 2^s within each 16-lane row (gfx9 DPP has no row_xmask: i^4 = (i^7)^3,
+    // i^8 = (i^15)^7)
+    const int x = (int)v;
+    if (s == 0) return (uint32_t)__builtin_amdgcn_update_dpp(0, x, 0xB1, 0xF, 0xF, false);
+    if (s == 1) return (uint32_t)__builtin_amdgcn_update_dpp(0, x, 0x4E, 0xF, 0xF, false);
+    if (s == 2)
+        return (uint32_t)__builtin_amdgcn_update_dpp(0, __builtin_amdgcn_update_dpp(0, x, 0x141, 0xF, 0xF, false),
+                                                     0x1B, 0xF, 0xF, false);
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, __builtin_amdgcn_update_dpp(0, x, 0x140, 0xF, 0xF, false), 0x141,
+                                                 0xF, 0xF, false);
+}
+
+template <int K>
+__global__ __launch_bounds__(256) void k_repack_win16(const uint8_t* __restrict__ src, uint64_t sp, uint64_t nq,
+                                                      uint64_t zq, uint64_t nchunks, uint64_t m,
+                                                      const uint32_t* __restrict__ win,
+                                                      const uint16_t* __restrict__ plan, uint8_t* __restrict__ dst,
+                                                      uint64_t dp) {
+    extern __shared__ u32x4_t colw[];
+    typedef uint32_t vk_t __attribute__((ext_vector_type(K)));
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const uint64_t c = blockIdx.x % nchunks, g = blockIdx.x / nchunks;
+    // this lane's plan entries of segments 2*wave and 2*wave+1 of chunk c (16 u16 each)
+    u32x4_t pe[4];
+    {
+        const u32x4_t* pp = reinterpret_cast<const u32x4_t*>(plan + (c * 8 + 2 * wave) * 1024 + 16 * lane);
+        pe[0] = pp[0];
+        pe[1] = pp[1];
+        pe[2] = pp[128];  // next segment: + 1024 u16 = 128 u32x4
+        pe[3] = pp[129];
+    }
+    const uint64_t lo4 = win[c], n4 = min(zq, nq - lo4);
+    uint32_t* l = reinterpret_cast<uint32_t*>(colw);
+    for (uint64_t q = t; q < n4; q += 256) {
+        u32x4_t v[K];
+#pragma unroll
+        for (int cc = 0; cc < K; cc++) {
+            const uint64_t j = g * K + cc;
+            v[cc] = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(src + (j < m ? j : m - 1) * sp) + lo4 + q);
+        }
+        if constexpr (K == 1) {
+            colw[q] = v[0];
+        } else {
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+                vk_t x;
+#pragma unroll
+                for (int cc = 0; cc < K; cc++) x[cc] = v[cc][e];
+                *reinterpret_cast<vk_t*>(l + (4 * q + e) * K) = x;
+            }
+        }
+    }
+    if (t < K) l[4 * zq * K + t] = 0;
+    __syncthreads();
+    const uint8_t* lb = reinterpret_cast<const uint8_t*>(colw);
+    const uint64_t ndp = dp / 4;
+    const int i = lane & 15, q = lane >> 4;
+#pragma unroll
+    for (int sg = 0; sg < 2; sg++) {
+        uint32_t a[K];
+#pragma unroll
+        for (int cc = 0; cc < K; cc++) a[cc] = 0;
+#pragma unroll
+        for (int k = 0; k < 16; k++) {
+            const uint32_t word = pe[2 * sg + (k >> 3)][(k >> 1) & 3];
+            const uint32_t e = (k & 1) ? word >> 16 : word & 0xffffu;
+            const vk_t x = *reinterpret_cast<const vk_t*>(lb + (e >> 4) * (4 * K));
+#pragma unroll
+            for (int cc = 0; cc < K; cc++) a[cc] |= __builtin_amdgcn_ubfe(x[cc], 2 * (e & 15u), 2) << (2 * k);
+        }
+        // 16 x 16 transpose of 2-bit pairs within each row: stage s swaps bit s of the lane index
+        // with bit s of the pair index
+#pragma unroll
+        for (int s = 0; s < 4; s++) {
+            const uint32_t m0 = s == 0 ? 0x33333333u : s == 1 ? 0x0F0F0F0Fu : s == 2 ? 0x00FF00FFu : 0x0000FFFFu;
+            const bool hi = (i >> s) & 1;
+            const uint32_t mk = hi ? ~m0 : m0;
+            const uint32_t rot = hi ? 2u << s : 32u - (2u << s);
+#pragma unroll
+            for (int cc = 0; cc < K; cc++) {
+                const uint32_t y = dpp_xor(a[cc], s);
+                const uint32_t sy = __builtin_amdgcn_alignbit(y, y, rot);
+                a[cc] = (a[cc] & mk) | (sy & ~mk);
+            }
+        }
+        const uint64_t d = (c * 8 + 2 * wave + sg) * 64 + 4 * i + q;
+        if (d < ndp) {
+#pragma unroll
+            for (int cc = 0; cc < K; cc++)
+                if (g * K + cc < m) reinterpret_cast<uint32_t*>(dst + (g * K + cc) * dp)[d] = a[cc];
+        }
+    }
+}
+
+// u16 lane-interleaved plan of k_repack_win16: code r of chunk c (8192 codes, 8 segments of 1024)
+// at [r & ~1023] + 16 * (r & 63) + ((r >> 6) & 15); entries past n_out point at the zero dword
+__global__ void k_repack_plan16(const uint64_t* __restrict__ idx, uint64_t n_out, uint64_t n_all, uint64_t zq,
+                                const uint32_t* __restrict__ win, uint16_t* __restrict__ plan) {
+    for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n_all; r += (uint64_t)gridDim.x * blockDim.x) {
+        uint32_t e = (uint32_t)(4 * zq) << 4;
+        if (r < n_out) {
+            const uint64_t i = idx[r];
+            e = (uint32_t)(((i >> 4) - 4ull * win[r / kRepackChunk]) << 4) | (uint32_t)(i & 15);
+        }
+        plan[(r & ~1023ull) + 16 * (r & 63) + ((r >> 6) & 15)] = (uint16_t)e;
+    }
+}
+
 template <int K>
 __global__ __launch_bounds__(1024) void k_repack_lds(const uint8_t* __restrict__ src, uint64_t sp, uint64_t nq,
                                                      uint64_t m, const uint32_t* __restrict__ plan, uint64_t n_out,
@@ -1395,7 +1513,12 @@ void launch_decode_std_fused(const uint8_t* packed, uint64_t pitch, uint64_t n, 
     SNPMI_LAUNCH_CHECK();
 }
 
-uint64_t repack_plan_entries(uint64_t n_out) { return round_up(std::max<uint64_t>(n_out, 1), 16); }
+// u32 entries: one per output code (k_repack_plan), or two u16 per code over whole 8192-code
+// chunks (k_repack_plan16)
+uint64_t repack_plan_entries(uint64_t n_out) {
+    const uint64_t n = std::max<uint64_t>(n_out, 1);
+    return std::max(round_up(n, 16), ceil_div(n, kRepackChunk) * kRepackChunk / 2);
+}
 uint64_t repack_win_entries(uint64_t n_out) { return 3 * ceil_div(std::max<uint64_t>(n_out, 1), 4096) + 64; }
 
 // Build the gather plan for one index list (once per call).  Narrow per-chunk source windows
@@ -1431,6 +1554,23 @@ RepackPlan launch_repack_plan(const uint64_t* idx, uint64_t n_out, uint64_t n_sr
         if (g_variant_decode == 11 && K == 4) K = 2;
         if (K > 0 && 2 * w <= nq) {
             SNPMI_HIP(hipMemcpyAsync(win, lo4.data(), nchunks * 4, hipMemcpyHostToDevice, st));
+            // lane-interleaved gather (k_repack_win16) when the zero dword's index fits the u16
+            // entry; decode variant 17 keeps the dword-per-lane k_repack_win for A/B runs
+            if (chunk == kRepackChunk && 4 * w < 4096 && g_variant_decode != 17) {
+                const uint64_t n_all = nchunks * kRepackChunk;
+                k_repack_plan16<<<grid_for(n_all, kBlock, 4096), kBlock, 0, st>>>(idx, n_out, n_all, w, win,
+                                                                                 (uint16_t*)plan);
+                SNPMI_LAUNCH_CHECK();
+                SNPMI_HIP(hipStreamSynchronize(st));  // lo4 is a local vector
+                P.plan = plan;
+                P.win = win;
+                P.K = K;
+                P.zq = w;
+                P.nchunks = nchunks;
+                P.chunk_words = chunk / 16;
+                P.lanes = true;
+                return P;
+            }
             k_repack_plan<<<grid_for(n_pad, kBlock, 4096), kBlock, 0, st>>>(idx, n_out, n_pad, w, K, win, chunk, plan);
             SNPMI_LAUNCH_CHECK();
             SNPMI_HIP(hipStreamSynchronize(st));  // lo4 is a local vector
@@ -1462,6 +1602,21 @@ void launch_repack(const uint8_t* src, uint64_t src_pitch, uint64_t n_src, const
         const uint64_t ng = ceil_div(n_sid, (uint64_t)P.K);
         SNPMI_REQUIRE(ng * P.nchunks < (1ull << 31), SNPMI_E_ARG, "too many repack workgroups");
         const size_t lds = (size_t)(P.K * P.zq + 1) * 16;
+        if (P.lanes) {
+#define SNPMI_REPACK_WIN16(KK)                                                                                     \
+    k_repack_win16<KK><<<(unsigned)(ng * P.nchunks), 256, lds, st>>>(src, src_pitch, nq, P.zq, P.nchunks, n_sid,    \
+                                                                    P.win, (const uint16_t*)P.plan, dst, dst_pitch)
+            if (P.K == 4) {
+                SNPMI_REPACK_WIN16(4);
+            } else if (P.K == 2) {
+                SNPMI_REPACK_WIN16(2);
+            } else {
+                SNPMI_REPACK_WIN16(1);
+            }
+#undef SNPMI_REPACK_WIN16
+            SNPMI_LAUNCH_CHECK();
+            return;
+        }
 #define SNPMI_REPACK_WIN(KK)                                                                                       \
     k_repack_win<KK><<<(unsigned)(ng * P.nchunks), 256, lds, st>>>(src, src_pitch, nq, P.zq, P.nchunks,             \
                                                                   P.chunk_words, n_sid,                             \

@@ -113,6 +113,7 @@ struct RepackPlan {
     uint64_t zq = 0;                 // u32x4 per staged column (window or whole column)
     uint64_t nchunks = 1;
     uint64_t chunk_words = 0;        // output words per windowed workgroup
+    bool lanes = false;              // u16 lane-interleaved plan of k_repack_win16
 };
 uint64_t repack_plan_entries(uint64_t n_out);
 uint64_t repack_win_entries(uint64_t n_out);

@@ -737,7 +737,7 @@ def test_fused_decode_standardize_equals_two_kernels(n, kind, use_stats, count_a
 
 
 @pytest.mark.parametrize("n,m", [(20_011, 40), (100_003, 2050), (250_001, 1501), (500_000, 1100), (700_003, 3)])
-@pytest.mark.parametrize("kind", ["random", "reversed_stride2", "sorted"])
+@pytest.mark.parametrize("kind", ["random", "reversed_stride2", "sorted", "stride7", "stride3_tail"])
 def test_dev_repack_random_gather(n, m, kind):
     """snpmi_dev_repack: columns staged in LDS in groups of K = 4 / 2 / 1 (by column size; more
     groups than workgroups, so the register prefetch of the next group runs), > 150 KiB columns
@@ -749,6 +749,11 @@ def test_dev_repack_random_gather(n, m, kind):
         idx = rng.choice(n, size=n // 3, replace=True).astype(np.uint64)
     elif kind == "reversed_stride2":
         idx = np.arange(n - 1, -1, -2, dtype=np.uint64)
+    elif kind == "stride7":  # windows of 2 columns per workgroup (K = 2)
+        idx = np.arange(3, n, 7, dtype=np.uint64)
+    elif kind == "stride3_tail":  # last 8192-code chunk holds one code
+        idx = np.arange(0, n, 3, dtype=np.uint64)
+        idx = idx[:max(len(idx) // 8192, 1) * 8192 + 1]
     else:
         idx = np.sort(rng.choice(n, size=n // 2 + 7, replace=False)).astype(np.uint64)
     n_out = len(idx)
@@ -765,6 +770,14 @@ def test_dev_repack_random_gather(n, m, kind):
     if n_out % 4:
         assert np.all((got[:, n_out // 4] >> (2 * (n_out % 4))) == 0)
     assert np.all(got[:, (n_out + 3) // 4:] == 0)
+    # the dword-per-lane windowed kernel (decode variant 17) writes the same bytes
+    N.call("snpmi_set_kernel_variant", b"decode", 17)
+    try:
+        N.call("snpmi_dev_memset", dst.p, 0x5A, pitch_out * m)
+        N.call("snpmi_dev_repack", buf.p, pitch, n, didx.p, n_out, m, dst.p, pitch_out)
+    finally:
+        N.call("snpmi_set_kernel_variant", b"decode", 0)
+    assert np.array_equal(dst.get(np.empty((m, pitch_out), dtype=np.uint8)), got)
 
 
 def test_diag_k_to_n_snp_side_and_trained():
