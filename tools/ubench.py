@@ -248,7 +248,7 @@ def syrk(args):
                     ref = chk.copy()
                 err = np.abs(chk.astype(np.float64) - ref).max() / max(np.abs(ref).max(), 1)
                 errs[v] = float(err)
-                assert v in (10, 11, 12, 13, 14, 15, 39, 63, 73, 74) or err < 1e-5, "variant %d differs: %g" % (v, err)
+                assert args.noassert or v in (10, 11, 12, 13, 14, 15, 39, 63, 73, 74) or err < 1e-5, "variant %d differs: %g" % (v, err)
     for v in variants:
         t = np.median(ts[v])
         print(json.dumps({"kernel": "syrk_" + args.dtype, "variant": v, "n": n, "m": m, "accumulate": args.acc,
@@ -266,6 +266,7 @@ if __name__ == "__main__":
     p.add_argument("--index", default="rev2", choices=["rev2", "random", "sorted"])
     p.add_argument("--variants", default="0,1,2,3,4,5,6")
     p.add_argument("--acc", type=int, default=0, help="syrk: accumulate into the tiles (rounds after the first)")
+    p.add_argument("--noassert", type=int, default=0)
     p.add_argument("--set-variant", default=None, help="kernel=variant applied once before the run")
     a = p.parse_args()
     if a.set_variant:
