@@ -63,3 +63,49 @@ def test_crt_rare_variant_blocks_use_fewer_moduli():
     err, R, launches = _grm_f64(v)
     assert launches >= 1 and R <= 14, R
     assert err <= 1e-12, err
+
+
+def test_crt_chunks_match_f64_mfma():
+    """N = 30000: the 7021 256-blocks need two residue chunks (4 GiB of scratch per chunk).  The
+    tiles equal the f64-MFMA path's (variant 71) to 1e-12 of max |K| after a fresh launch and
+    after an accumulating second launch, and tile (0, 0) matches the f64 oracle."""
+    from test_gpu_parity import Dev, synth_dev
+
+    n, m = 30000, 512
+    buf, pitch = synth_dev(n, 2 * m, 23)
+    lut, st = Dev(2 * m * 4 * 8), Dev(2 * m * 2 * 8)
+    N.call("snpmi_dev_snp_stats", buf.p, pitch, n, 2 * m, 0, N.STD_UNIT, 0.0, 0.0, 0, N.DT_F64, st.p, lut.p)
+    tb = N.lib().snpmi_grm_tile_bytes(n, N.DT_F64)
+    outs = []
+    for v in (0, 71):
+        tiles = Dev(tb)
+        N.call("snpmi_set_kernel_variant", b"syrk", v)
+        try:
+            N.call("snpmi_dev_syrk_packed", buf.p, pitch, n, m, lut.p, N.DT_F64, tiles.p, 0)
+            one = tiles.get(np.empty(tb // 8, dtype=np.float64))
+            N.call("snpmi_dev_syrk_packed", ctypes.c_void_p(buf.p.value + m * pitch), pitch, n, m,
+                   ctypes.c_void_p(lut.p.value + m * 32), N.DT_F64, tiles.p, 1)
+            two = tiles.get(np.empty(tb // 8, dtype=np.float64))
+        finally:
+            N.call("snpmi_set_kernel_variant", b"syrk", 0)
+        outs.append((one, two))
+    # compare K entries only: the pad rows/columns (iid >= n) of the last tile row/column are
+    # scratch that the extraction never reads, and the two paths leave different values there
+    nt = (n + 127) // 128
+    tj = np.repeat(np.arange(nt), np.arange(1, nt + 1))
+    ti = np.concatenate([np.arange(j + 1) for j in range(nt)])
+    vc = n - (nt - 1) * 128
+    for a, b in zip(outs[0], outs[1]):
+        for x in (a, b):
+            T = x.reshape(-1, 128, 128)
+            T[tj == nt - 1, :, vc:] = 0
+            T[ti == nt - 1, vc:, :] = 0
+        assert np.abs(a - b).max() <= 1e-12 * np.abs(b).max()
+    # tile (0, 0) = K[0:128, 0:128] over all 2m SNPs vs the oracle
+    packed = buf.get(np.empty((2 * m, pitch), dtype=np.uint8))
+    Z = O.decode(np.ascontiguousarray(packed[:, :(n + 3) // 4]).reshape(-1), n, 2 * m, dtype=np.float64)
+    O.standardize_native(Z)
+    Kref = Z[:128].dot(Z[:128].T)
+    got = outs[0][1][:128 * 128].reshape(128, 128)
+    iu = np.triu_indices(128)
+    assert np.abs(got[iu] - Kref[iu]).max() <= 1e-12 * np.abs(np.diag(Kref)).max()
