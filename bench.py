@@ -84,6 +84,8 @@ def parse(argv=None):
     p.add_argument("--grm-sid", type=int, default=500_000)
     p.add_argument("--grm-block", type=int, default=10_000)
     p.add_argument("--skip-grm", action="store_true")
+    p.add_argument("--grm-collective", choices=["reduce", "allreduce"], default="reduce",
+                   help="cfg4 at N > 1: K tiles summed onto rank 0 (read_kernel returns K to one caller) or onto every rank")
     p.add_argument("--grm-f64", choices=["on", "off"], default="on", help="cfg4 GRM in float64 (reference default)")
     p.add_argument("--grm5", choices=["on", "off"], default="on", help="cfg5 partitioned-K GRM leg")
     p.add_argument("--grm5-iid", type=int, default=500_000)
@@ -582,7 +584,10 @@ def leg_grm(N, args, dist, dtype):
             off += c
         if dist.rccl and timed:
             ev.record(len(ev.ev) - 2)
-            N.call("snpmi_rccl_allreduce_sum", tiles.p, tile_bytes // esz, dt)
+            if args.grm_collective == "reduce":
+                N.call("snpmi_rccl_reduce_sum", tiles.p, tile_bytes // esz, dt, 0)
+            else:
+                N.call("snpmi_rccl_allreduce_sum", tiles.p, tile_bytes // esz, dt)
             ev.record(len(ev.ev) - 1)
         N.call("snpmi_stream_sync")
 
@@ -605,6 +610,7 @@ def leg_grm(N, args, dist, dtype):
     N.call("snpmi_dev_grm_trace", tiles.p, n, dt, ctypes.byref(tr))
     nb = (n + 255) // 256
     exec_ratio = SPLIT_PRODUCTS * 2 * 256 * 256 * (nb * (nb + 1) // 2) / (n * (n + 1))  # executed fp16 / algorithmic
+    # allreduce_ms = the K-tile collective (ncclReduce by default, --grm-collective)
     res = dict(wall=wall, syrk_ms=syrk_ms, allreduce_ms=allreduce_ms, trace=tr.value, exec_ratio=exec_ratio,
                mean_tflops=(n * (n + 1) * my_m / (np.sum(syrk_ms) * 1e-3) / 1e12) if syrk_ms else 0.0,
                nblocks=len(blocks), my_m=my_m, crt_moduli=crt_moduli)
@@ -816,8 +822,12 @@ def grm_entry(args, dist, r, dtype):
     return {"workload": "cfg4: %d iid x %d SNP, Unit, block %d, %s SYRK, SNPs split into %d contiguous shard(s) "
                         "streamed in blocks%s" % (n, m, args.grm_block, "f32 (fp16x2 MFMA)" if f32 else
                                                  "f64 (int8 MFMA residues + CRT)",
-                                                 dist.world, ", RCCL all-reduce of K tiles" if dist.rccl else ""),
+                                                 dist.world, (", RCCL %s of K tiles" % (
+                                                     "reduce onto rank 0" if args.grm_collective == "reduce"
+                                                     else "all-reduce")) if dist.rccl else ""),
             "gflops": gf, "snps_per_s": m / r["wall"], "seconds": r["wall"], "scaling": "strong",
+            "collective": ("ncclReduce(sum, root 0)" if args.grm_collective == "reduce" else "ncclAllReduce(sum)")
+            if dist.rccl else None,
             "allreduce_ms": r["allreduce_ms"], "trace_K": r["trace"], "roofline": roof}
 
 

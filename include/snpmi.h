@@ -296,6 +296,10 @@ int snpmi_crt_moduli_stats(uint64_t* sum_r, uint64_t* launches, int reset);
 int snpmi_rccl_unique_id(uint8_t* id, uint64_t id_len);   /* id_len >= 128 */
 int snpmi_rccl_init(int nranks, int rank, const uint8_t* id, uint64_t id_len);
 int snpmi_rccl_allreduce_sum(void* buf, uint64_t count, int dtype);
+/* In-place sum of the K tiles onto rank `root` only (the caller of read_kernel holds K:
+ * snpreader.py:623-668 returns K to its one process); ncclReduce moves half the bytes of the
+ * all-reduce over xGMI.  buf on non-root ranks is left unspecified. */
+int snpmi_rccl_reduce_sum(void* buf, uint64_t count, int dtype, int root);
 /* cfg5: every rank contributes bytes_per_rank bytes; recv gets them concatenated in rank
  * order (send may alias recv + rank * bytes_per_rank) */
 int snpmi_rccl_allgather(const void* send, void* recv, uint64_t bytes_per_rank);

@@ -109,6 +109,7 @@ _SIGS = {
     "snpmi_rccl_unique_id": [_vp, _u64],
     "snpmi_rccl_init": [_i32, _i32, _vp, _u64],
     "snpmi_rccl_allreduce_sum": [_vp, _u64, _i32],
+    "snpmi_rccl_reduce_sum": [_vp, _u64, _i32, _i32],
     "snpmi_rccl_allgather": [_vp, _vp, _u64],
     "snpmi_rccl_host_allreduce_f64": [_vp, _u64, _i32],
     "snpmi_rccl_barrier": [],

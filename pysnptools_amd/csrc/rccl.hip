@@ -1,6 +1,7 @@
 // RCCL over xGMI for the SNP-sharded GRM: one process per GPU, each rank
-// accumulates the upper-triangle K tiles of its SNP blocks, then one in-place
-// ncclAllReduce(sum) of the tile buffer produces K on every rank.  In the K-partitioned
+// accumulates the upper-triangle K tiles of its SNP blocks, then one in-place ncclReduce(sum)
+// of the tile buffer produces K on the rank that returns it (ncclAllReduce when every rank
+// needs K, e.g. shard.grm_pieces).  In the K-partitioned
 // mode (cfg5) each rank uploads 1/p of a packed SNP block and ncclAllGather rebuilds the
 // whole block on every rank (packed codes are 16x smaller than the f32 values).  The unique id is
 // exchanged by the caller (bench.py: rank 0 writes it to an O_EXCL node-local file named by
@@ -50,6 +51,18 @@ int snpmi_rccl_allreduce_sum(void* buf, uint64_t count, int dtype) {
         ncclDataType_t t = dtype == SNPMI_DT_F64 ? ncclFloat64 : ncclFloat32;
         SNPMI_REQUIRE(dtype == SNPMI_DT_F32 || dtype == SNPMI_DT_F64, SNPMI_E_ARG, "all-reduce dtype must be f32/f64");
         SNPMI_NCCL(ncclAllReduce(buf, buf, count, t, ncclSum, g_comm, stream()));
+    });
+}
+
+int snpmi_rccl_reduce_sum(void* buf, uint64_t count, int dtype, int root) {
+    return guarded([&] {
+        SNPMI_REQUIRE(g_comm != nullptr, SNPMI_E_ARG, "RCCL communicator not initialised");
+        SNPMI_REQUIRE(dtype == SNPMI_DT_F32 || dtype == SNPMI_DT_F64, SNPMI_E_ARG, "reduce dtype must be f32/f64");
+        int nranks = 0;
+        SNPMI_NCCL(ncclCommCount(g_comm, &nranks));
+        SNPMI_REQUIRE(root >= 0 && root < nranks, SNPMI_E_ARG, "reduce root out of range");
+        const ncclDataType_t t = dtype == SNPMI_DT_F64 ? ncclFloat64 : ncclFloat32;
+        SNPMI_NCCL(ncclReduce(buf, buf, count, t, ncclSum, root, g_comm, stream()));
     });
 }
 

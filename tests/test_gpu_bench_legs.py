@@ -62,18 +62,20 @@ def test_grm_leg_partial_traces_sum_to_whole(world, dtype):
     assert 0 < whole["trace"] <= args.grm_iid * args.grm_sid * (1 + 1e-5)
 
 
-def test_bench_with_rccl_communicator_world1():
+@pytest.mark.parametrize("collective", ["reduce", "allreduce"])
+def test_bench_with_rccl_communicator_world1(collective):
     """The whole bench (every leg, parity checks, JSON line) with an RCCL communicator at world size
     1 (--force-rccl): the collective calls of the N > 1 plan run with their real buffers and sizes
     -- the in-place all-reduce of the K tiles (f32 and f64), the packed-block all-gather of the
-    partitioned GRM, the RCCL barrier and max-over-ranks -- and the line keeps its schema."""
+    partitioned GRM, the RCCL barrier and max-over-ranks -- and the line keeps its schema.  The K
+    tiles go through ncclReduce onto rank 0 (default) or ncclAllReduce (--grm-collective)."""
     import json
     import subprocess
 
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--force-rccl", "--steps", "1", "--warmup", "0",
            "--n-iid", "4099", "--n-sid", "6000", "--grm-iid", "5000", "--grm-sid", "12000", "--grm-block", "5000",
            "--grm5-iid", "20000", "--grm5-sid", "2048", "--e2e-sid", "4096", "--e2e-passes", "1",
-           "--cpu-seconds", "0.2"]
+           "--cpu-seconds", "0.2", "--grm-collective", collective]
     out = subprocess.run(cmd, capture_output=True, text=True, timeout=110)
     assert out.returncode == 0, out.stderr[-3000:]
     lines = [ln for ln in out.stdout.splitlines() if ln.strip()]
@@ -83,6 +85,7 @@ def test_bench_with_rccl_communicator_world1():
     for k in ("grm", "grm_f64"):
         assert d[k]["parity"]["pass"], d[k]["parity"]
         assert d[k]["allreduce_ms"] > 0
+        assert d[k]["collective"] == ("ncclReduce(sum, root 0)" if collective == "reduce" else "ncclAllReduce(sum)")
     assert d["grm5"]["parity"]["pass"] and d["grm5"]["parity"]["gathered_block_bit_exact"]
     assert d["grm5"]["allgather_ms"] > 0
     assert "+ RCCL all-gather" in d["grm5"]["workload"]
