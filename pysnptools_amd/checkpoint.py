@@ -1,0 +1,150 @@
+"""Checkpoint / resume for long GRMs ("Checkpoint / resume": the reference
+accumulates K in host RAM block by block and loses it on a crash, snpreader.py:643-655).
+
+``read_kernel_checkpointed`` computes the same K as ``Bed.read_kernel`` (snpreader.py:623-668)
+as one GPU GRM session over SNP blocks (``snpmi_grm_begin`` / ``snpmi_grm_add_bed_*`` /
+``snpmi_grm_end``) and, every ``every`` blocks, persists (the device K tiles, the next block,
+the per-SNP stats so far) next to ``path``.  A later call with the same reader, standardizer,
+block size and dtype restores the tiles into a new session and continues at the next block, so
+an interrupted run resumes instead of starting over; the resumed K is bit-identical to an
+uninterrupted checkpointed run (same blocks, same accumulation order).  The files are written
+to temporaries and renamed (tiles first, then the JSON that commits them), so a crash while
+saving leaves the previous checkpoint intact.  They are removed when the GRM completes.
+"""
+import hashlib
+import json
+import os
+
+import numpy as np
+
+from pysnptools_amd import _native as N
+
+
+class _Interrupted(RuntimeError):
+    """Raised by the ``_stop_after`` test hook (a simulated crash after that many blocks)."""
+
+
+def _digest(idx):
+    return None if idx is None else hashlib.sha1(np.ascontiguousarray(idx, dtype=np.uint64).tobytes()).hexdigest()
+
+
+def _fingerprint(bed_path, n, m, dtype, block_size, kind, a, b, use_stats, rows, cols, count_a1, stats_in):
+    st = os.stat(bed_path)
+    return {"bed": os.path.abspath(bed_path), "size": st.st_size, "mtime_ns": st.st_mtime_ns, "n": int(n),
+            "m": int(m), "dtype": np.dtype(dtype).str, "block_size": int(block_size), "kind": int(kind),
+            "a": None if np.isnan(a) else float(a), "b": None if np.isnan(b) else float(b),
+            "use_stats": bool(use_stats), "count_A1": bool(count_a1), "rows": _digest(rows), "cols": _digest(cols),
+            "stats_in": None if stats_in is None else hashlib.sha1(np.ascontiguousarray(stats_in).tobytes()).hexdigest()}
+
+
+def _paths(path):
+    return path + ".json", path + ".tiles.npy", path + ".stats.npy"
+
+
+def _session_tiles():
+    import ctypes
+
+    tiles, count = ctypes.c_void_p(), ctypes.c_uint64()
+    N.call("snpmi_grm_session_tiles", ctypes.byref(tiles), ctypes.byref(count))
+    return tiles, count.value
+
+
+def _save(path, meta, next_block, stats, dtype):
+    jpath, tpath, spath = _paths(path)
+    tiles, count = _session_tiles()
+    host = np.empty(count, dtype=dtype)
+    N.call("snpmi_stream_sync")
+    N.call("snpmi_memcpy_d2h", N.ptr(host), tiles, host.nbytes)
+    for p, arr in ((tpath, host), (spath, stats)):
+        with open(p + ".tmp", "wb") as f:
+            np.save(f, arr, allow_pickle=False)
+        os.replace(p + ".tmp", p)
+    with open(jpath + ".tmp", "w") as f:
+        json.dump(dict(meta, next_block=int(next_block)), f)
+    os.replace(jpath + ".tmp", jpath)
+
+
+def _restore(path, meta, dtype):
+    """next block and stats of a matching checkpoint (tiles copied into the open session), or None."""
+    jpath, tpath, spath = _paths(path)
+    if not os.path.exists(jpath):
+        return None
+    with open(jpath) as f:
+        saved = json.load(f)
+    nb = saved.pop("next_block")
+    if saved != meta:
+        raise ValueError("checkpoint '%s' belongs to another GRM (reader, standardizer, block size or dtype "
+                         "differ); remove it or choose another path" % path)
+    host = np.load(tpath, allow_pickle=False)
+    tiles, count = _session_tiles()
+    if host.dtype != np.dtype(dtype) or host.size != count:
+        raise ValueError("checkpoint '%s' tiles do not match this GRM" % path)
+    N.call("snpmi_memcpy_h2d", tiles, N.ptr(host), host.nbytes)
+    N.call("snpmi_stream_sync")
+    return nb, np.load(spath, allow_pickle=False)
+
+
+def read_kernel_checkpointed(reader, standardizer, path, block_size=10000, every=10, dtype=np.float64,
+                             num_threads=None, _stop_after=None):
+    """``reader.read_kernel(standardizer, block_size, dtype=dtype)`` with K checkpointed to
+    ``path`` every ``every`` SNP blocks and resumed from it.  ``reader`` is a Bed or a subset of
+    one; ``standardizer`` Unit / Beta / their trained forms / Identity.  Returns
+    (KernelData, trained standardizer)."""
+    from pysnptools_amd.kernelreader import KernelData
+    from pysnptools_amd.snpreader.bed import Bed
+    from pysnptools_amd.snpreader.snpreader import _resolve, _trained_from
+    from pysnptools_amd.standardizer.standardizer import _std_args
+    from pysnptools_amd.util import get_num_threads
+
+    dtype = np.dtype(dtype)
+    if dtype not in (np.float32, np.float64):
+        raise ValueError("GRM dtype must be float32 or float64")
+    args = _std_args(standardizer)
+    if args is None:
+        raise ValueError("read_kernel_checkpointed supports Unit/Beta/UnitTrained/BetaTrained/Identity")
+    kind, a, b, use_stats, _, _ = args
+    assert block_size >= 1 and every >= 1
+    base, rows, cols = _resolve(reader)
+    if not isinstance(base, Bed):
+        raise ValueError("read_kernel_checkpointed reads a Bed (or a subset of one)")
+    base._run_once()
+    n, m = reader.iid_count, reader.sid_count
+    sid = reader.sid
+    stats_in = np.ascontiguousarray(standardizer.stats_for(sid), dtype=dtype) if use_stats else None
+    meta = _fingerprint(base.filename, n, m, dtype, block_size, kind, a, b, use_stats, rows, cols, base.count_A1,
+                        stats_in)
+    col_index = np.arange(base.sid_count, dtype=np.uint64) if cols is None else np.asarray(cols, dtype=np.uint64)
+    ri = N.index_array(rows)
+    sfx = N.suffix(dtype)
+    threads = get_num_threads(num_threads if num_threads is not None else base._num_threads)
+    nblocks = (m + block_size - 1) // block_size
+    K = np.empty((n, n), dtype=dtype)
+    N.call("snpmi_grm_begin", n, N.dt_code(dtype))
+    done = False
+    try:
+        stats = stats_in.copy() if use_stats else np.zeros((m, 2), dtype=dtype)
+        got = _restore(path, meta, dtype)
+        start = 0
+        if got is not None:
+            start, stats = got
+        for k in range(start, nblocks):
+            s0 = k * block_size
+            ci = np.ascontiguousarray(col_index[s0:s0 + block_size])
+            pst = np.ascontiguousarray(stats[s0:s0 + len(ci)])
+            N.call("snpmi_grm_add_bed_" + sfx, base.filename.encode(), base.iid_count, base.sid_count,
+                   int(bool(base.count_A1)), N.ptr(ri), n, N.ptr(ci), len(ci), kind, a, b, int(use_stats),
+                   N.ptr(pst), threads)
+            if not use_stats:
+                stats[s0:s0 + len(ci)] = pst
+            if (k + 1) % every == 0 and k + 1 < nblocks:
+                _save(path, meta, k + 1, stats, dtype)
+            if _stop_after is not None and k + 1 >= _stop_after:
+                raise _Interrupted("stopped after %d blocks (test hook)" % (k + 1))
+        done = True
+    finally:
+        N.call("snpmi_grm_end", 0, None, N.ptr(K))
+    if done:
+        for p in _paths(path):
+            if os.path.exists(p):
+                os.remove(p)
+    return KernelData(iid=reader.iid, val=K), _trained_from(standardizer, kind, a, b, sid, stats)
