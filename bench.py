@@ -90,6 +90,8 @@ def parse(argv=None):
     p.add_argument("--grm5", choices=["on", "off"], default="on", help="cfg5 partitioned-K GRM leg")
     p.add_argument("--grm5-iid", type=int, default=500_000)
     p.add_argument("--grm5-sid", type=int, default=8192)
+    p.add_argument("--grm5-stream", type=int, default=2,
+                   help="cfg5: blocks streamed with the next upload under the current SYRK (0 = off)")
     p.add_argument("--e2e", choices=["on", "off"], default="on", help="pinned-host -> HBM streaming leg")
     p.add_argument("--e2e-sid", type=int, default=8192, help="SNPs held in pinned host memory")
     p.add_argument("--e2e-passes", type=int, default=4)
@@ -741,11 +743,60 @@ def leg_grm5(N, args, dist):
         res["gather_exact"] = bool(np.array_equal(sample, chk))
         del chk
         res["parity_sample"] = (picks, sample)
+    if args.grm5_stream > 0:  # after the parity copies: it accumulates into the same K part
+        res["stream"] = grm5_stream(N, args, dist, host, packed, lut, stats, blocks, n, m, ms, pitch, P)
     ev.destroy()
     N.call("snpmi_host_free", host)
     for d in (packed, lut, stats, blocks):
         d.free()
     return res
+
+
+def grm5_stream(N, args, dist, host, packed, lut, stats, blocks, n, m, ms, pitch, P):
+    """The streamed form of the cfg5 job (untimed leg above = one block): K blocks of m SNPs, the
+    rank's share of block k+1 uploaded on the copy stream (its own device buffer, events only) while
+    block k's stats + SYRK run on the compute stream, accumulating into the same K part.  Only the
+    first upload is exposed.  The host share is the same pinned buffer for every block (the same SNPs
+    streamed K times: identical work per block)."""
+    K = args.grm5_stream
+    second = Dev(N, pitch * m)
+    N.call("snpmi_dev_memset", second.p, 0, pitch * m)
+    bufs = [packed, second]
+    up = Events(N, K)  # copy stream: upload k done
+    done = Events(N, K)  # compute stream: SYRK k done (buffer k % 2 free again)
+    ce = Events(N, 2 * K + 1)  # compute stream: block k start (after its upload) / end; [2K] = t0
+    N.call("snpmi_stream_sync")
+    dist.barrier()
+    t0 = time.perf_counter()
+    ce.record(2 * K)
+    for k in range(min(2, K)):
+        N.call("snpmi_memcpy_async", bufs[k].at(dist.rank * ms * pitch), host, ms * pitch, 0, 1)
+        up.record(k, on_copy=1)
+    for k in range(K):
+        buf = bufs[k % 2]
+        N.call("snpmi_stream_wait_event", up.ev[k], 0)
+        ce.record(2 * k)
+        if dist.rccl:
+            N.call("snpmi_rccl_allgather", buf.at(dist.rank * ms * pitch), buf.p, ms * pitch)
+        N.call("snpmi_dev_snp_stats", buf.p, pitch, n, m, 0, N.STD_UNIT, 0.0, 0.0, 0, N.DT_F32, stats.p, lut.p)
+        N.call("snpmi_dev_syrk_packed_part", buf.p, pitch, n, m, lut.p, dist.rank, P, blocks.p, int(k > 0))
+        ce.record(2 * k + 1)
+        done.record(k)
+        if k + 2 < K:  # refill this buffer once its SYRK has read it
+            N.call("snpmi_stream_wait_event", done.ev[k], 1)
+            N.call("snpmi_memcpy_async", buf.at(dist.rank * ms * pitch), host, ms * pitch, 0, 1)
+            up.record(k + 2, on_copy=1)
+    N.call("snpmi_stream_sync")
+    dist.barrier()
+    wall = dist.max(time.perf_counter() - t0)
+    per_block = [ce.ms(2 * k, 2 * k + 1) for k in range(K)]
+    gaps = [ce.ms(2 * k - 1, 2 * k) for k in range(1, K)]  # compute idle waiting for an upload
+    first = ce.ms(2 * K, 0)  # the first upload (+ all-gather issue), exposed
+    for e in (up, done, ce):
+        e.destroy()
+    second.free()
+    return {"blocks": K, "seconds": wall, "block_ms": per_block, "upload_wait_ms_after_first": gaps,
+            "first_upload_ms": first}
 
 
 def grm5_parity(args, m, picks, sample):
@@ -884,6 +935,17 @@ def main(argv=None):
                 "projected_seconds_1M_snps": r3["wall"] * 1_000_000 / m5,
                 "projected_note": "per process; the 8 parts run concurrently on 8 GPUs, so this is the 8-GPU "
                                   "job time when N = 8, and N = 1 shows one part's share"}
+        if r3.get("stream"):
+            st5 = r3["stream"]
+            first = st5["first_upload_ms"] * 1e-3
+            grm5["streamed"] = {
+                "workload": "%d blocks of %d SNPs: block k+1's upload (copy stream, own buffer) under block k's "
+                            "stats + SYRK (compute stream), accumulating into this part's K" % (st5["blocks"], m5),
+                "blocks": st5["blocks"], "seconds": st5["seconds"], "block_ms": st5["block_ms"],
+                "upload_wait_ms_after_first": st5["upload_wait_ms_after_first"],
+                "exposed_first_upload_ms": first * 1e3,
+                "snps_per_s": st5["blocks"] * m5 / st5["seconds"],
+                "projected_seconds_1M_snps": first + np.mean(st5["block_ms"]) * 1e-3 * 1_000_000 / m5}
         if r3.get("parity_sample") is not None:
             grm5["parity"] = grm5_parity(args, m5, *r3["parity_sample"])
             grm5["parity"]["gathered_block_bit_exact"] = r3["gather_exact"]

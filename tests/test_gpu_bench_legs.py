@@ -88,4 +88,6 @@ def test_bench_with_rccl_communicator_world1(collective):
         assert d[k]["collective"] == ("ncclReduce(sum, root 0)" if collective == "reduce" else "ncclAllReduce(sum)")
     assert d["grm5"]["parity"]["pass"] and d["grm5"]["parity"]["gathered_block_bit_exact"]
     assert d["grm5"]["allgather_ms"] > 0
+    st5 = d["grm5"]["streamed"]  # two blocks, the second upload under the first SYRK
+    assert st5["blocks"] == 2 and len(st5["block_ms"]) == 2 and st5["seconds"] > 0
     assert "+ RCCL all-gather" in d["grm5"]["workload"]
