@@ -90,6 +90,9 @@ def parse(argv=None):
     p.add_argument("--grm5", choices=["on", "off"], default="on", help="cfg5 partitioned-K GRM leg")
     p.add_argument("--grm5-iid", type=int, default=500_000)
     p.add_argument("--grm5-sid", type=int, default=8192)
+    p.add_argument("--out-ld", type=int, default=8_000_000,
+                   help="decode leg: leading dimension (floats) of the f32 F-order block buffer: a 32 MB column "
+                        "pitch spreads the 4 GB block over 64 GB of HBM pages (DESIGN 3.1); 0 = round_up(n, 16)")
     p.add_argument("--grm5-stream", type=int, default=2,
                    help="cfg5: blocks streamed with the next upload under the current SYRK (0 = off)")
     p.add_argument("--e2e", choices=["on", "off"], default="on", help="pinned-host -> HBM streaming leg")
@@ -319,7 +322,17 @@ def leg_standardize(N, args, dist):
     packed = Dev(N, pitch * max(m, 1))
     synth(N, packed.p, pitch, n, lo, m, args.seed, 0.01)
     nblk = (m + B - 1) // B
-    lut, stats, out = Dev(N, B * 16), Dev(N, B * 8), Dev(N, B * ld * 4)
+    lut, stats = Dev(N, B * 16), Dev(N, B * 8)
+    tight = ld
+    out = None
+    if args.out_ld > ld and B * ld * 4 >= (1 << 30):  # only blocks of >= 1 GB gain from it
+        try:
+            out = Dev(N, B * (args.out_ld // 16 * 16) * 4)
+            ld = args.out_ld // 16 * 16
+        except Exception:  # not enough HBM for the spread layout: tight columns
+            out = None
+    if out is None:
+        out = Dev(N, B * ld * 4)
     ev = Events(N, 2 + 2 * nblk)
     N.call("snpmi_set_kernel_variant", b"decode", args.decode_variant)
 
@@ -370,7 +383,7 @@ def leg_standardize(N, args, dist):
     bytes_per_step = m * ((n + 3) // 4 + 4 * n)
     achieved_gbs = bytes_per_step * args.steps / (dec_ms_total * 1e-3) / 1e9 if dec_ms_total else 0.0
     # measured stream ceilings (untimed): device-to-device copy and write-only fill of the block buffer
-    cbytes = min(B * ld * 4, pitch * m)
+    cbytes = min(B * tight * 4, pitch * m)
     N.call("snpmi_dev_memcpy_d2d", out.p, packed.p, cbytes)
     N.call("snpmi_stream_sync")
     ev.record(0)
@@ -381,10 +394,10 @@ def leg_standardize(N, args, dist):
     copy_gbs = 2 * 5 * cbytes / (ev.ms(0, 1) * 1e-3) / 1e9
     ev.record(0)
     for _ in range(5):
-        N.call("snpmi_dev_memset", out.p, 0, B * ld * 4)
+        N.call("snpmi_dev_memset", out.p, 0, B * tight * 4)
     ev.record(1)
     N.call("snpmi_stream_sync")
-    fill_gbs = 5 * B * ld * 4 / (ev.ms(0, 1) * 1e-3) / 1e9
+    fill_gbs = 5 * B * tight * 4 / (ev.ms(0, 1) * 1e-3) / 1e9
     sample = gpu_cols = None
     if dist.rank == 0 and not args.skip_cpu:
         # parity sample: the first 512 columns, re-decoded by the same kernels (untimed)
@@ -392,11 +405,15 @@ def leg_standardize(N, args, dist):
         sample = np.empty((ncols, pitch), dtype=np.uint8)
         N.call("snpmi_memcpy_d2h", N.ptr(sample), packed.p, sample.nbytes)
         run_block(packed.p, ncols, False, 0)
-        gpu_cols = np.empty((ncols, ld), dtype=np.float32)
-        N.call("snpmi_memcpy_d2h", N.ptr(gpu_cols), out.p, gpu_cols.nbytes)
+        gpu_cols = np.empty((ncols, tight), dtype=np.float32)
+        if ld == tight:
+            N.call("snpmi_memcpy_d2h", N.ptr(gpu_cols), out.p, gpu_cols.nbytes)
+        else:
+            for j in range(ncols):
+                N.call("snpmi_memcpy_d2h", N.ptr(gpu_cols[j]), out.at(j * ld * 4), tight * 4)
     res = dict(wall=wall, weak_wall=weak_wall, dec_mean_ms=dec_mean_ms, achieved_gbs=achieved_gbs,
                copy_gbs=copy_gbs, fill_gbs=fill_gbs, full_block_bytes=B * ((n + 3) // 4 + 4 * n), launches=launches,
-               nblk=nblk, pitch=pitch, sample=sample, gpu_cols=gpu_cols, m=m)
+               nblk=nblk, pitch=pitch, sample=sample, gpu_cols=gpu_cols, m=m, out_ld=ld)
     ev.destroy()
     for d in (packed, lut, stats, out):
         d.free()
@@ -974,6 +991,7 @@ def main(argv=None):
                                    "HBM, SnpGen MAF curve, 1%% missing), SNPs split into %d contiguous shard(s), "
                                    "block %d SNPs, f32 F-order" % (n, args.n_sid, dist.world, args.block),
                        "n_iid": n, "n_sid": args.n_sid, "n_sid_per_gpu": r1["m"], "block": args.block,
+                       "block_buffer_ld": r1["out_ld"],
                        "parallelism": "snp-shard x%d" % dist.world},
             "weak": ({"value": args.n_sid * args.steps * dist.world / r1["weak_wall"], "unit": "SNPs/s",
                       "workload": "every rank streams 1M SNPs per step (its shard %d times)" % dist.world}
