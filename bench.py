@@ -93,6 +93,9 @@ def parse(argv=None):
     p.add_argument("--out-ld", type=int, default=8_000_000,
                    help="decode leg: leading dimension (floats) of the f32 F-order block buffer: a 32 MB column "
                         "pitch spreads the 4 GB block over 64 GB of HBM pages (DESIGN 3.1); 0 = round_up(n, 16)")
+    p.add_argument("--out-ld-c", type=int, default=32768,
+                   help="C-order decode leg: row pitch (floats) of the output: 128 KB rows spread the 4 GB over "
+                        "64 GB of HBM pages (DESIGN 3.1); 0 = the block width")
     p.add_argument("--grm5-stream", type=int, default=2,
                    help="cfg5: blocks streamed with the next upload under the current SYRK (0 = off)")
     p.add_argument("--e2e", choices=["on", "off"], default="on", help="pinned-host -> HBM streaming leg")
@@ -426,21 +429,31 @@ def leg_decode_c(N, args):
     pitch = N.lib().snpmi_packed_pitch(n)
     packed = Dev(N, pitch * B)
     synth(N, packed.p, pitch, n, 0, B, args.seed, 0.01)
-    lut, stats, out = Dev(N, B * 16), Dev(N, B * 8), Dev(N, B * n * 4)
+    lut, stats = Dev(N, B * 16), Dev(N, B * 8)
+    rld, out = B, None
+    if args.out_ld_c > B and B * n * 4 >= (1 << 30):
+        try:
+            out = Dev(N, n * (args.out_ld_c // 4 * 4) * 4)
+            rld = args.out_ld_c // 4 * 4
+        except Exception:  # not enough HBM for the spread rows: tight rows
+            out = None
+    if out is None:
+        out = Dev(N, B * n * 4)
     N.call("snpmi_dev_snp_stats", packed.p, pitch, n, B, 0, N.STD_UNIT, 0.0, 0.0, 0, N.DT_F32, stats.p, lut.p)
-    N.call("snpmi_dev_decode", packed.p, pitch, n, B, lut.p, N.DT_F32, 1, out.p, B)
+    N.call("snpmi_dev_decode", packed.p, pitch, n, B, lut.p, N.DT_F32, 1, out.p, rld)
     ev = Events(N, 2 * reps)
     N.call("snpmi_stream_sync")
     for r in range(reps):
         ev.record(2 * r)
-        N.call("snpmi_dev_decode", packed.p, pitch, n, B, lut.p, N.DT_F32, 1, out.p, B)
+        N.call("snpmi_dev_decode", packed.p, pitch, n, B, lut.p, N.DT_F32, 1, out.p, rld)
         ev.record(2 * r + 1)
     N.call("snpmi_stream_sync")
     ms = float(np.mean([ev.ms(2 * r, 2 * r + 1) for r in range(reps)]))
     nbytes = B * ((n + 3) // 4 + 4 * n)
     # parity: C-order rows equal the F-order decode transposed (first 64 iids x all SNPs)
     rows = np.empty((64, B), dtype=np.float32)
-    N.call("snpmi_memcpy_d2h", N.ptr(rows), out.p, rows.nbytes)
+    for i in range(64):
+        N.call("snpmi_memcpy_d2h", N.ptr(rows[i]), out.at(i * rld * 4), B * 4)
     ld = (n + 15) // 16 * 16
     fout = Dev(N, B * ld * 4)
     N.call("snpmi_dev_decode", packed.p, pitch, n, B, lut.p, N.DT_F32, 0, fout.p, ld)
@@ -451,7 +464,8 @@ def leg_decode_c(N, args):
     for d in (packed, lut, stats, out, fout):
         d.free()
     gbs = nbytes / (ms * 1e-3) / 1e9
-    return {"workload": "C-order decode of %d SNPs x %d iids (f32, rows of %d SNPs)" % (B, n, B),
+    return {"workload": "C-order decode of %d SNPs x %d iids (f32, rows of %d SNPs, row pitch %d floats)"
+                        % (B, n, B, rld), "row_ld": rld,
             "kernel": "k_decode_c_reg<float>", "mean_launch_ms": ms, "per_launch_bytes": nbytes,
             "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS,
             "parity": {"check": "rows 0..63 == F-order decode transposed", "bit_exact": same}}
