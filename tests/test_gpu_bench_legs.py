@@ -91,3 +91,20 @@ def test_bench_with_rccl_communicator_world1(collective):
     st5 = d["grm5"]["streamed"]  # two blocks, the second upload under the first SYRK
     assert st5["blocks"] == 2 and len(st5["block_ms"]) == 2 and st5["seconds"] > 0
     assert "+ RCCL all-gather" in d["grm5"]["workload"]
+
+
+def test_decode_leg_wide_block_buffer_same_values():
+    """The decode leg's 32 MB-pitch block buffer (--out-ld 8000000, used for blocks >= 1 GB) holds
+    the same values as tight columns: 131072 iids x 2048-SNP blocks (1 GB), first 512 columns
+    compared bit for bit, and against the oracle's decode + one-pass Unit."""
+    from oracle import oracle as O
+
+    base = ["--n-iid", "131072", "--n-sid", "4096", "--block", "2048", "--steps", "1", "--warmup", "0"]
+    wide = bench.leg_standardize(N, bench.parse(base + ["--out-ld", "8000000"]), FakeDist(0, 1))
+    tight = bench.leg_standardize(N, bench.parse(base + ["--out-ld", "0"]), FakeDist(0, 1))
+    assert wide["out_ld"] == 8_000_000 and tight["out_ld"] == 131072
+    assert np.array_equal(wide["gpu_cols"], tight["gpu_cols"])
+    n, ncols = 131072, wide["gpu_cols"].shape[0]
+    body = np.ascontiguousarray(wide["sample"][:, :(n + 3) // 4]).reshape(-1)
+    ref, _ = O.decode_standardize(body, n, ncols, dtype=np.float32)
+    assert np.array_equal(wide["gpu_cols"][:, :n].T, ref)
