@@ -14,8 +14,12 @@ Metric (BASELINE.json): "SNPs/sec standardized (500k x 1M) + GRM GF/s at 1/2/4/8
   e2e        = packed columns in pinned HOST memory -> H2D on the copy stream -> stats + decode on
                the compute stream (3-slot ring, events only) -> f32 in HBM: the PCIe-inclusive rate,
                with the measured H2D peak of the same buffer beside it.  Never `value`.
-  grm        = SnpKernel GRM of configs[3] (50k iid x 500k SNP, Unit, block 10k, f32): contiguous SNP
-               shards per rank, one RCCL all-reduce of the upper-triangle K tiles.  The f32
+  grm        = SnpKernel GRM of configs[3] (50k iid x 500k SNP, Unit, f32): rank r of N owns the
+               contiguous SNP span [r*M/N, (r+1)*M/N) and accumulates it through
+               pysnptools_amd.shard.ShardedGrm (the same code as shard.grm_sharded, which
+               Bed.read_kernel uses under an open process group) into upper-triangle K tiles in
+               HBM, <= 65536 SNPs per SYRK launch; then one ncclReduce(sum) of the tiles onto rank 0
+               (--grm-collective allreduce: ncclAllReduce).  The f32
                products run on the fp16 MFMA pipe as 3 fp16 products of each value's fp16x2 split
                (f32-level accuracy, f32 accumulate; bf16x3 = 6 bf16 products when a SNP's LUT is
                outside fp16's range).  gflops uses N(N+1)M (SYRK work); roofline
@@ -32,17 +36,24 @@ Metric (BASELINE.json): "SNPs/sec standardized (500k x 1M) + GRM GF/s at 1/2/4/8
                max(N, 8) for one 8192-SNP block uploaded from pinned host memory inside the timed
                region (1/N each + RCCL all-gather at N > 1), parity-checked on a diagonal and an
                off-diagonal block, projected to 1M SNPs.
+  beta       = configs[2]: 100k iid x 1M SNP, Beta(1,25) + NaN impute (21.8% missing, SnpGen's
+               rate), packed resident in HBM, stats + decode in 2048-SNP blocks (f32, F order).
+  file       = the reference's own call path on a synthetic 50k x 100k .bed written to local disk
+               (untimed; read from the page cache): Bed.read_kernel(Unit(), float32) with K left in
+               HBM and copied out, Bed[:, :10000].read(float32, xp='hbm'), and the cfg3 workload
+               Bed.read(float32, xp='hbm').standardize(Beta(1,25)) -- PCIe-inclusive, never `value`.
   cpu_baseline = the oracle's C/OpenMP decode + one-pass Unit standardize (the CPU restatement
                of bed-reader's read + standardize_f32) on a sample of the same packed columns,
-               rank 0 at N = 1 only, at the box's CPU share and at 1 thread; grm.cpu_baseline =
-               NumPy/OpenBLAS Z.dot(Z.T) (snpreader.py:655) with the BLAS pool pinned.
+               rank 0 at N = 1 only, at the largest usable thread count (affinity / cgroup quota)
+               and at 1 thread; grm.cpu_baseline = the reference's block step (NumPy/OpenBLAS
+               Z.dot(Z.T), snpdata.py:203-206, + the single-threaded K += of snpreader.py:655) on a
+               50k-iid slice, extrapolated to configs[3].
 
 Run: python bench.py [--gpus N --steps K --warmup W].  N > 1 either under torch.distributed.run
 (RANK / WORLD_SIZE / LOCAL_RANK from the environment) or as a plain `python bench.py --gpus N`, which
 spawns the N rank processes itself before anything touches the GPU and relays rank 0's line.
 """
 import argparse
-import contextlib
 import ctypes
 import json
 import os
@@ -106,6 +117,18 @@ def parse(argv=None):
     p.add_argument("--cpu-seconds", type=float, default=6.0)
     p.add_argument("--seed", type=int, default=5)
     p.add_argument("--force-rccl", action="store_true", help="build the RCCL communicator even at world size 1")
+    p.add_argument("--dist-timeout", type=float, default=300.0, help="seconds for the RCCL id wait and init")
+    p.add_argument("--tight-reps", type=int, default=8,
+                   help="decode leg: launches timed on a tight-column buffer beside the block buffer (frac_tight)")
+    p.add_argument("--beta", choices=["on", "off"], default="on", help="configs[2] leg: Beta(1,25) at 100k x 1M")
+    p.add_argument("--beta-iid", type=int, default=100_000)
+    p.add_argument("--beta-sid", type=int, default=1_000_000)
+    p.add_argument("--file", choices=["on", "off"], default="on", help="file-backed leg through the mirrored API")
+    p.add_argument("--file-iid", type=int, default=50_000)
+    p.add_argument("--file-sid", type=int, default=100_000)
+    p.add_argument("--file-dir", default=None, help="directory for the synthetic .bed (default: $TMPDIR)")
+    p.add_argument("--cpu-grm-iid", type=int, default=50_000, help="GRM CPU baseline: iids of the timed slice")
+    p.add_argument("--cpu-grm-sid", type=int, default=256, help="GRM CPU baseline: SNPs of the timed syrk")
     return p.parse_args(argv)
 
 
@@ -147,105 +170,6 @@ def spawn_ranks(args, argv):
             os.remove(os.path.join(tmp, f))
         os.rmdir(tmp)
     return rc
-
-
-@contextlib.contextmanager
-def stdout_to_stderr():
-    """RCCL prints a version banner on the C stdout (fd 1) around communicator setup; the bench's
-    stdout must carry only its one JSON line."""
-    sys.stdout.flush()
-    saved = os.dup(1)
-    os.dup2(2, 1)
-    try:
-        yield
-    finally:
-        os.dup2(saved, 1)
-        os.close(saved)
-
-
-def _id_file():
-    """Node-local path for the ncclUniqueId: given by the spawning parent, else derived from the
-    launcher (parent pid + its start time, so no stale file of an earlier launcher can match)."""
-    path = os.environ.get("SNPMI_RCCL_ID_FILE")
-    if path:
-        return path
-    ppid = os.getppid()
-    try:
-        start = open("/proc/%d/stat" % ppid).read().rsplit(")", 1)[1].split()[19]
-    except OSError:
-        start = "0"
-    key = "snpmi_rccl_%d_%s_%s.id" % (ppid, start, os.environ.get("MASTER_PORT", "0"))
-    return os.path.join(tempfile.gettempdir(), key)
-
-
-class Dist:
-    """Control plane for one process per GPU WITHOUT torch: importing torch would load its own
-    libamdhip64.so.7 (ROCm 7.0) next to libsnpmi's (ROCm 7.2) -- same SONAME, two runtimes.  The
-    ncclUniqueId goes from rank 0 to the others through an O_EXCL node-local file (removed once
-    every rank holds the communicator); barriers / max-over-ranks are RCCL all-reduces."""
-
-    def __init__(self, gpus, N, force_rccl=False):
-        self.N = N
-        self.world = int(os.environ.get("WORLD_SIZE", "1"))
-        self.rank = int(os.environ.get("RANK", "0"))
-        self.local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-        if self.world != gpus:
-            raise SystemExit("bench.py: --gpus %d but WORLD_SIZE=%d (one process per GPU)" % (gpus, self.world))
-        N.call("snpmi_set_device", self.local_rank)
-        self.rccl = False
-        self.n_gpus = 1
-        self._path = None
-        if self.world > 1 or force_rccl:
-            path = _id_file()
-            uid = (ctypes.c_uint8 * 128)()
-            if self.rank == 0:
-                with stdout_to_stderr():
-                    N.call("snpmi_rccl_unique_id", uid, 128)
-                tmp = path + ".tmp"
-                fd = os.open(tmp, os.O_WRONLY | os.O_CREAT | os.O_EXCL, 0o600)
-                with os.fdopen(fd, "wb") as f:
-                    f.write(bytes(uid))
-                try:
-                    os.link(tmp, path)  # fails if a file of that name exists: never overwrite
-                finally:
-                    os.remove(tmp)
-                self._path = path
-            else:
-                t0 = time.time()
-                while not os.path.exists(path):
-                    if time.time() - t0 > 300:
-                        raise TimeoutError("rank %d: no RCCL id from rank 0 at %s" % (self.rank, path))
-                    time.sleep(0.05)
-                with open(path, "rb") as f:
-                    uid = (ctypes.c_uint8 * 128).from_buffer_copy(f.read(128))
-            with stdout_to_stderr():
-                N.call("snpmi_rccl_init", self.world, self.rank, uid, 128)
-            self.rccl = True
-            self.barrier()
-            if self._path:
-                os.remove(self._path)
-                self._path = None
-            cnt = ctypes.c_int()
-            N.call("snpmi_rccl_comm_count", ctypes.byref(cnt))
-            self.n_gpus = cnt.value
-
-    def barrier(self):
-        if self.rccl:
-            self.N.call("snpmi_rccl_barrier")
-
-    def max(self, x):
-        if not self.rccl:
-            return x
-        v = (ctypes.c_double * 1)(float(x))
-        self.N.call("snpmi_rccl_host_allreduce_f64", v, 1, 1)
-        return float(v[0])
-
-    def close(self):
-        if self._path and os.path.exists(self._path):
-            os.remove(self._path)
-        if self.rccl:
-            with stdout_to_stderr():
-                self.N.call("snpmi_rccl_destroy")
 
 
 class Dev:
@@ -304,11 +228,48 @@ def synth(N, buf, pitch, n, sid0, m, seed, miss):
     N.call("snpmi_dev_synth_bed", buf, pitch, n, sid0, m, seed, miss, N.ptr(x), N.ptr(cdf), len(x))
 
 
+def cgroup_cpu_quota():
+    """CPUs the cgroup grants (cpu.max on cgroup v2, cfs quota/period on v1), None if unlimited."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        return None if quota == "max" else int(quota) / int(period)
+    except (OSError, ValueError):
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+            quota = int(f.read())
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+            period = int(f.read())
+        return None if quota <= 0 else quota / period
+    except (OSError, ValueError):
+        return None
+
+
+def cpu_counts():
+    """Every CPU count that bounds this process: the affinity mask, the cgroup quota, the
+    machine (os.cpu_count(): on the GPU box the whole host, not this job's share) and
+    OMP_NUM_THREADS (the box's per-GPU CPU share).  ``usable`` = the smallest bound."""
+    aff = len(os.sched_getaffinity(0))
+    quota = cgroup_cpu_quota()
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or None
+    usable = aff
+    if quota:
+        usable = min(usable, max(1, int(quota)))
+    if omp:
+        usable = min(usable, omp)
+    return {"affinity": aff, "cgroup_quota": quota, "os_cpu_count": os.cpu_count(), "omp_num_threads": omp,
+            "usable": usable}
+
+
 def cpu_threads():
-    """The CPU share this process may use: OMP_NUM_THREADS (16 per GPU on the box), else the
-    affinity mask.  os.cpu_count() on the box reports the whole machine."""
-    env = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
-    return env or len(os.sched_getaffinity(0))
+    return cpu_counts()["usable"]
+
+
+def _counts_text(c):
+    return ("affinity %d CPUs, cgroup quota %s, os.cpu_count() %d, OMP_NUM_THREADS %s -> %d threads"
+            % (c["affinity"], "none" if c["cgroup_quota"] is None else "%.1f" % c["cgroup_quota"],
+               c["os_cpu_count"] or 0, c["omp_num_threads"], c["usable"]))
 
 
 def shard(m, rank, world):
@@ -316,19 +277,30 @@ def shard(m, rank, world):
 
 
 # ---------------------------------------------------------------------------- leg 1: decode + standardize
-def leg_standardize(N, args, dist):
-    n, B = args.n_iid, args.block
-    lo, hi = shard(args.n_sid, dist.rank, dist.world)
+WIDE_MIN_BYTES = 512 << 20  # block buffers of >= 512 MB take the wide column pitch
+
+
+def leg_standardize(N, args, dist, n=None, n_sid=None, std=None, a=0.0, b=0.0, miss=0.01, seed=None):
+    """Stats + decode of this rank's SNP shard of the n x n_sid packed matrix (resident in HBM) in
+    blocks of args.block SNPs into an f32 F-order block buffer; Unit by default, Beta(a, b) with
+    std=N.STD_BETA.  Beside the timed steps (untimed): the same kernel on a tight-column buffer
+    (frac_tight) and the measured copy / fill ceilings."""
+    n = args.n_iid if n is None else n
+    n_sid = args.n_sid if n_sid is None else n_sid
+    std = N.STD_UNIT if std is None else std
+    seed = args.seed if seed is None else seed
+    B = args.block
+    lo, hi = shard(n_sid, dist.rank, dist.world)
     m = hi - lo
     pitch = N.lib().snpmi_packed_pitch(n)
     ld = (n + 15) // 16 * 16
     packed = Dev(N, pitch * max(m, 1))
-    synth(N, packed.p, pitch, n, lo, m, args.seed, 0.01)
+    synth(N, packed.p, pitch, n, lo, m, seed, miss)
     nblk = (m + B - 1) // B
     lut, stats = Dev(N, B * 16), Dev(N, B * 8)
     tight = ld
     out = None
-    if args.out_ld > ld and B * ld * 4 >= (1 << 30):  # only blocks of >= 1 GB gain from it
+    if args.out_ld > ld and B * ld * 4 >= WIDE_MIN_BYTES:
         try:
             out = Dev(N, B * (args.out_ld // 16 * 16) * 4)
             ld = args.out_ld // 16 * 16
@@ -336,14 +308,14 @@ def leg_standardize(N, args, dist):
             out = None
     if out is None:
         out = Dev(N, B * ld * 4)
-    ev = Events(N, 2 + 2 * nblk)
+    ev = Events(N, 2 + 2 * max(nblk, args.tight_reps))
     N.call("snpmi_set_kernel_variant", b"decode", args.decode_variant)
 
-    def run_block(src, cnt, timed, k):
-        N.call("snpmi_dev_snp_stats", src, pitch, n, cnt, 0, N.STD_UNIT, 0.0, 0.0, 0, N.DT_F32, stats.p, lut.p)
+    def run_block(src, cnt, timed, k, dst=None, dld=None):
+        N.call("snpmi_dev_snp_stats", src, pitch, n, cnt, 0, std, a, b, 0, N.DT_F32, stats.p, lut.p)
         if timed:
             ev.record(2 + 2 * k)
-        N.call("snpmi_dev_decode", src, pitch, n, cnt, lut.p, N.DT_F32, 0, out.p, ld)
+        N.call("snpmi_dev_decode", src, pitch, n, cnt, lut.p, N.DT_F32, 0, (dst or out).p, dld or ld)
         if timed:
             ev.record(3 + 2 * k)
 
@@ -371,7 +343,7 @@ def leg_standardize(N, args, dist):
     wall = dist.max(time.perf_counter() - t0)
     weak_wall = None
     if dist.world > 1:
-        # weak figure: every rank streams 1M SNPs per step (its shard `world` times)
+        # weak figure: every rank streams the whole n_sid per step (its shard `world` times)
         dist.barrier()
         t1 = time.perf_counter()
         for _ in range(args.steps * dist.world):
@@ -381,11 +353,23 @@ def leg_standardize(N, args, dist):
         weak_wall = dist.max(time.perf_counter() - t1)
     launches = args.steps * nblk
     dec_mean_ms = dec_ms_total / max(launches, 1)
-    # achieved = bytes of one full block / mean launch time (the last block of a shard is partial:
-    # count bytes over all launches instead)
+    # achieved = bytes of all launches / their summed time (the last block of a shard is partial)
     bytes_per_step = m * ((n + 3) // 4 + 4 * n)
     achieved_gbs = bytes_per_step * args.steps / (dec_ms_total * 1e-3) / 1e9 if dec_ms_total else 0.0
-    # measured stream ceilings (untimed): device-to-device copy and write-only fill of the block buffer
+    # the same kernel into a tight-column buffer (what Bed.read(xp='hbm') writes), full blocks only
+    tight_gbs, tight_ms = achieved_gbs, dec_mean_ms
+    full = [k for k in range(nblk) if (k + 1) * B <= m][:args.tight_reps]
+    if ld != tight and full:
+        out.free()
+        out = Dev(N, B * tight * 4)
+        for k in full[:2]:
+            run_block(packed.at(k * B * pitch), B, False, k, out, tight)
+        for i, k in enumerate(full):
+            run_block(packed.at(k * B * pitch), B, True, i, out, tight)
+        N.call("snpmi_stream_sync")
+        tight_ms = float(np.mean([ev.ms(2 + 2 * i, 3 + 2 * i) for i in range(len(full))]))
+        tight_gbs = B * ((n + 3) // 4 + 4 * n) / (tight_ms * 1e-3) / 1e9
+    # measured stream ceilings (untimed): device-to-device copy and write-only fill, tight bytes
     cbytes = min(B * tight * 4, pitch * m)
     N.call("snpmi_dev_memcpy_d2d", out.p, packed.p, cbytes)
     N.call("snpmi_stream_sync")
@@ -401,22 +385,24 @@ def leg_standardize(N, args, dist):
     ev.record(1)
     N.call("snpmi_stream_sync")
     fill_gbs = 5 * B * tight * 4 / (ev.ms(0, 1) * 1e-3) / 1e9
+    cur_ld = tight if ld != tight and full else ld
     sample = gpu_cols = None
     if dist.rank == 0 and not args.skip_cpu:
         # parity sample: the first 512 columns, re-decoded by the same kernels (untimed)
         ncols = min(512, m)
         sample = np.empty((ncols, pitch), dtype=np.uint8)
         N.call("snpmi_memcpy_d2h", N.ptr(sample), packed.p, sample.nbytes)
-        run_block(packed.p, ncols, False, 0)
+        run_block(packed.p, ncols, False, 0, out, cur_ld)
         gpu_cols = np.empty((ncols, tight), dtype=np.float32)
-        if ld == tight:
+        if cur_ld == tight:
             N.call("snpmi_memcpy_d2h", N.ptr(gpu_cols), out.p, gpu_cols.nbytes)
         else:
             for j in range(ncols):
-                N.call("snpmi_memcpy_d2h", N.ptr(gpu_cols[j]), out.at(j * ld * 4), tight * 4)
+                N.call("snpmi_memcpy_d2h", N.ptr(gpu_cols[j]), out.at(j * cur_ld * 4), tight * 4)
     res = dict(wall=wall, weak_wall=weak_wall, dec_mean_ms=dec_mean_ms, achieved_gbs=achieved_gbs,
+               tight_gbs=tight_gbs, tight_ms=tight_ms, tight_launches=len(full) if ld != tight else launches,
                copy_gbs=copy_gbs, fill_gbs=fill_gbs, full_block_bytes=B * ((n + 3) // 4 + 4 * n), launches=launches,
-               nblk=nblk, pitch=pitch, sample=sample, gpu_cols=gpu_cols, m=m, out_ld=ld)
+               nblk=nblk, pitch=pitch, sample=sample, gpu_cols=gpu_cols, m=m, out_ld=ld, n=n, n_sid=n_sid)
     ev.destroy()
     for d in (packed, lut, stats, out):
         d.free()
@@ -548,24 +534,25 @@ def leg_e2e(N, args):
             "parity": {"check": "last chunk == decode of the same columns resident in HBM", "bit_exact": same}}
 
 
-def cpu_baseline_standardize(args, sample, timed=True):
-    """Oracle C/OpenMP decode + one-pass Unit standardize on a bounded sample (rank 0), at the
-    box's CPU share and at 1 thread; with timed=False (N > 1) one untimed pass for parity."""
+def cpu_baseline_standardize(args, sample, timed=True, n=None, is_beta=False, a=np.nan, b=np.nan):
+    """Oracle C/OpenMP decode + one-pass standardize on a bounded sample (rank 0), at the largest
+    usable thread count and at 1 thread; with timed=False (N > 1) one untimed pass for parity."""
     from oracle import oracle as O
 
-    n = args.n_iid
-    threads = cpu_threads()
+    n = args.n_iid if n is None else n
+    counts = cpu_counts()
+    threads = counts["usable"]
     bpc = (n + 3) // 4
     body = np.ascontiguousarray(sample[:, :bpc]).reshape(-1)
     ncols = sample.shape[0]
-    ref, _ = O.decode_standardize(body, n, ncols, dtype=np.float32, num_threads=threads)
+    ref, _ = O.decode_standardize(body, n, ncols, is_beta=is_beta, a=a, b=b, dtype=np.float32, num_threads=threads)
     if not timed:
         return ref, None
 
     def rate(th, budget, max_reps):
         done, t0 = 0, time.perf_counter()
         while True:
-            O.decode_standardize(body, n, ncols, dtype=np.float32, num_threads=th)
+            O.decode_standardize(body, n, ncols, is_beta=is_beta, a=a, b=b, dtype=np.float32, num_threads=th)
             done += ncols
             el = time.perf_counter() - t0
             if el >= budget or done >= max_reps * ncols:
@@ -574,97 +561,101 @@ def cpu_baseline_standardize(args, sample, timed=True):
     v_all, reps_all, el_all = rate(threads, args.cpu_seconds, 64)
     v_one, reps_one, el_one = rate(1, args.cpu_seconds / 2, 4)
     return ref, {"value": v_all, "unit": "SNPs/s", "cores": threads, "kind": "port",
-                 "single_thread_value": v_one,
+                 "single_thread_value": v_one, "cpu_counts": counts,
                  "sample": "%d reps x %d SNP columns x %d iids (first packed columns of the same synthetic matrix), "
-                           "f32 Unit, oracle/bed_oracle.c oracle_decode_standardize_f32 at %d threads (the box's CPU "
-                           "share; os.cpu_count() = %d is the whole machine), %.1f s; 1 thread: %d reps, %.1f s"
-                           % (reps_all, ncols, n, threads, os.cpu_count() or 0, el_all, reps_one, el_one)}
+                           "f32 %s, oracle/bed_oracle.c oracle_decode_standardize_f32 at %d threads (%s), %.1f s; "
+                           "1 thread: %d reps, %.1f s"
+                           % (reps_all, ncols, n, "Beta(%g,%g)" % (a, b) if is_beta else "Unit", threads,
+                              _counts_text(counts), el_all, reps_one, el_one)}
 
 
 # ---------------------------------------------------------------------------- leg 2: GRM (cfg4)
-def leg_grm(N, args, dist, dtype):
-    from pysnptools_amd.shard import rank_span_blocks, snp_blocks
+def leg_grm(N, args, dist, dtype, keep_tiles=False):
+    """cfg4 through pysnptools_amd.shard.ShardedGrm: this rank's contiguous SNP span (packed codes
+    generated in HBM by global SNP id, so the shards of any world tile the same matrix) added to
+    a GRM session in one call (<= 65536 SNPs per SYRK launch), then the RCCL collective of the
+    tiles.  ``keep_tiles`` (tests): a host copy of this rank's tiles after the collective."""
+    from pysnptools_amd.shard import ShardedGrm, rank_span
 
-    n, m, B = args.grm_iid, args.grm_sid, args.grm_block
+    n, m = args.grm_iid, args.grm_sid
+    npdt = np.float32 if dtype == "f32" else np.float64
     dt, esz = (N.DT_F32, 4) if dtype == "f32" else (N.DT_F64, 8)
     pitch = N.lib().snpmi_packed_pitch(n)
-    blocks = snp_blocks(m, B)
-    mine = rank_span_blocks(m, B, dist.rank, dist.world)
-    my_m = sum(c for _, c in mine)
+    lo, hi = rank_span(m, dist.rank, dist.world)
+    my_m = hi - lo
     packed = Dev(N, max(1, my_m) * pitch)
-    off = 0
-    for s0, c in mine:  # generate exactly the global SNP ids this rank owns
-        synth(N, packed.at(off * pitch), pitch, n, s0, c, args.seed + 100, 0.01)
-        off += c
-    tile_bytes = N.lib().snpmi_grm_tile_bytes(n, dt)
-    tiles = Dev(N, tile_bytes)
-    lut, stats = Dev(N, B * 4 * esz), Dev(N, B * 2 * esz)
-    ev = Events(N, 2 + 2 * max(1, len(mine)) + 2)
+    if my_m:
+        synth(N, packed.p, pitch, n, lo, my_m, args.seed + 100, 0.01)
+    stats = Dev(N, max(1, my_m) * 2 * esz)
+    collective = args.grm_collective if dist.rccl else "none"
+    ev = Events(N, 4)
+    chunks = (my_m + 65535) // 65536 if my_m else 0
 
-    def run(timed, limit=None):
-        off = 0
-        todo = mine if limit is None else mine[:limit]
-        if not todo:
-            N.call("snpmi_dev_memset", tiles.p, 0, tile_bytes)
-        for k, (s0, c) in enumerate(todo):
-            src = packed.at(off * pitch)
-            N.call("snpmi_dev_snp_stats", src, pitch, n, c, 0, N.STD_UNIT, 0.0, 0.0, 0, dt, stats.p, lut.p)
-            if timed:
-                ev.record(2 + 2 * k)
-            N.call("snpmi_dev_syrk_packed", src, pitch, n, c, lut.p, dt, tiles.p, int(k > 0))
-            if timed:
-                ev.record(3 + 2 * k)
-            off += c
-        if dist.rccl and timed:
-            ev.record(len(ev.ev) - 2)
-            if args.grm_collective == "reduce":
-                N.call("snpmi_rccl_reduce_sum", tiles.p, tile_bytes // esz, dt, 0)
-            else:
-                N.call("snpmi_rccl_allreduce_sum", tiles.p, tile_bytes // esz, dt)
-            ev.record(len(ev.ev) - 1)
-        N.call("snpmi_stream_sync")
+    def session():
+        return ShardedGrm(n, npdt, dist if dist.rccl else None, collective, 0, dist.rank, dist.world)
 
-    run(False, limit=1)  # warm-up: one block
+    # warm-up: one 10k-SNP piece (scratch allocations, the session tiles, code objects)
+    g = session()
+    g.add_packed(packed.p, pitch, min(my_m, args.grm_block), N.STD_UNIT, 0.0, 0.0, 0, stats.p)
+    N.call("snpmi_stream_sync")
+    g.abort()
     sum_r, nlaunch = ctypes.c_uint64(), ctypes.c_uint64()
     if dtype == "f64":
         N.call("snpmi_crt_moduli_stats", ctypes.byref(sum_r), ctypes.byref(nlaunch), 1)
+    g = session()
     dist.barrier()
     t0 = time.perf_counter()
-    run(True)
+    ev.record(0)
+    g.add_packed(packed.p, pitch, my_m, N.STD_UNIT, 0.0, 0.0, 0, stats.p)
+    ev.record(1)
+    g.combine()
+    ev.record(2)
+    N.call("snpmi_stream_sync")
     dist.barrier()
     wall = dist.max(time.perf_counter() - t0)
     crt_moduli = None
     if dtype == "f64":  # moduli the timed blocks ran with (chosen per block on the device)
         N.call("snpmi_crt_moduli_stats", ctypes.byref(sum_r), ctypes.byref(nlaunch), 1)
         crt_moduli = sum_r.value / max(nlaunch.value, 1)
-    syrk_ms = [ev.ms(2 + 2 * k, 3 + 2 * k) for k in range(len(mine))]
-    allreduce_ms = ev.ms(len(ev.ev) - 2, len(ev.ev) - 1) if dist.rccl else 0.0
-    tr = ctypes.c_double()
-    N.call("snpmi_dev_grm_trace", tiles.p, n, dt, ctypes.byref(tr))
+    syrk_ms = ev.ms(0, 1) if my_m else 0.0
+    coll_ms = ev.ms(1, 2) if dist.rccl else 0.0
+    tiles, count = g.tiles()
+    trace = None
+    if g.holds_k():  # the other ranks' tiles are unspecified after an ncclReduce
+        tr = ctypes.c_double()
+        N.call("snpmi_dev_grm_trace", tiles, n, dt, ctypes.byref(tr))
+        trace = tr.value
+    host_tiles = None
+    if keep_tiles:
+        host_tiles = np.empty(count, dtype=npdt)
+        N.call("snpmi_memcpy_d2h", N.ptr(host_tiles), tiles, host_tiles.nbytes)
+    g.abort()  # K stays as tiles in HBM; the session ends without the n x n extraction
     nb = (n + 255) // 256
     exec_ratio = SPLIT_PRODUCTS * 2 * 256 * 256 * (nb * (nb + 1) // 2) / (n * (n + 1))  # executed fp16 / algorithmic
-    # allreduce_ms = the K-tile collective (ncclReduce by default, --grm-collective)
-    res = dict(wall=wall, syrk_ms=syrk_ms, allreduce_ms=allreduce_ms, trace=tr.value, exec_ratio=exec_ratio,
-               mean_tflops=(n * (n + 1) * my_m / (np.sum(syrk_ms) * 1e-3) / 1e12) if syrk_ms else 0.0,
-               nblocks=len(blocks), my_m=my_m, crt_moduli=crt_moduli)
+    res = dict(wall=wall, syrk_ms=syrk_ms, allreduce_ms=coll_ms, trace=trace, exec_ratio=exec_ratio,
+               mean_tflops=(n * (n + 1) * my_m / (syrk_ms * 1e-3) / 1e12) if syrk_ms else 0.0,
+               launches=chunks, snps_per_launch=(my_m + chunks - 1) // chunks if chunks else 0,
+               my_m=my_m, crt_moduli=crt_moduli, collective=collective, tiles=host_tiles)
     if dist.rank == 0 and not args.skip_cpu and my_m > 0:
         # parity sample (untimed): K rows 0..63 of the GRM of this rank's first 512 SNPs
         cm, rows = min(512, my_m), 64
-        N.call("snpmi_dev_snp_stats", packed.p, pitch, n, cm, 0, N.STD_UNIT, 0.0, 0.0, 0, dt, stats.p, lut.p)
-        N.call("snpmi_dev_syrk_packed", packed.p, pitch, n, cm, lut.p, dt, tiles.p, 0)
+        g = ShardedGrm(n, npdt, None, "none")
+        g.add_packed(packed.p, pitch, cm, N.STD_UNIT, 0.0, 0.0, 0, stats.p)
+        t, _ = g.tiles()
         ri = np.arange(rows, dtype=np.uint64)
         dri, dout = Dev(N, rows * 8), Dev(N, rows * n * esz)
         N.call("snpmi_memcpy_h2d", dri.p, N.ptr(ri), ri.nbytes)
-        N.call("snpmi_dev_grm_extract", tiles.p, n, dt, dri.p, rows, None, n, 1, 1.0, dout.p)
-        krows = np.empty((rows, n), dtype=np.float32 if esz == 4 else np.float64)
+        N.call("snpmi_dev_grm_extract", t, n, dt, dri.p, rows, None, n, 1, 1.0, dout.p)
+        krows = np.empty((rows, n), dtype=npdt)
         N.call("snpmi_memcpy_d2h", N.ptr(krows), dout.p, krows.nbytes)
+        g.abort()
         sample = np.empty((cm, pitch), dtype=np.uint8)
         N.call("snpmi_memcpy_d2h", N.ptr(sample), packed.p, sample.nbytes)
         res["parity_sample"] = (krows, sample, cm)
         dri.free()
         dout.free()
     ev.destroy()
-    for d in (packed, tiles, lut, stats):
+    for d in (packed, stats):
         d.free()
     return res
 
@@ -685,30 +676,43 @@ def grm_parity(args, krows, sample, cm, tol):
                      % (rows - 1, cm, n, krows.dtype), "max_abs_err_over_max_diag": err, "pass": err <= tol}
 
 
-def cpu_baseline_grm(dtype):
-    """NumPy Z.dot(Z.T) (OpenBLAS syrk, the reference's snpdata.py:203-206 / snpreader.py:655) with
-    the BLAS pool pinned to the box's CPU share; `cores` = the threads the BLAS pool reports."""
+def cpu_baseline_grm(args, dtype):
+    """The reference's GRM block step on the host (snpreader.py:651-655): NumPy Z.dot(Z.T)
+    (OpenBLAS syrk, snpdata.py:203-206) on a --cpu-grm-iid x --cpu-grm-sid slice, plus the
+    single-threaded K += of the n x n result, with the BLAS pool pinned to the usable CPU count;
+    extrapolated to configs[3]: 50 blocks of 10k SNPs = 50 x (syrk time x 10k / b + one K +=)."""
     from threadpoolctl import threadpool_info, threadpool_limits
 
-    n, b = 10_000, 2048
+    n, b = args.cpu_grm_iid, args.cpu_grm_sid
+    npdt = np.float32 if dtype == "f32" else np.float64
     rng = np.random.default_rng(0)
-    Z = rng.standard_normal((n, b)).astype(np.float32 if dtype == "f32" else np.float64)
-    want = cpu_threads()
+    Z = rng.standard_normal((n, b)).astype(npdt)
+    counts = cpu_counts()
+    want = counts["usable"]
+    K = np.zeros((n, n), dtype=npdt)  # snpreader.py:643
+    K.fill(0)  # touch the pages once: later blocks of the reference's loop add into a resident K
     with threadpool_limits(limits=want, user_api="blas"):
         used = [p.get("num_threads") for p in threadpool_info() if p.get("user_api") == "blas"]
-        Z.dot(Z.T)
+        Z[:2048].dot(Z[:2048].T)  # warm the BLAS pool
         t0 = time.perf_counter()
-        reps = 0
-        while True:
-            Z.dot(Z.T)
-            reps += 1
-            el = time.perf_counter() - t0
-            if el > 3.0 or reps >= 8:
-                break
+        Kb = Z.dot(Z.T)
+        t_syrk = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    K += Kb
+    t_add = time.perf_counter() - t0
+    del Kb, K
     cores = used[0] if used else want
-    return {"value": reps * n * (n + 1) * b / el / 1e9, "unit": "GF/s", "cores": cores, "kind": "port",
-            "sample": "%d x Z.dot(Z.T), Z = %d x %d %s (NumPy/OpenBLAS, BLAS pool pinned to %d threads), %.1f s"
-                      % (reps, n, b, dtype, cores, el)}
+    M, B = args.grm_sid, args.grm_block
+    nblocks = (M + B - 1) // B
+    per_block = t_syrk * B / b + t_add
+    total = nblocks * per_block
+    return {"value": n * (n + 1) * M / total / 1e9, "unit": "GF/s", "cores": cores,
+            "kind": "port", "cpu_counts": counts, "syrk_s": t_syrk, "k_add_s": t_add,
+            "projected_seconds": total,
+            "sample": "Z.dot(Z.T) of a %d x %d %s slice (NumPy/OpenBLAS syrk, BLAS pool pinned to %d threads; %s) "
+                      "%.2f s + one single-threaded K += of %d x %d %.2f s; projected to %d blocks of %d SNPs as "
+                      "%d x (syrk x %d/%d + K +=) = %.0f s" % (n, b, dtype, cores, _counts_text(counts), t_syrk, n, n,
+                                                               t_add, nblocks, B, nblocks, B, b, total)}
 
 
 # ---------------------------------------------------------------------------- leg 3: cfg5 partitioned GRM
@@ -875,42 +879,180 @@ def grm_entry(args, dist, r, dtype):
     n, m = args.grm_iid, args.grm_sid
     gf = n * (n + 1) * m / r["wall"] / 1e9
     f32 = dtype == "f32"
-    peak = SPLIT_PEAK_TFLOPS if f32 else MFMA_F64_PEAK_TFLOPS
-    roof = {"bound": "mfma", "achieved": r["mean_tflops"], "peak": peak, "unit": "TFLOP/s",
-            "frac": r["mean_tflops"] / peak, "per_launch_flops": n * (n + 1) * args.grm_block}
+    per_launch = {"launches_on_rank": r["launches"], "snps_per_launch": r["snps_per_launch"],
+                  "mean_launch_ms": r["syrk_ms"] / max(r["launches"], 1)}
     if f32:
-        roof.update({"traffic": pmc_traffic("f32w::k_syrk_h2", "grm", n, args.grm_block),
-                     "kernel": "f32w::k_syrk_h2<false,4>: f32 GRM as 3 fp16 MFMA products of each value's fp16x2 "
-                               "split, f32 accumulate (v_mfma_f32_32x32x16_f16); peak = 2.5 PF fp16 dense / 3; time "
-                               "per block includes k_lut_bf3, k_lut_h2 and the range-gated bf16x3 launch (exits at "
-                               "once for Unit)",
-                     "f32_mfma_peak": MFMA_F32_PEAK_TFLOPS,
-                     "mfma_util_executed": r["mean_tflops"] * r["exec_ratio"] / MFMA_BF16_PEAK_TFLOPS})
+        peak = SPLIT_PEAK_TFLOPS
+        roof = {"bound": "mfma", "achieved": r["mean_tflops"], "peak": peak, "unit": "TFLOP/s",
+                "frac": r["mean_tflops"] / peak, "per_launch_flops": n * (n + 1) * r["snps_per_launch"],
+                "traffic": pmc_traffic("f32w::k_syrk_h2", "grm", n, r["snps_per_launch"]),
+                "kernel": "f32w::k_syrk_h2<false,4>: f32 GRM as 3 fp16 MFMA products of each value's fp16x2 "
+                          "split, f32 accumulate (v_mfma_f32_32x32x16_f16); peak = 2.5 PF fp16 dense / 3; the timed "
+                          "span also holds k_snp_stats, k_lut_bf3, k_lut_h2 and the range-gated bf16x3 launch (exits "
+                          "at once for Unit) of each launch",
+                "f32_mfma_peak": MFMA_F32_PEAK_TFLOPS,
+                "mfma_util_executed": r["mean_tflops"] * r["exec_ratio"] / MFMA_BF16_PEAK_TFLOPS}
     else:
         nb = (n + 255) // 256
         R = r["crt_moduli"] or CRT_MODULI
-        ops = R * 2 * 256 * 256 * (nb * (nb + 1) // 2) * args.grm_block  # executed int8 ops per launch
-        launch_s = (np.mean(r["syrk_ms"]) * 1e-3) if r["syrk_ms"] else float("nan")
-        achieved = ops / launch_s / 1e12
+        ops = R * 2 * 256 * 256 * (nb * (nb + 1) // 2) * r["my_m"]  # executed int8 ops over the rank's span
+        achieved = ops / (r["syrk_ms"] * 1e-3) / 1e12 if r["syrk_ms"] else 0.0
         roof = {"bound": "mfma", "achieved": achieved, "peak": MFMA_I8_PEAK_TOPS, "unit": "TOP/s",
-                "frac": achieved / MFMA_I8_PEAK_TOPS, "per_launch_ops": ops, "traffic": None,
+                "frac": achieved / MFMA_I8_PEAK_TOPS,
+                "per_launch_ops": R * 2 * 256 * 256 * (nb * (nb + 1) // 2) * r["snps_per_launch"], "traffic": None,
                 "f64_equiv_tflops": r["mean_tflops"], "f64_mfma_peak": MFMA_F64_PEAK_TFLOPS,
                 "vs_f64_mfma_peak": r["mean_tflops"] / MFMA_F64_PEAK_TFLOPS,
                 "moduli_per_block": R, "moduli_max": CRT_MODULI,
                 "kernel": "k_syrk_i8r (v_mfma_i32_32x32x32_i8; grid = 256-blocks of a tile chunk x 15 moduli, those "
                           "past the block's R exit at once) + k_crt (Garner over R digits) + k_crt_exp/k_crt_lut/"
                           "k_crt_bound/k_crt_r; achieved = executed int8 ops (R moduli x full 256-blocks) / the whole "
-                          "per-block time"}
-    return {"workload": "cfg4: %d iid x %d SNP, Unit, block %d, %s SYRK, SNPs split into %d contiguous shard(s) "
-                        "streamed in blocks%s" % (n, m, args.grm_block, "f32 (fp16x2 MFMA)" if f32 else
-                                                 "f64 (int8 MFMA residues + CRT)",
-                                                 dist.world, (", RCCL %s of K tiles" % (
-                                                     "reduce onto rank 0" if args.grm_collective == "reduce"
-                                                     else "all-reduce")) if dist.rccl else ""),
+                          "timed span"}
+    roof.update(per_launch)
+    coll = {"reduce": "ncclReduce(sum, root 0)", "allreduce": "ncclAllReduce(sum)"}.get(r["collective"])
+    return {"workload": "cfg4: %d iid x %d SNP, Unit, %s SYRK; SNPs split into %d contiguous shard(s), each "
+                        "accumulated through shard.ShardedGrm in launches of <= 65536 SNPs (the reference's block_size "
+                        "%d bounds host memory, snpreader.py:651)%s"
+                        % (n, m, "f32 (fp16x2 MFMA)" if f32 else "f64 (int8 MFMA residues + CRT)", dist.world,
+                           args.grm_block, (", RCCL %s of the K tiles" % coll) if coll else ""),
             "gflops": gf, "snps_per_s": m / r["wall"], "seconds": r["wall"], "scaling": "strong",
-            "collective": ("ncclReduce(sum, root 0)" if args.grm_collective == "reduce" else "ncclAllReduce(sum)")
-            if dist.rccl else None,
-            "allreduce_ms": r["allreduce_ms"], "trace_K": r["trace"], "roofline": roof}
+            "collective": coll, "allreduce_ms": r["allreduce_ms"], "trace_K": r["trace"], "roofline": roof}
+
+
+# ---------------------------------------------------------------------------- leg 4: the reference's call path
+def write_bed(N, path, n, m, seed, miss):
+    """Synthetic .bed/.bim/.fam: packed columns generated on the GPU (SnpGen MAF curve), copied
+    back and written as the SNP-major body (untimed; the file then sits in the page cache)."""
+    pitch = N.lib().snpmi_packed_pitch(n)
+    bpc = (n + 3) // 4
+    step = max(1, min(m, (1 << 30) // pitch))
+    dev = Dev(N, pitch * step)
+    host = np.empty((step, pitch), dtype=np.uint8)
+    with open(path + ".bed", "wb") as f:
+        f.write(bytes([0x6C, 0x1B, 0x01]))
+        for s0 in range(0, m, step):
+            cnt = min(step, m - s0)
+            synth(N, dev.p, pitch, n, s0, cnt, seed, miss)
+            N.call("snpmi_memcpy_d2h", N.ptr(host), dev.p, cnt * pitch)
+            f.write(np.ascontiguousarray(host[:cnt, :bpc]).tobytes())
+    dev.free()
+    with open(path + ".fam", "w") as f:
+        f.write("".join("f%d i%d 0 0 0 0\n" % (i, i) for i in range(n)))
+    with open(path + ".bim", "w") as f:
+        f.write("".join("1\ts%d\t0\t%d\tA\tC\n" % (j, j + 1) for j in range(m)))
+
+
+def leg_file(N, args):
+    """Bed / SnpData / SnpKernel calls exactly as a PySnpTools user makes them, on a synthetic
+    args.file_iid x args.file_sid .bed in local storage (21.8% missing, SnpGen's rate), each with
+    parity against the oracle on a sample.  PCIe-inclusive; never `value`."""
+    import shutil
+
+    from oracle import oracle as O
+    from pysnptools_amd.snpreader import Bed
+    from pysnptools_amd.standardizer import Beta, Unit
+
+    n, m = args.file_iid, args.file_sid
+    tmp = tempfile.mkdtemp(prefix="snpmi_file_", dir=args.file_dir)
+    saved_xp = os.environ.get("ARRAY_MODULE")
+    out = {"workload": "synthetic %d iid x %d SNP .bed (%.2f GB packed, SnpGen MAF curve, 21.8%% missing) in local "
+                       "storage, read through the page cache" % (n, m, m * ((n + 3) // 4) / 1e9)}
+    try:
+        base = os.path.join(tmp, "cfg")
+        t0 = time.perf_counter()
+        write_bed(N, base, n, m, args.seed + 300, 0.218)
+        out["write_s"] = time.perf_counter() - t0
+        body = O.read_bed_bytes(base + ".bed")
+        bed = Bed(base + ".bed", count_A1=False)
+        bed.iid, bed.sid  # metadata outside the timed regions
+        flops = n * (n + 1) * m
+        # (1) Bed.read_kernel(Unit(), float32): K in HBM (ARRAY_MODULE=hbm), then K copied to the host
+        os.environ["ARRAY_MODULE"] = "hbm"
+        bed[:, :2000].read_kernel(Unit(), dtype=np.float32)  # warm-up: scratch + session tiles
+        t0 = time.perf_counter()
+        Kd = bed.read_kernel(Unit(), dtype=np.float32)
+        t_hbm = time.perf_counter() - t0
+        rows = 8
+        k_rows = np.empty((rows, n), dtype=np.float32)
+        for r in range(rows):
+            N.call("snpmi_memcpy_d2h", N.ptr(k_rows[r]), ctypes.c_void_p(Kd.val.ptr + r * n * 4), n * 4)
+        del Kd
+        os.environ.pop("ARRAY_MODULE")
+        t0 = time.perf_counter()
+        Kh = bed.read_kernel(Unit(), dtype=np.float32)
+        t_host = time.perf_counter() - t0
+        same_k = bool(np.array_equal(Kh.val[:rows], k_rows))
+        del Kh
+        # oracle: K rows 0..7 over every SNP, in 4096-SNP blocks (f64 one-pass Unit)
+        ref = np.zeros((rows, n))
+        for s0 in range(0, m, 4096):
+            sid = np.arange(s0, min(m, s0 + 4096), dtype=np.uint64)
+            Z, _ = O.decode_standardize(body, n, m, sid_index=sid, dtype=np.float64, num_threads=cpu_threads())
+            ref += Z[:rows].dot(Z.T)
+        err = float(np.abs(k_rows - ref).max() / np.abs(np.diag(ref[:, :rows])).max())
+        out["read_kernel_f32"] = {
+            "call": "Bed(path).read_kernel(Unit(), dtype=np.float32)", "reference": "snpreader.py:528-561,623-668",
+            "seconds_K_in_hbm": t_hbm, "tflops_K_in_hbm": flops / t_hbm / 1e12,
+            "seconds_K_to_host": t_host, "tflops_K_to_host": flops / t_host / 1e12, "K_GB": n * n * 4 / 1e9,
+            "parity": {"check": "K rows 0..%d vs oracle f64 over all %d SNPs; host K == HBM K" % (rows - 1, m),
+                       "max_abs_err_over_max_diag": err, "host_equals_hbm": same_k,
+                       "pass": err <= 1e-5 and same_k}}
+        # (2) Bed[:, :10000].read(float32, xp='hbm')
+        B = min(10_000, m)
+        sub = bed[:, :B]
+        sub.read(dtype=np.float32, xp="hbm")
+        t0 = time.perf_counter()
+        vd = sub.read(dtype=np.float32, xp="hbm")
+        t_read = time.perf_counter() - t0
+        cols = np.empty((64, n), dtype=np.float32)
+        N.call("snpmi_memcpy_d2h", N.ptr(cols), vd.val.snpmi_ptr, cols.nbytes)
+        del vd
+        refc = O.decode(body, n, m, sid_index=np.arange(64), dtype=np.float32)
+        out["read_hbm"] = {
+            "call": "Bed(path)[:, :%d].read(dtype=np.float32, xp='hbm')" % B, "reference": "bed.py:318-345",
+            "seconds": t_read, "snps_per_s": B / t_read, "values_GB": n * B * 4 / 1e9,
+            "packed_GBps": B * ((n + 3) // 4) / t_read / 1e9,
+            "parity": {"check": "first 64 columns vs oracle decode", "bit_exact":
+                       bool(np.array_equal(cols.T, refc, equal_nan=True))}}
+        # (3) the configs[2] workload: read + Beta(1,25) standardize, values in HBM
+        bed.read(dtype=np.float32, xp="hbm").standardize(Beta(1, 25))  # warm-up at full size
+        t0 = time.perf_counter()
+        sd = bed.read(dtype=np.float32, xp="hbm")
+        t_rd = time.perf_counter() - t0
+        sd.standardize(Beta(1, 25))
+        t_all = time.perf_counter() - t0
+        cols = np.empty((256, n), dtype=np.float32)
+        N.call("snpmi_memcpy_d2h", N.ptr(cols), sd.val.snpmi_ptr, cols.nbytes)
+        del sd
+        refb, _ = O.decode_standardize(body, n, m, sid_index=np.arange(256, dtype=np.uint64), is_beta=True, a=1.0,
+                                       b=25.0, dtype=np.float32)
+        rel = float(np.max(np.abs(cols.T.astype(np.float64) - refb) / np.maximum(np.abs(refb), 1e-30)))
+        out["read_standardize_beta"] = {
+            "call": "Bed(path).read(dtype=np.float32, xp='hbm').standardize(Beta(1, 25))",
+            "reference": "bed.py:318-345, beta.py:33-50, standardizer.py:176-211",
+            "seconds": t_all, "read_seconds": t_rd, "snps_per_s": m / t_all, "values_GB": n * m * 4 / 1e9,
+            "parity": {"check": "first 256 columns vs oracle one-pass Beta(1,25) (f32)", "max_rel_err": rel,
+                       "bit_exact": bool(np.array_equal(cols.T, refb)), "pass": rel <= 1e-5}}
+    finally:
+        if saved_xp is None:
+            os.environ.pop("ARRAY_MODULE", None)
+        else:
+            os.environ["ARRAY_MODULE"] = saved_xp
+        shutil.rmtree(tmp, ignore_errors=True)
+    return out
+
+
+def decode_entry(r, label):
+    """The decode leg's roofline object (k_decode_f<float>, HBM bound)."""
+    return {"bound": "hbm", "achieved": r["achieved_gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": r["achieved_gbs"] / HBM_PEAK_GBS,
+            "frac_tight": r["tight_gbs"] / HBM_PEAK_GBS, "achieved_tight": r["tight_gbs"],
+            "mean_launch_ms_tight": r["tight_ms"],
+            "tight_note": "the same kernel writing a tight-column buffer (ld = round_up(n,16), what Bed.read(xp='hbm') "
+                          "writes), %d full-block launches, same process" % r["tight_launches"],
+            "kernel": "k_decode_f<float> (after k_snp_stats%s)" % label,
+            "per_launch_bytes": r["full_block_bytes"], "mean_launch_ms": r["dec_mean_ms"],
+            "measured_stream_GBps": {"copy_16B_nt (1 read : 1 write)": r["copy_gbs"],
+                                     "hipMemset fill (write only)": r["fill_gbs"]}}
 
 
 def main(argv=None):
@@ -918,26 +1060,35 @@ def main(argv=None):
     args = parse(argv)
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(spawn_ranks(args, argv))  # before anything touches the GPU
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        raise SystemExit("bench.py: --gpus %d but WORLD_SIZE=%d (one process per GPU)" % (args.gpus, world))
     if os.environ.get("SNPMI_BENCH_DRYRUN"):
         # launcher check without a GPU (tests/test_bench_launch.py): report the rank layout and stop
-        world = int(os.environ.get("WORLD_SIZE", "1"))
-        if world != args.gpus:
-            raise SystemExit("bench.py: --gpus %d but WORLD_SIZE=%d (one process per GPU)" % (args.gpus, world))
         print(json.dumps({k: os.environ.get(k) for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR",
                                                          "MASTER_PORT", "SNPMI_RCCL_ID_FILE")}), flush=True)
         return
     from pysnptools_amd import _native as N
+    from pysnptools_amd import dist as D
 
-    dist = Dist(args.gpus, N, args.force_rccl)
+    try:
+        dist = D.init_from_env(force_rccl=args.force_rccl, timeout=args.dist_timeout)
+    except TimeoutError as e:  # a stuck RCCL init cannot be cancelled: leave at once, non-zero
+        sys.stderr.write("bench.py: %s\n" % e)
+        sys.stderr.flush()
+        os._exit(3)
 
     r1 = leg_standardize(N, args, dist)
     value = args.n_sid * args.steps / r1["wall"]
-    grm = grm64 = grm5 = dec_c = e2e = None
+    grm = grm64 = grm5 = dec_c = e2e = beta = filed = None
     if dist.rank == 0:
         dec_c = leg_decode_c(N, args)
         if args.e2e == "on":
             e2e = leg_e2e(N, args)
     dist.barrier()
+    if args.beta == "on":
+        rb = leg_standardize(N, args, dist, n=args.beta_iid, n_sid=args.beta_sid, std=N.STD_BETA, a=1.0, b=25.0,
+                             miss=0.218, seed=args.seed + 3)
     if not args.skip_grm:
         r2 = leg_grm(N, args, dist, "f32")
         grm = grm_entry(args, dist, r2, "f32")
@@ -981,6 +1132,8 @@ def main(argv=None):
             grm5["parity"] = grm5_parity(args, m5, *r3["parity_sample"])
             grm5["parity"]["gathered_block_bit_exact"] = r3["gather_exact"]
             grm5["parity"]["pass"] = grm5["parity"]["pass"] and r3["gather_exact"]
+    if dist.rank == 0 and args.file == "on":
+        filed = leg_file(N, args)
     if dist.rank == 0:
         cpu = parity = None
         if not args.skip_cpu and r1["sample"] is not None:
@@ -989,13 +1142,30 @@ def main(argv=None):
             parity = {"check": "first %d SNP columns x %d iids: GPU stats+decode vs oracle decode+one-pass "
                                "Unit (f32)" % (ref.shape[1], ref.shape[0]), "bit_exact": bool(same)}
             if grm is not None:
-                grm["cpu_baseline"] = cpu_baseline_grm("f32") if dist.world == 1 else None
+                grm["cpu_baseline"] = cpu_baseline_grm(args, "f32") if dist.world == 1 else None
                 if r2.get("parity_sample") is not None:
                     grm["parity"] = grm_parity(args, *r2["parity_sample"], tol=1e-5)
             if grm64 is not None:
-                grm64["cpu_baseline"] = cpu_baseline_grm("f64") if dist.world == 1 else None
+                grm64["cpu_baseline"] = cpu_baseline_grm(args, "f64") if dist.world == 1 else None
                 if r2d.get("parity_sample") is not None:
                     grm64["parity"] = grm_parity(args, *r2d["parity_sample"], tol=1e-10)
+        if args.beta == "on":
+            nb_, mb_ = args.beta_iid, args.beta_sid
+            beta = {"workload": "configs[2]: Beta(1,25) standardize + NaN impute of the %d iid x %d SNP matrix "
+                                "(packed resident in HBM, SnpGen MAF curve, 21.8%% missing), %d contiguous shard(s), "
+                                "block %d SNPs, f32 F-order" % (nb_, mb_, dist.world, args.block),
+                    "snps_per_s": mb_ * args.steps / rb["wall"], "seconds_per_pass": rb["wall"] / args.steps,
+                    "block_buffer_ld": rb["out_ld"], "roofline": decode_entry(rb, ", Beta(1,25) LUT")}
+            if not args.skip_cpu and rb["sample"] is not None:
+                refb, cpub = cpu_baseline_standardize(args, rb["sample"], timed=dist.world == 1, n=nb_, is_beta=True,
+                                                      a=1.0, b=25.0)
+                got = rb["gpu_cols"][:, :nb_].T.astype(np.float64)
+                rel = float(np.max(np.abs(got - refb) / np.maximum(np.abs(refb), 1e-30)))
+                beta["parity"] = {"check": "first %d SNP columns x %d iids: GPU vs oracle one-pass Beta(1,25) (f32)"
+                                           % (refb.shape[1], nb_), "max_rel_err": rel,
+                                  "bit_exact": bool(np.array_equal(rb["gpu_cols"][:, :nb_].T, refb)),
+                                  "pass": rel <= 1e-5}
+                beta["cpu_baseline"] = cpub
         n = args.n_iid
         line = {
             "metric": METRIC, "value": value, "unit": "SNPs/s", "n_gpus": dist.n_gpus, "steps": args.steps,
@@ -1003,31 +1173,27 @@ def main(argv=None):
             "scaling": "strong", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
             "config": {"workload": "decode+Unit standardize of the %d iid x %d SNP matrix (packed BED resident in "
                                    "HBM, SnpGen MAF curve, 1%% missing), SNPs split into %d contiguous shard(s), "
-                                   "block %d SNPs, f32 F-order" % (n, args.n_sid, dist.world, args.block),
+                                   "block %d SNPs, f32 F-order block buffer with a %d-float column pitch"
+                                   % (n, args.n_sid, dist.world, args.block, r1["out_ld"]),
                        "n_iid": n, "n_sid": args.n_sid, "n_sid_per_gpu": r1["m"], "block": args.block,
                        "block_buffer_ld": r1["out_ld"],
                        "parallelism": "snp-shard x%d" % dist.world},
             "weak": ({"value": args.n_sid * args.steps * dist.world / r1["weak_wall"], "unit": "SNPs/s",
                       "workload": "every rank streams 1M SNPs per step (its shard %d times)" % dist.world}
                      if r1["weak_wall"] else None),
-            "roofline": {"bound": "hbm", "achieved": r1["achieved_gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": r1["achieved_gbs"] / HBM_PEAK_GBS,
-                         "traffic": pmc_traffic("k_decode_f<float>", "dec", n, args.block),
-                         "kernel": "k_decode_f<float> (after k_snp_stats)",
-                         "per_launch_bytes": r1["full_block_bytes"],
-                         "mean_launch_ms": r1["dec_mean_ms"],
-                         "measured_stream_GBps": {"copy_16B_nt (1 read : 1 write)": r1["copy_gbs"],
-                                                  "hipMemset fill (write only)": r1["fill_gbs"]}},
+            "roofline": dict(decode_entry(r1, ""), traffic=pmc_traffic("k_decode_f<float>", "dec", n, args.block)),
             "cpu_baseline": cpu,
             "parity": parity,
             "decode_c": dec_c,
             "e2e": e2e,
+            "beta": beta,
             "grm": grm,
             "grm_f64": grm64,
             "grm5": grm5,
+            "file": filed,
         }
         print(json.dumps(line), flush=True)
-    dist.barrier()  # every rank leaves together (rank 0 ran the CPU baselines alone)
+    dist.barrier()  # every rank leaves together (rank 0 ran the CPU baselines and the file leg alone)
     dist.close()
 
 

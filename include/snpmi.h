@@ -191,7 +191,17 @@ int snpmi_grm_add_bed_f64(const char* path, uint64_t n_iid, uint64_t n_sid, int 
 /* add Z Z^T of an already standardized rows x cols block (F or C order) to the session */
 int snpmi_grm_add_dense_f32(const float* val, uint64_t rows, uint64_t cols, int order_c);
 int snpmi_grm_add_dense_f64(const double* val, uint64_t rows, uint64_t cols, int order_c);
+/* add packed SNP columns already in HBM ([n_sid][pitch] bytes, pitch = snpmi_packed_pitch(n_iid),
+ * every iid of the session) -- the per-rank shard of shard.grm_sharded / bench.py's cfg4 leg
+ * (the block loop of snpreader.py:651-655 over a device-resident BED body).  The library runs
+ * one stats + one SYRK launch per <= 65536 SNPs.  stats [n_sid][2]: host memory (synchronous) or
+ * device memory (the call only enqueues on the library stream). */
+int snpmi_grm_add_packed_f32(const uint8_t* packed, uint64_t pitch, uint64_t n_iid, uint64_t n_sid, int count_a1,
+                             int std_kind, double a, double b, int use_stats, float* stats);
+int snpmi_grm_add_packed_f64(const uint8_t* packed, uint64_t pitch, uint64_t n_iid, uint64_t n_sid, int count_a1,
+                             int std_kind, double a, double b, int use_stats, double* stats);
 int snpmi_grm_session_tiles(void** tiles, uint64_t* count);   /* device tiles + element count */
+/* K_out NULL: end the session without a result (a non-root rank after snpmi_rccl_reduce_sum) */
 int snpmi_grm_end(int diag_k_to_n, double* factor, void* K_out);
 int snpmi_diag_k_to_n_f32(float* K, uint64_t n, double* factor);
 /* SNP-side DiagKtoN (standardizer/diag_K_to_N.py:75-95): factor = rows / sum(val^2) (f64

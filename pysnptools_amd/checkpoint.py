@@ -7,10 +7,17 @@ as one GPU GRM session over SNP blocks (``snpmi_grm_begin`` / ``snpmi_grm_add_be
 the per-SNP stats so far) next to ``path``.  A later call with the same reader, standardizer,
 block size and dtype restores the tiles into a new session and continues at the next block, so
 an interrupted run resumes instead of starting over; the resumed K is bit-identical to an
-uninterrupted checkpointed run (same blocks, same accumulation order).  The files are written
-to temporaries and renamed (tiles first, then the JSON that commits them), so a crash while
-saving leaves the previous checkpoint intact.  They are removed when the GRM completes.
+uninterrupted checkpointed run (same blocks, same accumulation order).
+
+Commit protocol: each save is a new GENERATION (``path.g<next_block>.tiles.npy`` / ``.stats.npy``)
+written beside the previous one, never over it; the JSON names the generation's files and holds
+their SHA-1s, and renaming the JSON into place is the commit.  Only then is the previous
+generation deleted.  A crash at any point leaves a JSON that names a complete, hash-checked
+generation (the previous one until the JSON rename, the new one after), so no block can be
+counted twice.  ``_restore`` refuses files whose hash does not match.  Everything is removed
+when the GRM completes.
 """
+import glob
 import hashlib
 import json
 import os
@@ -37,8 +44,28 @@ def _fingerprint(bed_path, n, m, dtype, block_size, kind, a, b, use_stats, rows,
             "stats_in": None if stats_in is None else hashlib.sha1(np.ascontiguousarray(stats_in).tobytes()).hexdigest()}
 
 
-def _paths(path):
-    return path + ".json", path + ".tiles.npy", path + ".stats.npy"
+def _json_path(path):
+    return path + ".json"
+
+
+def _gen_paths(path, gen):
+    return "%s.g%d.tiles.npy" % (path, gen), "%s.g%d.stats.npy" % (path, gen)
+
+
+def _sha1_file(p):
+    h = hashlib.sha1()
+    with open(p, "rb") as f:
+        for chunk in iter(lambda: f.read(1 << 24), b""):
+            h.update(chunk)
+    return h.hexdigest()
+
+
+def _write_npy(p, arr):
+    with open(p + ".tmp", "wb") as f:
+        np.save(f, arr, allow_pickle=False)
+        f.flush()
+        os.fsync(f.fileno())
+    os.replace(p + ".tmp", p)
 
 
 def _session_tiles():
@@ -50,31 +77,53 @@ def _session_tiles():
 
 
 def _save(path, meta, next_block, stats, dtype):
-    jpath, tpath, spath = _paths(path)
+    """Write generation ``next_block`` (tiles, stats), then commit it by renaming the JSON that
+    names it and holds its hashes; then drop the previous generation."""
+    jpath = _json_path(path)
+    prev = None
+    if os.path.exists(jpath):
+        with open(jpath) as f:
+            prev = json.load(f).get("files")
     tiles, count = _session_tiles()
     host = np.empty(count, dtype=dtype)
     N.call("snpmi_stream_sync")
     N.call("snpmi_memcpy_d2h", N.ptr(host), tiles, host.nbytes)
-    for p, arr in ((tpath, host), (spath, stats)):
-        with open(p + ".tmp", "wb") as f:
-            np.save(f, arr, allow_pickle=False)
-        os.replace(p + ".tmp", p)
+    tpath, spath = _gen_paths(path, next_block)
+    _write_npy(tpath, host)
+    _write_npy(spath, np.ascontiguousarray(stats))
+    files = {"tiles": os.path.basename(tpath), "stats": os.path.basename(spath),
+             "tiles_sha1": _sha1_file(tpath), "stats_sha1": _sha1_file(spath)}
     with open(jpath + ".tmp", "w") as f:
-        json.dump(dict(meta, next_block=int(next_block)), f)
-    os.replace(jpath + ".tmp", jpath)
+        json.dump(dict(meta, next_block=int(next_block), files=files), f)
+        f.flush()
+        os.fsync(f.fileno())
+    os.replace(jpath + ".tmp", jpath)  # the commit
+    if prev:
+        for k in ("tiles", "stats"):
+            old = os.path.join(os.path.dirname(os.path.abspath(path)), prev[k])
+            if old not in (tpath, spath) and os.path.exists(old):
+                os.remove(old)
 
 
 def _restore(path, meta, dtype):
     """next block and stats of a matching checkpoint (tiles copied into the open session), or None."""
-    jpath, tpath, spath = _paths(path)
+    jpath = _json_path(path)
     if not os.path.exists(jpath):
         return None
     with open(jpath) as f:
         saved = json.load(f)
     nb = saved.pop("next_block")
+    files = saved.pop("files", None)
     if saved != meta:
         raise ValueError("checkpoint '%s' belongs to another GRM (reader, standardizer, block size or dtype "
                          "differ); remove it or choose another path" % path)
+    d = os.path.dirname(os.path.abspath(path))
+    if not files:
+        raise ValueError("checkpoint '%s' names no tile files" % path)
+    tpath, spath = os.path.join(d, files["tiles"]), os.path.join(d, files["stats"])
+    for p, key in ((tpath, "tiles_sha1"), (spath, "stats_sha1")):
+        if not os.path.exists(p) or _sha1_file(p) != files[key]:
+            raise ValueError("checkpoint '%s': %s is missing or does not match its recorded hash" % (path, p))
     host = np.load(tpath, allow_pickle=False)
     tiles, count = _session_tiles()
     if host.dtype != np.dtype(dtype) or host.size != count:
@@ -82,6 +131,12 @@ def _restore(path, meta, dtype):
     N.call("snpmi_memcpy_h2d", tiles, N.ptr(host), host.nbytes)
     N.call("snpmi_stream_sync")
     return nb, np.load(spath, allow_pickle=False)
+
+
+def _remove_all(path):
+    for p in [_json_path(path), _json_path(path) + ".tmp"] + glob.glob(glob.escape(path) + ".g*.npy*"):
+        if os.path.exists(p):
+            os.remove(p)
 
 
 def read_kernel_checkpointed(reader, standardizer, path, block_size=10000, every=10, dtype=np.float64,
@@ -144,7 +199,5 @@ def read_kernel_checkpointed(reader, standardizer, path, block_size=10000, every
     finally:
         N.call("snpmi_grm_end", 0, None, N.ptr(K))
     if done:
-        for p in _paths(path):
-            if os.path.exists(p):
-                os.remove(p)
+        _remove_all(path)
     return KernelData(iid=reader.iid, val=K), _trained_from(standardizer, kind, a, b, sid, stats)

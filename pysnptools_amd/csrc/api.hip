@@ -1050,6 +1050,48 @@ static void grm_add_dense_impl(const T* val, uint64_t rows, uint64_t cols, int o
     g_session.wrote = true;
     SNPMI_HIP(hipStreamSynchronize(d.stream));
 }
+
+// Packed SNP columns already in HBM ([m][pitch] bytes, every iid of the session) added to the
+// session: per chunk of <= 2^16 SNPs one stats launch (LUT) and one SYRK launch, so a rank's
+// whole SNP shard accumulates in registers over up to 65536 SNPs per K-tile round trip instead
+// of one per 10k block (the reference's block_size bounds host memory, snpreader.py:651).
+// stats may be host memory (copied synchronously) or device memory (the call then only enqueues).
+template <typename T>
+static void grm_add_packed_impl(const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m, int count_a1,
+                                int std_kind, double a, double b, int use_stats, T* stats) {
+    std::lock_guard<std::recursive_mutex> lk(g_call_mutex);
+    SNPMI_REQUIRE(g_session.active, SNPMI_E_ARG, "no GRM session (call snpmi_grm_begin)");
+    SNPMI_REQUIRE(g_session.dtype == DT<T>::v, SNPMI_E_ARG, "dtype differs from snpmi_grm_begin");
+    SNPMI_REQUIRE(n == g_session.n, SNPMI_E_ARG, "iid count differs from snpmi_grm_begin");
+    SNPMI_REQUIRE(pitch % 64 == 0 && pitch >= ceil_div(n, 4), SNPMI_E_ARG, "pitch must be snpmi_packed_pitch");
+    SNPMI_REQUIRE(std_kind >= SNPMI_STD_NONE && std_kind <= SNPMI_STD_BETA, SNPMI_E_ARG, "bad standardizer kind");
+    SNPMI_REQUIRE(stats != nullptr || std_kind == SNPMI_STD_NONE || m == 0, SNPMI_E_ARG, "stats is NULL");
+    if (m == 0 || n == 0) return;
+    SNPMI_REQUIRE(packed != nullptr, SNPMI_E_ARG, "packed is NULL");
+    Device& d = device();
+    SNPMI_REQUIRE(is_device_ptr(d, packed), SNPMI_E_ARG, "packed must be device memory of the current device");
+    T* tiles = (T*)session_tiles(d);
+    const bool host_stats = stats && std_kind != SNPMI_STD_NONE && !is_device_ptr(d, stats);
+    // equal chunks of <= 2^16 SNPs (the int32 / CRT accumulation cap), multiples of 256
+    const uint64_t nchunk = ceil_div(m, 1ull << 16);
+    const uint64_t step = std::min<uint64_t>(1ull << 16, round_up(ceil_div(m, nchunk), 256));
+    for (uint64_t s0 = 0; s0 < m; s0 += step) {
+        const uint64_t cnt = std::min(step, m - s0);
+        const uint8_t* src = packed + s0 * pitch;
+        T* lut = (T*)d.get(Device::S_LUT, cnt * 4 * sizeof(T));
+        T* st = (stats && !host_stats) ? stats + 2 * s0 : (T*)d.get(Device::S_STATS, cnt * 2 * sizeof(T));
+        if (host_stats && use_stats)
+            SNPMI_HIP(hipMemcpyAsync(st, stats + 2 * s0, cnt * 2 * sizeof(T), hipMemcpyHostToDevice, d.stream));
+        launch_snp_stats(src, pitch, n, cnt, count_a1, std_kind, a, b, use_stats, DT<T>::v, st, lut, d.stream);
+        syrk_packed_auto(d, src, pitch, n, cnt, lut, DT<T>::v, tiles, g_session.wrote ? 1 : 0);
+        g_session.wrote = true;
+        if (host_stats && !use_stats) {
+            SNPMI_HIP(hipMemcpyAsync(stats + 2 * s0, st, cnt * 2 * sizeof(T), hipMemcpyDeviceToHost, d.stream));
+            SNPMI_HIP(hipStreamSynchronize(d.stream));  // S_STATS is reused by the next chunk
+        }
+    }
+    if (host_stats) SNPMI_HIP(hipStreamSynchronize(d.stream));
+}
 }  // namespace snpmi
 
 // ====================================================================== exported C ABI
@@ -1227,6 +1269,15 @@ int snpmi_grm_begin(uint64_t n_out_iid, int dtype) {
 SNPMI_GRM_ADD(f32, float, SNPMI_DT_F32)
 SNPMI_GRM_ADD(f64, double, SNPMI_DT_F64)
 
+int snpmi_grm_add_packed_f32(const uint8_t* packed, uint64_t pitch, uint64_t n_iid, uint64_t n_sid, int count_a1,
+                             int std_kind, double a, double b, int use_stats, float* stats) {
+    return guarded([&] { grm_add_packed_impl<float>(packed, pitch, n_iid, n_sid, count_a1, std_kind, a, b, use_stats, stats); });
+}
+int snpmi_grm_add_packed_f64(const uint8_t* packed, uint64_t pitch, uint64_t n_iid, uint64_t n_sid, int count_a1,
+                             int std_kind, double a, double b, int use_stats, double* stats) {
+    return guarded([&] { grm_add_packed_impl<double>(packed, pitch, n_iid, n_sid, count_a1, std_kind, a, b, use_stats, stats); });
+}
+
 int snpmi_grm_add_dense_f32(const float* val, uint64_t rows, uint64_t cols, int order_c) {
     return guarded([&] { grm_add_dense_impl<float>(val, rows, cols, order_c); });
 }
@@ -1255,13 +1306,17 @@ int snpmi_grm_end(int diag_k_to_n, double* factor, void* K_out) {
     return guarded([&] {
         std::lock_guard<std::recursive_mutex> lk(g_call_mutex);
         SNPMI_REQUIRE(g_session.active, SNPMI_E_ARG, "no GRM session (call snpmi_grm_begin)");
-        SNPMI_REQUIRE(K_out != nullptr || g_session.n == 0, SNPMI_E_ARG, "K_out is NULL");
         Device& d = device();
+        g_session.active = false;
+        if (!K_out) {  // end without a result (a non-root rank after an RCCL reduce, an aborted GRM)
+            SNPMI_HIP(hipStreamSynchronize(d.stream));
+            if (factor) *factor = NAN;
+            return;
+        }
         void* t = session_tiles(d);
         if (!g_session.wrote)
             SNPMI_HIP(hipMemsetAsync(t, 0, n_tiles_upper(g_session.n) * kTile * kTile * dtype_size(g_session.dtype),
                                      d.stream));
-        g_session.active = false;
         if (g_session.dtype == SNPMI_DT_F32)
             grm_finish(d, (const float*)t, g_session.n, diag_k_to_n, factor, (float*)K_out);
         else

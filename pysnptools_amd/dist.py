@@ -1,0 +1,246 @@
+"""Process-group bootstrap for one process per GPU: the control plane of the
+SNP-sharded GRM (``shard.grm_sharded``), the DistributedBed GRM (``shard.grm_pieces``) and
+bench.py.  The reference has no multi-GPU code; its GRM loop (snpreader.py:643-668) is the
+single-process form of what the ranks split.
+
+    d = dist.init_from_env()      # RANK / WORLD_SIZE / LOCAL_RANK / LOCAL_WORLD_SIZE
+    K = Bed(path).read_kernel(Unit(), dtype=np.float32)   # SNP shards per rank + RCCL all-reduce
+    d.close()
+
+Torch-free on purpose: importing torch beside libsnpmi would load a second libamdhip64 (torch
+ships ROCm 7.0, the image 7.2).  The ncclUniqueId goes rank 0 -> other ranks through an O_EXCL
+node-local file; barriers and max-over-ranks are RCCL all-reduces.
+
+* Device: ``LOCAL_RANK`` when it is below the visible device count, else device 0 -- so a
+  launcher that narrows each rank to one GPU (per-rank ``HIP_VISIBLE_DEVICES``) works.
+* Single node: the id file is node-local, so ``WORLD_SIZE != LOCAL_WORLD_SIZE`` is refused at
+  once unless ``SNPMI_RCCL_ID_FILE`` names a path on storage every node shares.
+* Time limits: the id wait and ``ncclCommInitRank`` (which blocks until every rank joins) are
+  bounded by ``timeout`` seconds; past it ``init_from_env`` raises ``TimeoutError`` (a stuck
+  communicator init cannot be cancelled, so a caller should exit the process -- bench.py does,
+  with a non-zero status).
+"""
+import contextlib
+import ctypes
+import os
+import tempfile
+import threading
+import time
+
+_CURRENT = None
+
+
+@contextlib.contextmanager
+def stdout_to_stderr():
+    """RCCL prints a version banner on the C stdout (fd 1) around communicator setup; callers
+    whose stdout is a protocol (bench.py's one JSON line) keep it clean."""
+    import sys
+
+    sys.stdout.flush()
+    saved = os.dup(1)
+    os.dup2(2, 1)
+    try:
+        yield
+    finally:
+        os.dup2(saved, 1)
+        os.close(saved)
+
+
+def env_layout(env=None):
+    """(rank, world, local_rank, local_world) from the launcher's environment."""
+    env = os.environ if env is None else env
+    world = int(env.get("WORLD_SIZE", "1"))
+    rank = int(env.get("RANK", "0"))
+    local_rank = int(env.get("LOCAL_RANK", str(rank)))
+    local_world = int(env.get("LOCAL_WORLD_SIZE", str(world)))
+    if not (0 <= rank < world) or not (0 <= local_rank < max(local_world, 1)):
+        raise ValueError("bad rank layout: RANK=%d WORLD_SIZE=%d LOCAL_RANK=%d LOCAL_WORLD_SIZE=%d"
+                         % (rank, world, local_rank, local_world))
+    return rank, world, local_rank, local_world
+
+
+def pick_device(local_rank, n_visible):
+    """The device this rank drives: LOCAL_RANK if visible, else 0 (one GPU made visible per rank)."""
+    if n_visible < 1:
+        raise RuntimeError("no HIP device visible to this rank")
+    return local_rank if local_rank < n_visible else 0
+
+
+def id_file(env=None):
+    """Node-local path for the ncclUniqueId: SNPMI_RCCL_ID_FILE if set (bench.py's spawner sets
+    it), else derived from the launcher (parent pid + its start time + MASTER_PORT, so no stale
+    file of an earlier launcher can match)."""
+    env = os.environ if env is None else env
+    path = env.get("SNPMI_RCCL_ID_FILE")
+    if path:
+        return path
+    ppid = os.getppid()
+    try:
+        with open("/proc/%d/stat" % ppid) as f:
+            start = f.read().rsplit(")", 1)[1].split()[19]
+    except (OSError, IndexError):
+        start = "0"
+    key = "snpmi_rccl_%d_%s_%s.id" % (ppid, start, env.get("MASTER_PORT", "0"))
+    return os.path.join(tempfile.gettempdir(), key)
+
+
+def publish_id(path, uid):
+    """Rank 0: write the id atomically and never over an existing file (O_EXCL + link)."""
+    tmp = "%s.%d.tmp" % (path, os.getpid())
+    fd = os.open(tmp, os.O_WRONLY | os.O_CREAT | os.O_EXCL, 0o600)
+    with os.fdopen(fd, "wb") as f:
+        f.write(bytes(uid))
+    try:
+        os.link(tmp, path)  # fails if a file of that name exists
+    finally:
+        os.remove(tmp)
+
+
+def wait_id(path, timeout, nbytes=128, poll=0.05):
+    """Ranks > 0: the id rank 0 published, or TimeoutError after ``timeout`` seconds."""
+    t0 = time.time()
+    while True:
+        try:
+            with open(path, "rb") as f:
+                data = f.read(nbytes)
+            if len(data) == nbytes:
+                return data
+        except FileNotFoundError:
+            pass
+        if time.time() - t0 > timeout:
+            raise TimeoutError("no RCCL id from rank 0 at %s after %.0f s" % (path, timeout))
+        time.sleep(poll)
+
+
+def _run_bounded(fn, timeout, what):
+    """fn() on a helper thread (ctypes releases the GIL), TimeoutError if it has not returned."""
+    box = {}
+
+    def target():
+        try:
+            box["ok"] = fn()
+        except BaseException as e:  # re-raised on the caller's thread
+            box["err"] = e
+
+    t = threading.Thread(target=target, daemon=True)
+    t.start()
+    t.join(timeout)
+    if t.is_alive():
+        raise TimeoutError("%s did not finish within %.0f s" % (what, timeout))
+    if "err" in box:
+        raise box["err"]
+    return box.get("ok")
+
+
+class Dist(object):
+    """One rank of a single-node process group.  ``rccl`` is False at world size 1 (unless
+    forced): then barrier/max/sums are local no-ops and nothing touches RCCL."""
+
+    def __init__(self, rank, world, local_rank, device, rccl, n_gpus):
+        self.rank, self.world, self.local_rank, self.device = rank, world, local_rank, device
+        self.rccl, self.n_gpus = rccl, n_gpus
+        self._closed = False
+
+    def barrier(self):
+        if self.rccl:
+            from pysnptools_amd import _native as N
+
+            N.call("snpmi_rccl_barrier")
+
+    def max(self, x):
+        if not self.rccl:
+            return x
+        from pysnptools_amd import _native as N
+
+        v = (ctypes.c_double * 1)(float(x))
+        N.call("snpmi_rccl_host_allreduce_f64", v, 1, 1)
+        return float(v[0])
+
+    def sum_host(self, arr):
+        """Elementwise sum over ranks of a host float array (any size, through a device buffer)."""
+        import numpy as np
+
+        if not self.rccl:
+            return np.array(arr, copy=True)
+        from pysnptools_amd import _native as N
+
+        buf = np.ascontiguousarray(arr, dtype=np.float64)
+        if buf.size == 0:
+            return buf.astype(np.asarray(arr).dtype)
+        dev = ctypes.c_void_p()
+        N.call("snpmi_dev_alloc", ctypes.byref(dev), buf.nbytes)
+        try:
+            N.call("snpmi_memcpy_h2d", dev, N.ptr(buf), buf.nbytes)
+            N.call("snpmi_rccl_allreduce_sum", dev, buf.size, N.DT_F64)
+            N.call("snpmi_memcpy_d2h", N.ptr(buf), dev, buf.nbytes)
+        finally:
+            N.call("snpmi_dev_free", dev)
+        return buf.astype(np.asarray(arr).dtype)
+
+    def close(self):
+        global _CURRENT
+        if self._closed:
+            return
+        self._closed = True
+        if _CURRENT is self:
+            _CURRENT = None
+        if self.rccl:
+            from pysnptools_amd import _native as N
+
+            with stdout_to_stderr():
+                N.call("snpmi_rccl_destroy")
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+
+def init_from_env(force_rccl=False, timeout=300.0, env=None, set_current=True):
+    """Bind this process to its GPU and, at WORLD_SIZE > 1 (or ``force_rccl``), build the RCCL
+    communicator.  Returns the :class:`Dist`; it also becomes :func:`current`, which routes
+    ``read_kernel`` of a Bed through the SNP-sharded GRM while it is open."""
+    global _CURRENT
+    from pysnptools_amd import _native as N
+
+    env = os.environ if env is None else env
+    rank, world, local_rank, local_world = env_layout(env)
+    if world > 1 and local_world != world and not env.get("SNPMI_RCCL_ID_FILE"):
+        raise RuntimeError("pysnptools_amd.dist is single-node: WORLD_SIZE=%d but LOCAL_WORLD_SIZE=%d (set "
+                           "SNPMI_RCCL_ID_FILE to a path every node shares to run across nodes)" % (world, local_world))
+    device = pick_device(local_rank, N.device_count())
+    N.call("snpmi_set_device", device)
+    rccl, n_gpus = False, 1
+    if world > 1 or force_rccl:
+        path = id_file(env)
+        uid = (ctypes.c_uint8 * 128)()
+        if rank == 0:
+            with stdout_to_stderr():
+                N.call("snpmi_rccl_unique_id", uid, 128)
+            publish_id(path, uid)
+        else:
+            uid = (ctypes.c_uint8 * 128).from_buffer_copy(wait_id(path, timeout))
+        try:
+            with stdout_to_stderr():
+                _run_bounded(lambda: N.call("snpmi_rccl_init", world, rank, uid, 128), timeout,
+                             "ncclCommInitRank (rank %d of %d)" % (rank, world))
+        finally:
+            if rank == 0:
+                # every rank has read the id once the communicator exists (or we give up)
+                with contextlib.suppress(OSError):
+                    os.remove(path)
+        rccl = True
+        cnt = ctypes.c_int()
+        N.call("snpmi_rccl_comm_count", ctypes.byref(cnt))
+        n_gpus = cnt.value
+    d = Dist(rank, world, local_rank, device, rccl, n_gpus)
+    d.barrier()
+    if set_current:
+        _CURRENT = d
+    return d
+
+
+def current():
+    """The open process group of this process, or None."""
+    return _CURRENT

@@ -311,6 +311,17 @@ def _native_grm(reader, standardizer, dtype, num_threads, diag_k_to_n):
     fptr = factor.ctypes.data_as(N.ctypes.POINTER(N.ctypes.c_double))
     sfx = N.suffix(dtype)
     merged = _bed_pieces(base)
+    from pysnptools_amd import dist as dist_mod
+
+    group = dist_mod.current()
+    if group is not None and group.world > 1 and (merged is not None or isinstance(base, Bed)):
+        # one process per GPU (pysnptools_amd.dist.init_from_env): every rank calls read_kernel,
+        # streams its SNP shard / pieces, and the RCCL all-reduce gives every rank the same K
+        from pysnptools_amd import shard
+
+        run = shard.grm_pieces if merged is not None else shard.grm_sharded
+        return run(reader, standardizer, dtype=dtype, collective="allreduce", diag_k_to_n=diag_k_to_n, out=K,
+                   num_threads=num_threads, dist=group)
     if merged is not None:
         _grm_pieces(merged, rows, cols, n, kind, a, b, use_stats, stats, diag_k_to_n, fptr, K, dtype, num_threads)
     elif isinstance(base, Bed):

@@ -1,8 +1,9 @@
 """bench.py's multi-GPU plans on one GPU (no RCCL): each leg is run as every rank of a world of
 2 / 3 / 8 in turn (a stand-in for the Dist control plane without collectives), and the per-rank
 results must add up to the single-rank run -- the SNP shards of the decode leg cover the matrix
-once, and the traces of the per-rank partial GRMs sum to the trace of the whole GRM (what the
-RCCL all-reduce would produce).  Small shapes; the kernels are the real ones."""
+once, and the per-rank partial K tiles summed ELEMENTWISE equal the single-rank tiles (what the
+RCCL reduce would produce; a tile-placement or shard-offset bug that kept the trace would fail).
+Small shapes; the kernels are the real ones."""
 import os
 import sys
 
@@ -21,6 +22,7 @@ pytestmark = pytest.mark.gpu
 class FakeDist:
     def __init__(self, rank, world):
         self.rank, self.world, self.rccl, self.n_gpus = rank, world, False, 1
+        self.local_rank, self.device = rank, 0
 
     def barrier(self):
         pass
@@ -48,18 +50,54 @@ def test_decode_leg_shards_cover_the_matrix(world):
     assert all(a[1] == b[0] for a, b in zip(seen, seen[1:]))
 
 
+def _tiles_to_k(tiles, n):
+    """Full symmetric n x n K (f64) from the upper-triangle 128x128 tile buffer."""
+    nt = (n + 127) // 128
+    K = np.zeros((nt * 128, nt * 128))
+    t = tiles.reshape(-1, 128, 128)
+    for tj in range(nt):
+        for ti in range(tj + 1):
+            blk = t[tj * (tj + 1) // 2 + ti]
+            K[ti * 128:(ti + 1) * 128, tj * 128:(tj + 1) * 128] = blk
+            K[tj * 128:(tj + 1) * 128, ti * 128:(ti + 1) * 128] = blk.T
+    return K[:n, :n]
+
+
+_WHOLE = {}
+
+
 @pytest.mark.parametrize("dtype", ["f32", "f64"])
 @pytest.mark.parametrize("world", [2, 3, 8])
-def test_grm_leg_partial_traces_sum_to_whole(world, dtype):
+def test_grm_leg_partial_tiles_sum_to_whole(world, dtype):
+    """Every rank's tiles (its contiguous SNP span through shard.ShardedGrm) summed elementwise ==
+    the single-rank tiles, and the single-rank K == the oracle's on a SNP sample (parity leg)."""
     args = _args()
-    whole = bench.leg_grm(N, args, FakeDist(0, 1), dtype)
-    parts = [bench.leg_grm(N, args, FakeDist(r, world), dtype) for r in range(world)]
+    if dtype not in _WHOLE:
+        _WHOLE[dtype] = bench.leg_grm(N, args, FakeDist(0, 1), dtype, keep_tiles=True)
+    whole = _WHOLE[dtype]
+    parts = [bench.leg_grm(N, args, FakeDist(r, world), dtype, keep_tiles=True) for r in range(world)]
     assert sum(p["my_m"] for p in parts) == args.grm_sid
+    assert [p["collective"] for p in parts] == ["none"] * world
+    n = args.grm_iid
+    Kw = _tiles_to_k(whole["tiles"].astype(np.float64), n)
+    Ks = sum(_tiles_to_k(p["tiles"].astype(np.float64), n) for p in parts)
+    scale = np.abs(np.diag(Kw)).max()
     tol = 2e-6 if dtype == "f32" else 1e-12
-    total = sum(p["trace"] for p in parts)
-    assert abs(total - whole["trace"]) <= tol * abs(whole["trace"]), (total, whole["trace"])
+    err = np.abs(Ks - Kw).max() / scale
+    assert err <= tol, err
+    # the sum is not dominated by one rank: every rank contributed a non-trivial partial K
+    assert all(np.abs(np.diag(_tiles_to_k(p["tiles"].astype(np.float64), n))).max() > 0.01 * scale for p in parts)
     # trace(K) of Unit-standardized SNPs = the observed entries of the polymorphic SNPs <= N * M
-    assert 0 < whole["trace"] <= args.grm_iid * args.grm_sid * (1 + 1e-5)
+    assert 0 < whole["trace"] <= n * args.grm_sid * (1 + 1e-5)
+    assert abs(np.trace(Kw) - whole["trace"]) <= 1e-6 * whole["trace"]
+
+
+@pytest.mark.parametrize("dtype", ["f32", "f64"])
+def test_grm_leg_parity_vs_oracle(dtype):
+    args = bench.parse(["--grm-iid", "5000", "--grm-sid", "3000", "--steps", "1", "--warmup", "0"])
+    r = bench.leg_grm(N, args, FakeDist(0, 1), dtype)
+    p = bench.grm_parity(args, *r["parity_sample"], tol=1e-5 if dtype == "f32" else 1e-10)
+    assert p["pass"], p
 
 
 @pytest.mark.parametrize("collective", ["reduce", "allreduce"])
@@ -75,13 +113,20 @@ def test_bench_with_rccl_communicator_world1(collective):
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--force-rccl", "--steps", "1", "--warmup", "0",
            "--n-iid", "4099", "--n-sid", "6000", "--grm-iid", "5000", "--grm-sid", "12000", "--grm-block", "5000",
            "--grm5-iid", "20000", "--grm5-sid", "2048", "--e2e-sid", "4096", "--e2e-passes", "1",
-           "--cpu-seconds", "0.2", "--grm-collective", collective]
-    out = subprocess.run(cmd, capture_output=True, text=True, timeout=110)
+           "--cpu-seconds", "0.2", "--grm-collective", collective, "--beta-iid", "5001", "--beta-sid", "6000",
+           "--file-iid", "3001", "--file-sid", "5000", "--cpu-grm-iid", "3000", "--cpu-grm-sid", "64"]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=280)
     assert out.returncode == 0, out.stderr[-3000:]
     lines = [ln for ln in out.stdout.splitlines() if ln.strip()]
     assert len(lines) == 1, out.stdout  # stdout carries the JSON line only (RCCL banners go to stderr)
     d = json.loads(lines[0])
     assert d["n_gpus"] == 1 and d["value"] > 0 and d["parity"]["bit_exact"]
+    assert 0 < d["roofline"]["frac_tight"] and d["cpu_baseline"]["cpu_counts"]["usable"] >= 1
+    assert d["beta"]["parity"]["pass"] and d["beta"]["snps_per_s"] > 0, d["beta"]
+    f = d["file"]
+    assert f["read_kernel_f32"]["parity"]["pass"], f["read_kernel_f32"]["parity"]
+    assert f["read_hbm"]["parity"]["bit_exact"] and f["read_standardize_beta"]["parity"]["pass"], f
+    assert d["grm"]["cpu_baseline"]["projected_seconds"] > 0
     for k in ("grm", "grm_f64"):
         assert d[k]["parity"]["pass"], d[k]["parity"]
         assert d[k]["allreduce_ms"] > 0

@@ -41,7 +41,7 @@ def test_interrupted_grm_resumes_bit_identical(tmp_path, dtype, tol, std):
     assert np.array_equal(tr.stats, tr_full.stats)
     scale = np.abs(np.diag(ref)).max()
     assert np.abs(resumed.val.astype(np.float64) - ref).max() <= tol * scale
-    assert not os.path.exists(ck + ".json") and not os.path.exists(ck + ".tiles.npy")
+    assert not os.path.exists(ck + ".json") and not [p for p in os.listdir(tmp_path) if p.startswith("b.g")]
 
 
 def test_checkpoint_of_another_grm_is_refused(tmp_path):
@@ -51,3 +51,39 @@ def test_checkpoint_of_another_grm_is_refused(tmp_path):
         C.read_kernel_checkpointed(bed, Unit(), ck, block_size=200, every=1, _stop_after=2)
     with pytest.raises(ValueError, match="another GRM"):
         C.read_kernel_checkpointed(bed, Unit(), ck, block_size=300, every=1)
+
+
+def test_crash_before_the_commit_resumes_from_the_previous_generation(tmp_path, monkeypatch):
+    """The save after block 4 writes its tiles and stats, then dies before the JSON rename (the
+    commit): the resumed run must start from the previous committed generation (block 2) and give
+    the uninterrupted K -- never blocks 2..3 twice -- and a corrupted generation is refused."""
+    bed = _bed(tmp_path, n=700, m=4200)
+    full, tr_full = C.read_kernel_checkpointed(bed, Unit(), str(tmp_path / "a"), block_size=700, every=2)
+    ck = str(tmp_path / "b")
+    real_replace = os.replace
+
+    def failing_replace(src, dst):
+        if dst == ck + ".json" and os.path.exists(ck + ".g4.stats.npy"):
+            raise OSError("simulated crash before the commit")
+        return real_replace(src, dst)
+
+    monkeypatch.setattr(C.os, "replace", failing_replace)
+    with pytest.raises(OSError, match="simulated crash"):
+        C.read_kernel_checkpointed(bed, Unit(), ck, block_size=700, every=2)
+    monkeypatch.setattr(C.os, "replace", real_replace)
+    with open(ck + ".json") as f:
+        saved = json.load(f)
+    assert saved["next_block"] == 2 and saved["files"]["tiles"] == "b.g2.tiles.npy"
+    assert os.path.exists(ck + ".g4.tiles.npy")  # the uncommitted generation is ignored, not used
+    resumed, tr = C.read_kernel_checkpointed(bed, Unit(), ck, block_size=700, every=2)
+    assert np.array_equal(resumed.val, full.val)
+    assert np.array_equal(tr.stats, tr_full.stats)
+    assert not [p for p in os.listdir(tmp_path) if p.startswith("b.")]  # everything removed on completion
+    # a committed generation whose file was damaged is refused, not silently used
+    with pytest.raises(C._Interrupted):
+        C.read_kernel_checkpointed(bed, Unit(), ck, block_size=700, every=2, _stop_after=3)
+    with open(ck + ".g2.tiles.npy", "r+b") as f:
+        f.seek(-8, 2)
+        f.write(b"\x00" * 8)
+    with pytest.raises(ValueError, match="hash"):
+        C.read_kernel_checkpointed(bed, Unit(), ck, block_size=700, every=2)
