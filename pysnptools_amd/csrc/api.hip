@@ -669,8 +669,27 @@ static const uint32_t* lut_bf3(Device& d, const float* lut, uint64_t m, H2Lut* h
 
 // f64 GRM of packed SNPs: default = the int8 MFMA residue path (syrk_crt.hip; variant 70 forces
 // it), 71 = the f64 MFMA two-phase path (decode to a dense f64 block, then k_syrk_glds).
+static int g_f64_mfma = 0;  // public switch "f64" (pysnptools_amd.set_grm_f64): 1 = every f64 GRM on the f64 MFMA
 static bool use_crt(int dt) {
-    return dt == SNPMI_DT_F64 && (g_variant_syrk == 0 || (g_variant_syrk >= 70 && g_variant_syrk != 71 && g_variant_syrk <= 79));
+    return dt == SNPMI_DT_F64 && !g_f64_mfma &&
+           (g_variant_syrk == 0 || (g_variant_syrk >= 70 && g_variant_syrk != 71 && g_variant_syrk <= 79));
+}
+
+// f32 segment scratch pool of the current device (syrk.hip SegFlush): kSegSlots slots of 256 KiB
+// + their flags, zeroed once when the pool is first allocated (slots are released by the kernels)
+SegCtx seg_ctx() {
+    SegCtx c;
+    c.snps = g_seg_snps > 0 ? (uint32_t)g_seg_snps : 0u;
+    if (!c.snps) return c;
+    Device& d = device();
+    const bool fresh = d.cap[Device::S_SEG] == 0;
+    const uint64_t bytes = (uint64_t)kSegSlots * kSegSlotFloats * sizeof(float) + kSegSlots * sizeof(uint32_t);
+    uint8_t* base = (uint8_t*)d.get(Device::S_SEG, bytes);
+    c.nslots = kSegSlots;
+    c.scratch = (float*)base;
+    c.flags = (uint32_t*)(base + (uint64_t)kSegSlots * kSegSlotFloats * sizeof(float));
+    if (fresh) SNPMI_HIP(hipMemsetAsync(c.flags, 0, kSegSlots * sizeof(uint32_t), d.stream));
+    return c;
 }
 
 // per-device record of the CRT path's moduli counts: [0] = sum of R, [1] = launches
@@ -1171,6 +1190,11 @@ int snpmi_set_kernel_variant(const char* kernel, int variant) {
         else if (std::strcmp(kernel, "syrk_split") == 0) g_variant_syrk_split = variant;
         else if (std::strcmp(kernel, "dense_chunk") == 0) g_dense_chunk = std::max(variant, 0);
         else if (std::strcmp(kernel, "dense_codes") == 0) g_dense_codes = variant;
+        else if (std::strcmp(kernel, "seg") == 0) g_seg_snps = std::max(variant, 0);
+        else if (std::strcmp(kernel, "f64") == 0) {
+            SNPMI_REQUIRE(variant == 0 || variant == 1, SNPMI_E_ARG, "f64 GRM path: 0 = int8 residues + CRT, 1 = f64 MFMA");
+            g_f64_mfma = variant;
+        }
         else throw Error(SNPMI_E_ARG, std::string("unknown kernel ") + kernel);
     });
 }

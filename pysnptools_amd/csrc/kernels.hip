@@ -67,7 +67,7 @@ __device__ __forceinline__ double wave_sum_f64(double v) {
 // W waves per SNP column, 4/W SNPs per 256-thread block; 16-byte loads (64 iids per
 // lane-load), 4 in flight per lane.  W = 1 for short columns; W = 4 for long ones,
 // where one wave per SNP left 2 waves per SIMD streaming 125 KB columns (latency-bound).
-template <typename T, int W>
+template <typename T, int W, int U = 8>
 __global__ __launch_bounds__(kBlock) void k_snp_stats(const uint8_t* __restrict__ packed, uint64_t pitch,
                                                       uint64_t n, uint64_t m, int count_a1, int std_kind,
                                                       double a, double b, int use_stats, T* __restrict__ stats,
@@ -94,34 +94,45 @@ __global__ __launch_bounds__(kBlock) void k_snp_stats(const uint8_t* __restrict_
         uint32_t c1 = 0, c2 = 0, c3 = 0;
         if (valid) {
             const uint4* col = reinterpret_cast<const uint4*>(packed + s * pitch);
-            const uint64_t nq = (n + 63) / 64;
-            auto count16 = [&](const uint4& v, uint64_t q) {
+            // per 32-bit word (16 codes; bit 0 of a code = lo, bit 1 = hi): lo-count, hi-count
+            // and both-count (code 3); code 1 (missing) = lo - both, code 2 = hi - both.  7 VALU
+            // per word (the kernel was VALU-co-bound at 13 with a per-word tail test)
+            uint32_t clo = 0, chi = 0;
+            auto count_word = [&](uint32_t x) {
+                clo += __popc(x & 0x55555555u);
+                chi += __popc(x & 0xAAAAAAAAu);
+                c3 += __popc(x & (x >> 1) & 0x55555555u);
+            };
+            auto count16 = [&](const uint4& v) {
+                count_word(v.x);
+                count_word(v.y);
+                count_word(v.z);
+                count_word(v.w);
+            };
+            const uint64_t nfull = n / 64;  // 16-B items of 64 iids, all inside the column
+            constexpr uint64_t step = (uint64_t)W * kWave;
+            uint64_t q = (uint64_t)sub * kWave + lane;
+            for (; q + (U - 1) * step < nfull; q += U * step) {  // U independent 16-B loads in flight
+                uint4 v[U];
+#pragma unroll
+                for (int u = 0; u < U; u++) v[u] = col[q + u * step];
+#pragma unroll
+                for (int u = 0; u < U; u++) count16(v[u]);
+            }
+            for (; q < nfull; q += step) count16(col[q]);
+            if (q == nfull && n % 64) {  // the column's last, partial item: codes of iids >= n masked off
+                const uint4 v = col[q];
                 const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
                 for (int k = 0; k < 4; k++) {
-                    uint32_t lo = w4[k] & 0x55555555u, hi = (w4[k] >> 1) & 0x55555555u;
                     const uint64_t ib = q * 64 + 16 * k;
-                    if (ib + 16 > n) {
-                        const uint64_t valid_i = n > ib ? n - ib : 0;
-                        const uint32_t mk = ((1u << (2 * valid_i)) - 1u) & 0x55555555u;  // valid_i < 16 here
-                        lo &= mk;
-                        hi &= mk;
-                    }
-                    c3 += __popc(lo & hi);
-                    c2 += __popc(hi & ~lo);
-                    c1 += __popc(lo & ~hi);
+                    const uint64_t valid_i = n > ib ? min<uint64_t>(n - ib, 16) : 0;
+                    const uint32_t mk = valid_i >= 16 ? 0xffffffffu : ((1u << (2 * valid_i)) - 1u);
+                    count_word(w4[k] & mk);
                 }
-            };
-            constexpr uint64_t step = (uint64_t)W * kWave;
-            uint64_t q = (uint64_t)sub * kWave + lane;
-            for (; q + 3 * step < nq; q += 4 * step) {  // 4 independent loads in flight
-                const uint4 v0 = col[q], v1 = col[q + step], v2 = col[q + 2 * step], v3 = col[q + 3 * step];
-                count16(v0, q);
-                count16(v1, q + step);
-                count16(v2, q + 2 * step);
-                count16(v3, q + 3 * step);
             }
-            for (; q < nq; q += step) count16(col[q], q);
+            c1 = clo - c3;
+            c2 = chi - c3;
         }
         c1 = wave_sum_u32(c1);
         c2 = wave_sum_u32(c2);
@@ -1405,8 +1416,16 @@ void launch_snp_stats(const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_
 #define SNPMI_STATS(T, W, kind)                                                                                    \
     k_snp_stats<T, W><<<(unsigned)ceil_div(m, kBlock / kWave / W), kBlock, 0, st>>>(                               \
         packed, pitch, n, m, count_a1, kind, a, b, dtype == SNPMI_DT_I8 ? 0 : use_stats, (T*)stats, (T*)lut)
+#define SNPMI_STATS_U(T, W, U, kind)                                                                               \
+    k_snp_stats<T, W, U><<<(unsigned)ceil_div(m, kBlock / kWave / W), kBlock, 0, st>>>(                            \
+        packed, pitch, n, m, count_a1, kind, a, b, dtype == SNPMI_DT_I8 ? 0 : use_stats, (T*)stats, (T*)lut)
     if (dtype == SNPMI_DT_F32) {
-        if (wide) SNPMI_STATS(float, 4, std_kind);
+        // A/B of the load depth (decode variants 7 / 9: 4 / 16 loads in flight per lane) and of
+        // 2 waves per SNP (variant 8)
+        if (wide && g_variant_decode == 7) SNPMI_STATS_U(float, 4, 4, std_kind);
+        else if (wide && g_variant_decode == 9) SNPMI_STATS_U(float, 4, 16, std_kind);
+        else if (wide && g_variant_decode == 8) SNPMI_STATS(float, 2, std_kind);
+        else if (wide) SNPMI_STATS(float, 4, std_kind);
         else SNPMI_STATS(float, 1, std_kind);
     } else if (dtype == SNPMI_DT_F64) {
         if (wide) SNPMI_STATS(double, 4, std_kind);
@@ -1415,6 +1434,7 @@ void launch_snp_stats(const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_
         SNPMI_STATS(int8_t, 1, SNPMI_STD_NONE);
     }
 #undef SNPMI_STATS
+#undef SNPMI_STATS_U
     SNPMI_LAUNCH_CHECK();
 }
 

@@ -68,7 +68,7 @@ struct Device {
     // grow-only scratch slots
     enum Slot { S_PACKED, S_PACKED2, S_IDX, S_IDX2, S_LUT, S_STATS, S_OUT, S_TILES, S_K, S_DENSE,
                 S_DENSE2, S_RED, S_SESSION, S_PACKED_B, S_ZBLK, S_IDX32, S_LUT3, S_H2, S_OUT_B, S_STATS_B,
-                S_WIN, S_DPACK, S_DLUT, S_CRTREC, S_NUM };
+                S_WIN, S_DPACK, S_DLUT, S_CRTREC, S_SEG, S_NUM };
     void* buf[S_NUM] = {};
     // chunk pipeline events (slot = chunk parity), all on-device ordering, no host spin:
     hipEvent_t staged[2] = {};    // copy stream: H2D of pinned slot done (host may refill it)
@@ -96,6 +96,21 @@ void release_pinned();
 extern int g_variant_decode;
 extern int g_variant_syrk;
 extern int g_dense_chunk;
+// f32 GRM accumulation segments (syrk.hip SegFlush): every `snps` SNPs a workgroup adds its MFMA
+// accumulators into a private scratch slot (register-native layout, 256 KiB: 8 waves x 32 x 64
+// lanes x 16 B) and restarts them, so no f32 chain is longer than `snps`; the slot is taken from a
+// pool of `nslots` by atomic compare-and-swap on `flags` (0 = free) when the workgroup starts and
+// released when it ends.  snps = 0: one chain per launch.  Tuning hook "seg" (g_seg_snps).
+extern int g_seg_snps;
+struct SegCtx {
+    uint32_t snps = 0;
+    uint32_t nslots = 0;
+    uint32_t* flags = nullptr;
+    float* scratch = nullptr;
+};
+constexpr uint32_t kSegSlots = 1024;                 // > the resident workgroups of one launch (<= 256 x 2)
+constexpr uint64_t kSegSlotFloats = 8 * 32 * 64 * 4;  // per workgroup
+SegCtx seg_ctx();                                     // api.hip: the current device's pool (lazily allocated)
 void launch_snp_stats(const uint8_t* packed, uint64_t pitch, uint64_t n_iid, uint64_t n_sid, int count_a1,
                       int std_kind, double a, double b, int use_stats, int dtype, void* stats, void* lut,
                       hipStream_t st);

@@ -710,6 +710,110 @@ __device__ __forceinline__ void epilogue_pi(f32x16 (&acc)[4][2], float* __restri
         }
 }
 
+// Segmented accumulation (f32 GRM accuracy): the f32 MFMA accumulators absorb a long chain of
+// small additions into a large running sum (a rare variant's z^2 ~ n puts K_ii at ~1e5 early, then
+// every later 16-product step rounds at ulp(1e5)/2, and the tiny z^2 = 2 maf of rare SNPs at the
+// major genotype are lost), so a launch over 62.5k SNPs lands ~3e-5 of max diag from the f64 GRM
+// where NumPy's float32 K (OpenBLAS K-panels of a few hundred SNPs, then K += per block) is ~3e-7
+// (tools/diag_f32_accuracy.py, profiles/r03acc).  Every `seg.snps` SNPs a workgroup adds its
+// accumulators into a private scratch slot and restarts them at zero, so no f32 chain is longer
+// than that; the final epilogue adds the slot back.  The slot is in register-native layout
+// ([wave][32 f32x4][64 lanes], one 16-B buffer load + store per 4 accumulators, lane offset in one
+// VGPR, the rest constant soffsets -- with flat addresses the compiler hoists 32 loop-invariant
+// 64-bit addresses out of the k-loop and spills ~210 VGPRs), from a pool taken by atomic CAS
+// (SegCtx).  Flush points are staggered by workgroup (phase = wg mod trips).
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+struct SegFlush {
+    uint32_t trips = 0, trip = 0;
+    bool any = false;  // a segment was flushed into the slot
+    uint32_t slot = 0;
+    __amdgpu_buffer_rsrc_t rs;
+    int voff = 0;
+
+    // call once per kernel by every thread (contains a barrier when segmentation is on)
+    __device__ SegFlush(const SegCtx& c, uint32_t snps_per_trip, uint64_t wg, uint64_t total_trips, uint32_t* sh) {
+        if (c.snps == 0) return;
+        trips = max(1u, c.snps / snps_per_trip);
+        trip = (uint32_t)(wg % trips);
+        if (trips - trip >= total_trips) {  // no flush in this workgroup: no slot needed
+            trips = 0;
+            return;
+        }
+        if (threadIdx.x == 0) {
+            uint32_t i = (uint32_t)((wg * 97u) % c.nslots);
+            while (atomicCAS(c.flags + i, 0u, 1u) != 0u) i = i + 1 == c.nslots ? 0 : i + 1;
+            *sh = i;
+        }
+        __syncthreads();
+        slot = *sh;
+        const int wave = threadIdx.x >> 6;
+        float* base = c.scratch + (uint64_t)slot * kSegSlotFloats + (uint64_t)wave * (32 * 64 * 4);
+        const uint64_t b = reinterpret_cast<uint64_t>(base);
+        const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b), hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
+        rs = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uint64_t)hi << 32) | lo), 0, 32 * 64 * 16, 0x00020000);
+        voff = (threadIdx.x & 63) * 16;
+    }
+    // call once per trip; true when the accumulators should be flushed now
+    __device__ bool due(bool more) {
+        if (!trips || ++trip < trips) return false;
+        trip = 0;
+        return more;
+    }
+    template <int Q>
+    __device__ __forceinline__ void put(f32x16& a, int i) {
+        f32x4 v = __builtin_shufflevector(a, a, 4 * Q, 4 * Q + 1, 4 * Q + 2, 4 * Q + 3);
+        if (any) v += __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, i * 1024, 0));
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rs, voff, i * 1024, 0);
+    }
+    __device__ void flush(f32x16 (&a)[4][2]) {
+#pragma unroll
+        for (int x = 0; x < 4; x++)
+#pragma unroll
+            for (int y = 0; y < 2; y++) {
+                const int i = (x * 2 + y) * 4;
+                put<0>(a[x][y], i);
+                put<1>(a[x][y], i + 1);
+                put<2>(a[x][y], i + 2);
+                put<3>(a[x][y], i + 3);
+                a[x][y] = (f32x16){};
+            }
+        any = true;
+    }
+    // before the final epilogue: add the flushed segments back into the accumulators
+    template <int Q>
+    __device__ __forceinline__ void get(f32x16& a, int i) {
+        const f32x4 v = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, i * 1024, 0));
+        a[4 * Q] += v.x;
+        a[4 * Q + 1] += v.y;
+        a[4 * Q + 2] += v.z;
+        a[4 * Q + 3] += v.w;
+    }
+    __device__ void finish(f32x16 (&a)[4][2]) {
+        if (!any) return;
+#pragma unroll
+        for (int x = 0; x < 4; x++)
+#pragma unroll
+            for (int y = 0; y < 2; y++) {
+                const int i = (x * 2 + y) * 4;
+                get<0>(a[x][y], i);
+                get<1>(a[x][y], i + 1);
+                get<2>(a[x][y], i + 2);
+                get<3>(a[x][y], i + 3);
+            }
+    }
+    // after the final epilogue, by every thread: give the slot back
+    __device__ void release(const SegCtx& c) {
+        if (!trips) return;
+        __syncthreads();  // every wave has read its part of the slot back
+        if (threadIdx.x == 0) {
+            __threadfence();
+            atomicExch(c.flags + slot, 0u);
+        }
+    }
+};
+
 // MODE 0: load stage s+1 -> registers during stage s, expand + ds_write after its MFMAs.
 // MODE 1: codes/LUT of stage s+2 in flight (two register sets); stage s+1's expansion and
 //         ds_writes are issued plane by plane between the MFMA groups of stage s, so the VALU
@@ -726,7 +830,7 @@ __global__ __launch_bounds__(512, 1) void k_syrk_bf3(const uint8_t* __restrict__
                                                      float* __restrict__ tiles, int accumulate,
                                                      uint32_t part_rank = 0, uint32_t part_world = 1,
                                                      uint64_t kslice = 0, uint64_t slice_elems = 0,
-                                                     const uint32_t* __restrict__ gate = nullptr) {
+                                                     const uint32_t* __restrict__ gate = nullptr, SegCtx seg = SegCtx()) {
     __shared__ __attribute__((aligned(16))) short lds[2 * B3_STAGE];
     if (gate && *gate == 0) return;  // fallback of k_syrk_h2: runs only when its range flag is set
     if (gridDim.y > 1) {  // split-K: slice blockIdx.y covers SNPs [y*kslice, +kslice) into its own partial K
@@ -867,6 +971,8 @@ __global__ __launch_bounds__(512, 1) void k_syrk_bf3(const uint8_t* __restrict__
         if (nst > 1) load(1, r);
         __syncthreads();
         bf16x8_t B0s[2], B1s[2], B0t[2], B1t[2];
+        __shared__ uint32_t seg_slot;
+        SegFlush sf(seg, 2 * BK, wg, (nst + 1) / 2, &seg_slot);
         fragB(lds, 0, B0s);
         fragB(lds, 1, B1s);
         // MODE 5 (default): the hooks run unconditionally (the last stage expands into the idle
@@ -922,7 +1028,12 @@ __global__ __launch_bounds__(512, 1) void k_syrk_bf3(const uint8_t* __restrict__
         for (uint64_t s = 0; s < nst; s += 2) {
             stage(s, B0s, B1s, B0t, B1t);
             if (s + 1 < nst) stage(s + 1, B0t, B1t, B0s, B1s);
+            if (sf.due(s + 2 < nst)) sf.flush(acc);
         }
+        sf.finish(acc);
+        epilogue_pi<LOCAL>(acc, tiles, n, bi, bj, accumulate, lane, wm, wn, wg);
+        sf.release(seg);
+        return;
     } else if constexpr (MODE == 1) {
         // one register set: the codes/LUT of stage s+1 are expanded and stored plane by plane
         // after MFMA groups 0-3 of stage s, and right after the last plane the loads of stage
@@ -1118,7 +1229,8 @@ __global__ __launch_bounds__(512, 1) void k_syrk_h2(const uint8_t* __restrict__ 
                                                     uint64_t kdim, const uint32_t* __restrict__ lut2,
                                                     const uint32_t* __restrict__ flag, float* __restrict__ tiles,
                                                     int accumulate, uint32_t part_rank = 0, uint32_t part_world = 1,
-                                                    uint64_t kslice = 0, uint64_t slice_elems = 0) {
+                                                    uint64_t kslice = 0, uint64_t slice_elems = 0,
+                                                    SegCtx seg = SegCtx()) {
     // KS = 16-SNP k-steps per LDS stage (MODE 4/5: two, one barrier per 32 SNPs)
     // MODE 10 = MODE 4 with the loader's registers double-buffered: stage s+2's codes/LUT are
     // loaded at the START of stage s (a whole stage to arrive instead of one MFMA group)
@@ -1280,6 +1392,8 @@ __global__ __launch_bounds__(512, 1) void k_syrk_h2(const uint8_t* __restrict__ 
         issue(0, lds);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
+        __shared__ uint32_t seg_slot;
+        SegFlush sf(seg, SBK, wg, nst, &seg_slot);
         for (uint64_t s = 0; s < nst; s++) {
             const short* cur = lds + (s & 1) * STAGE;
             if (s + 1 < nst) issue(s + 1, lds + ((s + 1) & 1) * STAGE);
@@ -1296,12 +1410,23 @@ __global__ __launch_bounds__(512, 1) void k_syrk_h2(const uint8_t* __restrict__ 
             }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
+            if (sf.due(s + 1 < nst)) sf.flush(acc);
         }
+        sf.finish(acc);
         epilogue_pi<LOCAL>(acc, tiles, n, bi, bj, accumulate, lane, wm, wn, wg);
+        sf.release(seg);
         return;
     }
-    {
-        load(0);
+    // Segments (f32 accuracy, see SegFlush): the stages run in segments of seg_st stages, each with
+    // its own pipeline prologue and an epilogue that adds the accumulators into the K tiles, so no
+    // f32 accumulation chain is longer than seg_snps SNPs; the first segment of workgroup wg is
+    // shortened by a wg-dependent phase so the workgroups in flight flush at different times.
+    // (A flush INSIDE the pipelined loop spilled ~210 VGPRs: the loop-carried fragments and loader
+    // registers stay live across it; between segments only the accumulators are.)
+    uint64_t send = nst;  // end (exclusive) of the current segment: the loader clamps to it
+    f16x8_t B0s[2], B1s[2], B0t[2], B1t[2];
+    auto prologue = [&](uint64_t s0) {
+        load(s0);
 #pragma unroll
         for (int h = 0; h < KS; h++) {
             uint32_t sel[8];
@@ -1309,12 +1434,11 @@ __global__ __launch_bounds__(512, 1) void k_syrk_h2(const uint8_t* __restrict__ 
             store_plane(lds, 0, h, sel);
             store_plane(lds, 1, h, sel);
         }
-        load(nst > 1 ? 1 : 0);
-    }
-    __syncthreads();
-    f16x8_t B0s[2], B1s[2], B0t[2], B1t[2];
-    fragB(lds, 0, 0, B0s);
-    fragB(lds, 1, 0, B1s);
+        load(s0 + 1 < send ? s0 + 1 : send - 1);
+        __syncthreads();
+        fragB(lds, 0, 0, B0s);
+        fragB(lds, 1, 0, B1s);
+    };
     // The loader runs unconditionally (the last stage expands into the idle buffer and its code
     // loads clamp to the last stage) so each MFMA group and its VALU share one basic block.
     // MODE 2/3: stage s+1's A plane-0 fragments are read after the barrier too (a second A
@@ -1322,7 +1446,6 @@ __global__ __launch_bounds__(512, 1) void k_syrk_h2(const uint8_t* __restrict__ 
     // loader VALU between the MFMAs, MODE 1/2/4 leave the order to the compiler.
     constexpr bool kPreA = MODE == 2 || MODE == 3, kPin = MODE == 0 || MODE == 3 || MODE == 5;
     f16x8_t A0s[4], A0t[4];
-    if constexpr (kPreA) fragsA(lds, 0, 0, A0s);
     auto stage = [&](uint64_t s, f16x8_t (&B0)[2], f16x8_t (&B1)[2], f16x8_t (&A0)[4], f16x8_t (&B0n)[2],
                      f16x8_t (&B1n)[2], f16x8_t (&A0n)[4]) {
         const short* cur = lds + (s & 1) * STAGE;
@@ -1339,7 +1462,7 @@ __global__ __launch_bounds__(512, 1) void k_syrk_h2(const uint8_t* __restrict__ 
             group(A0, B1);
             store_plane(nxt, 1, 0, sel);
             if constexpr (kPin) pin(std::integral_constant<int, 1>{});
-            load(s + 2 < nst ? s + 2 : nst - 1);
+            load(s + 2 < send ? s + 2 : send - 1);
             __syncthreads();
             fragB(nxt, 0, 0, B0n);
             fragB(nxt, 1, 0, B1n);
@@ -1352,7 +1475,7 @@ __global__ __launch_bounds__(512, 1) void k_syrk_h2(const uint8_t* __restrict__ 
             f16x8_t Ax[4], Ay[4], C0[2], C1[2];
             fragsA(cur, 0, 0, Ax);
             fragsA(cur, 1, 0, Ay);
-            if constexpr (kLd2) load2(s + 2 < nst ? s + 2 : nst - 1);
+            if constexpr (kLd2) load2(s + 2 < send ? s + 2 : send - 1);
             uint32_t sel[8];
             group(Ax, B0);
             if constexpr (!kNoLd) {
@@ -1384,7 +1507,7 @@ __global__ __launch_bounds__(512, 1) void k_syrk_h2(const uint8_t* __restrict__ 
                     rl[h] = rl2[h];
                 }
             } else if constexpr (!kNoLd) {
-                load(s + 2 < nst ? s + 2 : nst - 1);
+                load(s + 2 < send ? s + 2 : send - 1);
             }
             __syncthreads();
             fragB(nxt, 0, 0, B0n);
@@ -1399,11 +1522,18 @@ __global__ __launch_bounds__(512, 1) void k_syrk_h2(const uint8_t* __restrict__ 
     } else if constexpr (MODE == 8) {
         if (__builtin_amdgcn_readfirstlane(t) < 256) __builtin_amdgcn_s_setprio(1);
     }
+    __shared__ uint32_t seg_slot;
+    SegFlush sf(seg, 2 * SBK, wg, (nst + 1) / 2, &seg_slot);
+    prologue(0);
+    if constexpr (kPreA) fragsA(lds, 0, 0, A0s);
     for (uint64_t s = 0; s < nst; s += 2) {
         stage(s, B0s, B1s, A0s, B0t, B1t, A0t);
         if (s + 1 < nst) stage(s + 1, B0t, B1t, A0t, B0s, B1s, A0s);
+        if (sf.due(s + 2 < nst)) sf.flush(acc);
     }
+    sf.finish(acc);
     epilogue_pi<LOCAL>(acc, tiles, n, bi, bj, accumulate, lane, wm, wn, wg);
+    sf.release(seg);
 }
 
 // ---------------------------------------------------------------- fp16x2 on v_mfma_f32_16x16x32_f16
@@ -2325,6 +2455,18 @@ __global__ __launch_bounds__(256, 2) void k_syrk_glds(const double* __restrict__
 }  // namespace
 
 int g_variant_syrk = 0;  // tuning hook (snpmi_set_kernel_variant "syrk")
+// 8192: 4.9e-6 of max diag at 50k x 100k on SnpGen-shaped data (21.8% missing) for +4.1% time;
+// 4096: 2.6e-6 for +6.0%; 16384: 6.9e-6 for +2.0%; none: 3.2e-5 (profiles/r03acc)
+int g_seg_snps = 8192;   // tuning hook "seg"
+
+// host-side segmentation for the f32-MFMA kernels without SegFlush (fallbacks and small-N
+// kernels): one launch per <= g_seg_snps / 2 SNPs, each accumulating onto the previous ones
+// (v_mfma_f32_32x32x2f32 adds 2 SNPs per rounding step where the fp16 kernels add 16 x 3 products)
+template <class F>
+static void for_segments(uint64_t m, int accumulate, F&& launch) {
+    const uint64_t seg = g_seg_snps > 0 ? round_up((uint64_t)g_seg_snps / 2, 64) : m;
+    for (uint64_t c0 = 0; c0 < m; c0 += seg) launch(c0, std::min(seg, m - c0), accumulate || c0 > 0);
+}
 
 void launch_syrk_packed(const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m, const void* lut, int dtype,
                         void* tiles, int accumulate, hipStream_t st) {
@@ -2345,10 +2487,19 @@ void launch_syrk_packed(const uint8_t* packed, uint64_t pitch, uint64_t n, uint6
         // (variant 20 below N = 4096) or by the ubench build's ablations.
         int v = g_variant_syrk;
         if (v == 0 || v == 20) v = n >= 4096 ? 4 : 5;
+        if (v == 4 || v == 5) {
+            for_segments(m, accumulate, [&](uint64_t c0, uint64_t cnt, int acc) {
+                if (v == 4)
+                    f32w::k_syrk256<1><<<(unsigned)(nb * (nb + 1) / 2), 512, 0, st>>>(packed + c0 * pitch, pitch, n, cnt,
+                                                                                     L + 4 * c0, Tt, acc);
+                else
+                    f32k::k_syrk<true, 16, 4><<<(unsigned)nt, 256, 0, st>>>(packed + c0 * pitch, pitch, cnt, L + 4 * c0,
+                                                                           Tt, acc);
+                SNPMI_HIP(hipGetLastError());
+            });
+            return;
+        }
         switch (v) {
-            case 4:
-                f32w::k_syrk256<1><<<(unsigned)(nb * (nb + 1) / 2), 512, 0, st>>>(packed, pitch, n, m, L, Tt, accumulate);
-                break;
 #ifdef SNPMI_UBENCH
             case 1: f32k::k_syrk<true, 32, 2><<<(unsigned)nt, 256, 0, st>>>(packed, pitch, m, L, Tt, accumulate); break;
             case 2: f32k::k_syrk_il<4><<<(unsigned)nt, 256, 0, st>>>(packed, pitch, m, L, Tt, accumulate); break;
@@ -2415,9 +2566,12 @@ void launch_syrk_packed_part(const uint8_t* packed, uint64_t pitch, uint64_t n, 
         if (!accumulate) SNPMI_HIP(hipMemsetAsync(blocks, 0, nloc * 256 * 256 * sizeof(float), st));
         return;
     }
-    f32w::k_syrk256<1, true><<<(unsigned)nloc, 512, 0, st>>>(packed, pitch, n, m, (const float*)lut, (float*)blocks,
-                                                             accumulate, (uint32_t)rank, (uint32_t)world);
-    SNPMI_HIP(hipGetLastError());
+    for_segments(m, accumulate, [&](uint64_t c0, uint64_t cnt, int acc) {
+        f32w::k_syrk256<1, true><<<(unsigned)nloc, 512, 0, st>>>(packed + c0 * pitch, pitch, n, cnt,
+                                                                 (const float*)lut + 4 * c0, (float*)blocks, acc,
+                                                                 (uint32_t)rank, (uint32_t)world);
+        SNPMI_HIP(hipGetLastError());
+    });
 }
 
 uint64_t lut_bf3_entries(uint64_t m) { return round_up(std::max<uint64_t>(m, 1), (uint64_t)2 * f32w::BK); }
@@ -2508,11 +2662,14 @@ void launch_syrk_dense_h2(const float* Z, uint64_t ldz, uint64_t n, uint64_t m, 
         f32w::k_image_h2<<<dim3((unsigned)nb, (unsigned)steps), 256, 0, st>>>(Z + c0 * ldz, ldz, n, cnt, (short*)img);
         SNPMI_HIP(hipGetLastError());
         f32w::k_syrk_h2<false, 6, true><<<(unsigned)g, 512, 0, st>>>((const uint8_t*)img, ldz, n, cnt, order, flag,
-                                                                      tiles, accumulate || c0 > 0);
+                                                                      tiles, accumulate || c0 > 0, 0, 1, 0, 0,
+                                                                      seg_ctx());
         SNPMI_HIP(hipGetLastError());
     }
-    f32w::k_syrk256d<><<<(unsigned)g, 512, 0, st>>>(Z, ldz, n, m, tiles, accumulate, 0, 1, flag);
-    SNPMI_HIP(hipGetLastError());
+    for_segments(m, accumulate, [&](uint64_t c0, uint64_t cnt, int acc) {
+        f32w::k_syrk256d<><<<(unsigned)g, 512, 0, st>>>(Z + c0 * ldz, ldz, n, cnt, tiles, acc, 0, 1, flag);
+        SNPMI_HIP(hipGetLastError());
+    });
 }
 
 void launch_syrk_packed_bf3(const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m, const uint32_t* lut3,
@@ -2567,11 +2724,13 @@ void launch_syrk_packed_bf3(const uint8_t* packed, uint64_t pitch, uint64_t n, u
             case 62: f32w::k_syrk_h2<false, 10><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles, accumulate); break;
             case 63: f32w::k_syrk_h2<false, 11><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles, accumulate); break;
 #endif
-            default: f32w::k_syrk_h2<false, 4><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles, accumulate);
+            default:
+                f32w::k_syrk_h2<false, 4><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles,
+                                                                      accumulate, 0, 1, 0, 0, seg_ctx());
         }
         SNPMI_HIP(hipGetLastError());
         f32w::k_syrk_bf3<false, false, 5><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, lut3, tiles, accumulate, 0, 1, 0, 0,
-                                                                      h2->flag);
+                                                                      h2->flag, seg_ctx());
         SNPMI_HIP(hipGetLastError());
         return;
     }
@@ -2584,7 +2743,9 @@ void launch_syrk_packed_bf3(const uint8_t* packed, uint64_t pitch, uint64_t n, u
         case 34: f32w::k_syrk_bf3<false, false, 2><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, lut3, tiles, accumulate); break;
         case 39: f32w::k_syrk_bf3<false, true, 9><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, lut3, tiles, accumulate); break;
 #endif
-        default: f32w::k_syrk_bf3<false, false, 5><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, lut3, tiles, accumulate);
+        default:
+            f32w::k_syrk_bf3<false, false, 5><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, lut3, tiles, accumulate, 0, 1,
+                                                                          0, 0, nullptr, seg_ctx());
     }
     SNPMI_HIP(hipGetLastError());
 }
@@ -2601,11 +2762,12 @@ void launch_syrk_packed_bf3_split(const uint8_t* packed, uint64_t pitch, uint64_
     SNPMI_REQUIRE(g < (1ull << 31) && S >= 1, SNPMI_E_ARG, "bad split");
     if (h2) {
         f32w::k_syrk_h2<><<<dim3((unsigned)g, S), 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, partial, 0, 0, 1,
-                                                                 kslice, elems);
+                                                                 kslice, elems, seg_ctx());
         SNPMI_HIP(hipGetLastError());
     }
     f32w::k_syrk_bf3<false, false, 5><<<dim3((unsigned)g, S), 512, 0, st>>>(packed, pitch, n, m, lut3, partial, 0, 0, 1,
-                                                                          kslice, elems, h2 ? h2->flag : nullptr);
+                                                                          kslice, elems, h2 ? h2->flag : nullptr,
+                                                                          seg_ctx());
     SNPMI_HIP(hipGetLastError());
     launch_tile_reduce(partial, S, elems, tiles, accumulate, st);
 }
@@ -2624,12 +2786,13 @@ void launch_syrk_packed_bf3_part(const uint8_t* packed, uint64_t pitch, uint64_t
     }
     if (h2) {
         f32w::k_syrk_h2<true><<<(unsigned)nloc, 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, blocks, accumulate,
-                                                               (uint32_t)rank, (uint32_t)world);
+                                                               (uint32_t)rank, (uint32_t)world, 0, 0,
+                                                               seg_ctx());
         SNPMI_HIP(hipGetLastError());
     }
     f32w::k_syrk_bf3<true, false, 5><<<(unsigned)nloc, 512, 0, st>>>(packed, pitch, n, m, lut3, blocks, accumulate,
                                                                      (uint32_t)rank, (uint32_t)world, 0, 0,
-                                                                     h2 ? h2->flag : nullptr);
+                                                                     h2 ? h2->flag : nullptr, seg_ctx());
     SNPMI_HIP(hipGetLastError());
 }
 
@@ -2643,9 +2806,11 @@ void launch_syrk_dense_part(const float* Z, uint64_t ldz, uint64_t n, uint64_t m
         if (!accumulate) SNPMI_HIP(hipMemsetAsync(blocks, 0, nloc * 256 * 256 * sizeof(float), st));
         return;
     }
-    f32w::k_syrk256d<true><<<(unsigned)nloc, 512, 0, st>>>(Z, ldz, n, m, (float*)blocks, accumulate, (uint32_t)rank,
-                                                           (uint32_t)world);
-    SNPMI_HIP(hipGetLastError());
+    for_segments(m, accumulate, [&](uint64_t c0, uint64_t cnt, int acc) {
+        f32w::k_syrk256d<true><<<(unsigned)nloc, 512, 0, st>>>(Z + c0 * ldz, ldz, n, cnt, (float*)blocks, acc,
+                                                               (uint32_t)rank, (uint32_t)world);
+        SNPMI_HIP(hipGetLastError());
+    });
 }
 
 void launch_syrk_dense(const void* Z, uint64_t ldz, uint64_t n, uint64_t m, int dtype, void* tiles, int accumulate,
@@ -2673,9 +2838,15 @@ void launch_syrk_dense(const void* Z, uint64_t ldz, uint64_t n, uint64_t m, int 
         else
 #endif
         if (n >= 4096 && ldz >= nb * 256 && g_variant_syrk != 5)
-            f32w::k_syrk256d<><<<g, 512, 0, st>>>(Zf, ldz, n, m, Tf, accumulate);
+            for_segments(m, accumulate, [&](uint64_t c0, uint64_t cnt, int acc) {
+                f32w::k_syrk256d<><<<g, 512, 0, st>>>(Zf + c0 * ldz, ldz, n, cnt, Tf, acc);
+                SNPMI_HIP(hipGetLastError());
+            });
         else
-            f32k::k_syrk<false, 16, 4><<<(unsigned)nt, 256, 0, st>>>(Z, ldz, m, nullptr, (float*)tiles, accumulate);
+            for_segments(m, accumulate, [&](uint64_t c0, uint64_t cnt, int acc) {
+                f32k::k_syrk<false, 16, 4><<<(unsigned)nt, 256, 0, st>>>(Zf + c0 * ldz, ldz, cnt, nullptr, Tf, acc);
+                SNPMI_HIP(hipGetLastError());
+            });
     }
 #ifdef SNPMI_UBENCH
     else if (g_variant_syrk == 5) {

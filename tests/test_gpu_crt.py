@@ -109,3 +109,38 @@ def test_crt_chunks_match_f64_mfma():
     got = outs[0][1][:128 * 128].reshape(128, 128)
     iu = np.triu_indices(128)
     assert np.abs(got[iu] - Kref[iu]).max() <= 1e-12 * np.abs(np.diag(Kref)).max()
+
+
+def test_public_f64_switch_selects_the_f64_mfma():
+    """pysnptools_amd.set_grm_f64: 'mfma' runs f64 GRMs on the f64 MFMA (no CRT launches), 'crt' back
+    to the int8 residues; both within 1e-12 of max diag of the reference's own toydata GRM."""
+    import ctypes
+    import os
+
+    import numpy as np
+
+    import pysnptools_amd
+    from conftest import DATA
+    from pysnptools_amd import _native as N
+    from pysnptools_amd.snpreader import Bed
+    from pysnptools_amd.standardizer import Unit
+
+    gold = np.load(os.path.join(DATA, "toydata.kernel.npz"))["val"]
+    bed = Bed(os.path.join(DATA, "toydata.bed"), count_A1=False)
+    sr, nl = ctypes.c_uint64(), ctypes.c_uint64()
+    out = {}
+    try:
+        for path in ("mfma", "crt"):
+            pysnptools_amd.set_grm_f64(path)
+            N.call("snpmi_crt_moduli_stats", ctypes.byref(sr), ctypes.byref(nl), 1)
+            out[path] = bed.read_kernel(Unit()).val
+            N.call("snpmi_crt_moduli_stats", ctypes.byref(sr), ctypes.byref(nl), 1)
+            assert (nl.value == 0) == (path == "mfma"), (path, nl.value)
+    finally:
+        pysnptools_amd.set_grm_f64("crt")
+    scale = np.abs(np.diag(gold)).max()
+    for path, K in out.items():
+        assert np.abs(K - gold).max() / scale <= 1e-12, path
+    import pytest
+    with pytest.raises(ValueError):
+        pysnptools_amd.set_grm_f64("f32")

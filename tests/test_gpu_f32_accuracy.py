@@ -1,0 +1,86 @@
+"""f32 GRM accuracy at large M on SnpGen-shaped data (rare-variant heavy MAF curve, 21.8% missing):
+the f32 accumulation chains of the SYRK kernels are cut every `seg` SNPs (8192; syrk.hip SegFlush /
+for_segments), so one launch over tens of thousands of SNPs stays within the f32 bar (1e-5 of max
+diag; asserted here at 6e-6) against the f64 oracle.  Before the segmentation one 62.5k-SNP launch of the fp16x2 kernel drifted 2e-5 of max
+diag at 50k x 100k (bench `file` leg), because the tiny z^2 of rare-variant SNPs were absorbed into
+K_ii ~ 1e5.  Checked for the three f32 kernels: fp16x2 (default), bf16x3 (its range fallback,
+variant 36) and the f32 MFMA (variant 20: 2 products per MFMA k-step, so twice the chain steps of
+the fp16 kernels per segment), and for the partitioned (cfg5) kernel."""
+import numpy as np
+import pytest
+
+from conftest import ROOT  # noqa: F401  (sys.path)
+import bench
+from oracle import oracle as O
+from pysnptools_amd import _native as N
+from pysnptools_amd.shard import ShardedGrm
+
+pytestmark = pytest.mark.gpu
+
+n, m, R = 20_000, 48_000, 8
+
+
+@pytest.fixture(scope="module")
+def data():
+    pitch = N.lib().snpmi_packed_pitch(n)
+    packed = bench.Dev(N, pitch * m)
+    bench.synth(N, packed.p, pitch, n, 0, m, 305, 0.218)
+    host = np.empty((m, pitch), dtype=np.uint8)
+    N.call("snpmi_memcpy_d2h", N.ptr(host), packed.p, host.nbytes)
+    body = np.ascontiguousarray(host[:, :(n + 3) // 4]).reshape(-1)
+    ref = np.zeros((R, n))
+    for s0 in range(0, m, 4096):
+        sid = np.arange(s0, min(m, s0 + 4096), dtype=np.uint64)
+        Z, _ = O.decode_standardize(body, n, m, sid_index=sid, dtype=np.float64)
+        ref += Z[:R].dot(Z.T)
+    yield packed, pitch, body, ref
+    packed.free()
+
+
+def _rows(packed, pitch):
+    stats = bench.Dev(N, m * 8)
+    g = ShardedGrm(n, np.float32, None, "none")
+    g.add_packed(packed.p, pitch, m, N.STD_UNIT, 0.0, 0.0, 0, stats.p)  # one launch of 48k SNPs
+    t, _ = g.tiles()
+    ri = np.arange(R, dtype=np.uint64)
+    dri, dout = bench.Dev(N, R * 8), bench.Dev(N, R * n * 4)
+    N.call("snpmi_memcpy_h2d", dri.p, N.ptr(ri), ri.nbytes)
+    N.call("snpmi_dev_grm_extract", t, n, N.DT_F32, dri.p, R, None, n, 1, 1.0, dout.p)
+    K = np.empty((R, n), dtype=np.float32)
+    N.call("snpmi_memcpy_d2h", N.ptr(K), dout.p, K.nbytes)
+    g.abort()
+    for d in (stats, dri, dout):
+        d.free()
+    return K
+
+
+@pytest.mark.parametrize("variant,tol", [(0, 6e-6), (36, 6e-6), (20, 6e-6)])
+def test_long_launch_within_f32_bar(data, variant, tol):
+    packed, pitch, _, ref = data
+    N.call("snpmi_set_kernel_variant", b"syrk", variant)
+    try:
+        K = _rows(packed, pitch)
+    finally:
+        N.call("snpmi_set_kernel_variant", b"syrk", 0)
+    scale = np.abs(np.diag(ref[:, :R])).max()
+    err = np.abs(K.astype(np.float64) - ref).max() / scale
+    assert err <= tol, err
+    diag_rel = np.max(np.abs(np.diag(K[:, :R]) - np.diag(ref[:, :R])) / np.diag(ref[:, :R]))
+    assert diag_rel <= tol, diag_rel
+
+
+def test_partitioned_blocks_within_f32_bar(data):
+    """cfg5 kernel (k_syrk_h2<LOCAL>): part 0 of 4 -- its first block (rows/cols 0..255) over all SNPs."""
+    packed, pitch, body, ref = data
+    lut, stats = bench.Dev(N, m * 16), bench.Dev(N, m * 8)
+    nloc = N.lib().snpmi_grm_part_blocks(n, 0, 4)
+    blocks = bench.Dev(N, nloc * 256 * 256 * 4)
+    N.call("snpmi_dev_snp_stats", packed.p, pitch, n, m, 0, N.STD_UNIT, 0.0, 0.0, 0, N.DT_F32, stats.p, lut.p)
+    N.call("snpmi_dev_syrk_packed_part", packed.p, pitch, n, m, lut.p, 0, 4, blocks.p, 0)
+    blk = np.empty((256, 256), dtype=np.float32)
+    N.call("snpmi_memcpy_d2h", N.ptr(blk), blocks.p, blk.nbytes)
+    for d in (lut, stats, blocks):
+        d.free()
+    scale = np.abs(np.diag(ref[:, :R])).max()
+    err = np.abs(blk[:R].astype(np.float64) - ref[:, :256]).max() / scale
+    assert err <= 6e-6, err

@@ -8,6 +8,7 @@ K rows 0..R-1 of an n x m synthetic matrix (SnpGen MAF curve, --miss missing) fr
 against the f64 oracle.  Reports max|dK| / max diag and where the maximum sits.
 """
 import argparse
+import ctypes
 import json
 import os
 import sys
@@ -25,7 +26,9 @@ def main():
     ap.add_argument("--miss", type=float, default=0.218)
     ap.add_argument("--seed", type=int, default=305)
     ap.add_argument("--rows", type=int, default=8)
-    ap.add_argument("--chunks", default="65536,10000,2048")
+    ap.add_argument("--chunks", default="65536")
+    ap.add_argument("--segs", default="0,4096,8192,16384", help="syrk 'seg' settings (SNPs per f32 chain)")
+    ap.add_argument("--variants", default="0,36,20")
     args = ap.parse_args()
     import bench
     from oracle import oracle as O
@@ -50,35 +53,48 @@ def main():
         ref32 += Z32[:R].dot(Z32.T)
     scale = np.abs(np.diag(ref[:, :R])).max()
 
-    def report(name, K):
+    def report(name, K, **extra):
         d = np.abs(K.astype(np.float64) - ref)
         i, j = np.unravel_index(np.argmax(d), d.shape)
         print(json.dumps({"path": name, "max_abs_err_over_max_diag": float(d.max() / scale),
                           "at": [int(i), int(j)], "ref_there": float(ref[i, j]), "max_diag": float(scale),
                           "mean_abs_err_over_max_diag": float(d.mean() / scale),
                           "diag_rel_err": float(np.max(np.abs(np.diag(K[:, :R]) - np.diag(ref[:, :R]))
-                                                       / np.abs(np.diag(ref[:, :R]))))}), flush=True)
+                                                       / np.abs(np.diag(ref[:, :R])))), **extra}), flush=True)
 
     report("reference_f32_numpy_blocks_10k", ref32)
     stats = bench.Dev(N, m * 8)
     ri = np.arange(R, dtype=np.uint64)
     dri, dout = bench.Dev(N, R * 8), bench.Dev(N, R * n * 4)
     N.call("snpmi_memcpy_h2d", dri.p, N.ptr(ri), ri.nbytes)
-    for variant, label in ((0, "fp16x2"), (36, "bf16x3"), (20, "f32_mfma")):
-        N.call("snpmi_set_kernel_variant", b"syrk", variant)
-        for chunk in [int(c) for c in args.chunks.split(",")]:
-            g = ShardedGrm(n, np.float32, None, "none")
-            for s0 in range(0, m, chunk):
-                c = min(chunk, m - s0)
-                g.add_packed(packed.at(s0 * pitch), pitch, c, N.STD_UNIT, 0.0, 0.0, 0, stats.at(s0 * 8))
-            t, _ = g.tiles()
-            N.call("snpmi_dev_grm_extract", t, n, N.DT_F32, dri.p, R, None, n, 1, 1.0, dout.p)
-            K = np.empty((R, n), dtype=np.float32)
-            N.call("snpmi_memcpy_d2h", N.ptr(K), dout.p, K.nbytes)
-            g.abort()
-            report("%s_chunk%d" % (label, chunk), K)
-            if variant:
-                break
+    ev = [ctypes.c_void_p(), ctypes.c_void_p()]
+    for e in ev:
+        N.call("snpmi_event_create", ctypes.byref(e))
+    for seg in [int(x) for x in args.segs.split(",")]:
+        N.call("snpmi_set_kernel_variant", b"seg", seg)
+        labels = {0: "fp16x2", 36: "bf16x3", 20: "f32_mfma"}
+        for variant in [int(v) for v in args.variants.split(",")]:
+            label = labels[variant]
+            N.call("snpmi_set_kernel_variant", b"syrk", variant)
+            for chunk in [int(c) for c in args.chunks.split(",")]:
+                g = ShardedGrm(n, np.float32, None, "none")
+                g.add_packed(packed.p, pitch, min(m, 256), N.STD_UNIT, 0.0, 0.0, 0, stats.p)  # warm-up
+                g.abort()
+                g = ShardedGrm(n, np.float32, None, "none")
+                N.call("snpmi_event_record", ev[0])
+                for s0 in range(0, m, chunk):
+                    c = min(chunk, m - s0)
+                    g.add_packed(packed.at(s0 * pitch), pitch, c, N.STD_UNIT, 0.0, 0.0, 0, stats.at(s0 * 8))
+                N.call("snpmi_event_record", ev[1])
+                ms = ctypes.c_float()
+                N.call("snpmi_event_elapsed_ms", ev[0], ev[1], ctypes.byref(ms))
+                t, _ = g.tiles()
+                N.call("snpmi_dev_grm_extract", t, n, N.DT_F32, dri.p, R, None, n, 1, 1.0, dout.p)
+                K = np.empty((R, n), dtype=np.float32)
+                N.call("snpmi_memcpy_d2h", N.ptr(K), dout.p, K.nbytes)
+                g.abort()
+                report("%s_chunk%d_seg%d" % (label, chunk, seg), K, ms=ms.value, tflops=n * (n + 1) * m / (ms.value * 1e-3) / 1e12)
+    N.call("snpmi_set_kernel_variant", b"seg", 8192)
     N.call("snpmi_set_kernel_variant", b"syrk", 0)
 
 
