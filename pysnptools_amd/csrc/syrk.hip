@@ -726,6 +726,11 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 struct SegFlush {
+    // Every `trips` trips the accumulators are flushed into the workgroup's slot and restart: the
+    // first flush stores them, later ones add to the slot with fire-and-forget f32 buffer atomics
+    // (the slot is private to the wave, so the adds never contend and their order is fixed), so a
+    // flush waits on nothing.  A read-modify-write flush (32 loads + 32 stores per lane at one
+    // barrier) cost +4.1% at 8192 SNPs.
     uint32_t trips = 0, trip = 0;
     bool any = false;  // a segment was flushed into the slot
     uint32_t slot = 0;
@@ -753,7 +758,7 @@ struct SegFlush {
         const uint64_t b = reinterpret_cast<uint64_t>(base);
         const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b), hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
         rs = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uint64_t)hi << 32) | lo), 0, 32 * 64 * 16, 0x00020000);
-        voff = (threadIdx.x & 63) * 16;
+        voff = (threadIdx.x & 63) * 4;
     }
     // call once per trip; true when the accumulators should be flushed now
     __device__ bool due(bool more) {
@@ -761,47 +766,44 @@ struct SegFlush {
         trip = 0;
         return more;
     }
-    template <int Q>
-    __device__ __forceinline__ void put(f32x16& a, int i) {
-        f32x4 v = __builtin_shufflevector(a, a, 4 * Q, 4 * Q + 1, 4 * Q + 2, 4 * Q + 3);
-        if (any) v += __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, i * 1024, 0));
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rs, voff, i * 1024, 0);
-    }
+    // slot layout per wave: sub-tile k = x*2+y, element e at float index (k*16 + e)*64 + lane
     __device__ void flush(f32x16 (&a)[4][2]) {
+        if (any) {
+#pragma unroll
+            for (int x = 0; x < 4; x++)
+#pragma unroll
+                for (int y = 0; y < 2; y++)
+#pragma unroll
+                    for (int e = 0; e < 16; e++)
+                        __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(a[x][y][e], rs, voff, ((x * 2 + y) * 16 + e) * 256, 0);
+        } else {
+#pragma unroll
+            for (int x = 0; x < 4; x++)
+#pragma unroll
+                for (int y = 0; y < 2; y++)
+#pragma unroll
+                    for (int e = 0; e < 16; e++) {
+                        const float v = a[x][y][e];  // (bit_cast of the element lvalue itself reads element 0)
+                        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), rs, voff, ((x * 2 + y) * 16 + e) * 256, 0);
+                    }
+        }
 #pragma unroll
         for (int x = 0; x < 4; x++)
 #pragma unroll
-            for (int y = 0; y < 2; y++) {
-                const int i = (x * 2 + y) * 4;
-                put<0>(a[x][y], i);
-                put<1>(a[x][y], i + 1);
-                put<2>(a[x][y], i + 2);
-                put<3>(a[x][y], i + 3);
-                a[x][y] = (f32x16){};
-            }
+            for (int y = 0; y < 2; y++) a[x][y] = (f32x16){};
         any = true;
     }
     // before the final epilogue: add the flushed segments back into the accumulators
-    template <int Q>
-    __device__ __forceinline__ void get(f32x16& a, int i) {
-        const f32x4 v = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, i * 1024, 0));
-        a[4 * Q] += v.x;
-        a[4 * Q + 1] += v.y;
-        a[4 * Q + 2] += v.z;
-        a[4 * Q + 3] += v.w;
-    }
     __device__ void finish(f32x16 (&a)[4][2]) {
         if (!any) return;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's adds have landed in L2
 #pragma unroll
         for (int x = 0; x < 4; x++)
 #pragma unroll
-            for (int y = 0; y < 2; y++) {
-                const int i = (x * 2 + y) * 4;
-                get<0>(a[x][y], i);
-                get<1>(a[x][y], i + 1);
-                get<2>(a[x][y], i + 2);
-                get<3>(a[x][y], i + 3);
-            }
+            for (int y = 0; y < 2; y++)
+#pragma unroll
+                for (int e = 0; e < 16; e++)  // glc: past the CU's vector cache
+                    a[x][y][e] += __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, voff, ((x * 2 + y) * 16 + e) * 256, 1));
     }
     // after the final epilogue, by every thread: give the slot back
     __device__ void release(const SegCtx& c) {
@@ -2455,8 +2457,8 @@ __global__ __launch_bounds__(256, 2) void k_syrk_glds(const double* __restrict__
 }  // namespace
 
 int g_variant_syrk = 0;  // tuning hook (snpmi_set_kernel_variant "syrk")
-// 8192: 4.9e-6 of max diag at 50k x 100k on SnpGen-shaped data (21.8% missing) for +4.1% time;
-// 4096: 2.6e-6 for +6.0%; 16384: 6.9e-6 for +2.0%; none: 3.2e-5 (profiles/r03acc)
+// 8192: 4.9e-6 of max diag at 50k x 100k on SnpGen-shaped data (21.8% missing) for +2.2% time;
+// 4096: 2.6e-6 for +3.8%; 16384: 6.9e-6 for +1.9%; none: 3.2e-5 (profiles/r03acc, r03seg)
 int g_seg_snps = 8192;   // tuning hook "seg"
 
 // host-side segmentation for the f32-MFMA kernels without SegFlush (fallbacks and small-N
