@@ -1419,13 +1419,8 @@ __global__ __launch_bounds__(512, 1) void k_syrk_h2(const uint8_t* __restrict__ 
         sf.release(seg);
         return;
     }
-    // Segments (f32 accuracy, see SegFlush): the stages run in segments of seg_st stages, each with
-    // its own pipeline prologue and an epilogue that adds the accumulators into the K tiles, so no
-    // f32 accumulation chain is longer than seg_snps SNPs; the first segment of workgroup wg is
-    // shortened by a wg-dependent phase so the workgroups in flight flush at different times.
-    // (A flush INSIDE the pipelined loop spilled ~210 VGPRs: the loop-carried fragments and loader
-    // registers stay live across it; between segments only the accumulators are.)
-    uint64_t send = nst;  // end (exclusive) of the current segment: the loader clamps to it
+    // f32 accuracy: SegFlush (above) cuts the accumulation chains every seg SNPs inside this loop.
+    const uint64_t send = nst;  // the loader clamps its stage index to send - 1
     f16x8_t B0s[2], B1s[2], B0t[2], B1t[2];
     auto prologue = [&](uint64_t s0) {
         load(s0);

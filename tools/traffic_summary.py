@@ -5,7 +5,7 @@ wide coalesced streaming read, so read bytes = 2 * FETCH_SIZE * 1024; WRITE_SIZE
 16-B-per-lane streaming stores; both counters are in KiB.  The bf16x3 SYRK (k_syrk_bf3) reads
 4-B-per-lane packed codes (64-B runs) and 16-B LUT rows, an access width the guide leaves
 uncalibrated: its FETCH_SIZE is reported raw (x1), marked "read_scale": 1.
-Usage: python tools/traffic_summary.py <prof_dir> <out.json>
+Usage: python tools/traffic_summary.py <prof_dir> <out.json> [dec_n,dec_block grm_n,grm_snps_per_launch]
 """
 import collections
 import csv
@@ -37,7 +37,7 @@ def load(path, counter):
     return by
 
 
-def main(prof, out):
+def main(prof, out, dec_cfg=(500000, 2048), grm_cfg=(50000, 10000)):
     res = {}
     for leg in ("dec", "grm"):
         f = load(os.path.join(prof, leg + "_FETCH_SIZE", "run_counter_collection.csv"), "FETCH_SIZE")
@@ -54,7 +54,7 @@ def main(prof, out):
             res.setdefault(k, {})[leg] = {"read_bytes": read_b, "write_bytes": write_b,
                                           "traffic_bytes": read_b + write_b, "launches": len(fv),
                                           "read_scale": scale}
-    res["_config"] = {"dec": [500000, 2048], "grm": [50000, 10000]}  # tools/profile.sh settings
+    res["_config"] = {"dec": list(dec_cfg), "grm": list(grm_cfg)}  # the profiling script's settings
     res["_source"] = ("rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes (tools/profile.sh); "
                       "read = 2*FETCH_SIZE (gfx950 correction), per full launch")
     json.dump(res, open(out, "w"), indent=1)
@@ -62,4 +62,5 @@ def main(prof, out):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2])
+    cfg = [tuple(int(x) for x in a.split(",")) for a in sys.argv[3:5]]
+    main(sys.argv[1], sys.argv[2], *cfg)
