@@ -198,13 +198,23 @@ template <typename V>
 __device__ __forceinline__ void store_nt(V* p, const V& v) {
     __builtin_nontemporal_store(v, p);
 }
+// ubench A/B of the store cache policy of the F-order decode (POL 0 = nt, the shipped policy)
+template <int POL>
+__device__ __forceinline__ void store_pol(f32x4_t* p, const f32x4_t& v) {
+    if constexpr (POL == 0) __builtin_nontemporal_store(v, p);
+    else if constexpr (POL == 1) *p = v;
+    else if constexpr (POL == 2) asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+    else if constexpr (POL == 3) asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(p), "v"(v) : "memory");
+    else if constexpr (POL == 4) asm volatile("global_store_dwordx4 %0, %1, off sc1 nt" ::"v"(p), "v"(v) : "memory");
+    else asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1 nt" ::"v"(p), "v"(v) : "memory");
+}
 
 // ORD (ubench-only A/B of the item order; 0 ships): 1 = each XCD takes a contiguous slice of
 // every grid pass, 2 = items column-interleaved (a wave's U items in U different columns),
 // 3 = store-only ablation (no code loads)
 // CS > 0: columns visited in stride-CS order (logical column l -> (l mod R) CS + l div R, R =
 // ceil(m / CS)), so the columns in flight at once sit CS columns apart in the output
-template <typename T, int U, int ORD = 0, int CS = 0>
+template <typename T, int U, int ORD = 0, int CS = 0, int POL = 0>
 __global__ __launch_bounds__(kBlock) void k_decode_f(const uint8_t* __restrict__ packed, uint64_t pitch, uint64_t n,
                                                      uint64_t m, const T* __restrict__ lut, T* __restrict__ out,
                                                      uint64_t ld) {
@@ -253,7 +263,7 @@ __global__ __launch_bounds__(kBlock) void k_decode_f(const uint8_t* __restrict__
                     v.z = sel4(l0, l1, l2, l3, (byte >> 4) & 3u);
                     v.w = sel4(l0, l1, l2, l3, byte >> 6);
                     if (i + 4 <= n) {
-                        store_nt(reinterpret_cast<f32x4_t*>(o + r * 256 + 4 * lane), v);
+                        store_pol<POL>(reinterpret_cast<f32x4_t*>(o + r * 256 + 4 * lane), v);
                     } else {
                         for (int t = 0; t < 4; t++)
                             if (i + t < n) o[r * 256 + 4 * lane + t] = v[t];
@@ -1455,6 +1465,20 @@ void launch_decode(const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m
             else if (g_variant_decode == 25) k_decode_f<float, 4, 1, 16><<<g8, kBlock, 0, st>>>(packed, pitch, n, m, L, O, ld);
             else if (g_variant_decode == 26) k_decode_f<float, 4, 1, 32><<<g8, kBlock, 0, st>>>(packed, pitch, n, m, L, O, ld);
             else k_decode_f<float, 4, 1, 64><<<g8, kBlock, 0, st>>>(packed, pitch, n, m, L, O, ld);
+            SNPMI_LAUNCH_CHECK();
+            return;
+        }
+        if (dtype == SNPMI_DT_F32 && g_variant_decode >= 31 && g_variant_decode <= 35) {
+            // store cache policy on the shipped XCD-sliced order: 31 plain, 32 sc1, 33 sc0 sc1,
+            // 34 sc1 nt, 35 sc0 sc1 nt (21 = nt, shipped)
+            const unsigned g8 = (unsigned)round_up(g, 8);
+            const float* L = (const float*)lut;
+            float* O = (float*)out;
+            if (g_variant_decode == 31) k_decode_f<float, 4, 1, 0, 1><<<g8, kBlock, 0, st>>>(packed, pitch, n, m, L, O, ld);
+            else if (g_variant_decode == 32) k_decode_f<float, 4, 1, 0, 2><<<g8, kBlock, 0, st>>>(packed, pitch, n, m, L, O, ld);
+            else if (g_variant_decode == 33) k_decode_f<float, 4, 1, 0, 3><<<g8, kBlock, 0, st>>>(packed, pitch, n, m, L, O, ld);
+            else if (g_variant_decode == 34) k_decode_f<float, 4, 1, 0, 4><<<g8, kBlock, 0, st>>>(packed, pitch, n, m, L, O, ld);
+            else k_decode_f<float, 4, 1, 0, 5><<<g8, kBlock, 0, st>>>(packed, pitch, n, m, L, O, ld);
             SNPMI_LAUNCH_CHECK();
             return;
         }
