@@ -197,8 +197,9 @@ class Events:
             self.ev.append(e)
 
     def record(self, i, on_copy=0):
+        """on_copy: 0 = the calling thread's current stream, 1 = copy stream, 2 = aux stream"""
         if on_copy:
-            self.N.call("snpmi_event_record_on", self.ev[i], 1)
+            self.N.call("snpmi_event_record_on", self.ev[i], on_copy)
         else:
             self.N.call("snpmi_event_record", self.ev[i])
 
@@ -402,7 +403,11 @@ def leg_standardize(N, args, dist, n=None, n_sid=None, std=None, a=0.0, b=0.0, m
     res = dict(wall=wall, weak_wall=weak_wall, dec_mean_ms=dec_mean_ms, achieved_gbs=achieved_gbs,
                tight_gbs=tight_gbs, tight_ms=tight_ms, tight_launches=len(full) if ld != tight else launches,
                copy_gbs=copy_gbs, fill_gbs=fill_gbs, full_block_bytes=B * ((n + 3) // 4 + 4 * n), launches=launches,
-               nblk=nblk, pitch=pitch, sample=sample, gpu_cols=gpu_cols, m=m, out_ld=ld, n=n, n_sid=n_sid)
+               nblk=nblk, pitch=pitch, sample=sample, gpu_cols=gpu_cols, m=m, out_ld=ld, n=n, n_sid=n_sid,
+               steps=args.steps,
+               # whole step: k_snp_stats reads every column once, the decode reads it again and writes it
+               step_bytes=m * (2 * ((n + 3) // 4) + 4 * n))
+    N.call("snpmi_stream_sync")
     ev.destroy()
     for d in (packed, lut, stats, out):
         d.free()
@@ -1052,7 +1057,11 @@ def decode_entry(r, label):
             "kernel": "k_decode_f<float> (after k_snp_stats%s)" % label,
             "per_launch_bytes": r["full_block_bytes"], "mean_launch_ms": r["dec_mean_ms"],
             "measured_stream_GBps": {"copy_16B_nt (1 read : 1 write)": r["copy_gbs"],
-                                     "hipMemset fill (write only)": r["fill_gbs"]}}
+                                     "hipMemset fill (write only)": r["fill_gbs"]},
+            "step": {"bytes": r["step_bytes"], "achieved": r["step_bytes"] * r["steps"] / r["wall"] / 1e9,
+                     "frac": r["step_bytes"] * r["steps"] / r["wall"] / 1e9 / HBM_PEAK_GBS,
+                     "note": "whole timed step (host wall): k_snp_stats read + decode read + write of every "
+                             "column, launch gaps included"}}
 
 
 def main(argv=None):

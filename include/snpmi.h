@@ -243,6 +243,14 @@ int snpmi_event_elapsed_ms(void* start, void* stop, float* ms);
  * kind: 0 = host->device, 1 = device->host, 2 = device->device.  snpmi_stream_sync waits for
  * both streams. */
 int snpmi_memcpy_async(void* dst, const void* src, uint64_t bytes, int kind, int on_copy);
+/* on_copy above may also be 2: the aux compute stream.  snpmi_set_stream(which) makes the calling
+ * thread's stateless device calls (snpmi_dev_snp_stats / _decode / _decode_standardize /
+ * _grm_extract / _memset / _memcpy_d2d, snpmi_event_record, the RCCL calls) enqueue on the compute
+ * stream (0, the default) or on the aux stream (2), so a caller can run block k+1's stats beside
+ * block k's decode (bench.py --overlap-stats); order the two with snpmi_event_record_on /
+ * snpmi_stream_wait_event.  The file-backed and GRM-session entry points always use the compute
+ * stream. */
+int snpmi_set_stream(int which);
 int snpmi_event_record_on(void* ev, int on_copy);
 int snpmi_stream_wait_event(void* ev, int on_copy);   /* that stream waits for ev (no host wait) */
 int snpmi_event_sync(void* ev);

@@ -90,6 +90,7 @@ _SIGS = {
     "snpmi_event_elapsed_ms": [_vp, _vp, ctypes.POINTER(ctypes.c_float)],
     "snpmi_memcpy_async": [_vp, _vp, _u64, _i32, _i32],
     "snpmi_event_record_on": [_vp, _i32],
+    "snpmi_set_stream": [_i32],
     "snpmi_stream_wait_event": [_vp, _i32],
     "snpmi_event_sync": [_vp],
     "snpmi_dev_synth_bed": [_vp, _u64, _u64, _u64, _u64, _u64, _f64, _vp, _vp, _i32],

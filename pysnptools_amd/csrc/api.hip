@@ -57,6 +57,7 @@ Device& device() {
         d->id = g_cur_dev;
         SNPMI_HIP(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
         SNPMI_HIP(hipStreamCreateWithFlags(&d->copy, hipStreamNonBlocking));
+        SNPMI_HIP(hipStreamCreateWithFlags(&d->aux, hipStreamNonBlocking));
         for (hipEvent_t* set : {d->staged, d->consumed, d->produced, d->bounce})
             for (int s = 0; s < 2; s++) SNPMI_HIP(hipEventCreateWithFlags(&set[s], hipEventDisableTiming));
         SNPMI_HIP(hipEventCreateWithFlags(&d->fence, hipEventDisableTiming));
@@ -67,7 +68,12 @@ Device& device() {
     return *d;
 }
 
-hipStream_t stream() { return device().stream; }
+static thread_local int g_sel_stream = 0;  // snpmi_set_stream: 0 compute, 2 aux
+
+hipStream_t stream() {
+    Device& d = device();
+    return g_sel_stream == 2 ? d.aux : d.stream;
+}
 
 void* Device::get(Slot s, size_t bytes) {
     if (bytes == 0) bytes = 256;
@@ -1478,11 +1484,21 @@ int snpmi_stream_sync(void) {
         Device& d = device();
         SNPMI_HIP(hipStreamSynchronize(d.stream));
         SNPMI_HIP(hipStreamSynchronize(d.copy));
+        SNPMI_HIP(hipStreamSynchronize(d.aux));
+    });
+}
+
+int snpmi_set_stream(int which) {
+    return guarded([&] {
+        SNPMI_REQUIRE(which == 0 || which == 2, SNPMI_E_ARG, "stream must be 0 (compute) or 2 (aux)");
+        g_sel_stream = which;
     });
 }
 
 // ---------------------------------------------------------------------- copy stream (streaming API)
-static hipStream_t pick_stream(Device& d, int on_copy) { return on_copy ? d.copy : d.stream; }
+static hipStream_t pick_stream(Device& d, int on_copy) {
+    return on_copy == 1 ? d.copy : on_copy == 2 ? d.aux : d.stream;
+}
 
 int snpmi_memcpy_async(void* dst, const void* src, uint64_t bytes, int kind, int on_copy) {
     return guarded([&] {

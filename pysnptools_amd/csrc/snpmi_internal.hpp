@@ -64,6 +64,8 @@ struct Device {
     int id = -1;
     hipStream_t stream = nullptr;  // compute: every kernel
     hipStream_t copy = nullptr;    // DMA: host<->device copies of streamed chunks, overlapping compute
+    hipStream_t aux = nullptr;     // second compute stream (snpmi_set_stream 2): e.g. block k+1's stats
+                                   // beside block k's write-bound decode
     int cu_count = 0;
     // grow-only scratch slots
     enum Slot { S_PACKED, S_PACKED2, S_IDX, S_IDX2, S_LUT, S_STATS, S_OUT, S_TILES, S_K, S_DENSE,
@@ -86,7 +88,7 @@ struct Device {
 };
 
 Device& device();                 // current device of this thread (lazily initialised)
-hipStream_t stream();
+hipStream_t stream();  // the calling thread's current stream (compute, or aux after snpmi_set_stream(2))
 
 // pinned host staging buffers (grow-only, per thread)
 void* pinned(int slot, size_t bytes);
