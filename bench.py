@@ -101,12 +101,15 @@ def parse(argv=None):
     p.add_argument("--grm5", choices=["on", "off"], default="on", help="cfg5 partitioned-K GRM leg")
     p.add_argument("--grm5-iid", type=int, default=500_000)
     p.add_argument("--grm5-sid", type=int, default=8192)
-    p.add_argument("--out-ld", type=int, default=8_000_000,
-                   help="decode leg: leading dimension (floats) of the f32 F-order block buffer: a 32 MB column "
-                        "pitch spreads the 4 GB block over 64 GB of HBM pages (DESIGN 3.1); 0 = round_up(n, 16)")
-    p.add_argument("--out-ld-c", type=int, default=32768,
-                   help="C-order decode leg: row pitch (floats) of the output: 128 KB rows spread the 4 GB over "
-                        "64 GB of HBM pages (DESIGN 3.1); 0 = the block width")
+    p.add_argument("--out-ld", type=int, default=0,
+                   help="decode legs: leading dimension (floats) of the timed f32 F-order block buffer; 0 = "
+                        "round_up(n, 16), the tight columns the library's reads write")
+    p.add_argument("--spread-ld", type=int, default=8_000_000,
+                   help="decode legs: column pitch (floats) of the side measurement (frac_spread): a 32 MB pitch "
+                        "spreads a 4 GB block over 64 GB of HBM pages (DESIGN 3.1); 0 = no side measurement")
+    p.add_argument("--out-ld-c", type=int, default=0,
+                   help="C-order decode leg: row pitch (floats) of the output: 0 = the block width (tight rows, "
+                        "as the library writes); 32768 = 128 KB rows spread over 64 GB of HBM pages (DESIGN 3.1)")
     p.add_argument("--grm5-stream", type=int, default=2,
                    help="cfg5: blocks streamed with the next upload under the current SYRK (0 = off)")
     p.add_argument("--e2e", choices=["on", "off"], default="on", help="pinned-host -> HBM streaming leg")
@@ -118,8 +121,9 @@ def parse(argv=None):
     p.add_argument("--seed", type=int, default=5)
     p.add_argument("--force-rccl", action="store_true", help="build the RCCL communicator even at world size 1")
     p.add_argument("--dist-timeout", type=float, default=300.0, help="seconds for the RCCL id wait and init")
-    p.add_argument("--tight-reps", type=int, default=8,
-                   help="decode leg: launches timed on a tight-column buffer beside the block buffer (frac_tight)")
+    p.add_argument("--side-reps", type=int, default=8,
+                   help="decode legs: launches timed on the other column layout beside the timed steps (tight "
+                        "if --out-ld spreads the block, else --spread-ld)")
     p.add_argument("--beta", choices=["on", "off"], default="on", help="configs[2] leg: Beta(1,25) at 100k x 1M")
     p.add_argument("--beta-iid", type=int, default=100_000)
     p.add_argument("--beta-sid", type=int, default=1_000_000)
@@ -309,7 +313,7 @@ def leg_standardize(N, args, dist, n=None, n_sid=None, std=None, a=0.0, b=0.0, m
             out = None
     if out is None:
         out = Dev(N, B * ld * 4)
-    ev = Events(N, 2 + 2 * max(nblk, args.tight_reps))
+    ev = Events(N, 2 + 2 * max(nblk, args.side_reps))
     N.call("snpmi_set_kernel_variant", b"decode", args.decode_variant)
 
     def run_block(src, cnt, timed, k, dst=None, dld=None):
@@ -357,19 +361,26 @@ def leg_standardize(N, args, dist, n=None, n_sid=None, std=None, a=0.0, b=0.0, m
     # achieved = bytes of all launches / their summed time (the last block of a shard is partial)
     bytes_per_step = m * ((n + 3) // 4 + 4 * n)
     achieved_gbs = bytes_per_step * args.steps / (dec_ms_total * 1e-3) / 1e9 if dec_ms_total else 0.0
-    # the same kernel into a tight-column buffer (what Bed.read(xp='hbm') writes), full blocks only
-    tight_gbs, tight_ms = achieved_gbs, dec_mean_ms
-    full = [k for k in range(nblk) if (k + 1) * B <= m][:args.tight_reps]
-    if ld != tight and full:
-        out.free()
-        out = Dev(N, B * tight * 4)
-        for k in full[:2]:
-            run_block(packed.at(k * B * pitch), B, False, k, out, tight)
-        for i, k in enumerate(full):
-            run_block(packed.at(k * B * pitch), B, True, i, out, tight)
-        N.call("snpmi_stream_sync")
-        tight_ms = float(np.mean([ev.ms(2 + 2 * i, 3 + 2 * i) for i in range(len(full))]))
-        tight_gbs = B * ((n + 3) // 4 + 4 * n) / (tight_ms * 1e-3) / 1e9
+    # side measurement: the same kernel on the other column layout (full blocks only) -- tight columns
+    # (what Bed.read(xp='hbm') writes) when the timed buffer is spread, else the spread pitch
+    side_ld = tight if ld != tight else args.spread_ld // 16 * 16
+    side_gbs = side_ms = None
+    full = [k for k in range(nblk) if (k + 1) * B <= m][:args.side_reps]
+    if side_ld > 0 and full and (side_ld == tight or (side_ld > ld and B * tight * 4 >= WIDE_MIN_BYTES)):
+        side = None
+        try:
+            side = Dev(N, B * side_ld * 4)
+        except Exception:  # the spread layout does not fit beside the matrix: no side figure
+            side = None
+        if side is not None:
+            for k in full[:2]:
+                run_block(packed.at(k * B * pitch), B, False, k, side, side_ld)
+            for i, k in enumerate(full):
+                run_block(packed.at(k * B * pitch), B, True, i, side, side_ld)
+            N.call("snpmi_stream_sync")
+            side_ms = float(np.mean([ev.ms(2 + 2 * i, 3 + 2 * i) for i in range(len(full))]))
+            side_gbs = B * ((n + 3) // 4 + 4 * n) / (side_ms * 1e-3) / 1e9
+            side.free()
     # measured stream ceilings (untimed): device-to-device copy and write-only fill, tight bytes
     cbytes = min(B * tight * 4, pitch * m)
     N.call("snpmi_dev_memcpy_d2d", out.p, packed.p, cbytes)
@@ -386,7 +397,7 @@ def leg_standardize(N, args, dist, n=None, n_sid=None, std=None, a=0.0, b=0.0, m
     ev.record(1)
     N.call("snpmi_stream_sync")
     fill_gbs = 5 * B * tight * 4 / (ev.ms(0, 1) * 1e-3) / 1e9
-    cur_ld = tight if ld != tight and full else ld
+    cur_ld = ld  # the parity sample is decoded into the timed buffer layout
     sample = gpu_cols = None
     if dist.rank == 0 and not args.skip_cpu:
         # parity sample: the first 512 columns, re-decoded by the same kernels (untimed)
@@ -401,7 +412,7 @@ def leg_standardize(N, args, dist, n=None, n_sid=None, std=None, a=0.0, b=0.0, m
             for j in range(ncols):
                 N.call("snpmi_memcpy_d2h", N.ptr(gpu_cols[j]), out.at(j * cur_ld * 4), tight * 4)
     res = dict(wall=wall, weak_wall=weak_wall, dec_mean_ms=dec_mean_ms, achieved_gbs=achieved_gbs,
-               tight_gbs=tight_gbs, tight_ms=tight_ms, tight_launches=len(full) if ld != tight else launches,
+               side_ld=side_ld, side_gbs=side_gbs, side_ms=side_ms, side_launches=len(full), tight=tight,
                copy_gbs=copy_gbs, fill_gbs=fill_gbs, full_block_bytes=B * ((n + 3) // 4 + 4 * n), launches=launches,
                nblk=nblk, pitch=pitch, sample=sample, gpu_cols=gpu_cols, m=m, out_ld=ld, n=n, n_sid=n_sid,
                steps=args.steps,
@@ -1048,12 +1059,20 @@ def leg_file(N, args):
 
 def decode_entry(r, label):
     """The decode leg's roofline object (k_decode_f<float>, HBM bound)."""
+    timed_tight = r["out_ld"] == r["tight"]
+    side = {"achieved": r["side_gbs"], "frac": r["side_gbs"] / HBM_PEAK_GBS if r["side_gbs"] else None,
+            "mean_launch_ms": r["side_ms"], "ld": r["side_ld"],
+            "note": "the same kernel, %d full-block launches in the same process, into a block buffer with %s"
+                    % (r["side_launches"], "tight columns (ld = round_up(n,16), what Bed.read(xp='hbm') writes)"
+                       if not timed_tight else "a %d-float (%d MB) column pitch (the block spread over that many times "
+                       "more HBM pages, DESIGN.md 3.1)" % (r["side_ld"], r["side_ld"] * 4 >> 20))}
     return {"bound": "hbm", "achieved": r["achieved_gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": r["achieved_gbs"] / HBM_PEAK_GBS,
-            "frac_tight": r["tight_gbs"] / HBM_PEAK_GBS, "achieved_tight": r["tight_gbs"],
-            "mean_launch_ms_tight": r["tight_ms"],
-            "tight_note": "the same kernel writing a tight-column buffer (ld = round_up(n,16), what Bed.read(xp='hbm') "
-                          "writes), %d full-block launches, same process" % r["tight_launches"],
+            "layout": "tight columns (ld = round_up(n,16), the library's read layout)" if timed_tight else
+                      "column pitch %d floats" % r["out_ld"],
+            "frac_tight": r["achieved_gbs"] / HBM_PEAK_GBS if timed_tight else side["frac"],
+            "frac_spread": side["frac"] if timed_tight else r["achieved_gbs"] / HBM_PEAK_GBS,
+            "side": side,
             "kernel": "k_decode_f<float> (after k_snp_stats%s)" % label,
             "per_launch_bytes": r["full_block_bytes"], "mean_launch_ms": r["dec_mean_ms"],
             "measured_stream_GBps": {"copy_16B_nt (1 read : 1 write)": r["copy_gbs"],

@@ -122,6 +122,7 @@ def test_bench_with_rccl_communicator_world1(collective):
     d = json.loads(lines[0])
     assert d["n_gpus"] == 1 and d["value"] > 0 and d["parity"]["bit_exact"]
     assert 0 < d["roofline"]["frac_tight"] and d["cpu_baseline"]["cpu_counts"]["usable"] >= 1
+    assert d["roofline"]["layout"].startswith("tight") and d["roofline"]["frac"] == d["roofline"]["frac_tight"]
     assert d["beta"]["parity"]["pass"] and d["beta"]["snps_per_s"] > 0, d["beta"]
     f = d["file"]
     assert f["read_kernel_f32"]["parity"]["pass"], f["read_kernel_f32"]["parity"]
@@ -139,15 +140,18 @@ def test_bench_with_rccl_communicator_world1(collective):
 
 
 def test_decode_leg_wide_block_buffer_same_values():
-    """The decode leg's 32 MB-pitch block buffer (--out-ld 8000000, used for blocks >= 1 GB) holds
-    the same values as tight columns: 131072 iids x 2048-SNP blocks (1 GB), first 512 columns
-    compared bit for bit, and against the oracle's decode + one-pass Unit."""
+    """A 32 MB-pitch block buffer (--out-ld 8000000; the default timed layout is tight, the spread
+    pitch is the side figure) holds the same values as tight columns: 131072 iids x 2048-SNP blocks
+    (1 GB), first 512 columns compared bit for bit, and against the oracle's decode + one-pass Unit;
+    each run times the other layout on the side."""
     from oracle import oracle as O
 
     base = ["--n-iid", "131072", "--n-sid", "4096", "--block", "2048", "--steps", "1", "--warmup", "0"]
     wide = bench.leg_standardize(N, bench.parse(base + ["--out-ld", "8000000"]), FakeDist(0, 1))
     tight = bench.leg_standardize(N, bench.parse(base + ["--out-ld", "0"]), FakeDist(0, 1))
     assert wide["out_ld"] == 8_000_000 and tight["out_ld"] == 131072
+    assert wide["side_ld"] == 131072 and tight["side_ld"] == 8_000_000
+    assert wide["side_gbs"] > 0 and tight["side_gbs"] > 0
     assert np.array_equal(wide["gpu_cols"], tight["gpu_cols"])
     n, ncols = 131072, wide["gpu_cols"].shape[0]
     body = np.ascontiguousarray(wide["sample"][:, :(n + 3) // 4]).reshape(-1)
