@@ -308,6 +308,313 @@ __global__ __launch_bounds__(kBlock) void k_decode_f(const uint8_t* __restrict__
     }
 }
 
+#ifdef SNPMI_UBENCH
+// ubench A/B of the write window (f32): items of RN x 256 iids, U items per wave, so the resident
+// waves' stores cover ~8192 x U x RN KiB of the output at once (hipMemset's fill sweeps ~8 MB;
+// k_decode_f<.,4> 128 MB)
+template <int RN, int U, int ORD>
+__global__ __launch_bounds__(kBlock) void k_decode_fine(const uint8_t* __restrict__ packed, uint64_t pitch, uint64_t n,
+                                                        uint64_t m, const float* __restrict__ lut, float* __restrict__ out,
+                                                        uint64_t ld) {
+    constexpr int IIDS = RN * 256;
+    const int lane = threadIdx.x & (kWave - 1);
+    const uint64_t chunks = (n + IIDS - 1) / IIDS, total = chunks * m, groups = (total + U - 1) / U;
+    const uint64_t nwaves = (uint64_t)gridDim.x * (kBlock / kWave);
+    uint64_t lb = blockIdx.x;
+    if constexpr (ORD == 1) lb = (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
+    for (uint64_t gi = lb * (kBlock / kWave) + threadIdx.x / kWave; gi < groups; gi += nwaves) {
+        uint32_t w[U];
+        uint64_t jv[U], cv[U];
+        bool val[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const uint64_t it = gi * U + u;
+            const uint64_t j = it / chunks, c = it - j * chunks;
+            jv[u] = j;
+            cv[u] = c;
+            val[u] = it < total;
+            const bool ok = val[u] && lane < 16 * RN && (c * IIDS + 16 * (uint64_t)lane < n);
+            w[u] = ok ? reinterpret_cast<const uint32_t*>(packed + j * pitch)[c * (16 * RN) + lane] : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            if (!val[u]) continue;
+            const uint64_t j = jv[u], i0 = cv[u] * IIDS;
+            const float l0 = lut[4 * j], l1 = lut[4 * j + 1], l2 = lut[4 * j + 2], l3 = lut[4 * j + 3];
+            float* o = out + j * ld + i0;
+#pragma unroll
+            for (int r = 0; r < RN; r++) {
+                const uint32_t src = __shfl(w[u], r * 16 + (lane >> 2), kWave);
+                const uint32_t byte = (src >> (8 * (lane & 3))) & 0xffu;
+                const uint64_t i = i0 + r * 256 + 4 * lane;
+                f32x4_t v;
+                v.x = sel4(l0, l1, l2, l3, byte & 3u);
+                v.y = sel4(l0, l1, l2, l3, (byte >> 2) & 3u);
+                v.z = sel4(l0, l1, l2, l3, (byte >> 4) & 3u);
+                v.w = sel4(l0, l1, l2, l3, byte >> 6);
+                if (i + 4 <= n) {
+                    store_nt(reinterpret_cast<f32x4_t*>(o + r * 256 + 4 * lane), v);
+                } else {
+                    for (int t = 0; t < 4; t++)
+                        if (i + t < n) o[r * 256 + 4 * lane + t] = v[t];
+                }
+            }
+        }
+    }
+}
+
+// ubench: hipMemset-shaped sweep (the ROCclr fill runs 0.60-0.63 ms per 4 GB on every buffer, the
+// decode 0.61-0.77 by placement): a persistent grid of G workgroups, items of 256 iids (1 KiB of
+// output) interleaved across waves -- store u of batch b of every wave lands in the contiguous
+// window of items (b U + u) nwaves .. +nwaves -- and the next batch's code dwords loaded before
+// the current batch's stores
+template <int U>
+__global__ __launch_bounds__(kBlock) void k_decode_sweep(const uint8_t* __restrict__ packed, uint64_t pitch, uint64_t n,
+                                                         uint64_t m, const float* __restrict__ lut, float* __restrict__ out,
+                                                         uint64_t ld) {
+    const int lane = threadIdx.x & (kWave - 1);
+    const uint64_t chunks = (n + 255) / 256, total = chunks * m;
+    const uint64_t nwaves = (uint64_t)gridDim.x * (kBlock / kWave);
+    const uint64_t wv = (uint64_t)blockIdx.x * (kBlock / kWave) + threadIdx.x / kWave;
+    auto load = [&](uint64_t it) -> uint32_t {
+        if (it >= total) return 0u;
+        const uint64_t j = it / chunks, c = it - j * chunks;
+        const bool ok = lane < 16 && c * 256 + 16 * (uint64_t)lane < n;
+        return ok ? reinterpret_cast<const uint32_t*>(packed + j * pitch)[c * 16 + lane] : 0u;
+    };
+    uint32_t w[U], wn[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) w[u] = load((uint64_t)u * nwaves + wv);
+    for (uint64_t b = 0; b * U * nwaves + wv < total; b++) {
+#pragma unroll
+        for (int u = 0; u < U; u++) wn[u] = load(((b + 1) * U + u) * nwaves + wv);
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const uint64_t it = (b * U + u) * nwaves + wv;
+            if (it >= total) break;
+            const uint64_t j = it / chunks, i0 = (it - j * chunks) * 256;
+            const float l0 = lut[4 * j], l1 = lut[4 * j + 1], l2 = lut[4 * j + 2], l3 = lut[4 * j + 3];
+            const uint32_t src = __shfl(w[u], lane >> 2, kWave);
+            const uint32_t byte = (src >> (8 * (lane & 3))) & 0xffu;
+            const uint64_t i = i0 + 4 * lane;
+            f32x4_t v;
+            v.x = sel4(l0, l1, l2, l3, byte & 3u);
+            v.y = sel4(l0, l1, l2, l3, (byte >> 2) & 3u);
+            v.z = sel4(l0, l1, l2, l3, (byte >> 4) & 3u);
+            v.w = sel4(l0, l1, l2, l3, byte >> 6);
+            float* o = out + j * ld + i;
+            if (i + 4 <= n) {
+                store_nt(reinterpret_cast<f32x4_t*>(o), v);
+            } else {
+                for (int t = 0; t < 4; t++)
+                    if (i + t < n) o[t] = v[t];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) w[u] = wn[u];
+    }
+}
+
+// ubench: the sweep with 16 items per wave and batch, one load instruction per 4 items (lane l
+// fetches dword l&15 of item 4q + l/16), next batch prefetched (32 items = 32 KiB in flight per
+// wave); NOLOAD = store-only ablation of the same pattern
+template <bool NOLOAD>
+__global__ __launch_bounds__(kBlock) void k_decode_sweep16(const uint8_t* __restrict__ packed, uint64_t pitch, uint64_t n,
+                                                           uint64_t m, const float* __restrict__ lut,
+                                                           float* __restrict__ out, uint64_t ld) {
+    constexpr int U = 16, Q = U / 4;
+    const int lane = threadIdx.x & (kWave - 1);
+    const uint64_t chunks = (n + 255) / 256, total = chunks * m;
+    const uint64_t nwaves = (uint64_t)gridDim.x * (kBlock / kWave);
+    const uint64_t wv = (uint64_t)blockIdx.x * (kBlock / kWave) + threadIdx.x / kWave;
+    auto load = [&](uint64_t b, int q) -> uint32_t {
+        const uint64_t it = (b * U + 4 * q + (lane >> 4)) * nwaves + wv;
+        if (NOLOAD || it >= total) return (uint32_t)lane * 0x9E3779B9u;
+        const uint64_t j = it / chunks, c = it - j * chunks;
+        const int d = lane & 15;
+        return c * 256 + 16 * (uint64_t)d < n ? reinterpret_cast<const uint32_t*>(packed + j * pitch)[c * 16 + d] : 0u;
+    };
+    uint32_t w[Q], wn[Q];
+#pragma unroll
+    for (int q = 0; q < Q; q++) w[q] = load(0, q);
+    for (uint64_t b = 0; b * U * nwaves + wv < total; b++) {
+#pragma unroll
+        for (int q = 0; q < Q; q++) wn[q] = load(b + 1, q);
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const uint64_t it = (b * U + u) * nwaves + wv;
+            if (it >= total) break;
+            const uint64_t j = it / chunks, i0 = (it - j * chunks) * 256;
+            const float l0 = lut[4 * j], l1 = lut[4 * j + 1], l2 = lut[4 * j + 2], l3 = lut[4 * j + 3];
+            const uint32_t src = __shfl(w[u >> 2], (u & 3) * 16 + (lane >> 2), kWave);
+            const uint32_t byte = (src >> (8 * (lane & 3))) & 0xffu;
+            const uint64_t i = i0 + 4 * lane;
+            f32x4_t v;
+            v.x = sel4(l0, l1, l2, l3, byte & 3u);
+            v.y = sel4(l0, l1, l2, l3, (byte >> 2) & 3u);
+            v.z = sel4(l0, l1, l2, l3, (byte >> 4) & 3u);
+            v.w = sel4(l0, l1, l2, l3, byte >> 6);
+            float* o = out + j * ld + i;
+            if (i + 4 <= n) {
+                store_nt(reinterpret_cast<f32x4_t*>(o), v);
+            } else {
+                for (int t = 0; t < 4; t++)
+                    if (i + t < n) o[t] = v[t];
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < Q; q++) w[q] = wn[q];
+    }
+}
+
+// sweep16 without per-item divisions or dependent LUT loads: (column, chunk) of the wave's k-th
+// item advanced incrementally (item k+1 = item k + nwaves), the batch's 16 LUT rows fetched with
+// its codes (lane l: entry l&3 of item l>>2) and broadcast by v_readlane
+template <bool NOLOAD>
+__global__ __launch_bounds__(kBlock) void k_decode_sweep16b(const uint8_t* __restrict__ packed, uint64_t pitch,
+                                                            uint64_t n, uint64_t m, const float* __restrict__ lut,
+                                                            float* __restrict__ out, uint64_t ld) {
+    constexpr int U = 16, Q = U / 4;
+    const int lane = threadIdx.x & (kWave - 1);
+    const uint64_t chunks = (n + 255) / 256, total = chunks * m;
+    const uint64_t nwaves = (uint64_t)gridDim.x * (kBlock / kWave);
+    const uint64_t wv = (uint64_t)blockIdx.x * (kBlock / kWave) + threadIdx.x / kWave;
+    const uint64_t dj = nwaves / chunks, dc = nwaves - dj * chunks;              // one item step
+    const uint64_t bstep = U * nwaves, dJ = bstep / chunks, dC = bstep - dJ * chunks;  // one batch step
+    auto split = [&](uint64_t it, uint64_t& j, uint64_t& c) {
+        j = it / chunks;
+        c = it - j * chunks;
+    };
+    auto adv = [&](uint64_t& j, uint64_t& c, uint64_t aj, uint64_t ac) {
+        c += ac;
+        j += aj;
+        if (c >= chunks) {
+            c -= chunks;
+            j++;
+        }
+    };
+    // per-lane item states: codes (q: item 4q + lane/16 of the batch), LUT (item lane/4)
+    uint64_t jq[Q], cq[Q], jl, cl;
+#pragma unroll
+    for (int q = 0; q < Q; q++) split((uint64_t)(4 * q + (lane >> 4)) * nwaves + wv, jq[q], cq[q]);
+    split((uint64_t)(lane >> 2) * nwaves + wv, jl, cl);
+    const int d = lane & 15;
+    auto load_codes = [&](int q) -> uint32_t {
+        if (NOLOAD || jq[q] >= m) return (uint32_t)lane * 0x9E3779B9u;
+        return cq[q] * 256 + 16 * (uint64_t)d < n ? reinterpret_cast<const uint32_t*>(packed + jq[q] * pitch)[cq[q] * 16 + d]
+                                                  : 0u;
+    };
+    auto load_lut = [&]() -> float { return jl < m ? lut[4 * jl + (lane & 3)] : 0.0f; };
+    uint32_t w[Q], wn[Q];
+    float lv = load_lut(), lvn;
+#pragma unroll
+    for (int q = 0; q < Q; q++) w[q] = load_codes(q);
+    uint64_t js, cs;  // the wave's current item (uniform)
+    split(wv, js, cs);
+    for (uint64_t b = 0; b * bstep + wv < total; b++) {
+#pragma unroll
+        for (int q = 0; q < Q; q++) {
+            adv(jq[q], cq[q], dJ, dC);
+            wn[q] = load_codes(q);
+        }
+        adv(jl, cl, dJ, dC);
+        lvn = load_lut();
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            if (js >= m) break;
+            const float l0 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, lv), 4 * u));
+            const float l1 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, lv), 4 * u + 1));
+            const float l2 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, lv), 4 * u + 2));
+            const float l3 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, lv), 4 * u + 3));
+            const uint32_t src = __shfl(w[u >> 2], (u & 3) * 16 + (lane >> 2), kWave);
+            const uint32_t byte = (src >> (8 * (lane & 3))) & 0xffu;
+            const uint64_t i = cs * 256 + 4 * lane;
+            f32x4_t v;
+            v.x = sel4(l0, l1, l2, l3, byte & 3u);
+            v.y = sel4(l0, l1, l2, l3, (byte >> 2) & 3u);
+            v.z = sel4(l0, l1, l2, l3, (byte >> 4) & 3u);
+            v.w = sel4(l0, l1, l2, l3, byte >> 6);
+            float* o = out + js * ld + i;
+            if (i + 4 <= n) {
+                store_nt(reinterpret_cast<f32x4_t*>(o), v);
+            } else {
+                for (int t = 0; t < 4; t++)
+                    if (i + t < n) o[t] = v[t];
+            }
+            adv(js, cs, dj, dc);
+        }
+#pragma unroll
+        for (int q = 0; q < Q; q++) w[q] = wn[q];
+        lv = lvn;
+    }
+}
+
+// sweep, lean form: the wave's item state is wave-uniform (SGPRs via readfirstlane), each lane
+// loads its own code byte (64 lanes x 1 B = the item's 64 B, no shuffle), the item's LUT row is a
+// scalar load, U items per batch with the next batch's loads issued before this batch's stores
+template <bool NOLOAD, int U>
+__global__ __launch_bounds__(kBlock) void k_decode_sweepc(const uint8_t* __restrict__ packed, uint64_t pitch,
+                                                          uint64_t n, uint64_t m, const float* __restrict__ lut,
+                                                          float* __restrict__ out, uint64_t ld) {
+    const int lane = threadIdx.x & (kWave - 1);
+    const uint64_t chunks = (n + 255) / 256, total = chunks * m;
+    const uint64_t nwaves = (uint64_t)gridDim.x * (kBlock / kWave);
+    const uint64_t wv = (uint64_t)__builtin_amdgcn_readfirstlane(blockIdx.x * (kBlock / kWave) + threadIdx.x / kWave);
+    const uint64_t dj = nwaves / chunks, dc = nwaves - dj * chunks;
+    uint64_t jl = wv / chunks, cl = wv - jl * chunks, js = jl, cs = cl;
+    auto adv = [&](uint64_t& j, uint64_t& c) {
+        c += dc;
+        j += dj;
+        if (c >= chunks) {
+            c -= chunks;
+            j++;
+        }
+    };
+    uint32_t code[U], coden[U];
+    float4 L[U], Ln[U];
+    auto fetch = [&](uint32_t (&cd)[U], float4 (&lt)[U]) {
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const bool ok = jl < m;
+            const uint64_t jj = ok ? jl : 0;
+            lt[u] = *reinterpret_cast<const float4*>(lut + 4 * jj);
+            if (NOLOAD) cd[u] = (uint32_t)lane * 37u;
+            else cd[u] = ok && cl * 256 + 4 * (uint64_t)lane < n ? packed[jj * pitch + cl * 64 + lane] : 0u;
+            adv(jl, cl);
+        }
+    };
+    fetch(code, L);
+    for (uint64_t k = 0; js < m; k += U) {
+        fetch(coden, Ln);
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            if (js >= m) break;
+            const uint32_t byte = code[u];
+            const uint64_t i = cs * 256 + 4 * lane;
+            f32x4_t v;
+            v.x = sel4(L[u].x, L[u].y, L[u].z, L[u].w, byte & 3u);
+            v.y = sel4(L[u].x, L[u].y, L[u].z, L[u].w, (byte >> 2) & 3u);
+            v.z = sel4(L[u].x, L[u].y, L[u].z, L[u].w, (byte >> 4) & 3u);
+            v.w = sel4(L[u].x, L[u].y, L[u].z, L[u].w, byte >> 6);
+            float* o = out + js * ld + i;
+            if (i + 4 <= n) {
+                store_nt(reinterpret_cast<f32x4_t*>(o), v);
+            } else {
+                for (int t = 0; t < 4; t++)
+                    if (i + t < n) o[t] = v[t];
+            }
+            adv(js, cs);
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            code[u] = coden[u];
+            L[u] = Ln[u];
+        }
+    }
+    (void)total;
+}
+#endif
+
 // Fused stats + decode, one workgroup per SNP column (large N): pass 1 counts the codes
 // (packed column read once from HBM), the LUT is built in f64 by one lane, pass 2 re-reads
 // the column (L2 / Infinity-Cache resident) and streams the values out with non-temporal
@@ -1465,6 +1772,72 @@ void launch_decode(const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m
             else if (g_variant_decode == 25) k_decode_f<float, 4, 1, 16><<<g8, kBlock, 0, st>>>(packed, pitch, n, m, L, O, ld);
             else if (g_variant_decode == 26) k_decode_f<float, 4, 1, 32><<<g8, kBlock, 0, st>>>(packed, pitch, n, m, L, O, ld);
             else k_decode_f<float, 4, 1, 64><<<g8, kBlock, 0, st>>>(packed, pitch, n, m, L, O, ld);
+            SNPMI_LAUNCH_CHECK();
+            return;
+        }
+        if (dtype == SNPMI_DT_F32 && g_variant_decode >= 70 && g_variant_decode <= 76) {
+            // 70/71: store-only sweepc on 256/1024 workgroups; 72-75: sweepc<8> on 256..2048; 76: sweepc<16> 512
+            const float* L = (const float*)lut;
+            float* O = (float*)out;
+            const int v = g_variant_decode;
+            if (v == 70) k_decode_sweepc<true, 8><<<256, kBlock, 0, st>>>(packed, pitch, n, m, L, O, ld);
+            else if (v == 71) k_decode_sweepc<true, 8><<<1024, kBlock, 0, st>>>(packed, pitch, n, m, L, O, ld);
+            else if (v == 76) k_decode_sweepc<false, 16><<<512, kBlock, 0, st>>>(packed, pitch, n, m, L, O, ld);
+            else k_decode_sweepc<false, 8><<<256u << (v - 72), kBlock, 0, st>>>(packed, pitch, n, m, L, O, ld);
+            SNPMI_LAUNCH_CHECK();
+            return;
+        }
+        if (dtype == SNPMI_DT_F32 && g_variant_decode >= 64 && g_variant_decode <= 69) {
+            // 64/65: store-only sweep16b on 256/1024 workgroups; 66-69: sweep16b on 256/512/1024/2048
+            const float* L = (const float*)lut;
+            float* O = (float*)out;
+            const int v = g_variant_decode;
+            if (v == 64) k_decode_sweep16b<true><<<256, kBlock, 0, st>>>(packed, pitch, n, m, L, O, ld);
+            else if (v == 65) k_decode_sweep16b<true><<<1024, kBlock, 0, st>>>(packed, pitch, n, m, L, O, ld);
+            else k_decode_sweep16b<false><<<256u << (v - 66), kBlock, 0, st>>>(packed, pitch, n, m, L, O, ld);
+            SNPMI_LAUNCH_CHECK();
+            return;
+        }
+        if (dtype == SNPMI_DT_F32 && g_variant_decode >= 58 && g_variant_decode <= 63) {
+            // 58/59: store-only sweep on 256/1024 workgroups; 60-63: sweep16 on 256/512/1024/2048
+            const float* L = (const float*)lut;
+            float* O = (float*)out;
+            const int v = g_variant_decode;
+            if (v == 58) k_decode_sweep16<true><<<256, kBlock, 0, st>>>(packed, pitch, n, m, L, O, ld);
+            else if (v == 59) k_decode_sweep16<true><<<1024, kBlock, 0, st>>>(packed, pitch, n, m, L, O, ld);
+            else k_decode_sweep16<false><<<256u << (v - 60), kBlock, 0, st>>>(packed, pitch, n, m, L, O, ld);
+            SNPMI_LAUNCH_CHECK();
+            return;
+        }
+        if (dtype == SNPMI_DT_F32 && g_variant_decode >= 50 && g_variant_decode <= 57) {
+            // hipMemset-shaped sweep (k_decode_sweep<U>) on G workgroups
+            const float* L = (const float*)lut;
+            float* O = (float*)out;
+            const int v = g_variant_decode;
+            const unsigned G = v == 50 || v == 53 ? 256 : v == 51 || v == 56 ? 512 : v == 52 || v == 54 ? 1024 : 2048;
+            if (v == 50 || v == 51 || v == 52) k_decode_sweep<4><<<G, kBlock, 0, st>>>(packed, pitch, n, m, L, O, ld);
+            else if (v == 53 || v == 56) k_decode_sweep<8><<<G, kBlock, 0, st>>>(packed, pitch, n, m, L, O, ld);
+            else k_decode_sweep<2><<<G, kBlock, 0, st>>>(packed, pitch, n, m, L, O, ld);
+            SNPMI_LAUNCH_CHECK();
+            return;
+        }
+        if (dtype == SNPMI_DT_F32 && g_variant_decode >= 40 && g_variant_decode <= 47) {
+            // write-window A/B (k_decode_fine<RN, U, ORD>)
+            const float* L = (const float*)lut;
+            float* O = (float*)out;
+            const int v = g_variant_decode;
+            const int rn = (v == 40 || v == 41 || v == 44 || v == 46) ? 1 : (v == 42 ? 2 : 4);
+            const int u = (v == 40 || v == 43 || v == 44) ? 1 : (v == 42 || v == 47) ? 2 : (v == 46 ? 8 : 4);
+            const uint64_t items = ceil_div(n, (uint64_t)rn * 256) * m;
+            const unsigned gg = (unsigned)round_up(grid_for(ceil_div(items, (uint64_t)u), kBlock / kWave, 256 * 16 * 8), 8);
+            if (v == 40) k_decode_fine<1, 1, 1><<<gg, kBlock, 0, st>>>(packed, pitch, n, m, L, O, ld);
+            else if (v == 41) k_decode_fine<1, 4, 1><<<gg, kBlock, 0, st>>>(packed, pitch, n, m, L, O, ld);
+            else if (v == 42) k_decode_fine<2, 2, 1><<<gg, kBlock, 0, st>>>(packed, pitch, n, m, L, O, ld);
+            else if (v == 43) k_decode_fine<4, 1, 1><<<gg, kBlock, 0, st>>>(packed, pitch, n, m, L, O, ld);
+            else if (v == 44) k_decode_fine<1, 1, 0><<<gg, kBlock, 0, st>>>(packed, pitch, n, m, L, O, ld);
+            else if (v == 45) k_decode_fine<4, 4, 0><<<gg, kBlock, 0, st>>>(packed, pitch, n, m, L, O, ld);
+            else if (v == 46) k_decode_fine<1, 8, 1><<<gg, kBlock, 0, st>>>(packed, pitch, n, m, L, O, ld);
+            else k_decode_fine<4, 2, 1><<<gg, kBlock, 0, st>>>(packed, pitch, n, m, L, O, ld);
             SNPMI_LAUNCH_CHECK();
             return;
         }

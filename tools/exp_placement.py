@@ -76,13 +76,34 @@ def main():
     N.call("snpmi_stream_sync")
     for r in range(a.rounds):
         for name, q, v, l in cases:
-            N.call("snpmi_set_kernel_variant", b"decode", v)
+            if v >= 0:
+                N.call("snpmi_set_kernel_variant", b"decode", v)
             ev.record(0)
             for _ in range(a.reps):
-                N.call("snpmi_dev_decode", packed.p, pitch, n, B, lut.p, N.DT_F32, 0, q, l)
+                if v < 0:  # variant -1: hipMemset of the same bytes (the fill ceiling on this buffer)
+                    N.call("snpmi_dev_memset", q, 0, B * l * 4)
+                else:
+                    N.call("snpmi_dev_decode", packed.p, pitch, n, B, lut.p, N.DT_F32, 0, q, l)
             ev.record(1)
             N.call("snpmi_stream_sync")
             times[(name, v, l)].append(ev.ms(0, 1) / a.reps)
+    # parity: every variant's output (first, middle, last column of the first buffer) equals the
+    # shipped kernel's
+    q0 = bufs[0][1]
+    ref = None
+    cols = [0, B // 2, B - 1]
+    for v in [0] + [x for x in variants if x >= 0 and x not in (23, 58, 59, 64, 65, 70, 71)]:  # store-only ablations
+        N.call("snpmi_set_kernel_variant", b"decode", v)
+        N.call("snpmi_dev_memset", q0, 0, B * ld * 4)
+        N.call("snpmi_dev_decode", packed.p, pitch, n, B, lut.p, N.DT_F32, 0, q0, ld)
+        got = np.empty((len(cols), n), dtype=np.float32)
+        for i, c in enumerate(cols):
+            N.call("snpmi_memcpy_d2h", N.ptr(got[i]), ctypes.c_void_p(q0.value + c * ld * 4), n * 4)
+        if ref is None:
+            ref = got
+        elif not np.array_equal(got, ref):
+            print(json.dumps({"variant": v, "parity": False}), flush=True)
+            raise SystemExit(1)
     N.call("snpmi_set_kernel_variant", b"decode", 0)
     nbytes = B * ((n + 3) // 4 + 4 * n)
     for name, q, v, l in cases:
