@@ -761,8 +761,8 @@ def leg_grm5(N, args, dist):
     ev.record(0)
     N.call("snpmi_memcpy_async", mine, host, ms * pitch, 0, 0)
     ev.record(1)
-    if dist.rccl:
-        N.call("snpmi_rccl_allgather", mine, packed.p, ms * pitch)
+    if dist.rccl or dist.world > 1:
+        dist.allgather_dev(mine, packed.p, ms * pitch)
     ev.record(2)
     N.call("snpmi_dev_snp_stats", packed.p, pitch, n, m, 0, N.STD_UNIT, 0.0, 0.0, 0, N.DT_F32, stats.p, lut.p)
     N.call("snpmi_dev_syrk_packed_part", packed.p, pitch, n, m, lut.p, dist.rank, P, blocks.p, 0)
@@ -827,8 +827,8 @@ def grm5_stream(N, args, dist, host, packed, lut, stats, blocks, n, m, ms, pitch
         buf = bufs[k % 2]
         N.call("snpmi_stream_wait_event", up.ev[k], 0)
         ce.record(2 * k)
-        if dist.rccl:
-            N.call("snpmi_rccl_allgather", buf.at(dist.rank * ms * pitch), buf.p, ms * pitch)
+        if dist.rccl or dist.world > 1:
+            dist.allgather_dev(buf.at(dist.rank * ms * pitch), buf.p, ms * pitch)
         N.call("snpmi_dev_snp_stats", buf.p, pitch, n, m, 0, N.STD_UNIT, 0.0, 0.0, 0, N.DT_F32, stats.p, lut.p)
         N.call("snpmi_dev_syrk_packed_part", buf.p, pitch, n, m, lut.p, dist.rank, P, blocks.p, int(k > 0))
         ce.record(2 * k + 1)
@@ -1100,7 +1100,10 @@ def main(argv=None):
     from pysnptools_amd import dist as D
 
     try:
-        dist = D.init_from_env(force_rccl=args.force_rccl, timeout=args.dist_timeout)
+        # not the "current" group: bench.py times its legs explicitly, and rank 0's file leg calls
+        # Bed.read_kernel alone -- routed through the group it would wait in an all-reduce the other
+        # ranks never join
+        dist = D.init_from_env(force_rccl=args.force_rccl, timeout=args.dist_timeout, set_current=False)
     except TimeoutError as e:  # a stuck RCCL init cannot be cancelled: leave at once, non-zero
         sys.stderr.write("bench.py: %s\n" % e)
         sys.stderr.flush()
@@ -1132,7 +1135,8 @@ def main(argv=None):
                             "blocks in %d parts (the 8-GPU plan), this process = part %d; the packed block comes "
                             "from pinned host memory inside the timed region (%d upload(s) of %d SNPs%s), no "
                             "reduction" % (n5, m5, P, dist.rank, 1, r3["ms"],
-                                           " + RCCL all-gather" if dist.rccl else ""),
+                                           " + RCCL all-gather" if dist.rccl else
+                                           (" + host all-gather (rehearsal group)" if dist.world > 1 else "")),
                 "h2d_ms": r3["h2d_ms"], "h2d_GBps": r3["ms"] * r3["pitch"] / (r3["h2d_ms"] * 1e-3) / 1e9,
                 "allgather_ms": r3["allgather_ms"], "syrk_ms": r3["syrk_ms"], "syrk_tflops": syrk_tf,
                 "seconds": r3["wall"], "gflops_per_gpu": flops_part / r3["wall"] / 1e9,
@@ -1205,7 +1209,10 @@ def main(argv=None):
                                    % (n, args.n_sid, dist.world, args.block, r1["out_ld"]),
                        "n_iid": n, "n_sid": args.n_sid, "n_sid_per_gpu": r1["m"], "block": args.block,
                        "block_buffer_ld": r1["out_ld"],
-                       "parallelism": "snp-shard x%d" % dist.world},
+                       "parallelism": "snp-shard x%d" % dist.world,
+                       "process_group": "rccl" if dist.rccl else ("host rehearsal (SNPMI_DIST_HOST: gloo barriers, "
+                                                                  "ranks share one GPU, no device reduce)"
+                                                                  if dist.world > 1 else "none")},
             "weak": ({"value": args.n_sid * args.steps * dist.world / r1["weak_wall"], "unit": "SNPs/s",
                       "workload": "every rank streams 1M SNPs per step (its shard %d times)" % dist.world}
                      if r1["weak_wall"] else None),

@@ -23,6 +23,8 @@ node-local file; barriers and max-over-ranks are RCCL all-reduces.
 import contextlib
 import ctypes
 import os
+import socket
+import struct
 import tempfile
 import threading
 import time
@@ -177,6 +179,17 @@ class Dist(object):
             N.call("snpmi_dev_free", dev)
         return buf.astype(np.asarray(arr).dtype)
 
+    def allgather_dev(self, send, recv, nbytes):
+        """Device all-gather of ``nbytes`` per rank: rank r's ``send`` lands at ``recv + r*nbytes``
+        on every rank (ncclAllGather; in place when ``send`` is that slot of ``recv``)."""
+        if not self.rccl:
+            if self.world > 1:
+                raise RuntimeError("an all-gather over %d ranks needs an RCCL communicator" % self.world)
+            return
+        from pysnptools_amd import _native as N
+
+        N.call("snpmi_rccl_allgather", send, recv, int(nbytes))
+
     def close(self):
         global _CURRENT
         if self._closed:
@@ -189,12 +202,126 @@ class Dist(object):
 
             with stdout_to_stderr():
                 N.call("snpmi_rccl_destroy")
+        self._close_host()
+
+    def _close_host(self):
+        pass
 
     def __enter__(self):
         return self
 
     def __exit__(self, *exc):
         self.close()
+
+
+def _send_frame(sock, payload):
+    sock.sendall(struct.pack("<Q", len(payload)) + payload)
+
+
+def _recv_exact(sock, n):
+    buf = bytearray()
+    while len(buf) < n:
+        chunk = sock.recv(min(n - len(buf), 1 << 20))
+        if not chunk:
+            raise ConnectionError("rehearsal group: a rank closed its connection")
+        buf += chunk
+    return bytes(buf)
+
+
+def _recv_frame(sock):
+    (n,) = struct.unpack("<Q", _recv_exact(sock, 8))
+    return _recv_exact(sock, n)
+
+
+class HostDist(Dist):
+    """Rehearsal process group (``SNPMI_DIST_HOST=1``): the rank layout, barriers, max-over-ranks,
+    host sums and device all-gathers of a world > 1 job, staged through host memory over local TCP
+    sockets (rank 0 relays; its ephemeral port is handed over through the node-local id file, as
+    the RCCL id is), with every rank free to share ONE GPU.  No RCCL, so device collectives of GRM
+    tiles are unavailable (``ShardedGrm`` refuses a reduce without RCCL; bench.py's legs use
+    collective "none").  Test infrastructure for the N > 1 control flow on a one-GPU box, where
+    RCCL refuses two ranks per device -- never a production path.  (Not torch.distributed: torch's
+    ROCm build carries its own HIP runtime, and loading it next to libsnpmi's corrupts the heap.)"""
+
+    def __init__(self, rank, world, local_rank, device, timeout=300.0, env=None):
+        Dist.__init__(self, rank, world, local_rank, device, False, world)
+        path = id_file(env)
+        self._peers, self._sock = [], None
+        if rank == 0:
+            srv = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
+            srv.bind(("127.0.0.1", 0))
+            srv.listen(world)
+            srv.settimeout(timeout)
+            publish_id(path, struct.pack("<Q", srv.getsockname()[1]).ljust(128, b"\0"))
+            peers = {}
+            try:
+                while len(peers) < world - 1:
+                    conn, _ = srv.accept()
+                    conn.settimeout(timeout)
+                    (r,) = struct.unpack("<I", _recv_exact(conn, 4))
+                    peers[r] = conn
+            finally:
+                srv.close()
+                with contextlib.suppress(OSError):
+                    os.remove(path)
+            self._peers = [peers[r] for r in range(1, world)]
+        else:
+            (port,) = struct.unpack("<Q", wait_id(path, timeout)[:8])
+            sock = socket.create_connection(("127.0.0.1", port), timeout=timeout)
+            sock.sendall(struct.pack("<I", rank))
+            self._sock = sock
+
+    def allgather_bytes(self, payload):
+        """Every rank's ``payload`` (bytes), in rank order, on every rank."""
+        payload = bytes(payload)
+        if self.rank == 0:
+            parts = [payload] + [_recv_frame(c) for c in self._peers]
+            blob = struct.pack("<I", len(parts)) + b"".join(struct.pack("<Q", len(p)) + p for p in parts)
+            for c in self._peers:
+                _send_frame(c, blob)
+        else:
+            _send_frame(self._sock, payload)
+            blob = _recv_frame(self._sock)
+        (cnt,) = struct.unpack_from("<I", blob, 0)
+        off, parts = 4, []
+        for _ in range(cnt):
+            (n,) = struct.unpack_from("<Q", blob, off)
+            parts.append(blob[off + 8:off + 8 + n])
+            off += 8 + n
+        return parts
+
+    def barrier(self):
+        self.allgather_bytes(b"")
+
+    def max(self, x):
+        return max(struct.unpack("<d", p)[0] for p in self.allgather_bytes(struct.pack("<d", float(x))))
+
+    def sum_host(self, arr):
+        import numpy as np
+
+        a = np.asarray(arr)
+        parts = self.allgather_bytes(np.ascontiguousarray(a, dtype=np.float64).tobytes())
+        tot = np.zeros(a.shape, dtype=np.float64)
+        for p in parts:
+            tot += np.frombuffer(p, dtype=np.float64).reshape(a.shape)
+        return tot.astype(a.dtype)
+
+    def allgather_dev(self, send, recv, nbytes):
+        import numpy as np
+
+        from pysnptools_amd import _native as N
+
+        nbytes = int(nbytes)
+        mine = np.empty(nbytes, dtype=np.uint8)
+        N.call("snpmi_memcpy_d2h", N.ptr(mine), send, nbytes)
+        host = np.frombuffer(b"".join(self.allgather_bytes(mine.tobytes())), dtype=np.uint8)
+        N.call("snpmi_memcpy_h2d", recv, N.ptr(host), host.nbytes)
+
+    def _close_host(self):
+        for c in self._peers + ([self._sock] if self._sock else []):
+            with contextlib.suppress(OSError):
+                c.close()
+        self._peers, self._sock = [], None
 
 
 def init_from_env(force_rccl=False, timeout=300.0, env=None, set_current=True):
@@ -211,6 +338,12 @@ def init_from_env(force_rccl=False, timeout=300.0, env=None, set_current=True):
                            "SNPMI_RCCL_ID_FILE to a path every node shares to run across nodes)" % (world, local_world))
     device = pick_device(local_rank, N.device_count())
     N.call("snpmi_set_device", device)
+    if world > 1 and env.get("SNPMI_DIST_HOST"):
+        d = HostDist(rank, world, local_rank, device, timeout, env)
+        d.barrier()
+        if set_current:
+            _CURRENT = d
+        return d
     rccl, n_gpus = False, 1
     if world > 1 or force_rccl:
         path = id_file(env)

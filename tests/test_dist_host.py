@@ -93,3 +93,36 @@ def test_id_handoff_between_processes(tmp_path, world):
     outs = [p.communicate(timeout=120)[0] for p in procs]
     assert all(p.returncode == 0 for p in procs)
     assert sorted(o.strip() for o in outs) == sorted("ok %d" % r for r in range(world))
+
+
+_HOST_WORKER = r"""
+import os, sys
+sys.path.insert(0, %r)
+import numpy as np
+from pysnptools_amd import dist as D
+rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+d = D.HostDist(rank, world, rank, 0, timeout=60)
+assert d.world == world and d.n_gpus == world and not d.rccl
+d.barrier()
+assert d.max(rank * 1.5) == (world - 1) * 1.5
+s = d.sum_host(np.arange(5, dtype=np.float32) * (rank + 1))
+assert s.dtype == np.float32 and np.array_equal(s, np.arange(5) * sum(range(1, world + 1)))
+parts = d.allgather_bytes(bytes([rank]) * (rank + 1000))
+assert [len(p) for p in parts] == [r + 1000 for r in range(world)] and all(p[:1] == bytes([r]) for r, p in enumerate(parts))
+d.barrier()
+d.close()
+print("ok", rank)
+"""
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_host_rehearsal_group_collectives(tmp_path, world):
+    """HostDist (SNPMI_DIST_HOST=1, the rehearsal group bench.py's N > 1 control flow runs on with
+    every rank on one GPU): barrier, max-over-ranks, host sums and byte all-gathers across real
+    processes through rank 0's socket hub (its port handed over in the id file)."""
+    env = dict(os.environ, SNPMI_RCCL_ID_FILE=str(tmp_path / "hub.id"), WORLD_SIZE=str(world))
+    procs = [subprocess.Popen([sys.executable, "-c", _HOST_WORKER % ROOT], env=dict(env, RANK=str(r)),
+                              stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for r in range(world)]
+    outs = [p.communicate(timeout=180) for p in procs]
+    assert all(p.returncode == 0 for p in procs), [o[1][-2000:] for o in outs]
+    assert sorted(o[0].strip() for o in outs) == sorted("ok %d" % r for r in range(world))

@@ -1,0 +1,59 @@
+"""bench.py's whole N > 1 control flow on ONE GPU: every rank of a world-2 / world-3 job runs on
+the box's single device inside the host rehearsal group (SNPMI_DIST_HOST=1, pysnptools_amd.dist.
+HostDist: gloo barriers and max-over-ranks, host-staged all-gather; RCCL refuses two ranks per
+device).  Both launch paths the driver uses -- bench.py's own spawner (--gpus N) and
+torch.distributed.run -- must end with exit 0 and exactly one JSON line from rank 0, the SNP
+shards covering the matrix, the cfg5 block rebuilt bit-exactly by the all-gather and every parity
+check passing.  Rank 0's rank-only legs (file, CPU baselines) run while the others wait at the
+final barrier."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+from conftest import ROOT
+
+pytestmark = pytest.mark.gpu
+
+SMALL = ["--steps", "1", "--warmup", "0", "--n-iid", "4099", "--n-sid", "6000", "--grm-iid", "5000",
+         "--grm-sid", "12000", "--grm-block", "5000", "--grm5-iid", "20000", "--grm5-sid", "2048",
+         "--e2e-sid", "4096", "--e2e-passes", "1", "--cpu-seconds", "0.2", "--beta-iid", "5001",
+         "--beta-sid", "6000", "--file-iid", "3001", "--file-sid", "5000", "--cpu-grm-iid", "3000",
+         "--cpu-grm-sid", "64", "--dist-timeout", "120"]
+
+
+def _check(out, world):
+    assert out.returncode == 0, out.stderr[-4000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, out.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == world and d["config"]["process_group"].startswith("host rehearsal")
+    assert d["config"]["n_sid_per_gpu"] == 6000 // world and d["value"] > 0
+    assert d["parity"]["bit_exact"] and d["beta"]["parity"]["pass"]
+    for k in ("grm", "grm_f64"):
+        assert d[k]["parity"]["pass"], d[k]["parity"]
+    g5 = d["grm5"]
+    assert g5["parity"]["pass"] and g5["parity"]["gathered_block_bit_exact"], g5["parity"]
+    assert "host all-gather" in g5["workload"]
+    f = d["file"]
+    assert f["read_kernel_f32"]["parity"]["pass"] and f["read_hbm"]["parity"]["bit_exact"]
+    return d
+
+
+def test_bench_spawned_world2_on_one_gpu():
+    env = dict(os.environ, SNPMI_DIST_HOST="1")
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"] + SMALL
+    _check(subprocess.run(cmd, capture_output=True, text=True, timeout=290, env=env), 2)
+
+
+def test_bench_torchrun_world3_on_one_gpu():
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    env = dict(os.environ, SNPMI_DIST_HOST="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "3", "--master-addr",
+           "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"), "--gpus", "3"] + SMALL
+    _check(subprocess.run(cmd, capture_output=True, text=True, timeout=290, env=env), 3)
