@@ -366,6 +366,120 @@ __global__ __launch_bounds__(512, 1) void k_syrk_i8r(const uint8_t* __restrict__
         }
 }
 
+#ifdef SNPMI_UBENCH
+// ubench (variant 77): 4 waves (2 x 2), one per SIMD, 128 x 128 per wave = 4 x 4
+// v_mfma_i32_32x32x32_i8 tiles (256 accumulator registers, AGPR-backed): 8 fragment reads per 16
+// MFMAs instead of k_syrk_i8r's 6 per 8 -- a third less LDS read traffic for the same residue
+// image; the loader is k_syrk_i8r's with twice the rows per thread.
+template <int SKT>
+__global__ __launch_bounds__(256, 1) void k_syrk_i8w(const uint8_t* __restrict__ P, uint64_t pitch, uint64_t kdim,
+                                                     uint64_t mpad, const uint32_t* __restrict__ lutr,
+                                                     const int* __restrict__ ctl, uint64_t b0, uint64_t nblk,
+                                                     uint8_t* __restrict__ res) {
+    constexpr int KS = SKT / 32, RPT = SKT / 8, PNL = SKT * RS, STG = 2 * PNL;
+    __shared__ __attribute__((aligned(16))) uint8_t lds[2 * STG];
+    if (ctl[1]) return;
+    const int r = blockIdx.y;
+    if (r >= ctl[2]) return;
+    const uint32_t* lr = lutr + (uint64_t)r * mpad;
+    uint32_t bi, bj;
+    tile_coords(b0 + blockIdx.x, bi, bj);
+    const uint64_t i0 = (uint64_t)bi * BW, j0 = (uint64_t)bj * BW;
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const int wm = wave >> 1, wn = wave & 1;
+    const int lp = __builtin_amdgcn_readfirstlane(t >> 7), kq = (t >> 4) & 7, d = t & 15;
+    const uint8_t* pbase = P + (lp ? j0 : i0) / 4;
+    const uint32_t pit = (uint32_t)pitch;
+    const uint32_t* lq = lr + RPT * kq;
+    const int g = lane >> 4, jj = (lane & 15) >> 1, pp = lane & 1;
+    const int rd = (16 * (g >> 1) + jj) * RS + 16 * (g & 1) + 8 * pp;
+
+    v16i acc[4][4];
+#pragma unroll
+    for (int x = 0; x < 4; x++)
+#pragma unroll
+        for (int y = 0; y < 4; y++) acc[x][y] = (v16i){};
+    const uint64_t nst = (kdim + SKT - 1) / SKT;
+    uint32_t cw[RPT];
+    uint4 cl[RPT / 4];
+    auto load = [&](uint64_t st) {
+        const uint8_t* sb = pbase + st * SKT * pitch;
+        const uint32_t lim = (uint32_t)(kdim - 1 - st * SKT);
+#pragma unroll
+        for (int h = 0; h < RPT; h++) {
+            const uint32_t row = min((uint32_t)(RPT * kq + h), lim);
+            cw[h] = *reinterpret_cast<const uint32_t*>(sb + (row * pit + 4 * d));
+        }
+#pragma unroll
+        for (int u = 0; u < RPT / 4; u++) cl[u] = *reinterpret_cast<const uint4*>(lq + SKT * st + 4 * u);
+    };
+    auto store = [&](uint8_t* S, int h0, int h1) {
+#pragma unroll
+        for (int h = h0; h < h1; h++) {
+            const uint4 c4 = cl[h >> 2];
+            const uint32_t L = (h & 3) == 0 ? c4.x : (h & 3) == 1 ? c4.y : (h & 3) == 2 ? c4.z : c4.w;
+            uint4 o;
+            o.x = __builtin_amdgcn_perm(L, L, cw[h] & 0x03030303u);
+            o.y = __builtin_amdgcn_perm(L, L, (cw[h] >> 2) & 0x03030303u);
+            o.z = __builtin_amdgcn_perm(L, L, (cw[h] >> 4) & 0x03030303u);
+            o.w = __builtin_amdgcn_perm(L, L, (cw[h] >> 6) & 0x03030303u);
+            *reinterpret_cast<uint4*>(S + lp * PNL + (RPT * kq + h) * RS + 16 * d) = o;
+        }
+    };
+    auto frag = [&](const uint8_t* S, int panel, int ks, int col) -> v4i {
+        const uint8_t* b = S + panel * PNL + 32 * ks * RS + rd + col;
+        const v2i x = lds_tr8(b), y = lds_tr8(b + 8 * RS);
+        return (v4i){x.x, x.y, y.x, y.y};
+    };
+    auto frags = [&](const uint8_t* S, int ks, v4i (&A)[4], v4i (&B)[4]) {
+#pragma unroll
+        for (int x = 0; x < 4; x++) A[x] = frag(S, 0, ks, wm * 128 + 32 * x);
+#pragma unroll
+        for (int y = 0; y < 4; y++) B[y] = frag(S, 1, ks, wn * 128 + 32 * y);
+    };
+    load(0);
+    store(lds, 0, RPT);
+    load(nst > 1 ? 1 : 0);
+    __syncthreads();
+    for (uint64_t s = 0; s < nst; s++) {
+        const uint8_t* cur = lds + (s & 1) * STG;
+        uint8_t* nxt = lds + ((s + 1) & 1) * STG;
+        v4i a[2][4], b[2][4];
+        frags(cur, 0, a[0], b[0]);
+#pragma unroll
+        for (int ks = 0; ks < KS; ks++) {
+            if (ks + 1 < KS) frags(cur, ks + 1, a[(ks + 1) & 1], b[(ks + 1) & 1]);
+#pragma unroll
+            for (int x = 0; x < 4; x++)
+#pragma unroll
+                for (int y = 0; y < 4; y++)
+                    acc[x][y] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[ks & 1][x], b[ks & 1][y], acc[x][y], 0, 0, 0);
+            store(nxt, ks * RPT / KS, (ks + 1) * RPT / KS);
+        }
+        load(s + 2 < nst ? s + 2 : nst - 1);
+        __syncthreads();
+    }
+    const int p = kMod[r];
+    const double invp = 1.0 / (double)p;
+    uint8_t* O = res + ((uint64_t)r * nblk + blockIdx.x) * (BW * BW);
+    const int hh = lane >> 5, colp = 16 * ((lane >> 4) & 1) + pi16(lane & 15);
+#pragma unroll
+    for (int x = 0; x < 4; x++)
+#pragma unroll
+        for (int y = 0; y < 4; y++) {
+            uint8_t* bp = O + (wm * 128 + 32 * x + hh) * BW + wn * 128 + 32 * y + colp;
+#pragma unroll
+            for (int q = 0; q < 16; q++) {
+                const int v = acc[x][y][q];
+                int rr = v - p * (int)floor((double)v * invp);
+                rr += rr < 0 ? p : 0;
+                rr -= rr >= p ? p : 0;
+                bp[(16 * (q >> 3) + 4 * (q & 3) + 2 * ((q >> 2) & 1)) * BW] = (uint8_t)rr;
+            }
+        }
+}
+#endif
+
 // ---------------------------------------------------------------- reconstruction
 // two elements per thread (packed f32 math: v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32); the
 // residues of the R planes -> K_int (Garner, exact: all digit arithmetic is on integers < 2^24
@@ -546,6 +660,8 @@ void launch_syrk_packed_crt(const uint8_t* packed, uint64_t pitch, uint64_t n, u
             k_syrk_i8r<SK, 0, 1><<<dim3((unsigned)cnt, kR), 512, 0, st>>>(packed, pitch, m, mpad, lutr, ctl, b0, cnt, res);
         else if (g_variant_syrk == 76)  // same, 64-SNP stages
             k_syrk_i8r<64, 0, 1><<<dim3((unsigned)cnt, kR), 512, 0, st>>>(packed, pitch, m, mpad, lutr, ctl, b0, cnt, res);
+        else if (g_variant_syrk == 77)  // 4 waves, one per SIMD, 128 x 128 per wave
+            k_syrk_i8w<SK><<<dim3((unsigned)cnt, kR), 256, 0, st>>>(packed, pitch, m, mpad, lutr, ctl, b0, cnt, res);
         else if (g_variant_syrk == 74)  // ablation: fragments read once per stage
             k_syrk_i8r<SK, 2><<<dim3((unsigned)cnt, kR), 512, 0, st>>>(packed, pitch, m, mpad, lutr, ctl, b0, cnt, res);
         else

@@ -84,3 +84,50 @@ def test_partitioned_blocks_within_f32_bar(data):
     scale = np.abs(np.diag(ref[:, :R])).max()
     err = np.abs(blk[:R].astype(np.float64) - ref[:, :256]).max() / scale
     assert err <= 6e-6, err
+
+
+@pytest.mark.parametrize("m_edge", [8191, 8193, 16415])
+@pytest.mark.parametrize("seg", [256, 8192])
+def test_segment_flush_edges_vs_oracle(m_edge, seg):
+    """SegFlush edge cases on the default fp16x2 kernel: SNP counts one short of / one past / 31
+    past a segment boundary, and a 256-SNP segment (a flush every 4 trips: the store-then-atomic
+    slot path runs dozens of times per workgroup, 78 workgroups share the slot pool); K rows 0..7
+    vs the f64 oracle at the f32 bar, and the segmented K within 2e-6 of max diag of the
+    unsegmented one."""
+    nn = 3000
+    pitch = N.lib().snpmi_packed_pitch(nn)
+    packed = bench.Dev(N, pitch * m_edge)
+    bench.synth(N, packed.p, pitch, nn, 0, m_edge, 17, 0.05)
+    host = np.empty((m_edge, pitch), dtype=np.uint8)
+    N.call("snpmi_memcpy_d2h", N.ptr(host), packed.p, host.nbytes)
+    body = np.ascontiguousarray(host[:, :(nn + 3) // 4]).reshape(-1)
+    Z, _ = O.decode_standardize(body, nn, m_edge, dtype=np.float64)
+    ref = Z[:R].dot(Z.T)
+
+    def rows(s):
+        N.call("snpmi_set_kernel_variant", b"seg", s)
+        try:
+            stats = bench.Dev(N, m_edge * 8)
+            g = ShardedGrm(nn, np.float32, None, "none")
+            g.add_packed(packed.p, pitch, m_edge, N.STD_UNIT, 0.0, 0.0, 0, stats.p)
+            t, _ = g.tiles()
+            ri = np.arange(R, dtype=np.uint64)
+            dri, dout = bench.Dev(N, R * 8), bench.Dev(N, R * nn * 4)
+            N.call("snpmi_memcpy_h2d", dri.p, N.ptr(ri), ri.nbytes)
+            N.call("snpmi_dev_grm_extract", t, nn, N.DT_F32, dri.p, R, None, nn, 1, 1.0, dout.p)
+            K = np.empty((R, nn), dtype=np.float32)
+            N.call("snpmi_memcpy_d2h", N.ptr(K), dout.p, K.nbytes)
+            g.abort()
+            for d in (stats, dri, dout):
+                d.free()
+            return K.astype(np.float64)
+        finally:
+            N.call("snpmi_set_kernel_variant", b"seg", 8192)
+
+    try:
+        Ks, K0 = rows(seg), rows(0)
+    finally:
+        packed.free()
+    scale = np.abs(np.diag(ref[:, :R])).max()
+    assert np.abs(Ks - ref).max() / scale <= 1e-5
+    assert np.abs(Ks - K0).max() / scale <= 2e-6
