@@ -877,6 +877,13 @@ def grm5_parity(args, m, picks, sample):
                      "oracle f64" % (m, n), "blocks": out, "max_abs_err_over_scale": worst, "pass": worst <= 1e-5}
 
 
+def input_sha256(sample, n):
+    """SHA-256 of the packed bytes of the sampled columns (pin the synthetic input)."""
+    import hashlib
+
+    return hashlib.sha256(np.ascontiguousarray(sample[:, :(n + 3) // 4]).tobytes()).hexdigest()
+
+
 def pmc_traffic(kernel, leg, n_iid, block):
     """Per-launch HBM bytes of ``kernel`` from the committed PMC summary, when its profile was
     taken at this configuration (tools/profile.sh + tools/traffic_summary.py); else None."""
@@ -1172,7 +1179,10 @@ def main(argv=None):
             ref, cpu = cpu_baseline_standardize(args, r1["sample"], timed=dist.world == 1)
             same = np.array_equal(r1["gpu_cols"][:, :args.n_iid].T, ref)
             parity = {"check": "first %d SNP columns x %d iids: GPU stats+decode vs oracle decode+one-pass "
-                               "Unit (f32)" % (ref.shape[1], ref.shape[0]), "bit_exact": bool(same)}
+                               "Unit (f32)" % (ref.shape[1], ref.shape[0]), "bit_exact": bool(same),
+                      "input_sha256": input_sha256(r1["sample"], args.n_iid),
+                      "input_hashed": "packed bytes (ceil(N/4) per column) of SNP columns 0..%d of the synthetic "
+                                      "matrix (counter-based generator, seed %d)" % (len(r1["sample"]) - 1, args.seed)}
             if grm is not None:
                 grm["cpu_baseline"] = cpu_baseline_grm(args, "f32") if dist.world == 1 else None
                 if r2.get("parity_sample") is not None:
@@ -1195,6 +1205,7 @@ def main(argv=None):
                 rel = float(np.max(np.abs(got - refb) / np.maximum(np.abs(refb), 1e-30)))
                 beta["parity"] = {"check": "first %d SNP columns x %d iids: GPU vs oracle one-pass Beta(1,25) (f32)"
                                            % (refb.shape[1], nb_), "max_rel_err": rel,
+                                  "input_sha256": input_sha256(rb["sample"], nb_),
                                   "bit_exact": bool(np.array_equal(rb["gpu_cols"][:, :nb_].T, refb)),
                                   "pass": rel <= 1e-5}
                 beta["cpu_baseline"] = cpub

@@ -123,6 +123,7 @@ def test_bench_with_rccl_communicator_world1(collective):
     assert d["n_gpus"] == 1 and d["value"] > 0 and d["parity"]["bit_exact"]
     assert 0 < d["roofline"]["frac_tight"] and d["cpu_baseline"]["cpu_counts"]["usable"] >= 1
     assert d["roofline"]["layout"].startswith("tight") and d["roofline"]["frac"] == d["roofline"]["frac_tight"]
+    assert len(d["parity"]["input_sha256"]) == 64 and len(d["beta"]["parity"]["input_sha256"]) == 64
     assert d["beta"]["parity"]["pass"] and d["beta"]["snps_per_s"] > 0, d["beta"]
     f = d["file"]
     assert f["read_kernel_f32"]["parity"]["pass"], f["read_kernel_f32"]["parity"]
