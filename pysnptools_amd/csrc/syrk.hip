@@ -1340,6 +1340,19 @@ __global__ __launch_bounds__(512, 1) void k_syrk_h2(const uint8_t* __restrict__ 
         v1.y = __builtin_amdgcn_perm(hi, lo, sel[5]);
         v1.z = __builtin_amdgcn_perm(hi, lo, sel[6]);
         v1.w = __builtin_amdgcn_perm(hi, lo, sel[7]);
+        if constexpr (MODE == 4) {
+            // two ds_write_b64 per 16-B half (6 LDS-transfer cycles per wave-instruction vs 13 for
+            // ds_write_b128; volatile + explicit LDS address space so they are neither re-merged
+            // nor turned into flat stores): +1.2-1.3% at 50k x 10k / 62.5k, bit-identical K
+            // (profiles/r03crt/ubench_lds_store_width.jsonl)
+            typedef __attribute__((address_space(3))) volatile uint64_t lds_u64;
+            lds_u64* q = (lds_u64*)(S + (lp * 2 + pl) * PLANE + (lk + BK * h) * B3_RS + 16 * ld_);
+            q[2 * sw] = (uint64_t)v0.x | ((uint64_t)v0.y << 32);
+            q[2 * sw + 1] = (uint64_t)v0.z | ((uint64_t)v0.w << 32);
+            q[2 * (sw ^ 1)] = (uint64_t)v1.x | ((uint64_t)v1.y << 32);
+            q[2 * (sw ^ 1) + 1] = (uint64_t)v1.z | ((uint64_t)v1.w << 32);
+            return;
+        }
         uint4* r4 = reinterpret_cast<uint4*>(S + (lp * 2 + pl) * PLANE + (lk + BK * h) * B3_RS + 16 * ld_);
         r4[sw] = v0;
         r4[sw ^ 1] = v1;

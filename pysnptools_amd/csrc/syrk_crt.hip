@@ -196,7 +196,9 @@ __device__ __forceinline__ v2i lds_tr8(const uint8_t* p) {
 // LDM 1: row-per-wave loader -- wave w expands rows 32(w&3)..+31 of panel w>>2, lane L the 4 iids
 // of LDS dword L (one code dword per lane, one v_perm), stored by ds_write_addtid_b32 (address =
 // M0 + 4 lane: 2 cycles per 256-B row vs 13 per ds_write_b128); the row's LUT word is uniform.
-template <int SKT, int ABL = 0, int LDM = 0>
+// ST 1 (ubench variant 78): each 16-B residue row written as two volatile ds_write_b64 (6 cycles
+// per wave-instruction on the LDS transfer path) instead of one ds_write_b128 (13)
+template <int SKT, int ABL = 0, int LDM = 0, int ST = 0>
 __global__ __launch_bounds__(512, 1) void k_syrk_i8r(const uint8_t* __restrict__ P, uint64_t pitch, uint64_t kdim,
                                                      uint64_t mpad, const uint32_t* __restrict__ lutr,
                                                      const int* __restrict__ ctl, uint64_t b0, uint64_t nblk,
@@ -254,7 +256,14 @@ __global__ __launch_bounds__(512, 1) void k_syrk_i8r(const uint8_t* __restrict__
             o.y = __builtin_amdgcn_perm(L, L, (cw[h] >> 2) & 0x03030303u);
             o.z = __builtin_amdgcn_perm(L, L, (cw[h] >> 4) & 0x03030303u);
             o.w = __builtin_amdgcn_perm(L, L, (cw[h] >> 6) & 0x03030303u);
-            *reinterpret_cast<uint4*>(S + lp * PNL + (RPT * kq + h) * RS + 16 * d) = o;
+            if constexpr (ST == 1) {
+                typedef __attribute__((address_space(3))) volatile uint64_t lds_u64;
+                lds_u64* q = (lds_u64*)(S + lp * PNL + (RPT * kq + h) * RS + 16 * d);
+                q[0] = (uint64_t)o.x | ((uint64_t)o.y << 32);
+                q[1] = (uint64_t)o.z | ((uint64_t)o.w << 32);
+            } else {
+                *reinterpret_cast<uint4*>(S + lp * PNL + (RPT * kq + h) * RS + 16 * d) = o;
+            }
         }
     };
     auto frag = [&](const uint8_t* S, int panel, int ks, int col) -> v4i {
@@ -660,6 +669,8 @@ void launch_syrk_packed_crt(const uint8_t* packed, uint64_t pitch, uint64_t n, u
             k_syrk_i8r<SK, 0, 1><<<dim3((unsigned)cnt, kR), 512, 0, st>>>(packed, pitch, m, mpad, lutr, ctl, b0, cnt, res);
         else if (g_variant_syrk == 76)  // same, 64-SNP stages
             k_syrk_i8r<64, 0, 1><<<dim3((unsigned)cnt, kR), 512, 0, st>>>(packed, pitch, m, mpad, lutr, ctl, b0, cnt, res);
+        else if (g_variant_syrk == 78)  // residue rows stored as two ds_write_b64
+            k_syrk_i8r<SK, 0, 0, 1><<<dim3((unsigned)cnt, kR), 512, 0, st>>>(packed, pitch, m, mpad, lutr, ctl, b0, cnt, res);
         else if (g_variant_syrk == 77)  // 4 waves, one per SIMD, 128 x 128 per wave
             k_syrk_i8w<SK><<<dim3((unsigned)cnt, kR), 256, 0, st>>>(packed, pitch, m, mpad, lutr, ctl, b0, cnt, res);
         else if (g_variant_syrk == 74)  // ablation: fragments read once per stage
