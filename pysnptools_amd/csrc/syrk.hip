@@ -1232,7 +1232,7 @@ __global__ __launch_bounds__(512, 1) void k_syrk_h2(const uint8_t* __restrict__ 
                                                     const uint32_t* __restrict__ flag, float* __restrict__ tiles,
                                                     int accumulate, uint32_t part_rank = 0, uint32_t part_world = 1,
                                                     uint64_t kslice = 0, uint64_t slice_elems = 0,
-                                                    SegCtx seg = SegCtx()) {
+                                                    SegCtx seg = SegCtx(), const uint32_t* __restrict__ order = nullptr) {
     // KS = 16-SNP k-steps per LDS stage (MODE 4/5: two, one barrier per 32 SNPs)
     // MODE 10 = MODE 4 with the loader's registers double-buffered: stage s+2's codes/LUT are
     // loaded at the START of stage s (a whole stage to arrive instead of one MFMA group)
@@ -1255,6 +1255,10 @@ __global__ __launch_bounds__(512, 1) void k_syrk_h2(const uint8_t* __restrict__ 
     if constexpr (DENSE) {
         // lut2 = block order table (supertile_order): the 256 blocks in flight share 32 panels
         const uint32_t c = lut2[wg];
+        bi = c & 0xffffu;
+        bj = c >> 16;
+    } else if (order) {  // ubench: supertile block order table (supertile_order)
+        const uint32_t c = order[wg];
         bi = c & 0xffffu;
         bj = c >> 16;
     } else {
@@ -2625,6 +2629,23 @@ void supertile_order(uint64_t nb, bool xcd, std::vector<uint32_t>& tab) {
         }
 }
 
+#ifdef SNPMI_UBENCH
+// device copy of supertile_order(nb, xcd) for the packed-SYRK order A/B (variants 65/66)
+static const uint32_t* ub_order(uint64_t nb, bool xcd) {
+    static uint32_t* tab[2] = {};
+    static uint64_t tnb[2] = {};
+    if (tnb[xcd] != nb) {
+        std::vector<uint32_t> t;
+        supertile_order(nb, xcd, t);
+        if (tab[xcd]) SNPMI_HIP(hipFree(tab[xcd]));
+        SNPMI_HIP(hipMalloc(&tab[xcd], t.size() * sizeof(uint32_t)));
+        SNPMI_HIP(hipMemcpy(tab[xcd], t.data(), t.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+        tnb[xcd] = nb;
+    }
+    return tab[xcd];
+}
+#endif
+
 int g_dense_chunk = 0;  // tuning / test hook (snpmi_set_kernel_variant "dense_chunk"): force chunk SNPs
 
 uint64_t dense_h2_chunk_snps(uint64_t n) {
@@ -2733,6 +2754,10 @@ void launch_syrk_packed_bf3(const uint8_t* packed, uint64_t pitch, uint64_t n, u
             case 48: f32w::k_syrk_h2<false, 8><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles, accumulate); break;
             case 62: f32w::k_syrk_h2<false, 10><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles, accumulate); break;
             case 63: f32w::k_syrk_h2<false, 11><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles, accumulate); break;
+            case 65:  // supertile block order (xcd-dealt), 66: supertile order, plain
+            case 66: f32w::k_syrk_h2<false, 4><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles,
+                                                                           accumulate, 0, 1, 0, 0, seg_ctx(),
+                                                                           ub_order(ceil_div(n, 256), g_variant_syrk == 65)); break;
 #endif
             default:
                 f32w::k_syrk_h2<false, 4><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles,
