@@ -694,7 +694,10 @@ SegCtx seg_ctx() {
     c.nslots = kSegSlots;
     c.scratch = (float*)base;
     c.flags = (uint32_t*)(base + (uint64_t)kSegSlots * kSegSlotFloats * sizeof(float));
-    if (fresh) SNPMI_HIP(hipMemsetAsync(c.flags, 0, kSegSlots * sizeof(uint32_t), d.stream));
+    if (fresh) {  // once per device; complete before any stream's first SYRK can take a slot
+        SNPMI_HIP(hipMemsetAsync(c.flags, 0, kSegSlots * sizeof(uint32_t), d.stream));
+        SNPMI_HIP(hipStreamSynchronize(d.stream));
+    }
     return c;
 }
 
@@ -915,6 +918,12 @@ static const uint32_t* dense_order(Device& d, uint64_t nb, bool xcd) {
         d.order_nb[xcd] = nb;
     }
     return d.order_tab[xcd];
+}
+
+// the packed fp16x2 SYRK's block order (syrk.hip): the same supertile table, cached per nb
+const uint32_t* packed_block_order(uint64_t nb) {
+    std::lock_guard<std::recursive_mutex> lk(g_call_mutex);
+    return dense_order(device(), nb, false);
 }
 
 // dense GRM operand on the device: f32 with n >= 4096 and the default variant takes the fp16x2

@@ -113,6 +113,9 @@ struct SegCtx {
 constexpr uint32_t kSegSlots = 1024;                 // > the resident workgroups of one launch (<= 256 x 2)
 constexpr uint64_t kSegSlotFloats = 8 * 32 * 64 * 4;  // per workgroup
 SegCtx seg_ctx();                                     // api.hip: the current device's pool (lazily allocated)
+// api.hip: device table of supertile_order(nb, false) for the current device (cached per nb): the
+// block order of the packed fp16x2 SYRK
+const uint32_t* packed_block_order(uint64_t nb);
 void launch_snp_stats(const uint8_t* packed, uint64_t pitch, uint64_t n_iid, uint64_t n_sid, int count_a1,
                       int std_kind, double a, double b, int use_stats, int dtype, void* stats, void* lut,
                       hipStream_t st);

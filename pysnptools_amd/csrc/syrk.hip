@@ -2754,14 +2754,23 @@ void launch_syrk_packed_bf3(const uint8_t* packed, uint64_t pitch, uint64_t n, u
             case 48: f32w::k_syrk_h2<false, 8><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles, accumulate); break;
             case 62: f32w::k_syrk_h2<false, 10><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles, accumulate); break;
             case 63: f32w::k_syrk_h2<false, 11><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles, accumulate); break;
-            case 65:  // supertile block order (xcd-dealt), 66: supertile order, plain
-            case 66: f32w::k_syrk_h2<false, 4><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles,
-                                                                           accumulate, 0, 1, 0, 0, seg_ctx(),
-                                                                           ub_order(ceil_div(n, 256), g_variant_syrk == 65)); break;
-#endif
-            default:
+            case 65:  // A/B: plain triangular block order
                 f32w::k_syrk_h2<false, 4><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles,
                                                                       accumulate, 0, 1, 0, 0, seg_ctx());
+                break;
+            case 66:  // A/B: supertile order with each supertile dealt over the 8 XCDs
+                f32w::k_syrk_h2<false, 4><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles,
+                                                                      accumulate, 0, 1, 0, 0, seg_ctx(),
+                                                                      ub_order(ceil_div(n, 256), true));
+                break;
+#endif
+            default:
+                // supertile block order: the ~256 blocks in flight share ~32 code panels instead of
+                // ~nb (+1.7-2.4% at 50k x 31.25k / 62.5k vs the triangular order,
+                // profiles/r03crt/ubench_block_order.jsonl)
+                f32w::k_syrk_h2<false, 4><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles,
+                                                                      accumulate, 0, 1, 0, 0, seg_ctx(),
+                                                                      packed_block_order(ceil_div(n, 256)));
         }
         SNPMI_HIP(hipGetLastError());
         f32w::k_syrk_bf3<false, false, 5><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, lut3, tiles, accumulate, 0, 1, 0, 0,
@@ -2797,7 +2806,7 @@ void launch_syrk_packed_bf3_split(const uint8_t* packed, uint64_t pitch, uint64_
     SNPMI_REQUIRE(g < (1ull << 31) && S >= 1, SNPMI_E_ARG, "bad split");
     if (h2) {
         f32w::k_syrk_h2<><<<dim3((unsigned)g, S), 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, partial, 0, 0, 1,
-                                                                 kslice, elems, seg_ctx());
+                                                                 kslice, elems, seg_ctx(), packed_block_order(nb));
         SNPMI_HIP(hipGetLastError());
     }
     f32w::k_syrk_bf3<false, false, 5><<<dim3((unsigned)g, S), 512, 0, st>>>(packed, pitch, n, m, lut3, partial, 0, 0, 1,
