@@ -613,6 +613,75 @@ __global__ __launch_bounds__(kBlock) void k_decode_sweepc(const uint8_t* __restr
     }
     (void)total;
 }
+
+// ubench (round 3b): the sweep with a DEEP code prefetch and the LUT in LDS.  The hipMemset fill
+// never waits on vmcnt, so its stores stay in flight without bound; a decode wave must wait vmcnt
+// for its code loads, and on gfx9 that counter also covers the wave's own earlier stores -- with
+// one batch of slack (the sweeps above) every wave stalls on its stores' completion, which a
+// narrow (1-4 waves per SIMD) grid cannot hide.  Here each wave keeps D items of code loads in
+// flight (a ring of D registers, item k's load issued right after item k-D's store), so the wait
+// for item k's codes covers only stores issued D items earlier; the LUT sits in LDS (lgkmcnt, not
+// vmcnt), the next item's LUT row is read one item ahead.  Items of 256 iids (1 KiB of output),
+// wave w takes items w, w + nwaves, ...: at any moment the grid writes one contiguous window.
+template <int D, bool NOLOAD>
+__global__ __launch_bounds__(kBlock) void k_decode_pf(const uint8_t* __restrict__ packed, uint64_t pitch,
+                                                      uint64_t n, uint64_t m, const float* __restrict__ lut,
+                                                      float* __restrict__ out, uint64_t ld) {
+    extern __shared__ float4 slut[];  // m rows
+    for (uint64_t j = threadIdx.x; j < m; j += kBlock) slut[j] = reinterpret_cast<const float4*>(lut)[j];
+    __syncthreads();
+    const int lane = threadIdx.x & (kWave - 1);
+    const uint64_t chunks = (n + 255) / 256;
+    const uint64_t nwaves = (uint64_t)gridDim.x * (kBlock / kWave);
+    const uint64_t wv = (uint64_t)__builtin_amdgcn_readfirstlane(blockIdx.x * (kBlock / kWave) + threadIdx.x / kWave);
+    const uint64_t dj = nwaves / chunks, dc = nwaves - dj * chunks;
+    uint64_t jl = wv / chunks, cl = wv - jl * chunks, js = jl, cs = cl;
+    auto adv = [&](uint64_t& j, uint64_t& c) {
+        c += dc;
+        j += dj;
+        if (c >= chunks) {
+            c -= chunks;
+            j++;
+        }
+    };
+    // unconditional loads: column clamped to m-1, byte c*64+lane < pitch always (pitch = 64 ceil(n/256))
+    auto fetch = [&]() -> uint32_t {
+        const uint64_t jj = jl < m ? jl : m - 1;
+        uint32_t v = NOLOAD ? (uint32_t)lane * 37u : (uint32_t)packed[jj * pitch + cl * 64 + lane];
+        adv(jl, cl);
+        return v;
+    };
+    uint32_t code[D];
+#pragma unroll
+    for (int u = 0; u < D; u++) code[u] = fetch();
+    float4 L = slut[js < m ? js : 0];
+    while (js < m) {
+#pragma unroll
+        for (int u = 0; u < D; u++) {
+            const bool act = js < m;  // wave-uniform; no break, so the ring unrolls into registers
+            const uint64_t jn = js + dj + (cs + dc >= chunks ? 1 : 0);
+            const float4 Ln = slut[jn < m ? jn : 0];
+            const uint32_t byte = code[u];
+            const uint64_t i = cs * 256 + 4 * lane;
+            f32x4_t v;
+            v.x = sel4(L.x, L.y, L.z, L.w, byte & 3u);
+            v.y = sel4(L.x, L.y, L.z, L.w, (byte >> 2) & 3u);
+            v.z = sel4(L.x, L.y, L.z, L.w, (byte >> 4) & 3u);
+            v.w = sel4(L.x, L.y, L.z, L.w, byte >> 6);
+            // branch-free store through a per-column buffer resource (num_records = the column's
+            // bytes, 0 past the last item): lanes past n are dropped by the range check, so every
+            // item issues exactly one store and the waitcnt pass counts it (n % 4 == 0 here)
+            const uint64_t ob = reinterpret_cast<uint64_t>(out + js * ld);
+            const uint32_t olo = __builtin_amdgcn_readfirstlane((uint32_t)ob), ohi = __builtin_amdgcn_readfirstlane((uint32_t)(ob >> 32));
+            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+                reinterpret_cast<void*>(((uint64_t)ohi << 32) | olo), (short)0, act ? (int)(n * 4) : 0, 0x00020000);
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v), rs, (int)(i * 4), 0, 2);
+            adv(js, cs);
+            code[u] = fetch();
+            L = Ln;
+        }
+    }
+}
 #endif
 
 // Fused stats + decode, one workgroup per SNP column (large N): pass 1 counts the codes
@@ -1772,6 +1841,25 @@ void launch_decode(const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m
             else if (g_variant_decode == 25) k_decode_f<float, 4, 1, 16><<<g8, kBlock, 0, st>>>(packed, pitch, n, m, L, O, ld);
             else if (g_variant_decode == 26) k_decode_f<float, 4, 1, 32><<<g8, kBlock, 0, st>>>(packed, pitch, n, m, L, O, ld);
             else k_decode_f<float, 4, 1, 64><<<g8, kBlock, 0, st>>>(packed, pitch, n, m, L, O, ld);
+            SNPMI_LAUNCH_CHECK();
+            return;
+        }
+        if (dtype == SNPMI_DT_F32 && g_variant_decode >= 80 && g_variant_decode <= 87 && m <= 8192 && n % 4 == 0 && n < (1ull << 29)) {
+            // deep-prefetch sweep k_decode_pf<D, NOLOAD> on G workgroups:
+            // 80 <16> 256, 81 <24> 256, 82 <16> 512, 83 store-only <16> 256, 84 <24> 512,
+            // 85 <8> 1024, 86 <24> 1024, 87 store-only <24> 512
+            const float* L = (const float*)lut;
+            float* O = (float*)out;
+            const int v = g_variant_decode;
+            const size_t sh = m * 16;
+            if (v == 80) k_decode_pf<16, false><<<256, kBlock, sh, st>>>(packed, pitch, n, m, L, O, ld);
+            else if (v == 81) k_decode_pf<24, false><<<256, kBlock, sh, st>>>(packed, pitch, n, m, L, O, ld);
+            else if (v == 82) k_decode_pf<16, false><<<512, kBlock, sh, st>>>(packed, pitch, n, m, L, O, ld);
+            else if (v == 83) k_decode_pf<16, true><<<256, kBlock, sh, st>>>(packed, pitch, n, m, L, O, ld);
+            else if (v == 84) k_decode_pf<24, false><<<512, kBlock, sh, st>>>(packed, pitch, n, m, L, O, ld);
+            else if (v == 85) k_decode_pf<8, false><<<1024, kBlock, sh, st>>>(packed, pitch, n, m, L, O, ld);
+            else if (v == 86) k_decode_pf<24, false><<<1024, kBlock, sh, st>>>(packed, pitch, n, m, L, O, ld);
+            else k_decode_pf<24, true><<<512, kBlock, sh, st>>>(packed, pitch, n, m, L, O, ld);
             SNPMI_LAUNCH_CHECK();
             return;
         }

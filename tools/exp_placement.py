@@ -92,7 +92,7 @@ def main():
     q0 = bufs[0][1]
     ref = None
     cols = [0, B // 2, B - 1]
-    for v in [0] + [x for x in variants if x >= 0 and x not in (23, 58, 59, 64, 65, 70, 71)]:  # store-only ablations
+    for v in [0] + [x for x in variants if x >= 0 and x not in (23, 58, 59, 64, 65, 70, 71, 83, 87)]:  # store-only ablations
         N.call("snpmi_set_kernel_variant", b"decode", v)
         N.call("snpmi_dev_memset", q0, 0, B * ld * 4)
         N.call("snpmi_dev_decode", packed.p, pitch, n, B, lut.p, N.DT_F32, 0, q0, ld)
