@@ -796,16 +796,13 @@ static void grm_finish(Device& d, const T* tiles, uint64_t n, int diag_k_to_n, d
     if (n == 0) return;
     const bool dev = is_device_ptr(d, K_out);
     const uint64_t rows_per = dev ? n : std::max<uint64_t>(1, std::min<uint64_t>(n, (1ull << 30) / (n * sizeof(T))));
-    std::vector<uint64_t> ri(rows_per);
-    uint64_t* dri = (uint64_t*)d.get(Device::S_IDX2, rows_per * 8);
     for (uint64_t r0 = 0; r0 < n; r0 += rows_per) {
         const uint64_t nr = std::min(rows_per, n - r0);
-        for (uint64_t r = 0; r < nr; r++) ri[r] = r0 + r;
-        // a device K_out is written in one extraction launch, no host copy
+        // a device K_out is written in one extraction launch, no host copy; a host K_out goes
+        // through 1 GiB row blocks (d2h_rows returns once the block has landed, so the next
+        // extraction may reuse the staging buffer)
         T* dk = dev ? K_out : (T*)d.get(Device::S_K, nr * n * sizeof(T));
-        SNPMI_HIP(hipStreamSynchronize(d.stream));  // ri reused across blocks
-        SNPMI_HIP(hipMemcpyAsync(dri, ri.data(), nr * 8, hipMemcpyHostToDevice, d.stream));
-        launch_grm_extract(tiles, n, DT<T>::v, dri, nr, nullptr, n, 1, scale, dk, d.stream);
+        launch_grm_extract_rows(tiles, n, DT<T>::v, r0, nr, scale, dk, d.stream);
         if (!dev) d2h_rows(d, K_out + r0 * n, n * sizeof(T), dk, n * sizeof(T), n * sizeof(T), nr, resolve_threads(0));
     }
     SNPMI_HIP(hipStreamSynchronize(d.stream));
@@ -830,28 +827,45 @@ static bool grm_stream_bed(Device& d, bool first, const char* path, uint64_t n_i
     // ~0.5 GiB of packed codes per chunk keeps >= 2 chunks in flight for cfg4-sized inputs
     const uint64_t C = chunk_snps(p.pitch_in + p.pitch_out, 1ull << 29);
     const bool has_stats = std_kind != SNPMI_STD_NONE && m_out > 0 && n_out > 0;
-    // stats go through pinned memory so the D2H/H2D copies stay asynchronous
+    // stats of every chunk stay on the device (16 B per SNP) and cross PCIe once, before / after
+    // the chunk loop: a per-chunk stats D2H on the compute stream shares a DMA engine with the
+    // next chunk's H2D and held that upload until the chunk's SYRK had finished (profiles/r03h)
     T* st_host = has_stats ? (T*)pinned(2, m_out * 2 * sizeof(T)) : nullptr;
-    if (has_stats && use_stats) std::memcpy(st_host, stats, m_out * 2 * sizeof(T));
+    T* st_all = (T*)d.get(Device::S_STATS, std::max<uint64_t>(m_out, 1) * 2 * sizeof(T));
+    if (has_stats && use_stats) {
+        std::memcpy(st_host, stats, m_out * 2 * sizeof(T));
+        SNPMI_HIP(hipMemcpyAsync(st_all, st_host, m_out * 2 * sizeof(T), hipMemcpyHostToDevice, d.stream));
+    }
     bool wrote = false;
-    for (uint64_t c0 = 0, ci = 0; c0 < m_out && n_out > 0; c0 += C, ci++) {
-        const uint64_t cnt = std::min(C, m_out - c0);
+    // the first chunk is an eighth of the others: its gather + upload is the one that cannot hide
+    // under a SYRK, the later ones stage while the previous chunk computes
+    const uint64_t C1 = std::max<uint64_t>(std::min<uint64_t>(C, 2048), C / 8);
+    if (m_out > C1 && n_out > 0) {  // size both staging slots for a full chunk up front: no regrowth
+        const uint64_t cmax = std::min(C, m_out);  // (a free + alloc) between the first two chunks
+        for (int slot = 0; slot < 2; slot++) {
+            SNPMI_HIP(hipEventSynchronize(d.staged[slot]));
+            (void)pinned(slot, cmax * p.pitch_in);
+            (void)d.get(slot ? Device::S_PACKED_B : Device::S_PACKED, cmax * p.pitch_in);
+        }
+        if (p.repack) (void)d.get(Device::S_PACKED2, cmax * p.pitch_out);
+    }
+    for (uint64_t c0 = 0, ci = 0; c0 < m_out && n_out > 0; ci++) {
+        const uint64_t cnt = std::min(ci == 0 ? C1 : C, m_out - c0);
         const uint8_t* packed = stage_chunk(d, m, sid_idx, c0, cnt, p, nthreads, (int)(ci & 1));
-        T* lut = (T*)d.get(Device::S_LUT, cnt * 4 * sizeof(T));
-        T* st_dev = (T*)d.get(Device::S_STATS, cnt * 2 * sizeof(T));
-        if (has_stats && use_stats)
-            SNPMI_HIP(hipMemcpyAsync(st_dev, st_host + 2 * c0, cnt * 2 * sizeof(T), hipMemcpyHostToDevice, d.stream));
+        T* lut = (T*)d.get(Device::S_LUT, std::min(C, m_out) * 4 * sizeof(T));
+        T* st_dev = st_all + 2 * c0;
         launch_snp_stats(packed, p.pitch_out, n_out, cnt, count_a1, std_kind, a, b, use_stats, dt, st_dev, lut,
                          d.stream);
         syrk(packed, p.pitch_out, n_out, cnt, (const T*)lut, !(first && !wrote));
         wrote = true;
-        if (has_stats && !use_stats)
-            SNPMI_HIP(hipMemcpyAsync(st_host + 2 * c0, st_dev, cnt * 2 * sizeof(T), hipMemcpyDeviceToHost, d.stream));
         chunk_done(d, (int)(ci & 1));
+        c0 += cnt;
     }
+    if (has_stats && !use_stats && n_out > 0)
+        SNPMI_HIP(hipMemcpyAsync(st_host, st_all, m_out * 2 * sizeof(T), hipMemcpyDeviceToHost, d.stream));
     SNPMI_HIP(hipStreamSynchronize(d.stream));
     SNPMI_HIP(hipStreamSynchronize(d.copy));
-    if (has_stats && !use_stats) std::memcpy(stats, st_host, m_out * 2 * sizeof(T));
+    if (has_stats && !use_stats && n_out > 0) std::memcpy(stats, st_host, m_out * 2 * sizeof(T));
     if (n_out == 0 && std_kind != SNPMI_STD_NONE && !use_stats) {
         for (uint64_t j = 0; j < m_out; j++) stats[2 * j] = stats[2 * j + 1] = (T)NAN;
     }
@@ -1695,7 +1709,11 @@ int snpmi_dev_syrk_dense(const void* Z, uint64_t ldz, uint64_t n_iid, uint64_t n
 int snpmi_dev_grm_extract(const void* K_tiles, uint64_t n_iid, int dtype, const uint64_t* ri, uint64_t nr,
                           const uint64_t* ci, uint64_t nc, int order_c, double scale, void* out) {
     return guarded([&] {
-        launch_grm_extract(K_tiles, n_iid, dtype, ri, nr, ci, nc, order_c, scale, out, stream());
+        // the whole K (K symmetric, so either order): the tile-blocked extraction
+        if (!ri && !ci && nr == n_iid && nc == n_iid)
+            launch_grm_extract_rows(K_tiles, n_iid, dtype, 0, n_iid, scale, out, stream());
+        else
+            launch_grm_extract(K_tiles, n_iid, dtype, ri, nr, ci, nc, order_c, scale, out, stream());
     });
 }
 

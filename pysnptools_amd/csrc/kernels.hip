@@ -1554,6 +1554,69 @@ __global__ __launch_bounds__(kBlock) void k_grm_extract(const T* __restrict__ ti
     }
 }
 
+// Full rows [r0, r0+nr) of K (row-major, n columns, identity column index) from the
+// upper-triangle tiles: one 64x64 output block per workgroup pass, read in its upper-triangle
+// orientation (rows of 64 contiguous tile elements, 16-B loads) into LDS and written row by row
+// with 16-B stores -- through the LDS transpose when the block lies below the diagonal.  The
+// generic k_grm_extract reads the mirrored half one element per 128-element tile row (a 32-B
+// sector per 4-B value): 32 ms for a 50k x 50k f32 K against ~3 ms here.
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_grm_extract_rows(const T* __restrict__ tiles, uint64_t n, uint64_t r0,
+                                                             uint64_t nr, double scale, T* __restrict__ out) {
+    constexpr int V = 16 / sizeof(T);  // elements per 16-B vector
+    constexpr int TPR = 64 / V;        // threads per 64-element row
+    constexpr int RPP = kBlock / TPR;  // rows per pass
+    typedef T vec_t __attribute__((ext_vector_type(V)));
+    __shared__ T S[64][64 + 1];
+    const int t = threadIdx.x, x = t % TPR;
+    const uint64_t rb0 = r0 / 64, nbr = (r0 + nr + 63) / 64 - rb0, nbc = (n + 63) / 64;
+    for (uint64_t b = blockIdx.x; b < nbr * nbc; b += gridDim.x) {
+        const uint64_t R0 = (rb0 + b / nbc) * 64, C0 = (b % nbc) * 64;
+        const uint64_t A0 = R0 < C0 ? R0 : C0, B0 = R0 < C0 ? C0 : R0;
+        for (int y = t / TPR; y < 64; y += RPP) {
+            const uint64_t i = A0 + y, j0 = B0 + (uint64_t)x * V;
+            T v[V];
+            if (A0 != B0 && i < n && j0 + V <= n) {
+                // i < j for the whole block; the V elements sit in one 128-element tile row
+                const vec_t q = *reinterpret_cast<const vec_t*>(
+                    tiles + tile_index(i / kTile, j0 / kTile) * (kTile * kTile) + (i % kTile) * kTile + (j0 % kTile));
+#pragma unroll
+                for (int e = 0; e < V; e++) v[e] = q[e];
+            } else {
+#pragma unroll
+                for (int e = 0; e < V; e++) {
+                    const uint64_t j = j0 + e, ii = i < j ? i : j, jj = i < j ? j : i;
+                    v[e] = (i < n && j < n) ? tiles[tile_index(ii / kTile, jj / kTile) * (kTile * kTile) +
+                                                    (ii % kTile) * kTile + (jj % kTile)]
+                                            : (T)0;
+                }
+            }
+#pragma unroll
+            for (int e = 0; e < V; e++) S[y][x * V + e] = v[e];
+        }
+        __syncthreads();
+        const bool up = R0 <= C0;
+        for (int y = t / TPR; y < 64; y += RPP) {
+            const uint64_t r = R0 + y, c0 = C0 + (uint64_t)x * V;
+            if (r < r0 || r >= r0 + nr || c0 >= n) continue;
+            vec_t w;
+#pragma unroll
+            for (int e = 0; e < V; e++) {
+                const T v = up ? S[y][x * V + e] : S[x * V + e][y];
+                w[e] = scale == 1.0 ? v : (T)((double)v * scale);
+            }
+            T* o = out + (r - r0) * n + c0;
+            if (c0 + V <= n && (reinterpret_cast<uintptr_t>(o) & 15) == 0) {
+                *reinterpret_cast<vec_t*>(o) = w;
+            } else {
+                for (int e = 0; e < V; e++)
+                    if (c0 + e < n) o[e] = w[e];
+            }
+        }
+        __syncthreads();
+    }
+}
+
 template <typename T>
 __global__ __launch_bounds__(kBlock) void k_grm_trace(const T* __restrict__ tiles, uint64_t n, double* trace) {
     __shared__ double red[kBlock / kWave];
@@ -2233,6 +2296,18 @@ void launch_grm_extract(const void* tiles, uint64_t, int dtype, const uint64_t* 
     else
         k_grm_extract<double><<<g, kBlock, 0, st>>>((const double*)tiles, ri, nr, ci, nc, order_c, scale,
                                                     (double*)out);
+    SNPMI_LAUNCH_CHECK();
+}
+
+void launch_grm_extract_rows(const void* tiles, uint64_t n, int dtype, uint64_t r0, uint64_t nr, double scale,
+                             void* out, hipStream_t st) {
+    if (nr == 0 || n == 0) return;
+    const uint64_t blocks = ((r0 + nr + 63) / 64 - r0 / 64) * ((n + 63) / 64);
+    const unsigned g = grid_for(blocks, 1, 256 * 16);
+    if (dtype == SNPMI_DT_F32)
+        k_grm_extract_rows<float><<<g, kBlock, 0, st>>>((const float*)tiles, n, r0, nr, scale, (float*)out);
+    else
+        k_grm_extract_rows<double><<<g, kBlock, 0, st>>>((const double*)tiles, n, r0, nr, scale, (double*)out);
     SNPMI_LAUNCH_CHECK();
 }
 

@@ -152,6 +152,9 @@ void launch_subset(const void* in, int in_dt, uint64_t rows, uint64_t cols, uint
                    void* out, int out_dt, hipStream_t st);
 void launch_transpose_to_f(const void* in, uint64_t rows, uint64_t cols, int dtype, void* out, uint64_t ld,
                            hipStream_t st);
+// rows [r0, r0+nr) of the full K (identity columns), row-major, LDS-transposed mirror half
+void launch_grm_extract_rows(const void* tiles, uint64_t n, int dtype, uint64_t r0, uint64_t nr, double scale,
+                             void* out, hipStream_t st);
 void launch_grm_extract(const void* tiles, uint64_t n, int dtype, const uint64_t* ri, uint64_t nr,
                         const uint64_t* ci, uint64_t nc, int order_c, double scale, void* out, hipStream_t st);
 void launch_grm_trace(const void* tiles, uint64_t n, int dtype, double* trace_dev, hipStream_t st);
