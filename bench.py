@@ -1024,6 +1024,24 @@ def leg_file(N, args):
             "parity": {"check": "K rows 0..%d vs oracle f64 over all %d SNPs; host K == HBM K" % (rows - 1, m),
                        "max_abs_err_over_max_diag": err, "host_equals_hbm": same_k,
                        "pass": err <= 1e-5 and same_k}}
+        # (1b) the same call in float64, the reference's default dtype (snpreader.py:528): int8 CRT SYRK
+        os.environ["ARRAY_MODULE"] = "hbm"
+        bed[:, :2000].read_kernel(Unit())  # warm-up: f64 scratch
+        t0 = time.perf_counter()
+        Kd = bed.read_kernel(Unit())
+        t_hbm64 = time.perf_counter() - t0
+        k64 = np.empty((rows, n), dtype=np.float64)
+        for r in range(rows):
+            N.call("snpmi_memcpy_d2h", N.ptr(k64[r]), ctypes.c_void_p(Kd.val.ptr + r * n * 8), n * 8)
+        del Kd
+        os.environ.pop("ARRAY_MODULE")
+        err64 = float(np.abs(k64 - ref).max() / np.abs(np.diag(ref[:, :rows])).max())
+        out["read_kernel_f64"] = {
+            "call": "Bed(path).read_kernel(Unit())  # float64, the reference's default",
+            "reference": "snpreader.py:528-561,623-668", "seconds_K_in_hbm": t_hbm64,
+            "tflops_K_in_hbm": flops / t_hbm64 / 1e12, "K_GB": n * n * 8 / 1e9,
+            "parity": {"check": "K rows 0..%d vs oracle f64 over all %d SNPs" % (rows - 1, m),
+                       "max_abs_err_over_max_diag": err64, "pass": err64 <= 1e-12}}
         # (2) Bed[:, :10000].read(float32, xp='hbm')
         B = min(10_000, m)
         sub = bed[:, :B]

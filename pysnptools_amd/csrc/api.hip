@@ -60,6 +60,7 @@ Device& device() {
         SNPMI_HIP(hipStreamCreateWithFlags(&d->aux, hipStreamNonBlocking));
         for (hipEvent_t* set : {d->staged, d->consumed, d->produced, d->bounce})
             for (int s = 0; s < 2; s++) SNPMI_HIP(hipEventCreateWithFlags(&set[s], hipEventDisableTiming));
+        for (int s = 0; s < kPieces; s++) SNPMI_HIP(hipEventCreateWithFlags(&d->piece[s], hipEventDisableTiming));
         SNPMI_HIP(hipEventCreateWithFlags(&d->fence, hipEventDisableTiming));
         hipDeviceProp_t p;
         SNPMI_HIP(hipGetDeviceProperties(&p, g_cur_dev));
@@ -107,7 +108,7 @@ void Device::release() {
 
 // pinned staging (two slots so a chunk can be gathered while the previous one uploads)
 static std::mutex g_pin_mutex;
-constexpr int kPinSlots = 6;  // 0/1: H2D staging, 2: stats, 3: unused, 4/5: D2H bounce
+constexpr int kPinSlots = 6 + kPieces;  // 0: encoder, 2: stats, 4/5: D2H bounce, 6..: H2D piece ring
 static void* g_pin[kPinSlots] = {};
 static size_t g_pin_cap[kPinSlots] = {};
 
@@ -242,7 +243,14 @@ struct BedMap {
     size_t size = 0;
     uint64_t bpc = 0;
     ~BedMap() {
-        if (base) munmap((void*)base, size);
+        // unmapping a page-cache mapping of a few GB tears down ~1M page-table entries (~4 ms at
+        // 1.25 GB, measured between the last SYRK and the K extraction, profiles/r03h): every
+        // gather from it has returned, so a large mapping goes away off the call's critical path
+        if (base && size >= (64u << 20)) {
+            std::thread([p = (void*)base, n = size] { munmap(p, n); }).detach();
+        } else if (base) {
+            munmap((void*)base, size);
+        }
         if (fd >= 0) close(fd);
     }
     const uint8_t* column(uint64_t s) const { return base + 3 + s * bpc; }
@@ -323,20 +331,31 @@ static IidPlan plan_iids(Device& d, const uint64_t* iid_idx, uint64_t n_iid, uin
 }
 
 // Upload SNP chunk [c0, c0+cnt) and return the device packed buffer for the selected iids.
-// Chunks alternate between two pinned host buffers and two device buffers (slot = chunk
-// parity).  The H2D runs on the copy stream: it waits only for the kernels that last read
-// this device slot (chunk c-2, event `consumed`), so the upload of chunk c overlaps the
-// kernels of chunk c-1, and the host gathers chunk c+1 from the mmap meanwhile.  The compute
-// stream waits on `staged` before touching the chunk.  Callers record consumed[slot] on the
-// compute stream after the chunk's last kernel (chunk_done).
+// Chunks alternate between two device buffers (slot = chunk parity).  The H2D runs on the copy
+// stream: it waits only for the kernels that last read this device slot (chunk c-2, event
+// `consumed`), so the upload of chunk c overlaps the kernels of chunk c-1.  The compute stream
+// waits on `staged` before touching the chunk.  Callers record consumed[slot] on the compute
+// stream after the chunk's last kernel (chunk_done).
+//
+// The host side goes through a ring of kPieces pinned pieces of <= kPieceBytes (not one pinned
+// buffer per chunk): the host gathers piece q+1 from the mmap while piece q crosses PCIe, and
+// only 4 x 32 MiB is ever pinned -- a first call no longer pays for pinning two chunk-sized
+// buffers (~0.5 GB at 50k iids), and ranks sharing a host hold less locked memory.  The host
+// blocks only when the ring is full, i.e. until chunk c-2's kernels are done.
 static const uint8_t* stage_chunk(Device& d, const BedMap& m, const uint64_t* sid_idx, uint64_t c0, uint64_t cnt,
                                   const IidPlan& p, int nthreads, int slot) {
-    SNPMI_HIP(hipEventSynchronize(d.staged[slot]));  // the pinned slot's previous H2D has finished
-    uint8_t* host = (uint8_t*)pinned(slot, cnt * p.pitch_in);
-    gather_columns(m, sid_idx, c0, cnt, p.pitch_in, host, nthreads);
     uint8_t* dev = (uint8_t*)d.get(slot ? Device::S_PACKED_B : Device::S_PACKED, cnt * p.pitch_in);
     SNPMI_HIP(hipStreamWaitEvent(d.copy, d.consumed[slot], 0));
-    SNPMI_HIP(hipMemcpyAsync(dev, host, cnt * p.pitch_in, hipMemcpyHostToDevice, d.copy));
+    const uint64_t per = std::max<uint64_t>(1, kPieceBytes / p.pitch_in);
+    for (uint64_t q0 = 0; q0 < cnt; q0 += per) {
+        const uint64_t qn = std::min(per, cnt - q0);
+        const int ps = (int)(d.piece_next++ % kPieces);
+        SNPMI_HIP(hipEventSynchronize(d.piece[ps]));  // this pinned piece's previous H2D has finished
+        uint8_t* host = (uint8_t*)pinned(6 + ps, std::min(cnt, per) * p.pitch_in);
+        gather_columns(m, sid_idx, c0 + q0, qn, p.pitch_in, host, nthreads);
+        SNPMI_HIP(hipMemcpyAsync(dev + q0 * p.pitch_in, host, qn * p.pitch_in, hipMemcpyHostToDevice, d.copy));
+        SNPMI_HIP(hipEventRecord(d.piece[ps], d.copy));
+    }
     SNPMI_HIP(hipEventRecord(d.staged[slot], d.copy));
     SNPMI_HIP(hipStreamWaitEvent(d.stream, d.staged[slot], 0));
     if (!p.repack) return dev;
@@ -840,13 +859,10 @@ static bool grm_stream_bed(Device& d, bool first, const char* path, uint64_t n_i
     // the first chunk is an eighth of the others: its gather + upload is the one that cannot hide
     // under a SYRK, the later ones stage while the previous chunk computes
     const uint64_t C1 = std::max<uint64_t>(std::min<uint64_t>(C, 2048), C / 8);
-    if (m_out > C1 && n_out > 0) {  // size both staging slots for a full chunk up front: no regrowth
+    if (m_out > C1 && n_out > 0) {  // size both device slots for a full chunk up front: no regrowth
         const uint64_t cmax = std::min(C, m_out);  // (a free + alloc) between the first two chunks
-        for (int slot = 0; slot < 2; slot++) {
-            SNPMI_HIP(hipEventSynchronize(d.staged[slot]));
-            (void)pinned(slot, cmax * p.pitch_in);
-            (void)d.get(slot ? Device::S_PACKED_B : Device::S_PACKED, cmax * p.pitch_in);
-        }
+        SNPMI_HIP(hipStreamSynchronize(d.copy));
+        for (int slot = 0; slot < 2; slot++) (void)d.get(slot ? Device::S_PACKED_B : Device::S_PACKED, cmax * p.pitch_in);
         if (p.repack) (void)d.get(Device::S_PACKED2, cmax * p.pitch_out);
     }
     for (uint64_t c0 = 0, ci = 0; c0 < m_out && n_out > 0; ci++) {

@@ -60,6 +60,10 @@ inline uint64_t n_tiles_upper(uint64_t n) { uint64_t t = n_tiles_1d(n); return t
 inline size_t dtype_size(int dt) { return dt == SNPMI_DT_F64 ? 8 : dt == SNPMI_DT_F32 ? 4 : 1; }
 
 // ------------------------------------------------------------------ per-device state
+// host -> device staging of file chunks: a ring of kPieces pinned pieces of <= kPieceBytes
+constexpr int kPieces = 4;
+constexpr uint64_t kPieceBytes = 32ull << 20;
+
 struct Device {
     int id = -1;
     hipStream_t stream = nullptr;  // compute: every kernel
@@ -78,6 +82,8 @@ struct Device {
     hipEvent_t produced[2] = {};  // compute stream: output slot written (its D2H may start)
     hipEvent_t bounce[2] = {};    // copy stream: D2H into pinned bounce slot done
     hipEvent_t fence = nullptr;   // compute stream: "all work so far", for a copy to wait on
+    hipEvent_t piece[kPieces] = {};  // copy stream: H2D from pinned piece q done (host may refill it)
+    uint64_t piece_next = 0;         // next piece of the ring (stage_chunk)
     size_t cap[S_NUM] = {};
     // upper-triangle 256-iid block order tables of the dense fp16x2 SYRK, built once per
     // (nb, xcd) and kept on this device (guarded by the device's own mutex)

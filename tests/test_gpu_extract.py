@@ -97,3 +97,37 @@ def test_host_k_in_row_blocks_equals_hbm_k(tmp_path, monkeypatch):
     Z = O.decode_standardize(body, n, m, dtype=np.float64)[0]
     ref = Z[rows].dot(Z.T)
     assert np.abs(Kh[rows] - ref).max() <= 1e-10 * np.abs(np.diag(Kh)).max()
+
+
+@pytest.fixture(scope="module")
+def wide_bed(tmp_path_factory):
+    """A 200k-iid x 24k-SNP .bed (1.2 GB; random codes, 25% missing): GRM calls on it stream 4
+    chunks (2048, 10618, 10618, 716 SNPs at 50 KB per column) through 16 pinned pieces each."""
+    n, m = 200_000, 24_000
+    base = os.path.join(str(tmp_path_factory.mktemp("wide")), "wide")
+    body = np.random.default_rng(9).integers(0, 256, size=m * (n // 4), dtype=np.uint8)
+    with open(base + ".bed", "wb") as f:
+        f.write(bytes([0x6C, 0x1B, 0x01]))
+        f.write(body.tobytes())
+    with open(base + ".fam", "w") as f:
+        f.write("".join("f%d i%d 0 0 0 0\n" % (i, i) for i in range(n)))
+    with open(base + ".bim", "w") as f:
+        f.write("".join("1\ts%d\t0\t%d\tA\tC\n" % (j, j + 1) for j in range(m)))
+    return base, body, n, m
+
+
+@pytest.mark.parametrize("dt,tol", [(np.float32, 1e-5), (np.float64, 1e-10)])
+def test_multi_chunk_file_grm_vs_oracle(wide_bed, dt, tol):
+    """Bed[iids, :].read_kernel(Unit()) over several chunks and pinned pieces (api.hip
+    stage_chunk / grm_stream_bed: 1/8-size first chunk, device-resident stats) vs the oracle's
+    blocked GRM of the same iid subset (snpreader.py:623-668), and the trained stats."""
+    from pysnptools_amd.snpreader import Bed
+    from pysnptools_amd.standardizer import Unit
+
+    base, body, n, m = wide_bed
+    iids = np.arange(0, n, 100)
+    bed = Bed(base + ".bed", count_A1=False)
+    K, trained = bed[iids, :]._read_kernel(Unit(), dtype=dt, return_trained=True)
+    ref, stats = O.grm_from_bed(body, n, m, iid_index=iids.astype(np.uint64), block_size=4096)
+    assert np.abs(K - ref).max() <= tol * np.abs(np.diag(ref)).max()
+    assert np.allclose(trained.stats, stats, rtol=1e-6 if dt == np.float32 else 1e-12, atol=0)
