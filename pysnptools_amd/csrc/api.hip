@@ -295,12 +295,26 @@ static bool is_identity(const uint64_t* idx, uint64_t n, uint64_t bound) {
 }
 
 // Gather SNP columns [c0, c0+cnt) of the selection into `dst` with `pitch` bytes each.
+// g_gather 0: memcpy from the mmap (every 4 KiB page of a fresh mapping faults once);
+// 1: pread() per column into the pinned piece (the kernel copies from the page cache, no faults)
+static int g_gather = 0;
 static void gather_columns(const BedMap& m, const uint64_t* sid_idx, uint64_t c0, uint64_t cnt, uint64_t pitch,
                            uint8_t* dst, int nthreads) {
+    const bool use_pread = g_gather == 1;
     parallel_for(cnt, nthreads, [&](uint64_t j) {
         const uint64_t s = sid_idx ? sid_idx[c0 + j] : c0 + j;
         uint8_t* d = dst + j * pitch;
-        std::memcpy(d, m.column(s), m.bpc);
+        if (use_pread) {
+            size_t got = 0;
+            while (got < m.bpc) {
+                const ssize_t r = pread(m.fd, d + got, m.bpc - got, (off_t)(3 + s * m.bpc + got));
+                if (r <= 0) break;
+                got += (size_t)r;
+            }
+            if (got < m.bpc) std::memcpy(d + got, m.column(s) + got, m.bpc - got);  // short read: the mapping
+        } else {
+            std::memcpy(d, m.column(s), m.bpc);
+        }
         if (pitch > m.bpc) std::memset(d + m.bpc, 0, pitch - m.bpc);
     });
 }
@@ -1236,6 +1250,7 @@ int snpmi_set_kernel_variant(const char* kernel, int variant) {
         else if (std::strcmp(kernel, "dense_chunk") == 0) g_dense_chunk = std::max(variant, 0);
         else if (std::strcmp(kernel, "dense_codes") == 0) g_dense_codes = variant;
         else if (std::strcmp(kernel, "seg") == 0) g_seg_snps = std::max(variant, 0);
+        else if (std::strcmp(kernel, "gather") == 0) g_gather = variant;  // host gather A/B (0 mmap, 1 pread)
         else if (std::strcmp(kernel, "f64") == 0) {
             SNPMI_REQUIRE(variant == 0 || variant == 1, SNPMI_E_ARG, "f64 GRM path: 0 = int8 residues + CRT, 1 = f64 MFMA");
             g_f64_mfma = variant;
