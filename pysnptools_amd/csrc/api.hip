@@ -295,8 +295,9 @@ static bool is_identity(const uint64_t* idx, uint64_t n, uint64_t bound) {
 }
 
 // Gather SNP columns [c0, c0+cnt) of the selection into `dst` with `pitch` bytes each.
-// g_gather 0: memcpy from the mmap (every 4 KiB page of a fresh mapping faults once);
-// 1: pread() per column into the pinned piece (the kernel copies from the page cache, no faults)
+// g_gather 0 (default): memcpy from the mmap; 1: pread() per column into the pinned piece.  A/B on
+// a 50k x 100k file in the page cache (tools/exp_gather.py, profiles/r03j): the full 1.25 GB read
+// into HBM at 37-47 GB/s of packed codes with the mmap vs 32-35 GB/s with pread, so the mmap stays
 static int g_gather = 0;
 static void gather_columns(const BedMap& m, const uint64_t* sid_idx, uint64_t c0, uint64_t cnt, uint64_t pitch,
                            uint8_t* dst, int nthreads) {

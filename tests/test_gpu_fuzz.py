@@ -90,7 +90,8 @@ def test_random_case_vs_oracle(tmp_path, case):
     order = "C" if rng.random() < 0.4 else "F"
     # decode, every dtype
     for dt in (np.float32, np.float64, np.int8):
-        got = sub.read(order=order, dtype=dt).val
+        # int8 stays int8 only with _require_float32_64=False (pstdata.py:139-147 widens it to f64)
+        got = sub.read(order=order, dtype=dt, _require_float32_64=dt != np.int8).val
         exp = O.decode(body, n, m, count_A1=count_a1, iid_index=ii, sid_index=si, order=order, dtype=dt)
         assert got.dtype == exp.dtype
         assert np.array_equal(got, exp, equal_nan=dt != np.int8)
