@@ -998,7 +998,11 @@ def leg_file(N, args):
         bed[:, :2000].read_kernel(Unit(), dtype=np.float32)  # warm-up: scratch + session tiles
         t0 = time.perf_counter()
         Kd = bed.read_kernel(Unit(), dtype=np.float32)
-        t_hbm = time.perf_counter() - t0
+        t_hbm = time.perf_counter() - t0  # the first full-size call (grows the chunk buffers)
+        del Kd
+        t0 = time.perf_counter()
+        Kd = bed.read_kernel(Unit(), dtype=np.float32)
+        t_hbm_warm = time.perf_counter() - t0
         rows = 8
         k_rows = np.empty((rows, n), dtype=np.float32)
         for r in range(rows):
@@ -1020,6 +1024,7 @@ def leg_file(N, args):
         out["read_kernel_f32"] = {
             "call": "Bed(path).read_kernel(Unit(), dtype=np.float32)", "reference": "snpreader.py:528-561,623-668",
             "seconds_K_in_hbm": t_hbm, "tflops_K_in_hbm": flops / t_hbm / 1e12,
+            "seconds_K_in_hbm_warm": t_hbm_warm, "tflops_K_in_hbm_warm": flops / t_hbm_warm / 1e12,
             "seconds_K_to_host": t_host, "tflops_K_to_host": flops / t_host / 1e12, "K_GB": n * n * 4 / 1e9,
             "parity": {"check": "K rows 0..%d vs oracle f64 over all %d SNPs; host K == HBM K" % (rows - 1, m),
                        "max_abs_err_over_max_diag": err, "host_equals_hbm": same_k,
