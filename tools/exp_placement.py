@@ -30,6 +30,9 @@ def main():
     p.add_argument("--plain", type=int, default=6)
     p.add_argument("--sub", type=int, default=4)
     p.add_argument("--contig", type=int, default=2)
+    p.add_argument("--ext-flags", default="", help="comma list of hipExtMallocWithFlags flags to add buffers for "
+                                                   "(1 fine-grained, 3 uncached, 4 contiguous); --per-flag each")
+    p.add_argument("--per-flag", type=int, default=2)
     p.add_argument("--outputs-first", action="store_true")
     p.add_argument("--rounds", type=int, default=4)
     p.add_argument("--reps", type=int, default=5)
@@ -58,6 +61,14 @@ def main():
                 bufs.append(("contiguous_%d" % i, q))
             else:
                 print(json.dumps({"contiguous_alloc_rc": rc}), flush=True)
+        for fl in [int(x) for x in a.ext_flags.split(",") if x]:
+            for i in range(a.per_flag):
+                q = ctypes.c_void_p()
+                rc = hip.hipExtMallocWithFlags(ctypes.byref(q), ctypes.c_size_t(ob), ctypes.c_uint(fl))
+                if rc == 0:
+                    bufs.append(("flags%d_%d" % (fl, i), q))
+                else:
+                    print(json.dumps({"ext_flags": fl, "alloc_rc": rc}), flush=True)
 
     if a.outputs_first:
         alloc_outputs()
