@@ -1,6 +1,8 @@
 """A/B of the host-K page pre-touch (api.hip HostPrefault, hook "prefault": 0 off, 1 on) on
 Bed(path).read_kernel(Unit(), dtype) with K returned as a NumPy array (the reference's default
-return, snpreader.py:623-668) on a synthetic 50k x 100k .bed; alternating, one JSON line per call."""
+return, snpreader.py:623-668) on a synthetic 50k x 100k .bed; alternating, one JSON line per call.
+The hook existed only for this A/B (no effect, profiles/r03j/host_k_prefault_ab.jsonl) and was removed
+from the library afterwards; the script documents how the numbers were taken."""
 import json
 import os
 import sys
