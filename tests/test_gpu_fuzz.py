@@ -66,9 +66,10 @@ def _rel_close(got, exp, tol):
     got = np.asarray(got, dtype=np.float64)
     exp = np.asarray(exp, dtype=np.float64)
     assert got.shape == exp.shape
-    both = np.isnan(got) & np.isnan(exp)
+    both = (np.isnan(got) & np.isnan(exp)) | (got == exp)  # NaN pairs and equal values (incl. inf)
     assert np.array_equal(np.isnan(got), np.isnan(exp))
-    d = np.abs(np.where(both, 0, got - exp))
+    with np.errstate(invalid="ignore"):
+        d = np.abs(np.where(both, 0, got - exp))
     assert np.all(d <= tol * np.maximum(np.abs(np.where(both, 0, exp)), 1e-30) + (0 if tol == 0 else 1e-300))
 
 
@@ -116,3 +117,68 @@ def test_random_case_vs_oracle(tmp_path, case):
         scale = max(np.abs(np.diag(ref)).max(), 1e-300)
         assert K.shape == ref.shape
         assert np.abs(K - ref).max() <= tol * scale, (dt, n, m)
+
+
+DENSE_CASES = 24
+
+
+@pytest.mark.parametrize("case", range(DENSE_CASES))
+def test_random_in_memory_case_vs_oracle(case):
+    """In-memory SnpData (host arrays, the reference's SnpData path): random genotype-valued
+    matrices with NaN (and, every third case, one column of arbitrary floats) in F or C order,
+    f32 / f64:
+
+    * SnpData.standardize(Unit() | Beta(a, b)) (standardizer.py:90-133) vs the oracle's one-pass
+      restatement: Unit bit-exact for genotype-valued matrices (<= 1e-6 / 1e-12 relative with a
+      float column, whose f64 sums depend on the addition order), Beta <= 1e-6 / 1e-12 relative;
+    * SnpData.read_kernel(Unit()) (snpdata.py:190-214 -> snpmi_grm_dense_*: genotype columns
+      re-encoded as codes + LUT, other columns on the dense kernels) and SnpKernel(...).read()
+      .standardize() with DiagKtoN (snpkernel.py, diag_K_to_N.py:54-64) vs the f64 oracle."""
+    from pysnptools_amd.kernelreader import SnpKernel
+    from pysnptools_amd.snpreader import SnpData
+    from pysnptools_amd.standardizer import Beta, Unit
+
+    rng = np.random.default_rng(5000 + case)
+    n = int(rng.choice([2, 3, 17, 64, 129, 300, 1000, 2048]))
+    m = int(rng.choice([1, 3, 16, 40, 129, 300]))
+    dt = np.float32 if rng.random() < 0.5 else np.float64
+    order = "C" if rng.random() < 0.5 else "F"
+    p = rng.uniform(0, 1, size=m)
+    g = rng.binomial(2, p[None, :], size=(n, m)).astype(np.float64)
+    g[rng.random((n, m)) < rng.uniform(0, 0.3)] = np.nan
+    genotype_only = not (case % 3 == 0 and m > 1)
+    if not genotype_only:
+        g[:, m // 2] = rng.normal(0, 3, size=n)  # not genotype-valued
+    val = np.array(g, dtype=dt, order=order)
+    iid = [["f", str(i)] for i in range(n)]
+    sid = [str(j) for j in range(m)]
+    # standardize (in place on a copy, as SnpData.standardize does)
+    exp = np.array(val, dtype=dt, order=order)
+    st = O.standardize_native(exp)
+    d, tr = SnpData(iid=iid, sid=sid, val=np.array(val, order=order)).standardize(Unit(), return_trained=True)
+    if genotype_only:  # integer sums: every summation order gives the same f64 stats
+        assert np.array_equal(d.val, exp, equal_nan=True)
+        assert np.array_equal(np.asarray(tr.stats), st, equal_nan=True)
+    else:  # a float column's f64 sums depend on the order of the additions (last bits)
+        _rel_close(d.val, exp, 1e-6 if dt == np.float32 else 1e-12)
+        _rel_close(tr.stats, st, 1e-6 if dt == np.float32 else 1e-12)
+    a, b = float(rng.uniform(0.5, 3)), float(rng.uniform(0.5, 30))
+    expb = np.array(val, dtype=dt, order=order)
+    O.standardize_native(expb, True, a, b)
+    db = SnpData(iid=iid, sid=sid, val=np.array(val, order=order)).standardize(Beta(a, b))
+    _rel_close(db.val, expb, 1e-6 if dt == np.float32 else 1e-12)
+    # GRM of the in-memory values
+    Z = np.array(val, dtype=np.float64, order="F")
+    O.standardize_native(Z)
+    Z = Z.astype(dt).astype(np.float64)  # the dtype's standardized values, as the GRM sees them
+    ref = Z.dot(Z.T)
+    scale = max(np.abs(np.diag(ref)).max(), 1e-300)
+    tol = 2e-6 if dt == np.float32 else 1e-10
+    sd = SnpData(iid=iid, sid=sid, val=np.array(val, order=order))
+    K = sd.read_kernel(Unit(), dtype=dt).val
+    assert np.abs(K - ref).max() <= tol * scale
+    kd = SnpKernel(sd, Unit()).read(dtype=dt).standardize()  # DiagKtoN
+    tr_ref = np.trace(ref)
+    if tr_ref > 0:
+        assert np.abs(kd.val - ref * (n / tr_ref)).max() <= tol * scale * (n / tr_ref) + 1e-300
+    assert np.array_equal(sd.val, np.array(val, order=order), equal_nan=True)  # input untouched
