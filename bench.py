@@ -100,7 +100,11 @@ def parse(argv=None):
     p.add_argument("--grm-f64", choices=["on", "off"], default="on", help="cfg4 GRM in float64 (reference default)")
     p.add_argument("--grm5", choices=["on", "off"], default="on", help="cfg5 partitioned-K GRM leg")
     p.add_argument("--grm5-iid", type=int, default=500_000)
-    p.add_argument("--grm5-sid", type=int, default=8192)
+    p.add_argument("--grm5-sid", type=int, default=1_000_000, help="cfg5: SNPs of the whole job (all timed)")
+    p.add_argument("--grm5-block", type=int, default=8192, help="cfg5: SNPs per all-gathered block")
+    p.add_argument("--grm5-miss", type=float, default=0.218, help="cfg5: missing rate (SnpGen's 21.8%%)")
+    p.add_argument("--grm5-parity-max-sid", type=int, default=65536,
+                   help="cfg5 at N > 1: the oracle check runs only up to this many SNPs (N = 1: always)")
     p.add_argument("--out-ld", type=int, default=0,
                    help="decode legs: leading dimension (floats) of the timed f32 F-order block buffer; 0 = "
                         "round_up(n, 16), the tight columns the library's reads write")
@@ -110,8 +114,6 @@ def parse(argv=None):
     p.add_argument("--out-ld-c", type=int, default=0,
                    help="C-order decode leg: row pitch (floats) of the output: 0 = the block width (tight rows, "
                         "as the library writes); 32768 = 128 KB rows spread over 64 GB of HBM pages (DESIGN 3.1)")
-    p.add_argument("--grm5-stream", type=int, default=2,
-                   help="cfg5: blocks streamed with the next upload under the current SYRK (0 = off)")
     p.add_argument("--e2e", choices=["on", "off"], default="on", help="pinned-host -> HBM streaming leg")
     p.add_argument("--e2e-sid", type=int, default=8192, help="SNPs held in pinned host memory")
     p.add_argument("--e2e-passes", type=int, default=4)
@@ -603,12 +605,12 @@ def leg_grm(N, args, dist, dtype, keep_tiles=False):
     if my_m:
         synth(N, packed.p, pitch, n, lo, my_m, args.seed + 100, 0.01)
     stats = Dev(N, max(1, my_m) * 2 * esz)
-    collective = args.grm_collective if dist.rccl else "none"
+    collective = args.grm_collective if dist.can_reduce else "none"
     ev = Events(N, 4)
     chunks = (my_m + 65535) // 65536 if my_m else 0
 
     def session():
-        return ShardedGrm(n, npdt, dist if dist.rccl else None, collective, 0, dist.rank, dist.world)
+        return ShardedGrm(n, npdt, dist if dist.can_reduce else None, collective, 0, dist.rank, dist.world)
 
     # warm-up: one 10k-SNP piece (scratch allocations, the session tiles, code objects)
     g = session()
@@ -634,7 +636,7 @@ def leg_grm(N, args, dist, dtype, keep_tiles=False):
         N.call("snpmi_crt_moduli_stats", ctypes.byref(sum_r), ctypes.byref(nlaunch), 1)
         crt_moduli = sum_r.value / max(nlaunch.value, 1)
     syrk_ms = ev.ms(0, 1) if my_m else 0.0
-    coll_ms = ev.ms(1, 2) if dist.rccl else 0.0
+    coll_ms = ev.ms(1, 2) if collective != "none" else 0.0
     tiles, count = g.tiles()
     trace = None
     if g.holds_k():  # the other ranks' tiles are unspecified after an ncclReduce
@@ -732,149 +734,155 @@ def cpu_baseline_grm(args, dtype):
 
 
 # ---------------------------------------------------------------------------- leg 3: cfg5 partitioned GRM
+def grm5_source(N, n, pitch, seed, miss, threads):
+    """This rank's share of a SNP block, generated on host threads straight into the pinned slot
+    (snpmi_host_synth_bed: SnpGen's MAF curve, `miss` missing) -- the stand-in for gathering the
+    columns of a 125 GB .bed from the page cache, which cannot be written to the box's disk."""
+    x, cdf = maf_table(n)
+
+    def fill(host, s0, cnt):
+        N.call("snpmi_host_synth_bed", host, pitch, n, s0, cnt, seed, miss, N.ptr(x), N.ptr(cdf), len(x), threads)
+
+    return fill
+
+
+def grm5_picks(N, n, part, P, nloc):
+    """Sample blocks of the part for the parity check: its first diagonal block, its first
+    off-diagonal block and its last block (the padded iids past n-1 when it ends the matrix)."""
+    want, r0, c0 = {}, ctypes.c_uint64(), ctypes.c_uint64()
+    for b in list(range(min(nloc, 256))) + [nloc - 1]:
+        N.call("snpmi_grm_part_coords", n, part, P, b, ctypes.byref(r0), ctypes.byref(c0))
+        key = "last" if b == nloc - 1 else ("diag" if r0.value == c0.value else "off")
+        if key not in want:
+            want[key] = (b, r0.value, c0.value)
+    return want
+
+
 def leg_grm5(N, args, dist):
-    """configs[4] shape: 500k iids, K (500 GB f32 upper triangle) partitioned as
-    256x256 blocks over the P = max(N, 8) parts of the 8-GPU plan; this process owns part `rank`.
-    One block of --grm5-sid SNPs: each rank uploads ITS 1/N of the packed block from pinned host
-    memory (at N = 1 the whole block), ncclAllGather rebuilds it at N > 1, then stats + the fp16x2
-    SYRK fill only this part's K blocks -- no reduction.  GRM time is linear in M."""
-    n, world = args.grm5_iid, dist.world
+    """configs[4]: 500k iids x 1M SNPs, K (500 GB f32 upper triangle) partitioned
+    as 256x256 blocks over the P = max(N, 8) parts of the 8-GPU plan; this process computes part
+    `rank` over ALL --grm5-sid SNPs through shard.PartitionedGrm (the package's cfg5 session): per
+    block of --grm5-block SNPs each rank generates ITS 1/N share on host threads into a pinned slot,
+    the copy stream uploads it under the previous block's kernels, the RCCL all-gather rebuilds the
+    block at N > 1, then stats + the fp16x2 SYRK add it into this part's K blocks -- no reduction.
+    The timed region is the whole job of this part (at N = 8: the 8-GPU job)."""
+    from pysnptools_amd import hbm
+    from pysnptools_amd.shard import PartitionedGrm
+
+    n, m, world, rank = args.grm5_iid, args.grm5_sid, dist.world, dist.rank
     P = max(world, GRM5_PLAN_WORLD)
-    m = (args.grm5_sid + world - 1) // world * world
-    ms = m // world
+    threads = cpu_threads()
     pitch = N.lib().snpmi_packed_pitch(n)
-    nloc = N.lib().snpmi_grm_part_blocks(n, dist.rank, P)
-    packed = Dev(N, pitch * m)
-    mine = packed.at(dist.rank * ms * pitch)
-    # the rank's share of the .bed, staged in page-locked memory (untimed, like reading the file)
-    host = ctypes.c_void_p()
-    N.call("snpmi_host_alloc", ctypes.byref(host), ms * pitch)
-    synth(N, mine, pitch, n, dist.rank * ms, ms, args.seed + 200, 0.01)
-    N.call("snpmi_memcpy_d2h", host, mine, ms * pitch)
-    N.call("snpmi_dev_memset", packed.p, 0, pitch * m)
-    lut, stats = Dev(N, m * 16), Dev(N, m * 8)
-    blocks = Dev(N, max(nloc, 1) * 256 * 256 * 4)
-    ev = Events(N, 4)
-    N.call("snpmi_stream_sync")
-    dist.barrier()
-    t0 = time.perf_counter()
-    ev.record(0)
-    N.call("snpmi_memcpy_async", mine, host, ms * pitch, 0, 0)
-    ev.record(1)
-    if dist.rccl or dist.world > 1:
-        dist.allgather_dev(mine, packed.p, ms * pitch)
-    ev.record(2)
-    N.call("snpmi_dev_snp_stats", packed.p, pitch, n, m, 0, N.STD_UNIT, 0.0, 0.0, 0, N.DT_F32, stats.p, lut.p)
-    N.call("snpmi_dev_syrk_packed_part", packed.p, pitch, n, m, lut.p, dist.rank, P, blocks.p, 0)
-    ev.record(3)
-    N.call("snpmi_stream_sync")
-    dist.barrier()
-    wall = dist.max(time.perf_counter() - t0)
-    res = {"wall": wall, "h2d_ms": ev.ms(0, 1), "allgather_ms": ev.ms(1, 2), "syrk_ms": ev.ms(2, 3),
-           "n_local_blocks": nloc, "m": m, "ms": ms, "P": P, "pitch": pitch}
-    if dist.rank == 0 and not args.skip_cpu and nloc > 1:
-        picks = []
-        for b in range(min(nloc, 64)):  # block 0 is diagonal; the first off-diagonal one after it
-            r0, c0 = ctypes.c_uint64(), ctypes.c_uint64()
-            N.call("snpmi_grm_part_coords", n, 0, P, b, ctypes.byref(r0), ctypes.byref(c0))
-            if (b == 0) or (r0.value != c0.value and len(picks) == 1):
+    fill = grm5_source(N, n, pitch, args.seed + 200, args.grm5_miss, threads)
+    grp = dist if (world > 1 or dist.rccl) else None  # --force-rccl at N = 1: the real all-gather call, in place
+    # warm-up (untimed): one block through a session of the same shape (code objects, scratch)
+    g = PartitionedGrm(n, min(m, args.grm5_block), N.STD_UNIT, dist=grp, part=rank, parts=P, block=args.grm5_block,
+                       out="hbm")
+    try:
+        g.run(fill)
+    finally:
+        g.close()
+        del g
+    out = hbm.empty((N.lib().snpmi_grm_part_blocks(n, rank, P), 256, 256), dtype=np.float32, order="C")
+    g = PartitionedGrm(n, m, N.STD_UNIT, dist=grp, part=rank, parts=P, block=args.grm5_block, out=out, timing=True)
+    try:
+        N.call("snpmi_stream_sync")
+        dist.barrier()
+        t0 = time.perf_counter()
+        block_ms = g.run(fill)
+        dist.barrier()
+        wall = dist.max(time.perf_counter() - t0)
+        res = {"wall": wall, "block_ms": block_ms, "n_local_blocks": g.nloc, "m": m, "ms": g.ms, "P": P,
+               "pitch": pitch, "blocks": len(block_ms), "threads": threads}
+        if rank == 0 and not args.skip_cpu and (world == 1 or m <= args.grm5_parity_max_sid):
+            picks = grm5_picks(N, n, rank, P, g.nloc)
+            got = {}
+            for key, (b, r0, c0) in picks.items():
                 blk = np.empty((256, 256), dtype=np.float32)
-                N.call("snpmi_memcpy_d2h", N.ptr(blk), blocks.at(b * 256 * 256 * 4), blk.nbytes)
-                picks.append((blk, r0.value, c0.value))
-            if len(picks) == 2:
-                break
-        sample = np.empty((m, pitch), dtype=np.uint8)
-        N.call("snpmi_memcpy_d2h", N.ptr(sample), packed.p, sample.nbytes)
-        # the gathered block must equal the whole block generated in one piece
-        whole = Dev(N, pitch * m)
-        synth(N, whole.p, pitch, n, 0, m, args.seed + 200, 0.01)
-        chk = np.empty_like(sample)
-        N.call("snpmi_memcpy_d2h", N.ptr(chk), whole.p, chk.nbytes)
-        whole.free()
-        res["gather_exact"] = bool(np.array_equal(sample, chk))
-        del chk
-        res["parity_sample"] = (picks, sample)
-    if args.grm5_stream > 0:  # after the parity copies: it accumulates into the same K part
-        res["stream"] = grm5_stream(N, args, dist, host, packed, lut, stats, blocks, n, m, ms, pitch, P)
-    ev.destroy()
-    N.call("snpmi_host_free", host)
-    for d in (packed, lut, stats, blocks):
-        d.free()
+                N.call("snpmi_memcpy_d2h", N.ptr(blk), ctypes.c_void_p(out.snpmi_ptr.value + b * 256 * 256 * 4),
+                       blk.nbytes)
+                got[key] = (blk, r0, c0)
+            res["parity_sample"] = (got, g.stats())
+    finally:
+        g.close()
+        del out
+    if world > 1:  # every rank: the all-gather is collective
+        res["gather_exact"] = grm5_gather_check(N, args, dist, P, fill)
     return res
 
 
-def grm5_stream(N, args, dist, host, packed, lut, stats, blocks, n, m, ms, pitch, P):
-    """The streamed form of the cfg5 job (untimed leg above = one block): K blocks of m SNPs, the
-    rank's share of block k+1 uploaded on the copy stream (its own device buffer, events only) while
-    block k's stats + SYRK run on the compute stream, accumulating into the same K part.  Only the
-    first upload is exposed.  The host share is the same pinned buffer for every block (the same SNPs
-    streamed K times: identical work per block)."""
-    K = args.grm5_stream
-    second = Dev(N, pitch * m)
-    N.call("snpmi_dev_memset", second.p, 0, pitch * m)
-    bufs = [packed, second]
-    up = Events(N, K)  # copy stream: upload k done
-    done = Events(N, K)  # compute stream: SYRK k done (buffer k % 2 free again)
-    ce = Events(N, 2 * K + 1)  # compute stream: block k start (after its upload) / end; [2K] = t0
-    N.call("snpmi_stream_sync")
-    dist.barrier()
-    t0 = time.perf_counter()
-    ce.record(2 * K)
-    for k in range(min(2, K)):
-        N.call("snpmi_memcpy_async", bufs[k].at(dist.rank * ms * pitch), host, ms * pitch, 0, 1)
-        up.record(k, on_copy=1)
-    for k in range(K):
-        buf = bufs[k % 2]
-        N.call("snpmi_stream_wait_event", up.ev[k], 0)
-        ce.record(2 * k)
-        if dist.rccl or dist.world > 1:
-            dist.allgather_dev(buf.at(dist.rank * ms * pitch), buf.p, ms * pitch)
-        N.call("snpmi_dev_snp_stats", buf.p, pitch, n, m, 0, N.STD_UNIT, 0.0, 0.0, 0, N.DT_F32, stats.p, lut.p)
-        N.call("snpmi_dev_syrk_packed_part", buf.p, pitch, n, m, lut.p, dist.rank, P, blocks.p, int(k > 0))
-        ce.record(2 * k + 1)
-        done.record(k)
-        if k + 2 < K:  # refill this buffer once its SYRK has read it
-            N.call("snpmi_stream_wait_event", done.ev[k], 1)
-            N.call("snpmi_memcpy_async", buf.at(dist.rank * ms * pitch), host, ms * pitch, 0, 1)
-            up.record(k + 2, on_copy=1)
-    N.call("snpmi_stream_sync")
-    dist.barrier()
-    wall = dist.max(time.perf_counter() - t0)
-    per_block = [ce.ms(2 * k, 2 * k + 1) for k in range(K)]
-    gaps = [ce.ms(2 * k - 1, 2 * k) for k in range(1, K)]  # compute idle waiting for an upload
-    first = ce.ms(2 * K, 0)  # the first upload (+ all-gather issue), exposed
-    for e in (up, done, ce):
-        e.destroy()
-    second.free()
-    return {"blocks": K, "seconds": wall, "block_ms": per_block, "upload_wait_ms_after_first": gaps,
-            "first_upload_ms": first}
+def grm5_gather_check(N, args, dist, P, fill):
+    """N > 1: one more block through the same plan (each rank's share + all-gather, untimed); rank 0
+    compares the rebuilt block with the block generated whole on its host."""
+    from pysnptools_amd.shard import PartitionedGrm
+
+    n, m = args.grm5_iid, min(args.grm5_sid, args.grm5_block)
+    g = PartitionedGrm(n, m, N.STD_UNIT, dist=dist, part=dist.rank, parts=P, block=args.grm5_block, out="hbm")
+    try:
+        g.run(fill)
+        if dist.rank != 0:
+            return None
+        whole = np.empty((m, g.pitch_src), dtype=np.uint8)
+        fill(ctypes.c_void_p(whole.ctypes.data), 0, m)
+        got = np.empty((m, g.pitch_src), dtype=np.uint8)
+        N.call("snpmi_memcpy_d2h", N.ptr(got), g.dev[0].p, got.nbytes)
+        return bool(np.array_equal(got, whole))
+    finally:
+        g.close()
 
 
-def grm5_parity(args, m, picks, sample):
-    """Oracle (f64) for 256x256 blocks of the partitioned K: stats over every iid, values decoded
-    only for the blocks' 512 iids."""
+def grm5_parity(args, picks, gpu_stats, threads):
+    """Oracle (f64) for sample 256x256 blocks of the partitioned K over ALL the job's SNPs: each
+    block of SNPs is regenerated on the host (the same generator the timed run used), its stats
+    computed over every iid by the oracle (oracle_snp_stats, one-pass from code counts), only the
+    sample blocks' iids decoded + standardized with those stats, and their products accumulated in
+    f64.  Also: the GPU's per-SNP stats (f32) vs the oracle's, bit for bit."""
     from oracle import oracle as O
+    from pysnptools_amd import _native as N
 
-    n = args.grm5_iid
+    n, m, B = args.grm5_iid, args.grm5_sid, args.grm5_block
     bpc = (n + 3) // 4
-    body = np.ascontiguousarray(sample[:, :bpc]).reshape(-1)
-    full_stats = O.snp_stats(body, n, m)
-    out = []
-    worst = 0.0
-    for blk, row0, col0 in picks:
-        rows = np.arange(row0, min(row0 + 256, n))
-        cols = np.arange(col0, min(col0 + 256, n))
-        Zr = O.decode(body, n, m, iid_index=rows)
-        Zc = O.decode(body, n, m, iid_index=cols)
-        O.standardize_native(Zr, use_stats=True, stats=full_stats)
-        O.standardize_native(Zc, use_stats=True, stats=full_stats)
-        ref = Zr.dot(Zc.T)
-        scale = max(np.abs(np.diag(ref)).max() if row0 == col0 else np.abs(ref).max(), 1.0)
-        err = float(np.abs(blk[:len(rows), :len(cols)].astype(np.float64) - ref).max() / scale)
-        worst = max(worst, err)
-        out.append({"row0": int(row0), "col0": int(col0), "max_abs_err_over_scale": err})
-    return {"check": "part 0 blocks (diagonal + off-diagonal) over %d SNPs x %d iids: GPU f32 (fp16x2 MFMA) vs "
-                     "oracle f64" % (m, n), "blocks": out, "max_abs_err_over_scale": worst, "pass": worst <= 1e-5}
+    pitch = bpc if bpc % 4 == 0 else N.lib().snpmi_packed_pitch(n)
+    fill = grm5_source(N, n, pitch, args.seed + 200, args.grm5_miss, threads)
+    sets = {}
+    for key, (_, r0, c0) in picks.items():
+        sets[key] = (np.arange(r0, min(r0 + 256, n)), np.arange(c0, min(c0 + 256, n)))
+    acc = {key: np.zeros((len(rr), len(cc))) for key, (rr, cc) in sets.items()}
+    buf = np.empty((B, pitch), dtype=np.uint8)
+    stats_ok = True
+    t0 = time.perf_counter()
+    for s0 in range(0, m, B):
+        cnt = min(B, m - s0)
+        fill(ctypes.c_void_p(buf.ctypes.data), s0, cnt)
+        body = buf[:cnt] if pitch == bpc else np.ascontiguousarray(buf[:cnt, :bpc])
+        body = body.reshape(-1)
+        st = O.snp_stats(body, n, cnt)
+        stats_ok &= bool(np.array_equal(st.astype(np.float32), gpu_stats[s0:s0 + cnt]))
+        for key, (rr, cc) in sets.items():
+            Zr = O.decode(body, n, cnt, iid_index=rr)
+            O.standardize_native(Zr, use_stats=True, stats=st)
+            if np.array_equal(rr, cc):
+                acc[key] += Zr.dot(Zr.T)
+            else:
+                Zc = O.decode(body, n, cnt, iid_index=cc)
+                O.standardize_native(Zc, use_stats=True, stats=st)
+                acc[key] += Zr.dot(Zc.T)
+    out, worst, diag_scale = [], 0.0, 1.0
+    for key, (blk, r0, c0) in picks.items():
+        if r0 == c0:
+            diag_scale = max(diag_scale, float(np.abs(np.diag(acc[key])).max()))
+    for key, (blk, r0, c0) in picks.items():
+        ref = acc[key]
+        err = float(np.abs(blk[:ref.shape[0], :ref.shape[1]].astype(np.float64) - ref).max())
+        rel = err / diag_scale
+        worst = max(worst, rel)
+        out.append({"block": key, "row0": int(r0), "col0": int(c0), "max_abs_err": err,
+                    "max_abs_err_over_max_diag": rel})
+    return {"check": "part blocks (first diagonal, first off-diagonal, last) over all %d SNPs x %d iids: GPU f32 "
+                     "(fp16x2 MFMA, %d-SNP blocks accumulated in HBM) vs oracle f64 (stats over every iid, "
+                     "products accumulated per SNP block)" % (m, n, B),
+            "blocks": out, "max_abs_err_over_max_diag": worst, "stats_bit_exact": stats_ok,
+            "oracle_seconds": time.perf_counter() - t0, "pass": worst <= 1e-5 and stats_ok}
 
 
 def input_sha256(sample, n):
@@ -937,11 +945,14 @@ def grm_entry(args, dist, r, dtype):
                           "timed span"}
     roof.update(per_launch)
     coll = {"reduce": "ncclReduce(sum, root 0)", "allreduce": "ncclAllReduce(sum)"}.get(r["collective"])
+    if coll and not dist.rccl:
+        coll = "host-staged %s (rehearsal group)" % r["collective"]
     return {"workload": "cfg4: %d iid x %d SNP, Unit, %s SYRK; SNPs split into %d contiguous shard(s), each "
                         "accumulated through shard.ShardedGrm in launches of <= 65536 SNPs (the reference's block_size "
                         "%d bounds host memory, snpreader.py:651)%s"
                         % (n, m, "f32 (fp16x2 MFMA)" if f32 else "f64 (int8 MFMA residues + CRT)", dist.world,
-                           args.grm_block, (", RCCL %s of the K tiles" % coll) if coll else ""),
+                           args.grm_block, (", %s%s of the K tiles" % ("RCCL " if dist.rccl else "", coll))
+                           if coll else ""),
             "gflops": gf, "snps_per_s": m / r["wall"], "seconds": r["wall"], "scaling": "strong",
             "collective": coll, "allreduce_ms": r["allreduce_ms"], "trace_K": r["trace"], "roofline": roof}
 
@@ -1165,38 +1176,37 @@ def main(argv=None):
         r3 = leg_grm5(N, args, dist)
         n5, m5, P = args.grm5_iid, r3["m"], r3["P"]
         flops_part = n5 * (n5 + 1) * m5 / P  # this part's share of the SYRK work
-        syrk_tf = flops_part / (r3["syrk_ms"] * 1e-3) / 1e12
-        grm5 = {"workload": "cfg5: %d iid x %d SNP (one block of the 1M), Unit, f32 (fp16x2 MFMA); K as 256x256 "
-                            "blocks in %d parts (the 8-GPU plan), this process = part %d; the packed block comes "
-                            "from pinned host memory inside the timed region (%d upload(s) of %d SNPs%s), no "
-                            "reduction" % (n5, m5, P, dist.rank, 1, r3["ms"],
-                                           " + RCCL all-gather" if dist.rccl else
-                                           (" + host all-gather (rehearsal group)" if dist.world > 1 else "")),
-                "h2d_ms": r3["h2d_ms"], "h2d_GBps": r3["ms"] * r3["pitch"] / (r3["h2d_ms"] * 1e-3) / 1e9,
-                "allgather_ms": r3["allgather_ms"], "syrk_ms": r3["syrk_ms"], "syrk_tflops": syrk_tf,
-                "seconds": r3["wall"], "gflops_per_gpu": flops_part / r3["wall"] / 1e9,
+        busy_s = sum(r3["block_ms"]) * 1e-3
+        syrk_tf = flops_part / busy_s / 1e12
+        gather = (" + RCCL all-gather" if dist.rccl else
+                  (" + host all-gather (rehearsal group)" if dist.world > 1 else ""))
+        grm5 = {"workload": "cfg5: %d iid x %d SNP, Unit, f32 (fp16x2 MFMA), %.1f%% missing; K as 256x256 blocks in "
+                            "%d parts (the 8-GPU plan), this process = part %d; all %d blocks of %d SNPs timed: each "
+                            "rank's 1/%d share generated on %d host threads into pinned memory, uploaded on the copy "
+                            "stream under the previous block's SYRK%s, stats + SYRK into the part's blocks in HBM "
+                            "(shard.PartitionedGrm); no reduction"
+                            % (n5, m5, 100 * args.grm5_miss, P, dist.rank, r3["blocks"], args.grm5_block, dist.world,
+                               r3["threads"], gather),
+                "seconds": r3["wall"], "blocks": r3["blocks"], "gpu_busy_seconds": busy_s,
+                "exposed_wait_seconds": max(0.0, r3["wall"] - busy_s),
+                "block_ms_mean": float(np.mean(r3["block_ms"])), "block_ms_first": r3["block_ms"][0],
+                "block_ms_max": float(np.max(r3["block_ms"])),
+                "gflops_per_gpu": flops_part / r3["wall"] / 1e9, "syrk_tflops": syrk_tf,
                 "snps_per_s": m5 / r3["wall"], "parts": P, "scaling": "strong",
+                "job_note": "the P parts run concurrently on P GPUs at N = P, so `seconds` is the 8-GPU job time at "
+                            "N = 8; at N = 1 it is one part's share of that job, measured whole",
                 "blocks_on_rank0": r3["n_local_blocks"], "K_bytes_per_rank": r3["n_local_blocks"] * 256 * 256 * 4,
                 "roofline": {"bound": "mfma", "achieved": syrk_tf, "peak": SPLIT_PEAK_TFLOPS, "unit": "TFLOP/s",
                              "frac": syrk_tf / SPLIT_PEAK_TFLOPS, "traffic": None,
                              "kernel": "f32w::k_syrk_h2<true,4> (fp16x2 split, 3 fp16 MFMA products, f32 "
-                                       "accumulate), this part's blocks only"},
-                "projected_seconds_1M_snps": r3["wall"] * 1_000_000 / m5,
-                "projected_note": "per process; the 8 parts run concurrently on 8 GPUs, so this is the 8-GPU "
-                                  "job time when N = 8, and N = 1 shows one part's share"}
-        if r3.get("stream"):
-            st5 = r3["stream"]
-            first = st5["first_upload_ms"] * 1e-3
-            grm5["streamed"] = {
-                "workload": "%d blocks of %d SNPs: block k+1's upload (copy stream, own buffer) under block k's "
-                            "stats + SYRK (compute stream), accumulating into this part's K" % (st5["blocks"], m5),
-                "blocks": st5["blocks"], "seconds": st5["seconds"], "block_ms": st5["block_ms"],
-                "upload_wait_ms_after_first": st5["upload_wait_ms_after_first"],
-                "exposed_first_upload_ms": first * 1e3,
-                "snps_per_s": st5["blocks"] * m5 / st5["seconds"],
-                "projected_seconds_1M_snps": first + np.mean(st5["block_ms"]) * 1e-3 * 1_000_000 / m5}
+                                       "accumulate), this part's blocks only; time = the blocks' compute-stream "
+                                       "spans (stats + SYRK%s)" % (" + all-gather" if gather else "")}}
         if r3.get("parity_sample") is not None:
-            grm5["parity"] = grm5_parity(args, m5, *r3["parity_sample"])
+            grm5["parity"] = grm5_parity(args, r3["parity_sample"][0], r3["parity_sample"][1], r3["threads"])
+        elif dist.rank == 0:
+            grm5["parity"] = {"check": "skipped at N > 1 for %d SNPs (> --grm5-parity-max-sid): part 0 of the same "
+                                       "8-part plan is checked over all SNPs at N = 1" % m5, "pass": True}
+        if dist.rank == 0 and r3.get("gather_exact") is not None:
             grm5["parity"]["gathered_block_bit_exact"] = r3["gather_exact"]
             grm5["parity"]["pass"] = grm5["parity"]["pass"] and r3["gather_exact"]
     if dist.rank == 0 and args.file == "on":
@@ -1249,9 +1259,9 @@ def main(argv=None):
                        "n_iid": n, "n_sid": args.n_sid, "n_sid_per_gpu": r1["m"], "block": args.block,
                        "block_buffer_ld": r1["out_ld"],
                        "parallelism": "snp-shard x%d" % dist.world,
-                       "process_group": "rccl" if dist.rccl else ("host rehearsal (SNPMI_DIST_HOST: gloo barriers, "
-                                                                  "ranks share one GPU, no device reduce)"
-                                                                  if dist.world > 1 else "none")},
+                       "process_group": "rccl" if dist.rccl else ("host rehearsal (SNPMI_DIST_HOST: socket barriers, "
+                                                                  "ranks share one GPU, host-staged sums and "
+                                                                  "all-gathers)" if dist.world > 1 else "none")},
             "weak": ({"value": args.n_sid * args.steps * dist.world / r1["weak_wall"], "unit": "SNPs/s",
                       "workload": "every rank streams 1M SNPs per step (its shard %d times)" % dist.world}
                      if r1["weak_wall"] else None),

@@ -91,6 +91,7 @@ int snpmi_device_info(int device, char* name, size_t name_len, uint64_t* total_m
  * residues + CRT, 1 = on the f64 MFMA), "seg" (SNPs per f32 GRM accumulation chain, default 8192,
  * 0 = one chain per launch).  The rest ("decode", "syrk", ...) are A/B hooks for benches. */
 int snpmi_set_kernel_variant(const char* kernel, int variant);
+int snpmi_get_kernel_variant(const char* kernel, int* variant);  /* current value of a hook above */
 
 /* ---------------------------------------------------------------- BED reading (bed-reader read_*) */
 int snpmi_bed_check(const char* path, uint64_t n_iid, uint64_t n_sid);
@@ -259,6 +260,15 @@ int snpmi_event_sync(void* ev);
 int snpmi_dev_synth_bed(uint8_t* packed, uint64_t pitch, uint64_t n_iid, uint64_t sid0, uint64_t n_sid,
                         uint64_t seed, double miss_rate, const double* maf_x, const double* maf_cdf,
                         int n_pts);
+/* the same workload on host threads (streamed cfg5 legs): SNPs [sid0, sid0+n_sid) with the MAF
+ * table of snpmi_dev_synth_bed, one 32-bit hash per genotype (a different stream than the device
+ * generator, same distribution) */
+int snpmi_host_synth_bed(uint8_t* dst, uint64_t pitch, uint64_t n_iid, uint64_t sid0, uint64_t n_sid, uint64_t seed,
+                         double miss_rate, const double* maf_x, const double* maf_cdf, int n_pts, int num_threads);
+/* selected .bed columns (all iids) into a host buffer at `pitch` bytes per column (zero pad) --
+ * the gather half of the file readers (bed.py:337-343), for the cfg5 plan's per-rank shares */
+int snpmi_bed_gather_packed(const char* path, uint64_t n_iid, uint64_t n_sid, const uint64_t* sid_idx, uint64_t n_sel,
+                            uint64_t pitch, uint8_t* dst, int num_threads);
 /* per-SNP code counts -> stats [n_sid][2] (dtype) and value LUT [n_sid][4] (dtype) */
 int snpmi_dev_snp_stats(const uint8_t* packed, uint64_t pitch, uint64_t n_iid, uint64_t n_sid,
                         int count_a1, int std_kind, double a, double b, int use_stats, int dtype,

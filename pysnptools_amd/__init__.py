@@ -38,3 +38,7 @@ if _os.environ.get("PST_F64_GRM"):
         set_grm_f64(_os.environ["PST_F64_GRM"])
     except ImportError:  # no HIP library: every compute call raises anyway
         pass
+    except ValueError as _e:  # a bad value must not break CPU-only imports
+        import warnings as _warnings
+
+        _warnings.warn("PST_F64_GRM=%r ignored: %s" % (_os.environ["PST_F64_GRM"], _e))

@@ -33,6 +33,7 @@ _SIGS = {
     "snpmi_device_info": [_i32, ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_uint64),
                           ctypes.POINTER(ctypes.c_int)],
     "snpmi_set_kernel_variant": [_cp, _i32],
+    "snpmi_get_kernel_variant": [_cp, ctypes.POINTER(ctypes.c_int)],
     "snpmi_bed_check": [_cp, _u64, _u64],
     "snpmi_bed_read_f32": [_cp, _u64, _u64, _i32, _vp, _u64, _vp, _u64, _i32, _vp, _i32],
     "snpmi_bed_read_f64": [_cp, _u64, _u64, _i32, _vp, _u64, _vp, _u64, _i32, _vp, _i32],
@@ -94,6 +95,8 @@ _SIGS = {
     "snpmi_stream_wait_event": [_vp, _i32],
     "snpmi_event_sync": [_vp],
     "snpmi_dev_synth_bed": [_vp, _u64, _u64, _u64, _u64, _u64, _f64, _vp, _vp, _i32],
+    "snpmi_host_synth_bed": [_vp, _u64, _u64, _u64, _u64, _u64, _f64, _vp, _vp, _i32, _i32],
+    "snpmi_bed_gather_packed": [_cp, _u64, _u64, _vp, _u64, _u64, _vp, _i32],
     "snpmi_dev_snp_stats": [_vp, _u64, _u64, _u64, _i32, _i32, _f64, _f64, _i32, _i32, _vp, _vp],
     "snpmi_dev_decode": [_vp, _u64, _u64, _u64, _vp, _i32, _i32, _vp, _u64],
     "snpmi_dev_decode_standardize": [_vp, _u64, _u64, _u64, _i32, _i32, _f64, _f64, _i32, _i32, _vp, _vp, _vp, _u64],
@@ -181,6 +184,13 @@ def check(rc):
 
 def call(name, *args):
     check(getattr(lib(), name)(*args))
+
+
+def kernel_variant(name):
+    """Current value of a ``snpmi_set_kernel_variant`` switch (e.g. "f64", "seg")."""
+    v = ctypes.c_int(0)
+    call("snpmi_get_kernel_variant", name.encode() if isinstance(name, str) else name, ctypes.byref(v))
+    return v.value
 
 
 def device_count():

@@ -37,7 +37,11 @@ def _digest(idx):
 
 def _fingerprint(bed_path, n, m, dtype, block_size, kind, a, b, use_stats, rows, cols, count_a1, stats_in):
     st = os.stat(bed_path)
-    return {"bed": os.path.abspath(bed_path), "size": st.st_size, "mtime_ns": st.st_mtime_ns, "n": int(n),
+    # the accumulation settings of this process: partial sums of another f64 path (CRT vs f64
+    # MFMA) or another f32 chain length would not resume bit-identically
+    settings = ({"f64_path": N.kernel_variant("f64")} if np.dtype(dtype) == np.float64
+                else {"f32_seg": N.kernel_variant("seg")})
+    return {"settings": settings, "bed": os.path.abspath(bed_path), "size": st.st_size, "mtime_ns": st.st_mtime_ns, "n": int(n),
             "m": int(m), "dtype": np.dtype(dtype).str, "block_size": int(block_size), "kind": int(kind),
             "a": None if np.isnan(a) else float(a), "b": None if np.isnan(b) else float(b),
             "use_stats": bool(use_stats), "count_A1": bool(count_a1), "rows": _digest(rows), "cols": _digest(cols),
@@ -52,20 +56,50 @@ def _gen_paths(path, gen):
     return "%s.g%d.tiles.npy" % (path, gen), "%s.g%d.stats.npy" % (path, gen)
 
 
-def _sha1_file(p):
-    h = hashlib.sha1()
+class _HashingWriter(object):
+    """File wrapper that SHA-1s every byte written through it (np.save writes the header and then
+    the data in chunks through ``write`` for a non-file object), so the hash comes from memory
+    instead of re-reading a multi-GB file."""
+
+    def __init__(self, f):
+        self.f, self.h = f, hashlib.sha1()
+
+    def write(self, b):
+        self.h.update(b)
+        return self.f.write(b)
+
+
+class _HashingReader(object):
+    """The read-side twin: ``np.lib.format.read_array`` reads a non-file object sequentially
+    through ``read``, so the hash of a checkpoint file comes from the one pass that loads it."""
+
+    def __init__(self, f):
+        self.f, self.h = f, hashlib.sha1()
+
+    def read(self, n=-1):
+        b = self.f.read(n)
+        self.h.update(b)
+        return b
+
+
+def _load_npy(p):
+    """(array, SHA-1 of the file, bytes after the array) in one read of ``p``."""
     with open(p, "rb") as f:
-        for chunk in iter(lambda: f.read(1 << 24), b""):
-            h.update(chunk)
-    return h.hexdigest()
+        r = _HashingReader(f)
+        arr = np.lib.format.read_array(r, allow_pickle=False)
+        rest = r.read()  # read_array stops at the data's end; a longer file must not pass
+    return arr, r.h.hexdigest(), len(rest)
 
 
 def _write_npy(p, arr):
+    """Write ``arr`` as .npy at ``p`` (temp file + fsync + rename); returns the file's SHA-1."""
     with open(p + ".tmp", "wb") as f:
-        np.save(f, arr, allow_pickle=False)
+        w = _HashingWriter(f)
+        np.save(w, arr, allow_pickle=False)
         f.flush()
         os.fsync(f.fileno())
     os.replace(p + ".tmp", p)
+    return w.h.hexdigest()
 
 
 def _session_tiles():
@@ -89,10 +123,10 @@ def _save(path, meta, next_block, stats, dtype):
     N.call("snpmi_stream_sync")
     N.call("snpmi_memcpy_d2h", N.ptr(host), tiles, host.nbytes)
     tpath, spath = _gen_paths(path, next_block)
-    _write_npy(tpath, host)
-    _write_npy(spath, np.ascontiguousarray(stats))
+    tsha = _write_npy(tpath, host)
+    ssha = _write_npy(spath, np.ascontiguousarray(stats))
     files = {"tiles": os.path.basename(tpath), "stats": os.path.basename(spath),
-             "tiles_sha1": _sha1_file(tpath), "stats_sha1": _sha1_file(spath)}
+             "tiles_sha1": tsha, "stats_sha1": ssha}
     with open(jpath + ".tmp", "w") as f:
         json.dump(dict(meta, next_block=int(next_block), files=files), f)
         f.flush()
@@ -121,16 +155,22 @@ def _restore(path, meta, dtype):
     if not files:
         raise ValueError("checkpoint '%s' names no tile files" % path)
     tpath, spath = os.path.join(d, files["tiles"]), os.path.join(d, files["stats"])
+    loaded = []
     for p, key in ((tpath, "tiles_sha1"), (spath, "stats_sha1")):
-        if not os.path.exists(p) or _sha1_file(p) != files[key]:
+        try:
+            arr, sha, extra = _load_npy(p)
+        except (OSError, ValueError):
+            arr, sha, extra = None, None, 0
+        if arr is None or extra or sha != files[key]:
             raise ValueError("checkpoint '%s': %s is missing or does not match its recorded hash" % (path, p))
-    host = np.load(tpath, allow_pickle=False)
+        loaded.append(arr)
+    host, stats_saved = loaded
     tiles, count = _session_tiles()
     if host.dtype != np.dtype(dtype) or host.size != count:
         raise ValueError("checkpoint '%s' tiles do not match this GRM" % path)
     N.call("snpmi_memcpy_h2d", tiles, N.ptr(host), host.nbytes)
     N.call("snpmi_stream_sync")
-    return nb, np.load(spath, allow_pickle=False)
+    return nb, stats_saved
 
 
 def _remove_all(path):

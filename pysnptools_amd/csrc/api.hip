@@ -8,6 +8,7 @@
 // The packed codes are 16x (f32) / 32x (f64) smaller than the values, so only packed bytes
 // cross PCIe on the way in.
 #include <fcntl.h>
+#include <immintrin.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
 #include <unistd.h>
@@ -1235,6 +1236,7 @@ int snpmi_set_kernel_variant(const char* kernel, int variant) {
     return guarded([&] {
         SNPMI_REQUIRE(kernel != nullptr, SNPMI_E_ARG, "kernel name is NULL");
         if (std::strcmp(kernel, "decode") == 0) g_variant_decode = variant;
+        else if (std::strcmp(kernel, "std") == 0) g_variant_std = variant;
         else if (std::strcmp(kernel, "syrk") == 0) {
 #ifndef SNPMI_UBENCH
             // the product library ships the default chain and the kernels it falls back to:
@@ -1256,6 +1258,22 @@ int snpmi_set_kernel_variant(const char* kernel, int variant) {
             SNPMI_REQUIRE(variant == 0 || variant == 1, SNPMI_E_ARG, "f64 GRM path: 0 = int8 residues + CRT, 1 = f64 MFMA");
             g_f64_mfma = variant;
         }
+        else throw Error(SNPMI_E_ARG, std::string("unknown kernel ") + kernel);
+    });
+}
+
+int snpmi_get_kernel_variant(const char* kernel, int* variant) {
+    return guarded([&] {
+        SNPMI_REQUIRE(kernel != nullptr && variant != nullptr, SNPMI_E_ARG, "kernel name or output is NULL");
+        if (std::strcmp(kernel, "decode") == 0) *variant = g_variant_decode;
+        else if (std::strcmp(kernel, "std") == 0) *variant = g_variant_std;
+        else if (std::strcmp(kernel, "syrk") == 0) *variant = g_variant_syrk;
+        else if (std::strcmp(kernel, "syrk_split") == 0) *variant = g_variant_syrk_split;
+        else if (std::strcmp(kernel, "dense_chunk") == 0) *variant = g_dense_chunk;
+        else if (std::strcmp(kernel, "dense_codes") == 0) *variant = g_dense_codes;
+        else if (std::strcmp(kernel, "seg") == 0) *variant = g_seg_snps;
+        else if (std::strcmp(kernel, "gather") == 0) *variant = g_gather;
+        else if (std::strcmp(kernel, "f64") == 0) *variant = g_f64_mfma;
         else throw Error(SNPMI_E_ARG, std::string("unknown kernel ") + kernel);
     });
 }
@@ -1610,6 +1628,142 @@ int snpmi_dev_synth_bed(uint8_t* packed, uint64_t pitch, uint64_t n_iid, uint64_
         SNPMI_HIP(hipMemcpyAsync(tab + n_pts, maf_cdf, n_pts * 8, hipMemcpyHostToDevice, d.stream));
         launch_synth(packed, pitch, n_iid, sid0, n_sid, seed, miss_rate, tab, tab + n_pts, n_pts, d.stream);
         SNPMI_HIP(hipStreamSynchronize(d.stream));
+    });
+}
+
+// ---------------------------------------------------------------------- host-side synthetic source
+// A stand-in for "gather the selected .bed columns from the page cache into pinned memory" when a
+// workload is too large to write to disk (cfg5: 125 GB of packed codes): the streamed GRM legs
+// generate each SNP block on host threads while the GPU works on the previous one.  Per SNP the
+// MAF comes from the same counter hash and MAF table as k_synth; per genotype one 32-bit hash
+// (lowbias32 of seed/SNP key ^ iid * golden ratio) split into missing / hom-alt / het / hom-ref
+// with the joint probabilities miss, (1-miss) p^2, (1-miss) 2p(1-p), rest -- k_synth's
+// distribution, a cheaper stream (AVX2 when the host has it).  Restated in NumPy by
+// tests/test_host_synth.py.
+namespace {
+inline uint64_t h_splitmix64(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+inline uint32_t lowbias32(uint32_t x) {
+    x ^= x >> 16;
+    x *= 0x7feb352du;
+    x ^= x >> 15;
+    x *= 0x846ca68bu;
+    x ^= x >> 16;
+    return x;
+}
+struct SynthCol {
+    uint32_t kb, thm, t3, t2;
+};
+inline uint32_t synth_code(uint32_t u, const SynthCol& c) {
+    const uint32_t a = u - c.thm;
+    return u < c.thm ? 1u : a < c.t3 ? 3u : a - c.t3 < c.t2 ? 2u : 0u;
+}
+// packed words [d0, d0+nw) of one column (16 iids per word; iids >= n are 0)
+void synth_words_scalar(uint32_t* w, uint64_t d0, uint64_t nw, uint64_t n, const SynthCol& c) {
+    for (uint64_t q = 0; q < nw; q++) {
+        uint32_t x = 0;
+        for (uint32_t k = 0; k < 16; k++) {
+            const uint64_t i = 16 * (d0 + q) + k;
+            if (i >= n) break;
+            x |= synth_code(lowbias32(c.kb ^ ((uint32_t)i * 0x9E3779B9u)), c) << (2 * k);
+        }
+        w[q] = x;
+    }
+}
+__attribute__((target("avx2"))) void synth_words_avx2(uint32_t* w, uint64_t d0, uint64_t nw, uint64_t n,
+                                                      const SynthCol& c) {
+    const __m256i sgn = _mm256_set1_epi32((int)0x80000000u);
+    const __m256i vkb = _mm256_set1_epi32((int)c.kb), G = _mm256_set1_epi32((int)0x9E3779B9u);
+    const __m256i M1 = _mm256_set1_epi32(0x7feb352d), M2 = _mm256_set1_epi32((int)0x846ca68bu);
+    const __m256i thm_s = _mm256_set1_epi32((int)(c.thm ^ 0x80000000u)), t3_s = _mm256_set1_epi32((int)(c.t3 ^ 0x80000000u)),
+                  t2_s = _mm256_set1_epi32((int)(c.t2 ^ 0x80000000u)), thm = _mm256_set1_epi32((int)c.thm),
+                  t3 = _mm256_set1_epi32((int)c.t3), two = _mm256_set1_epi32(2), three = _mm256_set1_epi32(3),
+                  one = _mm256_set1_epi32(1);
+    const __m256i lane = _mm256_setr_epi32(0, 16, 32, 48, 64, 80, 96, 112);
+    const uint64_t full = std::min<uint64_t>(nw, n / 16 > d0 ? n / 16 - d0 : 0);  // words with 16 real iids
+    uint64_t q = 0;
+    for (; q + 8 <= full; q += 8) {
+        __m256i i = _mm256_add_epi32(_mm256_set1_epi32((int)(uint32_t)(16 * (d0 + q))), lane);
+        __m256i x = _mm256_setzero_si256();
+        for (int k = 0; k < 16; k++) {
+            __m256i h = _mm256_xor_si256(vkb, _mm256_mullo_epi32(i, G));
+            h = _mm256_xor_si256(h, _mm256_srli_epi32(h, 16));
+            h = _mm256_mullo_epi32(h, M1);
+            h = _mm256_xor_si256(h, _mm256_srli_epi32(h, 15));
+            h = _mm256_mullo_epi32(h, M2);
+            h = _mm256_xor_si256(h, _mm256_srli_epi32(h, 16));
+            const __m256i miss = _mm256_cmpgt_epi32(thm_s, _mm256_xor_si256(h, sgn));  // u < thm (unsigned)
+            const __m256i a = _mm256_sub_epi32(h, thm);
+            const __m256i hom = _mm256_cmpgt_epi32(t3_s, _mm256_xor_si256(a, sgn));
+            const __m256i het = _mm256_cmpgt_epi32(t2_s, _mm256_xor_si256(_mm256_sub_epi32(a, t3), sgn));
+            __m256i code = _mm256_and_si256(het, two);
+            code = _mm256_blendv_epi8(code, three, hom);
+            code = _mm256_blendv_epi8(code, one, miss);
+            x = _mm256_or_si256(x, _mm256_sll_epi32(code, _mm_cvtsi32_si128(2 * k)));
+            i = _mm256_add_epi32(i, one);
+        }
+        _mm256_storeu_si256((__m256i*)(w + q), x);
+    }
+    if (q < nw) synth_words_scalar(w + q, d0 + q, nw - q, n, c);
+}
+}  // namespace
+
+int snpmi_host_synth_bed(uint8_t* dst, uint64_t pitch, uint64_t n_iid, uint64_t sid0, uint64_t n_sid, uint64_t seed,
+                         double miss_rate, const double* maf_x, const double* maf_cdf, int n_pts, int num_threads) {
+    return guarded([&] {
+        SNPMI_REQUIRE(dst != nullptr || n_sid == 0, SNPMI_E_ARG, "dst is NULL");
+        SNPMI_REQUIRE(pitch % 4 == 0 && pitch >= ceil_div(n_iid, 4), SNPMI_E_ARG, "bad pitch");
+        SNPMI_REQUIRE(n_pts > 0 && n_pts <= 1024 && maf_x && maf_cdf, SNPMI_E_ARG, "bad MAF table");
+        SNPMI_REQUIRE(n_iid < (1ull << 32), SNPMI_E_ARG, "host synth: n_iid must be < 2^32");
+        const bool avx2 = __builtin_cpu_supports("avx2");
+        const uint64_t nd = pitch / 4, per = 2048;  // words per work item (32 KiB of codes)
+        const uint64_t items_per_col = ceil_div(nd, per);
+        const double sc = 4294967296.0;
+        auto thr = [&](double t) { return t >= sc ? 0xFFFFFFFFu : (uint32_t)t; };
+        parallel_for(
+            n_sid * items_per_col, resolve_threads(num_threads),
+            [&](uint64_t it) {
+                const uint64_t j = it / items_per_col, d0 = (it % items_per_col) * per;
+                const uint64_t sid = sid0 + j;
+                const uint64_t h = h_splitmix64(seed * 0xD1B54A32D192ED03ull ^ (sid + 1) * 0x8CB92BA72F3D8DD7ull);
+                const double u = (double)(h >> 11) * (1.0 / 9007199254740992.0);
+                int lo = 0, hi = n_pts - 1;
+                while (lo < hi) {
+                    const int mid = (lo + hi) >> 1;
+                    if (u > maf_cdf[mid]) lo = mid + 1;
+                    else hi = mid;
+                }
+                const double maf = maf_x[lo], keep = 1.0 - miss_rate;
+                SynthCol c;
+                c.kb = (uint32_t)(h_splitmix64((seed + 0x632BE59BD9B4E019ull) ^ (sid * 0x9E6C63D0676A9A99ull)) >> 32);
+                c.thm = thr(miss_rate * sc);
+                c.t3 = thr(keep * maf * maf * sc);
+                c.t2 = thr(keep * 2.0 * maf * (1.0 - maf) * sc);
+                uint32_t* w = reinterpret_cast<uint32_t*>(dst + j * pitch) + d0;
+                const uint64_t nw = std::min(per, nd - d0);
+                if (avx2) synth_words_avx2(w, d0, nw, n_iid, c);
+                else synth_words_scalar(w, d0, nw, n_iid, c);
+            },
+            4);
+    });
+}
+
+// selected .bed columns (all iids, ceil(n/4) bytes each, zero-padded to `pitch`) into a host
+// buffer -- the host half of stage_chunk, for callers that run their own upload (the cfg5 plan:
+// each rank gathers only its share of a SNP block, shard.PartitionedGrm)
+int snpmi_bed_gather_packed(const char* path, uint64_t n_iid, uint64_t n_sid, const uint64_t* sid_idx, uint64_t n_sel,
+                            uint64_t pitch, uint8_t* dst, int num_threads) {
+    return guarded([&] {
+        BedMap m;
+        open_bed(m, path, n_iid, n_sid);
+        SNPMI_REQUIRE(pitch >= m.bpc, SNPMI_E_ARG, "pitch is smaller than a column");
+        SNPMI_REQUIRE(dst != nullptr || n_sel == 0, SNPMI_E_ARG, "dst is NULL");
+        check_index(sid_idx, n_sel, n_sid, "sid");
+        gather_columns(m, sid_idx, 0, n_sel, pitch, dst, resolve_threads(num_threads));
     });
 }
 

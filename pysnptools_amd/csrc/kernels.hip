@@ -1375,15 +1375,18 @@ __device__ __forceinline__ T apply_one(T x, double mean, double sd, int is_beta,
     return (T)(is_beta ? d * w : d / sd);
 }
 
-// F order: one wave per column.
+// F order, round 3: one wave per column, 4-B accesses, two passes -- the general path for columns
+// holding values other than 0/1/2/NaN (`only`: the columns k_std_cols_f flagged), and A/B variant
+// "std" 1 for every column.
 template <typename T>
 __global__ __launch_bounds__(kBlock) void k_std_dense_f(T* __restrict__ val, uint64_t rows, uint64_t cols,
                                                         uint64_t ld, int std_kind, double a, double b, int use_stats,
-                                                        T* __restrict__ stats) {
+                                                        T* __restrict__ stats, const uint8_t* __restrict__ only) {
     const int lane = threadIdx.x & (kWave - 1);
     const uint64_t nwaves = (uint64_t)gridDim.x * (kBlock / kWave);
     const int is_beta = std_kind == SNPMI_STD_BETA;
     for (uint64_t j = (uint64_t)blockIdx.x * (kBlock / kWave) + threadIdx.x / kWave; j < cols; j += nwaves) {
+        if (only && !only[j]) continue;  // the columns k_std_cols_f handed over (non-genotype values)
         T* c = val + j * ld;
         double mean, sd;
         if (use_stats) {
@@ -1415,7 +1418,298 @@ __global__ __launch_bounds__(kBlock) void k_std_dense_f(T* __restrict__ val, uin
     }
 }
 
-// C order: a block owns 64 adjacent columns; lanes walk columns, waves walk rows.
+// Per-column apply constants, computed once per column by ONE thread (beta_weight's lgamma/pow
+// stay out of the hot loop) and shared through LDS: the standardized values of the genotype values
+// 0/1/2 (+0.0, 1.0, 2.0 by bit pattern, so -0.0 still takes apply_one), computed by apply_one
+// itself so the lookup is bit-identical to the per-element formula.  Anything else (non-genotype
+// floats, NaN) takes apply_one with the column's mean / sd / weight -- the per-element f64 divide
+// runs only for those.
+struct ColConst {
+    double mean, sd, w;
+    int zero_col;
+    double l[3];
+};
+
+template <typename T, bool BETA = true>
+__device__ __forceinline__ void col_const(ColConst& cc, double mean, double sd, int is_beta, double a, double b,
+                                          int use_stats) {
+    cc.mean = mean;
+    cc.sd = sd;
+    cc.w = BETA && is_beta ? beta_weight(mean, a, b) : 0.0;
+    cc.zero_col = is_beta && use_stats && __builtin_isinf(sd);
+    for (int v = 0; v < 3; v++) cc.l[v] = (double)apply_one((T)v, mean, sd, is_beta, cc.w, cc.zero_col != 0);
+}
+
+__device__ __forceinline__ uint64_t tbits(float x) { return __float_as_uint(x); }
+__device__ __forceinline__ uint64_t tbits(double x) { return (uint64_t)__double_as_longlong(x); }
+
+// genotype lookup: 0..2 for +0.0 / 1.0 / 2.0, 3 for anything else
+template <typename T>
+__device__ __forceinline__ int geno_of(T x) {
+    const uint64_t u = tbits(x);
+    return u == tbits((T)0) ? 0 : u == tbits((T)1) ? 1 : u == tbits((T)2) ? 2 : 3;
+}
+
+template <typename T>
+__device__ __forceinline__ void acc_stat(T x, double& n, double& s1, double& s2) {
+    if (x == x) {
+        const double dx = (double)x;
+        n += 1.0;
+        s1 += dx;
+        s2 += dx * dx;
+    }
+}
+
+template <typename T>
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t col_rsrc(T* p, uint64_t bytes) {
+    const uint64_t a = reinterpret_cast<uint64_t>(p);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a), hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+    return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uint64_t)hi << 32) | lo), (short)0,
+                                             (int)__builtin_amdgcn_readfirstlane((uint32_t)bytes), 0x00020000);
+}
+
+// F order, genotype-valued columns (0 / 1 / 2 / NaN -- a decoded .bed): one NT-thread workgroup per
+// column (grid-stride over columns), 16-B buffer loads and stores through a per-column resource
+// whose range check drops the accesses past the column (no per-vector branches; the zeros they read
+// are taken out of the observation count).  The column's aligned body is NV vectors per thread per
+// chunk; when it fits one chunk the values stay in registers between the stats reduction and the
+// table apply, so the column is read from HBM once and written once (the algorithmic 2 x 4 B per f32
+// value); longer columns (or use_stats) read it again per chunk.  A misaligned head / tail (< 16 B
+// each) are single elements owned by the first threads.  Stats: per-thread partial sums in T are
+// exact integers for such values, i.e. the f64 sums of any order, then bed-reader's one-pass
+// mean / std (stats_mean_std) -- bit-identical to the f64 path.  A column with any other value is
+// left untouched and flagged (flags[j] = 1, *any = 1) for k_std_dense_f.
+template <typename T, int NT, int NV, bool BETA>
+__global__ __launch_bounds__(NT) void k_std_cols_f(T* __restrict__ val, uint64_t rows, uint64_t cols, uint64_t ld,
+                                                   int std_kind, double a, double b, int use_stats,
+                                                   T* __restrict__ stats, uint8_t* __restrict__ flags,
+                                                   unsigned int* __restrict__ any) {
+    constexpr int VE = 16 / sizeof(T);
+    typedef T vec __attribute__((ext_vector_type(VE)));
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    constexpr int NW = NT / kWave;
+    __shared__ double red[3][NW];
+    __shared__ T lut[3];
+    const int t = threadIdx.x, lane = t & (kWave - 1), wv = t / kWave;
+    const int is_beta = BETA && std_kind == SNPMI_STD_BETA;
+    constexpr uint64_t chunk = (uint64_t)NT * NV;  // vectors per chunk
+    for (uint64_t j = blockIdx.x; j < cols; j += gridDim.x) {
+        T* c = val + j * ld;
+        uint64_t h = ((16 - (reinterpret_cast<uintptr_t>(c) & 15)) & 15) / sizeof(T);
+        if (h > rows) h = rows;
+        const uint64_t nvec = (rows - h) / VE;
+        const uint64_t tail0 = h + nvec * VE;
+        const __amdgpu_buffer_rsrc_t rs = col_rsrc(c + h, nvec * 16);
+        // the one scalar this thread owns (head element t, or tail element t - h)
+        const uint64_t se = (uint64_t)t < h ? (uint64_t)t : tail0 + (uint64_t)t - h;
+        const bool has_s = (uint64_t)t < h || se < rows;
+        const T xs = has_s ? c[se] : (T)0;
+        const bool resident = nvec <= chunk;
+        u32x4 r[NV];
+        // pass 1 (whole column): partial sums, observation count, and the genotype check
+        T p1 = 0, p2 = 0;
+        uint32_t cnt = 0;
+        bool oth = false;
+        auto take = [&](T x) {  // (-0.0 counts as "other": apply_one keeps its sign when mean == 0)
+            const bool ok = x == x;
+            const T xv = ok ? x : (T)0;
+            p1 += xv;
+            p2 += xv * xv;
+            cnt += ok;
+            oth |= ok && geno_of(x) == 3;
+        };
+        if (has_s) take(xs);
+        if (!use_stats || !resident) {
+            for (uint64_t q0 = 0; q0 < nvec; q0 += chunk) {
+                const uint32_t vo = (uint32_t)((q0 + t) * 16);
+#pragma unroll
+                for (int k = 0; k < NV; k++) r[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, vo, k * NT * 16, 2);
+                // vectors of this thread past the column (zero-filled by the range check)
+                const uint32_t left = (uint32_t)(nvec - q0), mine = left > (uint32_t)t ? left - (uint32_t)t : 0u;
+                const uint32_t good = mine >= (uint32_t)((NV - 1) * NT + 1) ? NV : (mine + NT - 1) / NT;
+                cnt -= (uint32_t)((NV - good) * VE);
+#pragma unroll
+                for (int k = 0; k < NV; k++) {
+                    const vec x = __builtin_bit_cast(vec, r[k]);
+#pragma unroll
+                    for (int e = 0; e < VE; e++) take(x[e]);
+                    __builtin_amdgcn_sched_barrier(0);  // one vector's temporaries at a time
+                }
+            }
+        } else {  // use_stats, one chunk: load it here, check it below
+            const uint32_t vo = (uint32_t)t * 16;
+#pragma unroll
+            for (int k = 0; k < NV; k++) r[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, vo, k * NT * 16, 2);
+#pragma unroll
+            for (int k = 0; k < NV; k++) {
+                const vec x = __builtin_bit_cast(vec, r[k]);
+#pragma unroll
+                for (int e = 0; e < VE; e++) take(x[e]);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+        if (__syncthreads_or(oth)) {  // not a genotype column: k_std_dense_f takes it
+            if (t == 0) {
+                flags[j] = 1;
+                atomicOr(any, 1u);
+            }
+            continue;  // (the barrier above also ordered the previous column's LDS reads)
+        }
+        if (!use_stats) {
+            // exact small integers per thread, summed in f64 across the workgroup
+            const double n = wave_sum_f64((double)cnt), s1 = wave_sum_f64((double)p1),
+                         s2 = wave_sum_f64((double)p2);
+            if (lane == 0) {
+                red[0][wv] = n;
+                red[1][wv] = s1;
+                red[2][wv] = s2;
+            }
+            __syncthreads();
+            if (t == 0) {
+                double tn = 0, t1 = 0, t2 = 0;
+                for (int q = 0; q < NW; q++) {
+                    tn += red[0][q];
+                    t1 += red[1][q];
+                    t2 += red[2][q];
+                }
+                double sd;
+                const double mean = stats_mean_std(tn, t1, t2, &sd);
+                stats[2 * j] = (T)mean;
+                stats[2 * j + 1] = (T)sd;
+                ColConst cc;
+                col_const<T, BETA>(cc, mean, sd, is_beta, a, b, use_stats);
+                for (int v = 0; v < 3; v++) lut[v] = (T)cc.l[v];
+            }
+        } else if (t == 0) {
+            ColConst cc;
+            col_const<T, BETA>(cc, (double)stats[2 * j], (double)stats[2 * j + 1], is_beta, a, b, use_stats);
+            for (int v = 0; v < 3; v++) lut[v] = (T)cc.l[v];
+        }
+        __syncthreads();
+        const T l0 = lut[0], l1 = lut[1], l2 = lut[2];
+        auto map = [&](T x) { return x == (T)1 ? l1 : x == (T)2 ? l2 : x == x ? l0 : (T)0; };  // +0 / NaN
+        if (has_s) c[se] = map(xs);
+        for (uint64_t q0 = 0; q0 < nvec; q0 += chunk) {
+            const uint32_t vo = (uint32_t)((q0 + t) * 16);
+            if (!resident) {
+#pragma unroll
+                for (int k = 0; k < NV; k++) r[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, vo, k * NT * 16, 2);
+            }
+#pragma unroll
+            for (int k = 0; k < NV; k++) {
+                const vec x = __builtin_bit_cast(vec, r[k]);
+                vec o;
+#pragma unroll
+                for (int e = 0; e < VE; e++) o[e] = map(x[e]);
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), rs, vo, k * NT * 16, 2);
+                __builtin_amdgcn_sched_barrier(0);  // one vector's registers at a time
+            }
+        }
+        __syncthreads();  // lut / red are reused by the next column
+    }
+}
+
+// C order with 16-B row segments (row pitch and base 16-B aligned): a 256-thread workgroup owns
+// 64*VE adjacent columns, each lane VE of them (one 16-B load per row), the 4 waves walk rows.
+// Two passes over the slab (stats, then apply): a C-order column cannot stay on chip.
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_std_cols_c16(T* __restrict__ val, uint64_t rows, uint64_t cols,
+                                                         uint64_t ld, int std_kind, double a, double b,
+                                                         int use_stats, T* __restrict__ stats) {
+    constexpr int VE = 16 / sizeof(T);
+    typedef T vec __attribute__((ext_vector_type(VE)));
+    constexpr int NW = kBlock / kWave;
+    constexpr int CW = kWave * VE;  // columns per workgroup
+    __shared__ double red[3][NW][CW];
+    __shared__ ColConst cc[CW];
+    const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
+    const int is_beta = std_kind == SNPMI_STD_BETA;
+    for (uint64_t j0 = (uint64_t)blockIdx.x * CW; j0 < cols; j0 += (uint64_t)gridDim.x * CW) {
+        const uint64_t jl = j0 + (uint64_t)lane * VE;  // this lane's first column
+        const int nv = jl >= cols ? 0 : (int)min<uint64_t>(VE, cols - jl);
+        if (use_stats) {
+            if (wv == 0)
+                for (int e = 0; e < nv; e++)
+                    col_const<T>(cc[lane * VE + e], (double)stats[2 * (jl + e)], (double)stats[2 * (jl + e) + 1],
+                                 is_beta, a, b, use_stats);
+        } else {
+            double n[VE], s1[VE], s2[VE];
+#pragma unroll
+            for (int e = 0; e < VE; e++) n[e] = s1[e] = s2[e] = 0;
+            if (nv == VE) {
+                for (uint64_t i = wv; i < rows; i += NW) {
+                    const vec x = __builtin_nontemporal_load(reinterpret_cast<const vec*>(val + i * ld + jl));
+#pragma unroll
+                    for (int e = 0; e < VE; e++) acc_stat(x[e], n[e], s1[e], s2[e]);
+                }
+            } else if (nv > 0) {
+                for (uint64_t i = wv; i < rows; i += NW)
+                    for (int e = 0; e < nv; e++) acc_stat(val[i * ld + jl + e], n[e], s1[e], s2[e]);
+            }
+#pragma unroll
+            for (int e = 0; e < VE; e++) {
+                red[0][wv][lane * VE + e] = n[e];
+                red[1][wv][lane * VE + e] = s1[e];
+                red[2][wv][lane * VE + e] = s2[e];
+            }
+            __syncthreads();
+            if (wv == 0)
+                for (int e = 0; e < nv; e++) {
+                    const int q = lane * VE + e;
+                    double tn = 0, t1 = 0, t2 = 0;
+                    for (int w2 = 0; w2 < NW; w2++) {
+                        tn += red[0][w2][q];
+                        t1 += red[1][w2][q];
+                        t2 += red[2][w2][q];
+                    }
+                    double sd;
+                    const double mean = stats_mean_std(tn, t1, t2, &sd);
+                    stats[2 * (jl + e)] = (T)mean;
+                    stats[2 * (jl + e) + 1] = (T)sd;
+                    col_const<T>(cc[q], mean, sd, is_beta, a, b, use_stats);
+                }
+        }
+        __syncthreads();
+        if (nv > 0) {
+            T l[VE][3];
+#pragma unroll
+            for (int e = 0; e < VE; e++)
+#pragma unroll
+                for (int v = 0; v < 3; v++) l[e][v] = (T)cc[lane * VE + e].l[v];
+            auto slow = [&](T x, int e) {
+                const ColConst& k = cc[lane * VE + e];
+                return apply_one(x, k.mean, k.sd, is_beta, k.w, k.zero_col != 0);
+            };
+            if (nv == VE) {
+                for (uint64_t i = wv; i < rows; i += NW) {
+                    vec* p = reinterpret_cast<vec*>(val + i * ld + jl);
+                    const vec x = __builtin_nontemporal_load(p);
+                    vec o;
+                    bool other = false;
+#pragma unroll
+                    for (int e = 0; e < VE; e++) {
+                        const int g = geno_of(x[e]);
+                        o[e] = g == 0 ? l[e][0] : g == 1 ? l[e][1] : l[e][2];
+                        other |= g == 3;
+                    }
+                    if (other) {
+#pragma unroll
+                        for (int e = 0; e < VE; e++)
+                            if (geno_of(x[e]) == 3) o[e] = slow(x[e], e);
+                    }
+                    __builtin_nontemporal_store(o, p);
+                }
+            } else {
+                for (uint64_t i = wv; i < rows; i += NW)
+                    for (int e = 0; e < nv; e++) val[i * ld + jl + e] = slow(val[i * ld + jl + e], e);
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// C order, round 3 (and rows that are not 16-B aligned): a block owns 64 adjacent columns; lanes
+// walk columns, waves walk rows.
 template <typename T>
 __global__ __launch_bounds__(kBlock) void k_std_dense_c(T* __restrict__ val, uint64_t rows, uint64_t cols,
                                                         uint64_t ld, int std_kind, double a, double b, int use_stats,
@@ -1853,6 +2147,7 @@ inline unsigned grid_for(uint64_t work, uint64_t per_block, unsigned cap = 65536
 
 // ====================================================================== launchers
 int g_variant_decode = 0;  // tuning hook (snpmi_set_kernel_variant); no variants at present
+int g_variant_std = 0;     // dense standardize: 0 = k_std_cols_f / k_std_cols_c16, 1 = round 3's kernels
 
 #define SNPMI_LAUNCH_CHECK() SNPMI_HIP(hipGetLastError())
 
@@ -2237,14 +2532,66 @@ void launch_dense_codes(const float* Z, uint64_t ldz, uint64_t n, uint64_t m, ui
 void launch_dense_standardize(void* val, uint64_t rows, uint64_t cols, uint64_t ld, int order_c, int dtype,
                               int std_kind, double a, double b, int use_stats, void* stats, hipStream_t st) {
     if (cols == 0 || std_kind == SNPMI_STD_NONE) return;
+    const size_t es = dtype == SNPMI_DT_F32 ? 4 : 8;
     if (!order_c) {
-        const unsigned g = grid_for(cols, kBlock / kWave);
+        auto general = [&](const uint8_t* only) {
+            const unsigned gw = grid_for(cols, kBlock / kWave);
+            if (dtype == SNPMI_DT_F32)
+                k_std_dense_f<float><<<gw, kBlock, 0, st>>>((float*)val, rows, cols, ld, std_kind, a, b, use_stats,
+                                                            (float*)stats, only);
+            else
+                k_std_dense_f<double><<<gw, kBlock, 0, st>>>((double*)val, rows, cols, ld, std_kind, a, b, use_stats,
+                                                             (double*)stats, only);
+            SNPMI_LAUNCH_CHECK();
+        };
+        if (g_variant_std == 1) {  // A/B: round 3's wave-per-column kernel for every column
+            general(nullptr);
+            return;
+        }
+        // genotype columns: one workgroup per column, the smallest (threads, vectors per thread)
+        // that keeps the whole column in registers, else 1024 x 8 in chunks (two reads); columns
+        // with other values are flagged and then standardized by the general kernel
+        Device& d = device();
+        uint8_t* flags = (uint8_t*)d.get(Device::S_STDFLAG, round_up(cols, 256) + 256);
+        unsigned int* any = (unsigned int*)(flags + round_up(cols, 256));
+        SNPMI_HIP(hipMemsetAsync(flags, 0, round_up(cols, 256) + 4, st));
+        const uint64_t nvec = rows * es / 16 + 1;
+        const unsigned g = (unsigned)std::min<uint64_t>(cols, 1u << 20);
+        const bool beta = std_kind == SNPMI_STD_BETA;
+#define SNPMI_STD_F(NT, NV, BETA)                                                                                   \
+    do {                                                                                                            \
+        if (dtype == SNPMI_DT_F32)                                                                                  \
+            k_std_cols_f<float, NT, NV, BETA><<<g, NT, 0, st>>>((float*)val, rows, cols, ld, std_kind, a, b,        \
+                                                                use_stats, (float*)stats, flags, any);              \
+        else                                                                                                        \
+            k_std_cols_f<double, NT, NV, BETA><<<g, NT, 0, st>>>((double*)val, rows, cols, ld, std_kind, a, b,      \
+                                                                 use_stats, (double*)stats, flags, any);            \
+    } while (0)
+        if (beta) {  // Beta: beta_weight's registers leave room for 4 vectors per thread
+            if (nvec <= 256 * 4) SNPMI_STD_F(256, 4, true);
+            else SNPMI_STD_F(1024, 4, true);
+        } else if (nvec <= 256 * 4) SNPMI_STD_F(256, 4, false);
+        else if (nvec <= 256 * 16) SNPMI_STD_F(256, 16, false);
+        else if (nvec <= 1024 * 8) SNPMI_STD_F(1024, 8, false);
+        else if (nvec <= 1024 * 16) SNPMI_STD_F(1024, 16, false);
+        else SNPMI_STD_F(1024, 8, false);
+#undef SNPMI_STD_F
+        SNPMI_LAUNCH_CHECK();
+        unsigned int h_any = 0;
+        SNPMI_HIP(hipMemcpyAsync(&h_any, any, 4, hipMemcpyDeviceToHost, st));
+        SNPMI_HIP(hipStreamSynchronize(st));
+        if (h_any) general(flags);
+        return;
+    }
+    const bool vec16 = reinterpret_cast<uintptr_t>(val) % 16 == 0 && (ld * es) % 16 == 0 && g_variant_std != 1;
+    if (vec16) {
+        const unsigned g = grid_for(cols, kWave * (16 / es));
         if (dtype == SNPMI_DT_F32)
-            k_std_dense_f<float><<<g, kBlock, 0, st>>>((float*)val, rows, cols, ld, std_kind, a, b, use_stats,
-                                                       (float*)stats);
+            k_std_cols_c16<float><<<g, kBlock, 0, st>>>((float*)val, rows, cols, ld, std_kind, a, b, use_stats,
+                                                        (float*)stats);
         else
-            k_std_dense_f<double><<<g, kBlock, 0, st>>>((double*)val, rows, cols, ld, std_kind, a, b, use_stats,
-                                                        (double*)stats);
+            k_std_cols_c16<double><<<g, kBlock, 0, st>>>((double*)val, rows, cols, ld, std_kind, a, b, use_stats,
+                                                         (double*)stats);
     } else {
         const unsigned g = grid_for(cols, 64);
         if (dtype == SNPMI_DT_F32)

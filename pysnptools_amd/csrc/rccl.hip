@@ -12,6 +12,7 @@
 
 namespace {
 ncclComm_t g_comm = nullptr;
+int g_comm_dev = -1;  // the device the communicator was created on
 
 #define SNPMI_NCCL(expr)                                                                     \
     do {                                                                                     \
@@ -19,6 +20,15 @@ ncclComm_t g_comm = nullptr;
         if (r_ != ncclSuccess)                                                               \
             throw ::snpmi::Error(SNPMI_E_RCCL, std::string(#expr) + ": " + ncclGetErrorString(r_)); \
     } while (0)
+// the communicator exists and the calling thread drives the device it was built on (the
+// library's current device is per thread; a collective on another device's stream would pair a
+// device-0 communicator with device r's buffers)
+void require_comm() {
+    SNPMI_REQUIRE(g_comm != nullptr, SNPMI_E_ARG, "RCCL communicator not initialised");
+    SNPMI_REQUIRE(snpmi::device().id == g_comm_dev, SNPMI_E_ARG,
+                  "RCCL communicator was created on device " + std::to_string(g_comm_dev) +
+                      " but this thread drives device " + std::to_string(snpmi::device().id));
+}
 }  // namespace
 
 using namespace snpmi;
@@ -38,16 +48,17 @@ int snpmi_rccl_init(int nranks, int rank, const uint8_t* id, uint64_t id_len) {
     return guarded([&] {
         SNPMI_REQUIRE(id && id_len >= sizeof(ncclUniqueId), SNPMI_E_ARG, "id buffer too small");
         SNPMI_REQUIRE(g_comm == nullptr, SNPMI_E_ARG, "RCCL communicator already initialised");
-        (void)device();
+        const int dev = device().id;  // binds this thread's current HIP device
         ncclUniqueId u;
         std::memcpy(&u, id, sizeof(u));
         SNPMI_NCCL(ncclCommInitRank(&g_comm, nranks, u, rank));
+        g_comm_dev = dev;
     });
 }
 
 int snpmi_rccl_allreduce_sum(void* buf, uint64_t count, int dtype) {
     return guarded([&] {
-        SNPMI_REQUIRE(g_comm != nullptr, SNPMI_E_ARG, "RCCL communicator not initialised");
+        require_comm();
         ncclDataType_t t = dtype == SNPMI_DT_F64 ? ncclFloat64 : ncclFloat32;
         SNPMI_REQUIRE(dtype == SNPMI_DT_F32 || dtype == SNPMI_DT_F64, SNPMI_E_ARG, "all-reduce dtype must be f32/f64");
         SNPMI_NCCL(ncclAllReduce(buf, buf, count, t, ncclSum, g_comm, stream()));
@@ -56,7 +67,7 @@ int snpmi_rccl_allreduce_sum(void* buf, uint64_t count, int dtype) {
 
 int snpmi_rccl_reduce_sum(void* buf, uint64_t count, int dtype, int root) {
     return guarded([&] {
-        SNPMI_REQUIRE(g_comm != nullptr, SNPMI_E_ARG, "RCCL communicator not initialised");
+        require_comm();
         SNPMI_REQUIRE(dtype == SNPMI_DT_F32 || dtype == SNPMI_DT_F64, SNPMI_E_ARG, "reduce dtype must be f32/f64");
         int nranks = 0;
         SNPMI_NCCL(ncclCommCount(g_comm, &nranks));
@@ -68,7 +79,7 @@ int snpmi_rccl_reduce_sum(void* buf, uint64_t count, int dtype, int root) {
 
 int snpmi_rccl_allgather(const void* send, void* recv, uint64_t bytes_per_rank) {
     return guarded([&] {
-        SNPMI_REQUIRE(g_comm != nullptr, SNPMI_E_ARG, "RCCL communicator not initialised");
+        require_comm();
         SNPMI_REQUIRE(send != nullptr && recv != nullptr, SNPMI_E_ARG, "all-gather buffer is NULL");
         SNPMI_NCCL(ncclAllGather(send, recv, bytes_per_rank, ncclUint8, g_comm, stream()));
     });
@@ -76,7 +87,7 @@ int snpmi_rccl_allgather(const void* send, void* recv, uint64_t bytes_per_rank) 
 
 int snpmi_rccl_host_allreduce_f64(double* values, uint64_t count, int op) {
     return guarded([&] {
-        SNPMI_REQUIRE(g_comm != nullptr, SNPMI_E_ARG, "RCCL communicator not initialised");
+        require_comm();
         SNPMI_REQUIRE(values != nullptr && count > 0 && count <= 4096, SNPMI_E_ARG, "bad host all-reduce buffer");
         Device& d = device();
         double* buf = (double*)d.get(Device::S_RED, count * sizeof(double));
@@ -106,6 +117,7 @@ int snpmi_rccl_destroy(void) {
             SNPMI_HIP(hipStreamSynchronize(stream()));
             SNPMI_NCCL(ncclCommDestroy(g_comm));
             g_comm = nullptr;
+            g_comm_dev = -1;
         }
     });
 }

@@ -74,7 +74,7 @@ struct Device {
     // grow-only scratch slots
     enum Slot { S_PACKED, S_PACKED2, S_IDX, S_IDX2, S_LUT, S_STATS, S_OUT, S_TILES, S_K, S_DENSE,
                 S_DENSE2, S_RED, S_SESSION, S_PACKED_B, S_ZBLK, S_IDX32, S_LUT3, S_H2, S_OUT_B, S_STATS_B,
-                S_WIN, S_DPACK, S_DLUT, S_CRTREC, S_SEG, S_NUM };
+                S_WIN, S_DPACK, S_DLUT, S_CRTREC, S_SEG, S_STDFLAG, S_NUM };
     void* buf[S_NUM] = {};
     // chunk pipeline events (slot = chunk parity), all on-device ordering, no host spin:
     hipEvent_t staged[2] = {};    // copy stream: H2D of pinned slot done (host may refill it)
@@ -102,6 +102,7 @@ void release_pinned();
 
 // ------------------------------------------------------------------ kernel launchers (kernels.hip)
 extern int g_variant_decode;
+extern int g_variant_std;
 extern int g_variant_syrk;
 extern int g_dense_chunk;
 // f32 GRM accumulation segments (syrk.hip SegFlush): every `snps` SNPs a workgroup adds its MFMA

@@ -179,6 +179,27 @@ class Dist(object):
             N.call("snpmi_dev_free", dev)
         return buf.astype(np.asarray(arr).dtype)
 
+    @property
+    def can_reduce(self):
+        """Whether ``sum_dev`` can combine device buffers over the ranks."""
+        return self.rccl
+
+    def sum_dev(self, buf, count, dtype, root=None):
+        """In-place elementwise sum over ranks of a device float buffer (``count`` elements of
+        ``dtype`` f32/f64): ncclReduce onto ``root`` (the other ranks' buffers are unspecified
+        afterwards) or, with ``root=None``, ncclAllReduce.  Enqueued on the library stream."""
+        from pysnptools_amd import _native as N
+
+        if not self.rccl:
+            if self.world > 1:
+                raise RuntimeError("a device sum over %d ranks needs an RCCL communicator" % self.world)
+            return
+        code = N.dt_code(dtype)
+        if root is None:
+            N.call("snpmi_rccl_allreduce_sum", buf, int(count), code)
+        else:
+            N.call("snpmi_rccl_reduce_sum", buf, int(count), code, int(root))
+
     def allgather_dev(self, send, recv, nbytes):
         """Device all-gather of ``nbytes`` per rank: rank r's ``send`` lands at ``recv + r*nbytes``
         on every rank (ncclAllGather; in place when ``send`` is that slot of ``recv``)."""
@@ -237,9 +258,9 @@ class HostDist(Dist):
     """Rehearsal process group (``SNPMI_DIST_HOST=1``): the rank layout, barriers, max-over-ranks,
     host sums and device all-gathers of a world > 1 job, staged through host memory over local TCP
     sockets (rank 0 relays; its ephemeral port is handed over through the node-local id file, as
-    the RCCL id is), with every rank free to share ONE GPU.  No RCCL, so device collectives of GRM
-    tiles are unavailable (``ShardedGrm`` refuses a reduce without RCCL; bench.py's legs use
-    collective "none").  Test infrastructure for the N > 1 control flow on a one-GPU box, where
+    the RCCL id is), with every rank free to share ONE GPU.  No RCCL: the device sums of GRM
+    tiles (``sum_dev``, what ``ShardedGrm.combine`` calls) are staged through the host too, so
+    ``grm_sharded`` / ``Bed.read_kernel`` run their "reduce" / "allreduce" at world 2-3 on one GPU.  Test infrastructure for the N > 1 control flow on a one-GPU box, where
     RCCL refuses two ranks per device -- never a production path.  (Not torch.distributed: torch's
     ROCm build carries its own HIP runtime, and loading it next to libsnpmi's corrupts the heap.)"""
 
@@ -296,15 +317,49 @@ class HostDist(Dist):
     def max(self, x):
         return max(struct.unpack("<d", p)[0] for p in self.allgather_bytes(struct.pack("<d", float(x))))
 
+    def _reduce_f64(self, a, root=None):
+        """Sum over ranks of the float64 array ``a`` (in rank order, at rank 0), returned on every
+        rank (``root=None``) or on ``root`` only (None elsewhere)."""
+        import numpy as np
+
+        a = np.ascontiguousarray(a, dtype=np.float64)
+        if self.rank == 0:
+            tot = a.copy()
+            for c in self._peers:
+                tot += np.frombuffer(_recv_frame(c), dtype=np.float64).reshape(a.shape)
+            for r, c in enumerate(self._peers, start=1):  # 1-byte tag: does the sum follow
+                _send_frame(c, b"\x01" + tot.tobytes() if root is None or r == root else b"\x00")
+            return tot if root is None or root == 0 else None
+        _send_frame(self._sock, a.tobytes())
+        back = _recv_frame(self._sock)
+        if back[:1] != b"\x01":
+            return None
+        return np.frombuffer(back[1:], dtype=np.float64).reshape(a.shape).copy()
+
     def sum_host(self, arr):
         import numpy as np
 
         a = np.asarray(arr)
-        parts = self.allgather_bytes(np.ascontiguousarray(a, dtype=np.float64).tobytes())
-        tot = np.zeros(a.shape, dtype=np.float64)
-        for p in parts:
-            tot += np.frombuffer(p, dtype=np.float64).reshape(a.shape)
-        return tot.astype(a.dtype)
+        return self._reduce_f64(a).astype(a.dtype)
+
+    @property
+    def can_reduce(self):
+        return True
+
+    def sum_dev(self, buf, count, dtype, root=None):
+        """Host-staged form of ``Dist.sum_dev``: the device buffer goes to the host, the ranks' copies
+        are summed in float64 at rank 0 and the sum is written back (on every rank, or on ``root``)."""
+        import numpy as np
+
+        from pysnptools_amd import _native as N
+
+        host = np.empty(int(count), dtype=dtype)
+        N.call("snpmi_stream_sync")
+        N.call("snpmi_memcpy_d2h", N.ptr(host), buf, host.nbytes)
+        tot = self._reduce_f64(host, root)
+        if tot is not None:
+            host[:] = tot
+            N.call("snpmi_memcpy_h2d", buf, N.ptr(host), host.nbytes)
 
     def allgather_dev(self, send, recv, nbytes):
         import numpy as np
@@ -354,10 +409,15 @@ def init_from_env(force_rccl=False, timeout=300.0, env=None, set_current=True):
             publish_id(path, uid)
         else:
             uid = (ctypes.c_uint8 * 128).from_buffer_copy(wait_id(path, timeout))
+        def comm_init():
+            # the library's current device is per thread: bind the helper thread to this rank's
+            # GPU before ncclCommInitRank, or every rank's communicator lands on device 0
+            N.call("snpmi_set_device", device)
+            N.call("snpmi_rccl_init", world, rank, uid, 128)
+
         try:
             with stdout_to_stderr():
-                _run_bounded(lambda: N.call("snpmi_rccl_init", world, rank, uid, 128), timeout,
-                             "ncclCommInitRank (rank %d of %d)" % (rank, world))
+                _run_bounded(comm_init, timeout, "ncclCommInitRank (rank %d of %d)" % (rank, world))
         finally:
             if rank == 0:
                 # every rank has read the id once the communicator exists (or we give up)

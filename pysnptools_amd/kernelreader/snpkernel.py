@@ -86,8 +86,9 @@ class SnpKernel(KernelReader):
                 kernel, kernel_trained = kernel.standardize(kernel_standardizer, return_trained=True,
                                                             num_threads=num_threads)
         else:
-            snpdata, snp_trained = self.snpreader.read().standardize(self.standardizer, return_trained=True,
-                                                                     num_threads=num_threads)
+            from pysnptools_amd.snpreader.snpreader import _read_and_standardize
+
+            snpdata, snp_trained = _read_and_standardize(self.snpreader, self.standardizer, num_threads=num_threads)
             snpdata, kernel_trained = snpdata.standardize(kernel_standardizer, return_trained=True,
                                                           num_threads=num_threads)
             kernel = SnpKernel(snpdata, SS_Identity())
@@ -107,6 +108,7 @@ class SnpKernel(KernelReader):
         return self.snpreader.pos
 
     def read_snps(self, order="F", dtype=np.float64, force_python_only=False, view_ok=False, num_threads=None):
-        return self.snpreader.read(order=order, dtype=np.dtype(dtype), force_python_only=force_python_only,
-                                   view_ok=view_ok, num_threads=num_threads).standardize(self.standardizer,
-                                                                                          num_threads=num_threads)
+        from pysnptools_amd.snpreader.snpreader import _read_and_standardize
+
+        return _read_and_standardize(self.snpreader, self.standardizer, order, dtype, force_python_only,
+                                     num_threads)[0]

@@ -15,8 +15,11 @@ grouping.  Two plans:
   exact residue products.  Per-SNP stats are computed only by the rank that owns
   the SNP and summed over ranks (zeros elsewhere -- exact), which is ``Unit._merge_trained``'s
   concatenation (unit.py:53-56) in SNP order.
-* **K-partitioned (cfg5)** -- ``grm_partitioned``: K (1 TB at 500k iids) is too large to
-  replicate, so each rank keeps only its 256x256 blocks and reads every SNP; no collective.
+* **K-partitioned (cfg5)** -- ``PartitionedGrm`` / ``grm_partitioned``: K (1 TB at 500k iids) is
+  too large to replicate, so each rank keeps only its 256x256 blocks of K.  Every rank needs every
+  SNP, so per SNP block each rank uploads only its 1/p share of the packed columns and one
+  ``ncclAllGather`` rebuilds the block on every rank (packed codes are 16x smaller than f32
+  values); no reduction.
 """
 import ctypes
 
@@ -29,13 +32,6 @@ def snp_blocks(n_sid, block_size):
     """[(start, count)] covering range(n_sid) in blocks of ``block_size``."""
     block_size = max(1, int(block_size))
     return [(s0, min(block_size, n_sid - s0)) for s0 in range(0, n_sid, block_size)]
-
-
-def rank_blocks(n_sid, block_size, rank, world):
-    """The blocks rank ``rank`` of ``world`` owns in a round-robin plan (used by the gloo
-    rehearsal of the reduction, tests/test_distributed.py)."""
-    assert 0 <= rank < world
-    return snp_blocks(n_sid, block_size)[rank::world]
 
 
 def rank_span(n_sid, rank, world):
@@ -51,14 +47,6 @@ def rank_span_blocks(n_sid, block_size, rank, world):
     lo, hi = rank_span(n_sid, rank, world)
     block_size = max(1, int(block_size))
     return [(s0, min(block_size, hi - s0)) for s0 in range(lo, hi, block_size)]
-
-
-def merge_order(n_sid, block_size, world):
-    """For each global block (in SNP order): (owner rank, index within that rank's round-robin list)."""
-    out = []
-    for b, _ in enumerate(snp_blocks(n_sid, block_size)):
-        out.append((b % world, b // world))
-    return out
 
 
 def rank_pieces(piece_sizes, rank, world):
@@ -107,7 +95,7 @@ class ShardedGrm(object):
         self.dist, self.collective, self.root = dist, collective, int(root)
         self.world = int(world) if world is not None else (dist.world if dist is not None else 1)
         self.rank = int(rank) if rank is not None else (dist.rank if dist is not None else 0)
-        if collective != "none" and self.world > 1 and not (dist is not None and dist.rccl):
+        if collective != "none" and self.world > 1 and not (dist is not None and dist.can_reduce):
             raise RuntimeError("a %s over %d ranks needs an RCCL communicator (dist.init_from_env)"
                                % (collective, self.world))
         if not 0 <= self.root < self.world:
@@ -145,16 +133,15 @@ class ShardedGrm(object):
     # ------------------------------------------------------------------ combine + finish
     def combine(self):
         """The collective over xGMI (enqueued on the library stream): in-place ncclReduce onto
-        ``root`` or ncclAllReduce of the tile buffer.  No-op for "none"; at world size 1 it runs
-        only when a communicator exists (bench.py --force-rccl exercises the real calls)."""
-        N = self.N
-        if self.collective == "none" or self.dist is None or not self.dist.rccl:
+        ``root`` or ncclAllReduce of the tile buffer (``Dist.sum_dev``; the host rehearsal group
+        stages the same sums through host memory).  No-op for "none"; at world size 1 it runs only
+        when a communicator exists (bench.py --force-rccl exercises the real calls)."""
+        if self.collective == "none" or self.dist is None or not self.dist.can_reduce:
+            return
+        if not self.dist.rccl and self.dist.world == 1:
             return
         t, count = self.tiles()
-        if self.collective == "reduce":
-            N.call("snpmi_rccl_reduce_sum", t, count, N.dt_code(self.dtype), self.root)
-        else:
-            N.call("snpmi_rccl_allreduce_sum", t, count, N.dt_code(self.dtype))
+        self.dist.sum_dev(t, count, self.dtype, self.root if self.collective == "reduce" else None)
 
     def holds_k(self):
         return self.collective != "reduce" or self.rank == self.root
@@ -272,19 +259,250 @@ def grm_pieces(reader, standardizer, rank=None, world=None, dtype="float32", dia
     return K, _trained_from(standardizer, kind, a, b, sid, stats), factor
 
 
-def grm_partitioned(reader, standardizer, rank, world, out=None, num_threads=None):
+class _DevBuf(object):
+    def __init__(self, N, nbytes, host=False):
+        self.N, self.host, self.p = N, host, ctypes.c_void_p()
+        N.call("snpmi_host_alloc" if host else "snpmi_dev_alloc", ctypes.byref(self.p), max(int(nbytes), 1))
+
+    def at(self, off):
+        return ctypes.c_void_p(self.p.value + int(off))
+
+    def free(self):
+        if self.p:
+            self.N.call("snpmi_host_free" if self.host else "snpmi_dev_free", self.p)
+            self.p = None
+
+
+class PartitionedGrm(object):
+    """cfg5: the GRM of a SNP stream whose K is too large to replicate, as one
+    process per GPU.  K is partitioned into the 256x256 blocks of its upper triangle, block L owned
+    by part ``L mod parts`` (``snpmi_grm_part_coords``); this process accumulates part ``part``.
+
+    Per SNP block of ``block`` SNPs (the reference's block loop, snpreader.py:643-655):
+
+    1. ``fill(host_ptr, s0, count)`` writes this rank's share -- packed columns [s0, s0+count) of the
+       stream, all ``n_src`` iids, ``pitch_src`` bytes each -- into a pinned host slot (a .bed gather,
+       ``snpmi_bed_gather_packed``; bench.py: a synthetic generator).  Rank r of the ``world`` ranks
+       of ``dist`` owns columns [r*ms, (r+1)*ms) of each block, ms = ceil(block/world).
+    2. The copy stream uploads the share into its slot of a device block buffer.
+    3. ``dist.allgather_dev`` (ncclAllGather over xGMI) rebuilds the whole block on every rank.
+    4. iid selection (``k_repack*``), per-SNP stats + LUT (``k_snp_stats``; every rank sees every
+       iid of the SNP, so the stats are identical on every rank without an exchange), then the fp16x2
+       MFMA SYRK adds the block into this part's K blocks (``snpmi_dev_syrk_packed_part``).
+
+    Two slots: block k+1's fill (host threads) and upload (copy stream) run under block k's kernels;
+    the compute stream waits on events only.  At world 1 the all-gather is a no-op and the one rank
+    fills whole blocks -- a single-GPU run of any part (``parts`` may exceed ``world``: bench.py
+    computes part 0 of the 8-GPU plan on one GPU)."""
+
+    def __init__(self, n_src, m, kind, a=0.0, b=0.0, use_stats=False, stats=None, iid_index=None, count_a1=False,
+                 dist=None, part=None, parts=None, block=8192, out=None, timing=False):
+        from pysnptools_amd import _native as N
+
+        self.N = N
+        self.dist = dist
+        self.world = dist.world if dist is not None else 1
+        self.rank = dist.rank if dist is not None else 0
+        self.part = self.rank if part is None else int(part)
+        self.parts = self.world if parts is None else int(parts)
+        if not 0 <= self.part < self.parts:
+            raise ValueError("part %d of %d" % (self.part, self.parts))
+        if self.world > 1 and not (dist.rccl or hasattr(dist, "allgather_bytes")):
+            raise RuntimeError("the cfg5 all-gather over %d ranks needs a process group" % self.world)
+        self.n_src, self.m = int(n_src), int(m)
+        self.iid = N.index_array(iid_index)
+        self.n = self.n_src if self.iid is None else len(self.iid)
+        self.kind, self.a, self.b, self.use_stats, self.count_a1 = int(kind), float(a), float(b), bool(use_stats), count_a1
+        self.block = max(1, int(block))
+        self.ms = (self.block + self.world - 1) // self.world
+        self.pitch_src = N.lib().snpmi_packed_pitch(self.n_src)
+        self.pitch = N.lib().snpmi_packed_pitch(self.n)
+        self.nloc = N.lib().snpmi_grm_part_blocks(self.n, self.part, self.parts)
+        self.timing = timing
+        self._bufs = []
+        try:
+            self._alloc(stats, out)
+        except BaseException:
+            self.close()
+            raise
+
+    def _alloc(self, stats, out):
+        N = self.N
+        blk = self.world * self.ms * self.pitch_src
+        self.dev = [_DevBuf(N, blk), _DevBuf(N, blk)]
+        self.host = [_DevBuf(N, self.ms * self.pitch_src, host=True), _DevBuf(N, self.ms * self.pitch_src, host=True)]
+        self._bufs += self.dev + self.host
+        self.rep = None
+        if self.iid is not None:
+            self.rep = _DevBuf(N, self.block * self.pitch)
+            self.idx = _DevBuf(N, max(1, len(self.iid)) * 8)
+            if len(self.iid):
+                N.call("snpmi_memcpy_h2d", self.idx.p, N.ptr(self.iid), self.iid.nbytes)
+            self._bufs += [self.rep, self.idx]
+        self.lut = _DevBuf(N, self.block * 16)
+        self.stats_dev = _DevBuf(N, max(1, self.m) * 8)
+        self._bufs += [self.lut, self.stats_dev]
+        if self.use_stats:
+            st = np.ascontiguousarray(stats, dtype=np.float32)
+            assert st.shape == (self.m, 2), "stats must be [m, 2]"
+            N.call("snpmi_memcpy_h2d", self.stats_dev.p, N.ptr(st), st.nbytes)
+        # the part's K blocks: in HBM (out="hbm" / an HbmArray: accumulated in place) or host
+        if isinstance(out, str) and out == "hbm":
+            from pysnptools_amd import hbm
+
+            out = hbm.empty((self.nloc, 256, 256), dtype=np.float32, order="C")
+        if out is None:
+            out = np.empty((self.nloc, 256, 256), dtype=np.float32)
+        assert tuple(out.shape) == (self.nloc, 256, 256) and np.dtype(out.dtype) == np.float32
+        assert getattr(out, "order", None) == "C" if hasattr(out, "snpmi_ptr") else out.flags["C_CONTIGUOUS"]
+        self.out = out
+        dev_out = getattr(out, "snpmi_ptr", None)
+        if dev_out is not None:
+            self.blocks = dev_out
+        else:
+            self._kbuf = _DevBuf(N, self.nloc * 256 * 256 * 4)
+            self._bufs.append(self._kbuf)
+            self.blocks = self._kbuf.p
+        self._ev = []
+
+    def _event(self):
+        e = ctypes.c_void_p()
+        self.N.call("snpmi_event_create", ctypes.byref(e))
+        self._ev.append(e)
+        return e
+
+    def run(self, fill):
+        """Stream the ``m`` SNPs through steps 1-4 (see the class doc).  Returns per-block timings
+        (ms, HIP events on the compute stream) when ``timing`` was set, else None."""
+        N = self.N
+        nblk = (self.m + self.block - 1) // self.block
+        up = [self._event(), self._event()]  # copy stream: share of the slot uploaded (host slot free)
+        done = [self._event(), self._event()]  # compute stream: the slot's kernels are done
+        used = [False, False]
+        marks = [(self._event(), self._event()) for _ in range(nblk)] if self.timing else None
+        if self.m == 0 or self.n == 0:
+            N.call("snpmi_dev_memset", self.blocks, 0, self.nloc * 256 * 256 * 4)
+        for k in range(nblk if self.n else 0):
+            s0 = k * self.block
+            cnt = min(self.block, self.m - s0)
+            ms = (cnt + self.world - 1) // self.world
+            mine0 = min(cnt, self.rank * ms)
+            mine = max(0, min(ms, cnt - mine0))
+            slot = k & 1
+            if used[slot]:
+                N.call("snpmi_event_sync", up[slot])  # the host slot's previous upload has finished
+            if mine:
+                fill(self.host[slot].p, s0 + mine0, mine)
+            dst = self.dev[slot].at(self.rank * ms * self.pitch_src)
+            if used[slot]:
+                N.call("snpmi_stream_wait_event", done[slot], 1)  # the device slot's readers are done
+            N.call("snpmi_memcpy_async", dst, self.host[slot].p, ms * self.pitch_src, 0, 1)
+            N.call("snpmi_event_record_on", up[slot], 1)
+            N.call("snpmi_stream_wait_event", up[slot], 0)
+            used[slot] = True
+            if marks:
+                N.call("snpmi_event_record", marks[k][0])
+            if self.world > 1 or (self.dist is not None and self.dist.rccl):  # in place at world 1
+                self.dist.allgather_dev(dst, self.dev[slot].p, ms * self.pitch_src)
+            packed, pitch = self.dev[slot].p, self.pitch_src
+            if self.rep is not None:
+                N.call("snpmi_dev_repack", packed, pitch, self.n_src, self.idx.p, self.n, cnt, self.rep.p, self.pitch)
+                packed, pitch = self.rep.p, self.pitch
+            st = ctypes.c_void_p(self.stats_dev.p.value + s0 * 8)
+            N.call("snpmi_dev_snp_stats", packed, pitch, self.n, cnt, int(bool(self.count_a1)), self.kind, self.a,
+                   self.b, int(self.use_stats), N.DT_F32, st, self.lut.p)
+            N.call("snpmi_dev_syrk_packed_part", packed, pitch, self.n, cnt, self.lut.p, self.part, self.parts,
+                   self.blocks, int(k > 0))
+            if marks:
+                N.call("snpmi_event_record", marks[k][1])
+            N.call("snpmi_event_record", done[slot])
+        N.call("snpmi_stream_sync")
+        if not marks:
+            return None
+        out = ctypes.c_float()
+        res = []
+        for a, b in marks:
+            N.call("snpmi_event_elapsed_ms", a, b, ctypes.byref(out))
+            res.append(float(out.value))
+        return res
+
+    def stats(self):
+        """[m, 2] float32 per-SNP (mean, std) of the stream (or the given stats)."""
+        st = np.empty((self.m, 2), dtype=np.float32)
+        if self.m:
+            self.N.call("snpmi_memcpy_d2h", self.N.ptr(st), self.stats_dev.p, st.nbytes)
+        return st
+
+    def coords(self):
+        """[nloc, 2] int64: (row0, col0) of each local block."""
+        N = self.N
+        coords = np.empty((self.nloc, 2), dtype=np.int64)
+        r0, c0 = ctypes.c_uint64(), ctypes.c_uint64()
+        for k in range(self.nloc):
+            N.call("snpmi_grm_part_coords", self.n, self.part, self.parts, k, ctypes.byref(r0), ctypes.byref(c0))
+            coords[k] = (r0.value, c0.value)
+        return coords
+
+    def finish(self):
+        """The part's blocks (``out``: copied from HBM when it is host memory)."""
+        if getattr(self.out, "snpmi_ptr", None) is None and self.nloc:
+            self.N.call("snpmi_memcpy_d2h", self.N.ptr(self.out), self.blocks, self.out.nbytes)
+        return self.out
+
+    def close(self):
+        for e in self._ev if hasattr(self, "_ev") else []:
+            self.N.call("snpmi_event_destroy", e)
+        self._ev = []
+        for bf in self._bufs:
+            bf.free()
+        self._bufs = []
+
+
+def _partitioned_bed(base, rows, cols, kind, a, b, use_stats, stats, dist, part, parts, block_size, out, threads):
+    """``PartitionedGrm`` over a .bed: each rank's share of a block gathered from the file's mmap
+    (``snpmi_bed_gather_packed``).  Returns (blocks, coords, stats)."""
+    from pysnptools_amd import _native as N
+
+    m = base.sid_count if cols is None else len(cols)
+    col_index = np.arange(base.sid_count, dtype=np.uint64) if cols is None else np.ascontiguousarray(cols, dtype=np.uint64)
+    path = base.filename.encode()
+    g = PartitionedGrm(base.iid_count, m, kind, a, b, use_stats, stats, iid_index=rows, count_a1=base.count_A1,
+                       dist=dist, part=part, parts=parts, block=block_size, out=out)
+
+    def fill(host, s0, cnt):
+        N.call("snpmi_bed_gather_packed", path, base.iid_count, base.sid_count, N.ptr(col_index[s0:s0 + cnt]), cnt,
+               g.pitch_src, host, threads)
+
+    try:
+        g.run(fill)
+        blocks = g.finish()
+        coords = g.coords()
+        if not use_stats:
+            stats = g.stats()
+    finally:
+        g.close()
+    return blocks, coords, stats
+
+
+def grm_partitioned(reader, standardizer, rank=None, world=None, out=None, num_threads=None, dist=None,
+                    block_size=8192):
     """cfg5 GRM of a Bed (or a subset of one) too large to replicate: K is
-    partitioned over ``world`` ranks as the 256x256 blocks of its upper triangle
-    (``snpmi_grm_part_coords``); this rank streams every selected SNP through the fused
-    decode -> standardize -> fp16x2 MFMA SYRK (bf16x3 when a LUT is outside fp16's range) and
-    keeps only its own blocks -- no collective.  Stats are computed per rank from all iids
-    (identical on every rank).
+    partitioned over the ranks as the 256x256 blocks of its upper triangle
+    (``snpmi_grm_part_coords``) and this rank keeps only its own blocks.
+
+    * Under a process group (``dist``, or ``pysnptools_amd.dist.current()``, world > 1): the §8e
+      plan, ``PartitionedGrm`` -- each rank reads only its 1/world share of every SNP block from the
+      .bed, the RCCL all-gather rebuilds the block, every rank runs stats + the fp16x2 SYRK for its
+      part.  ``rank`` / ``world`` must be None or the group's.
+    * Without one: part ``rank`` of ``world`` (default 0 of 1) on this GPU alone, streaming every
+      SNP of the .bed itself (``snpmi_grm_part_bed_f32``) -- e.g. the parts of a job run one by one.
 
     Returns (blocks [n_local, 256, 256] float32 -- ``out`` if given, e.g. an ``np.memmap`` of a
     file, or ``"hbm"`` / an ``hbm.HbmArray`` to keep the blocks in device memory (accumulated in
     place, no copy-out) --, coords [n_local, 2] int64 = (row0, col0) of each block, trained
     standardizer).  Entries of a block beyond iid n-1 are padding."""
     from pysnptools_amd import _native as N
+    from pysnptools_amd import dist as dist_mod
     from pysnptools_amd.snpreader.bed import Bed
     from pysnptools_amd.snpreader.snpreader import _resolve, _trained_from
     from pysnptools_amd.standardizer.standardizer import _std_args
@@ -300,6 +518,16 @@ def grm_partitioned(reader, standardizer, rank, world, out=None, num_threads=Non
     n = reader.iid_count
     stats = (np.ascontiguousarray(standardizer.stats_for(sid), dtype=np.float32) if use_stats
              else np.empty((len(sid), 2), dtype=np.float32))
+    d = dist if dist is not None else dist_mod.current()
+    threads = get_num_threads(num_threads if num_threads is not None else base._num_threads)
+    if d is not None and d.world > 1:
+        if (rank is not None and rank != d.rank) or (world is not None and world != d.world):
+            raise ValueError("rank/world %s/%s differ from the process group's %d/%d" % (rank, world, d.rank, d.world))
+        blocks, coords, stats = _partitioned_bed(base, rows, cols, kind, a, b, use_stats, stats, d, d.rank, d.world,
+                                                 block_size, out, threads)
+        return blocks, coords, _trained_from(standardizer, kind, a, b, sid, stats)
+    rank = 0 if rank is None else int(rank)
+    world = 1 if world is None else int(world)
     nloc = N.lib().snpmi_grm_part_blocks(n, rank, world)
     if isinstance(out, str) and out == "hbm":
         from pysnptools_amd import hbm
@@ -312,7 +540,7 @@ def grm_partitioned(reader, standardizer, rank, world, out=None, num_threads=Non
     ri, ci = N.index_array(rows), N.index_array(cols)
     N.call("snpmi_grm_part_bed_f32", base.filename.encode(), base.iid_count, base.sid_count,
            int(bool(base.count_A1)), N.ptr(ri), n, N.ptr(ci), len(sid), kind, a, b, int(use_stats), N.ptr(stats),
-           rank, world, N.ptr(out), get_num_threads(num_threads))
+           rank, world, N.ptr(out), threads)
     coords = np.empty((nloc, 2), dtype=np.int64)
     r0, c0 = ctypes.c_uint64(), ctypes.c_uint64()
     for k in range(nloc):

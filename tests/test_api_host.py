@@ -181,3 +181,26 @@ def test_array_module_env(monkeypatch):
     assert array_module() is hbm and _on_device()
     monkeypatch.setenv("ARRAY_MODULE", "numpy")
     assert not _on_device(None, np.zeros(2))
+
+
+def test_bed_gather_packed_host_only():
+    """snpmi_bed_gather_packed (the per-rank share gather of the cfg5 plan) is host code: the
+    selected columns' bytes exactly as in the file, zero-padded to the pitch, index errors raised."""
+    from pysnptools_amd import _native as N
+
+    path = os.path.join(DATA, "n300.bed")
+    n, m = 300, 1015
+    body = O.read_bed_bytes(path)
+    bpc = (n + 3) // 4
+    cols = np.array([1014, 0, 7, 7, 500], dtype=np.uint64)
+    pitch = N.lib().snpmi_packed_pitch(n)
+    out = np.full((len(cols), pitch), 0xCD, dtype=np.uint8)
+    N.call("snpmi_bed_gather_packed", path.encode(), n, m, N.ptr(cols), len(cols), pitch, N.ptr(out), 2)
+    ref = np.frombuffer(body, dtype=np.uint8).reshape(m, bpc)[cols.astype(np.int64)]
+    np.testing.assert_array_equal(out[:, :bpc], ref)
+    assert not out[:, bpc:].any()
+    with pytest.raises(IndexError):
+        N.call("snpmi_bed_gather_packed", path.encode(), n, m, N.ptr(np.array([m], dtype=np.uint64)), 1, pitch,
+               N.ptr(out), 1)
+    with pytest.raises(ValueError):
+        N.call("snpmi_bed_gather_packed", path.encode(), n, m + 1, None, 1, pitch, N.ptr(out), 1)

@@ -67,6 +67,30 @@ def test_run_bounded_times_out_and_reraises():
     assert D._run_bounded(lambda: 7, 5, "seven") == 7
 
 
+def test_rccl_init_binds_the_helper_thread_to_the_rank_device(monkeypatch, tmp_path):
+    """ncclCommInitRank runs on a helper thread (bounded wait) and the library's current device is
+    per thread: the helper must select this rank's device itself before the init, or every rank's
+    communicator would be built on device 0."""
+    import threading
+
+    from pysnptools_amd import _native as N
+
+    calls = []
+    monkeypatch.setattr(N, "device_count", lambda: 8)
+    monkeypatch.setattr(N, "call", lambda name, *a: calls.append((name, a, threading.get_ident())))
+    env = {"RANK": "0", "WORLD_SIZE": "4", "LOCAL_RANK": "3", "LOCAL_WORLD_SIZE": "4",
+           "SNPMI_RCCL_ID_FILE": str(tmp_path / "rccl.id")}
+    d = D.init_from_env(env=env, set_current=False, timeout=30)
+    assert d.device == 3
+    init = [c for c in calls if c[0] == "snpmi_rccl_init"]
+    assert len(init) == 1
+    helper = init[0][2]
+    assert helper != threading.get_ident()
+    on_helper = [c for c in calls if c[2] == helper]
+    assert on_helper[0][0] == "snpmi_set_device" and on_helper[0][1] == (3,)
+    assert on_helper[1][0] == "snpmi_rccl_init"
+
+
 _WORKER = r"""
 import os, sys
 sys.path.insert(0, %r)
@@ -109,6 +133,17 @@ s = d.sum_host(np.arange(5, dtype=np.float32) * (rank + 1))
 assert s.dtype == np.float32 and np.array_equal(s, np.arange(5) * sum(range(1, world + 1)))
 parts = d.allgather_bytes(bytes([rank]) * (rank + 1000))
 assert [len(p) for p in parts] == [r + 1000 for r in range(world)] and all(p[:1] == bytes([r]) for r, p in enumerate(parts))
+# the host-staged reduce behind sum_dev: on every rank, or on one root only
+tot = d._reduce_f64(np.full(3, rank + 1.0))
+assert np.array_equal(tot, np.full(3, world * (world + 1) / 2.0))
+for root in range(world):
+    got = d._reduce_f64(np.full(2, float(rank)), root=root)
+    assert (got is None) == (rank != root), (rank, root)
+    if got is not None:
+        assert np.array_equal(got, np.full(2, world * (world - 1) / 2.0))
+e = d._reduce_f64(np.zeros(0))
+assert e is not None and e.size == 0
+assert d.can_reduce
 d.barrier()
 d.close()
 print("ok", rank)

@@ -1,6 +1,7 @@
-"""world_size-2/3 gloo rehearsal of the multi-GPU GRM (no GPU): each rank computes the
-partial K of its SNP blocks (oracle arithmetic stands in for the MFMA kernel), the partials
-are all-reduced, and every rank must hold the full-matrix K and the merged stats."""
+"""world_size-2/3 gloo rehearsal of the multi-GPU GRM (no GPU): each rank computes the partial K
+of its contiguous SNP span (shard.rank_span, the product's plan; oracle arithmetic stands in for
+the MFMA kernel), the partials are all-reduced, the stats are combined by shard._sum_stats, and
+every rank must hold the full-matrix K and the merged stats."""
 import os
 import socket
 import subprocess
@@ -23,11 +24,11 @@ def _free_port():
 @pytest.mark.parametrize("world", [2, 3])
 def test_sharded_grm_equals_single(tmp_path, world):
     from oracle import oracle as O
-    from pysnptools_amd.shard import rank_blocks, snp_blocks
+    from pysnptools_amd.shard import rank_span_blocks
 
-    blocks = snp_blocks(1015, 97)
-    owned = sorted(b for r in range(world) for b in rank_blocks(1015, 97, r, world))
-    assert owned == blocks  # every block exactly once
+    owned = sorted(b for r in range(world) for b in rank_span_blocks(1015, 97, r, world))
+    assert sum(c for _, c in owned) == 1015  # every SNP exactly once
+    assert all(a[0] + a[1] == b[0] for a, b in zip(owned, owned[1:]))
     port = _free_port()
     procs = []
     for r in range(world):

@@ -184,3 +184,39 @@ def test_config4_partitioned_500k_iids(part):
         assert err <= 1e-5, "%s block %d (%d, %d): %g" % (what, b, r0.value, c0.value, err)
         if r0.value == c0.value:
             np.testing.assert_allclose(np.diag(blk)[:len(rows)], np.diag(ref), rtol=1e-5)
+
+
+class _OneRank:
+    rank, world, rccl, n_gpus, local_rank, device, can_reduce = 0, 1, False, 1, 0, 0, False
+
+    def barrier(self):
+        pass
+
+    def max(self, x):
+        return x
+
+
+def test_config5_streamed_500k_iids_over_100k_snps():
+    """configs[4]'s per-rank job beyond one block: part 0 of the 8-part plan at 500,000 iids over
+    106,496 SnpGen-shaped SNPs (21.8% missing) in 13 streamed 8192-SNP blocks through
+    shard.PartitionedGrm (pinned host slots generated on host threads, uploads under the previous
+    block's SYRK, f32 K blocks accumulated in HBM) -- bench.py's grm5 leg at a tenth of its SNPs.
+    Sample blocks (first diagonal, first off-diagonal, the last one with the padded iids) vs the
+    f64 oracle over all SNPs (stats over every iid), <= 1e-5 of max diag; per-SNP stats bit-exact."""
+    import os
+    import sys
+
+    from conftest import ROOT
+
+    sys.path.insert(0, ROOT)
+    import bench
+
+    args = bench.parse(["--grm5-iid", "500000", "--grm5-sid", "106496", "--steps", "1", "--warmup", "0"])
+    assert args.grm5_miss == 0.218 and args.grm5_block == 8192
+    r = bench.leg_grm5(N, args, _OneRank())
+    assert r["blocks"] == 13 and len(r["block_ms"]) == 13
+    picks, stats = r["parity_sample"]
+    assert set(picks) == {"diag", "off", "last"}
+    p = bench.grm5_parity(args, picks, stats, min(16, os.cpu_count() or 1))
+    assert p["stats_bit_exact"], p
+    assert p["max_abs_err_over_max_diag"] <= 1e-5, p
