@@ -219,6 +219,15 @@ class Events:
             self.N.call("snpmi_event_destroy", e)
 
 
+_T0 = time.time()
+
+
+def progress(msg):
+    """One line on stderr per leg (a long default run is never silent for minutes)."""
+    sys.stderr.write("[bench %7.1fs] %s\n" % (time.time() - _T0, msg))
+    sys.stderr.flush()
+
+
 def maf_table(n_iid):
     # SnpGen's MAF curve (snpreader/snpgen.py:140-151); restated here so the product never
     # imports the oracle
@@ -789,7 +798,8 @@ def leg_grm5(N, args, dist):
         N.call("snpmi_stream_sync")
         dist.barrier()
         t0 = time.perf_counter()
-        block_ms = g.run(fill)
+        block_ms = g.run(fill, progress=lambda k, nb: progress("grm5 block %d/%d" % (k + 1, nb))
+                         if (k + 1) % 16 == 0 else None)
         dist.barrier()
         wall = dist.max(time.perf_counter() - t0)
         res = {"wall": wall, "block_ms": block_ms, "n_local_blocks": g.nloc, "m": m, "ms": g.ms, "P": P,
@@ -853,6 +863,8 @@ def grm5_parity(args, picks, gpu_stats, threads):
     t0 = time.perf_counter()
     for s0 in range(0, m, B):
         cnt = min(B, m - s0)
+        if (s0 // B) % 16 == 15:
+            progress("grm5 parity block %d/%d" % (s0 // B + 1, (m + B - 1) // B))
         fill(ctypes.c_void_p(buf.ctypes.data), s0, cnt)
         body = buf[:cnt] if pitch == bpc else np.ascontiguousarray(buf[:cnt, :bpc])
         body = body.reshape(-1)
@@ -1094,6 +1106,63 @@ def leg_file(N, args):
             "seconds": t_all, "read_seconds": t_rd, "snps_per_s": m / t_all, "values_GB": n * m * 4 / 1e9,
             "parity": {"check": "first 256 columns vs oracle one-pass Beta(1,25) (f32)", "max_rel_err": rel,
                        "bit_exact": bool(np.array_equal(cols.T, refb)), "pass": rel <= 1e-5}}
+        # (4) read + Unit standardize, values in HBM: the reference's two calls (the dense kernel
+        # k_std_cols_f timed with HIP events on the library stream -> its roofline; round 3's kernel
+        # beside it through the "std" hook), and the fused call its read().standardize() call sites
+        # now make (_as_snpdata, SnpKernel.read_snps)
+        from pysnptools_amd.snpreader.snpreader import _read_and_standardize
+
+        ev = Events(N, 2)
+        vals_gb = n * m * 4 / 1e9
+        std_ms = {}
+        for variant in (1, 0, 0):  # round 3's kernel, then the shipped one (warm, timed)
+            sd = bed.read(dtype=np.float32, xp="hbm")
+            N.call("snpmi_set_kernel_variant", b"std", variant)
+            try:
+                ev.record(0)
+                sd.standardize(Unit())
+                ev.record(1)
+            finally:
+                N.call("snpmi_set_kernel_variant", b"std", 0)
+            std_ms[variant] = ev.ms(0, 1)
+            if variant == 0:
+                two = np.empty((256, n), dtype=np.float32)
+                N.call("snpmi_memcpy_d2h", N.ptr(two), sd.val.snpmi_ptr, two.nbytes)
+            del sd
+        t0 = time.perf_counter()
+        sd = bed.read(dtype=np.float32, xp="hbm")
+        sd.standardize(Unit())
+        t_two = time.perf_counter() - t0
+        del sd
+        os.environ["ARRAY_MODULE"] = "hbm"
+        _read_and_standardize(bed, Unit(), "F", np.float32)  # warm-up
+        t0 = time.perf_counter()
+        one, _ = _read_and_standardize(bed, Unit(), "F", np.float32)
+        t_one = time.perf_counter() - t0
+        os.environ.pop("ARRAY_MODULE")
+        fused = np.empty((256, n), dtype=np.float32)
+        N.call("snpmi_memcpy_d2h", N.ptr(fused), one.val.snpmi_ptr, fused.nbytes)
+        del one
+        ev.destroy()
+        refu, _ = O.decode_standardize(body, n, m, sid_index=np.arange(256, dtype=np.uint64), dtype=np.float32)
+        ach = 2 * vals_gb / (std_ms[0] * 1e-3)
+        out["read_standardize_unit"] = {
+            "call": "Bed(path).read(dtype=np.float32, xp='hbm').standardize(Unit())",
+            "reference": "bed.py:318-345, unit.py:28-51, standardizer.py:90-133", "values_GB": vals_gb,
+            "seconds_two_calls": t_two, "snps_per_s_two_calls": m / t_two,
+            "standardize_ms": std_ms[0], "standardize_ms_round3_kernel": std_ms[1],
+            "roofline": {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
+                         "traffic": None, "per_call_bytes": 2 * vals_gb * 1e9,
+                         "kernel": "k_std_cols_f<float,1024,16,false>: one workgroup per column, the column held "
+                                   "in registers between the stats and the table apply (read once, written once = "
+                                   "2 x 4 B per value), plus the flag memset + 4-B readback of the call"},
+            "fused_call": "_read_and_standardize(bed, Unit()) = what _as_snpdata / SnpKernel.read_snps run: "
+                          "snpmi_bed_read_standardize_f32 (stats from code counts + table decode, values written once)",
+            "seconds_fused": t_one, "snps_per_s_fused": m / t_one,
+            "parity": {"check": "first 256 columns: two calls vs oracle decode + one-pass Unit (f32), fused vs two "
+                                "calls", "bit_exact": bool(np.array_equal(two.T, refu)),
+                       "fused_bit_exact": bool(np.array_equal(fused, two)),
+                       "pass": bool(np.array_equal(two.T, refu)) and bool(np.array_equal(fused, two))}}
     finally:
         if saved_xp is None:
             os.environ.pop("ARRAY_MODULE", None)
@@ -1155,24 +1224,29 @@ def main(argv=None):
         sys.stderr.flush()
         os._exit(3)
 
+    progress("decode + Unit standardize (value)")
     r1 = leg_standardize(N, args, dist)
     value = args.n_sid * args.steps / r1["wall"]
     grm = grm64 = grm5 = dec_c = e2e = beta = filed = None
     if dist.rank == 0:
+        progress("decode_c / e2e")
         dec_c = leg_decode_c(N, args)
         if args.e2e == "on":
             e2e = leg_e2e(N, args)
     dist.barrier()
     if args.beta == "on":
+        progress("beta (configs[2])")
         rb = leg_standardize(N, args, dist, n=args.beta_iid, n_sid=args.beta_sid, std=N.STD_BETA, a=1.0, b=25.0,
                              miss=0.218, seed=args.seed + 3)
     if not args.skip_grm:
+        progress("grm cfg4 f32 / f64")
         r2 = leg_grm(N, args, dist, "f32")
         grm = grm_entry(args, dist, r2, "f32")
         if args.grm_f64 == "on":
             r2d = leg_grm(N, args, dist, "f64")
             grm64 = grm_entry(args, dist, r2d, "f64")
     if args.grm5 == "on":
+        progress("grm5 cfg5 (part %d)" % dist.rank)
         r3 = leg_grm5(N, args, dist)
         n5, m5, P = args.grm5_iid, r3["m"], r3["P"]
         flops_part = n5 * (n5 + 1) * m5 / P  # this part's share of the SYRK work
@@ -1210,8 +1284,10 @@ def main(argv=None):
             grm5["parity"]["gathered_block_bit_exact"] = r3["gather_exact"]
             grm5["parity"]["pass"] = grm5["parity"]["pass"] and r3["gather_exact"]
     if dist.rank == 0 and args.file == "on":
+        progress("file leg")
         filed = leg_file(N, args)
     if dist.rank == 0:
+        progress("cpu baselines + parity")
         cpu = parity = None
         if not args.skip_cpu and r1["sample"] is not None:
             ref, cpu = cpu_baseline_standardize(args, r1["sample"], timed=dist.world == 1)

@@ -473,20 +473,18 @@ static void bed_read_impl(const char* path, uint64_t n_iid, uint64_t n_sid, int 
                 d2h_rows(d, out + q.c0, m_out * sizeof(T), q.dev_out, q.ldc * sizeof(T), q.cnt * sizeof(T), n_out,
                          nthreads, d.produced[q.slot]);
         }
-        if (stats_out) {
-            SNPMI_HIP(hipStreamWaitEvent(d.copy, d.produced[q.slot], 0));
-            SNPMI_HIP(hipMemcpyAsync(stats + 2 * q.c0, q.st_dev, q.cnt * 2 * sizeof(T), hipMemcpyDeviceToHost, d.copy));
-            SNPMI_HIP(hipStreamSynchronize(d.copy));
-        }
     };
+    // per-SNP stats stay on the device for the whole call and cross PCIe once each way (a per-chunk
+    // D2H on the copy stream would wait for that chunk's kernels and stall the next upload)
+    T* st_all = (T*)d.get(Device::S_STATS, m_out * 2 * sizeof(T));
+    if (std_kind != SNPMI_STD_NONE && use_stats)
+        SNPMI_HIP(hipMemcpyAsync(st_all, stats, m_out * 2 * sizeof(T), hipMemcpyHostToDevice, d.stream));
     for (uint64_t c0 = 0, ci = 0; c0 < m_out; c0 += C, ci++) {
         const uint64_t cnt = std::min(C, m_out - c0);
         const int slot = (int)(ci & 1);
         const uint8_t* packed = stage_chunk(d, m, sid_idx, c0, cnt, p, nthreads, slot);
         T* lut = (T*)d.get(Device::S_LUT, cnt * 4 * sizeof(T));
-        T* st_dev = (T*)d.get(slot ? Device::S_STATS_B : Device::S_STATS, cnt * 2 * sizeof(T));
-        if (std_kind != SNPMI_STD_NONE && use_stats)
-            SNPMI_HIP(hipMemcpyAsync(st_dev, stats + 2 * c0, cnt * 2 * sizeof(T), hipMemcpyHostToDevice, d.stream));
+        T* st_dev = st_all + 2 * c0;
         launch_snp_stats(packed, p.pitch_out, n_out, cnt, count_a1, std_kind, a, b, use_stats, dt, st_dev, lut,
                          d.stream);
         Pending q;
@@ -516,6 +514,7 @@ static void bed_read_impl(const char* path, uint64_t n_iid, uint64_t n_sid, int 
         pending = q;
     }
     if (pending.valid) drain(pending);
+    if (stats_out) SNPMI_HIP(hipMemcpyAsync(stats, st_all, m_out * 2 * sizeof(T), hipMemcpyDeviceToHost, d.stream));
     SNPMI_HIP(hipStreamSynchronize(d.stream));
     SNPMI_HIP(hipStreamSynchronize(d.copy));
 }
@@ -764,12 +763,27 @@ static void syrk_packed_crt(Device& d, const uint8_t* packed, uint64_t pitch, ui
     }
 }
 
+static void syrk_packed_f32_body(Device& d, const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m,
+                                 const void* lut, int dt, void* tiles, int accumulate);
+
 static void syrk_packed_auto(Device& d, const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m,
                              const void* lut, int dt, void* tiles, int accumulate) {
     if (use_crt(dt) && m > 0 && n > 0) {
         syrk_packed_crt(d, packed, pitch, n, m, (const double*)lut, (double*)tiles, accumulate);
         return;
     }
+    if (dt == SNPMI_DT_F32 && g_diag_exact && m > 0 && n > 0) {  // exact diagonal around the SYRK
+        double* diag = (double*)d.get(Device::S_DIAG, n * sizeof(double));
+        launch_diag_begin((const float*)tiles, n, 0, 0, accumulate, diag, d.stream);
+        syrk_packed_f32_body(d, packed, pitch, n, m, lut, dt, tiles, accumulate);
+        launch_diag_end(packed, pitch, n, m, (const float*)lut, (float*)tiles, 0, 0, diag, d.stream);
+        return;
+    }
+    syrk_packed_f32_body(d, packed, pitch, n, m, lut, dt, tiles, accumulate);
+}
+
+static void syrk_packed_f32_body(Device& d, const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m,
+                                 const void* lut, int dt, void* tiles, int accumulate) {
     if (use_bf3(dt)) {
         H2Lut h2;
         const bool h = use_h2() && m > 0;
@@ -795,7 +809,22 @@ static void syrk_packed_auto(Device& d, const uint8_t* packed, uint64_t pitch, u
     else for_z_blocks(d, packed, pitch, n, m, (const double*)lut, run);
 }
 
+static void syrk_packed_part_body(Device& d, const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m,
+                                  const float* lut, int rank, int world, void* blocks, int accumulate);
+
 static void syrk_packed_part_auto(Device& d, const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m,
+                                  const float* lut, int rank, int world, void* blocks, int accumulate) {
+    if (g_diag_exact && m > 0 && n > 0) {  // exact diagonal of the part's diagonal blocks
+        double* diag = (double*)d.get(Device::S_DIAG, n * sizeof(double));
+        launch_diag_begin((const float*)blocks, n, rank, world, accumulate, diag, d.stream);
+        syrk_packed_part_body(d, packed, pitch, n, m, lut, rank, world, blocks, accumulate);
+        launch_diag_end(packed, pitch, n, m, lut, (float*)blocks, rank, world, diag, d.stream);
+        return;
+    }
+    syrk_packed_part_body(d, packed, pitch, n, m, lut, rank, world, blocks, accumulate);
+}
+
+static void syrk_packed_part_body(Device& d, const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m,
                                   const float* lut, int rank, int world, void* blocks, int accumulate) {
     if (use_bf3(SNPMI_DT_F32)) {
         H2Lut h2;
@@ -1237,6 +1266,7 @@ int snpmi_set_kernel_variant(const char* kernel, int variant) {
         SNPMI_REQUIRE(kernel != nullptr, SNPMI_E_ARG, "kernel name is NULL");
         if (std::strcmp(kernel, "decode") == 0) g_variant_decode = variant;
         else if (std::strcmp(kernel, "std") == 0) g_variant_std = variant;
+        else if (std::strcmp(kernel, "diag") == 0) g_diag_exact = variant != 0;
         else if (std::strcmp(kernel, "syrk") == 0) {
 #ifndef SNPMI_UBENCH
             // the product library ships the default chain and the kernels it falls back to:
@@ -1267,6 +1297,7 @@ int snpmi_get_kernel_variant(const char* kernel, int* variant) {
         SNPMI_REQUIRE(kernel != nullptr && variant != nullptr, SNPMI_E_ARG, "kernel name or output is NULL");
         if (std::strcmp(kernel, "decode") == 0) *variant = g_variant_decode;
         else if (std::strcmp(kernel, "std") == 0) *variant = g_variant_std;
+        else if (std::strcmp(kernel, "diag") == 0) *variant = g_diag_exact;
         else if (std::strcmp(kernel, "syrk") == 0) *variant = g_variant_syrk;
         else if (std::strcmp(kernel, "syrk_split") == 0) *variant = g_variant_syrk_split;
         else if (std::strcmp(kernel, "dense_chunk") == 0) *variant = g_dense_chunk;

@@ -1968,6 +1968,72 @@ __global__ __launch_bounds__(kBlock) void k_sumsq(const T* __restrict__ p, uint6
     }
 }
 
+// ------------------------------------------------------------------ exact f32 GRM diagonal
+// K_ii = sum_s v_s(c_is)^2 is the largest entry of each K row and, in an f32 MFMA accumulation
+// chain, the one that rounds worst: it grows by ~1 per SNP (a rare variant adds ~1/(2 maf) at
+// once) while each step's increments are small, so after a few thousand SNPs the chain absorbs
+// them at ulp(K_ii)/2 (the round-3 maxima of |dK| / max diag all sat on the
+// diagonal).  These kernels give every f32 SYRK launch an exact diagonal: before the SYRK the
+// current tile diagonal is saved as f64 (0 when not accumulating), k_diag_sq adds the launch's
+// sum_s v^2 in f64 (each square of an f32 value is exact in f64; one f64 add per SNP), and after
+// the SYRK the tile diagonal is overwritten with the f64 value rounded once to f32.
+// Layout: part_world == 0 -> upper-triangle 128x128 tiles (index tj(tj+1)/2 + ti, row-major);
+// else the 256x256 blocks of part part_rank (block L = J(J+1)/2 + I, owner L mod part_world,
+// local index L / part_world, row-major), diagonal entries only where this part owns the block.
+__device__ __forceinline__ int64_t diag_offset(uint64_t i, int part_rank, int part_world) {
+    if (part_world == 0) {
+        const uint64_t t = i / 128, r = i % 128;
+        return (int64_t)((t * (t + 1) / 2 + t) * 128 * 128 + r * 128 + r);
+    }
+    const uint64_t J = i / 256, r = i % 256, L = J * (J + 1) / 2 + J;
+    if (L % (uint64_t)part_world != (uint64_t)part_rank) return -1;
+    return (int64_t)((L / (uint64_t)part_world) * 256 * 256 + r * 256 + r);
+}
+
+__global__ __launch_bounds__(kBlock) void k_diag_save(const float* __restrict__ K, uint64_t n, int part_rank,
+                                                      int part_world, int accumulate, double* __restrict__ diag) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const int64_t o = diag_offset(i, part_rank, part_world);
+        diag[i] = (accumulate && o >= 0) ? (double)K[o] : 0.0;
+    }
+}
+
+// grid.x: 16-iid words (one packed dword per thread and SNP, coalesced across the wave),
+// grid.y: SNP slices (enough threads to fill the chip at any n); one f64 atomic per iid and slice
+__global__ __launch_bounds__(kBlock) void k_diag_sq(const uint8_t* __restrict__ packed, uint64_t pitch, uint64_t n,
+                                                    uint64_t m, const float* __restrict__ lut, uint64_t per_slice,
+                                                    double* __restrict__ diag) {
+    const uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t nw = (n + 15) / 16;
+    if (w >= nw) return;
+    const uint64_t s0 = (uint64_t)blockIdx.y * per_slice, s1 = min(m, s0 + per_slice);
+    double acc[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) acc[k] = 0.0;
+    for (uint64_t s = s0; s < s1; s++) {
+        const uint32_t word = reinterpret_cast<const uint32_t*>(packed + s * pitch)[w];
+        const float4 l = reinterpret_cast<const float4*>(lut)[s];  // the same address on every lane
+        const double q0 = (double)l.x * (double)l.x, q1 = (double)l.y * (double)l.y, q2 = (double)l.z * (double)l.z,
+                     q3 = (double)l.w * (double)l.w;
+#pragma unroll
+        for (int k = 0; k < 16; k++) {
+            const uint32_t c = (word >> (2 * k)) & 3u;
+            acc[k] += c == 0 ? q0 : c == 1 ? q1 : c == 2 ? q2 : q3;
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 16; k++)
+        if (16 * w + k < n) atomicAdd(diag + 16 * w + k, acc[k]);
+}
+
+__global__ __launch_bounds__(kBlock) void k_diag_patch(float* __restrict__ K, uint64_t n, int part_rank,
+                                                       int part_world, const double* __restrict__ diag) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const int64_t o = diag_offset(i, part_rank, part_world);
+        if (o >= 0) K[o] = (float)diag[i];
+    }
+}
+
 // ------------------------------------------------------------------ synthetic genotypes
 __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
     x += 0x9E3779B97F4A7C15ull;
@@ -2147,6 +2213,7 @@ inline unsigned grid_for(uint64_t work, uint64_t per_block, unsigned cap = 65536
 
 // ====================================================================== launchers
 int g_variant_decode = 0;  // tuning hook (snpmi_set_kernel_variant); no variants at present
+int g_diag_exact = 1;     // exact f32 GRM diagonal (k_diag_*), hook "diag"
 int g_variant_std = 0;     // dense standardize: 0 = k_std_cols_f / k_std_cols_c16, 1 = round 3's kernels
 
 #define SNPMI_LAUNCH_CHECK() SNPMI_HIP(hipGetLastError())
@@ -2737,6 +2804,28 @@ void launch_tile_reduce(const float* partial, unsigned slices, uint64_t elems, f
     if (n4 == 0) return;
     k_tile_reduce<<<grid_for(n4, kBlock, 256 * 16), kBlock, 0, st>>>((const f32x4_t*)partial, slices, n4,
                                                                       (f32x4_t*)tiles, accumulate);
+    SNPMI_LAUNCH_CHECK();
+}
+
+void launch_diag_begin(const float* K, uint64_t n, int part_rank, int part_world, int accumulate, double* diag,
+                       hipStream_t st) {
+    if (n == 0) return;
+    k_diag_save<<<grid_for(n, kBlock), kBlock, 0, st>>>(K, n, part_rank, part_world, accumulate, diag);
+    SNPMI_LAUNCH_CHECK();
+}
+
+void launch_diag_end(const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m, const float* lut, float* K,
+                     int part_rank, int part_world, double* diag, hipStream_t st) {
+    if (n == 0) return;
+    if (m > 0) {
+        const uint64_t nw = (n + 15) / 16, bx = ceil_div(nw, kBlock);
+        // enough (word, slice) threads to fill 256 CUs several times over, slices of >= 64 SNPs
+        const uint64_t slices = std::max<uint64_t>(1, std::min<uint64_t>(ceil_div(m, 64), ceil_div(256 * 1024, nw)));
+        const uint64_t per = ceil_div(m, slices);
+        k_diag_sq<<<dim3((unsigned)bx, (unsigned)ceil_div(m, per)), kBlock, 0, st>>>(packed, pitch, n, m, lut, per, diag);
+        SNPMI_LAUNCH_CHECK();
+    }
+    k_diag_patch<<<grid_for(n, kBlock), kBlock, 0, st>>>(K, n, part_rank, part_world, diag);
     SNPMI_LAUNCH_CHECK();
 }
 

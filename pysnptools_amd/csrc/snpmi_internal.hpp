@@ -74,7 +74,7 @@ struct Device {
     // grow-only scratch slots
     enum Slot { S_PACKED, S_PACKED2, S_IDX, S_IDX2, S_LUT, S_STATS, S_OUT, S_TILES, S_K, S_DENSE,
                 S_DENSE2, S_RED, S_SESSION, S_PACKED_B, S_ZBLK, S_IDX32, S_LUT3, S_H2, S_OUT_B, S_STATS_B,
-                S_WIN, S_DPACK, S_DLUT, S_CRTREC, S_SEG, S_STDFLAG, S_NUM };
+                S_WIN, S_DPACK, S_DLUT, S_CRTREC, S_SEG, S_STDFLAG, S_DIAG, S_NUM };
     void* buf[S_NUM] = {};
     // chunk pipeline events (slot = chunk parity), all on-device ordering, no host spin:
     hipEvent_t staged[2] = {};    // copy stream: H2D of pinned slot done (host may refill it)
@@ -165,6 +165,14 @@ void launch_grm_extract_rows(const void* tiles, uint64_t n, int dtype, uint64_t 
 void launch_grm_extract(const void* tiles, uint64_t n, int dtype, const uint64_t* ri, uint64_t nr,
                         const uint64_t* ci, uint64_t nc, int order_c, double scale, void* out, hipStream_t st);
 void launch_grm_trace(const void* tiles, uint64_t n, int dtype, double* trace_dev, hipStream_t st);
+// exact f32 GRM diagonal around one f32 SYRK launch (kernels.hip k_diag_*): begin saves the current
+// diagonal as f64 (0 unless accumulating), end adds sum_s lut_s[code]^2 in f64 and writes it back
+// rounded once.  part_world == 0: upper-triangle tiles; else the blocks of part part_rank.
+extern int g_diag_exact;  // hook "diag": 1 (default) = on, 0 = the SYRK's own diagonal
+void launch_diag_begin(const float* K, uint64_t n, int part_rank, int part_world, int accumulate, double* diag,
+                       hipStream_t st);
+void launch_diag_end(const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m, const float* lut, float* K,
+                     int part_rank, int part_world, double* diag, hipStream_t st);
 void launch_dense_scale(void* p, uint64_t count, int dtype, double scale, hipStream_t st);
 void launch_sumsq(const void* p, uint64_t count, int dtype, double* out_dev, hipStream_t st);
 void launch_dense_trace(const void* K, uint64_t n, int dtype, double* trace_dev, hipStream_t st);

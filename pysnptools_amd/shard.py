@@ -371,9 +371,10 @@ class PartitionedGrm(object):
         self._ev.append(e)
         return e
 
-    def run(self, fill):
+    def run(self, fill, progress=None):
         """Stream the ``m`` SNPs through steps 1-4 (see the class doc).  Returns per-block timings
-        (ms, HIP events on the compute stream) when ``timing`` was set, else None."""
+        (ms, HIP events on the compute stream) when ``timing`` was set, else None.  ``progress(k,
+        nblk)`` (optional) is called on the host after block k is enqueued."""
         N = self.N
         nblk = (self.m + self.block - 1) // self.block
         up = [self._event(), self._event()]  # copy stream: share of the slot uploaded (host slot free)
@@ -416,6 +417,8 @@ class PartitionedGrm(object):
             if marks:
                 N.call("snpmi_event_record", marks[k][1])
             N.call("snpmi_event_record", done[slot])
+            if progress is not None:
+                progress(k, nblk)
         N.call("snpmi_stream_sync")
         if not marks:
             return None

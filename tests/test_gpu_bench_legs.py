@@ -129,6 +129,7 @@ def test_bench_with_rccl_communicator_world1(collective):
     f = d["file"]
     assert f["read_kernel_f32"]["parity"]["pass"], f["read_kernel_f32"]["parity"]
     assert f["read_hbm"]["parity"]["bit_exact"] and f["read_standardize_beta"]["parity"]["pass"], f
+    assert f["read_standardize_unit"]["parity"]["pass"], f["read_standardize_unit"]
     assert d["grm"]["cpu_baseline"]["projected_seconds"] > 0
     for k in ("grm", "grm_f64"):
         assert d[k]["parity"]["pass"], d[k]["parity"]

@@ -223,3 +223,19 @@ def test_synth_generator_properties():
     assert 0.003 < miss < 0.02
     assert np.nanmax(val) <= 2 and np.nanmin(val) >= 0
     assert np.all(a[:, 251:] == 0)
+
+
+@pytest.mark.parametrize("n", [1, 3, 4, 5, 299, 300, 4099])
+@pytest.mark.parametrize("count_A1", [False, True])
+def test_snp_stats_matches_decode_then_standardize(n, count_A1):
+    """oracle.snp_stats (code counts, whole bytes through a per-byte table) == the stats of decode +
+    one-pass standardize, including the pad codes of a partial last byte and all-missing columns."""
+    rng = np.random.default_rng(n)
+    m = 23
+    bpc = (n + 3) // 4
+    body = rng.integers(0, 256, size=m * bpc, dtype=np.uint8)
+    body[:bpc] = 0x55  # all missing (code 1)
+    Z = O.decode(body, n, m, count_A1=count_A1, dtype=np.float64)
+    st_dec = O.standardize_native(Z)
+    st = O.snp_stats(body, n, m, count_A1=count_A1)
+    np.testing.assert_array_equal(st, st_dec)

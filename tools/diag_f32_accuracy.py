@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--chunks", default="65536")
     ap.add_argument("--segs", default="0,4096,8192,16384", help="syrk 'seg' settings (SNPs per f32 chain)")
     ap.add_argument("--variants", default="0,36,20")
+    ap.add_argument("--diags", default="1,0", help="hook 'diag': 1 = exact f64 diagonal (round 4 default), 0 = off")
     args = ap.parse_args()
     import bench
     from oracle import oracle as O
@@ -55,6 +56,11 @@ def main():
 
     def report(name, K, **extra):
         d = np.abs(K.astype(np.float64) - ref)
+        off = d.copy()
+        off[np.arange(R), np.arange(R)] = 0  # the diagonal entries of rows 0..R-1
+        io, jo = np.unravel_index(np.argmax(off), off.shape)
+        extra = dict(extra, offdiag_max_abs_err_over_max_diag=float(off.max() / scale), offdiag_at=[int(io), int(jo)],
+                     offdiag_ref_there=float(ref[io, jo]))
         i, j = np.unravel_index(np.argmax(d), d.shape)
         print(json.dumps({"path": name, "max_abs_err_over_max_diag": float(d.max() / scale),
                           "at": [int(i), int(j)], "ref_there": float(ref[i, j]), "max_diag": float(scale),
@@ -70,7 +76,8 @@ def main():
     ev = [ctypes.c_void_p(), ctypes.c_void_p()]
     for e in ev:
         N.call("snpmi_event_create", ctypes.byref(e))
-    for seg in [int(x) for x in args.segs.split(",")]:
+    for dg, seg in [(int(d_), int(x)) for d_ in args.diags.split(",") for x in args.segs.split(",")]:
+        N.call("snpmi_set_kernel_variant", b"diag", dg)
         N.call("snpmi_set_kernel_variant", b"seg", seg)
         labels = {0: "fp16x2", 36: "bf16x3", 20: "f32_mfma"}
         for variant in [int(v) for v in args.variants.split(",")]:
@@ -93,9 +100,11 @@ def main():
                 K = np.empty((R, n), dtype=np.float32)
                 N.call("snpmi_memcpy_d2h", N.ptr(K), dout.p, K.nbytes)
                 g.abort()
-                report("%s_chunk%d_seg%d" % (label, chunk, seg), K, ms=ms.value, tflops=n * (n + 1) * m / (ms.value * 1e-3) / 1e12)
+                report("%s_chunk%d_seg%d_diag%d" % (label, chunk, seg, dg), K, ms=ms.value,
+                       tflops=n * (n + 1) * m / (ms.value * 1e-3) / 1e12)
     N.call("snpmi_set_kernel_variant", b"seg", 8192)
     N.call("snpmi_set_kernel_variant", b"syrk", 0)
+    N.call("snpmi_set_kernel_variant", b"diag", 1)
 
 
 if __name__ == "__main__":
