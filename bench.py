@@ -931,7 +931,7 @@ def grm_entry(args, dist, r, dtype):
                 "traffic": pmc_traffic("f32w::k_syrk_h2", "grm", n, r["snps_per_launch"]),
                 "traffic_note": "PMC HBM bytes per launch (profiles/traffic.json) vs algorithmic ~2 x 5 GB of K tiles "
                                 "(accumulate read + write) + 0.8 GB of codes at 50k x 62.5k: the rest is the SegFlush "
-                                "slots (256 KiB per workgroup, flushed every 8192 SNPs by f32 atomics at L2 and read "
+                                "slots (256 KiB per workgroup, flushed every 12288 SNPs by f32 atomics at L2 and read "
                                 "back once, DESIGN.md 3.4) and panel re-fetches from the MALL; at ~0.45 TB/s it is "
                                 "not the limiter of this MFMA-bound kernel",
                 "kernel": "f32w::k_syrk_h2<false,4>: f32 GRM as 3 fp16 MFMA products of each value's fp16x2 "

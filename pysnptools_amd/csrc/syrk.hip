@@ -2471,7 +2471,7 @@ __global__ __launch_bounds__(256, 2) void k_syrk_glds(const double* __restrict__
 int g_variant_syrk = 0;  // tuning hook (snpmi_set_kernel_variant "syrk")
 // 8192: 4.9e-6 of max diag at 50k x 100k on SnpGen-shaped data (21.8% missing) for +2.2% time;
 // 4096: 2.6e-6 for +3.8%; 16384: 6.9e-6 for +1.9%; none: 3.2e-5 (profiles/r03acc, r03seg)
-int g_seg_snps = 8192;   // tuning hook "seg"
+int g_seg_snps = 12288;  // tuning hook "seg" (round 4: 12288 with the exact f64 diagonal, k_diag_*)
 
 // host-side segmentation for the f32-MFMA kernels without SegFlush (fallbacks and small-N
 // kernels): one launch per <= g_seg_snps / 2 SNPs, each accumulating onto the previous ones

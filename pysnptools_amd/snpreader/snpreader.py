@@ -92,7 +92,8 @@ class SnpReader(PstReader):
         """The iid x iid kernel (GRM) of the standardized SNPs, as a KernelData (snpreader.py:528-561).
 
         Numerics: ``dtype=float32`` runs as the fp16x2 split on the fp16 MFMA (22 of f32's 24
-        bits per value, exact products, f32 accumulation restarted every 8192 SNPs): within ~5e-6
+        bits per value, exact products, f32 accumulation restarted every 12288 SNPs, the diagonal
+        accumulated exactly in f64): within ~1e-6
         of max diag(K) of the exact GRM.  ``dtype=float64`` (default) runs as exact integer products
         of 51-52-bit quantised values on the int8 MFMA (~1e-13 relative per value when a rare
         variant sets the block's scale); ``pysnptools_amd.set_grm_f64("mfma")`` selects the f64 MFMA

@@ -1,7 +1,8 @@
 """f32 GRM accuracy at large M on SnpGen-shaped data (rare-variant heavy MAF curve, 21.8% missing):
-the f32 accumulation chains of the SYRK kernels are cut every `seg` SNPs (8192; syrk.hip SegFlush /
-for_segments), so one launch over tens of thousands of SNPs stays within the f32 bar (1e-5 of max
-diag; asserted here at 6e-6) against the f64 oracle.  Before the segmentation one 62.5k-SNP launch of the fp16x2 kernel drifted 2e-5 of max
+the f32 accumulation chains of the SYRK kernels are cut every `seg` SNPs (12288; syrk.hip SegFlush /
+for_segments) and the diagonal is accumulated exactly in f64 (k_diag_*), so one launch over tens
+of thousands of SNPs stays within the f32 bar (1e-5 of max diag; asserted here at 6e-6, and at
+2e-6 over 200k SNPs) against the f64 oracle.  Before the segmentation one 62.5k-SNP launch of the fp16x2 kernel drifted 2e-5 of max
 diag at 50k x 100k (bench `file` leg), because the tiny z^2 of rare-variant SNPs were absorbed into
 K_ii ~ 1e5.  Checked for the three f32 kernels: fp16x2 (default), bf16x3 (its range fallback,
 variant 36) and the f32 MFMA (variant 20: 2 products per MFMA k-step, so twice the chain steps of
@@ -95,6 +96,7 @@ def test_segment_flush_edges_vs_oracle(m_edge, seg):
     vs the f64 oracle at the f32 bar, and the segmented K within 2e-6 of max diag of the
     unsegmented one."""
     nn = 3000
+    seg_default = N.kernel_variant("seg")
     pitch = N.lib().snpmi_packed_pitch(nn)
     packed = bench.Dev(N, pitch * m_edge)
     bench.synth(N, packed.p, pitch, nn, 0, m_edge, 17, 0.05)
@@ -122,7 +124,7 @@ def test_segment_flush_edges_vs_oracle(m_edge, seg):
                 d.free()
             return K.astype(np.float64)
         finally:
-            N.call("snpmi_set_kernel_variant", b"seg", 8192)
+            N.call("snpmi_set_kernel_variant", b"seg", seg_default)
 
     try:
         Ks, K0 = rows(seg), rows(0)
@@ -131,3 +133,45 @@ def test_segment_flush_edges_vs_oracle(m_edge, seg):
     scale = np.abs(np.diag(ref[:, :R])).max()
     assert np.abs(Ks - ref).max() / scale <= 1e-5
     assert np.abs(Ks - K0).max() / scale <= 2e-6
+
+
+def test_default_f32_grm_over_200k_snps_within_2e6():
+    """the default f32 GRM (fp16x2 SYRK, 12288-SNP chains, exact f64 diagonal)
+    at 50,000 iids x 204,800 SnpGen-shaped SNPs (21.8% missing) through ShardedGrm in launches of
+    <= 65536 SNPs, as Bed.read_kernel runs it: K rows 0..7 vs the f64 oracle within 2e-6 of max
+    diag (round 3: 4.1-4.9e-6), the diagonal within 1e-6 relative."""
+    nn, mm, rows = 50_000, 204_800, 8
+    pitch = N.lib().snpmi_packed_pitch(nn)
+    packed = bench.Dev(N, pitch * mm)
+    stats = bench.Dev(N, mm * 8)
+    try:
+        bench.synth(N, packed.p, pitch, nn, 0, mm, 311, 0.218)
+        g = ShardedGrm(nn, np.float32, None, "none")
+        g.add_packed(packed.p, pitch, mm, N.STD_UNIT, 0.0, 0.0, 0, stats.p)
+        t, _ = g.tiles()
+        ri = np.arange(rows, dtype=np.uint64)
+        dri, dout = bench.Dev(N, rows * 8), bench.Dev(N, rows * nn * 4)
+        N.call("snpmi_memcpy_h2d", dri.p, N.ptr(ri), ri.nbytes)
+        N.call("snpmi_dev_grm_extract", t, nn, N.DT_F32, dri.p, rows, None, nn, 1, 1.0, dout.p)
+        K = np.empty((rows, nn), dtype=np.float32)
+        N.call("snpmi_memcpy_d2h", N.ptr(K), dout.p, K.nbytes)
+        g.abort()
+        dri.free()
+        dout.free()
+        ref = np.zeros((rows, nn))
+        chunk = 8192
+        host = np.empty((chunk, pitch), dtype=np.uint8)
+        for s0 in range(0, mm, chunk):
+            c = min(chunk, mm - s0)
+            N.call("snpmi_memcpy_d2h", N.ptr(host), packed.at(s0 * pitch), c * pitch)
+            body = np.ascontiguousarray(host[:c, :(nn + 3) // 4]).reshape(-1)
+            Z, _ = O.decode_standardize(body, nn, c, dtype=np.float64, num_threads=16)
+            ref += Z[:rows].dot(Z.T)
+    finally:
+        packed.free()
+        stats.free()
+    scale = np.abs(np.diag(ref[:, :rows])).max()
+    err = np.abs(K.astype(np.float64) - ref).max() / scale
+    assert err <= 2e-6, err
+    diag_rel = np.max(np.abs(np.diag(K[:, :rows]) - np.diag(ref[:, :rows])) / np.diag(ref[:, :rows]))
+    assert diag_rel <= 1e-6, diag_rel

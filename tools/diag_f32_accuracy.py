@@ -102,7 +102,7 @@ def main():
                 g.abort()
                 report("%s_chunk%d_seg%d_diag%d" % (label, chunk, seg, dg), K, ms=ms.value,
                        tflops=n * (n + 1) * m / (ms.value * 1e-3) / 1e12)
-    N.call("snpmi_set_kernel_variant", b"seg", 8192)
+    N.call("snpmi_set_kernel_variant", b"seg", 12288)
     N.call("snpmi_set_kernel_variant", b"syrk", 0)
     N.call("snpmi_set_kernel_variant", b"diag", 1)
 
