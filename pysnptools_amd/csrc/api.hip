@@ -1267,6 +1267,7 @@ int snpmi_set_kernel_variant(const char* kernel, int variant) {
         if (std::strcmp(kernel, "decode") == 0) g_variant_decode = variant;
         else if (std::strcmp(kernel, "std") == 0) g_variant_std = variant;
         else if (std::strcmp(kernel, "diag") == 0) g_diag_exact = variant != 0;
+        else if (std::strcmp(kernel, "extract") == 0) g_variant_extract = variant;
         else if (std::strcmp(kernel, "syrk") == 0) {
 #ifndef SNPMI_UBENCH
             // the product library ships the default chain and the kernels it falls back to:
@@ -1298,6 +1299,7 @@ int snpmi_get_kernel_variant(const char* kernel, int* variant) {
         if (std::strcmp(kernel, "decode") == 0) *variant = g_variant_decode;
         else if (std::strcmp(kernel, "std") == 0) *variant = g_variant_std;
         else if (std::strcmp(kernel, "diag") == 0) *variant = g_diag_exact;
+        else if (std::strcmp(kernel, "extract") == 0) *variant = g_variant_extract;
         else if (std::strcmp(kernel, "syrk") == 0) *variant = g_variant_syrk;
         else if (std::strcmp(kernel, "syrk_split") == 0) *variant = g_variant_syrk_split;
         else if (std::strcmp(kernel, "dense_chunk") == 0) *variant = g_dense_chunk;

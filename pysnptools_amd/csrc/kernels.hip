@@ -1911,6 +1911,69 @@ __global__ __launch_bounds__(kBlock) void k_grm_extract_rows(const T* __restrict
     }
 }
 
+// The whole K (rows 0..n-1): one workgroup per upper-triangle 64x64 block (I <= J), read ONCE from
+// the tiles with 16-B loads into LDS and written twice -- as block (I, J) straight and as its
+// mirror (J, I) through the LDS transpose -- so the tiles cross HBM once (half the reads of
+// k_grm_extract_rows, which loads every upper block for both output positions).  A diagonal block
+// mirrors its own upper half.  Blocks are visited in triangular order, the grid strides over them.
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_grm_extract_sym(const T* __restrict__ tiles, uint64_t n, double scale,
+                                                            T* __restrict__ out) {
+    constexpr int V = 16 / sizeof(T);  // elements per 16-B vector
+    constexpr int TPR = 64 / V;        // threads per 64-element row
+    constexpr int RPP = kBlock / TPR;  // rows per pass
+    typedef T vec_t __attribute__((ext_vector_type(V)));
+    __shared__ T S[64][64 + 1];
+    const int t = threadIdx.x, x = t % TPR;
+    const uint64_t nb = (n + 63) / 64, total = nb * (nb + 1) / 2;
+    for (uint64_t L = blockIdx.x; L < total; L += gridDim.x) {
+        uint64_t J = (uint64_t)((sqrt(8.0 * (double)L + 1.0) - 1.0) * 0.5);
+        while ((J + 1) * (J + 2) / 2 <= L) J++;
+        while (J * (J + 1) / 2 > L) J--;
+        const uint64_t I = L - J * (J + 1) / 2;
+        const uint64_t R0 = I * 64, C0 = J * 64;
+        for (int y = t / TPR; y < 64; y += RPP) {
+            const uint64_t i = R0 + y, j0 = C0 + (uint64_t)x * V;
+            T v[V];
+            if (I != J && i < n && j0 + V <= n) {
+                const vec_t q = *reinterpret_cast<const vec_t*>(
+                    tiles + tile_index(i / kTile, j0 / kTile) * (kTile * kTile) + (i % kTile) * kTile + (j0 % kTile));
+#pragma unroll
+                for (int e = 0; e < V; e++) v[e] = q[e];
+            } else {
+#pragma unroll
+                for (int e = 0; e < V; e++) {
+                    const uint64_t j = j0 + e, ii = i < j ? i : j, jj = i < j ? j : i;
+                    v[e] = (i < n && j < n) ? tiles[tile_index(ii / kTile, jj / kTile) * (kTile * kTile) +
+                                                    (ii % kTile) * kTile + (jj % kTile)]
+                                            : (T)0;
+                }
+            }
+#pragma unroll
+            for (int e = 0; e < V; e++) S[y][x * V + e] = scale == 1.0 ? v[e] : (T)((double)v[e] * scale);
+        }
+        __syncthreads();
+        for (int pass = 0; pass < (I == J ? 1 : 2); pass++) {
+            const uint64_t rb = pass ? C0 : R0, cb = pass ? R0 : C0;
+            for (int y = t / TPR; y < 64; y += RPP) {
+                const uint64_t r = rb + y, c0 = cb + (uint64_t)x * V;
+                if (r >= n || c0 >= n) continue;
+                vec_t w;
+#pragma unroll
+                for (int e = 0; e < V; e++) w[e] = pass ? S[x * V + e][y] : S[y][x * V + e];
+                T* o = out + r * n + c0;
+                if (c0 + V <= n && (reinterpret_cast<uintptr_t>(o) & 15) == 0) {
+                    __builtin_nontemporal_store(w, reinterpret_cast<vec_t*>(o));
+                } else {
+                    for (int e = 0; e < V; e++)
+                        if (c0 + e < n) o[e] = w[e];
+                }
+            }
+        }
+        __syncthreads();
+    }
+}
+
 template <typename T>
 __global__ __launch_bounds__(kBlock) void k_grm_trace(const T* __restrict__ tiles, uint64_t n, double* trace) {
     __shared__ double red[kBlock / kWave];
@@ -2214,7 +2277,8 @@ inline unsigned grid_for(uint64_t work, uint64_t per_block, unsigned cap = 65536
 // ====================================================================== launchers
 int g_variant_decode = 0;  // tuning hook (snpmi_set_kernel_variant); no variants at present
 int g_diag_exact = 1;     // exact f32 GRM diagonal (k_diag_*), hook "diag"
-int g_variant_std = 0;     // dense standardize: 0 = k_std_cols_f / k_std_cols_c16, 1 = round 3's kernels
+int g_variant_std = 0;
+int g_variant_extract = 0;  // whole-K extraction: 0 = k_grm_extract_sym, 1 = round 3's k_grm_extract_rows     // dense standardize: 0 = k_std_cols_f / k_std_cols_c16, 1 = round 3's kernels
 
 #define SNPMI_LAUNCH_CHECK() SNPMI_HIP(hipGetLastError())
 
@@ -2716,6 +2780,16 @@ void launch_grm_extract(const void* tiles, uint64_t, int dtype, const uint64_t* 
 void launch_grm_extract_rows(const void* tiles, uint64_t n, int dtype, uint64_t r0, uint64_t nr, double scale,
                              void* out, hipStream_t st) {
     if (nr == 0 || n == 0) return;
+    if (r0 == 0 && nr == n && g_variant_extract == 0) {  // the whole K: each upper block read once
+        const uint64_t nb = (n + 63) / 64;
+        const unsigned g = grid_for(nb * (nb + 1) / 2, 1, 256 * 16);
+        if (dtype == SNPMI_DT_F32)
+            k_grm_extract_sym<float><<<g, kBlock, 0, st>>>((const float*)tiles, n, scale, (float*)out);
+        else
+            k_grm_extract_sym<double><<<g, kBlock, 0, st>>>((const double*)tiles, n, scale, (double*)out);
+        SNPMI_LAUNCH_CHECK();
+        return;
+    }
     const uint64_t blocks = ((r0 + nr + 63) / 64 - r0 / 64) * ((n + 63) / 64);
     const unsigned g = grid_for(blocks, 1, 256 * 16);
     if (dtype == SNPMI_DT_F32)

@@ -103,6 +103,7 @@ void release_pinned();
 // ------------------------------------------------------------------ kernel launchers (kernels.hip)
 extern int g_variant_decode;
 extern int g_variant_std;
+extern int g_variant_extract;
 extern int g_variant_syrk;
 extern int g_dense_chunk;
 // f32 GRM accumulation segments (syrk.hip SegFlush): every `snps` SNPs a workgroup adds its MFMA

@@ -285,13 +285,14 @@ class PartitionedGrm(object):
        ``snpmi_bed_gather_packed``; bench.py: a synthetic generator).  Rank r of the ``world`` ranks
        of ``dist`` owns columns [r*ms, (r+1)*ms) of each block, ms = ceil(block/world).
     2. The copy stream uploads the share into its slot of a device block buffer.
-    3. ``dist.allgather_dev`` (ncclAllGather over xGMI) rebuilds the whole block on every rank.
+    3. ``dist.allgather_dev`` (ncclAllGather over xGMI, on the library's aux stream) rebuilds the
+       whole block on every rank.
     4. iid selection (``k_repack*``), per-SNP stats + LUT (``k_snp_stats``; every rank sees every
        iid of the SNP, so the stats are identical on every rank without an exchange), then the fp16x2
        MFMA SYRK adds the block into this part's K blocks (``snpmi_dev_syrk_packed_part``).
 
-    Two slots: block k+1's fill (host threads) and upload (copy stream) run under block k's kernels;
-    the compute stream waits on events only.  At world 1 the all-gather is a no-op and the one rank
+    Two slots: block k+1's fill (host threads), upload (copy stream) and all-gather (aux stream) run
+    under block k's kernels; the compute stream waits on events only.  At world 1 the all-gather is a no-op and the one rank
     fills whole blocks -- a single-GPU run of any part (``parts`` may exceed ``world``: bench.py
     computes part 0 of the 8-GPU plan on one GPU)."""
 
@@ -379,6 +380,7 @@ class PartitionedGrm(object):
         nblk = (self.m + self.block - 1) // self.block
         up = [self._event(), self._event()]  # copy stream: share of the slot uploaded (host slot free)
         done = [self._event(), self._event()]  # compute stream: the slot's kernels are done
+        gathered = [self._event(), self._event()]  # aux stream: the slot's block is all-gathered
         used = [False, False]
         marks = [(self._event(), self._event()) for _ in range(nblk)] if self.timing else None
         if self.m == 0 or self.n == 0:
@@ -399,12 +401,22 @@ class PartitionedGrm(object):
                 N.call("snpmi_stream_wait_event", done[slot], 1)  # the device slot's readers are done
             N.call("snpmi_memcpy_async", dst, self.host[slot].p, ms * self.pitch_src, 0, 1)
             N.call("snpmi_event_record_on", up[slot], 1)
-            N.call("snpmi_stream_wait_event", up[slot], 0)
+            if self.world > 1 or (self.dist is not None and self.dist.rccl):  # in place at world 1
+                # the all-gather runs on the aux stream, so block k+1's exchange over xGMI overlaps
+                # block k's SYRK on the compute stream; the compute stream waits on its event
+                N.call("snpmi_stream_wait_event", up[slot], 2)
+                N.call("snpmi_set_stream", 2)
+                try:
+                    self.dist.allgather_dev(dst, self.dev[slot].p, ms * self.pitch_src)
+                finally:
+                    N.call("snpmi_set_stream", 0)
+                N.call("snpmi_event_record_on", gathered[slot], 2)
+                N.call("snpmi_stream_wait_event", gathered[slot], 0)
+            else:
+                N.call("snpmi_stream_wait_event", up[slot], 0)
             used[slot] = True
             if marks:
                 N.call("snpmi_event_record", marks[k][0])
-            if self.world > 1 or (self.dist is not None and self.dist.rccl):  # in place at world 1
-                self.dist.allgather_dev(dst, self.dev[slot].p, ms * self.pitch_src)
             packed, pitch = self.dev[slot].p, self.pitch_src
             if self.rep is not None:
                 N.call("snpmi_dev_repack", packed, pitch, self.n_src, self.idx.p, self.n, cnt, self.rep.p, self.pitch)
