@@ -39,6 +39,13 @@ __device__ __forceinline__ double beta_weight(double mean, double a, double b) {
     return pow(maf, a - 1.0) * pow(1.0 - maf, b - 1.0) / exp(lbeta);
 }
 
+// The same function behind a call: in k_std_cols_f it runs once per column on one thread, and
+// inlined its lgamma / pow would set the register count of the whole kernel (~35 VGPRs more,
+// which the column-in-registers path cannot spare).  Same code, so the same bits.
+__device__ __attribute__((noinline)) double beta_weight_call(double mean, double a, double b) {
+    return beta_weight(mean, a, b);
+}
+
 // value of code c (count_A1 selects the A1 LUT); -1 = missing
 __device__ __forceinline__ int code_value(int c, int count_a1) {
     // count_A1=False {0,-,1,2}; count_A1=True {2,-,1,0}
@@ -1435,7 +1442,7 @@ __device__ __forceinline__ void col_const(ColConst& cc, double mean, double sd, 
                                           int use_stats) {
     cc.mean = mean;
     cc.sd = sd;
-    cc.w = BETA && is_beta ? beta_weight(mean, a, b) : 0.0;
+    cc.w = BETA && is_beta ? beta_weight_call(mean, a, b) : 0.0;
     cc.zero_col = is_beta && use_stats && __builtin_isinf(sd);
     for (int v = 0; v < 3; v++) cc.l[v] = (double)apply_one((T)v, mean, sd, is_beta, cc.w, cc.zero_col != 0);
 }
@@ -2698,9 +2705,12 @@ void launch_dense_standardize(void* val, uint64_t rows, uint64_t cols, uint64_t 
             k_std_cols_f<double, NT, NV, BETA><<<g, NT, 0, st>>>((double*)val, rows, cols, ld, std_kind, a, b,      \
                                                                  use_stats, (double*)stats, flags, any);            \
     } while (0)
-        if (beta) {  // Beta: beta_weight's registers leave room for 4 vectors per thread
+        if (beta) {
             if (nvec <= 256 * 4) SNPMI_STD_F(256, 4, true);
-            else SNPMI_STD_F(1024, 4, true);
+            else if (nvec <= 256 * 16) SNPMI_STD_F(256, 16, true);
+            else if (nvec <= 1024 * 8) SNPMI_STD_F(1024, 8, true);
+            else if (nvec <= 1024 * 16) SNPMI_STD_F(1024, 16, true);
+            else SNPMI_STD_F(1024, 8, true);
         } else if (nvec <= 256 * 4) SNPMI_STD_F(256, 4, false);
         else if (nvec <= 256 * 16) SNPMI_STD_F(256, 16, false);
         else if (nvec <= 1024 * 8) SNPMI_STD_F(1024, 8, false);

@@ -35,7 +35,7 @@ class Dev:
 
 
 @pytest.mark.parametrize("dt,n", [(np.float32, 1000), (np.float32, 4157), (np.float64, 333), (np.float64, 2050),
-                                  (np.float32, 1), (np.float32, 64), (np.float32, 129), (np.float64, 65),
+                                  (np.float32, 2), (np.float32, 64), (np.float32, 129), (np.float64, 65),
                                   (np.float64, 128)])
 def test_identity_extract_matches_gather(dt, n):
     m = 300
