@@ -904,10 +904,14 @@ def input_sha256(sample, n):
     return hashlib.sha256(np.ascontiguousarray(sample[:, :(n + 3) // 4]).tobytes()).hexdigest()
 
 
+PMC_PROFILE = "r04e"  # this round's PMC passes (tools/profile_r04.sh -> profiles/<PMC_PROFILE>/traffic.json)
+
+
 def pmc_traffic(kernel, leg, n_iid, block):
-    """Per-launch HBM bytes of ``kernel`` from the committed PMC summary, when its profile was
-    taken at this configuration (tools/profile.sh + tools/traffic_summary.py); else None."""
-    path = os.path.join(ROOT, "profiles", "traffic.json")
+    """Per-launch HBM bytes of ``kernel`` from this round's committed PMC summary
+    (profiles/PMC_PROFILE/traffic.json), when that profile was taken at this configuration
+    ([n_iid, block] of the leg); else None."""
+    path = os.path.join(ROOT, "profiles", PMC_PROFILE, "traffic.json")
     try:
         d = json.load(open(path))
         e = d[kernel][leg]
@@ -1152,7 +1156,9 @@ def leg_file(N, args):
             "seconds_two_calls": t_two, "snps_per_s_two_calls": m / t_two,
             "standardize_ms": std_ms[0], "standardize_ms_round3_kernel": std_ms[1],
             "roofline": {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
-                         "traffic": None, "per_call_bytes": 2 * vals_gb * 1e9,
+                         "traffic": pmc_traffic("k_std_cols_f<float>", "std", n, m),
+                         "traffic_source": "profiles/%s/traffic.json (tools/exp_std_dense.py, same shape)" % PMC_PROFILE,
+                         "per_call_bytes": 2 * vals_gb * 1e9,
                          "kernel": "k_std_cols_f<float,1024,16,false>: one workgroup per column, the column held "
                                    "in registers between the stats and the table apply (read once, written once = "
                                    "2 x 4 B per value), plus the flag memset + 4-B readback of the call"},

@@ -1923,23 +1923,25 @@ __global__ __launch_bounds__(kBlock) void k_grm_extract_rows(const T* __restrict
 // mirror (J, I) through the LDS transpose -- so the tiles cross HBM once (half the reads of
 // k_grm_extract_rows, which loads every upper block for both output positions).  A diagonal block
 // mirrors its own upper half.  Blocks are visited in triangular order, the grid strides over them.
-template <typename T>
+// BS = 128 for f32 (a block is exactly one 64 KB tile, 512-B row segments both ways), 64 for f64
+// (the same 512-B rows in half the LDS).
+template <typename T, int BS>
 __global__ __launch_bounds__(kBlock) void k_grm_extract_sym(const T* __restrict__ tiles, uint64_t n, double scale,
                                                             T* __restrict__ out) {
     constexpr int V = 16 / sizeof(T);  // elements per 16-B vector
-    constexpr int TPR = 64 / V;        // threads per 64-element row
+    constexpr int TPR = BS / V;        // threads per BS-element row
     constexpr int RPP = kBlock / TPR;  // rows per pass
     typedef T vec_t __attribute__((ext_vector_type(V)));
-    __shared__ T S[64][64 + 1];
+    __shared__ T S[BS][BS + 1];
     const int t = threadIdx.x, x = t % TPR;
-    const uint64_t nb = (n + 63) / 64, total = nb * (nb + 1) / 2;
+    const uint64_t nb = (n + BS - 1) / BS, total = nb * (nb + 1) / 2;
     for (uint64_t L = blockIdx.x; L < total; L += gridDim.x) {
         uint64_t J = (uint64_t)((sqrt(8.0 * (double)L + 1.0) - 1.0) * 0.5);
         while ((J + 1) * (J + 2) / 2 <= L) J++;
         while (J * (J + 1) / 2 > L) J--;
         const uint64_t I = L - J * (J + 1) / 2;
-        const uint64_t R0 = I * 64, C0 = J * 64;
-        for (int y = t / TPR; y < 64; y += RPP) {
+        const uint64_t R0 = I * BS, C0 = J * BS;
+        for (int y = t / TPR; y < BS; y += RPP) {
             const uint64_t i = R0 + y, j0 = C0 + (uint64_t)x * V;
             T v[V];
             if (I != J && i < n && j0 + V <= n) {
@@ -1962,7 +1964,7 @@ __global__ __launch_bounds__(kBlock) void k_grm_extract_sym(const T* __restrict_
         __syncthreads();
         for (int pass = 0; pass < (I == J ? 1 : 2); pass++) {
             const uint64_t rb = pass ? C0 : R0, cb = pass ? R0 : C0;
-            for (int y = t / TPR; y < 64; y += RPP) {
+            for (int y = t / TPR; y < BS; y += RPP) {
                 const uint64_t r = rb + y, c0 = cb + (uint64_t)x * V;
                 if (r >= n || c0 >= n) continue;
                 vec_t w;
@@ -2791,12 +2793,12 @@ void launch_grm_extract_rows(const void* tiles, uint64_t n, int dtype, uint64_t 
                              void* out, hipStream_t st) {
     if (nr == 0 || n == 0) return;
     if (r0 == 0 && nr == n && g_variant_extract == 0) {  // the whole K: each upper block read once
-        const uint64_t nb = (n + 63) / 64;
+        const uint64_t bs = dtype == SNPMI_DT_F32 ? 128 : 64, nb = (n + bs - 1) / bs;
         const unsigned g = grid_for(nb * (nb + 1) / 2, 1, 256 * 16);
         if (dtype == SNPMI_DT_F32)
-            k_grm_extract_sym<float><<<g, kBlock, 0, st>>>((const float*)tiles, n, scale, (float*)out);
+            k_grm_extract_sym<float, 128><<<g, kBlock, 0, st>>>((const float*)tiles, n, scale, (float*)out);
         else
-            k_grm_extract_sym<double><<<g, kBlock, 0, st>>>((const double*)tiles, n, scale, (double*)out);
+            k_grm_extract_sym<double, 64><<<g, kBlock, 0, st>>>((const double*)tiles, n, scale, (double*)out);
         SNPMI_LAUNCH_CHECK();
         return;
     }

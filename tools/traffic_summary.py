@@ -18,7 +18,8 @@ KERNELS = {"k_decode_std_lds_f32": "k_decode_std_lds_f32", "k_decode_f<float, 4>
            "k_syrk256<1, true>": "f32w::k_syrk256<local>", "k_syrk256d<false": "f32w::k_syrk256d",
            "k_syrk256d<true": "f32w::k_syrk256d<local>", "k_snp_stats<float>": "k_snp_stats<float>",
            "k_syrk_bf3<false": "f32w::k_syrk_bf3", "k_syrk_bf3<true": "f32w::k_syrk_bf3<local>",
-           "k_syrk_h2<false": "f32w::k_syrk_h2", "k_syrk_h2<true": "f32w::k_syrk_h2<local>"}
+           "k_syrk_h2<false": "f32w::k_syrk_h2", "k_syrk_h2<true": "f32w::k_syrk_h2<local>",
+           "k_std_cols_f<float": "k_std_cols_f<float>", "k_diag_sq": "k_diag_sq"}
 
 
 def short(name):
@@ -37,9 +38,11 @@ def load(path, counter):
     return by
 
 
-def main(prof, out, dec_cfg=(500000, 2048), grm_cfg=(50000, 10000)):
+def main(prof, out, dec_cfg=(500000, 2048), grm_cfg=(50000, 10000), std_cfg=(50000, 100000)):
     res = {}
-    for leg in ("dec", "grm"):
+    for leg in ("dec", "grm", "std"):
+        if not os.path.isdir(os.path.join(prof, leg + "_FETCH_SIZE")):
+            continue
         f = load(os.path.join(prof, leg + "_FETCH_SIZE", "run_counter_collection.csv"), "FETCH_SIZE")
         w = load(os.path.join(prof, leg + "_WRITE_SIZE", "run_counter_collection.csv"), "WRITE_SIZE")
         for k in f:
@@ -54,7 +57,7 @@ def main(prof, out, dec_cfg=(500000, 2048), grm_cfg=(50000, 10000)):
             res.setdefault(k, {})[leg] = {"read_bytes": read_b, "write_bytes": write_b,
                                           "traffic_bytes": read_b + write_b, "launches": len(fv),
                                           "read_scale": scale}
-    res["_config"] = {"dec": list(dec_cfg), "grm": list(grm_cfg)}  # the profiling script's settings
+    res["_config"] = {"dec": list(dec_cfg), "grm": list(grm_cfg), "std": list(std_cfg)}  # the script's settings
     res["_source"] = ("rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes (tools/profile.sh); "
                       "read = 2*FETCH_SIZE (gfx950 correction), per full launch")
     json.dump(res, open(out, "w"), indent=1)
@@ -62,5 +65,5 @@ def main(prof, out, dec_cfg=(500000, 2048), grm_cfg=(50000, 10000)):
 
 
 if __name__ == "__main__":
-    cfg = [tuple(int(x) for x in a.split(",")) for a in sys.argv[3:5]]
+    cfg = [tuple(int(x) for x in a.split(",")) for a in sys.argv[3:6]]
     main(sys.argv[1], sys.argv[2], *cfg)
