@@ -1925,12 +1925,12 @@ __global__ __launch_bounds__(kBlock) void k_grm_extract_rows(const T* __restrict
 // mirrors its own upper half.  Blocks are visited in triangular order, the grid strides over them.
 // BS = 128 for f32 (a block is exactly one 64 KB tile, 512-B row segments both ways), 64 for f64
 // (the same 512-B rows in half the LDS).
-template <typename T, int BS>
-__global__ __launch_bounds__(kBlock) void k_grm_extract_sym(const T* __restrict__ tiles, uint64_t n, double scale,
-                                                            T* __restrict__ out) {
+template <typename T, int BS, int NT = kBlock>
+__global__ __launch_bounds__(NT) void k_grm_extract_sym(const T* __restrict__ tiles, uint64_t n, double scale,
+                                                        T* __restrict__ out) {
     constexpr int V = 16 / sizeof(T);  // elements per 16-B vector
     constexpr int TPR = BS / V;        // threads per BS-element row
-    constexpr int RPP = kBlock / TPR;  // rows per pass
+    constexpr int RPP = NT / TPR;      // rows per pass
     typedef T vec_t __attribute__((ext_vector_type(V)));
     __shared__ T S[BS][BS + 1];
     const int t = threadIdx.x, x = t % TPR;
@@ -2795,10 +2795,28 @@ void launch_grm_extract_rows(const void* tiles, uint64_t n, int dtype, uint64_t 
     if (r0 == 0 && nr == n && g_variant_extract == 0) {  // the whole K: each upper block read once
         const uint64_t bs = dtype == SNPMI_DT_F32 ? 128 : 64, nb = (n + bs - 1) / bs;
         const unsigned g = grid_for(nb * (nb + 1) / 2, 1, 256 * 16);
+        // f32: 128x128 blocks (one 64 KB tile) on 512 threads; f64: 64x64 on 256 (the other
+        // shapes of hook "extract" 2-4 were within 2-6% either way, profiles/r04f/extract_ab.jsonl)
         if (dtype == SNPMI_DT_F32)
-            k_grm_extract_sym<float, 128><<<g, kBlock, 0, st>>>((const float*)tiles, n, scale, (float*)out);
+            k_grm_extract_sym<float, 128, 512><<<g, 512, 0, st>>>((const float*)tiles, n, scale, (float*)out);
         else
             k_grm_extract_sym<double, 64><<<g, kBlock, 0, st>>>((const double*)tiles, n, scale, (double*)out);
+        SNPMI_LAUNCH_CHECK();
+        return;
+    }
+    if (r0 == 0 && nr == n && g_variant_extract >= 2) {  // A/B shapes of the read-once kernel
+        const int v = g_variant_extract;
+        const uint64_t bs = v == 2 || v == 4 ? 128 : 64, nb = (n + bs - 1) / bs;
+        const unsigned g = grid_for(nb * (nb + 1) / 2, 1, 256 * 16);
+        if (dtype == SNPMI_DT_F32) {
+            if (v == 2) k_grm_extract_sym<float, 128, 512><<<g, 512, 0, st>>>((const float*)tiles, n, scale, (float*)out);
+            else if (v == 3) k_grm_extract_sym<float, 64><<<g, kBlock, 0, st>>>((const float*)tiles, n, scale, (float*)out);
+            else k_grm_extract_sym<float, 128, 1024><<<g, 1024, 0, st>>>((const float*)tiles, n, scale, (float*)out);
+        } else {
+            if (v == 2) k_grm_extract_sym<double, 128, 512><<<g, 512, 0, st>>>((const double*)tiles, n, scale, (double*)out);
+            else if (v == 3) k_grm_extract_sym<double, 64, 512><<<g, 512, 0, st>>>((const double*)tiles, n, scale, (double*)out);
+            else k_grm_extract_sym<double, 128, 1024><<<g, 1024, 0, st>>>((const double*)tiles, n, scale, (double*)out);
+        }
         SNPMI_LAUNCH_CHECK();
         return;
     }
