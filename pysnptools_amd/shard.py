@@ -259,6 +259,26 @@ def grm_pieces(reader, standardizer, rank=None, world=None, dtype="float32", dia
     return K, _trained_from(standardizer, kind, a, b, sid, stats), factor
 
 
+def part_coords(n, part, parts):
+    """[nloc, 2] int64 (row0, col0) of the 256x256 upper-triangle blocks part ``part`` of ``parts``
+    owns -- ``snpmi_grm_part_coords`` for every local block at once (block L = J(J+1)/2 + I is
+    owned by part L mod parts; 238,755 blocks per part at 500k iids, one ctypes call each is slow).
+    The first and last entries are checked against the library."""
+    from pysnptools_amd import _native as N
+
+    nloc = N.lib().snpmi_grm_part_blocks(n, part, parts)
+    L = np.arange(nloc, dtype=np.int64) * parts + part
+    J = ((np.sqrt(8.0 * L.astype(np.float64) + 1.0) - 1.0) * 0.5).astype(np.int64)
+    J += (J + 1) * (J + 2) // 2 <= L  # float rounding at the triangle boundaries
+    J -= J * (J + 1) // 2 > L
+    coords = np.stack([(L - J * (J + 1) // 2) * 256, J * 256], axis=1)
+    r0, c0 = ctypes.c_uint64(), ctypes.c_uint64()
+    for k in {0, nloc - 1} if nloc else ():
+        N.call("snpmi_grm_part_coords", n, part, parts, k, ctypes.byref(r0), ctypes.byref(c0))
+        assert (r0.value, c0.value) == tuple(coords[k]), "part_coords disagrees with the library"
+    return coords
+
+
 class _DevBuf(object):
     def __init__(self, N, nbytes, host=False):
         self.N, self.host, self.p = N, host, ctypes.c_void_p()
@@ -292,9 +312,9 @@ class PartitionedGrm(object):
        MFMA SYRK adds the block into this part's K blocks (``snpmi_dev_syrk_packed_part``).
 
     Two slots: block k+1's fill (host threads), upload (copy stream) and all-gather (aux stream) run
-    under block k's kernels; the compute stream waits on events only.  At world 1 the all-gather is a no-op and the one rank
-    fills whole blocks -- a single-GPU run of any part (``parts`` may exceed ``world``: bench.py
-    computes part 0 of the 8-GPU plan on one GPU)."""
+    under block k's kernels; the compute stream waits on events only.  At world 1 the all-gather is
+    a no-op and the one rank fills whole blocks -- a single-GPU run of any part (``parts`` may exceed
+    ``world``: bench.py computes part 0 of the 8-GPU plan on one GPU)."""
 
     def __init__(self, n_src, m, kind, a=0.0, b=0.0, use_stats=False, stats=None, iid_index=None, count_a1=False,
                  dist=None, part=None, parts=None, block=8192, out=None, timing=False):
@@ -450,13 +470,7 @@ class PartitionedGrm(object):
 
     def coords(self):
         """[nloc, 2] int64: (row0, col0) of each local block."""
-        N = self.N
-        coords = np.empty((self.nloc, 2), dtype=np.int64)
-        r0, c0 = ctypes.c_uint64(), ctypes.c_uint64()
-        for k in range(self.nloc):
-            N.call("snpmi_grm_part_coords", self.n, self.part, self.parts, k, ctypes.byref(r0), ctypes.byref(c0))
-            coords[k] = (r0.value, c0.value)
-        return coords
+        return part_coords(self.n, self.part, self.parts)
 
     def finish(self):
         """The part's blocks (``out``: copied from HBM when it is host memory)."""
@@ -556,12 +570,7 @@ def grm_partitioned(reader, standardizer, rank=None, world=None, out=None, num_t
     N.call("snpmi_grm_part_bed_f32", base.filename.encode(), base.iid_count, base.sid_count,
            int(bool(base.count_A1)), N.ptr(ri), n, N.ptr(ci), len(sid), kind, a, b, int(use_stats), N.ptr(stats),
            rank, world, N.ptr(out), threads)
-    coords = np.empty((nloc, 2), dtype=np.int64)
-    r0, c0 = ctypes.c_uint64(), ctypes.c_uint64()
-    for k in range(nloc):
-        N.call("snpmi_grm_part_coords", n, rank, world, k, ctypes.byref(r0), ctypes.byref(c0))
-        coords[k] = (r0.value, c0.value)
-    return out, coords, _trained_from(standardizer, kind, a, b, sid, stats)
+    return out, part_coords(n, rank, world), _trained_from(standardizer, kind, a, b, sid, stats)
 
 
 def assemble_partitioned(parts, n):

@@ -204,3 +204,24 @@ def test_bed_gather_packed_host_only():
                N.ptr(out), 1)
     with pytest.raises(ValueError):
         N.call("snpmi_bed_gather_packed", path.encode(), n, m + 1, None, 1, pitch, N.ptr(out), 1)
+
+
+@pytest.mark.parametrize("n,parts", [(1, 1), (300, 1), (300, 3), (5000, 8), (70001, 7)])
+def test_part_coords_match_the_library(n, parts):
+    """shard.part_coords (vectorised) == snpmi_grm_part_coords for every local block of every part,
+    and the parts tile the upper triangle of 256-blocks exactly once (host code, no GPU)."""
+    import ctypes
+
+    from pysnptools_amd import _native as N
+    from pysnptools_amd.shard import part_coords
+
+    nb = (n + 255) // 256
+    seen = set()
+    r0, c0 = ctypes.c_uint64(), ctypes.c_uint64()
+    for part in range(parts):
+        co = part_coords(n, part, parts)
+        for k in range(len(co)):
+            N.call("snpmi_grm_part_coords", n, part, parts, k, ctypes.byref(r0), ctypes.byref(c0))
+            assert (r0.value, c0.value) == tuple(co[k])
+            seen.add(tuple(co[k]))
+    assert seen == {(256 * i, 256 * j) for j in range(nb) for i in range(j + 1)}

@@ -57,3 +57,23 @@ def test_bench_torchrun_world3_on_one_gpu():
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "3", "--master-addr",
            "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"), "--gpus", "3"] + SMALL
     _check(subprocess.run(cmd, capture_output=True, text=True, timeout=290, env=env), 3)
+
+
+def test_bench_spawned_world8_on_one_gpu():
+    """The driver's largest scaling point (N = 8) rehearsed on one GPU: 8 ranks of bench.py's own
+    spawner in the host group -- every rank owns one of the cfg5 plan's 8 parts and 1/8 of each
+    block's all-gather, the cfg4 reduce combines 8 partial tile sets."""
+    env = dict(os.environ, SNPMI_DIST_HOST="1")
+    small = [a for a in SMALL]
+    small[small.index("--n-sid") + 1] = "8000"
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "8"] + small
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=290, env=env)
+    assert out.returncode == 0, out.stderr[-4000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, out.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 8 and d["config"]["n_sid_per_gpu"] == 1000
+    for k in ("grm", "grm_f64"):
+        assert d[k]["parity"]["pass"], d[k]["parity"]
+    g5 = d["grm5"]
+    assert g5["parts"] == 8 and g5["parity"]["pass"] and g5["parity"]["gathered_block_bit_exact"], g5["parity"]
