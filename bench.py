@@ -101,7 +101,7 @@ def parse(argv=None):
     p.add_argument("--grm5", choices=["on", "off"], default="on", help="cfg5 partitioned-K GRM leg")
     p.add_argument("--grm5-iid", type=int, default=500_000)
     p.add_argument("--grm5-sid", type=int, default=1_000_000, help="cfg5: SNPs of the whole job (all timed)")
-    p.add_argument("--grm5-block", type=int, default=8192, help="cfg5: SNPs per all-gathered block")
+    p.add_argument("--grm5-block", type=int, default=32768, help="cfg5: SNPs per all-gathered block (the first: 1/4)")
     p.add_argument("--grm5-miss", type=float, default=0.218, help="cfg5: missing rate (SnpGen's 21.8%%)")
     p.add_argument("--grm5-parity-max-sid", type=int, default=65536,
                    help="cfg5 at N > 1: the oracle check runs only up to this many SNPs (N = 1: always)")
@@ -799,7 +799,7 @@ def leg_grm5(N, args, dist):
         dist.barrier()
         t0 = time.perf_counter()
         block_ms = g.run(fill, progress=lambda k, nb: progress("grm5 block %d/%d" % (k + 1, nb))
-                         if (k + 1) % 16 == 0 else None)
+                         if (k + 1) % 4 == 0 else None)
         dist.barrier()
         wall = dist.max(time.perf_counter() - t0)
         res = {"wall": wall, "block_ms": block_ms, "n_local_blocks": g.nloc, "m": m, "ms": g.ms, "P": P,
@@ -827,7 +827,8 @@ def grm5_gather_check(N, args, dist, P, fill):
     from pysnptools_amd.shard import PartitionedGrm
 
     n, m = args.grm5_iid, min(args.grm5_sid, args.grm5_block)
-    g = PartitionedGrm(n, m, N.STD_UNIT, dist=dist, part=dist.rank, parts=P, block=args.grm5_block, out="hbm")
+    g = PartitionedGrm(n, m, N.STD_UNIT, dist=dist, part=dist.rank, parts=P, block=args.grm5_block, out="hbm",
+                       first_block=m)  # one block: dev[0] holds all of it
     try:
         g.run(fill)
         if dist.rank != 0:
@@ -1261,7 +1262,7 @@ def main(argv=None):
         gather = (" + RCCL all-gather" if dist.rccl else
                   (" + host all-gather (rehearsal group)" if dist.world > 1 else ""))
         grm5 = {"workload": "cfg5: %d iid x %d SNP, Unit, f32 (fp16x2 MFMA), %.1f%% missing; K as 256x256 blocks in "
-                            "%d parts (the 8-GPU plan), this process = part %d; all %d blocks of %d SNPs timed: each "
+                            "%d parts (the 8-GPU plan), this process = part %d; all %d blocks (of %d SNPs, the first a quarter) timed: each "
                             "rank's 1/%d share generated on %d host threads into pinned memory, uploaded on the copy "
                             "stream under the previous block's SYRK%s, stats + SYRK into the part's blocks in HBM "
                             "(shard.PartitionedGrm); no reduction"

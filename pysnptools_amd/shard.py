@@ -298,7 +298,11 @@ class PartitionedGrm(object):
     process per GPU.  K is partitioned into the 256x256 blocks of its upper triangle, block L owned
     by part ``L mod parts`` (``snpmi_grm_part_coords``); this process accumulates part ``part``.
 
-    Per SNP block of ``block`` SNPs (the reference's block loop, snpreader.py:643-655):
+    Per SNP block of ``block`` SNPs (the reference's block loop, snpreader.py:643-655; the first
+    block is ``first_block`` = block/4 SNPs, so less host work precedes the first kernel; 32768-SNP
+    blocks amortise the read-modify-write of the part's K blocks that ends every SYRK launch, which
+    at 8192 cost ~5% of the launch -- the kernel holds one workgroup per CU, so that epilogue does
+    not overlap its MFMAs):
 
     1. ``fill(host_ptr, s0, count)`` writes this rank's share -- packed columns [s0, s0+count) of the
        stream, all ``n_src`` iids, ``pitch_src`` bytes each -- into a pinned host slot (a .bed gather,
@@ -317,7 +321,7 @@ class PartitionedGrm(object):
     ``world``: bench.py computes part 0 of the 8-GPU plan on one GPU)."""
 
     def __init__(self, n_src, m, kind, a=0.0, b=0.0, use_stats=False, stats=None, iid_index=None, count_a1=False,
-                 dist=None, part=None, parts=None, block=8192, out=None, timing=False):
+                 dist=None, part=None, parts=None, block=32768, out=None, timing=False, first_block=None):
         from pysnptools_amd import _native as N
 
         self.N = N
@@ -335,6 +339,8 @@ class PartitionedGrm(object):
         self.n = self.n_src if self.iid is None else len(self.iid)
         self.kind, self.a, self.b, self.use_stats, self.count_a1 = int(kind), float(a), float(b), bool(use_stats), count_a1
         self.block = max(1, int(block))
+        # a smaller first block: its fill and upload are the only exposed host work of the stream
+        self.first_block = max(1, min(self.block, int(first_block) if first_block else self.block // 4))
         self.ms = (self.block + self.world - 1) // self.world
         self.pitch_src = N.lib().snpmi_packed_pitch(self.n_src)
         self.pitch = N.lib().snpmi_packed_pitch(self.n)
@@ -397,7 +403,8 @@ class PartitionedGrm(object):
         (ms, HIP events on the compute stream) when ``timing`` was set, else None.  ``progress(k,
         nblk)`` (optional) is called on the host after block k is enqueued."""
         N = self.N
-        nblk = (self.m + self.block - 1) // self.block
+        spans = self.spans()
+        nblk = len(spans)
         up = [self._event(), self._event()]  # copy stream: share of the slot uploaded (host slot free)
         done = [self._event(), self._event()]  # compute stream: the slot's kernels are done
         gathered = [self._event(), self._event()]  # aux stream: the slot's block is all-gathered
@@ -406,8 +413,7 @@ class PartitionedGrm(object):
         if self.m == 0 or self.n == 0:
             N.call("snpmi_dev_memset", self.blocks, 0, self.nloc * 256 * 256 * 4)
         for k in range(nblk if self.n else 0):
-            s0 = k * self.block
-            cnt = min(self.block, self.m - s0)
+            s0, cnt = spans[k]
             ms = (cnt + self.world - 1) // self.world
             mine0 = min(cnt, self.rank * ms)
             mine = max(0, min(ms, cnt - mine0))
@@ -460,6 +466,15 @@ class PartitionedGrm(object):
             N.call("snpmi_event_elapsed_ms", a, b, ctypes.byref(out))
             res.append(float(out.value))
         return res
+
+    def spans(self):
+        """[(s0, count)] of the SNP blocks: ``first_block`` SNPs, then blocks of ``block``."""
+        out, s0 = [], 0
+        while s0 < self.m:
+            cnt = min(self.first_block if s0 == 0 else self.block, self.m - s0)
+            out.append((s0, cnt))
+            s0 += cnt
+        return out
 
     def stats(self):
         """[m, 2] float32 per-SNP (mean, std) of the stream (or the given stats)."""
@@ -514,7 +529,7 @@ def _partitioned_bed(base, rows, cols, kind, a, b, use_stats, stats, dist, part,
 
 
 def grm_partitioned(reader, standardizer, rank=None, world=None, out=None, num_threads=None, dist=None,
-                    block_size=8192):
+                    block_size=32768):
     """cfg5 GRM of a Bed (or a subset of one) too large to replicate: K is
     partitioned over the ranks as the 256x256 blocks of its upper triangle
     (``snpmi_grm_part_coords``) and this rank keeps only its own blocks.

@@ -198,7 +198,7 @@ class _OneRank:
 
 def test_config5_streamed_500k_iids_over_100k_snps():
     """configs[4]'s per-rank job beyond one block: part 0 of the 8-part plan at 500,000 iids over
-    106,496 SnpGen-shaped SNPs (21.8% missing) in 13 streamed 8192-SNP blocks through
+    106,496 SnpGen-shaped SNPs (21.8% missing) in 4 streamed blocks (8192, then 3 x 32768 SNPs) through
     shard.PartitionedGrm (pinned host slots generated on host threads, uploads under the previous
     block's SYRK, f32 K blocks accumulated in HBM) -- bench.py's grm5 leg at a tenth of its SNPs.
     Sample blocks (first diagonal, first off-diagonal, the last one with the padded iids) vs the
@@ -212,9 +212,9 @@ def test_config5_streamed_500k_iids_over_100k_snps():
     import bench
 
     args = bench.parse(["--grm5-iid", "500000", "--grm5-sid", "106496", "--steps", "1", "--warmup", "0"])
-    assert args.grm5_miss == 0.218 and args.grm5_block == 8192
+    assert args.grm5_miss == 0.218 and args.grm5_block == 32768
     r = bench.leg_grm5(N, args, _OneRank())
-    assert r["blocks"] == 13 and len(r["block_ms"]) == 13
+    assert r["blocks"] == 4 and len(r["block_ms"]) == 4
     picks, stats = r["parity_sample"]
     assert set(picks) == {"diag", "off", "last"}
     p = bench.grm5_parity(args, picks, stats, min(16, os.cpu_count() or 1))
