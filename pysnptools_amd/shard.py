@@ -293,6 +293,19 @@ class _DevBuf(object):
             self.p = None
 
 
+def block_spans(m, block, first_block=None):
+    """[(s0, count)] covering SNPs [0, m): ``first_block`` SNPs (default block/4, at least 1), then
+    blocks of ``block`` -- PartitionedGrm's stream plan."""
+    block = max(1, int(block))
+    first = max(1, min(block, int(first_block) if first_block else block // 4))
+    out, s0 = [], 0
+    while s0 < m:
+        cnt = min(first if s0 == 0 else block, m - s0)
+        out.append((s0, cnt))
+        s0 += cnt
+    return out
+
+
 class PartitionedGrm(object):
     """cfg5: the GRM of a SNP stream whose K is too large to replicate, as one
     process per GPU.  K is partitioned into the 256x256 blocks of its upper triangle, block L owned
@@ -468,13 +481,8 @@ class PartitionedGrm(object):
         return res
 
     def spans(self):
-        """[(s0, count)] of the SNP blocks: ``first_block`` SNPs, then blocks of ``block``."""
-        out, s0 = [], 0
-        while s0 < self.m:
-            cnt = min(self.first_block if s0 == 0 else self.block, self.m - s0)
-            out.append((s0, cnt))
-            s0 += cnt
-        return out
+        """[(s0, count)] of the SNP blocks (``block_spans``)."""
+        return block_spans(self.m, self.block, self.first_block)
 
     def stats(self):
         """[m, 2] float32 per-SNP (mean, std) of the stream (or the given stats)."""

@@ -225,3 +225,21 @@ def test_part_coords_match_the_library(n, parts):
             assert (r0.value, c0.value) == tuple(co[k])
             seen.add(tuple(co[k]))
     assert seen == {(256 * i, 256 * j) for j in range(nb) for i in range(j + 1)}
+
+
+@pytest.mark.parametrize("m,block,first", [(0, 32768, None), (1, 32768, None), (106496, 32768, None),
+                                           (1_000_000, 32768, None), (1000, 97, None), (50, 97, 50), (7, 1, None)])
+def test_block_spans_cover_the_stream(m, block, first):
+    """shard.block_spans (cfg5's stream plan): a quarter-size first block, then full blocks, covering
+    [0, m) once in order."""
+    from pysnptools_amd.shard import block_spans
+
+    spans = block_spans(m, block, first)
+    assert sum(c for _, c in spans) == m
+    assert all(s0 == sum(c for _, c in spans[:k]) for k, (s0, _) in enumerate(spans))
+    if spans:
+        assert spans[0][1] == min(m, first or max(1, block // 4))
+        assert all(0 < c <= block for _, c in spans)
+        assert all(c == block for _, c in spans[1:-1])
+    if (m, block) == (1_000_000, 32768):
+        assert len(spans) == 32
