@@ -1924,47 +1924,67 @@ __global__ __launch_bounds__(kBlock) void k_grm_extract_rows(const T* __restrict
 // k_grm_extract_rows, which loads every upper block for both output positions).  A diagonal block
 // mirrors its own upper half.  Blocks are visited in triangular order, the grid strides over them.
 // BS = 128 for f32 (a block is exactly one 64 KB tile, 512-B row segments both ways), 64 for f64
-// (the same 512-B rows in half the LDS).
-template <typename T, int BS, int NT = kBlock>
+// (the same 512-B rows in half the LDS).  PIPE: the next block's loads are issued into registers
+// before the current block's stores, so a workgroup keeps reads in flight while it writes.
+template <typename T, int BS, int NT = kBlock, bool PIPE = false>
 __global__ __launch_bounds__(NT) void k_grm_extract_sym(const T* __restrict__ tiles, uint64_t n, double scale,
                                                         T* __restrict__ out) {
     constexpr int V = 16 / sizeof(T);  // elements per 16-B vector
     constexpr int TPR = BS / V;        // threads per BS-element row
     constexpr int RPP = NT / TPR;      // rows per pass
+    constexpr int NR = BS / RPP;       // rows per thread
+    static_assert(BS % RPP == 0, "block rows must split evenly over the passes");
     typedef T vec_t __attribute__((ext_vector_type(V)));
     __shared__ T S[BS][BS + 1];
-    const int t = threadIdx.x, x = t % TPR;
+    const int t = threadIdx.x, x = t % TPR, y0 = t / TPR;
     const uint64_t nb = (n + BS - 1) / BS, total = nb * (nb + 1) / 2;
-    for (uint64_t L = blockIdx.x; L < total; L += gridDim.x) {
-        uint64_t J = (uint64_t)((sqrt(8.0 * (double)L + 1.0) - 1.0) * 0.5);
+    auto coords = [&](uint64_t L, uint64_t& I, uint64_t& J) {
+        J = (uint64_t)((sqrt(8.0 * (double)L + 1.0) - 1.0) * 0.5);
         while ((J + 1) * (J + 2) / 2 <= L) J++;
         while (J * (J + 1) / 2 > L) J--;
-        const uint64_t I = L - J * (J + 1) / 2;
+        I = L - J * (J + 1) / 2;
+    };
+    vec_t v[NR];
+    auto fetch = [&](uint64_t I, uint64_t J) {
         const uint64_t R0 = I * BS, C0 = J * BS;
-        for (int y = t / TPR; y < BS; y += RPP) {
-            const uint64_t i = R0 + y, j0 = C0 + (uint64_t)x * V;
-            T v[V];
-            if (I != J && i < n && j0 + V <= n) {
-                const vec_t q = *reinterpret_cast<const vec_t*>(
-                    tiles + tile_index(i / kTile, j0 / kTile) * (kTile * kTile) + (i % kTile) * kTile + (j0 % kTile));
 #pragma unroll
-                for (int e = 0; e < V; e++) v[e] = q[e];
+        for (int r = 0; r < NR; r++) {
+            const uint64_t i = R0 + y0 + r * RPP, j0 = C0 + (uint64_t)x * V;
+            if (I != J && i < n && j0 + V <= n) {
+                v[r] = *reinterpret_cast<const vec_t*>(tiles + tile_index(i / kTile, j0 / kTile) * (kTile * kTile) +
+                                                       (i % kTile) * kTile + (j0 % kTile));
             } else {
 #pragma unroll
                 for (int e = 0; e < V; e++) {
                     const uint64_t j = j0 + e, ii = i < j ? i : j, jj = i < j ? j : i;
-                    v[e] = (i < n && j < n) ? tiles[tile_index(ii / kTile, jj / kTile) * (kTile * kTile) +
-                                                    (ii % kTile) * kTile + (jj % kTile)]
-                                            : (T)0;
+                    v[r][e] = (i < n && j < n) ? tiles[tile_index(ii / kTile, jj / kTile) * (kTile * kTile) +
+                                                       (ii % kTile) * kTile + (jj % kTile)]
+                                               : (T)0;
                 }
             }
-#pragma unroll
-            for (int e = 0; e < V; e++) S[y][x * V + e] = scale == 1.0 ? v[e] : (T)((double)v[e] * scale);
         }
+    };
+    uint64_t L = blockIdx.x, I = 0, J = 0;
+    if (L < total) {
+        coords(L, I, J);
+        fetch(I, J);
+    }
+    for (; L < total; L += gridDim.x) {
+#pragma unroll
+        for (int r = 0; r < NR; r++)
+#pragma unroll
+            for (int e = 0; e < V; e++) S[y0 + r * RPP][x * V + e] = scale == 1.0 ? v[r][e] : (T)((double)v[r][e] * scale);
         __syncthreads();
-        for (int pass = 0; pass < (I == J ? 1 : 2); pass++) {
+        const uint64_t R0 = I * BS, C0 = J * BS;
+        const bool diag = I == J;
+        const uint64_t Ln = L + gridDim.x;
+        if (PIPE && Ln < total) {
+            coords(Ln, I, J);
+            fetch(I, J);
+        }
+        for (int pass = 0; pass < (diag ? 1 : 2); pass++) {
             const uint64_t rb = pass ? C0 : R0, cb = pass ? R0 : C0;
-            for (int y = t / TPR; y < BS; y += RPP) {
+            for (int y = y0; y < BS; y += RPP) {
                 const uint64_t r = rb + y, c0 = cb + (uint64_t)x * V;
                 if (r >= n || c0 >= n) continue;
                 vec_t w;
@@ -1980,6 +2000,10 @@ __global__ __launch_bounds__(NT) void k_grm_extract_sym(const T* __restrict__ ti
             }
         }
         __syncthreads();
+        if (!PIPE && Ln < total) {
+            coords(Ln, I, J);
+            fetch(I, J);
+        }
     }
 }
 
@@ -2286,8 +2310,10 @@ inline unsigned grid_for(uint64_t work, uint64_t per_block, unsigned cap = 65536
 // ====================================================================== launchers
 int g_variant_decode = 0;  // tuning hook (snpmi_set_kernel_variant); no variants at present
 int g_diag_exact = 1;     // exact f32 GRM diagonal (k_diag_*), hook "diag"
-int g_variant_std = 0;
-int g_variant_extract = 0;  // whole-K extraction: 0 = k_grm_extract_sym, 1 = round 3's k_grm_extract_rows     // dense standardize: 0 = k_std_cols_f / k_std_cols_c16, 1 = round 3's kernels
+int g_variant_std = 0;      // dense standardize: 0 = k_std_cols_f / k_std_cols_c16, 1 = round 3's kernels
+// whole-K extraction: 0 = k_grm_extract_sym, 1 = round 3's k_grm_extract_rows, 2-4 = other block
+// shapes, 5-7 = the pipelined (PIPE) kernel in three shapes
+int g_variant_extract = 0;
 
 #define SNPMI_LAUNCH_CHECK() SNPMI_HIP(hipGetLastError())
 
@@ -2801,6 +2827,23 @@ void launch_grm_extract_rows(const void* tiles, uint64_t n, int dtype, uint64_t 
             k_grm_extract_sym<float, 128, 512><<<g, 512, 0, st>>>((const float*)tiles, n, scale, (float*)out);
         else
             k_grm_extract_sym<double, 64><<<g, kBlock, 0, st>>>((const double*)tiles, n, scale, (double*)out);
+        SNPMI_LAUNCH_CHECK();
+        return;
+    }
+    if (r0 == 0 && nr == n && g_variant_extract >= 5) {  // A/B: the pipelined read-once kernel
+        const int v = g_variant_extract;
+        const bool f32 = dtype == SNPMI_DT_F32;
+        const uint64_t bs = v == 6 || (v == 5 && f32) ? 128 : 64, nb = (n + bs - 1) / bs;
+        const unsigned g = grid_for(nb * (nb + 1) / 2, 1, 256 * 16);
+        if (f32) {
+            if (v == 5) k_grm_extract_sym<float, 128, 512, true><<<g, 512, 0, st>>>((const float*)tiles, n, scale, (float*)out);
+            else if (v == 6) k_grm_extract_sym<float, 128, 1024, true><<<g, 1024, 0, st>>>((const float*)tiles, n, scale, (float*)out);
+            else k_grm_extract_sym<float, 64, kBlock, true><<<g, kBlock, 0, st>>>((const float*)tiles, n, scale, (float*)out);
+        } else {
+            if (v == 5) k_grm_extract_sym<double, 64, kBlock, true><<<g, kBlock, 0, st>>>((const double*)tiles, n, scale, (double*)out);
+            else if (v == 6) k_grm_extract_sym<double, 128, 1024, true><<<g, 1024, 0, st>>>((const double*)tiles, n, scale, (double*)out);
+            else k_grm_extract_sym<double, 64, 512, true><<<g, 512, 0, st>>>((const double*)tiles, n, scale, (double*)out);
+        }
         SNPMI_LAUNCH_CHECK();
         return;
     }

@@ -65,6 +65,41 @@ def test_identity_extract_matches_gather(dt, n):
     assert np.abs(outs[0]).max() > 0
 
 
+@pytest.mark.parametrize("dt,n", [(np.float32, 2), (np.float32, 129), (np.float32, 4157), (np.float64, 65),
+                                  (np.float64, 2050), (np.float64, 3001)])
+def test_every_extract_shape_matches_gather(dt, n):
+    """Hook "extract" 1-7 (round 3's row kernel, the read-once kernel's other block shapes, and the
+    pipelined kernel in three shapes) give the shipped kernel's K bit for bit, with a scale."""
+    m = 200
+    code = N.DT_F32 if dt == np.float32 else N.DT_F64
+    pitch = N.lib().snpmi_packed_pitch(n)
+    packed = Dev(pitch * m)
+    x, cdf = O.maf_table(n)
+    N.call("snpmi_dev_synth_bed", packed.p, pitch, n, 0, m, 13, 0.05, N.ptr(x), N.ptr(cdf), len(x))
+    es = np.dtype(dt).itemsize
+    lut, st = Dev(m * 4 * es), Dev(m * 2 * es)
+    N.call("snpmi_dev_snp_stats", packed.p, pitch, n, m, 0, N.STD_UNIT, 0.0, 0.0, 0, code, st.p, lut.p)
+    tiles = Dev(N.lib().snpmi_grm_tile_bytes(n, code))
+    N.call("snpmi_dev_syrk_packed", packed.p, pitch, n, m, lut.p, code, tiles.p, 0)
+    out = Dev(n * n * es)
+
+    def whole(v):
+        N.call("snpmi_set_kernel_variant", b"extract", v)
+        try:
+            N.call("snpmi_dev_memset", out.p, 0xff, n * n * es)
+            N.call("snpmi_dev_grm_extract", tiles.p, n, code, None, n, None, n, 1, 0.75, out.p)
+        finally:
+            N.call("snpmi_set_kernel_variant", b"extract", 0)
+        K = np.empty((n, n), dtype=dt)
+        N.call("snpmi_memcpy_d2h", N.ptr(K), out.p, K.nbytes)
+        return K
+
+    ref = whole(0)
+    assert np.array_equal(ref, ref.T) and np.isfinite(ref).all()
+    for v in range(1, 8):
+        assert np.array_equal(whole(v), ref), v
+
+
 def _write_bed(path, n, m, seed):
     rng = np.random.default_rng(seed)
     bpc = (n + 3) // 4
