@@ -105,6 +105,9 @@ void Device::release() {
         order_tab[x] = nullptr;
         order_nb[x] = 0;
     }
+    if (part_order_tab) (void)hipFree(part_order_tab);
+    part_order_tab = nullptr;
+    part_order_key[0] = part_order_key[1] = part_order_key[2] = 0;
 }
 
 // pinned staging (two slots so a chunk can be gathered while the previous one uploads)
@@ -999,6 +1002,30 @@ static const uint32_t* dense_order(Device& d, uint64_t nb, bool xcd) {
 const uint32_t* packed_block_order(uint64_t nb) {
     std::lock_guard<std::recursive_mutex> lk(g_call_mutex);
     return dense_order(device(), nb, false);
+}
+
+// the cfg5 part kernel's block order: the supertile table restricted to the blocks of part
+// `rank` of `world` (part_supertile_order), cached per (nb, rank, world) on the device
+const uint32_t* part_block_order(uint64_t nb, int rank, int world) {
+    std::lock_guard<std::recursive_mutex> lk(g_call_mutex);
+    Device& d = device();
+    const uint64_t key[3] = {nb, (uint64_t)rank, (uint64_t)world};
+    if (!d.part_order_tab || d.part_order_key[0] != key[0] || d.part_order_key[1] != key[1] ||
+        d.part_order_key[2] != key[2]) {
+        std::vector<uint32_t> tab;
+        part_supertile_order(nb, rank, world, tab);
+        if (d.part_order_tab) SNPMI_HIP(hipFree(d.part_order_tab));
+        d.part_order_tab = nullptr;
+        d.part_order_key[0] = d.part_order_key[1] = d.part_order_key[2] = 0;
+        if (tab.empty()) return nullptr;
+        if (hipMalloc(&d.part_order_tab, tab.size() * sizeof(uint32_t)) != hipSuccess) {
+            (void)hipGetLastError();
+            throw Error(SNPMI_E_NOMEM, "hipMalloc of the part block order table failed");
+        }
+        SNPMI_HIP(hipMemcpy(d.part_order_tab, tab.data(), tab.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+        for (int i = 0; i < 3; i++) d.part_order_key[i] = key[i];
+    }
+    return d.part_order_tab;
 }
 
 // dense GRM operand on the device: f32 with n >= 4096 and the default variant takes the fp16x2

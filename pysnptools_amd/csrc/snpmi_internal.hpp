@@ -89,6 +89,9 @@ struct Device {
     // (nb, xcd) and kept on this device (guarded by the device's own mutex)
     uint32_t* order_tab[2] = {};
     uint64_t order_nb[2] = {};
+    // the same order restricted to one part of the cfg5 plan, per (nb, rank, world)
+    uint32_t* part_order_tab = nullptr;
+    uint64_t part_order_key[3] = {};
     void* get(Slot s, size_t bytes);
     void release();
 };
@@ -124,6 +127,7 @@ SegCtx seg_ctx();                                     // api.hip: the current de
 // api.hip: device table of supertile_order(nb, false) for the current device (cached per nb): the
 // block order of the packed fp16x2 SYRK
 const uint32_t* packed_block_order(uint64_t nb);
+const uint32_t* part_block_order(uint64_t nb, int rank, int world);
 void launch_snp_stats(const uint8_t* packed, uint64_t pitch, uint64_t n_iid, uint64_t n_sid, int count_a1,
                       int std_kind, double a, double b, int use_stats, int dtype, void* stats, void* lut,
                       hipStream_t st);
@@ -209,6 +213,7 @@ void launch_lut_h2(const float* lut, uint64_t m, uint32_t* lut2, uint32_t* flag,
 // fp16x2 SYRK in supertile block order (order: device table of supertile_order), the f32-MFMA
 // k_syrk256d gated on the range flag
 void supertile_order(uint64_t nb, bool xcd, std::vector<uint32_t>& tab);
+void part_supertile_order(uint64_t nb, int rank, int world, std::vector<uint32_t>& tab);
 uint64_t dense_h2_chunk_snps(uint64_t n);
 uint64_t dense_h2_scratch_bytes(uint64_t n, uint64_t m);
 void launch_syrk_dense_h2(const float* Z, uint64_t ldz, uint64_t n, uint64_t m, uint16_t* img, uint32_t* flag,

@@ -1257,13 +1257,16 @@ __global__ __launch_bounds__(512, 1) void k_syrk_h2(const uint8_t* __restrict__ 
         const uint32_t c = lut2[wg];
         bi = c & 0xffffu;
         bj = c >> 16;
-    } else if (order) {  // ubench: supertile block order table (supertile_order)
+    } else if (order) {  // supertile block order table (supertile_order / part_supertile_order)
         const uint32_t c = order[wg];
         bi = c & 0xffffu;
         bj = c >> 16;
     } else {
         tile_coords(LOCAL ? wg * part_world + part_rank : wg, bi, bj);
     }
+    // LOCAL: the block's index among this part's blocks (its storage slot and SegFlush phase, so
+    // any block order gives the same K bit for bit); = wg in the triangular order
+    const uint64_t blk = LOCAL ? ((uint64_t)bj * (bj + 1) / 2 + bi) / part_world : wg;
     const uint64_t i0 = (uint64_t)bi * BW, j0 = (uint64_t)bj * BW;
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
     const int wm = wave >> 2, wn = wave & 3;
@@ -1412,7 +1415,7 @@ __global__ __launch_bounds__(512, 1) void k_syrk_h2(const uint8_t* __restrict__ 
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         __shared__ uint32_t seg_slot;
-        SegFlush sf(seg, SBK, wg, nst, &seg_slot);
+        SegFlush sf(seg, SBK, blk, nst, &seg_slot);
         for (uint64_t s = 0; s < nst; s++) {
             const short* cur = lds + (s & 1) * STAGE;
             if (s + 1 < nst) issue(s + 1, lds + ((s + 1) & 1) * STAGE);
@@ -1432,7 +1435,7 @@ __global__ __launch_bounds__(512, 1) void k_syrk_h2(const uint8_t* __restrict__ 
             if (sf.due(s + 1 < nst)) sf.flush(acc);
         }
         sf.finish(acc);
-        epilogue_pi<LOCAL>(acc, tiles, n, bi, bj, accumulate, lane, wm, wn, wg);
+        epilogue_pi<LOCAL>(acc, tiles, n, bi, bj, accumulate, lane, wm, wn, blk);
         sf.release(seg);
         return;
     }
@@ -1537,7 +1540,7 @@ __global__ __launch_bounds__(512, 1) void k_syrk_h2(const uint8_t* __restrict__ 
         if (__builtin_amdgcn_readfirstlane(t) < 256) __builtin_amdgcn_s_setprio(1);
     }
     __shared__ uint32_t seg_slot;
-    SegFlush sf(seg, 2 * SBK, wg, (nst + 1) / 2, &seg_slot);
+    SegFlush sf(seg, 2 * SBK, blk, (nst + 1) / 2, &seg_slot);
     prologue(0);
     if constexpr (kPreA) fragsA(lds, 0, 0, A0s);
     for (uint64_t s = 0; s < nst; s += 2) {
@@ -1546,7 +1549,7 @@ __global__ __launch_bounds__(512, 1) void k_syrk_h2(const uint8_t* __restrict__ 
         if (sf.due(s + 2 < nst)) sf.flush(acc);
     }
     sf.finish(acc);
-    epilogue_pi<LOCAL>(acc, tiles, n, bi, bj, accumulate, lane, wm, wn, wg);
+    epilogue_pi<LOCAL>(acc, tiles, n, bi, bj, accumulate, lane, wm, wn, blk);
     sf.release(seg);
 }
 
@@ -2629,6 +2632,19 @@ void supertile_order(uint64_t nb, bool xcd, std::vector<uint32_t>& tab) {
         }
 }
 
+// supertile_order(nb, false) restricted to the blocks of part `rank` (block L = bj(bj+1)/2 + bi,
+// owner L mod world): the ~256 blocks in flight come from ~8 supertiles instead of ~1-2 columns of
+// the triangle, as the replicated kernel's table does for the whole triangle
+void part_supertile_order(uint64_t nb, int rank, int world, std::vector<uint32_t>& tab) {
+    std::vector<uint32_t> all;
+    supertile_order(nb, false, all);
+    tab.clear();
+    for (uint32_t c : all) {
+        const uint64_t bi = c & 0xffffu, bj = c >> 16;
+        if ((bj * (bj + 1) / 2 + bi) % (uint64_t)world == (uint64_t)rank) tab.push_back(c);
+    }
+}
+
 #ifdef SNPMI_UBENCH
 // device copy of supertile_order(nb, xcd) for the packed-SYRK order A/B (variants 65/66)
 static const uint32_t* ub_order(uint64_t nb, bool xcd) {
@@ -2829,9 +2845,12 @@ void launch_syrk_packed_bf3_part(const uint8_t* packed, uint64_t pitch, uint64_t
         return;
     }
     if (h2) {
+        // supertile order over the part's blocks (variant 67: the triangular order)
+        const uint64_t nb = ceil_div(n, 256);  // table entries pack bi | bj << 16
+        const uint32_t* order = (g_variant_syrk == 67 || nb >= 65536) ? nullptr : part_block_order(nb, rank, world);
         f32w::k_syrk_h2<true><<<(unsigned)nloc, 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, blocks, accumulate,
                                                                (uint32_t)rank, (uint32_t)world, 0, 0,
-                                                               seg_ctx());
+                                                               seg_ctx(), order);
         SNPMI_HIP(hipGetLastError());
     }
     f32w::k_syrk_bf3<true, false, 5><<<(unsigned)nloc, 512, 0, st>>>(packed, pitch, n, m, lut3, blocks, accumulate,
