@@ -89,7 +89,8 @@ int snpmi_release_cache(void);               /* free cached device/pinned scratc
 int snpmi_device_info(int device, char* name, size_t name_len, uint64_t* total_mem, int* cu_count);
 /* select a kernel variant by name; 0 = default.  Public switches: "f64" (0 = f64 GRMs as int8
  * residues + CRT, 1 = on the f64 MFMA), "seg" (SNPs per f32 GRM accumulation chain, default 12288,
- * 0 = one chain per launch).  The rest ("decode", "syrk", ...) are A/B hooks for benches. */
+ * 0 = one chain per launch).  The rest ("decode", "syrk", "part_order" (1 = the cfg5 part
+ * kernel in triangular block order), ...) are A/B hooks for benches. */
 int snpmi_set_kernel_variant(const char* kernel, int variant);
 int snpmi_get_kernel_variant(const char* kernel, int* variant);  /* current value of a hook above */
 

@@ -1294,6 +1294,7 @@ int snpmi_set_kernel_variant(const char* kernel, int variant) {
         if (std::strcmp(kernel, "decode") == 0) g_variant_decode = variant;
         else if (std::strcmp(kernel, "std") == 0) g_variant_std = variant;
         else if (std::strcmp(kernel, "diag") == 0) g_diag_exact = variant != 0;
+        else if (std::strcmp(kernel, "part_order") == 0) g_part_triangular = variant != 0;
         else if (std::strcmp(kernel, "extract") == 0) g_variant_extract = variant;
         else if (std::strcmp(kernel, "syrk") == 0) {
 #ifndef SNPMI_UBENCH
@@ -1326,6 +1327,7 @@ int snpmi_get_kernel_variant(const char* kernel, int* variant) {
         if (std::strcmp(kernel, "decode") == 0) *variant = g_variant_decode;
         else if (std::strcmp(kernel, "std") == 0) *variant = g_variant_std;
         else if (std::strcmp(kernel, "diag") == 0) *variant = g_diag_exact;
+        else if (std::strcmp(kernel, "part_order") == 0) *variant = g_part_triangular;
         else if (std::strcmp(kernel, "extract") == 0) *variant = g_variant_extract;
         else if (std::strcmp(kernel, "syrk") == 0) *variant = g_variant_syrk;
         else if (std::strcmp(kernel, "syrk_split") == 0) *variant = g_variant_syrk_split;

@@ -128,6 +128,7 @@ SegCtx seg_ctx();                                     // api.hip: the current de
 // block order of the packed fp16x2 SYRK
 const uint32_t* packed_block_order(uint64_t nb);
 const uint32_t* part_block_order(uint64_t nb, int rank, int world);
+extern int g_part_triangular;  // hook "part_order": 1 = the cfg5 part kernel in triangular order
 void launch_snp_stats(const uint8_t* packed, uint64_t pitch, uint64_t n_iid, uint64_t n_sid, int count_a1,
                       int std_kind, double a, double b, int use_stats, int dtype, void* stats, void* lut,
                       hipStream_t st);

@@ -2474,6 +2474,7 @@ __global__ __launch_bounds__(256, 2) void k_syrk_glds(const double* __restrict__
 int g_variant_syrk = 0;  // tuning hook (snpmi_set_kernel_variant "syrk")
 // 8192: 4.9e-6 of max diag at 50k x 100k on SnpGen-shaped data (21.8% missing) for +2.2% time;
 // 4096: 2.6e-6 for +3.8%; 16384: 6.9e-6 for +1.9%; none: 3.2e-5 (profiles/r03acc, r03seg)
+int g_part_triangular = 0;
 int g_seg_snps = 12288;  // tuning hook "seg" (round 4: 12288 with the exact f64 diagonal, k_diag_*)
 
 // host-side segmentation for the f32-MFMA kernels without SegFlush (fallbacks and small-N
@@ -2845,9 +2846,9 @@ void launch_syrk_packed_bf3_part(const uint8_t* packed, uint64_t pitch, uint64_t
         return;
     }
     if (h2) {
-        // supertile order over the part's blocks (variant 67: the triangular order)
+        // supertile order over the part's blocks (hook "part_order" = 1: the triangular order)
         const uint64_t nb = ceil_div(n, 256);  // table entries pack bi | bj << 16
-        const uint32_t* order = (g_variant_syrk == 67 || nb >= 65536) ? nullptr : part_block_order(nb, rank, world);
+        const uint32_t* order = (g_part_triangular || nb >= 65536) ? nullptr : part_block_order(nb, rank, world);
         f32w::k_syrk_h2<true><<<(unsigned)nloc, 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, blocks, accumulate,
                                                                (uint32_t)rank, (uint32_t)world, 0, 0,
                                                                seg_ctx(), order);

@@ -1,5 +1,5 @@
 """cfg5 part kernel block order (syrk.hip part_supertile_order): k_syrk_h2<LOCAL> walks the part's
-256x256 blocks in supertile order by default and in the triangular order under hook syrk=67; each
+256x256 blocks in supertile order by default and in the triangular order under hook part_order=1; each
 block's storage slot and SegFlush phase follow the block, not the workgroup, so both orders give
 the same K blocks bit for bit (here with several SegFlush cuts per launch and a ragged last block),
 and the blocks match the f64 oracle at the f32 bar."""
@@ -29,11 +29,11 @@ def test_part_block_orders_agree(n, m, part, parts, seg):
         N.call("snpmi_dev_snp_stats", packed.p, pitch, n, m, 0, N.STD_UNIT, 0.0, 0.0, 0, N.DT_F32, stats.p, lut.p)
         N.call("snpmi_set_kernel_variant", b"seg", seg)
         for k, v in enumerate((0, 67)):
-            N.call("snpmi_set_kernel_variant", b"syrk", v)
+            N.call("snpmi_set_kernel_variant", b"part_order", int(v == 67))
             try:
                 N.call("snpmi_dev_syrk_packed_part", packed.p, pitch, n, m, lut.p, part, parts, blocks[k].p, 0)
             finally:
-                N.call("snpmi_set_kernel_variant", b"syrk", 0)
+                N.call("snpmi_set_kernel_variant", b"part_order", 0)
             b = np.empty((nloc, 256, 256), dtype=np.float32)
             N.call("snpmi_memcpy_d2h", N.ptr(b), blocks[k].p, b.nbytes)
             out.append(b)

@@ -1,5 +1,5 @@
-"""cfg5 part-kernel block order A/B (hook syrk: 0 = supertile order over the part's blocks,
-67 = round 4's triangular order): HIP-event time of snpmi_dev_syrk_packed_part on one SnpGen-shaped
+"""cfg5 part-kernel block order A/B (hook part_order: 0 = supertile order over the part's blocks,
+1 = round 4's triangular order; keyed 0 / 67 below): HIP-event time of snpmi_dev_syrk_packed_part on one SnpGen-shaped
 block of --m SNPs at --n iids, part 0 of 8, alternating rounds, and sampled blocks compared bit
 for bit.  Prints one JSON line."""
 import argparse
@@ -36,12 +36,12 @@ def main():
     res, samples = {0: [], 67: []}, {}
     for r in range(a.rounds + 1):
         for v in (67, 0):
-            N.call("snpmi_set_kernel_variant", b"syrk", v)
+            N.call("snpmi_set_kernel_variant", b"part_order", int(v == 67))
             ev.record(0)
             N.call("snpmi_dev_syrk_packed_part", packed.p, pitch, n, m, lut.p, 0, P, blocks.p, 0)
             ev.record(1)
             t = ev.ms(0, 1)
-            N.call("snpmi_set_kernel_variant", b"syrk", 0)
+            N.call("snpmi_set_kernel_variant", b"part_order", 0)
             if r:  # round 0 = warm-up (code objects, order table)
                 res[v].append(t)
             s = np.empty((len(picks), 256, 256), dtype=np.float32)
