@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round-4 profiling recipe, run ON THE GPU BOX (via gpurun).  Usage: tools/profile_r04.sh <tag>
-#  1. kernel trace + stats of the default bench (per-kernel average durations)
+#  1. kernel trace + stats of the default bench (per-kernel average durations; tools/trace_summary.py)
 #  2. separate PMC passes FETCH_SIZE / WRITE_SIZE on a decode-only run, a GRM-only run (cfg4 shape,
 #     2 launches of 62500 SNPs) and the dense standardize (50k x 100k f32 in HBM, round-4 kernel)
 #  3. one SQ pass on the GRM-only run: MFMA busy per SIMD and the loaded clock
@@ -13,6 +13,7 @@ export TMPDIR=/tmp
 DEC="--steps 1 --warmup 1 --skip-cpu --skip-grm --grm5 off --e2e off --beta off --file off"
 GRM="--n-iid 16384 --n-sid 16384 --steps 1 --warmup 0 --skip-cpu --grm-sid 125000 --grm-f64 off --grm5 off --e2e off --beta off --file off"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- python3 bench.py --skip-cpu > $OUT/bench_under_rocprof.json 2> $OUT/trace.log
+python3 tools/trace_summary.py $OUT/trace/run_kernel_trace.csv $OUT/bench_under_rocprof.json > $OUT/kernel_trace_summary.json 2>&1 || true
 for C in FETCH_SIZE WRITE_SIZE; do
   timeout -s KILL 120 rocprofv3 --pmc $C --kernel-trace -d $OUT/dec_$C -o run --output-format csv -- python3 bench.py $DEC > $OUT/dec_$C.log 2>&1
   timeout -s KILL 120 rocprofv3 --pmc $C --kernel-trace -d $OUT/grm_$C -o run --output-format csv -- python3 bench.py $GRM > $OUT/grm_$C.log 2>&1
