@@ -137,7 +137,8 @@ def test_bench_with_rccl_communicator_world1(collective):
         assert d[k]["collective"] == ("ncclReduce(sum, root 0)" if collective == "reduce" else "ncclAllReduce(sum)")
     g5 = d["grm5"]
     assert g5["parity"]["pass"] and g5["parity"]["stats_bit_exact"], g5["parity"]
-    assert g5["blocks"] == 2 and g5["seconds"] > 0 and g5["gpu_busy_seconds"] > 0  # 4096 SNPs in 2048-SNP blocks
+    # 4096 SNPs: a 512-SNP first block, then 2048-SNP blocks (shard.block_spans)
+    assert g5["blocks"] == 3 and g5["seconds"] > 0 and g5["gpu_busy_seconds"] > 0
     assert "+ RCCL all-gather" in g5["workload"]
 
 
