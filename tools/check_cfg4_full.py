@@ -15,7 +15,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def main():
+def check():
+    """Returns the JSON dict (see the module doc)."""
     import bench
     from oracle import oracle as O
     from pysnptools_amd import _native as N
@@ -72,7 +73,11 @@ def main():
                      "max_rel_err_diag": float(np.max(np.abs(K[np.arange(R), ri] - ref[np.arange(R), ri]) /
                                                       ref[np.arange(R), ri])),
                      "rms_err_over_max_diag": float(np.sqrt(np.mean(err ** 2)) / scale)}
-    print(json.dumps(out), flush=True)
+    return out
+
+
+def main():
+    print(json.dumps(check()), flush=True)
 
 
 if __name__ == "__main__":
