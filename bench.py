@@ -98,6 +98,9 @@ def parse(argv=None):
     p.add_argument("--grm-collective", choices=["reduce", "allreduce"], default="reduce",
                    help="cfg4 at N > 1: K tiles summed onto rank 0 (read_kernel returns K to one caller) or onto every rank")
     p.add_argument("--grm-f64", choices=["on", "off"], default="on", help="cfg4 GRM in float64 (reference default)")
+    p.add_argument("--grm-overlap-parts", type=int, default=4,
+                   help="cfg4 f32 at N > 1: column groups of the last SYRK launch whose K-tile collective "
+                        "overlaps the next group's SYRK (1 = SYRK, then one collective)")
     p.add_argument("--grm5", choices=["on", "off"], default="on", help="cfg5 partitioned-K GRM leg")
     p.add_argument("--grm5-iid", type=int, default=500_000)
     p.add_argument("--grm5-sid", type=int, default=1_000_000, help="cfg5: SNPs of the whole job (all timed)")
@@ -633,9 +636,11 @@ def leg_grm(N, args, dist, dtype, keep_tiles=False):
     dist.barrier()
     t0 = time.perf_counter()
     ev.record(0)
-    g.add_packed(packed.p, pitch, my_m, N.STD_UNIT, 0.0, 0.0, 0, stats.p)
-    ev.record(1)
-    g.combine()
+    # the SYRK of this rank's shard + the K-tile collective, overlapped under a real RCCL
+    # communicator (f32: the last launch in column groups, each group's tiles summed on the aux
+    # stream under the next group's SYRK); ev 1 = the last SYRK done, ev 2 = K combined
+    g.add_packed_combine(packed.p, pitch, my_m, N.STD_UNIT, 0.0, 0.0, 0, stats.p, parts=args.grm_overlap_parts,
+                         syrk_done=ev.ev[1])
     ev.record(2)
     N.call("snpmi_stream_sync")
     dist.barrier()
@@ -971,7 +976,12 @@ def grm_entry(args, dist, r, dtype):
                            args.grm_block, (", %s%s of the K tiles" % ("RCCL " if dist.rccl else "", coll))
                            if coll else ""),
             "gflops": gf, "snps_per_s": m / r["wall"], "seconds": r["wall"], "scaling": "strong",
-            "collective": coll, "allreduce_ms": r["allreduce_ms"], "trace_K": r["trace"], "roofline": roof}
+            "collective": coll, "allreduce_ms": r["allreduce_ms"],
+            "collective_overlap": ("the last SYRK launch in %d column groups, each group's tiles summed on the aux "
+                                   "stream under the next group's SYRK; allreduce_ms = the exposed tail after the "
+                                   "last SYRK" % args.grm_overlap_parts)
+            if (coll and dist.rccl and f32 and args.grm_overlap_parts > 1) else None,
+            "trace_K": r["trace"], "roofline": roof}
 
 
 # ---------------------------------------------------------------------------- leg 4: the reference's call path

@@ -204,6 +204,17 @@ int snpmi_grm_add_packed_f32(const uint8_t* packed, uint64_t pitch, uint64_t n_i
                              int std_kind, double a, double b, int use_stats, float* stats);
 int snpmi_grm_add_packed_f64(const uint8_t* packed, uint64_t pitch, uint64_t n_iid, uint64_t n_sid, int count_a1,
                              int std_kind, double a, double b, int use_stats, double* stats);
+/* snpmi_grm_add_packed_f32 (the session's LAST add) + the K-tile collective of the SNP-sharded
+ * GRM (snpmi_rccl_reduce_sum / _allreduce_sum; collective 1 = reduce onto root, 2 = all-reduce,
+ * 0 = none), overlapped: the last SNP chunk's SYRK runs as `parts` column groups of the triangle
+ * (same K bit for bit) and each finished group's contiguous tile range is summed on the aux stream
+ * under the next group's SYRK; the compute stream waits for the last sum.  stats must be device
+ * memory (or NULL for Identity).  syrk_done (optional hipEvent_t from snpmi_event_create) is
+ * recorded after the last group's SYRK.  Replaces the add + reduce pair of shard.ShardedGrm
+ * (the rank loop of snpreader.py:651-655 followed by the sum over ranks). */
+int snpmi_grm_add_packed_reduce_f32(const uint8_t* packed, uint64_t pitch, uint64_t n_iid, uint64_t n_sid,
+                                    int count_a1, int std_kind, double a, double b, int use_stats, float* stats,
+                                    int collective, int root, int parts, void* syrk_done);
 int snpmi_grm_session_tiles(void** tiles, uint64_t* count);   /* device tiles + element count */
 /* K_out NULL: end the session without a result (a non-root rank after snpmi_rccl_reduce_sum) */
 int snpmi_grm_end(int diag_k_to_n, double* factor, void* K_out);

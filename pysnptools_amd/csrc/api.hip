@@ -1228,6 +1228,128 @@ static void grm_add_packed_impl(const uint8_t* packed, uint64_t pitch, uint64_t 
     }
     if (host_stats) SNPMI_HIP(hipStreamSynchronize(d.stream));
 }
+// Column groups of the upper triangle for an overlapped collective: ranges [L0, L1) of 256-block
+// indices covering whole supertile columns (16 block columns), about equal block counts each.
+struct ColGroup {
+    uint64_t L0, L1;  // 256-block index range (supertile table and triangular order alike)
+    uint64_t c0, c1;  // block columns [c0, c1)
+};
+static std::vector<ColGroup> column_groups(uint64_t nb, int parts) {
+    const uint64_t ns = ceil_div(nb, 16);
+    auto B = [&](uint64_t c) { c = std::min(c, nb); return c * (c + 1) / 2; };
+    const uint64_t P = (uint64_t)std::max<int64_t>(1, std::min<int64_t>(parts, (int64_t)ns));
+    std::vector<ColGroup> out;
+    uint64_t J = 0;
+    for (uint64_t p = 0; p < P && J < ns; p++) {
+        const uint64_t target = B(nb) * (p + 1) / P;
+        uint64_t J1 = J + 1;
+        while (J1 < ns && B(16 * J1) < target) J1++;
+        if (p + 1 == P) J1 = ns;
+        out.push_back({B(16 * J), B(16 * J1), std::min(16 * J, nb), std::min(16 * J1, nb)});
+        J = J1;
+    }
+    return out;
+}
+
+// snpmi_grm_add_packed_f32 followed by the K-tile collective (collective 1 = ncclReduce onto
+// root, 2 = ncclAllReduce, 0 = none), overlapped: the last SNP chunk's SYRK runs as `parts` column
+// groups of the triangle (launch_syrk_packed_h2_cols, the same K bit for bit), and as soon as a
+// group's SYRK and diagonal write-back are done its contiguous range of tiles is summed over the
+// ranks on the aux stream while the next group's SYRK runs.  The compute stream waits for the last
+// sum before the call returns, so later work sees the combined K.  Paths without column groups
+// (split-K grids, the tuning variants, the f32 MFMA fallbacks) run the SYRK whole and sum after it.
+// syrk_done (optional hipEvent_t) is recorded on the compute stream after the last group's SYRK.
+static int g_last_groups = 0;  // column groups of the last grm_add_packed_reduce (read-only hook "overlap_groups")
+
+static void grm_add_packed_reduce_impl(const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m, int count_a1,
+                                       int std_kind, double a, double b, int use_stats, float* stats, int collective,
+                                       int root, int parts, hipEvent_t syrk_done) {
+    std::lock_guard<std::recursive_mutex> lk(g_call_mutex);
+    SNPMI_REQUIRE(g_session.active, SNPMI_E_ARG, "no GRM session (call snpmi_grm_begin)");
+    SNPMI_REQUIRE(g_session.dtype == SNPMI_DT_F32, SNPMI_E_ARG, "the overlapped collective is for f32 sessions");
+    SNPMI_REQUIRE(collective >= 0 && collective <= 2, SNPMI_E_ARG, "collective must be 0 (none), 1 (reduce), 2 (all-reduce)");
+    SNPMI_REQUIRE(collective == 0 || rccl_ready(), SNPMI_E_ARG, "RCCL communicator not initialised");
+    SNPMI_REQUIRE(parts >= 1, SNPMI_E_ARG, "parts must be >= 1");
+    Device& d = device();
+    const uint64_t count = n_tiles_upper(g_session.n) * kTile * kTile;
+    const int rt = collective == 1 ? root : -1;
+    const uint64_t nb = ceil_div(n, 256);
+    const bool grouped = m > 0 && n > 0 && n == g_session.n && use_bf3(SNPMI_DT_F32) && use_h2() && g_diag_exact &&
+                         bf3_split_slices(n, std::min<uint64_t>(m, 1ull << 16), d.cu_count) == 1 &&
+                         nb < 65536 && parts > 1;
+    g_last_groups = 1;
+    if (!grouped) {
+        grm_add_packed_impl<float>(packed, pitch, n, m, count_a1, std_kind, a, b, use_stats, stats);
+        float* t = (float*)session_tiles(d);
+        if (!g_session.wrote) {  // no SNPs on this rank: it contributes zeros
+            SNPMI_HIP(hipMemsetAsync(t, 0, count * sizeof(float), d.stream));
+            g_session.wrote = true;
+        }
+        if (syrk_done) SNPMI_HIP(hipEventRecord(syrk_done, d.stream));
+        if (collective) rccl_sum_on(t, count, SNPMI_DT_F32, rt, d.stream);
+        return;
+    }
+    SNPMI_REQUIRE(pitch % 64 == 0 && pitch >= ceil_div(n, 4), SNPMI_E_ARG, "pitch must be snpmi_packed_pitch");
+    SNPMI_REQUIRE(std_kind >= SNPMI_STD_NONE && std_kind <= SNPMI_STD_BETA, SNPMI_E_ARG, "bad standardizer kind");
+    SNPMI_REQUIRE(stats != nullptr || std_kind == SNPMI_STD_NONE, SNPMI_E_ARG, "stats is NULL");
+    SNPMI_REQUIRE(packed != nullptr && is_device_ptr(d, packed), SNPMI_E_ARG,
+                  "packed must be device memory of the current device");
+    SNPMI_REQUIRE(std_kind == SNPMI_STD_NONE || is_device_ptr(d, stats), SNPMI_E_ARG,
+                  "stats must be device memory for the overlapped collective");
+    // the chunks before the last one: the plain session path (same chunking as grm_add_packed_impl)
+    const uint64_t nchunk = ceil_div(m, 1ull << 16);
+    const uint64_t step = std::min<uint64_t>(1ull << 16, round_up(ceil_div(m, nchunk), 256));
+    const uint64_t s_last = ((m - 1) / step) * step;
+    if (s_last > 0)
+        grm_add_packed_impl<float>(packed, pitch, n, s_last, count_a1, std_kind, a, b, use_stats, stats);
+    float* tiles = (float*)session_tiles(d);
+    const int acc = g_session.wrote ? 1 : 0;
+    const uint64_t cnt = m - s_last;
+    const uint8_t* src = packed + s_last * pitch;
+    float* lut = (float*)d.get(Device::S_LUT, cnt * 4 * sizeof(float));
+    launch_snp_stats(src, pitch, n, cnt, count_a1, std_kind, a, b, use_stats, SNPMI_DT_F32,
+                     stats ? stats + 2 * s_last : (float*)d.get(Device::S_STATS, cnt * 2 * sizeof(float)), lut,
+                     d.stream);
+    H2Lut h2;
+    const uint32_t* l3 = lut_bf3(d, lut, cnt, &h2);
+    double* diag = (double*)d.get(Device::S_DIAG, n * sizeof(double));
+    launch_diag_begin(tiles, n, 0, 0, acc, diag, d.stream);
+    launch_diag_sq(src, pitch, n, cnt, lut, diag, d.stream);
+    g_session.wrote = true;
+    const auto groups = column_groups(nb, parts);
+    g_last_groups = (int)groups.size();
+    const uint64_t nt = n_tiles_1d(n);
+    auto T = [&](uint64_t t) { t = std::min(t, nt); return t * (t + 1) / 2 * (uint64_t)(kTile * kTile); };
+    std::vector<hipEvent_t> evs;
+    try {
+        for (const auto& gr : groups) {
+            launch_syrk_packed_h2_cols(src, pitch, n, cnt, l3, tiles, acc, d.stream, &h2, gr.L0, gr.L1);
+            // block columns [c0, c1): diagonal iids [256 c0, 256 c1), 128-tile columns [2 c0, 2 c1)
+            const uint64_t c0 = gr.c0, c1 = gr.c1;
+            launch_diag_patch(tiles, n, 256 * c0, 256 * c1, 0, 0, diag, d.stream);
+            if (!collective) continue;
+            hipEvent_t e;
+            SNPMI_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            evs.push_back(e);
+            SNPMI_HIP(hipEventRecord(e, d.stream));
+            SNPMI_HIP(hipStreamWaitEvent(d.aux, e, 0));
+            const uint64_t e0 = T(2 * c0), e1 = T(2 * c1);
+            if (e1 > e0) rccl_sum_on(tiles + e0, e1 - e0, SNPMI_DT_F32, rt, d.aux);
+        }
+        if (syrk_done) SNPMI_HIP(hipEventRecord(syrk_done, d.stream));
+        if (collective) {
+            hipEvent_t e;
+            SNPMI_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            evs.push_back(e);
+            SNPMI_HIP(hipEventRecord(e, d.aux));
+            SNPMI_HIP(hipStreamWaitEvent(d.stream, e, 0));
+        }
+    } catch (...) {
+        for (hipEvent_t e : evs) (void)hipEventDestroy(e);
+        throw;
+    }
+    for (hipEvent_t e : evs) SNPMI_HIP(hipEventDestroy(e));
+}
 }  // namespace snpmi
 
 // ====================================================================== exported C ABI
@@ -1328,6 +1450,7 @@ int snpmi_get_kernel_variant(const char* kernel, int* variant) {
         else if (std::strcmp(kernel, "std") == 0) *variant = g_variant_std;
         else if (std::strcmp(kernel, "diag") == 0) *variant = g_diag_exact;
         else if (std::strcmp(kernel, "part_order") == 0) *variant = g_part_triangular;
+        else if (std::strcmp(kernel, "overlap_groups") == 0) *variant = g_last_groups;
         else if (std::strcmp(kernel, "extract") == 0) *variant = g_variant_extract;
         else if (std::strcmp(kernel, "syrk") == 0) *variant = g_variant_syrk;
         else if (std::strcmp(kernel, "syrk_split") == 0) *variant = g_variant_syrk_split;
@@ -1441,6 +1564,15 @@ int snpmi_grm_add_packed_f32(const uint8_t* packed, uint64_t pitch, uint64_t n_i
 int snpmi_grm_add_packed_f64(const uint8_t* packed, uint64_t pitch, uint64_t n_iid, uint64_t n_sid, int count_a1,
                              int std_kind, double a, double b, int use_stats, double* stats) {
     return guarded([&] { grm_add_packed_impl<double>(packed, pitch, n_iid, n_sid, count_a1, std_kind, a, b, use_stats, stats); });
+}
+
+int snpmi_grm_add_packed_reduce_f32(const uint8_t* packed, uint64_t pitch, uint64_t n_iid, uint64_t n_sid,
+                                    int count_a1, int std_kind, double a, double b, int use_stats, float* stats,
+                                    int collective, int root, int parts, void* syrk_done) {
+    return guarded([&] {
+        grm_add_packed_reduce_impl(packed, pitch, n_iid, n_sid, count_a1, std_kind, a, b, use_stats, stats, collective,
+                                   root, parts, (hipEvent_t)syrk_done);
+    });
 }
 
 int snpmi_grm_add_dense_f32(const float* val, uint64_t rows, uint64_t cols, int order_c) {

@@ -2122,9 +2122,9 @@ __global__ __launch_bounds__(kBlock) void k_diag_sq(const uint8_t* __restrict__ 
         if (16 * w + k < n) atomicAdd(diag + 16 * w + k, acc[k]);
 }
 
-__global__ __launch_bounds__(kBlock) void k_diag_patch(float* __restrict__ K, uint64_t n, int part_rank,
+__global__ __launch_bounds__(kBlock) void k_diag_patch(float* __restrict__ K, uint64_t i0, uint64_t i1, int part_rank,
                                                        int part_world, const double* __restrict__ diag) {
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    for (uint64_t i = i0 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < i1; i += (uint64_t)gridDim.x * blockDim.x) {
         const int64_t o = diag_offset(i, part_rank, part_world);
         if (o >= 0) K[o] = (float)diag[i];
     }
@@ -2961,19 +2961,30 @@ void launch_diag_begin(const float* K, uint64_t n, int part_rank, int part_world
     SNPMI_LAUNCH_CHECK();
 }
 
+void launch_diag_sq(const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m, const float* lut, double* diag,
+                    hipStream_t st) {
+    if (n == 0 || m == 0) return;
+    const uint64_t nw = (n + 15) / 16, bx = ceil_div(nw, kBlock);
+    // enough (word, slice) threads to fill 256 CUs several times over, slices of >= 64 SNPs
+    const uint64_t slices = std::max<uint64_t>(1, std::min<uint64_t>(ceil_div(m, 64), ceil_div(256 * 1024, nw)));
+    const uint64_t per = ceil_div(m, slices);
+    k_diag_sq<<<dim3((unsigned)bx, (unsigned)ceil_div(m, per)), kBlock, 0, st>>>(packed, pitch, n, m, lut, per, diag);
+    SNPMI_LAUNCH_CHECK();
+}
+
+void launch_diag_patch(float* K, uint64_t n, uint64_t i0, uint64_t i1, int part_rank, int part_world,
+                       const double* diag, hipStream_t st) {
+    i1 = std::min(i1, n);
+    if (i0 >= i1) return;
+    k_diag_patch<<<grid_for(i1 - i0, kBlock), kBlock, 0, st>>>(K, i0, i1, part_rank, part_world, diag);
+    SNPMI_LAUNCH_CHECK();
+}
+
 void launch_diag_end(const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m, const float* lut, float* K,
                      int part_rank, int part_world, double* diag, hipStream_t st) {
     if (n == 0) return;
-    if (m > 0) {
-        const uint64_t nw = (n + 15) / 16, bx = ceil_div(nw, kBlock);
-        // enough (word, slice) threads to fill 256 CUs several times over, slices of >= 64 SNPs
-        const uint64_t slices = std::max<uint64_t>(1, std::min<uint64_t>(ceil_div(m, 64), ceil_div(256 * 1024, nw)));
-        const uint64_t per = ceil_div(m, slices);
-        k_diag_sq<<<dim3((unsigned)bx, (unsigned)ceil_div(m, per)), kBlock, 0, st>>>(packed, pitch, n, m, lut, per, diag);
-        SNPMI_LAUNCH_CHECK();
-    }
-    k_diag_patch<<<grid_for(n, kBlock), kBlock, 0, st>>>(K, n, part_rank, part_world, diag);
-    SNPMI_LAUNCH_CHECK();
+    launch_diag_sq(packed, pitch, n, m, lut, diag, st);
+    launch_diag_patch(K, n, 0, n, part_rank, part_world, diag, st);
 }
 
 void launch_synth(uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t sid0, uint64_t m, uint64_t seed,

@@ -31,6 +31,26 @@ void require_comm() {
 }
 }  // namespace
 
+namespace snpmi {
+// in-place sum of a device f32/f64 range over the ranks on stream st: ncclReduce onto root, or
+// ncclAllReduce for root < 0 (api.hip grm_add_packed_reduce: one per finished column group, on the
+// aux stream, under the next group's SYRK)
+void rccl_sum_on(void* buf, uint64_t count, int dtype, int root, hipStream_t st) {
+    require_comm();
+    SNPMI_REQUIRE(dtype == SNPMI_DT_F32 || dtype == SNPMI_DT_F64, SNPMI_E_ARG, "sum dtype must be f32/f64");
+    const ncclDataType_t t = dtype == SNPMI_DT_F64 ? ncclFloat64 : ncclFloat32;
+    if (root < 0) {
+        SNPMI_NCCL(ncclAllReduce(buf, buf, count, t, ncclSum, g_comm, st));
+        return;
+    }
+    int nranks = 0;
+    SNPMI_NCCL(ncclCommCount(g_comm, &nranks));
+    SNPMI_REQUIRE(root < nranks, SNPMI_E_ARG, "reduce root out of range");
+    SNPMI_NCCL(ncclReduce(buf, buf, count, t, ncclSum, root, g_comm, st));
+}
+bool rccl_ready() { return g_comm != nullptr; }
+}  // namespace snpmi
+
 using namespace snpmi;
 
 extern "C" {

@@ -179,6 +179,14 @@ void launch_diag_begin(const float* K, uint64_t n, int part_rank, int part_world
                        hipStream_t st);
 void launch_diag_end(const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m, const float* lut, float* K,
                      int part_rank, int part_world, double* diag, hipStream_t st);
+// launch_diag_end in two steps: the f64 squares of all iids, then the write-back of iids [i0, i1)
+void launch_diag_sq(const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m, const float* lut, double* diag,
+                    hipStream_t st);
+void launch_diag_patch(float* K, uint64_t n, uint64_t i0, uint64_t i1, int part_rank, int part_world,
+                       const double* diag, hipStream_t st);
+// rccl.hip: in-place sum over the ranks of a device range on stream st (root < 0: all-reduce)
+void rccl_sum_on(void* buf, uint64_t count, int dtype, int root, hipStream_t st);
+bool rccl_ready();
 void launch_dense_scale(void* p, uint64_t count, int dtype, double scale, hipStream_t st);
 void launch_sumsq(const void* p, uint64_t count, int dtype, double* out_dev, hipStream_t st);
 void launch_dense_trace(const void* K, uint64_t n, int dtype, double* trace_dev, hipStream_t st);
@@ -221,6 +229,9 @@ void launch_syrk_dense_h2(const float* Z, uint64_t ldz, uint64_t n, uint64_t m, 
                           const uint32_t* order, float* tiles, int accumulate, hipStream_t st);
 void launch_syrk_packed_bf3(const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m, const uint32_t* lut3,
                             float* tiles, int accumulate, hipStream_t st, const H2Lut* h2 = nullptr);
+void launch_syrk_packed_h2_cols(const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m, const uint32_t* lut3,
+                                float* tiles, int accumulate, hipStream_t st, const H2Lut* h2, uint64_t L0,
+                                uint64_t L1);
 void launch_syrk_packed_bf3_split(const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m, const uint32_t* lut3,
                                   int slices, float* partial, float* tiles, int accumulate, hipStream_t st,
                                   const H2Lut* h2 = nullptr);

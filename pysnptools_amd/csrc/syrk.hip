@@ -832,7 +832,8 @@ __global__ __launch_bounds__(512, 1) void k_syrk_bf3(const uint8_t* __restrict__
                                                      float* __restrict__ tiles, int accumulate,
                                                      uint32_t part_rank = 0, uint32_t part_world = 1,
                                                      uint64_t kslice = 0, uint64_t slice_elems = 0,
-                                                     const uint32_t* __restrict__ gate = nullptr, SegCtx seg = SegCtx()) {
+                                                     const uint32_t* __restrict__ gate = nullptr, SegCtx seg = SegCtx(),
+                                                     uint64_t wg0 = 0) {
     __shared__ __attribute__((aligned(16))) short lds[2 * B3_STAGE];
     if (gate && *gate == 0) return;  // fallback of k_syrk_h2: runs only when its range flag is set
     if (gridDim.y > 1) {  // split-K: slice blockIdx.y covers SNPs [y*kslice, +kslice) into its own partial K
@@ -842,7 +843,8 @@ __global__ __launch_bounds__(512, 1) void k_syrk_bf3(const uint8_t* __restrict__
         kdim = min(kslice, kdim - k0);
         tiles += (uint64_t)blockIdx.y * slice_elems;
     }
-    const uint64_t wg = XCD ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
+    // wg0: first block of a column-group launch (triangular order), as in k_syrk_h2
+    const uint64_t wg = wg0 + (XCD ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x);
     uint32_t bi, bj;
     tile_coords(LOCAL ? wg * part_world + part_rank : wg, bi, bj);
     const uint64_t i0 = (uint64_t)bi * BW, j0 = (uint64_t)bj * BW;
@@ -1232,7 +1234,10 @@ __global__ __launch_bounds__(512, 1) void k_syrk_h2(const uint8_t* __restrict__ 
                                                     const uint32_t* __restrict__ flag, float* __restrict__ tiles,
                                                     int accumulate, uint32_t part_rank = 0, uint32_t part_world = 1,
                                                     uint64_t kslice = 0, uint64_t slice_elems = 0,
-                                                    SegCtx seg = SegCtx(), const uint32_t* __restrict__ order = nullptr) {
+                                                    SegCtx seg = SegCtx(), const uint32_t* __restrict__ order = nullptr,
+                                                    uint64_t wg0 = 0) {
+    // wg0: first block of this launch in the full grid's order (a column group of the triangle,
+    // launch_syrk_packed_h2_cols); block identity, storage and SegFlush phase follow wg0 + blockIdx.x
     // KS = 16-SNP k-steps per LDS stage (MODE 4/5: two, one barrier per 32 SNPs)
     // MODE 10 = MODE 4 with the loader's registers double-buffered: stage s+2's codes/LUT are
     // loaded at the START of stage s (a whole stage to arrive instead of one MFMA group)
@@ -1250,7 +1255,7 @@ __global__ __launch_bounds__(512, 1) void k_syrk_h2(const uint8_t* __restrict__ 
         kdim = min(kslice, kdim - k0);
         tiles += (uint64_t)blockIdx.y * slice_elems;
     }
-    const uint64_t wg = blockIdx.x;
+    const uint64_t wg = wg0 + blockIdx.x;
     uint32_t bi, bj;
     if constexpr (DENSE) {
         // lut2 = block order table (supertile_order): the 256 blocks in flight share 32 panels
@@ -2808,6 +2813,28 @@ void launch_syrk_packed_bf3(const uint8_t* packed, uint64_t pitch, uint64_t n, u
             f32w::k_syrk_bf3<false, false, 5><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, lut3, tiles, accumulate, 0, 1,
                                                                           0, 0, nullptr, seg_ctx());
     }
+    SNPMI_HIP(hipGetLastError());
+}
+
+// One column group of the default f32 SYRK: the upper-triangle 256-blocks [L0, L1) -- whole
+// supertile columns, so the same blocks sit at [L0, L1) of both the supertile table (k_syrk_h2)
+// and the triangular order (the bf16x3 range fallback) -- each kernel with its full-grid block
+// identity (wg0 = L0), so a launch split into column groups writes the same K bit for bit as the
+// whole launch.  Used to overlap the K-tile collective of finished groups with the next group's
+// SYRK (api.hip grm_add_packed_reduce).
+void launch_syrk_packed_h2_cols(const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m, const uint32_t* lut3,
+                                float* tiles, int accumulate, hipStream_t st, const H2Lut* h2, uint64_t L0,
+                                uint64_t L1) {
+    const uint64_t nb = ceil_div(n, 256), g = nb * (nb + 1) / 2;
+    SNPMI_REQUIRE(h2 && L0 < L1 && L1 <= g && g < (1ull << 31), SNPMI_E_ARG, "bad SYRK column group");
+    SNPMI_REQUIRE(pitch % 64 == 0 && pitch * 4 >= nb * 256, SNPMI_E_ARG, "packed pitch must cover round_up(n, 256) iids");
+    if (m == 0) return;
+    f32w::k_syrk_h2<false, 4><<<(unsigned)(L1 - L0), 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles,
+                                                                  accumulate, 0, 1, 0, 0, seg_ctx(),
+                                                                  packed_block_order(nb), L0);
+    SNPMI_HIP(hipGetLastError());
+    f32w::k_syrk_bf3<false, false, 5><<<(unsigned)(L1 - L0), 512, 0, st>>>(packed, pitch, n, m, lut3, tiles, accumulate,
+                                                                          0, 1, 0, 0, h2->flag, seg_ctx(), L0);
     SNPMI_HIP(hipGetLastError());
 }
 

@@ -124,6 +124,27 @@ class ShardedGrm(object):
         N.call("snpmi_grm_add_packed_" + N.suffix(self.dtype), packed, pitch, self.n, n_sid, int(bool(count_a1)),
                kind, a, b, int(use_stats), stats if isinstance(stats, ctypes.c_void_p) else N.ptr(stats))
 
+    def add_packed_combine(self, packed, pitch, n_sid, kind, a, b, use_stats, stats, count_a1=False, parts=4,
+                           syrk_done=None):
+        """``add_packed`` of this rank's LAST SNPs + ``combine``, overlapped when a real RCCL
+        communicator and an f32 session allow it (``snpmi_grm_add_packed_reduce_f32``: the last
+        SYRK launch runs as ``parts`` column groups of the triangle and each finished group's tiles
+        are summed over the ranks on the aux stream under the next group's SYRK; the same K bit for
+        bit).  ``stats`` must then be device memory.  Otherwise the two calls run one after the
+        other (the host rehearsal group, f64, no collective).  ``syrk_done``: optional event
+        (``snpmi_event_create``) recorded after the last SYRK, for timing."""
+        N = self.N
+        dev_stats = isinstance(stats, ctypes.c_void_p)
+        if (self.dtype == np.float32 and self.collective != "none" and self.dist is not None and self.dist.rccl
+                and dev_stats):
+            N.call("snpmi_grm_add_packed_reduce_f32", packed, pitch, self.n, n_sid, int(bool(count_a1)), kind, a, b,
+                   int(use_stats), stats, 1 if self.collective == "reduce" else 2, self.root, int(parts), syrk_done)
+            return
+        self.add_packed(packed, pitch, n_sid, kind, a, b, use_stats, stats, count_a1)
+        if syrk_done is not None:
+            N.call("snpmi_event_record", syrk_done)
+        self.combine()
+
     def tiles(self):
         """(device pointer, element count) of this rank's tiles."""
         t, count = ctypes.c_void_p(), ctypes.c_uint64()

@@ -1,0 +1,108 @@
+"""The cfg4 K-tile collective overlapped with the SYRK (api.hip grm_add_packed_reduce,
+snpmi_grm_add_packed_reduce_f32, shard.ShardedGrm.add_packed_combine): the last SNP chunk's SYRK
+runs as column groups of the triangle (launch_syrk_packed_h2_cols: each kernel keeps its full-grid
+block identity, so storage and SegFlush phases are unchanged) with each group's diagonal written
+back before its tiles are summed on the aux stream.
+
+* without a collective, the grouped call leaves exactly the tiles of snpmi_grm_add_packed_f32 (bit
+  for bit) -- 1 to 5 groups, one or two SNP chunks, Unit / Beta(1,25) (rare-SNP weights outside
+  fp16's range: the bf16x3 fallback runs inside the groups) / count_A1, use_stats;
+* under a real RCCL communicator at world 1 (reduce onto 0 and all-reduce: sums over one rank),
+  the same tiles again, so the ranged collectives on the aux stream cover every tile exactly once
+  and the compute stream sees them finished."""
+import ctypes
+
+import numpy as np
+import pytest
+
+from conftest import ROOT  # noqa: F401  (sys.path)
+import bench
+from pysnptools_amd import _native as N
+from pysnptools_amd import dist as D
+from pysnptools_amd.shard import ShardedGrm
+
+pytestmark = pytest.mark.gpu
+
+
+def _data(n, m, seed):
+    pitch = N.lib().snpmi_packed_pitch(n)
+    packed = bench.Dev(N, pitch * m)
+    bench.synth(N, packed.p, pitch, n, 0, m, seed, 0.05)
+    return packed, pitch
+
+
+def _tiles(g):
+    t, count = g.tiles()
+    out = np.empty(count, dtype=np.float32)
+    N.call("snpmi_stream_sync")
+    N.call("snpmi_memcpy_d2h", N.ptr(out), t, out.nbytes)
+    return out
+
+
+def _run(n, m, packed, pitch, kind, a, b, count_a1, parts, collective, dist=None, use_stats=False):
+    stats = bench.Dev(N, m * 8)
+    try:
+        if use_stats:  # trained stats from a first pass
+            g = ShardedGrm(n, np.float32, None, "none")
+            g.add_packed(packed.p, pitch, m, kind, a, b, 0, stats.p, count_a1)
+            g.abort()
+        g = ShardedGrm(n, np.float32, dist, "none" if collective is None else collective)
+        if parts is None:
+            g.add_packed(packed.p, pitch, m, kind, a, b, int(use_stats), stats.p, count_a1)
+        elif collective is None:
+            N.call("snpmi_grm_add_packed_reduce_f32", packed.p, pitch, n, m, int(count_a1), kind, a, b,
+                   int(use_stats), stats.p, 0, 0, parts, None)
+        else:
+            ev = ctypes.c_void_p()
+            N.call("snpmi_event_create", ctypes.byref(ev))
+            g.add_packed_combine(packed.p, pitch, m, kind, a, b, int(use_stats), stats.p, count_a1, parts=parts,
+                                 syrk_done=ev)
+            N.call("snpmi_stream_sync")
+            N.call("snpmi_event_destroy", ev)
+        out = _tiles(g)
+        g.abort()
+        return out
+    finally:
+        stats.free()
+
+
+CASES = [(30000, 3000, "unit", False, False, 4), (30000, 70000, "unit", False, False, 3),
+         (40000, 2000, "beta", False, False, 5), (33000, 1500, "unit", True, True, 2),
+         (30000, 1000, "unit", False, False, 1)]
+
+
+@pytest.mark.parametrize("n,m,std,count_a1,use_stats,parts", CASES)
+def test_grouped_syrk_equals_whole_launch(n, m, std, count_a1, use_stats, parts):
+    kind, a, b = (N.STD_UNIT, 0.0, 0.0) if std == "unit" else (N.STD_BETA, 1.0, 25.0)
+    packed, pitch = _data(n, m, 41)
+    try:
+        ref = _run(n, m, packed, pitch, kind, a, b, count_a1, None, None, use_stats=use_stats)
+        got = _run(n, m, packed, pitch, kind, a, b, count_a1, parts, None, use_stats=use_stats)
+    finally:
+        packed.free()
+    groups = N.kernel_variant("overlap_groups")  # the grouped call ran last
+    assert groups == (1 if parts == 1 else min(parts, (n + 4095) // 4096)), groups
+    assert np.abs(ref).max() > 0
+    assert np.array_equal(ref, got)
+
+
+@pytest.fixture
+def rccl1():
+    d = D.init_from_env(force_rccl=True, env={"RANK": "0", "WORLD_SIZE": "1"}, timeout=120)
+    try:
+        yield d
+    finally:
+        d.close()
+
+
+@pytest.mark.parametrize("collective", ["reduce", "allreduce"])
+def test_overlapped_collective_world1(rccl1, collective):
+    n, m = 30000, 4000
+    packed, pitch = _data(n, m, 43)
+    try:
+        ref = _run(n, m, packed, pitch, N.STD_UNIT, 0.0, 0.0, False, None, None)
+        got = _run(n, m, packed, pitch, N.STD_UNIT, 0.0, 0.0, False, 4, collective, dist=rccl1)
+    finally:
+        packed.free()
+    assert N.kernel_variant("overlap_groups") == 4
+    assert np.array_equal(ref, got)
