@@ -98,7 +98,7 @@ def parse(argv=None):
     p.add_argument("--grm-collective", choices=["reduce", "allreduce"], default="reduce",
                    help="cfg4 at N > 1: K tiles summed onto rank 0 (read_kernel returns K to one caller) or onto every rank")
     p.add_argument("--grm-f64", choices=["on", "off"], default="on", help="cfg4 GRM in float64 (reference default)")
-    p.add_argument("--grm-overlap-parts", type=int, default=4,
+    p.add_argument("--grm-overlap-parts", type=int, default=2,
                    help="cfg4 f32 at N > 1: column groups of the last SYRK launch whose K-tile collective "
                         "overlaps the next group's SYRK (1 = SYRK, then one collective)")
     p.add_argument("--grm5", choices=["on", "off"], default="on", help="cfg5 partitioned-K GRM leg")

@@ -1229,7 +1229,10 @@ static void grm_add_packed_impl(const uint8_t* packed, uint64_t pitch, uint64_t 
     if (host_stats) SNPMI_HIP(hipStreamSynchronize(d.stream));
 }
 // Column groups of the upper triangle for an overlapped collective: ranges [L0, L1) of 256-block
-// indices covering whole supertile columns (16 block columns), about equal block counts each.
+// indices covering whole supertile columns (16 block columns).  The last group holds ~1/4 of the
+// blocks (its sum is the exposed tail), the others split the first ~3/4 evenly; every group
+// boundary costs about one round of workgroups (~4 ms at 50k iids, profiles/r04l), so the bench
+// uses 2 groups.
 struct ColGroup {
     uint64_t L0, L1;  // 256-block index range (supertile table and triangular order alike)
     uint64_t c0, c1;  // block columns [c0, c1)
@@ -1241,7 +1244,7 @@ static std::vector<ColGroup> column_groups(uint64_t nb, int parts) {
     std::vector<ColGroup> out;
     uint64_t J = 0;
     for (uint64_t p = 0; p < P && J < ns; p++) {
-        const uint64_t target = B(nb) * (p + 1) / P;
+        const uint64_t target = p + 1 == P ? B(nb) : (uint64_t)((double)B(nb) * 0.75 * (double)(p + 1) / (double)(P - 1));
         uint64_t J1 = J + 1;
         while (J1 < ns && B(16 * J1) < target) J1++;
         if (p + 1 == P) J1 = ns;

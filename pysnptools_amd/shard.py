@@ -124,7 +124,7 @@ class ShardedGrm(object):
         N.call("snpmi_grm_add_packed_" + N.suffix(self.dtype), packed, pitch, self.n, n_sid, int(bool(count_a1)),
                kind, a, b, int(use_stats), stats if isinstance(stats, ctypes.c_void_p) else N.ptr(stats))
 
-    def add_packed_combine(self, packed, pitch, n_sid, kind, a, b, use_stats, stats, count_a1=False, parts=4,
+    def add_packed_combine(self, packed, pitch, n_sid, kind, a, b, use_stats, stats, count_a1=False, parts=2,
                            syrk_done=None):
         """``add_packed`` of this rank's LAST SNPs + ``combine``, overlapped when a real RCCL
         communicator and an f32 session allow it (``snpmi_grm_add_packed_reduce_f32``: the last
