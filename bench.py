@@ -977,10 +977,12 @@ def grm_entry(args, dist, r, dtype):
                            if coll else ""),
             "gflops": gf, "snps_per_s": m / r["wall"], "seconds": r["wall"], "scaling": "strong",
             "collective": coll, "allreduce_ms": r["allreduce_ms"],
-            "collective_overlap": ("the last SYRK launch in %d column groups, each group's tiles summed on the aux "
-                                   "stream under the next group's SYRK; allreduce_ms = the exposed tail after the "
-                                   "last SYRK" % args.grm_overlap_parts)
-            if (coll and dist.rccl and f32 and args.grm_overlap_parts > 1) else None,
+            "collective_overlap": (("the last SYRK launch in %d column groups, each group's tiles summed on the aux "
+                                    "stream under the next group's SYRK" % args.grm_overlap_parts) if f32 else
+                                   "the CRT path's column-aligned residue chunks of the last launch, each chunk's f64 "
+                                   "tiles summed on the aux stream under the next chunk")
+            + "; allreduce_ms = the exposed tail after the last SYRK"
+            if (coll and dist.rccl and (args.grm_overlap_parts > 1 or not f32)) else None,
             "trace_K": r["trace"], "roofline": roof}
 
 

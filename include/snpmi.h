@@ -215,6 +215,11 @@ int snpmi_grm_add_packed_f64(const uint8_t* packed, uint64_t pitch, uint64_t n_i
 int snpmi_grm_add_packed_reduce_f32(const uint8_t* packed, uint64_t pitch, uint64_t n_iid, uint64_t n_sid,
                                     int count_a1, int std_kind, double a, double b, int use_stats, float* stats,
                                     int collective, int root, int parts, void* syrk_done);
+/* f64: the groups are the int8-CRT path's residue chunks of the last launch (cut at block-column
+ * boundaries; `parts` is ignored) */
+int snpmi_grm_add_packed_reduce_f64(const uint8_t* packed, uint64_t pitch, uint64_t n_iid, uint64_t n_sid,
+                                    int count_a1, int std_kind, double a, double b, int use_stats, double* stats,
+                                    int collective, int root, int parts, void* syrk_done);
 int snpmi_grm_session_tiles(void** tiles, uint64_t* count);   /* device tiles + element count */
 /* K_out NULL: end the session without a result (a non-root rank after snpmi_rccl_reduce_sum) */
 int snpmi_grm_end(int diag_k_to_n, double* factor, void* K_out);

@@ -66,6 +66,8 @@ _SIGS = {
     "snpmi_grm_add_packed_f64": [_vp, _u64, _u64, _u64, _i32, _i32, _f64, _f64, _i32, _vp],
     "snpmi_grm_add_packed_reduce_f32": [_vp, _u64, _u64, _u64, _i32, _i32, _f64, _f64, _i32, _vp, _i32, _i32, _i32,
                                         _vp],
+    "snpmi_grm_add_packed_reduce_f64": [_vp, _u64, _u64, _u64, _i32, _i32, _f64, _f64, _i32, _vp, _i32, _i32, _i32,
+                                        _vp],
     "snpmi_grm_add_dense_f32": [_vp, _u64, _u64, _i32],
     "snpmi_grm_add_dense_f64": [_vp, _u64, _u64, _i32],
     "snpmi_grm_session_tiles": [ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_uint64)],

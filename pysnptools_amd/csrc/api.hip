@@ -1353,6 +1353,94 @@ static void grm_add_packed_reduce_impl(const uint8_t* packed, uint64_t pitch, ui
     }
     for (hipEvent_t e : evs) SNPMI_HIP(hipEventDestroy(e));
 }
+// f64 form of grm_add_packed_reduce_impl: the groups are the CRT path's residue chunks of the last
+// SNP chunk (launch_syrk_packed_crt cuts them at block-column boundaries when given after_chunk;
+// ~5 at 50k iids, so no extra launch boundary), each chunk's f64 tiles summed on the aux stream
+// as soon as its CRT reconstruction is done.  The f64-MFMA fallback of a non-finite LUT (gated on
+// the device flag) runs before the chunks, so every sum sees final tiles.
+static void grm_add_packed_reduce_f64_impl(const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m,
+                                           int count_a1, int std_kind, double a, double b, int use_stats,
+                                           double* stats, int collective, int root, hipEvent_t syrk_done) {
+    std::lock_guard<std::recursive_mutex> lk(g_call_mutex);
+    SNPMI_REQUIRE(g_session.active, SNPMI_E_ARG, "no GRM session (call snpmi_grm_begin)");
+    SNPMI_REQUIRE(g_session.dtype == SNPMI_DT_F64, SNPMI_E_ARG, "dtype differs from snpmi_grm_begin");
+    SNPMI_REQUIRE(collective >= 0 && collective <= 2, SNPMI_E_ARG, "collective must be 0 (none), 1 (reduce), 2 (all-reduce)");
+    SNPMI_REQUIRE(collective == 0 || rccl_ready(), SNPMI_E_ARG, "RCCL communicator not initialised");
+    Device& d = device();
+    const uint64_t count = n_tiles_upper(g_session.n) * kTile * kTile;
+    const int rt = collective == 1 ? root : -1;
+    const uint64_t nchunk = m ? ceil_div(m, 1ull << 16) : 1;
+    const uint64_t step = std::min<uint64_t>(1ull << 16, round_up(ceil_div(m, nchunk), 256));
+    const bool grouped = m > 0 && n > 0 && n == g_session.n && use_crt(SNPMI_DT_F64) && step <= crt_max_snps() &&
+                         (std_kind == SNPMI_STD_NONE || (stats && is_device_ptr(d, stats)));
+    g_last_groups = 1;
+    if (!grouped) {
+        grm_add_packed_impl<double>(packed, pitch, n, m, count_a1, std_kind, a, b, use_stats, stats);
+        double* t = (double*)session_tiles(d);
+        if (!g_session.wrote) {
+            SNPMI_HIP(hipMemsetAsync(t, 0, count * sizeof(double), d.stream));
+            g_session.wrote = true;
+        }
+        if (syrk_done) SNPMI_HIP(hipEventRecord(syrk_done, d.stream));
+        if (collective) rccl_sum_on(t, count, SNPMI_DT_F64, rt, d.stream);
+        return;
+    }
+    SNPMI_REQUIRE(pitch % 64 == 0 && pitch >= ceil_div(n, 4), SNPMI_E_ARG, "pitch must be snpmi_packed_pitch");
+    SNPMI_REQUIRE(std_kind >= SNPMI_STD_NONE && std_kind <= SNPMI_STD_BETA, SNPMI_E_ARG, "bad standardizer kind");
+    SNPMI_REQUIRE(packed != nullptr && is_device_ptr(d, packed), SNPMI_E_ARG,
+                  "packed must be device memory of the current device");
+    const uint64_t s_last = ((m - 1) / step) * step;
+    if (s_last > 0)
+        grm_add_packed_impl<double>(packed, pitch, n, s_last, count_a1, std_kind, a, b, use_stats, stats);
+    double* tiles = (double*)session_tiles(d);
+    const int acc = g_session.wrote ? 1 : 0;
+    const uint64_t cnt = m - s_last;
+    const uint8_t* src = packed + s_last * pitch;
+    double* lut = (double*)d.get(Device::S_LUT, cnt * 4 * sizeof(double));
+    launch_snp_stats(src, pitch, n, cnt, count_a1, std_kind, a, b, use_stats, SNPMI_DT_F64,
+                     stats ? stats + 2 * s_last : (double*)d.get(Device::S_STATS, cnt * 2 * sizeof(double)), lut,
+                     d.stream);
+    g_session.wrote = true;
+    const uint64_t nb = ceil_div(n, 256);
+    const uint64_t res_bytes = std::min<uint64_t>(nb * (nb + 1) / 2 * (uint64_t)crt_moduli() * 65536, 4ull << 30);
+    uint8_t* res = (uint8_t*)d.get(Device::S_ZBLK, res_bytes);
+    void* ws = d.get(Device::S_LUT3, crt_lut_bytes(cnt, n));
+    unsigned long long* rec = crt_record(d);
+    const uint64_t nt = n_tiles_1d(n);
+    auto T = [&](uint64_t t) { t = std::min(t, nt); return t * (t + 1) / 2 * (uint64_t)(kTile * kTile); };
+    std::vector<hipEvent_t> evs;
+    int groups = 0;
+    const std::function<void()> pre = [&] {
+        launch_syrk_packed_f64_gated(src, pitch, n, cnt, lut, tiles, acc, (const int*)ws + 1, d.stream);
+    };
+    const std::function<void(uint64_t, uint64_t)> after = [&](uint64_t c0, uint64_t c1) {
+        groups++;
+        if (!collective) return;
+        hipEvent_t e;
+        SNPMI_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        evs.push_back(e);
+        SNPMI_HIP(hipEventRecord(e, d.stream));
+        SNPMI_HIP(hipStreamWaitEvent(d.aux, e, 0));
+        const uint64_t e0 = T(2 * c0), e1 = T(2 * c1);
+        if (e1 > e0) rccl_sum_on(tiles + e0, e1 - e0, SNPMI_DT_F64, rt, d.aux);
+    };
+    try {
+        launch_syrk_packed_crt(src, pitch, n, cnt, lut, tiles, acc, ws, res, res_bytes, rec, d.stream, &pre, &after);
+        g_last_groups = groups;
+        if (syrk_done) SNPMI_HIP(hipEventRecord(syrk_done, d.stream));
+        if (collective) {
+            hipEvent_t e;
+            SNPMI_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            evs.push_back(e);
+            SNPMI_HIP(hipEventRecord(e, d.aux));
+            SNPMI_HIP(hipStreamWaitEvent(d.stream, e, 0));
+        }
+    } catch (...) {
+        for (hipEvent_t e : evs) (void)hipEventDestroy(e);
+        throw;
+    }
+    for (hipEvent_t e : evs) SNPMI_HIP(hipEventDestroy(e));
+}
 }  // namespace snpmi
 
 // ====================================================================== exported C ABI
@@ -1575,6 +1663,16 @@ int snpmi_grm_add_packed_reduce_f32(const uint8_t* packed, uint64_t pitch, uint6
     return guarded([&] {
         grm_add_packed_reduce_impl(packed, pitch, n_iid, n_sid, count_a1, std_kind, a, b, use_stats, stats, collective,
                                    root, parts, (hipEvent_t)syrk_done);
+    });
+}
+
+int snpmi_grm_add_packed_reduce_f64(const uint8_t* packed, uint64_t pitch, uint64_t n_iid, uint64_t n_sid,
+                                    int count_a1, int std_kind, double a, double b, int use_stats, double* stats,
+                                    int collective, int root, int parts, void* syrk_done) {
+    (void)parts;  // the CRT path's own residue chunks are the groups
+    return guarded([&] {
+        grm_add_packed_reduce_f64_impl(packed, pitch, n_iid, n_sid, count_a1, std_kind, a, b, use_stats, stats,
+                                       collective, root, (hipEvent_t)syrk_done);
     });
 }
 

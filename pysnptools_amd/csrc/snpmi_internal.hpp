@@ -4,6 +4,7 @@
 
 #include <cstdint>
 #include <cstring>
+#include <functional>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -246,9 +247,15 @@ int crt_moduli();
 uint64_t crt_max_snps();
 uint64_t crt_lut_bytes(uint64_t m, uint64_t n);
 int crt_fraction_bits(uint64_t m);
+// before_chunks (optional) is enqueued after the per-launch bound/moduli kernels and before the
+// first residue chunk; after_chunk(c0, c1) (optional) after the chunk whose blocks are the whole
+// block columns [c0, c1) (chunks are then cut at column boundaries, so each one's tiles are one
+// contiguous range): the overlapped collective of api.hip grm_add_packed_reduce.
 void launch_syrk_packed_crt(const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m, const double* lut,
                             double* tiles, int accumulate, void* ws_lut, uint8_t* res, uint64_t res_bytes,
-                            unsigned long long* rec, hipStream_t st);
+                            unsigned long long* rec, hipStream_t st,
+                            const std::function<void()>* before_chunks = nullptr,
+                            const std::function<void(uint64_t, uint64_t)>* after_chunk = nullptr);
 // the f64-MFMA packed SYRK, run only when the device word *gate is non-zero (the CRT path's flag)
 void launch_syrk_packed_f64_gated(const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m, const double* lut,
                                   double* tiles, int accumulate, const int* gate, hipStream_t st);

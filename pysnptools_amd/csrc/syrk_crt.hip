@@ -639,7 +639,8 @@ static CrtLog crt_logs() {
 // scratch (>= kR * 65536); gate: device u32 set when the block must run on the f64 MFMA instead
 void launch_syrk_packed_crt(const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m, const double* lut,
                             double* tiles, int accumulate, void* ws_lut, uint8_t* res, uint64_t res_bytes,
-                            unsigned long long* rec, hipStream_t st) {
+                            unsigned long long* rec, hipStream_t st, const std::function<void()>* before_chunks,
+                            const std::function<void(uint64_t, uint64_t)>* after_chunk) {
     SNPMI_REQUIRE(m > 0 && m <= crt_max_snps(), SNPMI_E_ARG, "crt SYRK: SNP count per launch out of range");
     const uint64_t nb = ceil_div(n, BW), total = nb * (nb + 1) / 2;
     const uint64_t mpad = round_up(m, SK);
@@ -657,8 +658,17 @@ void launch_syrk_packed_crt(const uint8_t* packed, uint64_t pitch, uint64_t n, u
     k_crt_r<<<1, 1024, 0, st>>>(S, n, logs, ctl, rec);
     const uint64_t per = std::max<uint64_t>(1, res_bytes / ((uint64_t)kR * BW * BW));
     static const CrtConst cc = crt_constants();
-    for (uint64_t b0 = 0; b0 < total; b0 += per) {
-        const uint64_t cnt = std::min(per, total - b0);
+    if (before_chunks) (*before_chunks)();
+    uint64_t col = 0;  // after_chunk: chunks end at block-column boundaries (block column c ends at (c+1)(c+2)/2)
+    for (uint64_t b0 = 0, cnt = 0; b0 < total; b0 += cnt) {
+        cnt = std::min(per, total - b0);
+        uint64_t col1 = col;
+        if (after_chunk) {
+            while (col1 < nb && (col1 + 1) * (col1 + 2) / 2 <= b0 + cnt) col1++;
+            if (col1 == col) col1 = col + 1;  // one column at least (<= nb <= per blocks in practice)
+            cnt = col1 * (col1 + 1) / 2 - b0;
+            SNPMI_REQUIRE(cnt <= per, SNPMI_E_ARG, "crt SYRK: one block column exceeds the residue scratch");
+        }
         SNPMI_REQUIRE(cnt < (1ull << 23), SNPMI_E_ARG, "crt SYRK: chunk too large");
 #ifdef SNPMI_UBENCH
         if (g_variant_syrk == 72)  // 64-SNP stages (73.7 KiB of LDS)
@@ -679,6 +689,11 @@ void launch_syrk_packed_crt(const uint8_t* packed, uint64_t pitch, uint64_t n, u
 #endif
         k_syrk_i8r<SK><<<dim3((unsigned)cnt, kR), 512, 0, st>>>(packed, pitch, m, mpad, lutr, ctl, b0, cnt, res);
         k_crt<<<(unsigned)(cnt * 64), 256, 0, st>>>(res, b0, cnt, n, ctl, F, cc, tiles, accumulate);
+        if (after_chunk) {
+            SNPMI_HIP(hipGetLastError());
+            (*after_chunk)(col, col1);
+            col = col1;
+        }
     }
     SNPMI_HIP(hipGetLastError());
 }

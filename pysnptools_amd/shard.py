@@ -126,19 +126,19 @@ class ShardedGrm(object):
 
     def add_packed_combine(self, packed, pitch, n_sid, kind, a, b, use_stats, stats, count_a1=False, parts=2,
                            syrk_done=None):
-        """``add_packed`` of this rank's LAST SNPs + ``combine``, overlapped when a real RCCL
-        communicator and an f32 session allow it (``snpmi_grm_add_packed_reduce_f32``: the last
-        SYRK launch runs as ``parts`` column groups of the triangle and each finished group's tiles
-        are summed over the ranks on the aux stream under the next group's SYRK; the same K bit for
-        bit).  ``stats`` must then be device memory.  Otherwise the two calls run one after the
-        other (the host rehearsal group, f64, no collective).  ``syrk_done``: optional event
+        """``add_packed`` of this rank's LAST SNPs + ``combine``, overlapped under a real RCCL
+        communicator (``snpmi_grm_add_packed_reduce_f32/f64``: f32 runs the last SYRK launch as
+        ``parts`` column groups of the triangle, f64 uses the CRT path's residue chunks; each
+        finished group's tiles are summed over the ranks on the aux stream under the next group's
+        work; the same K bit for bit).  ``stats`` must then be device memory.  Otherwise the two
+        calls run one after the other (the host rehearsal group, no collective).  ``syrk_done``: optional event
         (``snpmi_event_create``) recorded after the last SYRK, for timing."""
         N = self.N
         dev_stats = isinstance(stats, ctypes.c_void_p)
-        if (self.dtype == np.float32 and self.collective != "none" and self.dist is not None and self.dist.rccl
-                and dev_stats):
-            N.call("snpmi_grm_add_packed_reduce_f32", packed, pitch, self.n, n_sid, int(bool(count_a1)), kind, a, b,
-                   int(use_stats), stats, 1 if self.collective == "reduce" else 2, self.root, int(parts), syrk_done)
+        if self.collective != "none" and self.dist is not None and self.dist.rccl and dev_stats:
+            N.call("snpmi_grm_add_packed_reduce_" + N.suffix(self.dtype), packed, pitch, self.n, n_sid,
+                   int(bool(count_a1)), kind, a, b, int(use_stats), stats, 1 if self.collective == "reduce" else 2,
+                   self.root, int(parts), syrk_done)
             return
         self.add_packed(packed, pitch, n_sid, kind, a, b, use_stats, stats, count_a1)
         if syrk_done is not None:

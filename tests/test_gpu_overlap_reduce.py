@@ -33,25 +33,25 @@ def _data(n, m, seed):
 
 def _tiles(g):
     t, count = g.tiles()
-    out = np.empty(count, dtype=np.float32)
+    out = np.empty(count, dtype=g.dtype)
     N.call("snpmi_stream_sync")
     N.call("snpmi_memcpy_d2h", N.ptr(out), t, out.nbytes)
     return out
 
 
-def _run(n, m, packed, pitch, kind, a, b, count_a1, parts, collective, dist=None, use_stats=False):
-    stats = bench.Dev(N, m * 8)
+def _run(n, m, packed, pitch, kind, a, b, count_a1, parts, collective, dist=None, use_stats=False, dtype=np.float32):
+    stats = bench.Dev(N, m * 2 * np.dtype(dtype).itemsize)
     try:
         if use_stats:  # trained stats from a first pass
-            g = ShardedGrm(n, np.float32, None, "none")
+            g = ShardedGrm(n, dtype, None, "none")
             g.add_packed(packed.p, pitch, m, kind, a, b, 0, stats.p, count_a1)
             g.abort()
-        g = ShardedGrm(n, np.float32, dist, "none" if collective is None else collective)
+        g = ShardedGrm(n, dtype, dist, "none" if collective is None else collective)
         if parts is None:
             g.add_packed(packed.p, pitch, m, kind, a, b, int(use_stats), stats.p, count_a1)
         elif collective is None:
-            N.call("snpmi_grm_add_packed_reduce_f32", packed.p, pitch, n, m, int(count_a1), kind, a, b,
-                   int(use_stats), stats.p, 0, 0, parts, None)
+            N.call("snpmi_grm_add_packed_reduce_" + N.suffix(np.dtype(dtype)), packed.p, pitch, n, m, int(count_a1),
+                   kind, a, b, int(use_stats), stats.p, 0, 0, parts, None)
         else:
             ev = ctypes.c_void_p()
             N.call("snpmi_event_create", ctypes.byref(ev))
@@ -105,4 +105,34 @@ def test_overlapped_collective_world1(rccl1, collective):
     finally:
         packed.free()
     assert N.kernel_variant("overlap_groups") == 4
+    assert np.array_equal(ref, got)
+
+
+@pytest.mark.parametrize("n,m,std", [(30000, 3000, "unit"), (20000, 70000, "beta")])
+def test_f64_crt_chunks_equal_whole_launch(n, m, std):
+    """f64: the CRT path's residue chunks cut at block-column boundaries (the overlap groups) give
+    the tiles of the plain call bit for bit (one or two SNP chunks)."""
+    kind, a, b = (N.STD_UNIT, 0.0, 0.0) if std == "unit" else (N.STD_BETA, 1.0, 25.0)
+    packed, pitch = _data(n, m, 47)
+    try:
+        ref = _run(n, m, packed, pitch, kind, a, b, False, None, None, dtype=np.float64)
+        got = _run(n, m, packed, pitch, kind, a, b, False, 2, None, dtype=np.float64)
+    finally:
+        packed.free()
+    nb = (n + 255) // 256
+    assert N.kernel_variant("overlap_groups") >= (2 if nb * (nb + 1) // 2 * 15 * 65536 > (4 << 30) else 1)
+    assert np.abs(ref).max() > 0
+    assert np.array_equal(ref, got)
+
+
+@pytest.mark.parametrize("collective", ["reduce", "allreduce"])
+def test_overlapped_collective_world1_f64(rccl1, collective):
+    n, m = 30000, 2000
+    packed, pitch = _data(n, m, 53)
+    try:
+        ref = _run(n, m, packed, pitch, N.STD_UNIT, 0.0, 0.0, False, None, None, dtype=np.float64)
+        got = _run(n, m, packed, pitch, N.STD_UNIT, 0.0, 0.0, False, 2, collective, dist=rccl1, dtype=np.float64)
+    finally:
+        packed.free()
+    assert N.kernel_variant("overlap_groups") >= 2
     assert np.array_equal(ref, got)
