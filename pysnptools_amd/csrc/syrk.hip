@@ -1228,7 +1228,14 @@ typedef _Float16 f16x8_t __attribute__((ext_vector_type(8)));
 // register set under group 2.  Runs only when *flag == 0 (see k_lut_h2).
 // DENSE: the operand is a float block already split by k_split_h2 into two fp16 planes
 // ([sid][plane][ldp], pitch = ldp elements, each 16-iid group pi-permuted), copied verbatim.
-template <bool LOCAL = false, int MODE = 4, bool DENSE = false>
+// ROT (MODE 4 only, default): the loader's ds_write_b64 stores place 8-B piece j of 16-iid group
+// d at slot (j + (d >> 2)) & 3 of the group's 32-B segment (a rotation; the other modes swap the
+// 16-B halves of groups with bit 2 set, which the 8-lane groups of ds_write_b128 need): with
+// piece j stored by instruction j, the 16 lanes of each ds_write_b64 group then hit 32 distinct
+// banks, where the swap layout left them 2-way conflicted (PMC SQ_LDS_BANK_CONFLICT = 29% of
+// SQ_LDS_IDX_ACTIVE, profiles/r04n).  The transposed fragment reads undo the rotation per lane
+// and stay conflict-free.
+template <bool LOCAL = false, int MODE = 4, bool DENSE = false, bool ROT = true>
 __global__ __launch_bounds__(512, 1) void k_syrk_h2(const uint8_t* __restrict__ P, uint64_t pitch, uint64_t n,
                                                     uint64_t kdim, const uint32_t* __restrict__ lut2,
                                                     const uint32_t* __restrict__ flag, float* __restrict__ tiles,
@@ -1282,9 +1289,16 @@ __global__ __launch_bounds__(512, 1) void k_syrk_h2(const uint8_t* __restrict__ 
     const uint32_t* lp2 = lut2 + 4 * lk;
     const uint16_t* dp = reinterpret_cast<const uint16_t*>(P) + (lp ? j0 : i0) + 16 * ld_;  // DENSE
     const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
-    const int rd_off = (8 * (g >> 1) + q) * B3_RS + 16 * (g & 1) + 4 * pp;
+    constexpr bool kRot = ROT && MODE == 4;
+    const int rd_base = (8 * (g >> 1) + q) * B3_RS + 16 * (g & 1);
+    const int rd_off = rd_base + 4 * pp;
     const int dswz = (pp >> 1) ? -8 : 8;
-    const int rd_offB = rd_off + ((wn & 1) ? dswz : 0);
+    // swap layout: A fragments x >= 2 and B fragments of odd wn sit in swapped segments;
+    // rotation layout: a fragment column c lies in segments rotated by (c / 64) & 3
+    const int rd_offA0 = kRot ? rd_base + 4 * ((pp + 2 * wm) & 3) : rd_off;
+    const int rd_offA1 = kRot ? rd_base + 4 * ((pp + 2 * wm + 1) & 3) : rd_off + dswz;
+    const int rd_offB = kRot ? rd_base + 4 * ((pp + wn) & 3) : rd_off + ((wn & 1) ? dswz : 0);
+    const int wrot = (ld_ >> 2) & 3;  // kRot: this lane's group rotation (store side)
 
     f32x16 acc[4][2];
 #pragma unroll
@@ -1359,6 +1373,13 @@ __global__ __launch_bounds__(512, 1) void k_syrk_h2(const uint8_t* __restrict__ 
             // (profiles/r03crt/ubench_lds_store_width.jsonl)
             typedef __attribute__((address_space(3))) volatile uint64_t lds_u64;
             lds_u64* q = (lds_u64*)(S + (lp * 2 + pl) * PLANE + (lk + BK * h) * B3_RS + 16 * ld_);
+            if constexpr (kRot) {
+                q[wrot] = (uint64_t)v0.x | ((uint64_t)v0.y << 32);
+                q[(wrot + 1) & 3] = (uint64_t)v0.z | ((uint64_t)v0.w << 32);
+                q[(wrot + 2) & 3] = (uint64_t)v1.x | ((uint64_t)v1.y << 32);
+                q[(wrot + 3) & 3] = (uint64_t)v1.z | ((uint64_t)v1.w << 32);
+                return;
+            }
             q[2 * sw] = (uint64_t)v0.x | ((uint64_t)v0.y << 32);
             q[2 * sw + 1] = (uint64_t)v0.z | ((uint64_t)v0.w << 32);
             q[2 * (sw ^ 1)] = (uint64_t)v1.x | ((uint64_t)v1.y << 32);
@@ -1380,7 +1401,7 @@ __global__ __launch_bounds__(512, 1) void k_syrk_h2(const uint8_t* __restrict__ 
     };
     auto fragsA = [&](const short* S, int pa, int h, f16x8_t (&a)[4]) {
 #pragma unroll
-        for (int x = 0; x < 4; x++) a[x] = frag(S, 0, pa, h, wm * 128 + 32 * x, x >= 2 ? rd_off + dswz : rd_off);
+        for (int x = 0; x < 4; x++) a[x] = frag(S, 0, pa, h, wm * 128 + 32 * x, x >= 2 ? rd_offA1 : rd_offA0);
     };
     auto group = [&](const f16x8_t (&a)[4], const f16x8_t (&b)[2]) {
 #pragma unroll
@@ -2776,6 +2797,11 @@ void launch_syrk_packed_bf3(const uint8_t* packed, uint64_t pitch, uint64_t n, u
             case 48: f32w::k_syrk_h2<false, 8><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles, accumulate); break;
             case 62: f32w::k_syrk_h2<false, 10><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles, accumulate); break;
             case 63: f32w::k_syrk_h2<false, 11><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles, accumulate); break;
+            case 64:  // A/B: MODE 4 with the round-3 swap layout of its ds_write_b64 stores
+                f32w::k_syrk_h2<false, 4, false, false><<<(unsigned)g, 512, 0, st>>>(
+                    packed, pitch, n, m, h2->lut2, h2->flag, tiles, accumulate, 0, 1, 0, 0, seg_ctx(),
+                    packed_block_order(ceil_div(n, 256)));
+                break;
             case 65:  // A/B: plain triangular block order
                 f32w::k_syrk_h2<false, 4><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles,
                                                                       accumulate, 0, 1, 0, 0, seg_ctx());
