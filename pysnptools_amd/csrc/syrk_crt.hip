@@ -198,7 +198,9 @@ __device__ __forceinline__ v2i lds_tr8(const uint8_t* p) {
 // M0 + 4 lane: 2 cycles per 256-B row vs 13 per ds_write_b128); the row's LUT word is uniform.
 // ST 1 (ubench variant 78): each 16-B residue row written as two volatile ds_write_b64 (6 cycles
 // per wave-instruction on the LDS transfer path) instead of one ds_write_b128 (13)
-template <int SKT, int ABL = 0, int LDM = 0, int ST = 0>
+// LD2 1 (ubench variant 79): two loader register sets, so each stage's code/LUT loads are issued
+// two stages before their expansion (a whole stage more latency to hide; +16 VGPRs)
+template <int SKT, int ABL = 0, int LDM = 0, int ST = 0, int LD2 = 0>
 __global__ __launch_bounds__(512, 1) void k_syrk_i8r(const uint8_t* __restrict__ P, uint64_t pitch, uint64_t kdim,
                                                      uint64_t mpad, const uint32_t* __restrict__ lutr,
                                                      const int* __restrict__ ctl, uint64_t b0, uint64_t nblk,
@@ -232,21 +234,22 @@ __global__ __launch_bounds__(512, 1) void k_syrk_i8r(const uint8_t* __restrict__
         for (int y = 0; y < 2; y++) acc[x][y] = (v16i){};
     const uint64_t nst = (kdim + SKT - 1) / SKT;
 
-    uint32_t cw[RPT];
-    uint4 cl[RPT / 4];
-    auto load = [&](uint64_t st) {
+    uint32_t cw[RPT], cw2[LD2 ? RPT : 1];
+    uint4 cl[RPT / 4], cl2[LD2 ? RPT / 4 : 1];
+    auto load_into = [&](uint64_t st, uint32_t* w, uint4* l) {
         const uint8_t* sb = pbase + st * SKT * pitch;
         const uint32_t lim = (uint32_t)(kdim - 1 - st * SKT);  // st < nst: >= 0
 #pragma unroll
         for (int h = 0; h < RPT; h++) {
             const uint32_t row = min((uint32_t)(RPT * kq + h), lim);
-            cw[h] = *reinterpret_cast<const uint32_t*>(sb + (row * pit + 4 * d));
+            w[h] = *reinterpret_cast<const uint32_t*>(sb + (row * pit + 4 * d));
         }
 #pragma unroll
         for (int u = 0; u < RPT / 4; u++)  // lutr is zero-padded to mpad >= nst * SKT
-            cl[u] = *reinterpret_cast<const uint4*>(lq + SKT * st + 4 * u);
+            l[u] = *reinterpret_cast<const uint4*>(lq + SKT * st + 4 * u);
     };
-    auto store = [&](uint8_t* S, int h0, int h1) {
+    auto load = [&](uint64_t st) { load_into(st, cw, cl); };
+    auto store_from = [&](uint8_t* S, int h0, int h1, const uint32_t* cw, const uint4* cl) {
 #pragma unroll
         for (int h = h0; h < h1; h++) {
             const uint4 c4 = cl[h >> 2];
@@ -266,6 +269,7 @@ __global__ __launch_bounds__(512, 1) void k_syrk_i8r(const uint8_t* __restrict__
             }
         }
     };
+    auto store = [&](uint8_t* S, int h0, int h1) { store_from(S, h0, h1, cw, cl); };
     auto frag = [&](const uint8_t* S, int panel, int ks, int col) -> v4i {
         const uint8_t* b = S + panel * PNL + 32 * ks * RS + rd + col;
         const v2i x = lds_tr8(b), y = lds_tr8(b + 8 * RS);
@@ -309,6 +313,38 @@ __global__ __launch_bounds__(512, 1) void k_syrk_i8r(const uint8_t* __restrict__
         }
     };
 
+    if constexpr (LD2 == 1) {
+        // invariant: during stage s the set holding stage s+1 is expanded into the idle buffer,
+        // then refilled with stage s+3 (clamped); the other set already holds stage s+2
+        load(0);
+        store(lds, 0, RPT);
+        load_into(nst > 1 ? 1 : 0, cw2, cl2);
+        load_into(nst > 2 ? 2 : nst - 1, cw, cl);
+        __syncthreads();
+        auto body = [&](uint64_t s, uint32_t* w, uint4* l) {
+            const uint8_t* cur = lds + (s & 1) * STG;
+            uint8_t* nxt = lds + ((s + 1) & 1) * STG;
+            v4i a[2][4], b[2][2];
+            frags(cur, 0, a[0], b[0]);
+#pragma unroll
+            for (int ks = 0; ks < KS; ks++) {
+                if (ks + 1 < KS) frags(cur, ks + 1, a[(ks + 1) & 1], b[(ks + 1) & 1]);
+#pragma unroll
+                for (int x = 0; x < 4; x++)
+#pragma unroll
+                    for (int y = 0; y < 2; y++)
+                        acc[x][y] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[ks & 1][x], b[ks & 1][y], acc[x][y], 0, 0, 0);
+                store_from(nxt, ks * RPT / KS, (ks + 1) * RPT / KS, w, l);
+            }
+            load_into(s + 3 < nst ? s + 3 : nst - 1, w, l);
+            __syncthreads();
+        };
+        for (uint64_t s = 0; s < nst; s += 2) {
+            body(s, cw2, cl2);
+            if (s + 1 < nst) body(s + 1, cw, cl);
+        }
+    }
+    if constexpr (LD2 == 0) {  // one loader register set: stage s+2's loads issued at the end of stage s
     if constexpr (LDM == 1) {
         load1(0);
         store1(lds, 0, RPW);
@@ -354,6 +390,7 @@ __global__ __launch_bounds__(512, 1) void k_syrk_i8r(const uint8_t* __restrict__
         }
         __syncthreads();
     }
+    }  // LD2 == 0
     // epilogue: acc mod p -> [0, p), one byte per element at its true (row, col) in the block
     const int p = kMod[r];
     const double invp = 1.0 / (double)p;
@@ -683,6 +720,8 @@ void launch_syrk_packed_crt(const uint8_t* packed, uint64_t pitch, uint64_t n, u
             k_syrk_i8r<SK, 0, 0, 1><<<dim3((unsigned)cnt, kR), 512, 0, st>>>(packed, pitch, m, mpad, lutr, ctl, b0, cnt, res);
         else if (g_variant_syrk == 77)  // 4 waves, one per SIMD, 128 x 128 per wave
             k_syrk_i8w<SK><<<dim3((unsigned)cnt, kR), 256, 0, st>>>(packed, pitch, m, mpad, lutr, ctl, b0, cnt, res);
+        else if (g_variant_syrk == 79)  // two loader register sets: loads two stages ahead
+            k_syrk_i8r<SK, 0, 0, 0, 1><<<dim3((unsigned)cnt, kR), 512, 0, st>>>(packed, pitch, m, mpad, lutr, ctl, b0, cnt, res);
         else if (g_variant_syrk == 74)  // ablation: fragments read once per stage
             k_syrk_i8r<SK, 2><<<dim3((unsigned)cnt, kR), 512, 0, st>>>(packed, pitch, m, mpad, lutr, ctl, b0, cnt, res);
         else
