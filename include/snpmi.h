@@ -208,8 +208,8 @@ int snpmi_grm_add_packed_f64(const uint8_t* packed, uint64_t pitch, uint64_t n_i
  * GRM (snpmi_rccl_reduce_sum / _allreduce_sum; collective 1 = reduce onto root, 2 = all-reduce,
  * 0 = none), overlapped: the last SNP chunk's SYRK runs as `parts` column groups of the triangle
  * (same K bit for bit) and each finished group's contiguous tile range is summed on the aux stream
- * under the next group's SYRK; the compute stream waits for the last sum.  stats must be device
- * memory (or NULL for Identity).  syrk_done (optional hipEvent_t from snpmi_event_create) is
+ * under the next group's SYRK; the compute stream waits for the last sum.  Host stats (or a path
+ * without column groups) run the add and then the collective, unoverlapped.  syrk_done (optional hipEvent_t from snpmi_event_create) is
  * recorded after the last group's SYRK.  Replaces the add + reduce pair of shard.ShardedGrm
  * (the rank loop of snpreader.py:651-655 followed by the sum over ranks). */
 int snpmi_grm_add_packed_reduce_f32(const uint8_t* packed, uint64_t pitch, uint64_t n_iid, uint64_t n_sid,

@@ -1279,7 +1279,8 @@ static void grm_add_packed_reduce_impl(const uint8_t* packed, uint64_t pitch, ui
     const uint64_t nb = ceil_div(n, 256);
     const bool grouped = m > 0 && n > 0 && n == g_session.n && use_bf3(SNPMI_DT_F32) && use_h2() && g_diag_exact &&
                          bf3_split_slices(n, std::min<uint64_t>(m, 1ull << 16), d.cu_count) == 1 &&
-                         nb < 65536 && parts > 1;
+                         nb < 65536 && parts > 1 &&
+                         (std_kind == SNPMI_STD_NONE || (stats && is_device_ptr(d, stats)));
     g_last_groups = 1;
     if (!grouped) {
         grm_add_packed_impl<float>(packed, pitch, n, m, count_a1, std_kind, a, b, use_stats, stats);
@@ -1297,8 +1298,6 @@ static void grm_add_packed_reduce_impl(const uint8_t* packed, uint64_t pitch, ui
     SNPMI_REQUIRE(stats != nullptr || std_kind == SNPMI_STD_NONE, SNPMI_E_ARG, "stats is NULL");
     SNPMI_REQUIRE(packed != nullptr && is_device_ptr(d, packed), SNPMI_E_ARG,
                   "packed must be device memory of the current device");
-    SNPMI_REQUIRE(std_kind == SNPMI_STD_NONE || is_device_ptr(d, stats), SNPMI_E_ARG,
-                  "stats must be device memory for the overlapped collective");
     // the chunks before the last one: the plain session path (same chunking as grm_add_packed_impl)
     const uint64_t nchunk = ceil_div(m, 1ull << 16);
     const uint64_t step = std::min<uint64_t>(1ull << 16, round_up(ceil_div(m, nchunk), 256));
