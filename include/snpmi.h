@@ -192,6 +192,18 @@ int snpmi_grm_add_bed_f64(const char* path, uint64_t n_iid, uint64_t n_sid, int 
                           const uint64_t* iid_idx, uint64_t n_out_iid, const uint64_t* sid_idx,
                           uint64_t n_out_sid, int std_kind, double a, double b, int use_stats,
                           double* stats, int num_threads);
+/* snpmi_grm_add_bed_{f32,f64} as the session's LAST add (a rank's SNP span of a .bed) + the K-tile
+ * collective (1 = reduce onto root, 2 = all-reduce, 0 = none), overlapped on the file stream's last
+ * chunk as in snpmi_grm_add_packed_reduce_*: shard.grm_sharded under RCCL (snpreader.py:623-668
+ * per rank, then the sum over ranks).  Same K bit for bit as the add followed by the collective. */
+int snpmi_grm_add_bed_reduce_f32(const char* path, uint64_t n_iid, uint64_t n_sid, int count_a1, const uint64_t* iid_idx,
+                                 uint64_t n_out_iid, const uint64_t* sid_idx, uint64_t n_out_sid, int std_kind,
+                                 double a, double b, int use_stats, float* stats, int num_threads, int collective,
+                                 int root, int parts);
+int snpmi_grm_add_bed_reduce_f64(const char* path, uint64_t n_iid, uint64_t n_sid, int count_a1, const uint64_t* iid_idx,
+                                 uint64_t n_out_iid, const uint64_t* sid_idx, uint64_t n_out_sid, int std_kind,
+                                 double a, double b, int use_stats, double* stats, int num_threads, int collective,
+                                 int root, int parts);
 /* add Z Z^T of an already standardized rows x cols block (F or C order) to the session */
 int snpmi_grm_add_dense_f32(const float* val, uint64_t rows, uint64_t cols, int order_c);
 int snpmi_grm_add_dense_f64(const double* val, uint64_t rows, uint64_t cols, int order_c);

@@ -62,6 +62,10 @@ _SIGS = {
     "snpmi_grm_begin": [_u64, _i32],
     "snpmi_grm_add_bed_f32": [_cp, _u64, _u64, _i32, _vp, _u64, _vp, _u64, _i32, _f64, _f64, _i32, _vp, _i32],
     "snpmi_grm_add_bed_f64": [_cp, _u64, _u64, _i32, _vp, _u64, _vp, _u64, _i32, _f64, _f64, _i32, _vp, _i32],
+    "snpmi_grm_add_bed_reduce_f32": [_cp, _u64, _u64, _i32, _vp, _u64, _vp, _u64, _i32, _f64, _f64, _i32, _vp, _i32,
+                                     _i32, _i32, _i32],
+    "snpmi_grm_add_bed_reduce_f64": [_cp, _u64, _u64, _i32, _vp, _u64, _vp, _u64, _i32, _f64, _f64, _i32, _vp, _i32,
+                                     _i32, _i32, _i32],
     "snpmi_grm_add_packed_f32": [_vp, _u64, _u64, _u64, _i32, _i32, _f64, _f64, _i32, _vp],
     "snpmi_grm_add_packed_f64": [_vp, _u64, _u64, _u64, _i32, _i32, _f64, _f64, _i32, _vp],
     "snpmi_grm_add_packed_reduce_f32": [_vp, _u64, _u64, _u64, _i32, _i32, _f64, _f64, _i32, _vp, _i32, _i32, _i32,

@@ -23,6 +23,8 @@
 
 #include "snpmi_internal.hpp"
 
+#include <type_traits>
+
 namespace snpmi {
 
 // ====================================================================== errors / devices
@@ -1262,183 +1264,217 @@ static std::vector<ColGroup> column_groups(uint64_t nb, int parts) {
 // sum before the call returns, so later work sees the combined K.  Paths without column groups
 // (split-K grids, the tuning variants, the f32 MFMA fallbacks) run the SYRK whole and sum after it.
 // syrk_done (optional hipEvent_t) is recorded on the compute stream after the last group's SYRK.
-static int g_last_groups = 0;  // column groups of the last grm_add_packed_reduce (read-only hook "overlap_groups")
+static int g_last_groups = 0;  // column groups of the last overlapped collective (read-only hook "overlap_groups")
 
-static void grm_add_packed_reduce_impl(const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m, int count_a1,
-                                       int std_kind, double a, double b, int use_stats, float* stats, int collective,
-                                       int root, int parts, hipEvent_t syrk_done) {
-    std::lock_guard<std::recursive_mutex> lk(g_call_mutex);
-    SNPMI_REQUIRE(g_session.active, SNPMI_E_ARG, "no GRM session (call snpmi_grm_begin)");
-    SNPMI_REQUIRE(g_session.dtype == SNPMI_DT_F32, SNPMI_E_ARG, "the overlapped collective is for f32 sessions");
-    SNPMI_REQUIRE(collective >= 0 && collective <= 2, SNPMI_E_ARG, "collective must be 0 (none), 1 (reduce), 2 (all-reduce)");
-    SNPMI_REQUIRE(collective == 0 || rccl_ready(), SNPMI_E_ARG, "RCCL communicator not initialised");
-    SNPMI_REQUIRE(parts >= 1, SNPMI_E_ARG, "parts must be >= 1");
-    Device& d = device();
-    const uint64_t count = n_tiles_upper(g_session.n) * kTile * kTile;
-    const int rt = collective == 1 ? root : -1;
-    const uint64_t nb = ceil_div(n, 256);
-    const bool grouped = m > 0 && n > 0 && n == g_session.n && use_bf3(SNPMI_DT_F32) && use_h2() && g_diag_exact &&
-                         bf3_split_slices(n, std::min<uint64_t>(m, 1ull << 16), d.cu_count) == 1 &&
-                         nb < 65536 && parts > 1 &&
-                         (std_kind == SNPMI_STD_NONE || (stats && is_device_ptr(d, stats)));
-    g_last_groups = 1;
-    if (!grouped) {
-        grm_add_packed_impl<float>(packed, pitch, n, m, count_a1, std_kind, a, b, use_stats, stats);
-        float* t = (float*)session_tiles(d);
-        if (!g_session.wrote) {  // no SNPs on this rank: it contributes zeros
-            SNPMI_HIP(hipMemsetAsync(t, 0, count * sizeof(float), d.stream));
-            g_session.wrote = true;
-        }
-        if (syrk_done) SNPMI_HIP(hipEventRecord(syrk_done, d.stream));
-        if (collective) rccl_sum_on(t, count, SNPMI_DT_F32, rt, d.stream);
-        return;
+// Events of one overlapped collective: compute-stream events the aux stream waits on before each
+// group's sum, then one aux event the compute stream waits on; destroyed at the end.
+struct OverlapSums {
+    Device& d;
+    int collective, root, dtype;
+    std::vector<hipEvent_t> evs;
+    OverlapSums(Device& dev, int coll, int rt, int dt) : d(dev), collective(coll), root(rt), dtype(dt) {}
+    ~OverlapSums() {
+        for (hipEvent_t e : evs) (void)hipEventDestroy(e);
     }
-    SNPMI_REQUIRE(pitch % 64 == 0 && pitch >= ceil_div(n, 4), SNPMI_E_ARG, "pitch must be snpmi_packed_pitch");
-    SNPMI_REQUIRE(std_kind >= SNPMI_STD_NONE && std_kind <= SNPMI_STD_BETA, SNPMI_E_ARG, "bad standardizer kind");
-    SNPMI_REQUIRE(stats != nullptr || std_kind == SNPMI_STD_NONE, SNPMI_E_ARG, "stats is NULL");
-    SNPMI_REQUIRE(packed != nullptr && is_device_ptr(d, packed), SNPMI_E_ARG,
-                  "packed must be device memory of the current device");
-    // the chunks before the last one: the plain session path (same chunking as grm_add_packed_impl)
-    const uint64_t nchunk = ceil_div(m, 1ull << 16);
-    const uint64_t step = std::min<uint64_t>(1ull << 16, round_up(ceil_div(m, nchunk), 256));
-    const uint64_t s_last = ((m - 1) / step) * step;
-    if (s_last > 0)
-        grm_add_packed_impl<float>(packed, pitch, n, s_last, count_a1, std_kind, a, b, use_stats, stats);
-    float* tiles = (float*)session_tiles(d);
-    const int acc = g_session.wrote ? 1 : 0;
-    const uint64_t cnt = m - s_last;
-    const uint8_t* src = packed + s_last * pitch;
-    float* lut = (float*)d.get(Device::S_LUT, cnt * 4 * sizeof(float));
-    launch_snp_stats(src, pitch, n, cnt, count_a1, std_kind, a, b, use_stats, SNPMI_DT_F32,
-                     stats ? stats + 2 * s_last : (float*)d.get(Device::S_STATS, cnt * 2 * sizeof(float)), lut,
-                     d.stream);
+    hipEvent_t event() {
+        hipEvent_t e;
+        SNPMI_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        evs.push_back(e);
+        return e;
+    }
+    // the tiles of 128-tile columns [t0, t1) are final on the compute stream: sum them on aux
+    void range(void* tiles, uint64_t n, uint64_t t0, uint64_t t1) {
+        if (!collective) return;
+        const uint64_t nt = n_tiles_1d(n);
+        auto T = [&](uint64_t t) { t = std::min(t, nt); return t * (t + 1) / 2 * (uint64_t)(kTile * kTile); };
+        const uint64_t e0 = T(t0), e1 = T(t1);
+        if (e1 <= e0) return;
+        hipEvent_t e = event();
+        SNPMI_HIP(hipEventRecord(e, d.stream));
+        SNPMI_HIP(hipStreamWaitEvent(d.aux, e, 0));
+        rccl_sum_on((uint8_t*)tiles + e0 * dtype_size(dtype), e1 - e0, dtype, root, d.aux);
+    }
+    void join() {
+        if (!collective) return;
+        hipEvent_t e = event();
+        SNPMI_HIP(hipEventRecord(e, d.aux));
+        SNPMI_HIP(hipStreamWaitEvent(d.stream, e, 0));
+    }
+};
+
+// The overlapped last SYRK of an f32 GRM: `cnt` SNPs (device codes + f32 LUT) added into `tiles`
+// in column groups (launch_syrk_packed_h2_cols, K bit-identical to one launch) with the exact
+// diagonal written back per group, each group's tiles summed over the ranks on the aux stream
+// under the next group's SYRK.  Returns the group count.
+static bool f32_groupable(Device& d, uint64_t n, uint64_t cnt, int parts) {
+    return cnt > 0 && n > 0 && use_bf3(SNPMI_DT_F32) && use_h2() && g_diag_exact && parts > 1 &&
+           bf3_split_slices(n, std::min<uint64_t>(cnt, 1ull << 16), d.cu_count) == 1 && ceil_div(n, 256) < 65536;
+}
+static int grouped_reduce_f32(Device& d, const uint8_t* src, uint64_t pitch, uint64_t n, uint64_t cnt,
+                              const float* lut, float* tiles, int acc, int collective, int rt, int parts,
+                              hipEvent_t syrk_done) {
     H2Lut h2;
     const uint32_t* l3 = lut_bf3(d, lut, cnt, &h2);
     double* diag = (double*)d.get(Device::S_DIAG, n * sizeof(double));
     launch_diag_begin(tiles, n, 0, 0, acc, diag, d.stream);
     launch_diag_sq(src, pitch, n, cnt, lut, diag, d.stream);
-    g_session.wrote = true;
-    const auto groups = column_groups(nb, parts);
-    g_last_groups = (int)groups.size();
-    const uint64_t nt = n_tiles_1d(n);
-    auto T = [&](uint64_t t) { t = std::min(t, nt); return t * (t + 1) / 2 * (uint64_t)(kTile * kTile); };
-    std::vector<hipEvent_t> evs;
-    try {
-        for (const auto& gr : groups) {
-            launch_syrk_packed_h2_cols(src, pitch, n, cnt, l3, tiles, acc, d.stream, &h2, gr.L0, gr.L1);
-            // block columns [c0, c1): diagonal iids [256 c0, 256 c1), 128-tile columns [2 c0, 2 c1)
-            const uint64_t c0 = gr.c0, c1 = gr.c1;
-            launch_diag_patch(tiles, n, 256 * c0, 256 * c1, 0, 0, diag, d.stream);
-            if (!collective) continue;
-            hipEvent_t e;
-            SNPMI_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-            evs.push_back(e);
-            SNPMI_HIP(hipEventRecord(e, d.stream));
-            SNPMI_HIP(hipStreamWaitEvent(d.aux, e, 0));
-            const uint64_t e0 = T(2 * c0), e1 = T(2 * c1);
-            if (e1 > e0) rccl_sum_on(tiles + e0, e1 - e0, SNPMI_DT_F32, rt, d.aux);
-        }
-        if (syrk_done) SNPMI_HIP(hipEventRecord(syrk_done, d.stream));
-        if (collective) {
-            hipEvent_t e;
-            SNPMI_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-            evs.push_back(e);
-            SNPMI_HIP(hipEventRecord(e, d.aux));
-            SNPMI_HIP(hipStreamWaitEvent(d.stream, e, 0));
-        }
-    } catch (...) {
-        for (hipEvent_t e : evs) (void)hipEventDestroy(e);
-        throw;
+    const auto groups = column_groups(ceil_div(n, 256), parts);
+    OverlapSums sums(d, collective, rt, SNPMI_DT_F32);
+    for (const auto& gr : groups) {
+        launch_syrk_packed_h2_cols(src, pitch, n, cnt, l3, tiles, acc, d.stream, &h2, gr.L0, gr.L1);
+        // block columns [c0, c1): diagonal iids [256 c0, 256 c1), 128-tile columns [2 c0, 2 c1)
+        launch_diag_patch(tiles, n, 256 * gr.c0, 256 * gr.c1, 0, 0, diag, d.stream);
+        sums.range(tiles, n, 2 * gr.c0, 2 * gr.c1);
     }
-    for (hipEvent_t e : evs) SNPMI_HIP(hipEventDestroy(e));
+    if (syrk_done) SNPMI_HIP(hipEventRecord(syrk_done, d.stream));
+    sums.join();
+    return (int)groups.size();
 }
-// f64 form of grm_add_packed_reduce_impl: the groups are the CRT path's residue chunks of the last
-// SNP chunk (launch_syrk_packed_crt cuts them at block-column boundaries when given after_chunk;
-// ~5 at 50k iids, so no extra launch boundary), each chunk's f64 tiles summed on the aux stream
-// as soon as its CRT reconstruction is done.  The f64-MFMA fallback of a non-finite LUT (gated on
-// the device flag) runs before the chunks, so every sum sees final tiles.
-static void grm_add_packed_reduce_f64_impl(const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m,
-                                           int count_a1, int std_kind, double a, double b, int use_stats,
-                                           double* stats, int collective, int root, hipEvent_t syrk_done) {
-    std::lock_guard<std::recursive_mutex> lk(g_call_mutex);
-    SNPMI_REQUIRE(g_session.active, SNPMI_E_ARG, "no GRM session (call snpmi_grm_begin)");
-    SNPMI_REQUIRE(g_session.dtype == SNPMI_DT_F64, SNPMI_E_ARG, "dtype differs from snpmi_grm_begin");
-    SNPMI_REQUIRE(collective >= 0 && collective <= 2, SNPMI_E_ARG, "collective must be 0 (none), 1 (reduce), 2 (all-reduce)");
-    SNPMI_REQUIRE(collective == 0 || rccl_ready(), SNPMI_E_ARG, "RCCL communicator not initialised");
-    Device& d = device();
-    const uint64_t count = n_tiles_upper(g_session.n) * kTile * kTile;
-    const int rt = collective == 1 ? root : -1;
-    const uint64_t nchunk = m ? ceil_div(m, 1ull << 16) : 1;
-    const uint64_t step = std::min<uint64_t>(1ull << 16, round_up(ceil_div(m, nchunk), 256));
-    const bool grouped = m > 0 && n > 0 && n == g_session.n && use_crt(SNPMI_DT_F64) && step <= crt_max_snps() &&
-                         (std_kind == SNPMI_STD_NONE || (stats && is_device_ptr(d, stats)));
-    g_last_groups = 1;
-    if (!grouped) {
-        grm_add_packed_impl<double>(packed, pitch, n, m, count_a1, std_kind, a, b, use_stats, stats);
-        double* t = (double*)session_tiles(d);
-        if (!g_session.wrote) {
-            SNPMI_HIP(hipMemsetAsync(t, 0, count * sizeof(double), d.stream));
-            g_session.wrote = true;
-        }
-        if (syrk_done) SNPMI_HIP(hipEventRecord(syrk_done, d.stream));
-        if (collective) rccl_sum_on(t, count, SNPMI_DT_F64, rt, d.stream);
-        return;
+
+// f64 counterpart: the groups are the CRT path's residue chunks of the last <= crt_max_snps() SNPs
+// (launch_syrk_packed_crt cuts them at block-column boundaries when given after_chunk; ~5 at 50k
+// iids, so no extra launch boundary), each chunk's f64 tiles summed on the aux stream once its
+// CRT reconstruction is done.  The f64-MFMA fallback of a non-finite LUT (gated on the device
+// flag) runs before the chunks, so every sum sees final tiles.
+static int crt_reduce_f64(Device& d, const uint8_t* src, uint64_t pitch, uint64_t n, uint64_t cnt, const double* lut,
+                          double* tiles, int acc, int collective, int rt, hipEvent_t syrk_done) {
+    const uint64_t step = crt_max_snps();
+    if (cnt > step) {  // the leading SNPs the plain way, the last <= step overlapped
+        const uint64_t lead = ((cnt - 1) / step) * step;
+        syrk_packed_crt(d, src, pitch, n, lead, lut, tiles, acc);
+        src += lead * pitch;
+        lut += 4 * lead;
+        cnt -= lead;
+        acc = 1;
     }
-    SNPMI_REQUIRE(pitch % 64 == 0 && pitch >= ceil_div(n, 4), SNPMI_E_ARG, "pitch must be snpmi_packed_pitch");
-    SNPMI_REQUIRE(std_kind >= SNPMI_STD_NONE && std_kind <= SNPMI_STD_BETA, SNPMI_E_ARG, "bad standardizer kind");
-    SNPMI_REQUIRE(packed != nullptr && is_device_ptr(d, packed), SNPMI_E_ARG,
-                  "packed must be device memory of the current device");
-    const uint64_t s_last = ((m - 1) / step) * step;
-    if (s_last > 0)
-        grm_add_packed_impl<double>(packed, pitch, n, s_last, count_a1, std_kind, a, b, use_stats, stats);
-    double* tiles = (double*)session_tiles(d);
-    const int acc = g_session.wrote ? 1 : 0;
-    const uint64_t cnt = m - s_last;
-    const uint8_t* src = packed + s_last * pitch;
-    double* lut = (double*)d.get(Device::S_LUT, cnt * 4 * sizeof(double));
-    launch_snp_stats(src, pitch, n, cnt, count_a1, std_kind, a, b, use_stats, SNPMI_DT_F64,
-                     stats ? stats + 2 * s_last : (double*)d.get(Device::S_STATS, cnt * 2 * sizeof(double)), lut,
-                     d.stream);
-    g_session.wrote = true;
     const uint64_t nb = ceil_div(n, 256);
     const uint64_t res_bytes = std::min<uint64_t>(nb * (nb + 1) / 2 * (uint64_t)crt_moduli() * 65536, 4ull << 30);
     uint8_t* res = (uint8_t*)d.get(Device::S_ZBLK, res_bytes);
     void* ws = d.get(Device::S_LUT3, crt_lut_bytes(cnt, n));
     unsigned long long* rec = crt_record(d);
-    const uint64_t nt = n_tiles_1d(n);
-    auto T = [&](uint64_t t) { t = std::min(t, nt); return t * (t + 1) / 2 * (uint64_t)(kTile * kTile); };
-    std::vector<hipEvent_t> evs;
+    OverlapSums sums(d, collective, rt, SNPMI_DT_F64);
     int groups = 0;
     const std::function<void()> pre = [&] {
         launch_syrk_packed_f64_gated(src, pitch, n, cnt, lut, tiles, acc, (const int*)ws + 1, d.stream);
     };
     const std::function<void(uint64_t, uint64_t)> after = [&](uint64_t c0, uint64_t c1) {
         groups++;
-        if (!collective) return;
-        hipEvent_t e;
-        SNPMI_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-        evs.push_back(e);
-        SNPMI_HIP(hipEventRecord(e, d.stream));
-        SNPMI_HIP(hipStreamWaitEvent(d.aux, e, 0));
-        const uint64_t e0 = T(2 * c0), e1 = T(2 * c1);
-        if (e1 > e0) rccl_sum_on(tiles + e0, e1 - e0, SNPMI_DT_F64, rt, d.aux);
+        sums.range(tiles, n, 2 * c0, 2 * c1);
     };
-    try {
-        launch_syrk_packed_crt(src, pitch, n, cnt, lut, tiles, acc, ws, res, res_bytes, rec, d.stream, &pre, &after);
-        g_last_groups = groups;
-        if (syrk_done) SNPMI_HIP(hipEventRecord(syrk_done, d.stream));
-        if (collective) {
-            hipEvent_t e;
-            SNPMI_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-            evs.push_back(e);
-            SNPMI_HIP(hipEventRecord(e, d.aux));
-            SNPMI_HIP(hipStreamWaitEvent(d.stream, e, 0));
-        }
-    } catch (...) {
-        for (hipEvent_t e : evs) (void)hipEventDestroy(e);
-        throw;
+    launch_syrk_packed_crt(src, pitch, n, cnt, lut, tiles, acc, ws, res, res_bytes, rec, d.stream, &pre, &after);
+    if (syrk_done) SNPMI_HIP(hipEventRecord(syrk_done, d.stream));
+    sums.join();
+    return groups;
+}
+
+// whole-buffer collective after an unoverlapped add (paths without groups); zeros if nothing was added
+template <typename T>
+static void session_sum_whole(Device& d, int collective, int rt, hipEvent_t syrk_done) {
+    T* t = (T*)session_tiles(d);
+    const uint64_t count = n_tiles_upper(g_session.n) * kTile * kTile;
+    if (!g_session.wrote) {
+        SNPMI_HIP(hipMemsetAsync(t, 0, count * sizeof(T), d.stream));
+        g_session.wrote = true;
     }
-    for (hipEvent_t e : evs) SNPMI_HIP(hipEventDestroy(e));
+    if (syrk_done) SNPMI_HIP(hipEventRecord(syrk_done, d.stream));
+    if (collective) rccl_sum_on(t, count, DT<T>::v, rt, d.stream);
+}
+
+template <typename T>
+static void check_reduce_args(int collective, int parts) {
+    SNPMI_REQUIRE(g_session.active, SNPMI_E_ARG, "no GRM session (call snpmi_grm_begin)");
+    SNPMI_REQUIRE(g_session.dtype == DT<T>::v, SNPMI_E_ARG, "dtype differs from snpmi_grm_begin");
+    SNPMI_REQUIRE(collective >= 0 && collective <= 2, SNPMI_E_ARG, "collective must be 0 (none), 1 (reduce), 2 (all-reduce)");
+    SNPMI_REQUIRE(collective == 0 || rccl_ready(), SNPMI_E_ARG, "RCCL communicator not initialised");
+    SNPMI_REQUIRE(parts >= 1, SNPMI_E_ARG, "parts must be >= 1");
+}
+
+// snpmi_grm_add_packed_{f32,f64} (the session's last add) + the K-tile collective, overlapped:
+// the last SNP chunk (same chunking as grm_add_packed_impl) runs through grouped_reduce_f32 /
+// crt_reduce_f64.  Host stats, or a path without groups, add first and sum after.
+template <typename T>
+static void grm_add_packed_reduce_impl(const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m, int count_a1,
+                                       int std_kind, double a, double b, int use_stats, T* stats, int collective,
+                                       int root, int parts, hipEvent_t syrk_done) {
+    std::lock_guard<std::recursive_mutex> lk(g_call_mutex);
+    check_reduce_args<T>(collective, parts);
+    Device& d = device();
+    const int rt = collective == 1 ? root : -1;
+    const bool f64 = DT<T>::v == SNPMI_DT_F64;
+    const uint64_t nchunk = m ? ceil_div(m, 1ull << 16) : 1;
+    const uint64_t step = std::min<uint64_t>(1ull << 16, round_up(ceil_div(m, nchunk), 256));
+    const bool grouped = m > 0 && n > 0 && n == g_session.n &&
+                         (f64 ? use_crt(SNPMI_DT_F64) : f32_groupable(d, n, std::min(m, step), parts)) &&
+                         (std_kind == SNPMI_STD_NONE || (stats && is_device_ptr(d, stats)));
+    g_last_groups = 1;
+    if (!grouped) {
+        grm_add_packed_impl<T>(packed, pitch, n, m, count_a1, std_kind, a, b, use_stats, stats);
+        session_sum_whole<T>(d, collective, rt, syrk_done);
+        return;
+    }
+    SNPMI_REQUIRE(pitch % 64 == 0 && pitch >= ceil_div(n, 4), SNPMI_E_ARG, "pitch must be snpmi_packed_pitch");
+    SNPMI_REQUIRE(std_kind >= SNPMI_STD_NONE && std_kind <= SNPMI_STD_BETA, SNPMI_E_ARG, "bad standardizer kind");
+    SNPMI_REQUIRE(packed != nullptr && is_device_ptr(d, packed), SNPMI_E_ARG,
+                  "packed must be device memory of the current device");
+    const uint64_t s_last = ((m - 1) / step) * step;
+    if (s_last > 0) grm_add_packed_impl<T>(packed, pitch, n, s_last, count_a1, std_kind, a, b, use_stats, stats);
+    T* tiles = (T*)session_tiles(d);
+    const int acc = g_session.wrote ? 1 : 0;
+    const uint64_t cnt = m - s_last;
+    const uint8_t* src = packed + s_last * pitch;
+    T* lut = (T*)d.get(Device::S_LUT, cnt * 4 * sizeof(T));
+    launch_snp_stats(src, pitch, n, cnt, count_a1, std_kind, a, b, use_stats, DT<T>::v,
+                     stats ? stats + 2 * s_last : (T*)d.get(Device::S_STATS, cnt * 2 * sizeof(T)), lut, d.stream);
+    g_session.wrote = true;
+    if constexpr (std::is_same<T, double>::value)
+        g_last_groups = crt_reduce_f64(d, src, pitch, n, cnt, lut, tiles, acc, collective, rt, syrk_done);
+    else
+        g_last_groups = grouped_reduce_f32(d, src, pitch, n, cnt, lut, tiles, acc, collective, rt, parts, syrk_done);
+}
+
+// snpmi_grm_add_bed_{f32,f64} (the session's last add: a rank's SNP span of a .bed) + the K-tile
+// collective, overlapped the same way on the file stream's last chunk.
+template <typename T>
+static void grm_add_bed_reduce_impl(const char* path, uint64_t n_iid, uint64_t n_sid, int count_a1,
+                                    const uint64_t* iid_idx, uint64_t n_out_iid, const uint64_t* sid_idx,
+                                    uint64_t n_out_sid, int std_kind, double a, double b, int use_stats, T* stats,
+                                    int num_threads, int collective, int root, int parts) {
+    std::lock_guard<std::recursive_mutex> lk(g_call_mutex);
+    check_reduce_args<T>(collective, parts);
+    SNPMI_REQUIRE((iid_idx ? n_out_iid : n_iid) == g_session.n, SNPMI_E_ARG, "iid count differs from snpmi_grm_begin");
+    Device& d = device();
+    const int rt = collective == 1 ? root : -1;
+    const uint64_t n = g_session.n, total = sid_idx ? n_out_sid : n_sid;
+    T* tiles = (T*)session_tiles(d);
+    uint64_t done = 0;
+    int groups = 1;
+    const bool wrote = grm_stream_bed<T>(
+        d, !g_session.wrote, path, n_iid, n_sid, count_a1, iid_idx, n_out_iid, sid_idx, n_out_sid, std_kind, a, b,
+        use_stats, stats, num_threads,
+        [&](const uint8_t* packed, uint64_t pitch, uint64_t nn, uint64_t cnt, const T* lut, bool acc) {
+            done += cnt;
+            const bool last = done == total;
+            if constexpr (std::is_same<T, double>::value) {
+                if (last && use_crt(SNPMI_DT_F64)) {
+                    groups = crt_reduce_f64(d, packed, pitch, nn, cnt, lut, tiles, acc, collective, rt, nullptr);
+                    return;
+                }
+            } else {
+                if (last && f32_groupable(d, nn, cnt, parts)) {
+                    groups = grouped_reduce_f32(d, packed, pitch, nn, cnt, lut, tiles, acc, collective, rt, parts,
+                                                nullptr);
+                    return;
+                }
+            }
+            syrk_packed_auto(d, packed, pitch, nn, cnt, lut, DT<T>::v, tiles, acc);
+            if (last && collective) rccl_sum_on(tiles, n_tiles_upper(n) * kTile * kTile, DT<T>::v, rt, d.stream);
+        });
+    g_last_groups = groups;
+    if (wrote && done == total) {
+        g_session.wrote = true;
+        return;  // the last chunk summed the tiles
+    }
+    session_sum_whole<T>(d, collective, rt, nullptr);  // no SNP on this rank: zeros join the sum
 }
 }  // namespace snpmi
 
@@ -1660,18 +1696,38 @@ int snpmi_grm_add_packed_reduce_f32(const uint8_t* packed, uint64_t pitch, uint6
                                     int count_a1, int std_kind, double a, double b, int use_stats, float* stats,
                                     int collective, int root, int parts, void* syrk_done) {
     return guarded([&] {
-        grm_add_packed_reduce_impl(packed, pitch, n_iid, n_sid, count_a1, std_kind, a, b, use_stats, stats, collective,
-                                   root, parts, (hipEvent_t)syrk_done);
+        grm_add_packed_reduce_impl<float>(packed, pitch, n_iid, n_sid, count_a1, std_kind, a, b, use_stats, stats,
+                                          collective, root, parts, (hipEvent_t)syrk_done);
     });
 }
 
 int snpmi_grm_add_packed_reduce_f64(const uint8_t* packed, uint64_t pitch, uint64_t n_iid, uint64_t n_sid,
                                     int count_a1, int std_kind, double a, double b, int use_stats, double* stats,
                                     int collective, int root, int parts, void* syrk_done) {
-    (void)parts;  // the CRT path's own residue chunks are the groups
+    // parts: the CRT path's own residue chunks are the groups
     return guarded([&] {
-        grm_add_packed_reduce_f64_impl(packed, pitch, n_iid, n_sid, count_a1, std_kind, a, b, use_stats, stats,
-                                       collective, root, (hipEvent_t)syrk_done);
+        grm_add_packed_reduce_impl<double>(packed, pitch, n_iid, n_sid, count_a1, std_kind, a, b, use_stats, stats,
+                                           collective, root, std::max(parts, 1), (hipEvent_t)syrk_done);
+    });
+}
+
+int snpmi_grm_add_bed_reduce_f32(const char* path, uint64_t n_iid, uint64_t n_sid, int count_a1, const uint64_t* iid_idx,
+                                 uint64_t n_out_iid, const uint64_t* sid_idx, uint64_t n_out_sid, int std_kind,
+                                 double a, double b, int use_stats, float* stats, int num_threads, int collective,
+                                 int root, int parts) {
+    return guarded([&] {
+        grm_add_bed_reduce_impl<float>(path, n_iid, n_sid, count_a1, iid_idx, n_out_iid, sid_idx, n_out_sid, std_kind,
+                                       a, b, use_stats, stats, num_threads, collective, root, parts);
+    });
+}
+int snpmi_grm_add_bed_reduce_f64(const char* path, uint64_t n_iid, uint64_t n_sid, int count_a1, const uint64_t* iid_idx,
+                                 uint64_t n_out_iid, const uint64_t* sid_idx, uint64_t n_out_sid, int std_kind,
+                                 double a, double b, int use_stats, double* stats, int num_threads, int collective,
+                                 int root, int parts) {
+    return guarded([&] {
+        grm_add_bed_reduce_impl<double>(path, n_iid, n_sid, count_a1, iid_idx, n_out_iid, sid_idx, n_out_sid,
+                                        std_kind, a, b, use_stats, stats, num_threads, collective, root,
+                                        std::max(parts, 1));
     });
 }
 

@@ -117,6 +117,27 @@ class ShardedGrm(object):
                int(bool(bed.count_A1)), N.ptr(ri), self.n, N.ptr(ci), len(ci), kind, a, b, int(use_stats),
                N.ptr(stats), get_num_threads(num_threads))
 
+    def add_bed_combine(self, bed, iid_index, sid_index, kind, a, b, use_stats, stats, num_threads=None, parts=2):
+        """``add_bed`` of this rank's LAST SNPs + ``combine``, overlapped under a real RCCL
+        communicator (``snpmi_grm_add_bed_reduce_*``: the file stream's last chunk runs as column
+        groups / CRT chunks whose tiles are summed on the aux stream under the rest of that chunk's
+        SYRK; the same K bit for bit).  Otherwise the two calls run one after the other."""
+        if not (self.collective != "none" and self.dist is not None and self.dist.rccl):
+            self.add_bed(bed, iid_index, sid_index, kind, a, b, use_stats, stats, num_threads)
+            self.combine()
+            return
+        from pysnptools_amd.util import get_num_threads
+
+        N = self.N
+        ri, ci = N.index_array(iid_index), N.index_array(sid_index)
+        if len(ci) == 0:  # no SNPs on this rank: its zero tiles join the sum
+            self.combine()
+            return
+        N.call("snpmi_grm_add_bed_reduce_" + N.suffix(self.dtype), bed.filename.encode(), bed.iid_count,
+               bed.sid_count, int(bool(bed.count_A1)), N.ptr(ri), self.n, N.ptr(ci), len(ci), kind, a, b,
+               int(use_stats), N.ptr(stats), get_num_threads(num_threads),
+               1 if self.collective == "reduce" else 2, self.root, int(parts))
+
     def add_packed(self, packed, pitch, n_sid, kind, a, b, use_stats, stats, count_a1=False):
         """Packed SNP columns already in HBM (device pointer, [n_sid][pitch] bytes of all the
         session's iids); ``stats`` host or device [n_sid, 2]."""
@@ -231,9 +252,8 @@ def grm_sharded(reader, standardizer, rank=None, world=None, dtype=np.float32, c
         mine = np.zeros((hi - lo, 2), dtype=dtype)
     g = ShardedGrm(n, dtype, d, collective, root, rank, world)
     try:
-        g.add_bed(base, rows, col_index[lo:hi], kind, a, b, use_stats, mine,
-                  num_threads if num_threads is not None else base._num_threads)
-        g.combine()
+        g.add_bed_combine(base, rows, col_index[lo:hi], kind, a, b, use_stats, mine,
+                          num_threads if num_threads is not None else base._num_threads)
         if kind != 0 and not use_stats:
             stats[lo:hi] = mine
             stats = _sum_stats(d, stats, collective, world)

@@ -136,3 +136,40 @@ def test_overlapped_collective_world1_f64(rccl1, collective):
         packed.free()
     assert N.kernel_variant("overlap_groups") >= 2
     assert np.array_equal(ref, got)
+
+
+def _write_bed(path, n, m, seed):
+    rng = np.random.default_rng(seed)
+    bpc = (n + 3) // 4
+    codes = rng.choice(np.array([0, 1, 2, 3], dtype=np.uint8), size=(m, bpc * 4), p=[0.3, 0.05, 0.35, 0.3])
+    codes[:, n:] = 0
+    body = (codes[:, 0::4] | (codes[:, 1::4] << 2) | (codes[:, 2::4] << 4) | (codes[:, 3::4] << 6)).astype(np.uint8)
+    with open(path + ".bed", "wb") as f:
+        f.write(bytes([0x6C, 0x1B, 0x01]))
+        f.write(body.tobytes())
+    with open(path + ".fam", "w") as f:
+        f.write("".join("f%d i%d 0 0 0 0\n" % (i, i) for i in range(n)))
+    with open(path + ".bim", "w") as f:
+        f.write("".join("1\ts%d\t0\t%d\tA\tC\n" % (j, j + 1) for j in range(m)))
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+@pytest.mark.parametrize("collective", ["reduce", "allreduce"])
+def test_grm_sharded_bed_overlapped_world1(rccl1, tmp_path, dtype, collective):
+    """shard.grm_sharded from a .bed under a real RCCL communicator: the file stream's last chunk
+    runs as column groups (f32) / column-aligned CRT chunks (f64) with the tiles summed on the aux
+    stream (snpmi_grm_add_bed_reduce_*); K and the trained stats equal the unoverlapped call
+    (collective "none" at world 1) bit for bit."""
+    from pysnptools_amd import shard
+    from pysnptools_amd.snpreader import Bed
+    from pysnptools_amd.standardizer import Unit
+
+    path = str(tmp_path / "w")
+    _write_bed(path, 30000, 3000, 61)
+    bed = Bed(path, count_A1=False)
+    K1, t1, _ = shard.grm_sharded(bed, Unit(), dtype=dtype, collective=collective, dist=rccl1)
+    groups = N.kernel_variant("overlap_groups")
+    K0, t0, _ = shard.grm_sharded(bed, Unit(), dtype=dtype, collective="none", dist=rccl1)
+    assert groups >= 2, groups
+    assert np.array_equal(K1, K0)
+    np.testing.assert_array_equal(t1.stats, t0.stats)
