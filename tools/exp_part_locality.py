@@ -1,4 +1,4 @@
-"""Why does the cfg5 part kernel run ~4% below the replicated one?  Same n = 50,000 iids, same
+"""Why does the cfg5 part kernel run ~4% below the replicated one?  Same n = 150,000 iids (enough blocks per part that the last round of workgroups does not dominate), same
 codes: k_syrk_h2<LOCAL> over all blocks (parts = 1) vs over part 0 of 8 (every 8th block of the
 supertile order, as cfg5), time per block, alternating rounds.  Prints one JSON line."""
 import json
@@ -13,7 +13,7 @@ def main():
     import bench
     from pysnptools_amd import _native as N
 
-    n, m, rounds = 50_000, 31_250, 3
+    n, m, rounds = 150_000, 16_384, 3
     pitch = N.lib().snpmi_packed_pitch(n)
     p = bench.Dev(N, pitch * m)
     bench.synth(N, p.p, pitch, n, 0, m, 5, 0.218)
