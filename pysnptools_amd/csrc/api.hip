@@ -109,7 +109,7 @@ void Device::release() {
     }
     if (part_order_tab) (void)hipFree(part_order_tab);
     part_order_tab = nullptr;
-    part_order_key[0] = part_order_key[1] = part_order_key[2] = 0;
+    for (int i = 0; i < 4; i++) part_order_key[i] = 0;
 }
 
 // pinned staging (two slots so a chunk can be gathered while the previous one uploads)
@@ -1011,21 +1011,22 @@ const uint32_t* packed_block_order(uint64_t nb) {
 const uint32_t* part_block_order(uint64_t nb, int rank, int world) {
     std::lock_guard<std::recursive_mutex> lk(g_call_mutex);
     Device& d = device();
-    const uint64_t key[3] = {nb, (uint64_t)rank, (uint64_t)world};
+    const uint64_t S = g_part_triangular == 2 ? 16 : 64;
+    const uint64_t key[4] = {nb, (uint64_t)rank, (uint64_t)world, S};
     if (!d.part_order_tab || d.part_order_key[0] != key[0] || d.part_order_key[1] != key[1] ||
-        d.part_order_key[2] != key[2]) {
+        d.part_order_key[2] != key[2] || d.part_order_key[3] != key[3]) {
         std::vector<uint32_t> tab;
-        part_supertile_order(nb, rank, world, tab);
+        part_supertile_order(nb, rank, world, tab, S);
         if (d.part_order_tab) SNPMI_HIP(hipFree(d.part_order_tab));
         d.part_order_tab = nullptr;
-        d.part_order_key[0] = d.part_order_key[1] = d.part_order_key[2] = 0;
+        for (int i = 0; i < 4; i++) d.part_order_key[i] = 0;
         if (tab.empty()) return nullptr;
         if (hipMalloc(&d.part_order_tab, tab.size() * sizeof(uint32_t)) != hipSuccess) {
             (void)hipGetLastError();
             throw Error(SNPMI_E_NOMEM, "hipMalloc of the part block order table failed");
         }
         SNPMI_HIP(hipMemcpy(d.part_order_tab, tab.data(), tab.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
-        for (int i = 0; i < 3; i++) d.part_order_key[i] = key[i];
+        for (int i = 0; i < 4; i++) d.part_order_key[i] = key[i];
     }
     return d.part_order_tab;
 }
@@ -1542,7 +1543,7 @@ int snpmi_set_kernel_variant(const char* kernel, int variant) {
         if (std::strcmp(kernel, "decode") == 0) g_variant_decode = variant;
         else if (std::strcmp(kernel, "std") == 0) g_variant_std = variant;
         else if (std::strcmp(kernel, "diag") == 0) g_diag_exact = variant != 0;
-        else if (std::strcmp(kernel, "part_order") == 0) g_part_triangular = variant != 0;
+        else if (std::strcmp(kernel, "part_order") == 0) g_part_triangular = variant;
         else if (std::strcmp(kernel, "extract") == 0) g_variant_extract = variant;
         else if (std::strcmp(kernel, "syrk") == 0) {
 #ifndef SNPMI_UBENCH

@@ -92,7 +92,7 @@ struct Device {
     uint64_t order_nb[2] = {};
     // the same order restricted to one part of the cfg5 plan, per (nb, rank, world)
     uint32_t* part_order_tab = nullptr;
-    uint64_t part_order_key[3] = {};
+    uint64_t part_order_key[4] = {};
     void* get(Slot s, size_t bytes);
     void release();
 };
@@ -129,7 +129,7 @@ SegCtx seg_ctx();                                     // api.hip: the current de
 // block order of the packed fp16x2 SYRK
 const uint32_t* packed_block_order(uint64_t nb);
 const uint32_t* part_block_order(uint64_t nb, int rank, int world);
-extern int g_part_triangular;  // hook "part_order": 1 = the cfg5 part kernel in triangular order
+extern int g_part_triangular;  // hook "part_order": 0 = 64-block supertiles, 1 = triangular, 2 = 16-block supertiles
 void launch_snp_stats(const uint8_t* packed, uint64_t pitch, uint64_t n_iid, uint64_t n_sid, int count_a1,
                       int std_kind, double a, double b, int use_stats, int dtype, void* stats, void* lut,
                       hipStream_t st);
@@ -223,7 +223,7 @@ void launch_lut_h2(const float* lut, uint64_t m, uint32_t* lut2, uint32_t* flag,
 // fp16x2 SYRK in supertile block order (order: device table of supertile_order), the f32-MFMA
 // k_syrk256d gated on the range flag
 void supertile_order(uint64_t nb, bool xcd, std::vector<uint32_t>& tab);
-void part_supertile_order(uint64_t nb, int rank, int world, std::vector<uint32_t>& tab);
+void part_supertile_order(uint64_t nb, int rank, int world, std::vector<uint32_t>& tab, uint64_t S);
 uint64_t dense_h2_chunk_snps(uint64_t n);
 uint64_t dense_h2_scratch_bytes(uint64_t n, uint64_t m);
 void launch_syrk_dense_h2(const float* Z, uint64_t ldz, uint64_t n, uint64_t m, uint16_t* img, uint32_t* flag,

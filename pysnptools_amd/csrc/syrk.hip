@@ -2659,17 +2659,20 @@ void supertile_order(uint64_t nb, bool xcd, std::vector<uint32_t>& tab) {
         }
 }
 
-// supertile_order(nb, false) restricted to the blocks of part `rank` (block L = bj(bj+1)/2 + bi,
-// owner L mod world): the ~256 blocks in flight come from ~8 supertiles instead of ~1-2 columns of
-// the triangle, as the replicated kernel's table does for the whole triangle
-void part_supertile_order(uint64_t nb, int rank, int world, std::vector<uint32_t>& tab) {
-    std::vector<uint32_t> all;
-    supertile_order(nb, false, all);
+// The blocks of part `rank` (block L = bj(bj+1)/2 + bi, owner L mod world) in supertile order
+// with S x S-block supertiles (S = 16: the replicated kernel's table).  The part owns every
+// world-th block, so the ~256 blocks in flight span more panels than the replicated kernel's
+// (~46 code panels per 256 blocks there): ~153 with S = 16, ~108 with S = 64 (host count at
+// 150k iids, 8 parts; tools/exp_part_locality.py measures the part kernel 8% slower per block).
+void part_supertile_order(uint64_t nb, int rank, int world, std::vector<uint32_t>& tab, uint64_t S) {
     tab.clear();
-    for (uint32_t c : all) {
-        const uint64_t bi = c & 0xffffu, bj = c >> 16;
-        if ((bj * (bj + 1) / 2 + bi) % (uint64_t)world == (uint64_t)rank) tab.push_back(c);
-    }
+    const uint64_t ns = ceil_div(nb, S);
+    for (uint64_t J = 0; J < ns; J++)
+        for (uint64_t I = 0; I <= J; I++)
+            for (uint64_t bj = S * J; bj < std::min(S * J + S, nb); bj++)
+                for (uint64_t bi = S * I; bi < std::min(S * I + S, bj + 1); bi++)
+                    if ((bj * (bj + 1) / 2 + bi) % (uint64_t)world == (uint64_t)rank)
+                        tab.push_back((uint32_t)(bi | (bj << 16)));
 }
 
 #ifdef SNPMI_UBENCH
@@ -2901,7 +2904,7 @@ void launch_syrk_packed_bf3_part(const uint8_t* packed, uint64_t pitch, uint64_t
     if (h2) {
         // supertile order over the part's blocks (hook "part_order" = 1: the triangular order)
         const uint64_t nb = ceil_div(n, 256);  // table entries pack bi | bj << 16
-        const uint32_t* order = (g_part_triangular || nb >= 65536) ? nullptr : part_block_order(nb, rank, world);
+        const uint32_t* order = (g_part_triangular == 1 || nb >= 65536) ? nullptr : part_block_order(nb, rank, world);
         f32w::k_syrk_h2<true><<<(unsigned)nloc, 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, blocks, accumulate,
                                                                (uint32_t)rank, (uint32_t)world, 0, 0,
                                                                seg_ctx(), order);

@@ -1,5 +1,5 @@
-"""cfg5 part-kernel block order A/B (hook part_order: 0 = supertile order over the part's blocks,
-1 = round 4's triangular order; keyed 0 / 67 below): HIP-event time of snpmi_dev_syrk_packed_part on one SnpGen-shaped
+"""cfg5 part-kernel block order A/B (hook part_order: 0 = 64-block supertiles, 1 = triangular
+order, 2 = 16-block supertiles; keyed 0 / 67 / 16 below): HIP-event time of snpmi_dev_syrk_packed_part on one SnpGen-shaped
 block of --m SNPs at --n iids, part 0 of 8, alternating rounds, and sampled blocks compared bit
 for bit.  Prints one JSON line."""
 import argparse
@@ -33,10 +33,10 @@ def main():
     N.call("snpmi_dev_snp_stats", packed.p, pitch, n, m, 0, N.STD_UNIT, 0.0, 0.0, 0, N.DT_F32, stats.p, lut.p)
     ev = bench.Events(N, 2)
     picks = sorted({0, 1, nloc // 3, nloc // 2, nloc - 2, nloc - 1})
-    res, samples = {0: [], 67: []}, {}
+    res, samples = {0: [], 67: [], 16: []}, {}
     for r in range(a.rounds + 1):
-        for v in (67, 0):
-            N.call("snpmi_set_kernel_variant", b"part_order", int(v == 67))
+        for v in (67, 16, 0):
+            N.call("snpmi_set_kernel_variant", b"part_order", {0: 0, 67: 1, 16: 2}[v])
             ev.record(0)
             N.call("snpmi_dev_syrk_packed_part", packed.p, pitch, n, m, lut.p, 0, P, blocks.p, 0)
             ev.record(1)
@@ -50,11 +50,14 @@ def main():
             samples[v] = s
     flops = n * (n + 1) * m / P
     print(json.dumps({"n": n, "m": m, "parts": P, "local_blocks": nloc,
-                      "supertile_ms": res[0], "triangular_ms": res[67],
-                      "supertile_TF": flops / (min(res[0]) * 1e-3) / 1e12,
+                      "supertile64_ms": res[0], "supertile16_ms": res[16], "triangular_ms": res[67],
+                      "supertile64_TF": flops / (min(res[0]) * 1e-3) / 1e12,
+                      "supertile16_TF": flops / (min(res[16]) * 1e-3) / 1e12,
                       "triangular_TF": flops / (min(res[67]) * 1e-3) / 1e12,
-                      "speedup": min(res[67]) / min(res[0]),
-                      "sampled_blocks_bit_equal": bool(np.array_equal(samples[0], samples[67]))}), flush=True)
+                      "speedup_64_vs_triangular": min(res[67]) / min(res[0]),
+                      "speedup_64_vs_16": min(res[16]) / min(res[0]),
+                      "sampled_blocks_bit_equal": bool(np.array_equal(samples[0], samples[67]) and
+                                                       np.array_equal(samples[16], samples[67]))}), flush=True)
     ev.destroy()
     for d in (packed, lut, stats, blocks):
         d.free()
