@@ -233,6 +233,12 @@ int snpmi_grm_add_packed_reduce_f64(const uint8_t* packed, uint64_t pitch, uint6
                                     int count_a1, int std_kind, double a, double b, int use_stats, double* stats,
                                     int collective, int root, int parts, void* syrk_done);
 int snpmi_grm_session_tiles(void** tiles, uint64_t* count);   /* device tiles + element count */
+/* The session's K-tile collective over the ranks (1 = reduce onto root, 2 = all-reduce), without
+ * an add: the same RCCL calls, in the same order, as snpmi_grm_add_*_reduce_* with the same
+ * `parts` -- a rank that owns no SNPs (or added its SNPs unoverlapped) joins the others' ranged sums
+ * with this call.  The calls depend only on n, dtype, parts and the kernel configuration, never on
+ * a rank's SNP count.  Replaces the sum over ranks after the block loop of snpreader.py:651-655. */
+int snpmi_grm_session_sum(int collective, int root, int parts);
 /* K_out NULL: end the session without a result (a non-root rank after snpmi_rccl_reduce_sum) */
 int snpmi_grm_end(int diag_k_to_n, double* factor, void* K_out);
 int snpmi_diag_k_to_n_f32(float* K, uint64_t n, double* factor);

@@ -75,6 +75,7 @@ _SIGS = {
     "snpmi_grm_add_dense_f32": [_vp, _u64, _u64, _i32],
     "snpmi_grm_add_dense_f64": [_vp, _u64, _u64, _i32],
     "snpmi_grm_session_tiles": [ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_uint64)],
+    "snpmi_grm_session_sum": [_i32, _i32, _i32],
     "snpmi_grm_end": [_i32, _dp, _vp],
     "snpmi_diag_k_to_n_snps_f32": [_vp, _u64, _u64, _dp],
     "snpmi_diag_k_to_n_snps_f64": [_vp, _u64, _u64, _dp],

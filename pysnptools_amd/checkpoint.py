@@ -38,9 +38,11 @@ def _digest(idx):
 def _fingerprint(bed_path, n, m, dtype, block_size, kind, a, b, use_stats, rows, cols, count_a1, stats_in):
     st = os.stat(bed_path)
     # the accumulation settings of this process: partial sums of another f64 path (CRT vs f64
-    # MFMA) or another f32 chain length would not resume bit-identically
+    # MFMA), another f32 chain length, exact diagonal on/off or another f32 SYRK kernel would not
+    # resume bit-identically
     settings = ({"f64_path": N.kernel_variant("f64")} if np.dtype(dtype) == np.float64
-                else {"f32_seg": N.kernel_variant("seg")})
+                else {"f32_seg": N.kernel_variant("seg"), "f32_diag": N.kernel_variant("diag"),
+                      "f32_syrk": N.kernel_variant("syrk")})
     return {"settings": settings, "bed": os.path.abspath(bed_path), "size": st.st_size, "mtime_ns": st.st_mtime_ns, "n": int(n),
             "m": int(m), "dtype": np.dtype(dtype).str, "block_size": int(block_size), "kind": int(kind),
             "a": None if np.isnan(a) else float(a), "b": None if np.isnan(b) else float(b),
@@ -148,6 +150,11 @@ def _restore(path, meta, dtype):
         saved = json.load(f)
     nb = saved.pop("next_block")
     files = saved.pop("files", None)
+    if saved.get("settings") != meta["settings"] and \
+            {k: v for k, v in saved.items() if k != "settings"} == {k: v for k, v in meta.items() if k != "settings"}:
+        raise ValueError("checkpoint '%s' was written with other GRM kernel settings (%s) than this process's (%s); "
+                         "restore them (snpmi_set_kernel_variant) or remove the checkpoint"
+                         % (path, saved.get("settings", "none recorded"), meta["settings"]))
     if saved != meta:
         raise ValueError("checkpoint '%s' belongs to another GRM (reader, standardizer, block size or dtype "
                          "differ); remove it or choose another path" % path)

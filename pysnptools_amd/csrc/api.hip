@@ -778,7 +778,7 @@ static void syrk_packed_auto(Device& d, const uint8_t* packed, uint64_t pitch, u
         return;
     }
     if (dt == SNPMI_DT_F32 && g_diag_exact && m > 0 && n > 0) {  // exact diagonal around the SYRK
-        double* diag = (double*)d.get(Device::S_DIAG, n * sizeof(double));
+        double* diag = (double*)d.get(Device::S_DIAG, diag_scratch_bytes(n, m));
         launch_diag_begin((const float*)tiles, n, 0, 0, accumulate, diag, d.stream);
         syrk_packed_f32_body(d, packed, pitch, n, m, lut, dt, tiles, accumulate);
         launch_diag_end(packed, pitch, n, m, (const float*)lut, (float*)tiles, 0, 0, diag, d.stream);
@@ -820,7 +820,7 @@ static void syrk_packed_part_body(Device& d, const uint8_t* packed, uint64_t pit
 static void syrk_packed_part_auto(Device& d, const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m,
                                   const float* lut, int rank, int world, void* blocks, int accumulate) {
     if (g_diag_exact && m > 0 && n > 0) {  // exact diagonal of the part's diagonal blocks
-        double* diag = (double*)d.get(Device::S_DIAG, n * sizeof(double));
+        double* diag = (double*)d.get(Device::S_DIAG, diag_scratch_bytes(n, m));
         launch_diag_begin((const float*)blocks, n, rank, world, accumulate, diag, d.stream);
         syrk_packed_part_body(d, packed, pitch, n, m, lut, rank, world, blocks, accumulate);
         launch_diag_end(packed, pitch, n, m, lut, (float*)blocks, rank, world, diag, d.stream);
@@ -1269,11 +1269,19 @@ static int g_last_groups = 0;  // column groups of the last overlapped collectiv
 
 // Events of one overlapped collective: compute-stream events the aux stream waits on before each
 // group's sum, then one aux event the compute stream waits on; destroyed at the end.
+// The RCCL calls of the last K-tile collective (read-only hooks "overlap_calls" / "overlap_sig":
+// their number and a hash of their element ranges -- tests check every rank issues the same ones)
+static int g_last_sum_calls = 0;
+static uint64_t g_last_sum_sig = 0;
+
 struct OverlapSums {
     Device& d;
     int collective, root, dtype;
     std::vector<hipEvent_t> evs;
-    OverlapSums(Device& dev, int coll, int rt, int dt) : d(dev), collective(coll), root(rt), dtype(dt) {}
+    OverlapSums(Device& dev, int coll, int rt, int dt) : d(dev), collective(coll), root(rt), dtype(dt) {
+        g_last_sum_calls = 0;
+        g_last_sum_sig = 1469598103934665603ull;
+    }
     ~OverlapSums() {
         for (hipEvent_t e : evs) (void)hipEventDestroy(e);
     }
@@ -1290,6 +1298,8 @@ struct OverlapSums {
         auto T = [&](uint64_t t) { t = std::min(t, nt); return t * (t + 1) / 2 * (uint64_t)(kTile * kTile); };
         const uint64_t e0 = T(t0), e1 = T(t1);
         if (e1 <= e0) return;
+        g_last_sum_calls++;
+        g_last_sum_sig = (g_last_sum_sig ^ (e0 * 0x9E3779B97F4A7C15ull + e1)) * 1099511628211ull;
         hipEvent_t e = event();
         SNPMI_HIP(hipEventRecord(e, d.stream));
         SNPMI_HIP(hipStreamWaitEvent(d.aux, e, 0));
@@ -1303,20 +1313,62 @@ struct OverlapSums {
     }
 };
 
+// Whether the last SYRK of an f32 GRM can run as column groups (launch_syrk_packed_h2_cols) --
+// decided from state every rank shares (n, parts, the kernel configuration), never from the rank's
+// own SNP count: ranks whose spans differ by a SNP, or that own none, must issue the same RCCL
+// calls.  The split-K check uses the largest chunk: a chunk of fewer SNPs only narrows
+// the slice counts bf3_split_slices may choose, so "no split at 65536" holds for every chunk.
+static bool f32_groupable(Device& d, uint64_t n, int parts) {
+    return n > 0 && use_bf3(SNPMI_DT_F32) && use_h2() && g_diag_exact && parts > 1 &&
+           bf3_split_slices(n, 1ull << 16, d.cu_count) == 1 && ceil_div(n, 256) < 65536;
+}
+
+static uint64_t crt_res_bytes(uint64_t n) {
+    const uint64_t nb = ceil_div(n, 256);
+    return std::min<uint64_t>(nb * (nb + 1) / 2 * (uint64_t)crt_moduli() * 65536, 4ull << 30);
+}
+
+// The K-tile collective of one session as RCCL calls: 128-tile column ranges [t0, t1) of the
+// triangle, each one in-place sum.  f32: the column groups of the overlapped SYRK; f64 on the CRT
+// path: its column-aligned residue chunks; otherwise one range over the whole triangle.  Every path
+// that sums a session's tiles (overlapped or not, with or without SNPs on this rank) issues exactly
+// these calls, in this order.
+struct SumPlan {
+    std::vector<std::pair<uint64_t, uint64_t>> ranges;
+    bool grouped = false;  // the ranges are the overlapped SYRK's groups
+};
+static SumPlan sum_plan(Device& d, uint64_t n, int dtype, int parts) {
+    SumPlan p;
+    if (dtype == SNPMI_DT_F32 && f32_groupable(d, n, parts)) {
+        for (const auto& g : column_groups(ceil_div(n, 256), parts)) p.ranges.push_back({2 * g.c0, 2 * g.c1});
+        p.grouped = true;
+    } else if (dtype == SNPMI_DT_F64 && use_crt(SNPMI_DT_F64) && n > 0) {
+        for (const auto& c : crt_column_chunks(n, crt_res_bytes(n))) p.ranges.push_back({2 * c.first, 2 * c.second});
+        p.grouped = true;
+    } else {
+        p.ranges.push_back({0, n_tiles_1d(n)});
+    }
+    return p;
+}
+
+// The plan's sums after everything enqueued so far on the compute stream (aux stream, then the
+// compute stream waits for the last one)
+static void sum_by_plan(Device& d, const SumPlan& p, void* tiles, uint64_t n, int collective, int rt, int dtype) {
+    OverlapSums sums(d, collective, rt, dtype);
+    for (const auto& r : p.ranges) sums.range(tiles, n, r.first, r.second);
+    sums.join();
+}
+
 // The overlapped last SYRK of an f32 GRM: `cnt` SNPs (device codes + f32 LUT) added into `tiles`
 // in column groups (launch_syrk_packed_h2_cols, K bit-identical to one launch) with the exact
 // diagonal written back per group, each group's tiles summed over the ranks on the aux stream
 // under the next group's SYRK.  Returns the group count.
-static bool f32_groupable(Device& d, uint64_t n, uint64_t cnt, int parts) {
-    return cnt > 0 && n > 0 && use_bf3(SNPMI_DT_F32) && use_h2() && g_diag_exact && parts > 1 &&
-           bf3_split_slices(n, std::min<uint64_t>(cnt, 1ull << 16), d.cu_count) == 1 && ceil_div(n, 256) < 65536;
-}
 static int grouped_reduce_f32(Device& d, const uint8_t* src, uint64_t pitch, uint64_t n, uint64_t cnt,
                               const float* lut, float* tiles, int acc, int collective, int rt, int parts,
                               hipEvent_t syrk_done) {
     H2Lut h2;
     const uint32_t* l3 = lut_bf3(d, lut, cnt, &h2);
-    double* diag = (double*)d.get(Device::S_DIAG, n * sizeof(double));
+    double* diag = (double*)d.get(Device::S_DIAG, diag_scratch_bytes(n, cnt));
     launch_diag_begin(tiles, n, 0, 0, acc, diag, d.stream);
     launch_diag_sq(src, pitch, n, cnt, lut, diag, d.stream);
     const auto groups = column_groups(ceil_div(n, 256), parts);
@@ -1348,29 +1400,33 @@ static int crt_reduce_f64(Device& d, const uint8_t* src, uint64_t pitch, uint64_
         cnt -= lead;
         acc = 1;
     }
-    const uint64_t nb = ceil_div(n, 256);
-    const uint64_t res_bytes = std::min<uint64_t>(nb * (nb + 1) / 2 * (uint64_t)crt_moduli() * 65536, 4ull << 30);
+    const uint64_t res_bytes = crt_res_bytes(n);
     uint8_t* res = (uint8_t*)d.get(Device::S_ZBLK, res_bytes);
     void* ws = d.get(Device::S_LUT3, crt_lut_bytes(cnt, n));
     unsigned long long* rec = crt_record(d);
+    const SumPlan plan = sum_plan(d, n, SNPMI_DT_F64, 1);
     OverlapSums sums(d, collective, rt, SNPMI_DT_F64);
-    int groups = 0;
+    size_t groups = 0;
     const std::function<void()> pre = [&] {
         launch_syrk_packed_f64_gated(src, pitch, n, cnt, lut, tiles, acc, (const int*)ws + 1, d.stream);
     };
     const std::function<void(uint64_t, uint64_t)> after = [&](uint64_t c0, uint64_t c1) {
+        SNPMI_REQUIRE(groups < plan.ranges.size() && plan.ranges[groups] == std::make_pair(2 * c0, 2 * c1),
+                      SNPMI_E_ARG, "CRT chunks differ from the collective plan");
         groups++;
         sums.range(tiles, n, 2 * c0, 2 * c1);
     };
     launch_syrk_packed_crt(src, pitch, n, cnt, lut, tiles, acc, ws, res, res_bytes, rec, d.stream, &pre, &after);
+    SNPMI_REQUIRE(groups == plan.ranges.size(), SNPMI_E_ARG, "CRT chunks differ from the collective plan");
     if (syrk_done) SNPMI_HIP(hipEventRecord(syrk_done, d.stream));
     sums.join();
-    return groups;
+    return (int)groups;
 }
 
-// whole-buffer collective after an unoverlapped add (paths without groups); zeros if nothing was added
+// the session's collective after an unoverlapped add (or on a rank without SNPs): the same RCCL
+// calls as the overlapped path (sum_plan); zeros join the sum if nothing was added
 template <typename T>
-static void session_sum_whole(Device& d, int collective, int rt, hipEvent_t syrk_done) {
+static void session_sum_planned(Device& d, int collective, int rt, int parts, hipEvent_t syrk_done) {
     T* t = (T*)session_tiles(d);
     const uint64_t count = n_tiles_upper(g_session.n) * kTile * kTile;
     if (!g_session.wrote) {
@@ -1378,7 +1434,7 @@ static void session_sum_whole(Device& d, int collective, int rt, hipEvent_t syrk
         g_session.wrote = true;
     }
     if (syrk_done) SNPMI_HIP(hipEventRecord(syrk_done, d.stream));
-    if (collective) rccl_sum_on(t, count, DT<T>::v, rt, d.stream);
+    if (collective) sum_by_plan(d, sum_plan(d, g_session.n, DT<T>::v, parts), t, g_session.n, collective, rt, DT<T>::v);
 }
 
 template <typename T>
@@ -1404,13 +1460,13 @@ static void grm_add_packed_reduce_impl(const uint8_t* packed, uint64_t pitch, ui
     const bool f64 = DT<T>::v == SNPMI_DT_F64;
     const uint64_t nchunk = m ? ceil_div(m, 1ull << 16) : 1;
     const uint64_t step = std::min<uint64_t>(1ull << 16, round_up(ceil_div(m, nchunk), 256));
-    const bool grouped = m > 0 && n > 0 && n == g_session.n &&
-                         (f64 ? use_crt(SNPMI_DT_F64) : f32_groupable(d, n, std::min(m, step), parts)) &&
+    (void)f64;
+    const bool grouped = m > 0 && n > 0 && n == g_session.n && sum_plan(d, n, DT<T>::v, parts).grouped &&
                          (std_kind == SNPMI_STD_NONE || (stats && is_device_ptr(d, stats)));
     g_last_groups = 1;
     if (!grouped) {
         grm_add_packed_impl<T>(packed, pitch, n, m, count_a1, std_kind, a, b, use_stats, stats);
-        session_sum_whole<T>(d, collective, rt, syrk_done);
+        session_sum_planned<T>(d, collective, rt, parts, syrk_done);
         return;
     }
     SNPMI_REQUIRE(pitch % 64 == 0 && pitch >= ceil_div(n, 4), SNPMI_E_ARG, "pitch must be snpmi_packed_pitch");
@@ -1449,33 +1505,30 @@ static void grm_add_bed_reduce_impl(const char* path, uint64_t n_iid, uint64_t n
     T* tiles = (T*)session_tiles(d);
     uint64_t done = 0;
     int groups = 1;
+    const SumPlan plan = sum_plan(d, n, DT<T>::v, parts);
     const bool wrote = grm_stream_bed<T>(
         d, !g_session.wrote, path, n_iid, n_sid, count_a1, iid_idx, n_out_iid, sid_idx, n_out_sid, std_kind, a, b,
         use_stats, stats, num_threads,
         [&](const uint8_t* packed, uint64_t pitch, uint64_t nn, uint64_t cnt, const T* lut, bool acc) {
             done += cnt;
             const bool last = done == total;
-            if constexpr (std::is_same<T, double>::value) {
-                if (last && use_crt(SNPMI_DT_F64)) {
+            if (last && plan.grouped) {
+                if constexpr (std::is_same<T, double>::value)
                     groups = crt_reduce_f64(d, packed, pitch, nn, cnt, lut, tiles, acc, collective, rt, nullptr);
-                    return;
-                }
-            } else {
-                if (last && f32_groupable(d, nn, cnt, parts)) {
+                else
                     groups = grouped_reduce_f32(d, packed, pitch, nn, cnt, lut, tiles, acc, collective, rt, parts,
                                                 nullptr);
-                    return;
-                }
+                return;
             }
             syrk_packed_auto(d, packed, pitch, nn, cnt, lut, DT<T>::v, tiles, acc);
-            if (last && collective) rccl_sum_on(tiles, n_tiles_upper(n) * kTile * kTile, DT<T>::v, rt, d.stream);
+            if (last && collective) sum_by_plan(d, plan, tiles, n, collective, rt, DT<T>::v);
         });
     g_last_groups = groups;
     if (wrote && done == total) {
         g_session.wrote = true;
         return;  // the last chunk summed the tiles
     }
-    session_sum_whole<T>(d, collective, rt, nullptr);  // no SNP on this rank: zeros join the sum
+    session_sum_planned<T>(d, collective, rt, parts, nullptr);  // no SNP on this rank: zeros join the sum
 }
 }  // namespace snpmi
 
@@ -1578,6 +1631,8 @@ int snpmi_get_kernel_variant(const char* kernel, int* variant) {
         else if (std::strcmp(kernel, "diag") == 0) *variant = g_diag_exact;
         else if (std::strcmp(kernel, "part_order") == 0) *variant = g_part_triangular;
         else if (std::strcmp(kernel, "overlap_groups") == 0) *variant = g_last_groups;
+        else if (std::strcmp(kernel, "overlap_calls") == 0) *variant = g_last_sum_calls;
+        else if (std::strcmp(kernel, "overlap_sig") == 0) *variant = (int)(g_last_sum_sig & 0x7fffffff);
         else if (std::strcmp(kernel, "extract") == 0) *variant = g_variant_extract;
         else if (std::strcmp(kernel, "syrk") == 0) *variant = g_variant_syrk;
         else if (std::strcmp(kernel, "syrk_split") == 0) *variant = g_variant_syrk_split;
@@ -1753,6 +1808,23 @@ int snpmi_grm_session_tiles(void** tiles, uint64_t* count) {
         }
         if (tiles) *tiles = t;
         if (count) *count = cnt;
+    });
+}
+
+int snpmi_grm_session_sum(int collective, int root, int parts) {
+    return guarded([&] {
+        std::lock_guard<std::recursive_mutex> lk(g_call_mutex);
+        SNPMI_REQUIRE(g_session.active, SNPMI_E_ARG, "no GRM session (call snpmi_grm_begin)");
+        Device& d = device();
+        const int rt = collective == 1 ? root : -1;
+        g_last_groups = 1;
+        if (g_session.dtype == SNPMI_DT_F64) {
+            check_reduce_args<double>(collective, parts);
+            session_sum_planned<double>(d, collective, rt, parts, nullptr);
+        } else {
+            check_reduce_args<float>(collective, parts);
+            session_sum_planned<float>(d, collective, rt, parts, nullptr);
+        }
     });
 }
 

@@ -2095,10 +2095,12 @@ __global__ __launch_bounds__(kBlock) void k_diag_save(const float* __restrict__ 
 }
 
 // grid.x: 16-iid words (one packed dword per thread and SNP, coalesced across the wave),
-// grid.y: SNP slices (enough threads to fill the chip at any n); one f64 atomic per iid and slice
+// grid.y: SNP slices (enough threads to fill the chip at any n); each slice's f64 partial sums go
+// to their own row of `part` (plain stores), folded into diag in slice order by k_diag_fold -- the
+// same bits on every run (f64 atomics would add the slices in arrival order)
 __global__ __launch_bounds__(kBlock) void k_diag_sq(const uint8_t* __restrict__ packed, uint64_t pitch, uint64_t n,
                                                     uint64_t m, const float* __restrict__ lut, uint64_t per_slice,
-                                                    double* __restrict__ diag) {
+                                                    uint64_t part_ld, double* __restrict__ part) {
     const uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const uint64_t nw = (n + 15) / 16;
     if (w >= nw) return;
@@ -2117,9 +2119,18 @@ __global__ __launch_bounds__(kBlock) void k_diag_sq(const uint8_t* __restrict__ 
             acc[k] += c == 0 ? q0 : c == 1 ? q1 : c == 2 ? q2 : q3;
         }
     }
+    double2* dst = reinterpret_cast<double2*>(part + (uint64_t)blockIdx.y * part_ld + 16 * w);
 #pragma unroll
-    for (int k = 0; k < 16; k++)
-        if (16 * w + k < n) atomicAdd(diag + 16 * w + k, acc[k]);
+    for (int k = 0; k < 8; k++) dst[k] = make_double2(acc[2 * k], acc[2 * k + 1]);
+}
+
+__global__ __launch_bounds__(kBlock) void k_diag_fold(uint64_t n, uint64_t slices, uint64_t part_ld,
+                                                      const double* __restrict__ part, double* __restrict__ diag) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        double s = diag[i];
+        for (uint64_t y = 0; y < slices; y++) s += part[y * part_ld + i];
+        diag[i] = s;
+    }
 }
 
 __global__ __launch_bounds__(kBlock) void k_diag_patch(float* __restrict__ K, uint64_t i0, uint64_t i1, int part_rank,
@@ -2961,14 +2972,26 @@ void launch_diag_begin(const float* K, uint64_t n, int part_rank, int part_world
     SNPMI_LAUNCH_CHECK();
 }
 
+// SNP slices of k_diag_sq: enough (word, slice) threads to fill 256 CUs several times over,
+// slices of >= 64 SNPs
+static uint64_t diag_slices(uint64_t n, uint64_t m) {
+    const uint64_t nw = (n + 15) / 16;
+    return std::max<uint64_t>(1, std::min<uint64_t>(ceil_div(std::max<uint64_t>(m, 1), 64), ceil_div(256 * 1024, nw)));
+}
+// diag (n f64, from round_up(n, 16)) followed by the per-slice partial rows
+uint64_t diag_scratch_bytes(uint64_t n, uint64_t m) {
+    return (1 + diag_slices(n, m)) * round_up(std::max<uint64_t>(n, 1), 16) * sizeof(double);
+}
+
 void launch_diag_sq(const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m, const float* lut, double* diag,
                     hipStream_t st) {
     if (n == 0 || m == 0) return;
-    const uint64_t nw = (n + 15) / 16, bx = ceil_div(nw, kBlock);
-    // enough (word, slice) threads to fill 256 CUs several times over, slices of >= 64 SNPs
-    const uint64_t slices = std::max<uint64_t>(1, std::min<uint64_t>(ceil_div(m, 64), ceil_div(256 * 1024, nw)));
-    const uint64_t per = ceil_div(m, slices);
-    k_diag_sq<<<dim3((unsigned)bx, (unsigned)ceil_div(m, per)), kBlock, 0, st>>>(packed, pitch, n, m, lut, per, diag);
+    const uint64_t nw = (n + 15) / 16, bx = ceil_div(nw, kBlock), ld = round_up(n, 16);
+    const uint64_t per = ceil_div(m, diag_slices(n, m)), slices = ceil_div(m, per);
+    double* part = diag + ld;
+    k_diag_sq<<<dim3((unsigned)bx, (unsigned)slices), kBlock, 0, st>>>(packed, pitch, n, m, lut, per, ld, part);
+    SNPMI_LAUNCH_CHECK();
+    k_diag_fold<<<grid_for(n, kBlock), kBlock, 0, st>>>(n, slices, ld, part, diag);
     SNPMI_LAUNCH_CHECK();
 }
 

@@ -180,6 +180,9 @@ void launch_diag_begin(const float* K, uint64_t n, int part_rank, int part_world
                        hipStream_t st);
 void launch_diag_end(const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m, const float* lut, float* K,
                      int part_rank, int part_world, double* diag, hipStream_t st);
+// diag: diag_scratch_bytes(n, m) of device scratch (n f64 + per-slice partial rows, folded in a
+// fixed order so the diagonal is the same bits on every run)
+uint64_t diag_scratch_bytes(uint64_t n, uint64_t m);
 // launch_diag_end in two steps: the f64 squares of all iids, then the write-back of iids [i0, i1)
 void launch_diag_sq(const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m, const float* lut, double* diag,
                     hipStream_t st);
@@ -247,6 +250,8 @@ int crt_moduli();
 uint64_t crt_max_snps();
 uint64_t crt_lut_bytes(uint64_t m, uint64_t n);
 int crt_fraction_bits(uint64_t m);
+// block columns [c0, c1) of each residue chunk of the overlapped form (after_chunk below)
+std::vector<std::pair<uint64_t, uint64_t>> crt_column_chunks(uint64_t n, uint64_t res_bytes);
 // before_chunks (optional) is enqueued after the per-launch bound/moduli kernels and before the
 // first residue chunk; after_chunk(c0, c1) (optional) after the chunk whose blocks are the whole
 // block columns [c0, c1) (chunks are then cut at column boundaries, so each one's tiles are one

@@ -672,6 +672,26 @@ static CrtLog crt_logs() {
     return L;
 }
 
+// The residue chunks of launch_syrk_packed_crt's overlapped form as block columns [c0, c1): each
+// chunk holds as many whole block columns as `res_bytes` of residues allow (at least one; block
+// column c ends at block (c+1)(c+2)/2).  A function of n and res_bytes only, so every rank of an
+// overlapped collective cuts the same chunks (api.hip sum_plan).
+std::vector<std::pair<uint64_t, uint64_t>> crt_column_chunks(uint64_t n, uint64_t res_bytes) {
+    const uint64_t nb = ceil_div(n, BW), total = nb * (nb + 1) / 2;
+    const uint64_t per = std::max<uint64_t>(1, res_bytes / ((uint64_t)kR * BW * BW));
+    std::vector<std::pair<uint64_t, uint64_t>> out;
+    uint64_t col = 0;
+    for (uint64_t b0 = 0; b0 < total;) {
+        uint64_t col1 = col;
+        while (col1 < nb && (col1 + 1) * (col1 + 2) / 2 <= b0 + std::min(per, total - b0)) col1++;
+        if (col1 == col) col1 = col + 1;  // one column at least (<= nb <= per blocks in practice)
+        out.push_back({col, col1});
+        b0 = col1 * (col1 + 1) / 2;
+        col = col1;
+    }
+    return out;
+}
+
 // K_tiles (+)= Z Z^T for packed codes + f64 LUT; ws_lut: crt_lut_bytes(m); res: res_bytes of
 // scratch (>= kR * 65536); gate: device u32 set when the block must run on the f64 MFMA instead
 void launch_syrk_packed_crt(const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m, const double* lut,
@@ -696,14 +716,16 @@ void launch_syrk_packed_crt(const uint8_t* packed, uint64_t pitch, uint64_t n, u
     const uint64_t per = std::max<uint64_t>(1, res_bytes / ((uint64_t)kR * BW * BW));
     static const CrtConst cc = crt_constants();
     if (before_chunks) (*before_chunks)();
-    uint64_t col = 0;  // after_chunk: chunks end at block-column boundaries (block column c ends at (c+1)(c+2)/2)
+    // after_chunk: chunks end at block-column boundaries (crt_column_chunks)
+    const std::vector<std::pair<uint64_t, uint64_t>> cols =
+        after_chunk ? crt_column_chunks(n, res_bytes) : std::vector<std::pair<uint64_t, uint64_t>>();
+    size_t ci = 0;
     for (uint64_t b0 = 0, cnt = 0; b0 < total; b0 += cnt) {
         cnt = std::min(per, total - b0);
-        uint64_t col1 = col;
         if (after_chunk) {
-            while (col1 < nb && (col1 + 1) * (col1 + 2) / 2 <= b0 + cnt) col1++;
-            if (col1 == col) col1 = col + 1;  // one column at least (<= nb <= per blocks in practice)
-            cnt = col1 * (col1 + 1) / 2 - b0;
+            SNPMI_REQUIRE(ci < cols.size() && cols[ci].first * (cols[ci].first + 1) / 2 == b0, SNPMI_E_ARG,
+                          "crt SYRK: column chunks out of step");
+            cnt = cols[ci].second * (cols[ci].second + 1) / 2 - b0;
             SNPMI_REQUIRE(cnt <= per, SNPMI_E_ARG, "crt SYRK: one block column exceeds the residue scratch");
         }
         SNPMI_REQUIRE(cnt < (1ull << 23), SNPMI_E_ARG, "crt SYRK: chunk too large");
@@ -730,8 +752,8 @@ void launch_syrk_packed_crt(const uint8_t* packed, uint64_t pitch, uint64_t n, u
         k_crt<<<(unsigned)(cnt * 64), 256, 0, st>>>(res, b0, cnt, n, ctl, F, cc, tiles, accumulate);
         if (after_chunk) {
             SNPMI_HIP(hipGetLastError());
-            (*after_chunk)(col, col1);
-            col = col1;
+            (*after_chunk)(cols[ci].first, cols[ci].second);
+            ci++;
         }
     }
     SNPMI_HIP(hipGetLastError());

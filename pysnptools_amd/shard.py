@@ -124,14 +124,14 @@ class ShardedGrm(object):
         SYRK; the same K bit for bit).  Otherwise the two calls run one after the other."""
         if not (self.collective != "none" and self.dist is not None and self.dist.rccl):
             self.add_bed(bed, iid_index, sid_index, kind, a, b, use_stats, stats, num_threads)
-            self.combine()
+            self.combine(parts)
             return
         from pysnptools_amd.util import get_num_threads
 
         N = self.N
         ri, ci = N.index_array(iid_index), N.index_array(sid_index)
-        if len(ci) == 0:  # no SNPs on this rank: its zero tiles join the sum
-            self.combine()
+        if len(ci) == 0:  # no SNPs on this rank: its zero tiles join the others' ranged sums
+            self.combine(parts)
             return
         N.call("snpmi_grm_add_bed_reduce_" + N.suffix(self.dtype), bed.filename.encode(), bed.iid_count,
                bed.sid_count, int(bool(bed.count_A1)), N.ptr(ri), self.n, N.ptr(ci), len(ci), kind, a, b,
@@ -164,7 +164,7 @@ class ShardedGrm(object):
         self.add_packed(packed, pitch, n_sid, kind, a, b, use_stats, stats, count_a1)
         if syrk_done is not None:
             N.call("snpmi_event_record", syrk_done)
-        self.combine()
+        self.combine(parts)
 
     def tiles(self):
         """(device pointer, element count) of this rank's tiles."""
@@ -173,14 +173,20 @@ class ShardedGrm(object):
         return t, count.value
 
     # ------------------------------------------------------------------ combine + finish
-    def combine(self):
-        """The collective over xGMI (enqueued on the library stream): in-place ncclReduce onto
-        ``root`` or ncclAllReduce of the tile buffer (``Dist.sum_dev``; the host rehearsal group
-        stages the same sums through host memory).  No-op for "none"; at world size 1 it runs only
-        when a communicator exists (bench.py --force-rccl exercises the real calls)."""
+    def combine(self, parts=2):
+        """The collective over xGMI: under RCCL, ``snpmi_grm_session_sum`` -- in-place ncclReduce
+        onto ``root`` or ncclAllReduce of the tile buffer as the same ranged calls the overlapped
+        ``add_*_combine(parts=parts)`` issue (a function of n, dtype and ``parts`` only), so a rank
+        that owns no SNPs, or adds them unoverlapped, pairs its calls with every other rank's.  The
+        host rehearsal group stages one sum of the whole buffer through host memory
+        (``Dist.sum_dev``).  No-op for "none"; at world size 1 it runs only when a communicator
+        exists (bench.py --force-rccl exercises the real calls)."""
         if self.collective == "none" or self.dist is None or not self.dist.can_reduce:
             return
         if not self.dist.rccl and self.dist.world == 1:
+            return
+        if self.dist.rccl:
+            self.N.call("snpmi_grm_session_sum", 1 if self.collective == "reduce" else 2, self.root, int(parts))
             return
         t, count = self.tiles()
         self.dist.sum_dev(t, count, self.dtype, self.root if self.collective == "reduce" else None)

@@ -232,7 +232,8 @@ def _read_and_standardize(reader, standardizer, order="F", dtype=np.float64, for
     ``snpmi_bed_read_standardize_*`` computes each SNP's stats from its code counts and decodes
     straight to standardized values through a per-SNP table (the same f64 formula, so the values and
     stats are bit-identical to the two calls), writing the values once instead of decoding them and
-    then reading + rewriting them.  Other readers / standardizers take the two calls."""
+    then reading + rewriting them.  Other readers / standardizers, and ``force_python_only=True``
+    (the caller asked for the reference's separate read + standardize steps), take the two calls."""
     from pysnptools_amd import hbm
     from pysnptools_amd.snpreader.bed import Bed
     from pysnptools_amd.snpreader.snpdata import SnpData
@@ -242,7 +243,7 @@ def _read_and_standardize(reader, standardizer, order="F", dtype=np.float64, for
     dtype = np.dtype(dtype)
     args = _std_args(standardizer) if dtype in (np.float32, np.float64) else None
     base, rows, cols = _resolve(reader) if args is not None and args[0] != N.STD_NONE else (None, None, None)
-    if not isinstance(base, Bed):
+    if force_python_only or not isinstance(base, Bed):
         return reader.read(order=order, dtype=dtype).standardize(standardizer, return_trained=True,
                                                                  force_python_only=force_python_only,
                                                                  num_threads=num_threads)

@@ -40,3 +40,24 @@ def test_foreign_checkpoint_is_refused_before_any_device_call(tmp_path):
         C._restore(ck, _meta(str(bed)), np.float32)
     assert C._restore(str(tmp_path / "none"), _meta(str(bed)), np.float32) is None
     assert os.path.exists(ck + ".json")  # a refused checkpoint is left in place
+
+
+def test_settings_only_difference_names_the_setting(tmp_path):
+    """A checkpoint of the same GRM written under other kernel settings (here the exact-diagonal
+    switch, which changes f32 K bits) is refused with an error naming the settings; one written
+    before the settings were recorded likewise."""
+    bed = tmp_path / "x.bed"
+    bed.write_bytes(b"\x6c\x1b\x01" + bytes(20))
+    meta = _meta(str(bed))
+    assert set(meta["settings"]) == {"f32_seg", "f32_diag", "f32_syrk"}
+    ck = str(tmp_path / "ck")
+    other = dict(meta, settings=dict(meta["settings"], f32_diag=1 - meta["settings"]["f32_diag"]))
+    with open(ck + ".json", "w") as f:
+        json.dump(dict(other, next_block=2), f)
+    with pytest.raises(ValueError, match="other GRM kernel settings"):
+        C._restore(ck, meta, np.float32)
+    legacy = {k: v for k, v in meta.items() if k != "settings"}
+    with open(ck + ".json", "w") as f:
+        json.dump(dict(legacy, next_block=2), f)
+    with pytest.raises(ValueError, match="none recorded"):
+        C._restore(ck, meta, np.float32)

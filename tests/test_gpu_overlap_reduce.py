@@ -173,3 +173,61 @@ def test_grm_sharded_bed_overlapped_world1(rccl1, tmp_path, dtype, collective):
     assert groups >= 2, groups
     assert np.array_equal(K1, K0)
     np.testing.assert_array_equal(t1.stats, t0.stats)
+
+
+def _calls():
+    return N.kernel_variant("overlap_calls"), N.kernel_variant("overlap_sig")
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+@pytest.mark.parametrize("n", [30000, 6144])
+def test_collective_calls_do_not_depend_on_the_ranks_snp_count(rccl1, n, dtype):
+    """every rank must issue the same RCCL calls.  Ranks' spans differ by one SNP
+    and may straddle a split-K threshold (n = 6144: 1500 SNPs fit one 256-block grid round unsplit,
+    3000 SNPs would pick a split grid), and a rank may own no SNPs at all -- the ranged sums
+    (count and element ranges) are the same in every case, and K is unchanged by how they ran."""
+    sigs = {}
+    for m in (1, 700, 1500, 3000, 70000):
+        packed, pitch = _data(n, m, 67)
+        try:
+            ref = _run(n, m, packed, pitch, N.STD_UNIT, 0.0, 0.0, False, None, None, dtype=dtype)
+            got = _run(n, m, packed, pitch, N.STD_UNIT, 0.0, 0.0, False, 2, "allreduce", dist=rccl1, dtype=dtype)
+            sigs[m] = _calls()
+        finally:
+            packed.free()
+        assert np.array_equal(ref, got), m
+    g = ShardedGrm(n, dtype, rccl1, "allreduce")  # a rank without SNPs: its zero tiles join the sums
+    try:
+        g.combine(2)
+        sigs[0] = _calls()
+        assert not np.any(_tiles(g))
+    finally:
+        g.abort()
+    assert len(set(sigs.values())) == 1, sigs
+    calls = sigs[0][0]
+    nb = (n + 255) // 256
+    if dtype == np.float32:
+        assert calls == (2 if n == 30000 else 1), calls  # n = 6144 picks split grids: no column groups
+    else:
+        assert calls >= (2 if nb * (nb + 1) // 2 * 15 * 65536 > (4 << 30) else 1)
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+def test_bed_rank_without_snps_issues_the_same_calls(rccl1, tmp_path, dtype):
+    """The .bed path: a rank whose span is empty (add_bed_combine with no SNPs) issues the calls of a
+    rank that streams SNPs."""
+    from pysnptools_amd.snpreader import Bed
+
+    path = str(tmp_path / "e")
+    _write_bed(path, 30000, 700, 71)
+    bed = Bed(path, count_A1=False)
+    sigs = []
+    for cols in (np.arange(700, dtype=np.uint64), np.arange(3, dtype=np.uint64), np.zeros(0, dtype=np.uint64)):
+        g = ShardedGrm(30000, dtype, rccl1, "reduce")
+        stats = np.zeros((len(cols), 2), dtype=dtype)
+        try:
+            g.add_bed_combine(bed, None, cols, N.STD_UNIT, 0.0, 0.0, 0, stats)
+            sigs.append(_calls())
+        finally:
+            g.abort()
+    assert sigs[0] == sigs[1] == sigs[2], sigs
