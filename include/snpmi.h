@@ -328,15 +328,25 @@ int snpmi_dev_repack(const uint8_t* src, uint64_t src_pitch, uint64_t n_src_iid,
 uint64_t snpmi_grm_tile_bytes(uint64_t n_iid, int dtype);
 int snpmi_dev_syrk_packed(const uint8_t* packed, uint64_t pitch, uint64_t n_iid, uint64_t n_sid,
                           const void* lut, int dtype, void* K_tiles, int accumulate);
-/* cfg5 mode (K too large to replicate): rank `part_rank` of `part_world` owns the
- * 256x256 blocks L = b*part_world + part_rank (b = 0..n_local-1) of the upper-triangle block
- * list of the n x n K and stores each as a full row-major 256x256 f32 block at blocks + b*65536.
- * Every rank reads all SNPs; no reduction is needed. */
+/* cfg5 mode (K too large to replicate): the upper triangle of the n x n K as 256x256
+ * blocks, grouped into S x S-block supertiles (S = 16 once there are >= 4 supertiles per part,
+ * else the largest power of two that gives as many) dealt round-robin in triangular supertile
+ * order: supertile T = J(J+1)/2 + I belongs to part T mod part_world.  Part `part_rank` stores its
+ * n_local blocks densely, each a full row-major 256x256 f32 block at blocks + b*65536, in its
+ * walk order (its supertiles in T order, inside each block column by block column);
+ * snpmi_grm_part_coords gives block b's (row0, col0), snpmi_grm_part_coords_all all of them
+ * ([n_local][2]).  Every rank reads all SNPs; no reduction is needed.  The K sub-matrices the
+ * reference's KernelReader serves (kernelreader.py:245-302) are read back from these blocks. */
 uint64_t snpmi_grm_part_blocks(uint64_t n_iid, int part_rank, int part_world);
 int snpmi_grm_part_coords(uint64_t n_iid, int part_rank, int part_world, uint64_t local_block,
                           uint64_t* row0, uint64_t* col0);
+int snpmi_grm_part_coords_all(uint64_t n_iid, int part_rank, int part_world, uint64_t* coords);
 int snpmi_dev_syrk_packed_part(const uint8_t* packed, uint64_t pitch, uint64_t n_iid, uint64_t n_sid,
                                const void* lut, int part_rank, int part_world, void* blocks, int accumulate);
+/* the same in float64 (the reference's default GRM dtype, snpreader.py:528,623): f64 LUT [n_sid][4],
+ * blocks of 256x256 f64; computed on the int8 MFMA as exact residue products + CRT */
+int snpmi_dev_syrk_packed_part_f64(const uint8_t* packed, uint64_t pitch, uint64_t n_iid, uint64_t n_sid,
+                                   const double* lut, int part_rank, int part_world, double* blocks, int accumulate);
 /* cfg5 from a .bed file (SnpReader._read_kernel, snpreader.py:623-668, with K partitioned as
  * above): this rank streams every selected SNP, standardizes it with stats over all selected
  * iids (stats in/out as snpmi_grm_bed_f32), accumulates only its own blocks and writes them to
@@ -346,6 +356,24 @@ int snpmi_grm_part_bed_f32(const char* path, uint64_t n_iid, uint64_t n_sid, int
                            const uint64_t* iid_idx, uint64_t n_out_iid, const uint64_t* sid_idx, uint64_t n_out_sid,
                            int std_kind, double a, double b, int use_stats, float* stats, int part_rank,
                            int part_world, float* blocks_out, int num_threads);
+int snpmi_grm_part_bed_f64(const char* path, uint64_t n_iid, uint64_t n_sid, int count_a1,
+                           const uint64_t* iid_idx, uint64_t n_out_iid, const uint64_t* sid_idx, uint64_t n_out_sid,
+                           int std_kind, double a, double b, int use_stats, double* stats, int part_rank,
+                           int part_world, double* blocks_out, int num_threads);
+/* K[ri[r], ci[c]] (ri/ci host arrays, NULL = identity; order_c: out row-major) restricted to the
+ * blocks part `part_rank` owns, 0 elsewhere, times `scale` (DiagKtoN) -- summed over the parts the
+ * sub-matrix; out host or device.  The reader of a partitioned K (shard.PartitionedKernel, the
+ * KernelReader._read of kernelreader.py:245-302 / snpkernel.py:78-101 for a K that is not
+ * replicated).  IndexError for indices >= n. */
+int snpmi_grm_part_extract_f32(const float* blocks, uint64_t n_iid, int part_rank, int part_world, const uint64_t* ri,
+                               uint64_t nr, const uint64_t* ci, uint64_t nc, int order_c, double scale, float* out);
+int snpmi_grm_part_extract_f64(const double* blocks, uint64_t n_iid, int part_rank, int part_world, const uint64_t* ri,
+                               uint64_t nr, const uint64_t* ci, uint64_t nc, int order_c, double scale, double* out);
+/* this part's share of trace(K) (DiagKtoN over a partitioned K, diag_K_to_N.py:54-59) */
+int snpmi_grm_part_trace_f32(const float* blocks, uint64_t n_iid, int part_rank, int part_world, double* trace);
+int snpmi_grm_part_trace_f64(const double* blocks, uint64_t n_iid, int part_rank, int part_world, double* trace);
+/* free / total HBM of the current device (hipMemGetInfo): whether a replicated K fits */
+int snpmi_device_memory(uint64_t* free_bytes, uint64_t* total_bytes);
 int snpmi_dev_syrk_dense(const void* Z, uint64_t ldz, uint64_t n_iid, uint64_t n_sid, int dtype,
                          void* K_tiles, int accumulate);
 /* tiles -> K[ri[r], ci[c]] (ri/ci NULL = identity), scaled by `scale` */

@@ -38,7 +38,7 @@ def build():
 def lib():
     global _LIB
     if _LIB is None:
-        path = os.path.join(_HERE, "liboracle.so")
+        path = os.environ.get("ORACLE_LIB") or os.path.join(_HERE, "liboracle.so")  # tools/sanitize.sh
         if not os.path.exists(path):
             build()
         L = ctypes.CDLL(path)

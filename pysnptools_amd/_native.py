@@ -114,9 +114,18 @@ _SIGS = {
     "snpmi_dev_syrk_packed": [_vp, _u64, _u64, _u64, _vp, _i32, _vp, _i32],
     "snpmi_grm_part_blocks": [_u64, _i32, _i32],
     "snpmi_grm_part_coords": [_u64, _i32, _i32, _u64, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)],
+    "snpmi_grm_part_coords_all": [_u64, _i32, _i32, _vp],
     "snpmi_dev_syrk_packed_part": [_vp, _u64, _u64, _u64, _vp, _i32, _i32, _vp, _i32],
     "snpmi_grm_part_bed_f32": [ctypes.c_char_p, _u64, _u64, _i32, _vp, _u64, _vp, _u64, _i32, ctypes.c_double,
                                ctypes.c_double, _i32, _vp, _i32, _i32, _vp, _i32],
+    "snpmi_grm_part_bed_f64": [ctypes.c_char_p, _u64, _u64, _i32, _vp, _u64, _vp, _u64, _i32, ctypes.c_double,
+                               ctypes.c_double, _i32, _vp, _i32, _i32, _vp, _i32],
+    "snpmi_dev_syrk_packed_part_f64": [_vp, _u64, _u64, _u64, _vp, _i32, _i32, _vp, _i32],
+    "snpmi_grm_part_extract_f32": [_vp, _u64, _i32, _i32, _vp, _u64, _vp, _u64, _i32, _f64, _vp],
+    "snpmi_grm_part_extract_f64": [_vp, _u64, _i32, _i32, _vp, _u64, _vp, _u64, _i32, _f64, _vp],
+    "snpmi_grm_part_trace_f32": [_vp, _u64, _i32, _i32, _dp],
+    "snpmi_grm_part_trace_f64": [_vp, _u64, _i32, _i32, _dp],
+    "snpmi_device_memory": [ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)],
     "snpmi_dev_syrk_dense": [_vp, _u64, _u64, _u64, _i32, _vp, _i32],
     "snpmi_dev_grm_extract": [_vp, _u64, _i32, _vp, _u64, _vp, _u64, _i32, _f64, _vp],
     "snpmi_dev_grm_trace": [_vp, _u64, _i32, _dp],

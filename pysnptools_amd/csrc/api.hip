@@ -107,9 +107,9 @@ void Device::release() {
         order_tab[x] = nullptr;
         order_nb[x] = 0;
     }
-    if (part_order_tab) (void)hipFree(part_order_tab);
-    part_order_tab = nullptr;
-    for (int i = 0; i < 4; i++) part_order_key[i] = 0;
+    if (part_tab) (void)hipFree(part_tab);
+    part_tab = nullptr;
+    for (int i = 0; i < 3; i++) part_key[i] = 0;
 }
 
 // pinned staging (two slots so a chunk can be gathered while the previous one uploads)
@@ -779,9 +779,9 @@ static void syrk_packed_auto(Device& d, const uint8_t* packed, uint64_t pitch, u
     }
     if (dt == SNPMI_DT_F32 && g_diag_exact && m > 0 && n > 0) {  // exact diagonal around the SYRK
         double* diag = (double*)d.get(Device::S_DIAG, diag_scratch_bytes(n, m));
-        launch_diag_begin((const float*)tiles, n, 0, 0, accumulate, diag, d.stream);
+        launch_diag_begin((const float*)tiles, n, nullptr, accumulate, diag, d.stream);
         syrk_packed_f32_body(d, packed, pitch, n, m, lut, dt, tiles, accumulate);
-        launch_diag_end(packed, pitch, n, m, (const float*)lut, (float*)tiles, 0, 0, diag, d.stream);
+        launch_diag_end(packed, pitch, n, m, (const float*)lut, (float*)tiles, nullptr, diag, d.stream);
         return;
     }
     syrk_packed_f32_body(d, packed, pitch, n, m, lut, dt, tiles, accumulate);
@@ -821,12 +821,50 @@ static void syrk_packed_part_auto(Device& d, const uint8_t* packed, uint64_t pit
                                   const float* lut, int rank, int world, void* blocks, int accumulate) {
     if (g_diag_exact && m > 0 && n > 0) {  // exact diagonal of the part's diagonal blocks
         double* diag = (double*)d.get(Device::S_DIAG, diag_scratch_bytes(n, m));
-        launch_diag_begin((const float*)blocks, n, rank, world, accumulate, diag, d.stream);
+        const int32_t* dslot = part_tables(ceil_div(n, 256), rank, world).dslot;
+        launch_diag_begin((const float*)blocks, n, dslot, accumulate, diag, d.stream);
         syrk_packed_part_body(d, packed, pitch, n, m, lut, rank, world, blocks, accumulate);
-        launch_diag_end(packed, pitch, n, m, lut, (float*)blocks, rank, world, diag, d.stream);
+        launch_diag_end(packed, pitch, n, m, lut, (float*)blocks, dslot, diag, d.stream);
         return;
     }
     syrk_packed_part_body(d, packed, pitch, n, m, lut, rank, world, blocks, accumulate);
+}
+
+// f64 part (cfg5 in the reference's default dtype): the int8 CRT path over the part's layout
+// (launch_syrk_packed_crt with the layout table: residue chunks of the part's blocks, K written as
+// dense f64 blocks), its f64-MFMA fallback gated on the non-finite flag; hook "f64" = 1: every
+// block on the f64 MFMA
+static void syrk_packed_part_f64(Device& d, const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m,
+                                 const double* lut, int rank, int world, double* blocks, int accumulate) {
+    const uint64_t nloc = grm_part_blocks(n, rank, world);
+    if (nloc == 0) return;
+    SNPMI_REQUIRE(4 * nloc < (1ull << 31), SNPMI_E_ARG, "too many GRM blocks for one launch");
+    SNPMI_REQUIRE(pitch % 64 == 0 && pitch * 4 >= ceil_div(n, 256) * 256, SNPMI_E_ARG,
+                  "packed pitch must cover round_up(n, 256) iids");
+    if (m == 0) {
+        if (!accumulate) SNPMI_HIP(hipMemsetAsync(blocks, 0, nloc * 256 * 256 * sizeof(double), d.stream));
+        return;
+    }
+    const PartTables pt = part_tables(ceil_div(n, 256), rank, world);
+    const uint64_t step = crt_max_snps();
+    if (!use_crt(SNPMI_DT_F64)) {
+        for (uint64_t s0 = 0; s0 < m; s0 += step)
+            launch_syrk_packed_f64_gated(packed + s0 * pitch, pitch, n, std::min(step, m - s0), lut + 4 * s0, blocks,
+                                         accumulate || s0 > 0, nullptr, d.stream, pt.tab, nloc);
+        return;
+    }
+    const uint64_t res_bytes = std::min<uint64_t>(nloc * (uint64_t)crt_moduli() * 65536, 4ull << 30);
+    uint8_t* res = (uint8_t*)d.get(Device::S_ZBLK, res_bytes);
+    void* ws = d.get(Device::S_LUT3, crt_lut_bytes(std::min(m, step), n));
+    unsigned long long* rec = crt_record(d);
+    for (uint64_t s0 = 0; s0 < m; s0 += step) {
+        const uint64_t cnt = std::min(step, m - s0);
+        const int acc = accumulate || s0 > 0;
+        launch_syrk_packed_crt(packed + s0 * pitch, pitch, n, cnt, lut + 4 * s0, blocks, acc, ws, res, res_bytes, rec,
+                               d.stream, nullptr, nullptr, pt.tab, nloc);
+        launch_syrk_packed_f64_gated(packed + s0 * pitch, pitch, n, cnt, lut + 4 * s0, blocks, acc, (const int*)ws + 1,
+                                     d.stream, pt.tab, nloc);
+    }
 }
 
 static void syrk_packed_part_body(Device& d, const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m,
@@ -1006,29 +1044,45 @@ const uint32_t* packed_block_order(uint64_t nb) {
     return dense_order(device(), nb, false);
 }
 
-// the cfg5 part kernel's block order: the supertile table restricted to the blocks of part
-// `rank` of `world` (part_supertile_order), cached per (nb, rank, world) on the device
-const uint32_t* part_block_order(uint64_t nb, int rank, int world) {
+// the cfg5 part layout of part `rank` of `world` on the current device (syrk.hip part_layout):
+// one allocation = the layout table (u32 per local block) + the diagonal-slot table (i32 per block
+// column) + the block-slot table (i32 per upper-triangle block), cached per (nb, rank, world)
+PartTables part_tables(uint64_t nb, int rank, int world) {
     std::lock_guard<std::recursive_mutex> lk(g_call_mutex);
     Device& d = device();
-    const uint64_t S = g_part_triangular == 2 ? 16 : 64;
-    const uint64_t key[4] = {nb, (uint64_t)rank, (uint64_t)world, S};
-    if (!d.part_order_tab || d.part_order_key[0] != key[0] || d.part_order_key[1] != key[1] ||
-        d.part_order_key[2] != key[2] || d.part_order_key[3] != key[3]) {
+    const uint64_t key[3] = {nb, (uint64_t)rank, (uint64_t)world};
+    const uint64_t ntab = grm_part_blocks(nb * 256, rank, world), off = round_up(std::max<uint64_t>(ntab, 1), 64);
+    const uint64_t off2 = off + round_up(std::max<uint64_t>(nb, 1), 64), total = nb * (nb + 1) / 2;
+    if (!d.part_tab || d.part_key[0] != key[0] || d.part_key[1] != key[1] || d.part_key[2] != key[2]) {
         std::vector<uint32_t> tab;
-        part_supertile_order(nb, rank, world, tab, S);
-        if (d.part_order_tab) SNPMI_HIP(hipFree(d.part_order_tab));
-        d.part_order_tab = nullptr;
-        for (int i = 0; i < 4; i++) d.part_order_key[i] = 0;
-        if (tab.empty()) return nullptr;
-        if (hipMalloc(&d.part_order_tab, tab.size() * sizeof(uint32_t)) != hipSuccess) {
-            (void)hipGetLastError();
-            throw Error(SNPMI_E_NOMEM, "hipMalloc of the part block order table failed");
+        part_layout(nb, rank, world, tab);
+        SNPMI_REQUIRE(tab.size() == ntab, SNPMI_E_ARG, "part layout size mismatch");
+        std::vector<int32_t> dslot(nb, -1), lslot(total, -1);
+        for (uint64_t w = 0; w < tab.size(); w++) {
+            const uint64_t bi = tab[w] & 0xffffu, bj = tab[w] >> 16;
+            if (bi == bj) dslot[bj] = (int32_t)w;
+            lslot[bj * (bj + 1) / 2 + bi] = (int32_t)w;
         }
-        SNPMI_HIP(hipMemcpy(d.part_order_tab, tab.data(), tab.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
-        for (int i = 0; i < 4; i++) d.part_order_key[i] = key[i];
+        std::vector<uint32_t> buf(off2 + total);
+        std::copy(tab.begin(), tab.end(), buf.begin());
+        std::memcpy(buf.data() + off, dslot.data(), nb * sizeof(int32_t));
+        std::memcpy(buf.data() + off2, lslot.data(), total * sizeof(int32_t));
+        if (d.part_tab) SNPMI_HIP(hipFree(d.part_tab));
+        d.part_tab = nullptr;
+        for (int i = 0; i < 3; i++) d.part_key[i] = 0;
+        if (hipMalloc(&d.part_tab, buf.size() * sizeof(uint32_t)) != hipSuccess) {
+            (void)hipGetLastError();
+            d.part_tab = nullptr;
+            throw Error(SNPMI_E_NOMEM, "hipMalloc of the part layout table failed");
+        }
+        SNPMI_HIP(hipMemcpy(d.part_tab, buf.data(), buf.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+        for (int i = 0; i < 3; i++) d.part_key[i] = key[i];
     }
-    return d.part_order_tab;
+    PartTables t;
+    t.tab = (const uint32_t*)d.part_tab;
+    t.dslot = (const int32_t*)((const uint32_t*)d.part_tab + off);
+    t.lslot = (const int32_t*)((const uint32_t*)d.part_tab + off2);
+    return t;
 }
 
 // dense GRM operand on the device: f32 with n >= 4096 and the default variant takes the fp16x2
@@ -1369,14 +1423,14 @@ static int grouped_reduce_f32(Device& d, const uint8_t* src, uint64_t pitch, uin
     H2Lut h2;
     const uint32_t* l3 = lut_bf3(d, lut, cnt, &h2);
     double* diag = (double*)d.get(Device::S_DIAG, diag_scratch_bytes(n, cnt));
-    launch_diag_begin(tiles, n, 0, 0, acc, diag, d.stream);
+    launch_diag_begin(tiles, n, nullptr, acc, diag, d.stream);
     launch_diag_sq(src, pitch, n, cnt, lut, diag, d.stream);
     const auto groups = column_groups(ceil_div(n, 256), parts);
     OverlapSums sums(d, collective, rt, SNPMI_DT_F32);
     for (const auto& gr : groups) {
         launch_syrk_packed_h2_cols(src, pitch, n, cnt, l3, tiles, acc, d.stream, &h2, gr.L0, gr.L1);
         // block columns [c0, c1): diagonal iids [256 c0, 256 c1), 128-tile columns [2 c0, 2 c1)
-        launch_diag_patch(tiles, n, 256 * gr.c0, 256 * gr.c1, 0, 0, diag, d.stream);
+        launch_diag_patch(tiles, n, 256 * gr.c0, 256 * gr.c1, nullptr, diag, d.stream);
         sums.range(tiles, n, 2 * gr.c0, 2 * gr.c1);
     }
     if (syrk_done) SNPMI_HIP(hipEventRecord(syrk_done, d.stream));
@@ -1596,7 +1650,6 @@ int snpmi_set_kernel_variant(const char* kernel, int variant) {
         if (std::strcmp(kernel, "decode") == 0) g_variant_decode = variant;
         else if (std::strcmp(kernel, "std") == 0) g_variant_std = variant;
         else if (std::strcmp(kernel, "diag") == 0) g_diag_exact = variant != 0;
-        else if (std::strcmp(kernel, "part_order") == 0) g_part_triangular = variant;
         else if (std::strcmp(kernel, "extract") == 0) g_variant_extract = variant;
         else if (std::strcmp(kernel, "syrk") == 0) {
 #ifndef SNPMI_UBENCH
@@ -1629,7 +1682,6 @@ int snpmi_get_kernel_variant(const char* kernel, int* variant) {
         if (std::strcmp(kernel, "decode") == 0) *variant = g_variant_decode;
         else if (std::strcmp(kernel, "std") == 0) *variant = g_variant_std;
         else if (std::strcmp(kernel, "diag") == 0) *variant = g_diag_exact;
-        else if (std::strcmp(kernel, "part_order") == 0) *variant = g_part_triangular;
         else if (std::strcmp(kernel, "overlap_groups") == 0) *variant = g_last_groups;
         else if (std::strcmp(kernel, "overlap_calls") == 0) *variant = g_last_sum_calls;
         else if (std::strcmp(kernel, "overlap_sig") == 0) *variant = (int)(g_last_sum_sig & 0x7fffffff);
@@ -2248,17 +2300,42 @@ uint64_t snpmi_grm_part_blocks(uint64_t n_iid, int part_rank, int part_world) {
     return grm_part_blocks(n_iid, part_rank, part_world);
 }
 
+// host copy of the last part layout asked for (snpmi_grm_part_coords is called per block)
+static std::mutex g_layout_mutex;
+static std::vector<uint32_t> g_layout;
+static uint64_t g_layout_key[3] = {~0ull, 0, 0};
+static const std::vector<uint32_t>& host_layout(uint64_t nb, int rank, int world) {
+    if (g_layout_key[0] != nb || g_layout_key[1] != (uint64_t)rank || g_layout_key[2] != (uint64_t)world) {
+        part_layout(nb, rank, world, g_layout);
+        g_layout_key[0] = nb;
+        g_layout_key[1] = (uint64_t)rank;
+        g_layout_key[2] = (uint64_t)world;
+    }
+    return g_layout;
+}
+
 int snpmi_grm_part_coords(uint64_t n_iid, int part_rank, int part_world, uint64_t local_block, uint64_t* row0,
                           uint64_t* col0) {
     return guarded([&] {
         SNPMI_REQUIRE(part_world >= 1 && part_rank >= 0 && part_rank < part_world, SNPMI_E_ARG, "bad partition");
-        SNPMI_REQUIRE(local_block < grm_part_blocks(n_iid, part_rank, part_world), SNPMI_E_INDEX, "block out of range");
-        const uint64_t L = local_block * part_world + part_rank;
-        uint64_t j = (uint64_t)((std::sqrt(8.0 * (double)L + 1.0) - 1.0) * 0.5);
-        while ((j + 1) * (j + 2) / 2 <= L) j++;
-        while (j * (j + 1) / 2 > L) j--;
-        if (row0) *row0 = (L - j * (j + 1) / 2) * 256;
-        if (col0) *col0 = j * 256;
+        std::lock_guard<std::mutex> lk(g_layout_mutex);
+        const auto& tab = host_layout(ceil_div(n_iid, 256), part_rank, part_world);
+        SNPMI_REQUIRE(local_block < tab.size(), SNPMI_E_INDEX, "block out of range");
+        if (row0) *row0 = (uint64_t)(tab[local_block] & 0xffffu) * 256;
+        if (col0) *col0 = (uint64_t)(tab[local_block] >> 16) * 256;
+    });
+}
+
+int snpmi_grm_part_coords_all(uint64_t n_iid, int part_rank, int part_world, uint64_t* coords) {
+    return guarded([&] {
+        SNPMI_REQUIRE(part_world >= 1 && part_rank >= 0 && part_rank < part_world, SNPMI_E_ARG, "bad partition");
+        std::lock_guard<std::mutex> lk(g_layout_mutex);
+        const auto& tab = host_layout(ceil_div(n_iid, 256), part_rank, part_world);
+        SNPMI_REQUIRE(coords != nullptr || tab.empty(), SNPMI_E_ARG, "coords is NULL");
+        for (uint64_t w = 0; w < tab.size(); w++) {
+            coords[2 * w] = (uint64_t)(tab[w] & 0xffffu) * 256;
+            coords[2 * w + 1] = (uint64_t)(tab[w] >> 16) * 256;
+        }
     });
 }
 
@@ -2266,32 +2343,63 @@ int snpmi_grm_part_coords(uint64_t n_iid, int part_rank, int part_world, uint64_
 // the .bed (stats need all iids of a SNP; each rank computes them itself -- no exchange) and
 // accumulates only its own 256x256 K blocks (snpmi_grm_part_coords) in HBM, then copies them to
 // blocks_out (n_local x 65536 f32, row-major blocks; may be a memory-mapped file).
+}  // extern "C"
+
+namespace snpmi {
+template <typename T>
+static void grm_part_bed_impl(const char* path, uint64_t n_iid, uint64_t n_sid, int count_a1, const uint64_t* iid_idx,
+                              uint64_t n_out_iid, const uint64_t* sid_idx, uint64_t n_out_sid, int std_kind, double a,
+                              double b, int use_stats, T* stats, int part_rank, int part_world, T* blocks_out,
+                              int num_threads) {
+    std::lock_guard<std::recursive_mutex> lk(g_call_mutex);
+    SNPMI_REQUIRE(part_world >= 1 && part_rank >= 0 && part_rank < part_world, SNPMI_E_ARG, "bad rank / world");
+    const uint64_t n_out = iid_idx ? n_out_iid : n_iid;
+    const uint64_t nloc = grm_part_blocks(n_out, part_rank, part_world);
+    SNPMI_REQUIRE(blocks_out != nullptr || nloc == 0, SNPMI_E_ARG, "blocks_out is NULL");
+    Device& d = device();
+    const uint64_t bytes = std::max<uint64_t>(nloc, 1) * 256 * 256 * sizeof(T);
+    // blocks_out in device memory: the SYRK accumulates into it directly (K stays in HBM, no
+    // scratch, no copy-out); host memory: scratch tiles + a pinned-bounce copy at the end
+    const bool dev_out = nloc && is_device_ptr(d, blocks_out);
+    T* blocks = dev_out ? blocks_out : (T*)d.get(Device::S_TILES, bytes);
+    const bool wrote = grm_stream_bed<T>(
+        d, true, path, n_iid, n_sid, count_a1, iid_idx, n_out_iid, sid_idx, n_out_sid, std_kind, a, b, use_stats,
+        stats, num_threads,
+        [&](const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t cnt, const T* lut, bool acc) {
+            if constexpr (std::is_same<T, double>::value)
+                syrk_packed_part_f64(d, packed, pitch, n, cnt, lut, part_rank, part_world, blocks, acc);
+            else
+                syrk_packed_part_auto(d, packed, pitch, n, cnt, lut, part_rank, part_world, blocks, acc);
+        });
+    if (!wrote) SNPMI_HIP(hipMemsetAsync(blocks, 0, dev_out ? nloc * 256 * 256 * sizeof(T) : bytes, d.stream));
+    const size_t bb = 256 * 256 * sizeof(T);  // one block per "row" of the pinned-bounce copy
+    if (nloc && !dev_out) d2h_rows(d, blocks_out, bb, blocks, bb, bb, nloc, resolve_threads(num_threads));
+    SNPMI_HIP(hipStreamSynchronize(d.stream));
+}
+}  // namespace snpmi
+
+extern "C" {
+
+// cfg5 from a file (K too large to replicate): rank part_rank of part_world streams EVERY SNP of
+// the .bed (stats need all iids of a SNP; each rank computes them itself -- no exchange) and
+// accumulates only its own 256x256 K blocks (snpmi_grm_part_coords) in HBM, then copies them to
+// blocks_out (n_local x 65536 values, row-major blocks; may be a memory-mapped file).
 int snpmi_grm_part_bed_f32(const char* path, uint64_t n_iid, uint64_t n_sid, int count_a1, const uint64_t* iid_idx,
                            uint64_t n_out_iid, const uint64_t* sid_idx, uint64_t n_out_sid, int std_kind, double a,
                            double b, int use_stats, float* stats, int part_rank, int part_world, float* blocks_out,
                            int num_threads) {
     return guarded([&] {
-        std::lock_guard<std::recursive_mutex> lk(g_call_mutex);
-        SNPMI_REQUIRE(part_world >= 1 && part_rank >= 0 && part_rank < part_world, SNPMI_E_ARG, "bad rank / world");
-        const uint64_t n_out = iid_idx ? n_out_iid : n_iid;
-        const uint64_t nloc = grm_part_blocks(n_out, part_rank, part_world);
-        SNPMI_REQUIRE(blocks_out != nullptr || nloc == 0, SNPMI_E_ARG, "blocks_out is NULL");
-        Device& d = device();
-        const uint64_t bytes = std::max<uint64_t>(nloc, 1) * 256 * 256 * sizeof(float);
-        // blocks_out in device memory: the SYRK accumulates into it directly (K stays in HBM, no
-        // scratch, no copy-out); host memory: scratch tiles + a pinned-bounce copy at the end
-        const bool dev_out = nloc && is_device_ptr(d, blocks_out);
-        float* blocks = dev_out ? blocks_out : (float*)d.get(Device::S_TILES, bytes);
-        const bool wrote = grm_stream_bed<float>(
-            d, true, path, n_iid, n_sid, count_a1, iid_idx, n_out_iid, sid_idx, n_out_sid, std_kind, a, b, use_stats,
-            stats, num_threads,
-            [&](const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t cnt, const float* lut, bool acc) {
-                syrk_packed_part_auto(d, packed, pitch, n, cnt, lut, part_rank, part_world, blocks, acc);
-            });
-        if (!wrote) SNPMI_HIP(hipMemsetAsync(blocks, 0, dev_out ? nloc * 256 * 256 * sizeof(float) : bytes, d.stream));
-        const size_t bb = 256 * 256 * sizeof(float);  // one block per "row" of the pinned-bounce copy
-        if (nloc && !dev_out) d2h_rows(d, blocks_out, bb, blocks, bb, bb, nloc, resolve_threads(num_threads));
-        SNPMI_HIP(hipStreamSynchronize(d.stream));
+        grm_part_bed_impl<float>(path, n_iid, n_sid, count_a1, iid_idx, n_out_iid, sid_idx, n_out_sid, std_kind, a, b,
+                                 use_stats, stats, part_rank, part_world, blocks_out, num_threads);
+    });
+}
+int snpmi_grm_part_bed_f64(const char* path, uint64_t n_iid, uint64_t n_sid, int count_a1, const uint64_t* iid_idx,
+                           uint64_t n_out_iid, const uint64_t* sid_idx, uint64_t n_out_sid, int std_kind, double a,
+                           double b, int use_stats, double* stats, int part_rank, int part_world, double* blocks_out,
+                           int num_threads) {
+    return guarded([&] {
+        grm_part_bed_impl<double>(path, n_iid, n_sid, count_a1, iid_idx, n_out_iid, sid_idx, n_out_sid, std_kind, a,
+                                  b, use_stats, stats, part_rank, part_world, blocks_out, num_threads);
     });
 }
 
@@ -2303,6 +2411,97 @@ int snpmi_dev_syrk_packed_part(const uint8_t* packed, uint64_t pitch, uint64_t n
         SNPMI_REQUIRE(pitch % 64 == 0 && pitch >= ceil_div(n_iid, 4), SNPMI_E_ARG, "pitch must be snpmi_packed_pitch");
         syrk_packed_part_auto(device(), packed, pitch, n_iid, n_sid, (const float*)lut, part_rank, part_world, blocks,
                               accumulate);
+    });
+}
+
+}  // extern "C"
+
+namespace snpmi {
+// K[ri, ci] restricted to part `part_rank`'s blocks (the rest 0): the parts' outputs summed over
+// the ranks are the sub-matrix (snpmi_grm_part_extract_*, the PartitionedKernel reader)
+template <typename T>
+static void part_extract_impl(const T* blocks, uint64_t n, int part_rank, int part_world, const uint64_t* ri,
+                              uint64_t nr, const uint64_t* ci, uint64_t nc, int order_c, double scale, T* out) {
+    std::lock_guard<std::recursive_mutex> lk(g_call_mutex);
+    SNPMI_REQUIRE(part_world >= 1 && part_rank >= 0 && part_rank < part_world, SNPMI_E_ARG, "bad partition");
+    SNPMI_REQUIRE(out != nullptr || nr * nc == 0, SNPMI_E_ARG, "out is NULL");
+    Device& d = device();
+    const uint64_t nloc = grm_part_blocks(n, part_rank, part_world);
+    SNPMI_REQUIRE(nloc == 0 || (blocks && is_device_ptr(d, blocks)), SNPMI_E_ARG,
+                  "blocks must be device memory of the current device");
+    for (uint64_t k = 0; ri && k < nr; k++) SNPMI_REQUIRE(ri[k] < n, SNPMI_E_INDEX, "iid0 index out of range");
+    for (uint64_t k = 0; ci && k < nc; k++) SNPMI_REQUIRE(ci[k] < n, SNPMI_E_INDEX, "iid1 index out of range");
+    SNPMI_REQUIRE(ri || nr <= n, SNPMI_E_INDEX, "iid0 count exceeds n");
+    SNPMI_REQUIRE(ci || nc <= n, SNPMI_E_INDEX, "iid1 count exceeds n");
+    if (nr * nc == 0) return;
+    const PartTables pt = part_tables(ceil_div(n, 256), part_rank, part_world);
+    uint64_t* dri = nullptr;
+    uint64_t* dci = nullptr;
+    if (ri) {
+        dri = (uint64_t*)d.get(Device::S_IDX, nr * 8);
+        SNPMI_HIP(hipMemcpyAsync(dri, ri, nr * 8, hipMemcpyHostToDevice, d.stream));
+    }
+    if (ci) {
+        dci = (uint64_t*)d.get(Device::S_IDX2, nc * 8);
+        SNPMI_HIP(hipMemcpyAsync(dci, ci, nc * 8, hipMemcpyHostToDevice, d.stream));
+    }
+    const bool dev = is_device_ptr(d, out);
+    T* o = dev ? out : (T*)d.get(Device::S_K, nr * nc * sizeof(T));
+    launch_part_extract(blocks, pt.lslot, DT<T>::v, dri, nr, dci, nc, order_c, scale, o, d.stream);
+    if (!dev) SNPMI_HIP(hipMemcpyAsync(out, o, nr * nc * sizeof(T), hipMemcpyDeviceToHost, d.stream));
+    SNPMI_HIP(hipStreamSynchronize(d.stream));
+}
+
+template <typename T>
+static void part_trace_impl(const T* blocks, uint64_t n, int part_rank, int part_world, double* trace) {
+    std::lock_guard<std::recursive_mutex> lk(g_call_mutex);
+    SNPMI_REQUIRE(part_world >= 1 && part_rank >= 0 && part_rank < part_world, SNPMI_E_ARG, "bad partition");
+    SNPMI_REQUIRE(trace != nullptr, SNPMI_E_ARG, "trace is NULL");
+    Device& d = device();
+    *trace = 0.0;
+    if (n == 0 || grm_part_blocks(n, part_rank, part_world) == 0) return;
+    SNPMI_REQUIRE(blocks && is_device_ptr(d, blocks), SNPMI_E_ARG, "blocks must be device memory of the current device");
+    const PartTables pt = part_tables(ceil_div(n, 256), part_rank, part_world);
+    double* tr = (double*)d.get(Device::S_RED, 64);
+    launch_part_trace(blocks, pt.dslot, n, DT<T>::v, tr, d.stream);
+    SNPMI_HIP(hipMemcpyAsync(trace, tr, 8, hipMemcpyDeviceToHost, d.stream));
+    SNPMI_HIP(hipStreamSynchronize(d.stream));
+}
+}  // namespace snpmi
+
+extern "C" {
+
+int snpmi_grm_part_extract_f32(const float* blocks, uint64_t n_iid, int part_rank, int part_world, const uint64_t* ri,
+                               uint64_t nr, const uint64_t* ci, uint64_t nc, int order_c, double scale, float* out) {
+    return guarded([&] { part_extract_impl<float>(blocks, n_iid, part_rank, part_world, ri, nr, ci, nc, order_c, scale, out); });
+}
+int snpmi_grm_part_extract_f64(const double* blocks, uint64_t n_iid, int part_rank, int part_world, const uint64_t* ri,
+                               uint64_t nr, const uint64_t* ci, uint64_t nc, int order_c, double scale, double* out) {
+    return guarded([&] { part_extract_impl<double>(blocks, n_iid, part_rank, part_world, ri, nr, ci, nc, order_c, scale, out); });
+}
+int snpmi_grm_part_trace_f32(const float* blocks, uint64_t n_iid, int part_rank, int part_world, double* trace) {
+    return guarded([&] { part_trace_impl<float>(blocks, n_iid, part_rank, part_world, trace); });
+}
+int snpmi_grm_part_trace_f64(const double* blocks, uint64_t n_iid, int part_rank, int part_world, double* trace) {
+    return guarded([&] { part_trace_impl<double>(blocks, n_iid, part_rank, part_world, trace); });
+}
+int snpmi_device_memory(uint64_t* free_bytes, uint64_t* total_bytes) {
+    return guarded([&] {
+        device();
+        size_t f = 0, t = 0;
+        SNPMI_HIP(hipMemGetInfo(&f, &t));
+        if (free_bytes) *free_bytes = f;
+        if (total_bytes) *total_bytes = t;
+    });
+}
+
+int snpmi_dev_syrk_packed_part_f64(const uint8_t* packed, uint64_t pitch, uint64_t n_iid, uint64_t n_sid,
+                                   const double* lut, int part_rank, int part_world, double* blocks, int accumulate) {
+    return guarded([&] {
+        std::lock_guard<std::recursive_mutex> lk(g_call_mutex);  // shared scratch slots
+        SNPMI_REQUIRE(part_world >= 1 && part_rank >= 0 && part_rank < part_world, SNPMI_E_ARG, "bad partition");
+        SNPMI_REQUIRE(pitch % 64 == 0 && pitch >= ceil_div(n_iid, 4), SNPMI_E_ARG, "pitch must be snpmi_packed_pitch");
+        syrk_packed_part_f64(device(), packed, pitch, n_iid, n_sid, lut, part_rank, part_world, blocks, accumulate);
     });
 }
 

@@ -2023,6 +2023,64 @@ __global__ __launch_bounds__(kBlock) void k_grm_trace(const T* __restrict__ tile
     }
 }
 
+// cfg5: K[ri, ci] from one part's dense 256x256 blocks (syrk.hip part_layout).  Entries whose
+// block this part owns are read (upper-triangle orientation: K[i, j] = K[min, max], so the result
+// is exactly symmetric, as k_grm_extract's), all others are 0 -- the sum of every part's output
+// (one owner per entry; x + 0 is exact) is the sub-matrix.  lslot[L] = local slot of upper-triangle
+// block L = J(J+1)/2 + I, -1 where another part owns it.
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_part_extract(const T* __restrict__ blocks, const int32_t* __restrict__ lslot,
+                                                         const uint64_t* __restrict__ ri, uint64_t nr,
+                                                         const uint64_t* __restrict__ ci, uint64_t nc, int out_c,
+                                                         double scale, T* __restrict__ out) {
+    const uint64_t total = nr * nc;
+    for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+         t += (uint64_t)gridDim.x * blockDim.x) {
+        uint64_t r, c;
+        if (out_c) {
+            r = t / nc;
+            c = t - r * nc;
+        } else {
+            c = t / nr;
+            r = t - c * nr;
+        }
+        uint64_t i = ri ? ri[r] : r, j = ci ? ci[c] : c;
+        if (i > j) {
+            const uint64_t s = i;
+            i = j;
+            j = s;
+        }
+        const uint64_t I = i / 256, J = j / 256;
+        const int32_t w = lslot[J * (J + 1) / 2 + I];
+        T v = (T)0;
+        if (w >= 0) {
+            v = blocks[(uint64_t)w * 65536 + (i % 256) * 256 + (j % 256)];
+            if (scale != 1.0) v = (T)((double)v * scale);
+        }
+        out[t] = v;
+    }
+}
+
+// sum of the K diagonal entries i < n held by one part (one workgroup, fixed reduction order)
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_part_trace(const T* __restrict__ blocks, const int32_t* __restrict__ dslot,
+                                                       uint64_t n, double* trace) {
+    __shared__ double red[kBlock / kWave];
+    double s = 0;
+    for (uint64_t i = threadIdx.x; i < n; i += blockDim.x) {
+        const int32_t w = dslot[i / 256];
+        if (w >= 0) s += (double)blocks[(uint64_t)w * 65536 + (i % 256) * 257];
+    }
+    s = wave_sum_f64(s);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double t = 0;
+        for (int q = 0; q < kBlock / kWave; q++) t += red[q];
+        *trace = t;
+    }
+}
+
 template <typename T>
 __global__ __launch_bounds__(kBlock) void k_dense_trace(const T* __restrict__ K, uint64_t n, double* trace) {
     __shared__ double red[kBlock / kWave];
@@ -2073,23 +2131,24 @@ __global__ __launch_bounds__(kBlock) void k_sumsq(const T* __restrict__ p, uint6
 // current tile diagonal is saved as f64 (0 when not accumulating), k_diag_sq adds the launch's
 // sum_s v^2 in f64 (each square of an f32 value is exact in f64; one f64 add per SNP), and after
 // the SYRK the tile diagonal is overwritten with the f64 value rounded once to f32.
-// Layout: part_world == 0 -> upper-triangle 128x128 tiles (index tj(tj+1)/2 + ti, row-major);
-// else the 256x256 blocks of part part_rank (block L = J(J+1)/2 + I, owner L mod part_world,
-// local index L / part_world, row-major), diagonal entries only where this part owns the block.
-__device__ __forceinline__ int64_t diag_offset(uint64_t i, int part_rank, int part_world) {
-    if (part_world == 0) {
+// Layout: dslot == nullptr -> upper-triangle 128x128 tiles (index tj(tj+1)/2 + ti, row-major);
+// else the 256x256 blocks of one cfg5 part (syrk.hip part_layout): dslot[J] = the local slot of
+// diagonal block J (-1 where another part owns it), row-major blocks.
+__device__ __forceinline__ int64_t diag_offset(uint64_t i, const int32_t* __restrict__ dslot) {
+    if (!dslot) {
         const uint64_t t = i / 128, r = i % 128;
         return (int64_t)((t * (t + 1) / 2 + t) * 128 * 128 + r * 128 + r);
     }
-    const uint64_t J = i / 256, r = i % 256, L = J * (J + 1) / 2 + J;
-    if (L % (uint64_t)part_world != (uint64_t)part_rank) return -1;
-    return (int64_t)((L / (uint64_t)part_world) * 256 * 256 + r * 256 + r);
+    const int32_t w = dslot[i / 256];
+    const uint64_t r = i % 256;
+    return w < 0 ? -1 : (int64_t)((uint64_t)w * 256 * 256 + r * 256 + r);
 }
 
-__global__ __launch_bounds__(kBlock) void k_diag_save(const float* __restrict__ K, uint64_t n, int part_rank,
-                                                      int part_world, int accumulate, double* __restrict__ diag) {
+__global__ __launch_bounds__(kBlock) void k_diag_save(const float* __restrict__ K, uint64_t n,
+                                                      const int32_t* __restrict__ dslot, int accumulate,
+                                                      double* __restrict__ diag) {
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
-        const int64_t o = diag_offset(i, part_rank, part_world);
+        const int64_t o = diag_offset(i, dslot);
         diag[i] = (accumulate && o >= 0) ? (double)K[o] : 0.0;
     }
 }
@@ -2133,10 +2192,10 @@ __global__ __launch_bounds__(kBlock) void k_diag_fold(uint64_t n, uint64_t slice
     }
 }
 
-__global__ __launch_bounds__(kBlock) void k_diag_patch(float* __restrict__ K, uint64_t i0, uint64_t i1, int part_rank,
-                                                       int part_world, const double* __restrict__ diag) {
+__global__ __launch_bounds__(kBlock) void k_diag_patch(float* __restrict__ K, uint64_t i0, uint64_t i1,
+                                                       const int32_t* __restrict__ dslot, const double* __restrict__ diag) {
     for (uint64_t i = i0 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < i1; i += (uint64_t)gridDim.x * blockDim.x) {
-        const int64_t o = diag_offset(i, part_rank, part_world);
+        const int64_t o = diag_offset(i, dslot);
         if (o >= 0) K[o] = (float)diag[i];
     }
 }
@@ -2891,6 +2950,28 @@ void launch_grm_trace(const void* tiles, uint64_t n, int dtype, double* trace_de
     SNPMI_LAUNCH_CHECK();
 }
 
+void launch_part_extract(const void* blocks, const int32_t* lslot, int dtype, const uint64_t* ri, uint64_t nr,
+                         const uint64_t* ci, uint64_t nc, int order_c, double scale, void* out, hipStream_t st) {
+    if (nr == 0 || nc == 0) return;
+    const unsigned g = grid_for(nr * nc, kBlock, 256 * 32);
+    if (dtype == SNPMI_DT_F32)
+        k_part_extract<float><<<g, kBlock, 0, st>>>((const float*)blocks, lslot, ri, nr, ci, nc, order_c, scale,
+                                                    (float*)out);
+    else
+        k_part_extract<double><<<g, kBlock, 0, st>>>((const double*)blocks, lslot, ri, nr, ci, nc, order_c, scale,
+                                                     (double*)out);
+    SNPMI_LAUNCH_CHECK();
+}
+
+void launch_part_trace(const void* blocks, const int32_t* dslot, uint64_t n, int dtype, double* trace_dev,
+                       hipStream_t st) {
+    if (dtype == SNPMI_DT_F32)
+        k_part_trace<float><<<1, kBlock, 0, st>>>((const float*)blocks, dslot, n, trace_dev);
+    else
+        k_part_trace<double><<<1, kBlock, 0, st>>>((const double*)blocks, dslot, n, trace_dev);
+    SNPMI_LAUNCH_CHECK();
+}
+
 void launch_dense_trace(const void* K, uint64_t n, int dtype, double* trace_dev, hipStream_t st) {
     if (dtype == SNPMI_DT_F32)
         k_dense_trace<float><<<1, kBlock, 0, st>>>((const float*)K, n, trace_dev);
@@ -2965,10 +3046,9 @@ void launch_tile_reduce(const float* partial, unsigned slices, uint64_t elems, f
     SNPMI_LAUNCH_CHECK();
 }
 
-void launch_diag_begin(const float* K, uint64_t n, int part_rank, int part_world, int accumulate, double* diag,
-                       hipStream_t st) {
+void launch_diag_begin(const float* K, uint64_t n, const int32_t* dslot, int accumulate, double* diag, hipStream_t st) {
     if (n == 0) return;
-    k_diag_save<<<grid_for(n, kBlock), kBlock, 0, st>>>(K, n, part_rank, part_world, accumulate, diag);
+    k_diag_save<<<grid_for(n, kBlock), kBlock, 0, st>>>(K, n, dslot, accumulate, diag);
     SNPMI_LAUNCH_CHECK();
 }
 
@@ -2995,19 +3075,19 @@ void launch_diag_sq(const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t 
     SNPMI_LAUNCH_CHECK();
 }
 
-void launch_diag_patch(float* K, uint64_t n, uint64_t i0, uint64_t i1, int part_rank, int part_world,
-                       const double* diag, hipStream_t st) {
+void launch_diag_patch(float* K, uint64_t n, uint64_t i0, uint64_t i1, const int32_t* dslot, const double* diag,
+                       hipStream_t st) {
     i1 = std::min(i1, n);
     if (i0 >= i1) return;
-    k_diag_patch<<<grid_for(i1 - i0, kBlock), kBlock, 0, st>>>(K, i0, i1, part_rank, part_world, diag);
+    k_diag_patch<<<grid_for(i1 - i0, kBlock), kBlock, 0, st>>>(K, i0, i1, dslot, diag);
     SNPMI_LAUNCH_CHECK();
 }
 
 void launch_diag_end(const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m, const float* lut, float* K,
-                     int part_rank, int part_world, double* diag, hipStream_t st) {
+                     const int32_t* dslot, double* diag, hipStream_t st) {
     if (n == 0) return;
     launch_diag_sq(packed, pitch, n, m, lut, diag, st);
-    launch_diag_patch(K, n, 0, n, part_rank, part_world, diag, st);
+    launch_diag_patch(K, n, 0, n, dslot, diag, st);
 }
 
 void launch_synth(uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t sid0, uint64_t m, uint64_t seed,

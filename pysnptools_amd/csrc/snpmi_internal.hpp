@@ -90,9 +90,9 @@ struct Device {
     // (nb, xcd) and kept on this device (guarded by the device's own mutex)
     uint32_t* order_tab[2] = {};
     uint64_t order_nb[2] = {};
-    // the same order restricted to one part of the cfg5 plan, per (nb, rank, world)
-    uint32_t* part_order_tab = nullptr;
-    uint64_t part_order_key[4] = {};
+    // the cfg5 part layout (part_layout table + diagonal slots), per (nb, rank, world)
+    void* part_tab = nullptr;
+    uint64_t part_key[3] = {};
     void* get(Slot s, size_t bytes);
     void release();
 };
@@ -128,8 +128,18 @@ SegCtx seg_ctx();                                     // api.hip: the current de
 // api.hip: device table of supertile_order(nb, false) for the current device (cached per nb): the
 // block order of the packed fp16x2 SYRK
 const uint32_t* packed_block_order(uint64_t nb);
-const uint32_t* part_block_order(uint64_t nb, int rank, int world);
-extern int g_part_triangular;  // hook "part_order": 0 = 64-block supertiles, 1 = triangular, 2 = 16-block supertiles
+// cfg5 K partition (syrk.hip part_layout): part `rank` of `world` owns whole S x S-block
+// supertiles (S = part_unit) dealt round-robin; its blocks are stored densely in the order of its
+// layout table (entry bi | bj << 16 per local slot).  part_tables: that table and the local slot
+// of each diagonal block (bi = bj = J; -1 if another part owns it) on the current device (cached)
+uint64_t part_unit(uint64_t nb, int world);
+void part_layout(uint64_t nb, int rank, int world, std::vector<uint32_t>& tab);
+struct PartTables {
+    const uint32_t* tab = nullptr;
+    const int32_t* dslot = nullptr;
+    const int32_t* lslot = nullptr;  // per upper-triangle block L = J(J+1)/2 + I: local slot or -1
+};
+PartTables part_tables(uint64_t nb, int rank, int world);
 void launch_snp_stats(const uint8_t* packed, uint64_t pitch, uint64_t n_iid, uint64_t n_sid, int count_a1,
                       int std_kind, double a, double b, int use_stats, int dtype, void* stats, void* lut,
                       hipStream_t st);
@@ -172,22 +182,28 @@ void launch_grm_extract_rows(const void* tiles, uint64_t n, int dtype, uint64_t 
 void launch_grm_extract(const void* tiles, uint64_t n, int dtype, const uint64_t* ri, uint64_t nr,
                         const uint64_t* ci, uint64_t nc, int order_c, double scale, void* out, hipStream_t st);
 void launch_grm_trace(const void* tiles, uint64_t n, int dtype, double* trace_dev, hipStream_t st);
+// cfg5 part blocks -> K[ri, ci] restricted to this part's blocks (0 elsewhere; the parts' outputs
+// sum to the sub-matrix) / the part's share of trace(K) (kernels.hip k_part_*)
+void launch_part_extract(const void* blocks, const int32_t* lslot, int dtype, const uint64_t* ri, uint64_t nr,
+                         const uint64_t* ci, uint64_t nc, int order_c, double scale, void* out, hipStream_t st);
+void launch_part_trace(const void* blocks, const int32_t* dslot, uint64_t n, int dtype, double* trace_dev,
+                       hipStream_t st);
 // exact f32 GRM diagonal around one f32 SYRK launch (kernels.hip k_diag_*): begin saves the current
 // diagonal as f64 (0 unless accumulating), end adds sum_s lut_s[code]^2 in f64 and writes it back
-// rounded once.  part_world == 0: upper-triangle tiles; else the blocks of part part_rank.
+// rounded once.  dslot == nullptr: upper-triangle tiles; else the blocks of one cfg5 part
+// (PartTables::dslot: local slot of each diagonal block, -1 if not owned).
 extern int g_diag_exact;  // hook "diag": 1 (default) = on, 0 = the SYRK's own diagonal
-void launch_diag_begin(const float* K, uint64_t n, int part_rank, int part_world, int accumulate, double* diag,
-                       hipStream_t st);
+void launch_diag_begin(const float* K, uint64_t n, const int32_t* dslot, int accumulate, double* diag, hipStream_t st);
 void launch_diag_end(const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m, const float* lut, float* K,
-                     int part_rank, int part_world, double* diag, hipStream_t st);
+                     const int32_t* dslot, double* diag, hipStream_t st);
 // diag: diag_scratch_bytes(n, m) of device scratch (n f64 + per-slice partial rows, folded in a
 // fixed order so the diagonal is the same bits on every run)
 uint64_t diag_scratch_bytes(uint64_t n, uint64_t m);
 // launch_diag_end in two steps: the f64 squares of all iids, then the write-back of iids [i0, i1)
 void launch_diag_sq(const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m, const float* lut, double* diag,
                     hipStream_t st);
-void launch_diag_patch(float* K, uint64_t n, uint64_t i0, uint64_t i1, int part_rank, int part_world,
-                       const double* diag, hipStream_t st);
+void launch_diag_patch(float* K, uint64_t n, uint64_t i0, uint64_t i1, const int32_t* dslot, const double* diag,
+                       hipStream_t st);
 // rccl.hip: in-place sum over the ranks of a device range on stream st (root < 0: all-reduce)
 void rccl_sum_on(void* buf, uint64_t count, int dtype, int root, hipStream_t st);
 bool rccl_ready();
@@ -226,7 +242,6 @@ void launch_lut_h2(const float* lut, uint64_t m, uint32_t* lut2, uint32_t* flag,
 // fp16x2 SYRK in supertile block order (order: device table of supertile_order), the f32-MFMA
 // k_syrk256d gated on the range flag
 void supertile_order(uint64_t nb, bool xcd, std::vector<uint32_t>& tab);
-void part_supertile_order(uint64_t nb, int rank, int world, std::vector<uint32_t>& tab, uint64_t S);
 uint64_t dense_h2_chunk_snps(uint64_t n);
 uint64_t dense_h2_scratch_bytes(uint64_t n, uint64_t m);
 void launch_syrk_dense_h2(const float* Z, uint64_t ldz, uint64_t n, uint64_t m, uint16_t* img, uint32_t* flag,
@@ -260,10 +275,15 @@ void launch_syrk_packed_crt(const uint8_t* packed, uint64_t pitch, uint64_t n, u
                             double* tiles, int accumulate, void* ws_lut, uint8_t* res, uint64_t res_bytes,
                             unsigned long long* rec, hipStream_t st,
                             const std::function<void()>* before_chunks = nullptr,
-                            const std::function<void(uint64_t, uint64_t)>* after_chunk = nullptr);
-// the f64-MFMA packed SYRK, run only when the device word *gate is non-zero (the CRT path's flag)
+                            const std::function<void(uint64_t, uint64_t)>* after_chunk = nullptr,
+                            const uint32_t* part_tab = nullptr, uint64_t part_blocks = 0);
+// part_tab (cfg5): tiles = the part's part_blocks dense 256x256 f64 blocks in the order of its
+// layout table (PartTables::tab); no after_chunk.
+// the f64-MFMA packed SYRK, run only when the device word *gate is non-zero (the CRT path's flag);
+// with part_tab: into the part's dense blocks (all four 128-quadrants of each)
 void launch_syrk_packed_f64_gated(const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m, const double* lut,
-                                  double* tiles, int accumulate, const int* gate, hipStream_t st);
+                                  double* tiles, int accumulate, const int* gate, hipStream_t st,
+                                  const uint32_t* part_tab = nullptr, uint64_t part_blocks = 0);
 void launch_syrk_packed_bf3_part(const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m, const uint32_t* lut3,
                                  int rank, int world, float* blocks, int accumulate, hipStream_t st,
                                  const H2Lut* h2 = nullptr);

@@ -425,9 +425,9 @@ __device__ __forceinline__ void epilogue(f32x16 (&acc)[4][2], float* __restrict_
         }
 }
 
-// LOCAL (cfg5, K too large to replicate): this rank owns blocks L = blockIdx.x * world + rank
-// of the upper-triangle block list and writes each as a full 256x256 row-major block at
-// tiles + blockIdx.x * 65536 (no cross-rank reduction is needed).
+// LOCAL (cfg5, K too large to replicate): workgroup w computes block part_tab[w] of this part's
+// layout (part_layout) and writes it as a full 256x256 row-major block at tiles + w * 65536 (no
+// cross-rank reduction is needed).
 // IL: the next stage's LUT expansion + ds_write is split into 4 pieces issued between the
 // MFMA groups of the current stage (after kk = 1, 3, 5, 7) instead of after all of them.
 // ROT: odd SNP rows of the LDS panels are stored rotated by 32 floats, so the two k-rows one
@@ -437,10 +437,15 @@ template <int MINB, bool LOCAL = false, bool IL = false, bool ROT = false>
 __global__ __launch_bounds__(512, MINB) void k_syrk256(const uint8_t* __restrict__ P, uint64_t pitch, uint64_t n,
                                                       uint64_t kdim, const float* __restrict__ lut,
                                                       float* __restrict__ tiles, int accumulate,
-                                                      uint32_t part_rank = 0, uint32_t part_world = 1) {
+                                                      const uint32_t* __restrict__ part_tab = nullptr) {
     __shared__ __attribute__((aligned(16))) float lds[2][2][BK * LDA];
     uint32_t bi, bj;
-    tile_coords(LOCAL ? (uint64_t)blockIdx.x * part_world + part_rank : (uint64_t)blockIdx.x, bi, bj);
+    if constexpr (LOCAL) {  // slot blockIdx.x of the part's layout table (part_layout)
+        bi = part_tab[blockIdx.x] & 0xffffu;
+        bj = part_tab[blockIdx.x] >> 16;
+    } else {
+        tile_coords(blockIdx.x, bi, bj);
+    }
     const uint64_t i0 = (uint64_t)bi * BW, j0 = (uint64_t)bj * BW;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int wm = wave >> 2, wn = wave & 3;
@@ -550,14 +555,22 @@ template <bool LOCAL = false, int BKD = 16, int NBUF = 2, bool XCD = false>
 __global__ __launch_bounds__(512, 1) void k_syrk256d(const float* __restrict__ Z, uint64_t ldz, uint64_t n,
                                                     uint64_t kdim, float* __restrict__ tiles, int accumulate,
                                                     uint32_t part_rank = 0, uint32_t part_world = 1,
-                                                    const uint32_t* __restrict__ gate = nullptr) {
+                                                    const uint32_t* __restrict__ gate = nullptr,
+                                                    const uint32_t* __restrict__ part_tab = nullptr) {
     static_assert(NBUF == 2 || NBUF == 3, "2 or 3 LDS stages");
     constexpr int G = 2 * BKD / 8;  // glds per wave per stage (8 waves, one 1 KiB row each)
     __shared__ __attribute__((aligned(16))) float lds[NBUF][2][BKD * LDA];
     if (gate && *gate == 0) return;  // fallback of the dense fp16x2 kernel (range flag raised)
     const uint64_t wg = XCD ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
     uint32_t bi, bj;
-    tile_coords(LOCAL ? wg * part_world + part_rank : wg, bi, bj);
+    if constexpr (LOCAL) {  // slot wg of the part's layout table (part_layout)
+        bi = part_tab[wg] & 0xffffu;
+        bj = part_tab[wg] >> 16;
+    } else {
+        tile_coords(wg, bi, bj);
+    }
+    (void)part_rank;
+    (void)part_world;
     const uint64_t i0 = (uint64_t)bi * BW, j0 = (uint64_t)bj * BW;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int wm = wave >> 2, wn = wave & 3;
@@ -833,7 +846,7 @@ __global__ __launch_bounds__(512, 1) void k_syrk_bf3(const uint8_t* __restrict__
                                                      uint32_t part_rank = 0, uint32_t part_world = 1,
                                                      uint64_t kslice = 0, uint64_t slice_elems = 0,
                                                      const uint32_t* __restrict__ gate = nullptr, SegCtx seg = SegCtx(),
-                                                     uint64_t wg0 = 0) {
+                                                     uint64_t wg0 = 0, const uint32_t* __restrict__ part_tab = nullptr) {
     __shared__ __attribute__((aligned(16))) short lds[2 * B3_STAGE];
     if (gate && *gate == 0) return;  // fallback of k_syrk_h2: runs only when its range flag is set
     if (gridDim.y > 1) {  // split-K: slice blockIdx.y covers SNPs [y*kslice, +kslice) into its own partial K
@@ -846,7 +859,12 @@ __global__ __launch_bounds__(512, 1) void k_syrk_bf3(const uint8_t* __restrict__
     // wg0: first block of a column-group launch (triangular order), as in k_syrk_h2
     const uint64_t wg = wg0 + (XCD ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x);
     uint32_t bi, bj;
-    tile_coords(LOCAL ? wg * part_world + part_rank : wg, bi, bj);
+    if constexpr (LOCAL) {  // slot wg of the part's layout table (part_layout)
+        bi = part_tab[wg] & 0xffffu;
+        bj = part_tab[wg] >> 16;
+    } else {
+        tile_coords(wg, bi, bj);
+    }
     const uint64_t i0 = (uint64_t)bi * BW, j0 = (uint64_t)bj * BW;
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
     const int wm = wave >> 2, wn = wave & 3;
@@ -1269,16 +1287,15 @@ __global__ __launch_bounds__(512, 1) void k_syrk_h2(const uint8_t* __restrict__ 
         const uint32_t c = lut2[wg];
         bi = c & 0xffffu;
         bj = c >> 16;
-    } else if (order) {  // supertile block order table (supertile_order / part_supertile_order)
+    } else if (LOCAL || order) {  // block order table (supertile_order) / the part's layout table (part_layout)
         const uint32_t c = order[wg];
         bi = c & 0xffffu;
         bj = c >> 16;
     } else {
-        tile_coords(LOCAL ? wg * part_world + part_rank : wg, bi, bj);
+        tile_coords(wg, bi, bj);
     }
-    // LOCAL: the block's index among this part's blocks (its storage slot and SegFlush phase, so
-    // any block order gives the same K bit for bit); = wg in the triangular order
-    const uint64_t blk = LOCAL ? ((uint64_t)bj * (bj + 1) / 2 + bi) / part_world : wg;
+    // LOCAL: slot wg of the part's layout table is the block's storage slot and SegFlush phase
+    const uint64_t blk = wg;
     const uint64_t i0 = (uint64_t)bi * BW, j0 = (uint64_t)bj * BW;
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
     const int wm = wave >> 2, wn = wave & 3;
@@ -1649,7 +1666,8 @@ __global__ __launch_bounds__(512, 1) void k_syrk_h2x(const uint8_t* __restrict__
     }
     const uint64_t wg = blockIdx.x;
     uint32_t bi, bj;
-    tile_coords(LOCAL ? wg * part_world + part_rank : wg, bi, bj);
+    static_assert(!LOCAL, "the cfg5 part kernels read the part layout table (k_syrk_h2 / k_syrk_bf3)");
+    tile_coords(wg, bi, bj);
     const uint64_t i0 = (uint64_t)bi * BW, j0 = (uint64_t)bj * BW;
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
     const int wm = wave >> 2, wn = wave & 3;
@@ -1812,7 +1830,8 @@ __global__ __launch_bounds__(256, 1) void k_syrk_h2q(const uint8_t* __restrict__
     }
     const uint64_t wg = blockIdx.x;
     uint32_t bi, bj;
-    tile_coords(LOCAL ? wg * part_world + part_rank : wg, bi, bj);
+    static_assert(!LOCAL, "the cfg5 part kernels read the part layout table (k_syrk_h2 / k_syrk_bf3)");
+    tile_coords(wg, bi, bj);
     const uint64_t i0 = (uint64_t)bi * BW, j0 = (uint64_t)bj * BW;
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
     const int wm = wave >> 1, wn = wave & 1;
@@ -2020,7 +2039,8 @@ __global__ __launch_bounds__(256, 1) void k_syrk_h2w(const uint8_t* __restrict__
     }
     const uint64_t wg = blockIdx.x;
     uint32_t bi, bj;
-    tile_coords(LOCAL ? wg * part_world + part_rank : wg, bi, bj);
+    static_assert(!LOCAL, "the cfg5 part kernels read the part layout table (k_syrk_h2 / k_syrk_bf3)");
+    tile_coords(wg, bi, bj);
     const uint64_t i0 = (uint64_t)bi * BW, j0 = (uint64_t)bj * BW;
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
     const int wm = wave >> 1, wn = wave & 1;
@@ -2358,24 +2378,24 @@ __device__ __forceinline__ void compute_store(const double* As, const double* Bs
     }
 }
 
-// f64 16x16x4 C/D layout: col = lane&15, row = (lane>>4) + 4*r
-__device__ __forceinline__ void epilogue(f64x4 (&acc)[4][4], double* __restrict__ tiles, int accumulate, int lane,
-                                         int wm, int wn) {
-    double* T = tiles + (uint64_t)blockIdx.x * (BM * BM);
+// f64 16x16x4 C/D layout: col = lane&15, row = (lane>>4) + 4*r.  T: the 128x128 output tile,
+// row stride ldo (BM for the tile store, 256 inside a cfg5 part's dense block)
+__device__ __forceinline__ void epilogue(f64x4 (&acc)[4][4], double* __restrict__ T, uint64_t ldo, int accumulate,
+                                         int lane, int wm, int wn) {
 #pragma unroll
     for (int x = 0; x < 4; x++)
 #pragma unroll
         for (int y = 0; y < 4; y++) {
-            double* base = T + (wm * 64 + 16 * x + (lane >> 4)) * BM + wn * 64 + 16 * y + (lane & 15);
+            double* base = T + (wm * 64 + 16 * x + (lane >> 4)) * ldo + wn * 64 + 16 * y + (lane & 15);
             if (accumulate) {
                 double old[4];
 #pragma unroll
-                for (int r = 0; r < 4; r++) old[r] = base[4 * r * BM];
+                for (int r = 0; r < 4; r++) old[r] = base[4 * r * ldo];
 #pragma unroll
                 for (int r = 0; r < 4; r++) acc[x][y][r] += old[r];
             }
 #pragma unroll
-            for (int r = 0; r < 4; r++) base[4 * r * BM] = acc[x][y][r];
+            for (int r = 0; r < 4; r++) base[4 * r * ldo] = acc[x][y][r];
         }
 }
 
@@ -2384,11 +2404,23 @@ __device__ __forceinline__ void epilogue(f64x4 (&acc)[4][4], double* __restrict_
 template <bool PACKED, int MODE = 0>
 __global__ __launch_bounds__(256, 2) void k_syrk(const void* __restrict__ src, uint64_t ld, uint64_t kdim,
                                                  const double* __restrict__ lut, double* __restrict__ tiles,
-                                                 int accumulate, const int* __restrict__ gate = nullptr) {
+                                                 int accumulate, const int* __restrict__ gate = nullptr,
+                                                 const uint32_t* __restrict__ part_tab = nullptr) {
     __shared__ __attribute__((aligned(16))) double lds[2][2][BK * LDA];
     if (gate && *gate == 0) return;  // fallback of the CRT path: runs only when its flag is set
     uint32_t ti, tj;
-    tile_coords(blockIdx.x, ti, tj);
+    double* T;
+    uint64_t ldo = BM;
+    if (part_tab) {  // cfg5: quadrant q of slot w of the part's layout, written into its dense block
+        const uint64_t w = blockIdx.x >> 2, q = blockIdx.x & 3;
+        ti = 2 * (part_tab[w] & 0xffffu) + (uint32_t)(q & 1);
+        tj = 2 * (part_tab[w] >> 16) + (uint32_t)(q >> 1);
+        T = tiles + w * 65536 + (q & 1) * 128 * 256 + (q >> 1) * 128;
+        ldo = 256;
+    } else {
+        tile_coords(blockIdx.x, ti, tj);
+        T = tiles + (uint64_t)blockIdx.x * (BM * BM);
+    }
     const uint64_t i0 = (uint64_t)ti * BM, j0 = (uint64_t)tj * BM;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int wm = wave >> 1, wn = wave & 1;
@@ -2445,7 +2477,7 @@ __global__ __launch_bounds__(256, 2) void k_syrk(const void* __restrict__ src, u
         }
         __syncthreads();
     }
-    epilogue(acc, tiles, accumulate, lane, wm, wn);
+    epilogue(acc, T, ldo, accumulate, lane, wm, wn);
 }
 
 // Dense f64 operand (F order, ldz >= round_up(n, 128)) streamed global -> LDS with
@@ -2491,7 +2523,7 @@ __global__ __launch_bounds__(256, 2) void k_syrk_glds(const double* __restrict__
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
     }
-    epilogue(acc, tiles, accumulate, lane, wm, wn);
+    epilogue(acc, tiles + (uint64_t)blockIdx.x * (BM * BM), BM, accumulate, lane, wm, wn);
 }
 }  // namespace f64k
 
@@ -2500,7 +2532,6 @@ __global__ __launch_bounds__(256, 2) void k_syrk_glds(const double* __restrict__
 int g_variant_syrk = 0;  // tuning hook (snpmi_set_kernel_variant "syrk")
 // 8192: 4.9e-6 of max diag at 50k x 100k on SnpGen-shaped data (21.8% missing) for +2.2% time;
 // 4096: 2.6e-6 for +3.8%; 16384: 6.9e-6 for +1.9%; none: 3.2e-5 (profiles/r03acc, r03seg)
-int g_part_triangular = 0;
 int g_seg_snps = 12288;  // tuning hook "seg" (round 4: 12288 with the exact f64 diagonal, k_diag_*)
 
 // host-side segmentation for the f32-MFMA kernels without SegFlush (fallbacks and small-N
@@ -2588,17 +2619,56 @@ void launch_syrk_packed(const uint8_t* packed, uint64_t pitch, uint64_t n, uint6
 }
 
 void launch_syrk_packed_f64_gated(const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m, const double* lut,
-                                  double* tiles, int accumulate, const int* gate, hipStream_t st) {
-    const uint64_t nt = n_tiles_upper(n);
+                                  double* tiles, int accumulate, const int* gate, hipStream_t st,
+                                  const uint32_t* part_tab, uint64_t part_blocks) {
+    const uint64_t nt = part_tab ? 4 * part_blocks : n_tiles_upper(n);
     if (nt == 0 || m == 0) return;
     SNPMI_REQUIRE(nt < (1ull << 31), SNPMI_E_ARG, "too many GRM tiles for one launch");
-    f64k::k_syrk<true, 4><<<(unsigned)nt, 256, 0, st>>>(packed, pitch, m, lut, tiles, accumulate, gate);
+    f64k::k_syrk<true, 4><<<(unsigned)nt, 256, 0, st>>>(packed, pitch, m, lut, tiles, accumulate, gate, part_tab);
     SNPMI_HIP(hipGetLastError());
 }
 
+// cfg5 ownership of K (round 5).  The upper triangle of 256-iid blocks is cut into S x S-block
+// supertiles (S = part_unit: 16 once there are enough supertiles to deal out, else smaller),
+// dealt round-robin in triangular order: supertile T = J(J+1)/2 + I belongs to part T mod world.
+// A part stores its blocks densely in walk order -- its supertiles in T order, each supertile's
+// blocks column by column (bj outer, bi <= bj inner) -- and every LOCAL kernel reads block
+// (bi, bj) of workgroup w from that table (entry bi | bj << 16) and writes it to slot w.  So the
+// ~256 blocks in flight share ~32 code panels, as in the replicated kernel's supertile order,
+// instead of the ~108 of round 4's single-block round-robin ownership.
+uint64_t part_unit(uint64_t nb, int world) {
+    for (uint64_t S = 16; S > 1; S /= 2) {
+        const uint64_t ns = ceil_div(nb, S);
+        if (ns * (ns + 1) / 2 >= 4 * (uint64_t)std::max(world, 1)) return S;
+    }
+    return 1;
+}
+
+static uint64_t supertile_blocks(uint64_t nb, uint64_t S, uint64_t I, uint64_t J) {
+    const uint64_t c = std::min(S, nb - S * J);
+    return I == J ? c * (c + 1) / 2 : std::min(S, nb - S * I) * c;
+}
+
 uint64_t grm_part_blocks(uint64_t n, int rank, int world) {
-    const uint64_t nb = ceil_div(n, 256), total = nb * (nb + 1) / 2;
-    return total > (uint64_t)rank ? (total - rank + world - 1) / world : 0;
+    const uint64_t nb = ceil_div(n, 256), S = part_unit(nb, world), ns = ceil_div(nb, S);
+    uint64_t cnt = 0;
+    for (uint64_t J = 0, T = 0; J < ns; J++)
+        for (uint64_t I = 0; I <= J; I++, T++)
+            if (T % (uint64_t)world == (uint64_t)rank) cnt += supertile_blocks(nb, S, I, J);
+    return cnt;
+}
+
+void part_layout(uint64_t nb, int rank, int world, std::vector<uint32_t>& tab) {
+    SNPMI_REQUIRE(nb < 65536, SNPMI_E_ARG, "partitioned GRM: too many 256-iid blocks (n >= 2^24)");
+    tab.clear();
+    const uint64_t S = part_unit(nb, world), ns = ceil_div(nb, S);
+    for (uint64_t J = 0, T = 0; J < ns; J++)
+        for (uint64_t I = 0; I <= J; I++, T++) {
+            if (T % (uint64_t)world != (uint64_t)rank) continue;
+            for (uint64_t bj = S * J; bj < std::min(S * J + S, nb); bj++)
+                for (uint64_t bi = S * I; bi < std::min(S * I + S, bj + 1); bi++)
+                    tab.push_back((uint32_t)(bi | (bj << 16)));
+        }
 }
 
 void launch_syrk_packed_part(const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m, const void* lut,
@@ -2610,10 +2680,10 @@ void launch_syrk_packed_part(const uint8_t* packed, uint64_t pitch, uint64_t n, 
         if (!accumulate) SNPMI_HIP(hipMemsetAsync(blocks, 0, nloc * 256 * 256 * sizeof(float), st));
         return;
     }
+    const uint32_t* tab = part_tables(ceil_div(n, 256), rank, world).tab;
     for_segments(m, accumulate, [&](uint64_t c0, uint64_t cnt, int acc) {
         f32w::k_syrk256<1, true><<<(unsigned)nloc, 512, 0, st>>>(packed + c0 * pitch, pitch, n, cnt,
-                                                                 (const float*)lut + 4 * c0, (float*)blocks, acc,
-                                                                 (uint32_t)rank, (uint32_t)world);
+                                                                 (const float*)lut + 4 * c0, (float*)blocks, acc, tab);
         SNPMI_HIP(hipGetLastError());
     });
 }
@@ -2657,22 +2727,6 @@ void supertile_order(uint64_t nb, bool xcd, std::vector<uint32_t>& tab) {
                     left--;
                 }
         }
-}
-
-// The blocks of part `rank` (block L = bj(bj+1)/2 + bi, owner L mod world) in supertile order
-// with S x S-block supertiles (S = 16: the replicated kernel's table).  The part owns every
-// world-th block, so the ~256 blocks in flight span more panels than the replicated kernel's
-// (~46 code panels per 256 blocks there): ~153 with S = 16, ~108 with S = 64 (host count at
-// 150k iids, 8 parts; tools/exp_part_locality.py measures the part kernel 8% slower per block).
-void part_supertile_order(uint64_t nb, int rank, int world, std::vector<uint32_t>& tab, uint64_t S) {
-    tab.clear();
-    const uint64_t ns = ceil_div(nb, S);
-    for (uint64_t J = 0; J < ns; J++)
-        for (uint64_t I = 0; I <= J; I++)
-            for (uint64_t bj = S * J; bj < std::min(S * J + S, nb); bj++)
-                for (uint64_t bi = S * I; bi < std::min(S * I + S, bj + 1); bi++)
-                    if ((bj * (bj + 1) / 2 + bi) % (uint64_t)world == (uint64_t)rank)
-                        tab.push_back((uint32_t)(bi | (bj << 16)));
 }
 
 #ifdef SNPMI_UBENCH
@@ -2901,18 +2955,15 @@ void launch_syrk_packed_bf3_part(const uint8_t* packed, uint64_t pitch, uint64_t
         if (!accumulate) SNPMI_HIP(hipMemsetAsync(blocks, 0, nloc * 256 * 256 * sizeof(float), st));
         return;
     }
+    const uint32_t* tab = part_tables(ceil_div(n, 256), rank, world).tab;
     if (h2) {
-        // supertile order over the part's blocks (hook "part_order" = 1: the triangular order)
-        const uint64_t nb = ceil_div(n, 256);  // table entries pack bi | bj << 16
-        const uint32_t* order = (g_part_triangular == 1 || nb >= 65536) ? nullptr : part_block_order(nb, rank, world);
         f32w::k_syrk_h2<true><<<(unsigned)nloc, 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, blocks, accumulate,
-                                                               (uint32_t)rank, (uint32_t)world, 0, 0,
-                                                               seg_ctx(), order);
+                                                               0, 1, 0, 0, seg_ctx(), tab);
         SNPMI_HIP(hipGetLastError());
     }
     f32w::k_syrk_bf3<true, false, 5><<<(unsigned)nloc, 512, 0, st>>>(packed, pitch, n, m, lut3, blocks, accumulate,
-                                                                     (uint32_t)rank, (uint32_t)world, 0, 0,
-                                                                     h2 ? h2->flag : nullptr, seg_ctx());
+                                                                     0, 1, 0, 0, h2 ? h2->flag : nullptr, seg_ctx(),
+                                                                     0, tab);
     SNPMI_HIP(hipGetLastError());
 }
 
@@ -2926,9 +2977,10 @@ void launch_syrk_dense_part(const float* Z, uint64_t ldz, uint64_t n, uint64_t m
         if (!accumulate) SNPMI_HIP(hipMemsetAsync(blocks, 0, nloc * 256 * 256 * sizeof(float), st));
         return;
     }
+    const uint32_t* tab = part_tables(ceil_div(n, 256), rank, world).tab;
     for_segments(m, accumulate, [&](uint64_t c0, uint64_t cnt, int acc) {
-        f32w::k_syrk256d<true><<<(unsigned)nloc, 512, 0, st>>>(Z + c0 * ldz, ldz, n, cnt, (float*)blocks, acc,
-                                                               (uint32_t)rank, (uint32_t)world);
+        f32w::k_syrk256d<true><<<(unsigned)nloc, 512, 0, st>>>(Z + c0 * ldz, ldz, n, cnt, (float*)blocks, acc, 0, 1,
+                                                               nullptr, tab);
         SNPMI_HIP(hipGetLastError());
     });
 }

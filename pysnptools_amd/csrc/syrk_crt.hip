@@ -204,7 +204,8 @@ template <int SKT, int ABL = 0, int LDM = 0, int ST = 0, int LD2 = 0>
 __global__ __launch_bounds__(512, 1) void k_syrk_i8r(const uint8_t* __restrict__ P, uint64_t pitch, uint64_t kdim,
                                                      uint64_t mpad, const uint32_t* __restrict__ lutr,
                                                      const int* __restrict__ ctl, uint64_t b0, uint64_t nblk,
-                                                     uint8_t* __restrict__ res) {
+                                                     uint8_t* __restrict__ res,
+                                                     const uint32_t* __restrict__ part_tab = nullptr) {
     constexpr int KS = SKT / 32, RPT = SKT / 16, PNL = SKT * RS, STG = 2 * PNL;
     __shared__ __attribute__((aligned(16))) uint8_t lds[2 * STG];
     if (ctl[1]) return;  // non-finite LUT: the f64 MFMA kernel runs instead
@@ -212,7 +213,13 @@ __global__ __launch_bounds__(512, 1) void k_syrk_i8r(const uint8_t* __restrict__
     if (r >= ctl[2]) return;  // K_int fits the first ctl[2] moduli
     const uint32_t* lr = lutr + (uint64_t)r * mpad;
     uint32_t bi, bj;
-    tile_coords(b0 + blockIdx.x, bi, bj);
+    if (part_tab) {  // cfg5: slot b0 + blockIdx.x of the part's layout (syrk.hip part_layout)
+        const uint32_t c = part_tab[b0 + blockIdx.x];
+        bi = c & 0xffffu;
+        bj = c >> 16;
+    } else {
+        tile_coords(b0 + blockIdx.x, bi, bj);
+    }
     const uint64_t i0 = (uint64_t)bi * BW, j0 = (uint64_t)bj * BW;
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
     const int wm = wave >> 2, wn = wave & 3;
@@ -584,17 +591,23 @@ __device__ __forceinline__ void digits(f2 (&v)[2][kR], const uint8_t* __restrict
 
 // grid: 64 workgroups per 256-block (four rows each), 256 threads = 4 rows x 64 column quads;
 // one 4-B load per residue plane and thread, two independent packed-f32 Garner chains
+// part (cfg5): the block of slot b0 + blk is written whole (256 x 256 row-major, f64) at
+// tiles + (b0 + blk) * 65536, as the f32 part kernels write theirs
 __global__ __launch_bounds__(256) void k_crt(const uint8_t* __restrict__ res, uint64_t b0, uint64_t nblk, uint64_t n,
                                              const int* __restrict__ ctl, int F, CrtConst cc, double* __restrict__ tiles,
-                                             int accumulate) {
+                                             int accumulate, int part) {
     if (ctl[1]) return;
     const uint64_t blk = blockIdx.x >> 6;
     const int row = 4 * (blockIdx.x & 63) + (threadIdx.x >> 6), col = 4 * (threadIdx.x & 63);
-    uint32_t bi, bj;
-    tile_coords(b0 + blk, bi, bj);
-    const uint64_t ti = 2 * (uint64_t)bi + (row >> 7), tj = 2 * (uint64_t)bj + (col >> 7);
-    const uint64_t nt128 = (n + 127) / 128;
-    if (ti > tj || tj >= nt128) return;
+    uint64_t ti = 0, tj = 0;
+    if (!part) {
+        uint32_t bi, bj;
+        tile_coords(b0 + blk, bi, bj);
+        ti = 2 * (uint64_t)bi + (row >> 7);
+        tj = 2 * (uint64_t)bj + (col >> 7);
+        const uint64_t nt128 = (n + 127) / 128;
+        if (ti > tj || tj >= nt128) return;
+    }
     const uint64_t e_off = (blk * BW + row) * BW + col, plane = nblk * (BW * BW);
     f2 v[2][kR];
     {
@@ -607,8 +620,9 @@ __global__ __launch_bounds__(256) void k_crt(const uint8_t* __restrict__ res, ui
     }
     digits<1>(v, res, plane, e_off, cc, ctl[2]);
     const int sh = 2 * (ctl[0] - F);
-    double2* T = reinterpret_cast<double2*>(tiles + (tj * (tj + 1) / 2 + ti) * (uint64_t)(128 * 128) +
-                                            (row & 127) * 128 + (col & 127));
+    double2* T = reinterpret_cast<double2*>(
+        part ? tiles + ((b0 + blk) * BW + row) * BW + col
+             : tiles + (tj * (tj + 1) / 2 + ti) * (uint64_t)(128 * 128) + (row & 127) * 128 + (col & 127));
 #pragma unroll
     for (int h = 0; h < 2; h++) {
         double X0 = (double)v[h][kR - 1].x, X1 = (double)v[h][kR - 1].y;
@@ -697,9 +711,12 @@ std::vector<std::pair<uint64_t, uint64_t>> crt_column_chunks(uint64_t n, uint64_
 void launch_syrk_packed_crt(const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m, const double* lut,
                             double* tiles, int accumulate, void* ws_lut, uint8_t* res, uint64_t res_bytes,
                             unsigned long long* rec, hipStream_t st, const std::function<void()>* before_chunks,
-                            const std::function<void(uint64_t, uint64_t)>* after_chunk) {
+                            const std::function<void(uint64_t, uint64_t)>* after_chunk, const uint32_t* part_tab,
+                            uint64_t part_blocks) {
     SNPMI_REQUIRE(m > 0 && m <= crt_max_snps(), SNPMI_E_ARG, "crt SYRK: SNP count per launch out of range");
-    const uint64_t nb = ceil_div(n, BW), total = nb * (nb + 1) / 2;
+    SNPMI_REQUIRE(!part_tab || !after_chunk, SNPMI_E_ARG, "crt SYRK: column chunks of a part");
+    const uint64_t nb = ceil_div(n, BW), total = part_tab ? part_blocks : nb * (nb + 1) / 2;
+    if (total == 0) return;
     const uint64_t mpad = round_up(m, SK);
     int* ctl = (int*)ws_lut;
     uint32_t* lutr = (uint32_t*)((uint8_t*)ws_lut + 256);
@@ -748,8 +765,9 @@ void launch_syrk_packed_crt(const uint8_t* packed, uint64_t pitch, uint64_t n, u
             k_syrk_i8r<SK, 2><<<dim3((unsigned)cnt, kR), 512, 0, st>>>(packed, pitch, m, mpad, lutr, ctl, b0, cnt, res);
         else
 #endif
-        k_syrk_i8r<SK><<<dim3((unsigned)cnt, kR), 512, 0, st>>>(packed, pitch, m, mpad, lutr, ctl, b0, cnt, res);
-        k_crt<<<(unsigned)(cnt * 64), 256, 0, st>>>(res, b0, cnt, n, ctl, F, cc, tiles, accumulate);
+        k_syrk_i8r<SK><<<dim3((unsigned)cnt, kR), 512, 0, st>>>(packed, pitch, m, mpad, lutr, ctl, b0, cnt, res,
+                                                               part_tab);
+        k_crt<<<(unsigned)(cnt * 64), 256, 0, st>>>(res, b0, cnt, n, ctl, F, cc, tiles, accumulate, part_tab ? 1 : 0);
         if (after_chunk) {
             SNPMI_HIP(hipGetLastError());
             (*after_chunk)(cols[ci].first, cols[ci].second);

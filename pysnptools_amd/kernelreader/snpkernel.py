@@ -43,13 +43,52 @@ class SnpKernel(KernelReader):
         copier.input(self.snpreader)
         copier.input(self.standardizer)
 
+    def _partitioned(self, dtype, num_threads=None):
+        """The K of this SnpKernel computed partitioned over the process group (cfg5,
+        ``shard.grm_partitioned``: each rank keeps its 256x256 blocks in HBM) when
+        ``partitionedkernel.use_partitioned`` says the replicated K does not fit (or the mode is
+        "always"), as a ``PartitionedKernel`` -- cached per dtype, so later sub-matrix reads of this
+        SnpKernel reuse the blocks.  None: the replicated path applies."""
+        from pysnptools_amd import dist as dist_mod
+        from pysnptools_amd.kernelreader.partitionedkernel import PartitionedKernel, use_partitioned
+        from pysnptools_amd.snpreader.bed import Bed
+        from pysnptools_amd.snpreader.snpreader import _resolve
+        from pysnptools_amd.standardizer.standardizer import _std_args
+
+        dtype = np.dtype(dtype)
+        cache = self.__dict__.setdefault("_pk", {})
+        if dtype in cache:
+            return cache[dtype]
+        group = dist_mod.current()
+        if dtype not in (np.float32, np.float64) or _std_args(self.standardizer) is None:
+            return None
+        if not isinstance(_resolve(self.snpreader)[0], Bed) or not use_partitioned(self.snpreader.iid_count, dtype,
+                                                                                   group):
+            return None
+        from pysnptools_amd import shard
+
+        kw = {} if self.block_size is None else {"block_size": int(self.block_size)}
+        blocks, _, trained = shard.grm_partitioned(self.snpreader, self.standardizer, out="hbm", dtype=dtype,
+                                                   num_threads=num_threads, dist=group, **kw)
+        pk = PartitionedKernel(self.snpreader.iid, blocks, dist=group, name=str(self))
+        pk.snp_trained = trained
+        cache[dtype] = pk
+        return pk
+
     def _read(self, row_index_or_none, col_index_or_none, order, dtype, force_python_only, view_ok, num_threads):
         dtype = np.dtype(dtype)
         if (self.standardizer.is_constant and row_index_or_none is not None and col_index_or_none is not None
                 and np.array_equal(row_index_or_none, col_index_or_none)):
-            return self.snpreader[row_index_or_none, :]._read_kernel(self.standardizer, self.block_size, order, dtype,
-                                                                     force_python_only, view_ok,
-                                                                     num_threads=num_threads)
+            sub = SnpKernel(self.snpreader[row_index_or_none, :], self.standardizer, block_size=self.block_size)
+            pk = sub._partitioned(dtype, num_threads)
+            if pk is not None:
+                return pk._read(None, None, order, dtype, force_python_only, view_ok, num_threads)
+            return sub.snpreader._read_kernel(self.standardizer, self.block_size, order, dtype, force_python_only,
+                                              view_ok, num_threads=num_threads)
+        pk = self._partitioned(dtype, num_threads)
+        if pk is not None:
+            return pk._read(row_index_or_none, col_index_or_none, order, dtype, force_python_only, view_ok,
+                            num_threads)
         whole = self.snpreader._read_kernel(self.standardizer, self.block_size, order, dtype, force_python_only,
                                             view_ok, num_threads=num_threads)
         val, _ = self._apply_sparray_or_slice_to_val(whole, row_index_or_none, col_index_or_none, order, dtype,
@@ -71,6 +110,11 @@ class SnpKernel(KernelReader):
         """(K, snp_trained, kernel_trained) as FaST-LMM uses it (snpkernel.py:104-132).  With the
         default DiagKtoN, the trace and scale run on the GPU before K is copied out."""
         logging.info("Starting '_read_with_standardizing'")
+        pk = self._partitioned(np.float64, num_threads) if to_kerneldata else None
+        if pk is not None:  # K partitioned over the group: DiagKtoN from the trace summed over the parts
+            kernel, _, kernel_trained = pk._read_with_standardizing(to_kerneldata, None, kernel_standardizer,
+                                                                    return_trained=True, num_threads=num_threads)
+            return (kernel, pk.snp_trained, kernel_trained) if return_trained else kernel
         if to_kerneldata:
             from pysnptools_amd.standardizer import DiagKtoNTrained
             from pysnptools_amd.standardizer.diag_K_to_N import DiagKtoN as _DiagKtoN

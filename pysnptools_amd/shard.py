@@ -308,22 +308,14 @@ def grm_pieces(reader, standardizer, rank=None, world=None, dtype="float32", dia
 
 def part_coords(n, part, parts):
     """[nloc, 2] int64 (row0, col0) of the 256x256 upper-triangle blocks part ``part`` of ``parts``
-    owns -- ``snpmi_grm_part_coords`` for every local block at once (block L = J(J+1)/2 + I is
-    owned by part L mod parts; 238,755 blocks per part at 500k iids, one ctypes call each is slow).
-    The first and last entries are checked against the library."""
+    owns, in its storage order (``snpmi_grm_part_coords_all``: whole supertiles dealt round-robin,
+    include/snpmi.h)."""
     from pysnptools_amd import _native as N
 
     nloc = N.lib().snpmi_grm_part_blocks(n, part, parts)
-    L = np.arange(nloc, dtype=np.int64) * parts + part
-    J = ((np.sqrt(8.0 * L.astype(np.float64) + 1.0) - 1.0) * 0.5).astype(np.int64)
-    J += (J + 1) * (J + 2) // 2 <= L  # float rounding at the triangle boundaries
-    J -= J * (J + 1) // 2 > L
-    coords = np.stack([(L - J * (J + 1) // 2) * 256, J * 256], axis=1)
-    r0, c0 = ctypes.c_uint64(), ctypes.c_uint64()
-    for k in {0, nloc - 1} if nloc else ():
-        N.call("snpmi_grm_part_coords", n, part, parts, k, ctypes.byref(r0), ctypes.byref(c0))
-        assert (r0.value, c0.value) == tuple(coords[k]), "part_coords disagrees with the library"
-    return coords
+    coords = np.empty((nloc, 2), dtype=np.uint64)
+    N.call("snpmi_grm_part_coords_all", n, part, parts, N.ptr(coords))
+    return coords.astype(np.int64)
 
 
 class _DevBuf(object):
@@ -355,8 +347,9 @@ def block_spans(m, block, first_block=None):
 
 class PartitionedGrm(object):
     """cfg5: the GRM of a SNP stream whose K is too large to replicate, as one
-    process per GPU.  K is partitioned into the 256x256 blocks of its upper triangle, block L owned
-    by part ``L mod parts`` (``snpmi_grm_part_coords``); this process accumulates part ``part``.
+    process per GPU.  K is partitioned into the 256x256 blocks of its upper triangle, grouped into
+    16x16-block supertiles dealt round-robin over the parts (``part_coords``); this process
+    accumulates part ``part``.
 
     Per SNP block of ``block`` SNPs (the reference's block loop, snpreader.py:643-655; the first
     block is ``first_block`` = block/4 SNPs, so less host work precedes the first kernel; 32768-SNP
@@ -381,10 +374,14 @@ class PartitionedGrm(object):
     ``world``: bench.py computes part 0 of the 8-GPU plan on one GPU)."""
 
     def __init__(self, n_src, m, kind, a=0.0, b=0.0, use_stats=False, stats=None, iid_index=None, count_a1=False,
-                 dist=None, part=None, parts=None, block=32768, out=None, timing=False, first_block=None):
+                 dist=None, part=None, parts=None, block=32768, out=None, timing=False, first_block=None,
+                 dtype=np.float32):
         from pysnptools_amd import _native as N
 
         self.N = N
+        self.dtype = np.dtype(dtype)
+        if self.dtype not in (np.float32, np.float64):
+            raise ValueError("GRM dtype must be float32 or float64")
         self.dist = dist
         self.world = dist.world if dist is not None else 1
         self.rank = dist.rank if dist is not None else 0
@@ -426,28 +423,29 @@ class PartitionedGrm(object):
             if len(self.iid):
                 N.call("snpmi_memcpy_h2d", self.idx.p, N.ptr(self.iid), self.iid.nbytes)
             self._bufs += [self.rep, self.idx]
-        self.lut = _DevBuf(N, self.block * 16)
-        self.stats_dev = _DevBuf(N, max(1, self.m) * 8)
+        isz = self.dtype.itemsize
+        self.lut = _DevBuf(N, self.block * 4 * isz)
+        self.stats_dev = _DevBuf(N, max(1, self.m) * 2 * isz)
         self._bufs += [self.lut, self.stats_dev]
         if self.use_stats:
-            st = np.ascontiguousarray(stats, dtype=np.float32)
+            st = np.ascontiguousarray(stats, dtype=self.dtype)
             assert st.shape == (self.m, 2), "stats must be [m, 2]"
             N.call("snpmi_memcpy_h2d", self.stats_dev.p, N.ptr(st), st.nbytes)
         # the part's K blocks: in HBM (out="hbm" / an HbmArray: accumulated in place) or host
         if isinstance(out, str) and out == "hbm":
             from pysnptools_amd import hbm
 
-            out = hbm.empty((self.nloc, 256, 256), dtype=np.float32, order="C")
+            out = hbm.empty((self.nloc, 256, 256), dtype=self.dtype, order="C")
         if out is None:
-            out = np.empty((self.nloc, 256, 256), dtype=np.float32)
-        assert tuple(out.shape) == (self.nloc, 256, 256) and np.dtype(out.dtype) == np.float32
+            out = np.empty((self.nloc, 256, 256), dtype=self.dtype)
+        assert tuple(out.shape) == (self.nloc, 256, 256) and np.dtype(out.dtype) == self.dtype
         assert getattr(out, "order", None) == "C" if hasattr(out, "snpmi_ptr") else out.flags["C_CONTIGUOUS"]
         self.out = out
         dev_out = getattr(out, "snpmi_ptr", None)
         if dev_out is not None:
             self.blocks = dev_out
         else:
-            self._kbuf = _DevBuf(N, self.nloc * 256 * 256 * 4)
+            self._kbuf = _DevBuf(N, self.nloc * 256 * 256 * isz)
             self._bufs.append(self._kbuf)
             self.blocks = self._kbuf.p
         self._ev = []
@@ -471,7 +469,7 @@ class PartitionedGrm(object):
         used = [False, False]
         marks = [(self._event(), self._event()) for _ in range(nblk)] if self.timing else None
         if self.m == 0 or self.n == 0:
-            N.call("snpmi_dev_memset", self.blocks, 0, self.nloc * 256 * 256 * 4)
+            N.call("snpmi_dev_memset", self.blocks, 0, self.nloc * 256 * 256 * self.dtype.itemsize)
         for k in range(nblk if self.n else 0):
             s0, cnt = spans[k]
             ms = (cnt + self.world - 1) // self.world
@@ -507,11 +505,11 @@ class PartitionedGrm(object):
             if self.rep is not None:
                 N.call("snpmi_dev_repack", packed, pitch, self.n_src, self.idx.p, self.n, cnt, self.rep.p, self.pitch)
                 packed, pitch = self.rep.p, self.pitch
-            st = ctypes.c_void_p(self.stats_dev.p.value + s0 * 8)
+            st = ctypes.c_void_p(self.stats_dev.p.value + s0 * 2 * self.dtype.itemsize)
             N.call("snpmi_dev_snp_stats", packed, pitch, self.n, cnt, int(bool(self.count_a1)), self.kind, self.a,
-                   self.b, int(self.use_stats), N.DT_F32, st, self.lut.p)
-            N.call("snpmi_dev_syrk_packed_part", packed, pitch, self.n, cnt, self.lut.p, self.part, self.parts,
-                   self.blocks, int(k > 0))
+                   self.b, int(self.use_stats), N.dt_code(self.dtype), st, self.lut.p)
+            N.call("snpmi_dev_syrk_packed_part" + ("_f64" if self.dtype == np.float64 else ""), packed, pitch, self.n,
+                   cnt, self.lut.p, self.part, self.parts, self.blocks, int(k > 0))
             if marks:
                 N.call("snpmi_event_record", marks[k][1])
             N.call("snpmi_event_record", done[slot])
@@ -532,8 +530,8 @@ class PartitionedGrm(object):
         return block_spans(self.m, self.block, self.first_block)
 
     def stats(self):
-        """[m, 2] float32 per-SNP (mean, std) of the stream (or the given stats)."""
-        st = np.empty((self.m, 2), dtype=np.float32)
+        """[m, 2] per-SNP (mean, std) of the stream (or the given stats), in the GRM dtype."""
+        st = np.empty((self.m, 2), dtype=self.dtype)
         if self.m:
             self.N.call("snpmi_memcpy_d2h", self.N.ptr(st), self.stats_dev.p, st.nbytes)
         return st
@@ -557,7 +555,8 @@ class PartitionedGrm(object):
         self._bufs = []
 
 
-def _partitioned_bed(base, rows, cols, kind, a, b, use_stats, stats, dist, part, parts, block_size, out, threads):
+def _partitioned_bed(base, rows, cols, kind, a, b, use_stats, stats, dist, part, parts, block_size, out, threads,
+                     dtype=np.float32):
     """``PartitionedGrm`` over a .bed: each rank's share of a block gathered from the file's mmap
     (``snpmi_bed_gather_packed``).  Returns (blocks, coords, stats)."""
     from pysnptools_amd import _native as N
@@ -566,7 +565,7 @@ def _partitioned_bed(base, rows, cols, kind, a, b, use_stats, stats, dist, part,
     col_index = np.arange(base.sid_count, dtype=np.uint64) if cols is None else np.ascontiguousarray(cols, dtype=np.uint64)
     path = base.filename.encode()
     g = PartitionedGrm(base.iid_count, m, kind, a, b, use_stats, stats, iid_index=rows, count_a1=base.count_A1,
-                       dist=dist, part=part, parts=parts, block=block_size, out=out)
+                       dist=dist, part=part, parts=parts, block=block_size, out=out, dtype=dtype)
 
     def fill(host, s0, cnt):
         N.call("snpmi_bed_gather_packed", path, base.iid_count, base.sid_count, N.ptr(col_index[s0:s0 + cnt]), cnt,
@@ -584,7 +583,7 @@ def _partitioned_bed(base, rows, cols, kind, a, b, use_stats, stats, dist, part,
 
 
 def grm_partitioned(reader, standardizer, rank=None, world=None, out=None, num_threads=None, dist=None,
-                    block_size=32768):
+                    block_size=32768, dtype=np.float32):
     """cfg5 GRM of a Bed (or a subset of one) too large to replicate: K is
     partitioned over the ranks as the 256x256 blocks of its upper triangle
     (``snpmi_grm_part_coords``) and this rank keeps only its own blocks.
@@ -596,7 +595,10 @@ def grm_partitioned(reader, standardizer, rank=None, world=None, out=None, num_t
     * Without one: part ``rank`` of ``world`` (default 0 of 1) on this GPU alone, streaming every
       SNP of the .bed itself (``snpmi_grm_part_bed_f32``) -- e.g. the parts of a job run one by one.
 
-    Returns (blocks [n_local, 256, 256] float32 -- ``out`` if given, e.g. an ``np.memmap`` of a
+    ``dtype``: float32 (fp16x2 MFMA, exact diagonal) or float64 -- the reference's default GRM
+    dtype (snpreader.py:528,623) -- on the int8 MFMA as exact residue products.
+
+    Returns (blocks [n_local, 256, 256] of ``dtype`` -- ``out`` if given, e.g. an ``np.memmap`` of a
     file, or ``"hbm"`` / an ``hbm.HbmArray`` to keep the blocks in device memory (accumulated in
     place, no copy-out) --, coords [n_local, 2] int64 = (row0, col0) of each block, trained
     standardizer).  Entries of a block beyond iid n-1 are padding."""
@@ -615,15 +617,18 @@ def grm_partitioned(reader, standardizer, rank=None, world=None, out=None, num_t
     base._run_once()
     sid = reader.sid
     n = reader.iid_count
-    stats = (np.ascontiguousarray(standardizer.stats_for(sid), dtype=np.float32) if use_stats
-             else np.empty((len(sid), 2), dtype=np.float32))
+    dtype = np.dtype(dtype)
+    if dtype not in (np.float32, np.float64):
+        raise ValueError("GRM dtype must be float32 or float64")
+    stats = (np.ascontiguousarray(standardizer.stats_for(sid), dtype=dtype) if use_stats
+             else np.empty((len(sid), 2), dtype=dtype))
     d = dist if dist is not None else dist_mod.current()
     threads = get_num_threads(num_threads if num_threads is not None else base._num_threads)
     if d is not None and d.world > 1:
         if (rank is not None and rank != d.rank) or (world is not None and world != d.world):
             raise ValueError("rank/world %s/%s differ from the process group's %d/%d" % (rank, world, d.rank, d.world))
         blocks, coords, stats = _partitioned_bed(base, rows, cols, kind, a, b, use_stats, stats, d, d.rank, d.world,
-                                                 block_size, out, threads)
+                                                 block_size, out, threads, dtype)
         return blocks, coords, _trained_from(standardizer, kind, a, b, sid, stats)
     rank = 0 if rank is None else int(rank)
     world = 1 if world is None else int(world)
@@ -631,22 +636,24 @@ def grm_partitioned(reader, standardizer, rank=None, world=None, out=None, num_t
     if isinstance(out, str) and out == "hbm":
         from pysnptools_amd import hbm
 
-        out = hbm.empty((nloc, 256, 256), dtype=np.float32, order="C")
+        out = hbm.empty((nloc, 256, 256), dtype=dtype, order="C")
     elif out is None:
-        out = np.empty((nloc, 256, 256), dtype=np.float32)
-    assert tuple(out.shape) == (nloc, 256, 256) and np.dtype(out.dtype) == np.float32
+        out = np.empty((nloc, 256, 256), dtype=dtype)
+    assert tuple(out.shape) == (nloc, 256, 256) and np.dtype(out.dtype) == dtype
     assert getattr(out, "order", None) == "C" if hasattr(out, "snpmi_ptr") else out.flags["C_CONTIGUOUS"]
     ri, ci = N.index_array(rows), N.index_array(cols)
-    N.call("snpmi_grm_part_bed_f32", base.filename.encode(), base.iid_count, base.sid_count,
+    N.call("snpmi_grm_part_bed_" + N.suffix(dtype), base.filename.encode(), base.iid_count, base.sid_count,
            int(bool(base.count_A1)), N.ptr(ri), n, N.ptr(ci), len(sid), kind, a, b, int(use_stats), N.ptr(stats),
            rank, world, N.ptr(out), threads)
     return out, part_coords(n, rank, world), _trained_from(standardizer, kind, a, b, sid, stats)
 
 
 def assemble_partitioned(parts, n):
-    """Full symmetric n x n K (float32) from every rank's (blocks, coords) -- for sizes that fit."""
+    """Full symmetric n x n K (the blocks' dtype) from every rank's (blocks, coords) -- for sizes
+    that fit."""
     nb = (n + 255) // 256
-    K = np.zeros((nb * 256, nb * 256), dtype=np.float32)
+    dt = next((np.dtype(b.dtype) for b, _ in parts if len(b)), np.dtype(np.float32))
+    K = np.zeros((nb * 256, nb * 256), dtype=dt)
     for blocks, coords in parts:
         for blk, (i, j) in zip(blocks, coords):
             K[i:i + 256, j:j + 256] = blk

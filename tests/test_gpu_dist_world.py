@@ -119,3 +119,86 @@ def test_partitioned_allgather_plan(world_run, name, beta):
     np.testing.assert_array_equal(c0, _load(out, "%s_part_%s_coords" % (name, tag), 0))
     K0 = shard.assemble_partitioned([(b0, c0)] + parts[1:], len(rows))
     assert _err(K0, Kref) <= 1e-5
+
+
+@pytest.mark.parametrize("name", ["n300", "toydata"])
+def test_partitioned_f64_under_the_group(world_run, name):
+    """cfg5 in float64 (the reference's default dtype) under the group: each rank's f64 blocks equal
+    the same part computed by one process, and the parts assembled match the f64 oracle within
+    1e-12 of max diag."""
+    from pysnptools_amd import shard
+    from pysnptools_amd.snpreader import Bed
+    from pysnptools_amd.standardizer import Unit
+
+    world, out = world_run
+    n, m = FIX[name]
+    rows = np.arange(n - 1, 0, -2)
+    Kref, sref = _oracle(name, iid_index=rows)
+    bed = Bed(os.path.join(DATA, name + ".bed"), count_A1=False)
+    parts = []
+    for r in range(world):
+        blocks = _load(out, "%s_part_f64_blocks" % name, r)
+        coords = _load(out, "%s_part_f64_coords" % name, r)
+        np.testing.assert_array_equal(_load(out, "%s_part_f64_stats" % name, r), sref)
+        b1, c1, _ = shard._partitioned_bed(bed, rows, None, 1, 0.0, 0.0, False, None, None, r, world, 97, None, 4,
+                                           np.float64)
+        np.testing.assert_array_equal(coords, c1)
+        np.testing.assert_array_equal(blocks, b1)
+        parts.append((blocks, coords))
+    assert _err(shard.assemble_partitioned(parts, len(rows)), Kref) <= 1e-12
+
+
+@pytest.mark.parametrize("dtype", ["float32", "float64"])
+def test_partitioned_many_blocks_under_the_group(world_run, dtype):
+    """A 2300-iid K (9 x 9 blocks): every part of the world-2/3 plan owns blocks; the parts tile K
+    once and assemble to the f64 oracle (f32 1e-5, f64 1e-12 of max diag)."""
+    from _gpu_dist_worker import SYNTH
+    from pysnptools_amd import shard
+
+    world, out = world_run
+    n, m = SYNTH
+    body = O.read_bed_bytes(os.path.join(str(out), "synth.bed"))
+    Z = O.decode(body, n, m, dtype=np.float64)
+    O.standardize_native(Z)
+    Kref = Z.dot(Z.T)
+    parts = [(_load(out, "synth_part_%s_blocks" % dtype, r), _load(out, "synth_part_%s_coords" % dtype, r))
+             for r in range(world)]
+    assert all(len(b) for b, _ in parts)
+    assert sum(len(c) for _, c in parts) == 45
+    assert _err(shard.assemble_partitioned(parts, n), Kref) <= (1e-12 if dtype == "float64" else 1e-5)
+
+
+@pytest.mark.parametrize("name", ["n300", "synth"])
+def test_partitioned_k_through_the_kernelreader_api(world_run, name):
+    """with K partitioned over the group (set_grm_partition("always")), the
+    reference's KernelReader entry points -- SnpKernel(bed, Unit())[rows, cols].read(),
+    Bed.read_kernel, SnpKernel._read_with_standardizing (DiagKtoN) -- return on EVERY rank the K the
+    oracle computes (f32 <= 1e-5, f64 <= 1e-12 of max diag, elementwise), and the blocks written by
+    PartitionedKernel.write and read back by PartitionedKernel.load serve the same sub-matrix."""
+    from _gpu_dist_worker import SYNTH, pk_indices
+
+    world, out = world_run
+    if name == "n300":
+        n, m = FIX[name]
+        body = O.read_bed_bytes(os.path.join(DATA, name + ".bed"))
+    else:
+        n, m = SYNTH
+        body = O.read_bed_bytes(os.path.join(str(out), "synth.bed"))
+    Z = O.decode(body, n, m, dtype=np.float64)
+    O.standardize_native(Z)
+    Kref = Z.dot(Z.T)
+    rows, cols = pk_indices(n)
+    sub = Kref[np.ix_(rows, cols)]
+    scale = np.abs(np.diag(Kref)).max()
+    factor = n / np.trace(Kref)
+    for r in range(world):
+        for dt, tol in (("float32", 1e-5), ("float64", 1e-12)):
+            got = _load(out, "%s_pk_sub_%s" % (name, dt), r)
+            assert got.dtype == np.dtype(dt) and got.shape == sub.shape
+            assert np.abs(got - sub).max() / scale <= tol, (r, dt)
+            full = _load(out, "%s_pk_full_%s" % (name, dt), r)
+            assert np.abs(full - Kref).max() / scale <= tol, (r, dt)
+            assert np.array_equal(full, full.T)
+        np.testing.assert_allclose(_load(out, "%s_pk_factor" % name, r)[0], factor, rtol=1e-13)
+        assert np.abs(_load(out, "%s_pk_diag" % name, r) - Kref * factor).max() / (scale * factor) <= 1e-12
+        np.testing.assert_array_equal(_load(out, "%s_pk_loaded" % name, r), _load(out, "%s_pk_sub_float32" % name, r))

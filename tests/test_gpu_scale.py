@@ -133,57 +133,67 @@ def test_grm_config4_50k_x_500k():
     assert np.array_equal(K, K.T)
 
 
-@pytest.mark.parametrize("part", [0, 5])
-def test_config4_partitioned_500k_iids(part):
+@pytest.mark.parametrize("part,dtype,m", [(0, np.float32, 2048), (5, np.float32, 2048), (0, np.float64, 8192)])
+def test_config4_partitioned_500k_iids(part, dtype, m):
     """BASELINE configs[4] at its iid count: K of 500,000 iids is 500 GB (f32 upper triangle), so it
-    is partitioned as 256x256 blocks over the 8 parts of the 8-GPU plan (snpmi_dev_syrk_packed_part);
-    this runs part `part` of 8 over 2048 synthetic SNPs (~64 GB of K blocks in HBM) and checks a
-    diagonal and an off-diagonal block against the f64 oracle on just those iids, with stats over
-    all 500k iids (the reference replicates K, snpreader.py:643-655, which cannot hold this)."""
-    n, m, P = 500_000, 2048, 8
+    is partitioned as 256x256 blocks over the 8 parts of the 8-GPU plan (snpmi_dev_syrk_packed_part,
+    whole 16x16-block supertiles per part); this runs part `part` of 8 over `m` synthetic SNPs (~64
+    GB of f32 / ~125 GB of f64 K blocks in HBM) and checks a diagonal and an off-diagonal block and
+    the part's last one against the f64 oracle on just those iids, with stats over all 500k iids
+    (the reference replicates K, snpreader.py:643-655, which cannot hold this).  float64 -- the
+    reference's default GRM dtype (snpreader.py:528,623) -- runs the int8-CRT part kernels
+    (snpmi_dev_syrk_packed_part_f64) and must match within 1e-12 of max diag; f32 within 1e-5."""
+    n, P = 500_000, 8
+    isz = np.dtype(dtype).itemsize
     pitch = N.lib().snpmi_packed_pitch(n)
     nloc = N.lib().snpmi_grm_part_blocks(n, part, P)
     nb = (n + 255) // 256
-    assert nloc == (nb * (nb + 1) // 2 - part + P - 1) // P
+    assert sum(N.lib().snpmi_grm_part_blocks(n, r, P) for r in range(P)) == nb * (nb + 1) // 2
     packed = Dev(pitch * m)
     x, cdf = O.maf_table(n)
     N.call("snpmi_dev_synth_bed", packed.p, pitch, n, 0, m, 11, 0.01, N.ptr(x), N.ptr(cdf), len(x))
-    lut, st = Dev(m * 16), Dev(m * 8)
-    blocks = Dev(nloc * 256 * 256 * 4)
-    N.call("snpmi_dev_snp_stats", packed.p, pitch, n, m, 0, N.STD_UNIT, 0.0, 0.0, 0, N.DT_F32, st.p, lut.p)
-    N.call("snpmi_dev_syrk_packed_part", packed.p, pitch, n, m, lut.p, part, P, blocks.p, 0)
+    lut, st = Dev(m * 4 * isz), Dev(m * 2 * isz)
+    blocks = Dev(nloc * 256 * 256 * isz)
+    N.call("snpmi_dev_snp_stats", packed.p, pitch, n, m, 0, N.STD_UNIT, 0.0, 0.0, 0, N.dt_code(np.dtype(dtype)), st.p,
+           lut.p)
+    if dtype == np.float64:
+        N.call("snpmi_dev_syrk_packed_part_f64", packed.p, pitch, n, m, lut.p, part, P, blocks.p, 0)
+    else:
+        N.call("snpmi_dev_syrk_packed_part", packed.p, pitch, n, m, lut.p, part, P, blocks.p, 0)
     N.call("snpmi_stream_sync")
     host = np.empty((m, pitch), dtype=np.uint8)
     N.call("snpmi_memcpy_d2h", N.ptr(host), packed.p, host.nbytes)
+    del packed
     body = np.ascontiguousarray(host[:, :(n + 3) // 4]).reshape(-1)
     stats = O.snp_stats(body, n, m)
     # the part's diagonal block nearest the start, an off-diagonal one, and its very last block
     # (which touches the padded iids 499,968..500,223 when it sits in the last block column)
     want = {"diag": None, "off": None, "last": nloc - 1}
     r0, c0 = ctypes.c_uint64(), ctypes.c_uint64()
-    for b in range(min(nloc, 200)):
+    for b in range(min(nloc, 300)):
         N.call("snpmi_grm_part_coords", n, part, P, b, ctypes.byref(r0), ctypes.byref(c0))
         if r0.value == c0.value and want["diag"] is None:
             want["diag"] = b
         if r0.value != c0.value and want["off"] is None:
             want["off"] = b
     assert want["diag"] is not None and want["off"] is not None
+    tol = 1e-12 if dtype == np.float64 else 1e-5
     for what, b in want.items():
         N.call("snpmi_grm_part_coords", n, part, P, b, ctypes.byref(r0), ctypes.byref(c0))
         rows = np.arange(r0.value, min(r0.value + 256, n))
         cols = np.arange(c0.value, min(c0.value + 256, n))
-        blk = np.empty((256, 256), dtype=np.float32)
-        N.call("snpmi_memcpy_d2h", N.ptr(blk), blocks.at(b * 256 * 256 * 4), blk.nbytes)
-        Zr = O.decode(body, n, m, iid_index=rows)
-        Zc = O.decode(body, n, m, iid_index=cols)
+        blk = np.empty((256, 256), dtype=dtype)
+        N.call("snpmi_memcpy_d2h", N.ptr(blk), blocks.at(b * 256 * 256 * isz), blk.nbytes)
+        Zr = O.decode(body, n, m, iid_index=rows, dtype=np.float64)
+        Zc = O.decode(body, n, m, iid_index=cols, dtype=np.float64)
         O.standardize_native(Zr, use_stats=True, stats=stats)
         O.standardize_native(Zc, use_stats=True, stats=stats)
         ref = Zr.dot(Zc.T)
         scale = max(np.abs(np.diag(ref)).max() if r0.value == c0.value else np.abs(ref).max(), 1.0)
         err = np.abs(blk[:len(rows), :len(cols)].astype(np.float64) - ref).max() / scale
-        assert err <= 1e-5, "%s block %d (%d, %d): %g" % (what, b, r0.value, c0.value, err)
+        assert err <= tol, "%s block %d (%d, %d): %g" % (what, b, r0.value, c0.value, err)
         if r0.value == c0.value:
-            np.testing.assert_allclose(np.diag(blk)[:len(rows)], np.diag(ref), rtol=1e-5)
+            np.testing.assert_allclose(np.diag(blk)[:len(rows)], np.diag(ref), rtol=tol)
 
 
 class _OneRank:
