@@ -31,11 +31,14 @@ Metric (BASELINE.json): "SNPs/sec standardized (500k x 1M) + GRM GF/s at 1/2/4/8
                added to the f64 K (syrk_crt.hip).  roofline vs the int8 dense peak (2 x bf16 =
                5.0 POP/s) on the executed ops; f64_equiv_tflops = N(N+1)M / time, beside the f64
                MFMA's 78.6 TF dense peak.
-  grm5       = configs[4] shape: 500k iids, K (500 GB f32 upper triangle) partitioned over the 8
-               ranks of the 8-GPU plan as 256x256 blocks; this process computes part `rank` of
-               max(N, 8) for one 8192-SNP block uploaded from pinned host memory inside the timed
-               region (1/N each + RCCL all-gather at N > 1), parity-checked on a diagonal and an
-               off-diagonal block, projected to 1M SNPs.
+  grm5       = configs[4]: 500k iids x 1M SNPs, K (500 GB f32 upper triangle) partitioned over the
+               8 parts of the 8-GPU plan as 256x256 blocks owned by whole 16x16-block supertiles;
+               this process computes part `rank` of max(N, 8) over ALL the job's SNPs, streamed in
+               32768-SNP blocks (the first a quarter) from pinned host memory inside the timed
+               region (each rank's 1/N share + RCCL all-gather at N > 1) -- the whole per-part job
+               measured, no projection; parity of sample blocks vs the f64 oracle over all SNPs.
+               At N < 8 the rate fields are `part_*` (one part of 8); `single_gpu_job_*_projected`
+               = 8 parts one after another on this GPU, labelled as the projection it is.
   beta       = configs[2]: 100k iid x 1M SNP, Beta(1,25) + NaN impute (21.8% missing, SnpGen's
                rate), packed resident in HBM, stats + decode in 2048-SNP blocks (f32, F order).
   file       = the reference's own call path on a synthetic 50k x 100k .bed written to local disk
@@ -826,6 +829,14 @@ def leg_grm5(N, args, dist):
     return res
 
 
+def grm5_part_spread(n, P):
+    """(largest - smallest) / smallest block count over the P parts of the plan."""
+    from pysnptools_amd import _native as N
+
+    c = [N.lib().snpmi_grm_part_blocks(n, r, P) for r in range(P)]
+    return (max(c) - min(c)) / max(min(c), 1)
+
+
 def grm5_gather_check(N, args, dist, P, fill):
     """N > 1: one more block through the same plan (each rank's share + all-gather, untimed); rank 0
     compares the rebuilt block with the block generated whole on its host."""
@@ -1284,16 +1295,25 @@ def main(argv=None):
                 "exposed_wait_seconds": max(0.0, r3["wall"] - busy_s),
                 "block_ms_mean": float(np.mean(r3["block_ms"])), "block_ms_first": r3["block_ms"][0],
                 "block_ms_max": float(np.max(r3["block_ms"])),
-                "gflops_per_gpu": flops_part / r3["wall"] / 1e9, "syrk_tflops": syrk_tf,
-                "snps_per_s": m5 / r3["wall"], "parts": P, "scaling": "strong",
+                "syrk_tflops": syrk_tf, "parts": P, "scaling": "strong",
                 "job_note": "the P parts run concurrently on P GPUs at N = P, so `seconds` is the 8-GPU job time at "
-                            "N = 8; at N = 1 it is one part's share of that job, measured whole",
+                            "N = 8; at N < P it is one part's share of that job, measured whole (`part_*` rates; "
+                            "`single_gpu_job_*_projected` = all P parts one after another on one GPU)",
                 "blocks_on_rank0": r3["n_local_blocks"], "K_bytes_per_rank": r3["n_local_blocks"] * 256 * 256 * 4,
                 "roofline": {"bound": "mfma", "achieved": syrk_tf, "peak": SPLIT_PEAK_TFLOPS, "unit": "TFLOP/s",
                              "frac": syrk_tf / SPLIT_PEAK_TFLOPS, "traffic": None,
                              "kernel": "f32w::k_syrk_h2<true,4> (fp16x2 split, 3 fp16 MFMA products, f32 "
                                        "accumulate), this part's blocks only; time = the blocks' compute-stream "
                                        "spans (stats + SYRK%s)" % (" + all-gather" if gather else "")}}
+        if dist.world >= P:  # every part runs: the job measured whole
+            grm5.update({"gflops_per_gpu": flops_part / r3["wall"] / 1e9, "snps_per_s": m5 / r3["wall"]})
+        else:
+            grm5.update({"part_gflops": flops_part / r3["wall"] / 1e9, "part_snps_per_s": m5 / r3["wall"],
+                         "single_gpu_job_seconds_projected": P * r3["wall"],
+                         "single_gpu_job_snps_per_s_projected": m5 / (P * r3["wall"]),
+                         "projection_note": "projection, not a measurement: part %d of %d measured whole, times %d "
+                                            "(the parts are the same size within %.1f%%)"
+                                            % (dist.rank, P, P, 100.0 * grm5_part_spread(n5, P))})
         if r3.get("parity_sample") is not None:
             grm5["parity"] = grm5_parity(args, r3["parity_sample"][0], r3["parity_sample"][1], r3["threads"])
         elif dist.rank == 0:

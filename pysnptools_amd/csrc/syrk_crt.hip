@@ -419,6 +419,144 @@ __global__ __launch_bounds__(512, 1) void k_syrk_i8r(const uint8_t* __restrict__
         }
 }
 
+// Ring form (round 5): a ring of 4 LDS slots of 64 SNPs (4 x 36 KiB = 144 KiB), stage s+2's
+// residue rows expanded and stored while stage s is multiplied, one barrier per 64-SNP stage.
+// Because a slot is complete one full stage before it is read, each wave reads the NEXT stage's
+// first fragments before the barrier (PF): the post-barrier fragment-read latency that the
+// two-slot form exposes at the head of every 128-SNP stage is hidden under the barrier wait.
+// PRIO: s_setprio 1 on waves 4-7 (the later-dispatched partner of each SIMD pair) for the loop.
+template <int PF = 1, int PRIO = 0>
+__global__ __launch_bounds__(512, 1) void k_syrk_i8q(const uint8_t* __restrict__ P, uint64_t pitch, uint64_t kdim,
+                                                     uint64_t mpad, const uint32_t* __restrict__ lutr,
+                                                     const int* __restrict__ ctl, uint64_t b0, uint64_t nblk,
+                                                     uint8_t* __restrict__ res,
+                                                     const uint32_t* __restrict__ part_tab = nullptr) {
+    constexpr int SKT = 64, KS = SKT / 32, RPT = SKT / 16, PNL = SKT * RS, STG = 2 * PNL, NSLOT = 4;
+    __shared__ __attribute__((aligned(16))) uint8_t lds[NSLOT * STG];
+    if (ctl[1]) return;  // non-finite LUT: the f64 MFMA kernel runs instead
+    const int r = blockIdx.y;
+    if (r >= ctl[2]) return;  // K_int fits the first ctl[2] moduli
+    const uint32_t* lr = lutr + (uint64_t)r * mpad;
+    uint32_t bi, bj;
+    if (part_tab) {
+        const uint32_t c = part_tab[b0 + blockIdx.x];
+        bi = c & 0xffffu;
+        bj = c >> 16;
+    } else {
+        tile_coords(b0 + blockIdx.x, bi, bj);
+    }
+    const uint64_t i0 = (uint64_t)bi * BW, j0 = (uint64_t)bj * BW;
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const int wm = wave >> 2, wn = wave & 3;
+    const int lp = __builtin_amdgcn_readfirstlane(t >> 8), kq = (t >> 4) & 15, d = t & 15;
+    const uint8_t* pbase = P + (lp ? j0 : i0) / 4;
+    const uint32_t pit = (uint32_t)pitch;
+    const uint32_t* lq = lr + RPT * kq;
+    const int g = lane >> 4, jj = (lane & 15) >> 1, pp = lane & 1;
+    const int rd = (16 * (g >> 1) + jj) * RS + 16 * (g & 1) + 8 * pp;
+
+    v16i acc[4][2];
+#pragma unroll
+    for (int x = 0; x < 4; x++)
+#pragma unroll
+        for (int y = 0; y < 2; y++) acc[x][y] = (v16i){};
+    const uint64_t nst = (kdim + SKT - 1) / SKT;
+    uint32_t cw[RPT];
+    uint4 cl[RPT / 4];
+    auto load = [&](uint64_t st) {  // st < nst
+        const uint8_t* sb = pbase + st * SKT * pitch;
+        const uint32_t lim = (uint32_t)(kdim - 1 - st * SKT);
+#pragma unroll
+        for (int h = 0; h < RPT; h++) {
+            const uint32_t row = min((uint32_t)(RPT * kq + h), lim);
+            cw[h] = *reinterpret_cast<const uint32_t*>(sb + (row * pit + 4 * d));
+        }
+#pragma unroll
+        for (int u = 0; u < RPT / 4; u++) cl[u] = *reinterpret_cast<const uint4*>(lq + SKT * st + 4 * u);
+    };
+    auto store = [&](uint8_t* S, int h0, int h1) {
+#pragma unroll
+        for (int h = h0; h < h1; h++) {
+            const uint4 c4 = cl[h >> 2];
+            const uint32_t L = (h & 3) == 0 ? c4.x : (h & 3) == 1 ? c4.y : (h & 3) == 2 ? c4.z : c4.w;
+            uint4 o;
+            o.x = __builtin_amdgcn_perm(L, L, cw[h] & 0x03030303u);
+            o.y = __builtin_amdgcn_perm(L, L, (cw[h] >> 2) & 0x03030303u);
+            o.z = __builtin_amdgcn_perm(L, L, (cw[h] >> 4) & 0x03030303u);
+            o.w = __builtin_amdgcn_perm(L, L, (cw[h] >> 6) & 0x03030303u);
+            *reinterpret_cast<uint4*>(S + lp * PNL + (RPT * kq + h) * RS + 16 * d) = o;
+        }
+    };
+    auto frag = [&](const uint8_t* S, int panel, int ks, int col) -> v4i {
+        const uint8_t* b = S + panel * PNL + 32 * ks * RS + rd + col;
+        const v2i x = lds_tr8(b), y = lds_tr8(b + 8 * RS);
+        return (v4i){x.x, x.y, y.x, y.y};
+    };
+    auto frags = [&](const uint8_t* S, int ks, v4i (&A)[4], v4i (&B)[2]) {
+#pragma unroll
+        for (int x = 0; x < 4; x++) A[x] = frag(S, 0, ks, wm * 128 + 32 * x);
+#pragma unroll
+        for (int y = 0; y < 2; y++) B[y] = frag(S, 1, ks, wn * 64 + 32 * y);
+    };
+    auto slot = [&](uint64_t st) { return lds + (st & (NSLOT - 1)) * STG; };
+    // prologue: stages 0 and 1 stored, stage 2's codes in registers
+    load(0);
+    store(slot(0), 0, RPT);
+    load(nst > 1 ? 1 : 0);
+    store(slot(1), 0, RPT);
+    load(nst > 2 ? 2 : nst - 1);
+    __syncthreads();
+    if constexpr (PRIO) {
+        if (wave >= 4) __builtin_amdgcn_s_setprio(1);
+    }
+    v4i a[2][4], b[2][2];
+    frags(slot(0), 0, a[0], b[0]);
+    for (uint64_t s = 0; s < nst; s++) {
+        const uint8_t* cur = slot(s);
+        uint8_t* nxt = slot(s + 2);  // stage s+2 (read two stages from now; its slot was last read in stage s-2)
+#pragma unroll
+        for (int ks = 0; ks < KS; ks++) {
+            const int q = (ks + 1) & 1;
+            if (ks + 1 < KS) {
+                frags(cur, ks + 1, a[q], b[q]);
+            } else if constexpr (PF) {
+                // stage s+1 was stored during stage s-1: complete since the last barrier
+                frags(slot(s + 1), 0, a[q], b[q]);
+            }
+#pragma unroll
+            for (int x = 0; x < 4; x++)
+#pragma unroll
+                for (int y = 0; y < 2; y++)
+                    acc[x][y] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[ks & 1][x], b[ks & 1][y], acc[x][y], 0, 0, 0);
+            store(nxt, ks * RPT / KS, (ks + 1) * RPT / KS);
+        }
+        load(s + 3 < nst ? s + 3 : nst - 1);
+        __syncthreads();
+        if constexpr (!PF) frags(slot(s + 1), 0, a[0], b[0]);
+    }
+    if constexpr (PRIO) {
+        if (wave >= 4) __builtin_amdgcn_s_setprio(0);
+    }
+    const int p = kMod[r];
+    const double invp = 1.0 / (double)p;
+    uint8_t* O = res + ((uint64_t)r * nblk + blockIdx.x) * (BW * BW);
+    const int hh = lane >> 5, colp = 16 * ((lane >> 4) & 1) + pi16(lane & 15);
+#pragma unroll
+    for (int x = 0; x < 4; x++)
+#pragma unroll
+        for (int y = 0; y < 2; y++) {
+            uint8_t* bp = O + (wm * 128 + 32 * x + hh) * BW + wn * 64 + 32 * y + colp;
+#pragma unroll
+            for (int q = 0; q < 16; q++) {
+                const int v = acc[x][y][q];
+                int rr = v - p * (int)floor((double)v * invp);
+                rr += rr < 0 ? p : 0;
+                rr -= rr >= p ? p : 0;
+                bp[(16 * (q >> 3) + 4 * (q & 3) + 2 * ((q >> 2) & 1)) * BW] = (uint8_t)rr;
+            }
+        }
+}
+
 #ifdef SNPMI_UBENCH
 // ubench (variant 77): 4 waves (2 x 2), one per SIMD, 128 x 128 per wave = 4 x 4
 // v_mfma_i32_32x32x32_i8 tiles (256 accumulator registers, AGPR-backed): 8 fragment reads per 16
@@ -763,6 +901,15 @@ void launch_syrk_packed_crt(const uint8_t* packed, uint64_t pitch, uint64_t n, u
             k_syrk_i8r<SK, 0, 0, 0, 1><<<dim3((unsigned)cnt, kR), 512, 0, st>>>(packed, pitch, m, mpad, lutr, ctl, b0, cnt, res);
         else if (g_variant_syrk == 74)  // ablation: fragments read once per stage
             k_syrk_i8r<SK, 2><<<dim3((unsigned)cnt, kR), 512, 0, st>>>(packed, pitch, m, mpad, lutr, ctl, b0, cnt, res);
+        else if (g_variant_syrk == 80)  // 4-slot ring of 64-SNP stages, next stage's fragments read before the barrier
+            k_syrk_i8q<1, 0><<<dim3((unsigned)cnt, kR), 512, 0, st>>>(packed, pitch, m, mpad, lutr, ctl, b0, cnt, res,
+                                                                     part_tab);
+        else if (g_variant_syrk == 81)  // the ring without the cross-barrier prefetch
+            k_syrk_i8q<0, 0><<<dim3((unsigned)cnt, kR), 512, 0, st>>>(packed, pitch, m, mpad, lutr, ctl, b0, cnt, res,
+                                                                     part_tab);
+        else if (g_variant_syrk == 82)  // ring + prefetch + s_setprio 1 on waves 4-7
+            k_syrk_i8q<1, 1><<<dim3((unsigned)cnt, kR), 512, 0, st>>>(packed, pitch, m, mpad, lutr, ctl, b0, cnt, res,
+                                                                     part_tab);
         else
 #endif
         k_syrk_i8r<SK><<<dim3((unsigned)cnt, kR), 512, 0, st>>>(packed, pitch, m, mpad, lutr, ctl, b0, cnt, res,
