@@ -419,7 +419,10 @@ __global__ __launch_bounds__(512, 1) void k_syrk_i8r(const uint8_t* __restrict__
         }
 }
 
-// Ring form (round 5): a ring of 4 LDS slots of 64 SNPs (4 x 36 KiB = 144 KiB), stage s+2's
+#ifdef SNPMI_UBENCH
+// Ring form (round 5, ubench variants 80-82; LOST: 777-783 ms vs 721 ms for k_syrk_i8r at 50k x
+// 62.5k, profiles/r05e/ubench_crt_ring.jsonl -- the barrier every 64 SNPs costs more than the
+// hidden post-barrier fragment reads save; s_setprio on waves 4-7 changes nothing): a ring of 4 LDS slots of 64 SNPs (4 x 36 KiB = 144 KiB), stage s+2's
 // residue rows expanded and stored while stage s is multiplied, one barrier per 64-SNP stage.
 // Because a slot is complete one full stage before it is read, each wave reads the NEXT stage's
 // first fragments before the barrier (PF): the post-barrier fragment-read latency that the
@@ -557,7 +560,6 @@ __global__ __launch_bounds__(512, 1) void k_syrk_i8q(const uint8_t* __restrict__
         }
 }
 
-#ifdef SNPMI_UBENCH
 // ubench (variant 77): 4 waves (2 x 2), one per SIMD, 128 x 128 per wave = 4 x 4
 // v_mfma_i32_32x32x32_i8 tiles (256 accumulator registers, AGPR-backed): 8 fragment reads per 16
 // MFMAs instead of k_syrk_i8r's 6 per 8 -- a third less LDS read traffic for the same residue
