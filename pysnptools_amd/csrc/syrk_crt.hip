@@ -200,7 +200,12 @@ __device__ __forceinline__ v2i lds_tr8(const uint8_t* p) {
 // per wave-instruction on the LDS transfer path) instead of one ds_write_b128 (13)
 // LD2 1 (ubench variant 79): two loader register sets, so each stage's code/LUT loads are issued
 // two stages before their expansion (a whole stage more latency to hide; +16 VGPRs)
-template <int SKT, int ABL = 0, int LDM = 0, int ST = 0, int LD2 = 0>
+// STAG (round 5, ubench variants 83/84): the two waves of each SIMD (waves w and w + 4) take
+// complementary roles within a stage -- the "early" half expands and stores all of stage s+1's
+// residue rows during k-steps 0-1 (and issues stage s+2's code loads right after), then runs
+// k-steps 2-3 as pure MFMA; the other half runs k-steps 0-1 as pure MFMA and stores during 2-3.
+// 1: waves 4-7 early; 2: waves 0-3 early (MI355X_MICROARCH.md "Two waves per SIMD" item 9).
+template <int SKT, int ABL = 0, int LDM = 0, int ST = 0, int LD2 = 0, int STAG = 0>
 __global__ __launch_bounds__(512, 1) void k_syrk_i8r(const uint8_t* __restrict__ P, uint64_t pitch, uint64_t kdim,
                                                      uint64_t mpad, const uint32_t* __restrict__ lutr,
                                                      const int* __restrict__ ctl, uint64_t b0, uint64_t nblk,
@@ -362,7 +367,41 @@ __global__ __launch_bounds__(512, 1) void k_syrk_i8r(const uint8_t* __restrict__
         load(nst > 1 ? 1 : 0);
     }
     __syncthreads();
-    for (uint64_t s = 0; s < nst; s++) {
+    const bool early = STAG == 1 ? wave >= 4 : wave < 4;  // wave-uniform
+    for (uint64_t s = 0; s < nst && STAG != 0; s++) {
+        const uint8_t* cur = lds + (s & 1) * STG;
+        uint8_t* nxt = lds + ((s + 1) & 1) * STG;
+        v4i a[2][4], b[2][2];
+        frags(cur, 0, a[0], b[0]);
+        constexpr int H = KS / 2, RH = RPT / H;  // k-steps per half, rows stored per k-step
+        if (early) {
+#pragma unroll
+            for (int ks = 0; ks < KS; ks++) {
+                if (ks + 1 < KS) frags(cur, ks + 1, a[(ks + 1) & 1], b[(ks + 1) & 1]);
+#pragma unroll
+                for (int x = 0; x < 4; x++)
+#pragma unroll
+                    for (int y = 0; y < 2; y++)
+                        acc[x][y] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[ks & 1][x], b[ks & 1][y], acc[x][y], 0, 0, 0);
+                if (ks < H) store(nxt, ks * RH, (ks + 1) * RH);
+                if (ks == H - 1) load(s + 2 < nst ? s + 2 : nst - 1);
+            }
+        } else {
+#pragma unroll
+            for (int ks = 0; ks < KS; ks++) {
+                if (ks + 1 < KS) frags(cur, ks + 1, a[(ks + 1) & 1], b[(ks + 1) & 1]);
+#pragma unroll
+                for (int x = 0; x < 4; x++)
+#pragma unroll
+                    for (int y = 0; y < 2; y++)
+                        acc[x][y] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[ks & 1][x], b[ks & 1][y], acc[x][y], 0, 0, 0);
+                if (ks >= H) store(nxt, (ks - H) * RH, (ks - H + 1) * RH);
+            }
+            load(s + 2 < nst ? s + 2 : nst - 1);
+        }
+        __syncthreads();
+    }
+    for (uint64_t s = 0; s < nst && STAG == 0; s++) {
         const uint8_t* cur = lds + (s & 1) * STG;
         uint8_t* nxt = lds + ((s + 1) & 1) * STG;
         v4i a[2][4], b[2][2];
@@ -903,6 +942,12 @@ void launch_syrk_packed_crt(const uint8_t* packed, uint64_t pitch, uint64_t n, u
             k_syrk_i8r<SK, 0, 0, 0, 1><<<dim3((unsigned)cnt, kR), 512, 0, st>>>(packed, pitch, m, mpad, lutr, ctl, b0, cnt, res);
         else if (g_variant_syrk == 74)  // ablation: fragments read once per stage
             k_syrk_i8r<SK, 2><<<dim3((unsigned)cnt, kR), 512, 0, st>>>(packed, pitch, m, mpad, lutr, ctl, b0, cnt, res);
+        else if (g_variant_syrk == 83)  // complementary halves: waves 4-7 store early
+            k_syrk_i8r<SK, 0, 0, 0, 0, 1><<<dim3((unsigned)cnt, kR), 512, 0, st>>>(packed, pitch, m, mpad, lutr, ctl, b0,
+                                                                                cnt, res, part_tab);
+        else if (g_variant_syrk == 84)  // complementary halves: waves 0-3 store early
+            k_syrk_i8r<SK, 0, 0, 0, 0, 2><<<dim3((unsigned)cnt, kR), 512, 0, st>>>(packed, pitch, m, mpad, lutr, ctl, b0,
+                                                                                cnt, res, part_tab);
         else if (g_variant_syrk == 80)  // 4-slot ring of 64-SNP stages, next stage's fragments read before the barrier
             k_syrk_i8q<1, 0><<<dim3((unsigned)cnt, kR), 512, 0, st>>>(packed, pitch, m, mpad, lutr, ctl, b0, cnt, res,
                                                                      part_tab);
