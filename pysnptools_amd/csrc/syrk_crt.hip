@@ -599,6 +599,136 @@ __global__ __launch_bounds__(512, 1) void k_syrk_i8q(const uint8_t* __restrict__
         }
 }
 
+// ubench (variant 85): k_syrk_i8r on v_mfma_i32_16x16x64_i8 -- the same MACs per cycle, the same
+// LDS image and fragment bytes per MAC, but the chip may hold a higher clock on the 16x16 shape
+// under load (MI355X_MICROARCH.md, DVFS give-back item 7).  Wave tile 128 x 64 = 8 x 4 tiles of
+// 16 x 16 (128 accumulator registers); per 64-deep k-step 8 A and 4 B fragments of 16 B (lane l:
+// iid column l & 15 of its 16-group, k rows 16 (l >> 4) .. +15: two ds_read_b64_tr_b8 of 8 rows),
+// 32 MFMAs; B double-buffered across k-steps, each A fragment reloaded right after its last use.
+__global__ __launch_bounds__(512, 1) void k_syrk_i8s(const uint8_t* __restrict__ P, uint64_t pitch, uint64_t kdim,
+                                                     uint64_t mpad, const uint32_t* __restrict__ lutr,
+                                                     const int* __restrict__ ctl, uint64_t b0, uint64_t nblk,
+                                                     uint8_t* __restrict__ res,
+                                                     const uint32_t* __restrict__ part_tab = nullptr) {
+    constexpr int SKT = SK, KS = SKT / 64, RPT = SKT / 16, PNL = SKT * RS, STG = 2 * PNL;
+    __shared__ __attribute__((aligned(16))) uint8_t lds[2 * STG];
+    if (ctl[1]) return;
+    const int r = blockIdx.y;
+    if (r >= ctl[2]) return;
+    const uint32_t* lr = lutr + (uint64_t)r * mpad;
+    uint32_t bi, bj;
+    if (part_tab) {
+        const uint32_t c = part_tab[b0 + blockIdx.x];
+        bi = c & 0xffffu;
+        bj = c >> 16;
+    } else {
+        tile_coords(b0 + blockIdx.x, bi, bj);
+    }
+    const uint64_t i0 = (uint64_t)bi * BW, j0 = (uint64_t)bj * BW;
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const int wm = wave >> 2, wn = wave & 3;
+    const int lp = __builtin_amdgcn_readfirstlane(t >> 8), kq = (t >> 4) & 15, d = t & 15;
+    const uint8_t* pbase = P + (lp ? j0 : i0) / 4;
+    const uint32_t pit = (uint32_t)pitch;
+    const uint32_t* lq = lr + RPT * kq;
+    const int g = lane >> 4, jj = (lane & 15) >> 1, pp = lane & 1;
+    const int rd = (16 * g + jj) * RS + 8 * pp;
+
+    v4i acc[8][4];
+#pragma unroll
+    for (int x = 0; x < 8; x++)
+#pragma unroll
+        for (int y = 0; y < 4; y++) acc[x][y] = (v4i){0, 0, 0, 0};
+    const uint64_t nst = (kdim + SKT - 1) / SKT;
+    uint32_t cw[RPT];
+    uint4 cl[RPT / 4];
+    auto load = [&](uint64_t st) {
+        const uint8_t* sb = pbase + st * SKT * pitch;
+        const uint32_t lim = (uint32_t)(kdim - 1 - st * SKT);
+#pragma unroll
+        for (int h = 0; h < RPT; h++) {
+            const uint32_t row = min((uint32_t)(RPT * kq + h), lim);
+            cw[h] = *reinterpret_cast<const uint32_t*>(sb + (row * pit + 4 * d));
+        }
+#pragma unroll
+        for (int u = 0; u < RPT / 4; u++) cl[u] = *reinterpret_cast<const uint4*>(lq + SKT * st + 4 * u);
+    };
+    auto store = [&](uint8_t* S, int h0, int h1) {
+#pragma unroll
+        for (int h = h0; h < h1; h++) {
+            const uint4 c4 = cl[h >> 2];
+            const uint32_t L = (h & 3) == 0 ? c4.x : (h & 3) == 1 ? c4.y : (h & 3) == 2 ? c4.z : c4.w;
+            uint4 o;
+            o.x = __builtin_amdgcn_perm(L, L, cw[h] & 0x03030303u);
+            o.y = __builtin_amdgcn_perm(L, L, (cw[h] >> 2) & 0x03030303u);
+            o.z = __builtin_amdgcn_perm(L, L, (cw[h] >> 4) & 0x03030303u);
+            o.w = __builtin_amdgcn_perm(L, L, (cw[h] >> 6) & 0x03030303u);
+            *reinterpret_cast<uint4*>(S + lp * PNL + (RPT * kq + h) * RS + 16 * d) = o;
+        }
+    };
+    auto frag = [&](const uint8_t* S, int panel, int ks, int col) -> v4i {
+        const uint8_t* b = S + panel * PNL + 64 * ks * RS + rd + col;
+        const v2i x = lds_tr8(b), y = lds_tr8(b + 8 * RS);
+        return (v4i){x.x, x.y, y.x, y.y};
+    };
+    load(0);
+    store(lds, 0, RPT);
+    load(nst > 1 ? 1 : 0);
+    __syncthreads();
+    v4i a[8], bb[2][4];
+#pragma unroll
+    for (int x = 0; x < 8; x++) a[x] = frag(lds, 0, 0, wm * 128 + 16 * x);
+#pragma unroll
+    for (int y = 0; y < 4; y++) bb[0][y] = frag(lds, 1, 0, wn * 64 + 16 * y);
+    for (uint64_t s = 0; s < nst; s++) {
+        const uint8_t* cur = lds + (s & 1) * STG;
+        uint8_t* nxt = lds + ((s + 1) & 1) * STG;
+#pragma unroll
+        for (int ks = 0; ks < KS; ks++) {
+            const int cb = ks & 1;
+            const bool more = ks + 1 < KS;  // the next k-step's fragments are in this stage
+            if (more) {
+#pragma unroll
+                for (int y = 0; y < 4; y++) bb[cb ^ 1][y] = frag(cur, 1, ks + 1, wn * 64 + 16 * y);
+            }
+#pragma unroll
+            for (int x = 0; x < 8; x++) {
+#pragma unroll
+                for (int y = 0; y < 4; y++)
+                    acc[x][y] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[x], bb[cb][y], acc[x][y], 0, 0, 0);
+                if (more) a[x] = frag(cur, 0, ks + 1, wm * 128 + 16 * x);
+                if (x & 1) store(nxt, ks * (RPT / KS) + (x >> 1) * (RPT / KS / 4),
+                                 ks * (RPT / KS) + ((x >> 1) + 1) * (RPT / KS / 4));
+            }
+        }
+        load(s + 2 < nst ? s + 2 : nst - 1);
+        __syncthreads();
+        // stage s+1's first fragments (KS is even: the last k-step used bb[1], refill bb[0])
+#pragma unroll
+        for (int x = 0; x < 8; x++) a[x] = frag(nxt, 0, 0, wm * 128 + 16 * x);
+#pragma unroll
+        for (int y = 0; y < 4; y++) bb[0][y] = frag(nxt, 1, 0, wn * 64 + 16 * y);
+    }
+    const int p = kMod[r];
+    const double invp = 1.0 / (double)p;
+    uint8_t* O = res + ((uint64_t)r * nblk + blockIdx.x) * (BW * BW);
+    const int cq = lane & 15, rq = 4 * (lane >> 4);
+#pragma unroll
+    for (int x = 0; x < 8; x++)
+#pragma unroll
+        for (int y = 0; y < 4; y++) {
+            uint8_t* bp = O + (wm * 128 + 16 * x) * BW + wn * 64 + 16 * y + pi16(cq);
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const int v = acc[x][y][q];
+                int rr = v - p * (int)floor((double)v * invp);
+                rr += rr < 0 ? p : 0;
+                rr -= rr >= p ? p : 0;
+                bp[pi16(rq + q) * BW] = (uint8_t)rr;
+            }
+        }
+}
+
 // ubench (variant 77): 4 waves (2 x 2), one per SIMD, 128 x 128 per wave = 4 x 4
 // v_mfma_i32_32x32x32_i8 tiles (256 accumulator registers, AGPR-backed): 8 fragment reads per 16
 // MFMAs instead of k_syrk_i8r's 6 per 8 -- a third less LDS read traffic for the same residue
@@ -948,6 +1078,8 @@ void launch_syrk_packed_crt(const uint8_t* packed, uint64_t pitch, uint64_t n, u
         else if (g_variant_syrk == 84)  // complementary halves: waves 0-3 store early
             k_syrk_i8r<SK, 0, 0, 0, 0, 2><<<dim3((unsigned)cnt, kR), 512, 0, st>>>(packed, pitch, m, mpad, lutr, ctl, b0,
                                                                                 cnt, res, part_tab);
+        else if (g_variant_syrk == 85)  // v_mfma_i32_16x16x64_i8 shape
+            k_syrk_i8s<<<dim3((unsigned)cnt, kR), 512, 0, st>>>(packed, pitch, m, mpad, lutr, ctl, b0, cnt, res, part_tab);
         else if (g_variant_syrk == 80)  // 4-slot ring of 64-SNP stages, next stage's fragments read before the barrier
             k_syrk_i8q<1, 0><<<dim3((unsigned)cnt, kR), 512, 0, st>>>(packed, pitch, m, mpad, lutr, ctl, b0, cnt, res,
                                                                      part_tab);
