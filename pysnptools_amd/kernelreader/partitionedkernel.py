@@ -65,7 +65,9 @@ def use_partitioned(n, dtype, group):
     N.call("snpmi_device_memory", ctypes.byref(free), ctypes.byref(total))
     tiles = int(N.lib().snpmi_grm_tile_bytes(int(n), N.dt_code(np.dtype(dtype))))
     need = tiles + int(n) * int(n) * np.dtype(dtype).itemsize // 8  # + the extraction row blocks
-    return need > 0.8 * free.value
+    # one decision for the whole group (free memory differs between ranks; ranks that decided
+    # differently would run different collectives)
+    return bool(group.max(1.0 if need > 0.8 * free.value else 0.0) > 0.5)
 
 
 class PartitionedKernel(KernelReader):
