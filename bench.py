@@ -109,6 +109,9 @@ def parse(argv=None):
     p.add_argument("--grm5-sid", type=int, default=1_000_000, help="cfg5: SNPs of the whole job (all timed)")
     p.add_argument("--grm5-block", type=int, default=32768, help="cfg5: SNPs per all-gathered block (the first: 1/4)")
     p.add_argument("--grm5-miss", type=float, default=0.218, help="cfg5: missing rate (SnpGen's 21.8%%)")
+    p.add_argument("--grm5-dtype", choices=["f32", "f64"], default="f32",
+                   help="cfg5 K dtype: f32 (fp16x2 MFMA) or f64 (the reference's default; int8 MFMA residues + CRT, "
+                        "125 GB of blocks per part at 500k iids)")
     p.add_argument("--grm5-parity-max-sid", type=int, default=65536,
                    help="cfg5 at N > 1: the oracle check runs only up to this many SNPs (N = 1: always)")
     p.add_argument("--out-ld", type=int, default=0,
@@ -787,6 +790,7 @@ def leg_grm5(N, args, dist):
     from pysnptools_amd.shard import PartitionedGrm
 
     n, m, world, rank = args.grm5_iid, args.grm5_sid, dist.world, dist.rank
+    dt = np.dtype(np.float64 if args.grm5_dtype == "f64" else np.float32)
     P = max(world, GRM5_PLAN_WORLD)
     threads = cpu_threads()
     pitch = N.lib().snpmi_packed_pitch(n)
@@ -794,14 +798,18 @@ def leg_grm5(N, args, dist):
     grp = dist if (world > 1 or dist.rccl) else None  # --force-rccl at N = 1: the real all-gather call, in place
     # warm-up (untimed): one block through a session of the same shape (code objects, scratch)
     g = PartitionedGrm(n, min(m, args.grm5_block), N.STD_UNIT, dist=grp, part=rank, parts=P, block=args.grm5_block,
-                       out="hbm")
+                       out="hbm", dtype=dt)
     try:
         g.run(fill)
     finally:
         g.close()
         del g
-    out = hbm.empty((N.lib().snpmi_grm_part_blocks(n, rank, P), 256, 256), dtype=np.float32, order="C")
-    g = PartitionedGrm(n, m, N.STD_UNIT, dist=grp, part=rank, parts=P, block=args.grm5_block, out=out, timing=True)
+    out = hbm.empty((N.lib().snpmi_grm_part_blocks(n, rank, P), 256, 256), dtype=dt, order="C")
+    sum_r, nlaunch = ctypes.c_uint64(), ctypes.c_uint64()
+    if dt == np.float64:
+        N.call("snpmi_crt_moduli_stats", ctypes.byref(sum_r), ctypes.byref(nlaunch), 1)
+    g = PartitionedGrm(n, m, N.STD_UNIT, dist=grp, part=rank, parts=P, block=args.grm5_block, out=out, timing=True,
+                       dtype=dt)
     try:
         N.call("snpmi_stream_sync")
         dist.barrier()
@@ -811,13 +819,16 @@ def leg_grm5(N, args, dist):
         dist.barrier()
         wall = dist.max(time.perf_counter() - t0)
         res = {"wall": wall, "block_ms": block_ms, "n_local_blocks": g.nloc, "m": m, "ms": g.ms, "P": P,
-               "pitch": pitch, "blocks": len(block_ms), "threads": threads}
+               "pitch": pitch, "blocks": len(block_ms), "threads": threads, "dtype": dt}
+        if dt == np.float64:  # moduli per launch the timed blocks ran with (chosen on the device)
+            N.call("snpmi_crt_moduli_stats", ctypes.byref(sum_r), ctypes.byref(nlaunch), 1)
+            res["crt_moduli"] = sum_r.value / max(nlaunch.value, 1)
         if rank == 0 and not args.skip_cpu and (world == 1 or m <= args.grm5_parity_max_sid):
             picks = grm5_picks(N, n, rank, P, g.nloc)
             got = {}
             for key, (b, r0, c0) in picks.items():
-                blk = np.empty((256, 256), dtype=np.float32)
-                N.call("snpmi_memcpy_d2h", N.ptr(blk), ctypes.c_void_p(out.snpmi_ptr.value + b * 256 * 256 * 4),
+                blk = np.empty((256, 256), dtype=dt)
+                N.call("snpmi_memcpy_d2h", N.ptr(blk), ctypes.c_void_p(out.snpmi_ptr.value + b * blk.nbytes),
                        blk.nbytes)
                 got[key] = (blk, r0, c0)
             res["parity_sample"] = (got, g.stats())
@@ -886,7 +897,7 @@ def grm5_parity(args, picks, gpu_stats, threads):
         body = buf[:cnt] if pitch == bpc else np.ascontiguousarray(buf[:cnt, :bpc])
         body = body.reshape(-1)
         st = O.snp_stats(body, n, cnt)
-        stats_ok &= bool(np.array_equal(st.astype(np.float32), gpu_stats[s0:s0 + cnt]))
+        stats_ok &= bool(np.array_equal(st.astype(gpu_stats.dtype), gpu_stats[s0:s0 + cnt]))
         for key, (rr, cc) in sets.items():
             Zr = O.decode(body, n, cnt, iid_index=rr)
             O.standardize_native(Zr, use_stats=True, stats=st)
@@ -907,11 +918,13 @@ def grm5_parity(args, picks, gpu_stats, threads):
         worst = max(worst, rel)
         out.append({"block": key, "row0": int(r0), "col0": int(c0), "max_abs_err": err,
                     "max_abs_err_over_max_diag": rel})
-    return {"check": "part blocks (first diagonal, first off-diagonal, last) over all %d SNPs x %d iids: GPU f32 "
-                     "(fp16x2 MFMA, %d-SNP blocks accumulated in HBM) vs oracle f64 (stats over every iid, "
-                     "products accumulated per SNP block)" % (m, n, B),
-            "blocks": out, "max_abs_err_over_max_diag": worst, "stats_bit_exact": stats_ok,
-            "oracle_seconds": time.perf_counter() - t0, "pass": worst <= 1e-5 and stats_ok}
+    f64 = gpu_stats.dtype == np.float64
+    tol = 1e-12 if f64 else 1e-5
+    return {"check": "part blocks (first diagonal, first off-diagonal, last) over all %d SNPs x %d iids: GPU %s "
+                     "(%d-SNP blocks accumulated in HBM) vs oracle f64 (stats over every iid, products accumulated "
+                     "per SNP block)" % (m, n, "f64 (int8 MFMA residues + CRT)" if f64 else "f32 (fp16x2 MFMA)", B),
+            "blocks": out, "max_abs_err_over_max_diag": worst, "stats_bit_exact": stats_ok, "tolerance": tol,
+            "oracle_seconds": time.perf_counter() - t0, "pass": worst <= tol and stats_ok}
 
 
 def input_sha256(sample, n):
@@ -1284,12 +1297,24 @@ def main(argv=None):
         syrk_tf = flops_part / busy_s / 1e12
         gather = (" + RCCL all-gather" if dist.rccl else
                   (" + host all-gather (rehearsal group)" if dist.world > 1 else ""))
-        grm5 = {"workload": "cfg5: %d iid x %d SNP, Unit, f32 (fp16x2 MFMA), %.1f%% missing; K as 256x256 blocks in "
+        f64_5 = r3["dtype"] == np.float64
+        if f64_5:  # the CRT path: executed int8 ops against the int8 peak, beside the f64-equivalent rate
+            nloc5 = r3["n_local_blocks"]
+            R5 = r3.get("crt_moduli") or CRT_MODULI
+            ops5 = R5 * 2 * 256 * 256 * nloc5 * m5
+            roof5 = {"bound": "mfma", "achieved": ops5 / busy_s / 1e12, "peak": MFMA_I8_PEAK_TOPS, "unit": "TOP/s",
+                     "frac": ops5 / busy_s / 1e12 / MFMA_I8_PEAK_TOPS, "traffic": None,
+                     "f64_equiv_tflops": syrk_tf, "f64_mfma_peak": MFMA_F64_PEAK_TFLOPS, "moduli_per_block": R5,
+                     "kernel": "k_syrk_i8r in part mode (int8 residues of the quantised LUT, R moduli per block) + "
+                               "k_crt into the part's f64 blocks; time = the blocks' compute-stream spans (stats + CRT "
+                               "SYRK%s)" % (" + all-gather" if gather else "")}
+        grm5 = {"workload": "cfg5: %d iid x %d SNP, Unit, %s, %.1f%% missing; K as 256x256 blocks in "
                             "%d parts (the 8-GPU plan), this process = part %d; all %d blocks (of %d SNPs, the first a quarter) timed: each "
                             "rank's 1/%d share generated on %d host threads into pinned memory, uploaded on the copy "
                             "stream under the previous block's SYRK%s, stats + SYRK into the part's blocks in HBM "
                             "(shard.PartitionedGrm); no reduction"
-                            % (n5, m5, 100 * args.grm5_miss, P, dist.rank, r3["blocks"], args.grm5_block, dist.world,
+                            % (n5, m5, "f64 (int8 MFMA residues + CRT)" if f64_5 else "f32 (fp16x2 MFMA)",
+                               100 * args.grm5_miss, P, dist.rank, r3["blocks"], args.grm5_block, dist.world,
                                r3["threads"], gather),
                 "seconds": r3["wall"], "blocks": r3["blocks"], "gpu_busy_seconds": busy_s,
                 "exposed_wait_seconds": max(0.0, r3["wall"] - busy_s),
@@ -1299,12 +1324,16 @@ def main(argv=None):
                 "job_note": "the P parts run concurrently on P GPUs at N = P, so `seconds` is the 8-GPU job time at "
                             "N = 8; at N < P it is one part's share of that job, measured whole (`part_*` rates; "
                             "`single_gpu_job_*_projected` = all P parts one after another on one GPU)",
-                "blocks_on_rank0": r3["n_local_blocks"], "K_bytes_per_rank": r3["n_local_blocks"] * 256 * 256 * 4,
+                "blocks_on_rank0": r3["n_local_blocks"],
+                "K_bytes_per_rank": r3["n_local_blocks"] * 256 * 256 * r3["dtype"].itemsize,
                 "roofline": {"bound": "mfma", "achieved": syrk_tf, "peak": SPLIT_PEAK_TFLOPS, "unit": "TFLOP/s",
                              "frac": syrk_tf / SPLIT_PEAK_TFLOPS, "traffic": None,
                              "kernel": "f32w::k_syrk_h2<true,4> (fp16x2 split, 3 fp16 MFMA products, f32 "
                                        "accumulate), this part's blocks only; time = the blocks' compute-stream "
                                        "spans (stats + SYRK%s)" % (" + all-gather" if gather else "")}}
+        if f64_5:
+            grm5["roofline"] = roof5
+            grm5["f64_equiv_tflops"] = grm5.pop("syrk_tflops")
         if dist.world >= P:  # every part runs: the job measured whole
             grm5.update({"gflops_per_gpu": flops_part / r3["wall"] / 1e9, "snps_per_s": m5 / r3["wall"]})
         else:
