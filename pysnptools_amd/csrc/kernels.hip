@@ -3052,11 +3052,12 @@ void launch_diag_begin(const float* K, uint64_t n, const int32_t* dslot, int acc
     SNPMI_LAUNCH_CHECK();
 }
 
-// SNP slices of k_diag_sq: enough (word, slice) threads to fill 256 CUs several times over,
-// slices of >= 64 SNPs
+// SNP slices of k_diag_sq: ~1M (word, slice) threads, slices of >= 64 SNPs.  Each thread's loop has
+// one dependent code load per SNP, so the kernel is latency-bound and needs the waves: round 4's
+// ~262k threads (9 slices at 500k iids) ran a 32768-SNP block in 6.1 ms (0.7 TB/s of codes)
 static uint64_t diag_slices(uint64_t n, uint64_t m) {
     const uint64_t nw = (n + 15) / 16;
-    return std::max<uint64_t>(1, std::min<uint64_t>(ceil_div(std::max<uint64_t>(m, 1), 64), ceil_div(256 * 1024, nw)));
+    return std::max<uint64_t>(1, std::min<uint64_t>(ceil_div(std::max<uint64_t>(m, 1), 64), ceil_div(1024 * 1024, nw)));
 }
 // diag (n f64, from round_up(n, 16)) followed by the per-slice partial rows
 uint64_t diag_scratch_bytes(uint64_t n, uint64_t m) {

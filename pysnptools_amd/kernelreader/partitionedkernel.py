@@ -104,10 +104,15 @@ class PartitionedKernel(KernelReader):
         assert tuple(blocks.shape) == (nloc, 256, 256), "blocks must be [%d, 256, 256]" % nloc
         self.dtype = np.dtype(blocks.dtype)
         assert self.dtype in (np.float32, np.float64), "blocks must be float32 or float64"
-        if getattr(blocks, "snpmi_ptr", None) is None:  # host blocks: one upload
+        if getattr(blocks, "snpmi_ptr", None) is None:  # host blocks (e.g. a memory map): uploaded in 1 GiB pieces
+            import ctypes
+
             dev = hbm.empty((nloc, 256, 256), dtype=self.dtype, order="C")
-            if nloc:
-                N.call("snpmi_memcpy_h2d", dev.snpmi_ptr, N.ptr(np.ascontiguousarray(blocks)), dev.nbytes)
+            bb = 256 * 256 * self.dtype.itemsize
+            per = max(1, (1 << 30) // bb)
+            for b0 in range(0, nloc, per):
+                piece = np.ascontiguousarray(blocks[b0:b0 + per])
+                N.call("snpmi_memcpy_h2d", ctypes.c_void_p(dev.snpmi_ptr.value + b0 * bb), N.ptr(piece), piece.nbytes)
             blocks = dev
         self.blocks = blocks
         self.scale = float(scale)
