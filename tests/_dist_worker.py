@@ -56,5 +56,48 @@ def main(out_dir, block):
     dist.destroy_process_group()
 
 
+def partitioned(out_dir):
+    """cfg5's read of K[iid0, iid1] (kernelreader.PartitionedKernel) over gloo: each rank holds only
+    the 256x256 blocks of its part (the library's layout, shard.part_coords), fills the entries of
+    the requested sub-matrix that its blocks hold (0 elsewhere; NumPy standing in for
+    k_part_extract) and the ranks' outputs are summed -- every rank must get the sub-matrix."""
+    import torch.distributed as dist
+
+    from pysnptools_amd.shard import part_coords
+
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    d = GlooDist(rank, world)
+    n = 2300
+    rng = np.random.default_rng(11)
+    Z = rng.standard_normal((n, 40))
+    K = Z.dot(Z.T)  # every rank builds the same K; each keeps only its blocks
+    coords = part_coords(n, rank, world)
+    slot = {(int(r0) // 256, int(c0) // 256): b for b, (r0, c0) in enumerate(coords)}
+    nb = (n + 255) // 256
+    blocks = np.zeros((len(coords), 256, 256))
+    Kp = np.zeros((nb * 256, nb * 256))
+    Kp[:n, :n] = K
+    for (I, J), b in slot.items():
+        blocks[b] = Kp[256 * I:256 * I + 256, 256 * J:256 * J + 256]
+    rows, cols = rng.permutation(n)[:300], np.arange(n - 1, 0, -7)
+    out = np.zeros((len(rows), len(cols)))
+    for a, i in enumerate(rows):
+        for c, j in enumerate(cols):
+            lo, hi = min(i, j), max(i, j)
+            b = slot.get((lo // 256, hi // 256))
+            if b is not None:
+                out[a, c] = blocks[b, lo % 256, hi % 256]
+    out = d.sum_host(out)
+    np.save(os.path.join(out_dir, "P%d.npy" % rank), out)
+    np.save(os.path.join(out_dir, "Pref.npy"), K[np.ix_(rows, cols)])
+    np.save(os.path.join(out_dir, "Pn%d.npy" % rank), np.array([len(coords)]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
 if __name__ == "__main__":
-    main(sys.argv[1], int(sys.argv[2]))
+    if sys.argv[2] == "partitioned":
+        partitioned(sys.argv[1])
+    else:
+        main(sys.argv[1], int(sys.argv[2]))

@@ -59,3 +59,23 @@ def test_rank_span_blocks_cover_once_balanced(world):
     assert all(0 < c <= bs for sp in spans for _, c in sp) and cover[-1] == m - 1
     per = [sum(c for _, c in sp) for sp in spans]
     assert max(per) - min(per) <= 1
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_partitioned_k_read_over_gloo(tmp_path, world):
+    """The partitioned K's sub-matrix read (PartitionedKernel: each rank's blocks in the library's
+    layout, non-owned entries 0, summed over the group) rehearsed over gloo: every rank gets
+    K[rows, cols] exactly, and the parts cover the 45 blocks of a 2300-iid K once."""
+    port = _free_port()
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                   OMP_NUM_THREADS="1")
+        procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "_dist_worker.py"), str(tmp_path),
+                                       "partitioned"], env=env))
+    for p in procs:
+        assert p.wait(timeout=300) == 0
+    ref = np.load(tmp_path / "Pref.npy")
+    assert sum(int(np.load(tmp_path / ("Pn%d.npy" % r))[0]) for r in range(world)) == 45
+    for r in range(world):
+        np.testing.assert_array_equal(np.load(tmp_path / ("P%d.npy" % r)), ref)
