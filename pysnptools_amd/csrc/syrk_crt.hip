@@ -599,6 +599,120 @@ __global__ __launch_bounds__(512, 1) void k_syrk_i8q(const uint8_t* __restrict__
         }
 }
 
+// ubench (variant 86): k_syrk_i8r with 16 waves (4 per SIMD), 64 x 64 per wave (2 x 2 tiles, 64
+// accumulator registers): more waves to hide the LDS-read and barrier latencies, at a third more
+// fragment bytes per MFMA (1 KiB instead of 0.75).  Same LDS image, stages, barrier and loader
+// (4 rows per thread per stage).
+__global__ __launch_bounds__(1024, 1) void k_syrk_i8h(const uint8_t* __restrict__ P, uint64_t pitch, uint64_t kdim,
+                                                      uint64_t mpad, const uint32_t* __restrict__ lutr,
+                                                      const int* __restrict__ ctl, uint64_t b0, uint64_t nblk,
+                                                      uint8_t* __restrict__ res,
+                                                      const uint32_t* __restrict__ part_tab = nullptr) {
+    constexpr int SKT = SK, KS = SKT / 32, RPT = SKT / 32, PNL = SKT * RS, STG = 2 * PNL;
+    __shared__ __attribute__((aligned(16))) uint8_t lds[2 * STG];
+    if (ctl[1]) return;
+    const int r = blockIdx.y;
+    if (r >= ctl[2]) return;
+    const uint32_t* lr = lutr + (uint64_t)r * mpad;
+    uint32_t bi, bj;
+    if (part_tab) {
+        const uint32_t c = part_tab[b0 + blockIdx.x];
+        bi = c & 0xffffu;
+        bj = c >> 16;
+    } else {
+        tile_coords(b0 + blockIdx.x, bi, bj);
+    }
+    const uint64_t i0 = (uint64_t)bi * BW, j0 = (uint64_t)bj * BW;
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const int wm = wave >> 2, wn = wave & 3;
+    const int lp = __builtin_amdgcn_readfirstlane(t >> 9), kq = (t >> 4) & 31, d = t & 15;
+    const uint8_t* pbase = P + (lp ? j0 : i0) / 4;
+    const uint32_t pit = (uint32_t)pitch;
+    const uint32_t* lq = lr + RPT * kq;
+    const int g = lane >> 4, jj = (lane & 15) >> 1, pp = lane & 1;
+    const int rd = (16 * (g >> 1) + jj) * RS + 16 * (g & 1) + 8 * pp;
+
+    v16i acc[2][2];
+#pragma unroll
+    for (int x = 0; x < 2; x++)
+#pragma unroll
+        for (int y = 0; y < 2; y++) acc[x][y] = (v16i){};
+    const uint64_t nst = (kdim + SKT - 1) / SKT;
+    uint32_t cw[RPT];
+    uint4 cl;
+    auto load = [&](uint64_t st) {
+        const uint8_t* sb = pbase + st * SKT * pitch;
+        const uint32_t lim = (uint32_t)(kdim - 1 - st * SKT);
+#pragma unroll
+        for (int h = 0; h < RPT; h++) {
+            const uint32_t row = min((uint32_t)(RPT * kq + h), lim);
+            cw[h] = *reinterpret_cast<const uint32_t*>(sb + (row * pit + 4 * d));
+        }
+        cl = *reinterpret_cast<const uint4*>(lq + SKT * st);
+    };
+    auto store = [&](uint8_t* S, int h) {
+        const uint32_t L = h == 0 ? cl.x : h == 1 ? cl.y : h == 2 ? cl.z : cl.w;
+        uint4 o;
+        o.x = __builtin_amdgcn_perm(L, L, cw[h] & 0x03030303u);
+        o.y = __builtin_amdgcn_perm(L, L, (cw[h] >> 2) & 0x03030303u);
+        o.z = __builtin_amdgcn_perm(L, L, (cw[h] >> 4) & 0x03030303u);
+        o.w = __builtin_amdgcn_perm(L, L, (cw[h] >> 6) & 0x03030303u);
+        *reinterpret_cast<uint4*>(S + lp * PNL + (RPT * kq + h) * RS + 16 * d) = o;
+    };
+    auto frag = [&](const uint8_t* S, int panel, int ks, int col) -> v4i {
+        const uint8_t* b = S + panel * PNL + 32 * ks * RS + rd + col;
+        const v2i x = lds_tr8(b), y = lds_tr8(b + 8 * RS);
+        return (v4i){x.x, x.y, y.x, y.y};
+    };
+    auto frags = [&](const uint8_t* S, int ks, v4i (&A)[2], v4i (&B)[2]) {
+#pragma unroll
+        for (int x = 0; x < 2; x++) A[x] = frag(S, 0, ks, wm * 64 + 32 * x);
+#pragma unroll
+        for (int y = 0; y < 2; y++) B[y] = frag(S, 1, ks, wn * 64 + 32 * y);
+    };
+    load(0);
+#pragma unroll
+    for (int h = 0; h < RPT; h++) store(lds, h);
+    load(nst > 1 ? 1 : 0);
+    __syncthreads();
+    for (uint64_t s = 0; s < nst; s++) {
+        const uint8_t* cur = lds + (s & 1) * STG;
+        uint8_t* nxt = lds + ((s + 1) & 1) * STG;
+        v4i a[2][2], b[2][2];
+        frags(cur, 0, a[0], b[0]);
+#pragma unroll
+        for (int ks = 0; ks < KS; ks++) {
+            if (ks + 1 < KS) frags(cur, ks + 1, a[(ks + 1) & 1], b[(ks + 1) & 1]);
+#pragma unroll
+            for (int x = 0; x < 2; x++)
+#pragma unroll
+                for (int y = 0; y < 2; y++)
+                    acc[x][y] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[ks & 1][x], b[ks & 1][y], acc[x][y], 0, 0, 0);
+            store(nxt, ks);  // KS == RPT: one row per k-step
+        }
+        load(s + 2 < nst ? s + 2 : nst - 1);
+        __syncthreads();
+    }
+    const int p = kMod[r];
+    const double invp = 1.0 / (double)p;
+    uint8_t* O = res + ((uint64_t)r * nblk + blockIdx.x) * (BW * BW);
+    const int hh = lane >> 5, colp = 16 * ((lane >> 4) & 1) + pi16(lane & 15);
+#pragma unroll
+    for (int x = 0; x < 2; x++)
+#pragma unroll
+        for (int y = 0; y < 2; y++) {
+            uint8_t* bp = O + (wm * 64 + 32 * x + hh) * BW + wn * 64 + 32 * y + colp;
+#pragma unroll
+            for (int q = 0; q < 16; q++) {
+                const int v = acc[x][y][q];
+                int rr = v - p * (int)floor((double)v * invp);
+                rr += rr < 0 ? p : 0;
+                rr -= rr >= p ? p : 0;
+                bp[(16 * (q >> 3) + 4 * (q & 3) + 2 * ((q >> 2) & 1)) * BW] = (uint8_t)rr;
+            }
+        }
+}
+
 // ubench (variant 85; LOST: 761 vs 720 ms at 50k x 62.5k, K bit-identical, profiles/r05i): k_syrk_i8r on v_mfma_i32_16x16x64_i8 -- the same MACs per cycle, the same
 // LDS image and fragment bytes per MAC, but the chip may hold a higher clock on the 16x16 shape
 // under load (MI355X_MICROARCH.md, DVFS give-back item 7).  Wave tile 128 x 64 = 8 x 4 tiles of
@@ -1078,6 +1192,8 @@ void launch_syrk_packed_crt(const uint8_t* packed, uint64_t pitch, uint64_t n, u
         else if (g_variant_syrk == 84)  // complementary halves: waves 0-3 store early
             k_syrk_i8r<SK, 0, 0, 0, 0, 2><<<dim3((unsigned)cnt, kR), 512, 0, st>>>(packed, pitch, m, mpad, lutr, ctl, b0,
                                                                                 cnt, res, part_tab);
+        else if (g_variant_syrk == 86)  // 16 waves, 64 x 64 per wave
+            k_syrk_i8h<<<dim3((unsigned)cnt, kR), 1024, 0, st>>>(packed, pitch, m, mpad, lutr, ctl, b0, cnt, res, part_tab);
         else if (g_variant_syrk == 85)  // v_mfma_i32_16x16x64_i8 shape
             k_syrk_i8s<<<dim3((unsigned)cnt, kR), 512, 0, st>>>(packed, pitch, m, mpad, lutr, ctl, b0, cnt, res, part_tab);
         else if (g_variant_syrk == 80)  // 4-slot ring of 64-SNP stages, next stage's fragments read before the barrier
