@@ -599,7 +599,7 @@ __global__ __launch_bounds__(512, 1) void k_syrk_i8q(const uint8_t* __restrict__
         }
 }
 
-// ubench (variant 86): k_syrk_i8r with 16 waves (4 per SIMD), 64 x 64 per wave (2 x 2 tiles, 64
+// ubench (variant 86; LOST: 761 vs 726 ms at 50k x 62.5k, K bit-identical, profiles/r05k): k_syrk_i8r with 16 waves (4 per SIMD), 64 x 64 per wave (2 x 2 tiles, 64
 // accumulator registers): more waves to hide the LDS-read and barrier latencies, at a third more
 // fragment bytes per MFMA (1 KiB instead of 0.75).  Same LDS image, stages, barrier and loader
 // (4 rows per thread per stage).
