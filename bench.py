@@ -128,6 +128,8 @@ def parse(argv=None):
     p.add_argument("--e2e-passes", type=int, default=4)
     p.add_argument("--skip-cpu", action="store_true")
     p.add_argument("--decode-variant", type=int, default=0, help="snpmi_set_kernel_variant('decode', v) (A/B runs)")
+    p.add_argument("--hook", action="append", default=[], metavar="NAME=V",
+                   help="snpmi_set_kernel_variant(NAME, V) before the legs (A/B runs; repeatable)")
     p.add_argument("--cpu-seconds", type=float, default=6.0)
     p.add_argument("--seed", type=int, default=5)
     p.add_argument("--force-rccl", action="store_true", help="build the RCCL communicator even at world size 1")
@@ -335,6 +337,9 @@ def leg_standardize(N, args, dist, n=None, n_sid=None, std=None, a=0.0, b=0.0, m
         out = Dev(N, B * ld * 4)
     ev = Events(N, 2 + 2 * max(nblk, args.side_reps))
     N.call("snpmi_set_kernel_variant", b"decode", args.decode_variant)
+    for h in args.hook:
+        name, v = h.split("=")
+        N.call("snpmi_set_kernel_variant", name.encode(), int(v))
 
     def run_block(src, cnt, timed, k, dst=None, dld=None):
         N.call("snpmi_dev_snp_stats", src, pitch, n, cnt, 0, std, a, b, 0, N.DT_F32, stats.p, lut.p)

@@ -130,6 +130,7 @@ _SIGS = {
     "snpmi_dev_grm_extract": [_vp, _u64, _i32, _vp, _u64, _vp, _u64, _i32, _f64, _vp],
     "snpmi_dev_grm_trace": [_vp, _u64, _i32, _dp],
     "snpmi_crt_moduli_stats": [_u64p, _u64p, _i32],
+    "snpmi_seg_flush_stats": [_u64p, _u64p, _i32],
     "snpmi_rccl_unique_id": [_vp, _u64],
     "snpmi_rccl_init": [_i32, _i32, _vp, _u64],
     "snpmi_rccl_allreduce_sum": [_vp, _u64, _i32],
@@ -167,6 +168,8 @@ def lib():
                        "There is no CPU fallback." % (LIB_PATH, e))
         raise ImportError(_load_error)
     for name, args in _SIGS.items():
+        if "SNPMI_LIB" in os.environ and not hasattr(L, name):
+            continue  # an A/B build of an earlier revision (SNPMI_LIB): calls to what it lacks raise
         fn = getattr(L, name)
         fn.argtypes = args
         fn.restype = _RESTYPES.get(name, ctypes.c_int)
