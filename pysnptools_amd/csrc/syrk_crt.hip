@@ -178,8 +178,8 @@ __device__ __forceinline__ v2i lds_tr8(const uint8_t* p) {
 }
 
 // ---------------------------------------------------------------- residue SYRK
-// grid (blocks of this chunk, R): block (bi, bj) = upper-triangle 256-block b0 + blockIdx.x,
-// modulus kMod[blockIdx.y].  8 waves (2 x 4), each 128 x 64 = 4 x 2 v_mfma_i32_32x32x32_i8 tiles.
+// grid: kR workgroups per block of this chunk (MAP below): block (bi, bj) = upper-triangle 256-block
+// b0 + bx (or slot b0 + bx of a cfg5 part's layout), modulus kMod[r].  8 waves (2 x 4), each 128 x 64 = 4 x 2 v_mfma_i32_32x32x32_i8 tiles.
 // LDS: per stage and panel SKT SNP rows x 256 iids of int8 residues ([k][iid], RS-byte rows, the
 // 16 iids of a group in pi16 order as the loader's byte permutes leave them), double-buffered.
 // Loader: thread (panel lp, 16-iid group d, row block kq) expands SKT/16 consecutive SNP rows
@@ -190,7 +190,7 @@ __device__ __forceinline__ v2i lds_tr8(const uint8_t* p) {
 // Per 32-SNP k-step: the next k-step's fragments are read under this one's 8 MFMAs, and a
 // share of the next stage's rows is expanded and stored; one barrier per stage.
 // Epilogue: residue of each int32 sum, one byte per element, written as a dense 256 x 256 block
-// (true iid order) at res + (blockIdx.y * nblk + blockIdx.x) * 65536.
+// (true iid order) at res + (r * nblk + bx) * 65536.
 // ABL (ubench ablations, wrong results): 1 = no loader after the prologue, 2 = fragments read once
 // per stage (k-step 0) and reused by all four k-steps.
 // LDM 1: row-per-wave loader -- wave w expands rows 32(w&3)..+31 of panel w>>2, lane L the 4 iids
@@ -205,7 +205,7 @@ __device__ __forceinline__ v2i lds_tr8(const uint8_t* p) {
 // residue rows during k-steps 0-1 (and issues stage s+2's code loads right after), then runs
 // k-steps 2-3 as pure MFMA; the other half runs k-steps 0-1 as pure MFMA and stores during 2-3.
 // 1: waves 4-7 early; 2: waves 0-3 early (MI355X_MICROARCH.md "Two waves per SIMD" item 9).
-template <int SKT, int ABL = 0, int LDM = 0, int ST = 0, int LD2 = 0, int STAG = 0>
+template <int SKT, int ABL = 0, int LDM = 0, int ST = 0, int LD2 = 0, int STAG = 0, int MAP = 0>
 __global__ __launch_bounds__(512, 1) void k_syrk_i8r(const uint8_t* __restrict__ P, uint64_t pitch, uint64_t kdim,
                                                      uint64_t mpad, const uint32_t* __restrict__ lutr,
                                                      const int* __restrict__ ctl, uint64_t b0, uint64_t nblk,
@@ -214,16 +214,29 @@ __global__ __launch_bounds__(512, 1) void k_syrk_i8r(const uint8_t* __restrict__
     constexpr int KS = SKT / 32, RPT = SKT / 16, PNL = SKT * RS, STG = 2 * PNL;
     __shared__ __attribute__((aligned(16))) uint8_t lds[2 * STG];
     if (ctl[1]) return;  // non-finite LUT: the f64 MFMA kernel runs instead
-    const int r = blockIdx.y;
-    if (r >= ctl[2]) return;  // K_int fits the first ctl[2] moduli
+    // MAP 0: grid (blocks, moduli), block-fastest.  MAP 1 (1-D grid of round_up(nblk, 8) * kR):
+    // workgroup w runs on XCD w % 8; its kR consecutive slots there are the kR moduli of block
+    // 8 (w / 8 / kR) + w % 8, so the workgroups an XCD holds at once share their code panels in
+    // that XCD's L2
+    uint32_t r, bx;
+    if constexpr (MAP == 1) {
+        const uint32_t w = blockIdx.x, q = w >> 3, u = q / kR;
+        r = q - u * kR;
+        bx = 8 * u + (w & 7);
+        if (bx >= nblk) return;
+    } else {
+        r = blockIdx.y;
+        bx = blockIdx.x;
+    }
+    if ((int)r >= ctl[2]) return;  // K_int fits the first ctl[2] moduli
     const uint32_t* lr = lutr + (uint64_t)r * mpad;
     uint32_t bi, bj;
-    if (part_tab) {  // cfg5: slot b0 + blockIdx.x of the part's layout (syrk.hip part_layout)
-        const uint32_t c = part_tab[b0 + blockIdx.x];
+    if (part_tab) {  // cfg5: slot b0 + bx of the part's layout (syrk.hip part_layout)
+        const uint32_t c = part_tab[b0 + bx];
         bi = c & 0xffffu;
         bj = c >> 16;
     } else {
-        tile_coords(b0 + blockIdx.x, bi, bj);
+        tile_coords(b0 + bx, bi, bj);
     }
     const uint64_t i0 = (uint64_t)bi * BW, j0 = (uint64_t)bj * BW;
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
@@ -440,7 +453,7 @@ __global__ __launch_bounds__(512, 1) void k_syrk_i8r(const uint8_t* __restrict__
     // epilogue: acc mod p -> [0, p), one byte per element at its true (row, col) in the block
     const int p = kMod[r];
     const double invp = 1.0 / (double)p;
-    uint8_t* O = res + ((uint64_t)r * nblk + blockIdx.x) * (BW * BW);
+    uint8_t* O = res + ((uint64_t)r * nblk + bx) * (BW * BW);
     const int hh = lane >> 5, colp = 16 * ((lane >> 4) & 1) + pi16(lane & 15);
 #pragma unroll
     for (int x = 0; x < 4; x++)
@@ -1194,6 +1207,9 @@ void launch_syrk_packed_crt(const uint8_t* packed, uint64_t pitch, uint64_t n, u
                                                                                 cnt, res, part_tab);
         else if (g_variant_syrk == 86)  // 16 waves, 64 x 64 per wave
             k_syrk_i8h<<<dim3((unsigned)cnt, kR), 1024, 0, st>>>(packed, pitch, m, mpad, lutr, ctl, b0, cnt, res, part_tab);
+        else if (g_variant_syrk == 88)  // round-5 order: grid (blocks, moduli), block-fastest (MAP 0)
+            k_syrk_i8r<SK><<<dim3((unsigned)cnt, kR), 512, 0, st>>>(packed, pitch, m, mpad, lutr, ctl, b0, cnt, res,
+                                                                   part_tab);
         else if (g_variant_syrk == 85)  // v_mfma_i32_16x16x64_i8 shape
             k_syrk_i8s<<<dim3((unsigned)cnt, kR), 512, 0, st>>>(packed, pitch, m, mpad, lutr, ctl, b0, cnt, res, part_tab);
         else if (g_variant_syrk == 80)  // 4-slot ring of 64-SNP stages, next stage's fragments read before the barrier
@@ -1207,8 +1223,10 @@ void launch_syrk_packed_crt(const uint8_t* packed, uint64_t pitch, uint64_t n, u
                                                                      part_tab);
         else
 #endif
-        k_syrk_i8r<SK><<<dim3((unsigned)cnt, kR), 512, 0, st>>>(packed, pitch, m, mpad, lutr, ctl, b0, cnt, res,
-                                                               part_tab);
+        // MAP 1: the kR moduli of a block on one XCD at once (FETCH 951 -> 149 GB per 62.5k-SNP
+        // launch at 50k iids, the clock 2.21 -> 2.36 GHz, -3.6%: profiles/r05m)
+        k_syrk_i8r<SK, 0, 0, 0, 0, 0, 1><<<(unsigned)(round_up(cnt, 8) * kR), 512, 0, st>>>(
+            packed, pitch, m, mpad, lutr, ctl, b0, cnt, res, part_tab);
         k_crt<<<(unsigned)(cnt * 64), 256, 0, st>>>(res, b0, cnt, n, ctl, F, cc, tiles, accumulate, part_tab ? 1 : 0);
         if (after_chunk) {
             SNPMI_HIP(hipGetLastError());
