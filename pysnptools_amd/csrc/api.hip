@@ -717,7 +717,7 @@ static const uint32_t* lut_bf3(Device& d, const float* lut, uint64_t m, H2Lut* h
 static int g_f64_mfma = 0;  // public switch "f64" (pysnptools_amd.set_grm_f64): 1 = every f64 GRM on the f64 MFMA
 static bool use_crt(int dt) {
     return dt == SNPMI_DT_F64 && !g_f64_mfma &&
-           (g_variant_syrk == 0 || (g_variant_syrk >= 70 && g_variant_syrk != 71 && g_variant_syrk <= 89));
+           (g_variant_syrk == 0 || (g_variant_syrk >= 70 && g_variant_syrk != 71 && g_variant_syrk <= 99));
 }
 
 // f32 segment scratch pool of the current device (syrk.hip SegFlush): kSegSlots slots of 256 KiB

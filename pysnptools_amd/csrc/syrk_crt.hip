@@ -1207,6 +1207,17 @@ void launch_syrk_packed_crt(const uint8_t* packed, uint64_t pitch, uint64_t n, u
                                                                                 cnt, res, part_tab);
         else if (g_variant_syrk == 86)  // 16 waves, 64 x 64 per wave
             k_syrk_i8h<<<dim3((unsigned)cnt, kR), 1024, 0, st>>>(packed, pitch, m, mpad, lutr, ctl, b0, cnt, res, part_tab);
+        else if (g_variant_syrk >= 90 && g_variant_syrk <= 93) {  // MAP 1 + 78 / 79 / 83 / 84
+            const unsigned g1 = (unsigned)(round_up(cnt, 8) * kR);
+            if (g_variant_syrk == 90)
+                k_syrk_i8r<SK, 0, 0, 1, 0, 0, 1><<<g1, 512, 0, st>>>(packed, pitch, m, mpad, lutr, ctl, b0, cnt, res, part_tab);
+            else if (g_variant_syrk == 91)
+                k_syrk_i8r<SK, 0, 0, 0, 1, 0, 1><<<g1, 512, 0, st>>>(packed, pitch, m, mpad, lutr, ctl, b0, cnt, res, part_tab);
+            else if (g_variant_syrk == 92)
+                k_syrk_i8r<SK, 0, 0, 0, 0, 1, 1><<<g1, 512, 0, st>>>(packed, pitch, m, mpad, lutr, ctl, b0, cnt, res, part_tab);
+            else
+                k_syrk_i8r<SK, 0, 0, 0, 0, 2, 1><<<g1, 512, 0, st>>>(packed, pitch, m, mpad, lutr, ctl, b0, cnt, res, part_tab);
+        }
         else if (g_variant_syrk == 88)  // round-5 order: grid (blocks, moduli), block-fastest (MAP 0)
             k_syrk_i8r<SK><<<dim3((unsigned)cnt, kR), 512, 0, st>>>(packed, pitch, m, mpad, lutr, ctl, b0, cnt, res,
                                                                    part_tab);
