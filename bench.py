@@ -971,8 +971,8 @@ def grm_entry(args, dist, r, dtype):
                 "traffic_note": "PMC HBM bytes per launch (profiles/traffic.json) vs algorithmic ~2 x 5 GB of K tiles "
                                 "(accumulate read + write) + 0.8 GB of codes at 50k x 62.5k: the rest is the SegFlush "
                                 "slots (256 KiB per workgroup, flushed every 12288 SNPs by f32 atomics at L2 and read "
-                                "back once, DESIGN.md 3.4) and panel re-fetches from the MALL; at ~0.45 TB/s it is "
-                                "not the limiter of this MFMA-bound kernel",
+                                "back once, DESIGN.md 3.4) and panel re-fetches from the MALL; the flushes cost "
+                                "1.6-3% of the launch (profiles/r05sc), the accuracy they buy is DESIGN.md 3.4's table",
                 "kernel": "f32w::k_syrk_h2<false,4>: f32 GRM as 3 fp16 MFMA products of each value's fp16x2 "
                           "split, f32 accumulate (v_mfma_f32_32x32x16_f16); peak = 2.5 PF fp16 dense / 3; the timed "
                           "span also holds k_snp_stats, k_lut_bf3, k_lut_h2 and the range-gated bf16x3 launch (exits "
