@@ -616,6 +616,7 @@ __global__ __launch_bounds__(512, 1) void k_syrk_i8q(const uint8_t* __restrict__
 // accumulator registers): more waves to hide the LDS-read and barrier latencies, at a third more
 // fragment bytes per MFMA (1 KiB instead of 0.75).  Same LDS image, stages, barrier and loader
 // (4 rows per thread per stage).
+template <int MAP = 0>
 __global__ __launch_bounds__(1024, 1) void k_syrk_i8h(const uint8_t* __restrict__ P, uint64_t pitch, uint64_t kdim,
                                                       uint64_t mpad, const uint32_t* __restrict__ lutr,
                                                       const int* __restrict__ ctl, uint64_t b0, uint64_t nblk,
@@ -624,16 +625,25 @@ __global__ __launch_bounds__(1024, 1) void k_syrk_i8h(const uint8_t* __restrict_
     constexpr int SKT = SK, KS = SKT / 32, RPT = SKT / 32, PNL = SKT * RS, STG = 2 * PNL;
     __shared__ __attribute__((aligned(16))) uint8_t lds[2 * STG];
     if (ctl[1]) return;
-    const int r = blockIdx.y;
-    if (r >= ctl[2]) return;
+    uint32_t r, bx;  // MAP as in k_syrk_i8r
+    if constexpr (MAP == 1) {
+        const uint32_t w = blockIdx.x, q = w >> 3, u = q / kR;
+        r = q - u * kR;
+        bx = 8 * u + (w & 7);
+        if (bx >= nblk) return;
+    } else {
+        r = blockIdx.y;
+        bx = blockIdx.x;
+    }
+    if ((int)r >= ctl[2]) return;
     const uint32_t* lr = lutr + (uint64_t)r * mpad;
     uint32_t bi, bj;
     if (part_tab) {
-        const uint32_t c = part_tab[b0 + blockIdx.x];
+        const uint32_t c = part_tab[b0 + bx];
         bi = c & 0xffffu;
         bj = c >> 16;
     } else {
-        tile_coords(b0 + blockIdx.x, bi, bj);
+        tile_coords(b0 + bx, bi, bj);
     }
     const uint64_t i0 = (uint64_t)bi * BW, j0 = (uint64_t)bj * BW;
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
@@ -708,7 +718,7 @@ __global__ __launch_bounds__(1024, 1) void k_syrk_i8h(const uint8_t* __restrict_
     }
     const int p = kMod[r];
     const double invp = 1.0 / (double)p;
-    uint8_t* O = res + ((uint64_t)r * nblk + blockIdx.x) * (BW * BW);
+    uint8_t* O = res + ((uint64_t)r * nblk + bx) * (BW * BW);
     const int hh = lane >> 5, colp = 16 * ((lane >> 4) & 1) + pi16(lane & 15);
 #pragma unroll
     for (int x = 0; x < 2; x++)
@@ -1206,7 +1216,10 @@ void launch_syrk_packed_crt(const uint8_t* packed, uint64_t pitch, uint64_t n, u
             k_syrk_i8r<SK, 0, 0, 0, 0, 2><<<dim3((unsigned)cnt, kR), 512, 0, st>>>(packed, pitch, m, mpad, lutr, ctl, b0,
                                                                                 cnt, res, part_tab);
         else if (g_variant_syrk == 86)  // 16 waves, 64 x 64 per wave
-            k_syrk_i8h<<<dim3((unsigned)cnt, kR), 1024, 0, st>>>(packed, pitch, m, mpad, lutr, ctl, b0, cnt, res, part_tab);
+            k_syrk_i8h<><<<dim3((unsigned)cnt, kR), 1024, 0, st>>>(packed, pitch, m, mpad, lutr, ctl, b0, cnt, res, part_tab);
+        else if (g_variant_syrk == 94)  // 16 waves on the XCD-grouped grid
+            k_syrk_i8h<1><<<(unsigned)(round_up(cnt, 8) * kR), 1024, 0, st>>>(packed, pitch, m, mpad, lutr, ctl, b0, cnt,
+                                                                           res, part_tab);
         else if (g_variant_syrk >= 90 && g_variant_syrk <= 93) {  // MAP 1 + 78 / 79 / 83 / 84
             const unsigned g1 = (unsigned)(round_up(cnt, 8) * kR);
             if (g_variant_syrk == 90)
