@@ -224,6 +224,12 @@ __global__ __launch_bounds__(512, 1) void k_syrk_i8r(const uint8_t* __restrict__
         r = q - u * kR;
         bx = 8 * u + (w & 7);
         if (bx >= nblk) return;
+    } else if constexpr (MAP == 2) {  // ubench: 2 kR consecutive slots of an XCD = blocks 2p, 2p+1 (one
+        // column: they share the j panel) x kR moduli, so both blocks stream their panels in step
+        const uint32_t w = blockIdx.x, q = w >> 3, u = q / (2 * kR), j = q - u * (2 * kR), h = j / kR;
+        r = j - h * kR;
+        bx = 2 * (8 * u + (w & 7)) + h;
+        if (bx >= nblk) return;
     } else {
         r = blockIdx.y;
         bx = blockIdx.x;
@@ -1217,6 +1223,9 @@ void launch_syrk_packed_crt(const uint8_t* packed, uint64_t pitch, uint64_t n, u
                                                                                 cnt, res, part_tab);
         else if (g_variant_syrk == 86)  // 16 waves, 64 x 64 per wave
             k_syrk_i8h<><<<dim3((unsigned)cnt, kR), 1024, 0, st>>>(packed, pitch, m, mpad, lutr, ctl, b0, cnt, res, part_tab);
+        else if (g_variant_syrk == 95)  // pairs of blocks per XCD (MAP 2)
+            k_syrk_i8r<SK, 0, 0, 0, 0, 0, 2><<<(unsigned)(round_up(cnt, 16) * kR), 512, 0, st>>>(
+                packed, pitch, m, mpad, lutr, ctl, b0, cnt, res, part_tab);
         else if (g_variant_syrk == 94)  // 16 waves on the XCD-grouped grid
             k_syrk_i8h<1><<<(unsigned)(round_up(cnt, 8) * kR), 1024, 0, st>>>(packed, pitch, m, mpad, lutr, ctl, b0, cnt,
                                                                            res, part_tab);
