@@ -1425,6 +1425,8 @@ def main(argv=None):
             "grm5": grm5,
             "file": filed,
         }
+        if args.hook or args.decode_variant:  # an A/B run, not the default configuration
+            line["config"]["ab_hooks"] = list(args.hook) + (["decode=%d" % args.decode_variant] if args.decode_variant else [])
         print(json.dumps(line), flush=True)
     dist.barrier()  # every rank leaves together (rank 0 ran the CPU baselines and the file leg alone)
     dist.close()
