@@ -98,8 +98,10 @@ def parse(argv=None):
     p.add_argument("--grm-sid", type=int, default=500_000)
     p.add_argument("--grm-block", type=int, default=10_000)
     p.add_argument("--skip-grm", action="store_true")
-    p.add_argument("--grm-collective", choices=["reduce", "allreduce"], default="reduce",
-                   help="cfg4 at N > 1: K tiles summed onto rank 0 (read_kernel returns K to one caller) or onto every rank")
+    p.add_argument("--grm-collective", choices=["auto", "reduce", "allreduce"], default="auto",
+                   help="cfg4 at N > 1: the timed K-tile collective; auto = allreduce, the RCCL all-reduce configs[3] "
+                        "names (every rank gets K, as Bed.read_kernel under a group); reduce = ncclReduce onto rank 0 "
+                        "(timed unoverlapped beside it either way: grm.reduce_ms)")
     p.add_argument("--grm-f64", choices=["on", "off"], default="on", help="cfg4 GRM in float64 (reference default)")
     p.add_argument("--grm-overlap-parts", type=int, default=2,
                    help="cfg4 f32 at N > 1: column groups of the last SYRK launch whose K-tile collective "
@@ -134,6 +136,14 @@ def parse(argv=None):
     p.add_argument("--seed", type=int, default=5)
     p.add_argument("--force-rccl", action="store_true", help="build the RCCL communicator even at world size 1")
     p.add_argument("--dist-timeout", type=float, default=300.0, help="seconds for the RCCL id wait and init")
+    p.add_argument("--watchdog", type=float, default=300.0,
+                   help="N > 1: seconds without a progress mark before a rank dumps its diagnostics (leg, block, "
+                        "collective trace) to stderr, rank 0 prints a partial JSON line, and the job exits 4")
+    p.add_argument("--watchdog-final", type=float, default=1800.0,
+                   help="the watchdog's limit while ranks > 0 wait at the final barrier for rank 0's rank-only legs")
+    p.add_argument("--selfcheck", choices=["on", "off"], default="on",
+                   help="early group self-check leg: communicator size, a small K-tile all-reduce vs the oracle, "
+                        "one cfg5 all-gather bit-exact")
     p.add_argument("--side-reps", type=int, default=8,
                    help="decode legs: launches timed on the other column layout beside the timed steps (tight "
                         "if --out-ld spreads the block, else --spread-ld)")
@@ -149,11 +159,189 @@ def parse(argv=None):
     return p.parse_args(argv)
 
 
+# ---------------------------------------------------------------------------- the box
+def _sysfs_card(pci):
+    """/sys/class/drm/cardN/device of the GPU at PCI domain:bus:device (None if not found)."""
+    import glob
+
+    want = "%04x:%02x:%02x" % tuple(pci)
+    for dev in sorted(glob.glob("/sys/class/drm/card[0-9]*/device")):
+        try:
+            if os.path.basename(os.path.realpath(dev)).startswith(want):
+                return dev
+        except OSError:
+            continue
+    return None
+
+
+def _read(path):
+    try:
+        with open(path) as f:
+            return f.read().strip()
+    except OSError:
+        return None
+
+
+def read_sclk_mhz(card):
+    """The GPU's current shader clock from sysfs: hwmon freq1_input (Hz), else the starred level of
+    pp_dpm_sclk; None if neither is readable."""
+    import glob
+
+    if card is None:
+        return None
+    for f in glob.glob(os.path.join(card, "hwmon", "hwmon*", "freq1_input")):
+        v = _read(f)
+        if v and v.isdigit():
+            return int(v) / 1e6
+    t = _read(os.path.join(card, "pp_dpm_sclk"))
+    if t:
+        for ln in t.splitlines():
+            if ln.strip().endswith("*"):
+                try:
+                    return float(ln.split(":")[1].strip().rstrip("*").strip().lower().rstrip("mhz"))
+                except (IndexError, ValueError):
+                    return None
+    return None
+
+
+def box_info(N, dist):
+    """Device ids of the GPU this rank measures on: name, CUs, HBM, UUID, PCI
+    address, max SCLK, the sysfs unique_id / serial when readable, the host name."""
+    name = ctypes.create_string_buffer(64)
+    mem, cus = ctypes.c_uint64(), ctypes.c_int()
+    uuid = (ctypes.c_uint8 * 16)()
+    pci = (ctypes.c_int * 3)()
+    clk = ctypes.c_int()
+    N.call("snpmi_device_info", dist.device, name, 64, ctypes.byref(mem), ctypes.byref(cus))
+    N.call("snpmi_device_ids", dist.device, uuid, pci, ctypes.byref(clk))
+    card = _sysfs_card(list(pci))
+    return {"gpu": name.value.decode(errors="replace"), "cus": cus.value, "hbm_bytes": mem.value,
+            "uuid": bytes(uuid).hex(), "pci": "%04x:%02x:%02x" % tuple(pci), "sclk_max_mhz": clk.value / 1e3,
+            "unique_id": _read(os.path.join(card, "unique_id")) if card else None,
+            "serial": _read(os.path.join(card, "serial_number")) if card else None,
+            "sysfs": card, "host": socket.gethostname(), "sclk_idle_mhz": read_sclk_mhz(card)}
+
+
+class ClockSampler(object):
+    """Samples the GPU's SCLK from sysfs every 50 ms on a thread while a leg runs (the loaded clock
+    the leg's rate depends on; MI355X_MICROARCH.md: devices differ by ~12%)."""
+
+    def __init__(self, box, period=0.05):
+        import threading
+
+        self.card, self.period, self.v = box.get("sysfs"), period, []
+        self._stop = threading.Event()
+        self._t = threading.Thread(target=self._run, daemon=True)
+
+    def _run(self):
+        while not self._stop.wait(self.period):
+            c = read_sclk_mhz(self.card)
+            if c is not None:
+                self.v.append(c)
+
+    def __enter__(self):
+        self._t.start()
+        return self
+
+    def __exit__(self, *exc):
+        self._stop.set()
+        self._t.join(timeout=2)
+
+    def summary(self):
+        if not self.v:
+            return {"samples": 0, "note": "no readable sysfs clock on this box (%s)" % self.card}
+        v = np.asarray(self.v)
+        return {"samples": int(v.size), "mean": float(v.mean()), "median": float(np.median(v)), "min": float(v.min()),
+                "max": float(v.max()), "source": "sysfs (%s), every 50 ms during the leg" % self.card}
+
+
+# ---------------------------------------------------------------------------- leg 0: group self-check
+SELF_N, SELF_M = 600, 3000
+
+
+def leg_selfcheck(N, args, dist):
+    """Before the long legs: does the group work?  (1) the communicator holds
+    WORLD_SIZE ranks; (2) a small K-tile all-reduce through the cfg4 code path (ShardedGrm.
+    add_packed_combine: each rank its SNP span of a 600-iid x 3000-SNP matrix, Unit, f32, the
+    overlapped column groups) -- every rank's K identical (checksums over the group) and rank 0's K vs
+    the oracle (f64); (3) one cfg5 block through PartitionedGrm's all-gather, rebuilt bit-exactly;
+    (4) every rank issued the same RCCL calls (count and call-sequence signature)."""
+    from pysnptools_amd.shard import ShardedGrm, rank_span
+
+    t0 = time.perf_counter()
+    res = {"world": dist.world, "n_gpus": dist.n_gpus, "group_size_ok": dist.n_gpus == dist.world}
+    n, m = SELF_N, SELF_M
+    pitch = N.lib().snpmi_packed_pitch(n)
+    full = Dev(N, pitch * m)
+    synth(N, full.p, pitch, n, 0, m, args.seed + 900, 0.05)
+    lo, hi = rank_span(m, dist.rank, dist.world)
+    stats = Dev(N, max(1, hi - lo) * 8)
+    coll = "allreduce" if dist.can_reduce and (dist.world > 1 or dist.rccl) else "none"
+    g = ShardedGrm(n, np.float32, dist if dist.can_reduce else None, coll, 0, dist.rank, dist.world)
+    K = np.empty((n, n), dtype=np.float32)
+    try:
+        g.add_packed_combine(full.at(lo * pitch), pitch, hi - lo, N.STD_UNIT, 0.0, 0.0, 0, stats.p,
+                             parts=args.grm_overlap_parts)
+        N.call("snpmi_stream_sync")
+        t, _ = g.tiles()
+        ri = np.arange(n, dtype=np.uint64)
+        dri, dout = Dev(N, n * 8), Dev(N, n * n * 4)
+        N.call("snpmi_memcpy_h2d", dri.p, N.ptr(ri), ri.nbytes)
+        N.call("snpmi_dev_grm_extract", t, n, N.DT_F32, dri.p, n, None, n, 1, 1.0, dout.p)
+        N.call("snpmi_memcpy_d2h", N.ptr(K), dout.p, K.nbytes)
+        dri.free()
+        dout.free()
+    finally:
+        g.abort()
+    k64 = K.astype(np.float64)
+    sums = (float(k64.sum()), float((k64 * np.arange(1, n + 1)).sum()))
+    same = all(dist.max(x) == -dist.max(-x) for x in sums)
+    res["allreduce"] = {"collective": coll, "workload": "%d iids x %d SNPs, f32, each rank its SNP span" % (n, m),
+                        "every_rank_same_K": bool(same)}
+    if dist.rank == 0:
+        from oracle import oracle as O
+
+        bpc = (n + 3) // 4
+        host = np.empty((m, pitch), dtype=np.uint8)
+        N.call("snpmi_memcpy_d2h", N.ptr(host), full.p, host.nbytes)
+        Z = O.decode(np.ascontiguousarray(host[:, :bpc]).reshape(-1), n, m, dtype=np.float64)
+        O.standardize_native(Z)
+        ref = Z.dot(Z.T)
+        err = float(np.abs(k64 - ref).max() / np.abs(np.diag(ref)).max())
+        res["allreduce"].update(max_abs_err_over_max_diag=err, tolerance=2e-6)
+    full.free()
+    stats.free()
+    if dist.world > 1 or dist.rccl:
+        mark(None, "selfcheck all-gather")
+        x, cdf = maf_table(4096)
+
+        def fill(host, s0, cnt):
+            N.call("snpmi_host_synth_bed", host, N.lib().snpmi_packed_pitch(4096), 4096, s0, cnt, args.seed + 901, 0.05,
+                   N.ptr(x), N.ptr(cdf), len(x), 1)
+
+        res["allgather_bit_exact"] = gather_check(N, dist, max(dist.world, GRM5_PLAN_WORLD), fill, 4096, 1024, 1024)
+    tr = N.rccl_trace()
+    calls, sig48 = float(tr["calls"]), float(int(tr["sig"], 16) & ((1 << 48) - 1))
+    res["rccl_calls"] = tr["calls"]
+    res["rccl_same_calls_every_rank"] = bool(all(dist.max(v) == -dist.max(-v) for v in (calls, sig48)))
+    res["seconds"] = time.perf_counter() - t0
+    ok = res["group_size_ok"] and same and res["rccl_same_calls_every_rank"]
+    if dist.rank == 0:
+        ok = ok and res["allreduce"]["max_abs_err_over_max_diag"] <= 2e-6
+    if res.get("allgather_bit_exact") is False:
+        ok = False
+    res["pass"] = bool(ok) if dist.rank == 0 else None
+    return res
+
+
 # ---------------------------------------------------------------------------- process launch
 def _free_port():
     with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
         s.bind(("127.0.0.1", 0))
         return s.getsockname()[1]
+
+
+SPAWN_GRACE_S = 15.0
 
 
 def spawn_ranks(args, argv):
@@ -167,7 +355,7 @@ def spawn_ranks(args, argv):
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=port, SNPMI_RCCL_ID_FILE=os.path.join(tmp, "rccl.id"))
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env,
                                       stdout=None if r == 0 else sys.stderr))
-    rc = 0
+    rc, deadline = 0, None
     try:
         while procs:
             for p in list(procs):
@@ -175,10 +363,15 @@ def spawn_ranks(args, argv):
                 if code is None:
                     continue
                 procs.remove(p)
-                if code != 0:
-                    rc = rc or code
-                    for q in procs:  # one rank failed: the others would wait in a collective forever
-                        q.kill()
+                if code != 0 and not rc:
+                    # one rank failed: its watchdog left the job's abort file, so the others dump their
+                    # diagnostics and exit within a second; whoever is still running after the grace
+                    # period would wait in a collective forever
+                    rc = code
+                    deadline = time.time() + SPAWN_GRACE_S
+            if deadline is not None and time.time() > deadline:
+                for q in procs:
+                    q.kill()
             time.sleep(0.2)
     finally:
         for q in procs:
@@ -233,10 +426,44 @@ class Events:
 _T0 = time.time()
 
 
-def progress(msg):
-    """One line on stderr per leg (a long default run is never silent for minutes)."""
+WD = None  # this rank's pysnptools_amd.dist.Watchdog (N > 1)
+RANK = 0
+# rank 0: the line's fields measured so far -- what the watchdog prints as a partial JSON line
+PARTIAL = {}
+
+
+def mark(leg=None, detail=None, limit=None):
+    """Watchdog progress mark (no output)."""
+    if WD is not None:
+        WD.mark(leg, detail, limit)
+
+
+def progress(msg, limit=None):
+    """One line on stderr per leg (a long default run is never silent for minutes) and a watchdog
+    mark.  SNPMI_BENCH_STALL="R:PREFIX" (tests) makes rank R hang here at the first leg whose label
+    starts with PREFIX, as a rank stuck inside a leg would."""
     sys.stderr.write("[bench %7.1fs] %s\n" % (time.time() - _T0, msg))
     sys.stderr.flush()
+    mark(msg, None, limit)
+    stall = os.environ.get("SNPMI_BENCH_STALL", "")
+    if stall:
+        r, _, prefix = stall.partition(":")
+        if int(r) == RANK and msg.startswith(prefix):
+            sys.stderr.write("[bench] rank %d: SNPMI_BENCH_STALL -- hanging in leg %r\n" % (RANK, msg))
+            sys.stderr.flush()
+            while True:
+                time.sleep(3600)
+
+
+def partial_line(diag):
+    """The watchdog's partial JSON line (rank 0): what was measured before the stall, marked as such."""
+    if PARTIAL.get("_printed"):  # the full line is out already (a stall at the final barrier)
+        return
+    line = {"metric": METRIC, "value": None, "unit": "SNPs/s", "higher_is_better": True, "partial": True,
+            "error": "watchdog: %s (rank %d, leg %r)" % (diag["reason"], diag["rank"], diag["leg"])}
+    line.update(PARTIAL)
+    line["watchdog"] = diag
+    print(json.dumps(line, default=str), flush=True)
 
 
 def maf_table(n_iid):
@@ -628,7 +855,8 @@ def leg_grm(N, args, dist, dtype, keep_tiles=False):
     if my_m:
         synth(N, packed.p, pitch, n, lo, my_m, args.seed + 100, 0.01)
     stats = Dev(N, max(1, my_m) * 2 * esz)
-    collective = args.grm_collective if dist.can_reduce else "none"
+    want = "allreduce" if args.grm_collective == "auto" else args.grm_collective
+    collective = want if dist.can_reduce else "none"
     ev = Events(N, 4)
     chunks = (my_m + 65535) // 65536 if my_m else 0
 
@@ -672,13 +900,27 @@ def leg_grm(N, args, dist, dtype, keep_tiles=False):
     if keep_tiles:
         host_tiles = np.empty(count, dtype=npdt)
         N.call("snpmi_memcpy_d2h", N.ptr(host_tiles), tiles, host_tiles.nbytes)
+    unoverlapped = {}
+    if collective != "none" and dist.world > 1:
+        # beside the timed line (untimed; the tiles are overwritten): each collective alone over the
+        # whole tile buffer, unoverlapped -- ncclReduce onto rank 0 (half the bytes: K for one caller)
+        # and ncclAllReduce (K on every rank, the configs[3] exchange)
+        for name, root in (("reduce", 0), ("allreduce", None)):
+            mark(None, "grm %s unoverlapped %s" % (dtype, name))
+            dist.barrier()
+            ev.record(0)
+            dist.sum_dev(tiles, count, npdt, root)
+            ev.record(3)
+            N.call("snpmi_stream_sync")
+            unoverlapped[name + "_ms"] = dist.max(ev.ms(0, 3))
+        unoverlapped["bytes"] = count * esz
     g.abort()  # K stays as tiles in HBM; the session ends without the n x n extraction
     nb = (n + 255) // 256
     exec_ratio = SPLIT_PRODUCTS * 2 * 256 * 256 * (nb * (nb + 1) // 2) / (n * (n + 1))  # executed fp16 / algorithmic
     res = dict(wall=wall, syrk_ms=syrk_ms, allreduce_ms=coll_ms, trace=trace, exec_ratio=exec_ratio,
                mean_tflops=(n * (n + 1) * my_m / (syrk_ms * 1e-3) / 1e12) if syrk_ms else 0.0,
                launches=chunks, snps_per_launch=(my_m + chunks - 1) // chunks if chunks else 0,
-               my_m=my_m, crt_moduli=crt_moduli, collective=collective, tiles=host_tiles)
+               my_m=my_m, crt_moduli=crt_moduli, collective=collective, tiles=host_tiles, unoverlapped=unoverlapped)
     if dist.rank == 0 and not args.skip_cpu and my_m > 0:
         # parity sample (untimed): K rows 0..63 of the GRM of this rank's first 512 SNPs
         cm, rows = min(512, my_m), 64
@@ -820,7 +1062,7 @@ def leg_grm5(N, args, dist):
         dist.barrier()
         t0 = time.perf_counter()
         block_ms = g.run(fill, progress=lambda k, nb: progress("grm5 block %d/%d" % (k + 1, nb))
-                         if (k + 1) % 4 == 0 else None)
+                         if (k + 1) % 4 == 0 else mark(None, "grm5 block %d/%d" % (k + 1, nb)))
         dist.barrier()
         wall = dist.max(time.perf_counter() - t0)
         res = {"wall": wall, "block_ms": block_ms, "n_local_blocks": g.nloc, "m": m, "ms": g.ms, "P": P,
@@ -856,10 +1098,15 @@ def grm5_part_spread(n, P):
 def grm5_gather_check(N, args, dist, P, fill):
     """N > 1: one more block through the same plan (each rank's share + all-gather, untimed); rank 0
     compares the rebuilt block with the block generated whole on its host."""
+    return gather_check(N, dist, P, fill, args.grm5_iid, min(args.grm5_sid, args.grm5_block), args.grm5_block)
+
+
+def gather_check(N, dist, P, fill, n, m, block):
+    """One block of m SNPs x n iids through PartitionedGrm's share + all-gather plan; rank 0 returns
+    whether the rebuilt block equals the block generated whole on its host (other ranks: None)."""
     from pysnptools_amd.shard import PartitionedGrm
 
-    n, m = args.grm5_iid, min(args.grm5_sid, args.grm5_block)
-    g = PartitionedGrm(n, m, N.STD_UNIT, dist=dist, part=dist.rank, parts=P, block=args.grm5_block, out="hbm",
+    g = PartitionedGrm(n, m, N.STD_UNIT, dist=dist, part=dist.rank, parts=P, block=block, out="hbm",
                        first_block=m)  # one block: dev[0] holds all of it
     try:
         g.run(fill)
@@ -898,6 +1145,8 @@ def grm5_parity(args, picks, gpu_stats, threads):
         cnt = min(B, m - s0)
         if (s0 // B) % 16 == 15:
             progress("grm5 parity block %d/%d" % (s0 // B + 1, (m + B - 1) // B))
+        else:
+            mark(None, "grm5 parity block %d" % (s0 // B + 1))
         fill(ctypes.c_void_p(buf.ctypes.data), s0, cnt)
         body = buf[:cnt] if pitch == bpc else np.ascontiguousarray(buf[:cnt, :bpc])
         body = body.reshape(-1)
@@ -1006,6 +1255,10 @@ def grm_entry(args, dist, r, dtype):
                            if coll else ""),
             "gflops": gf, "snps_per_s": m / r["wall"], "seconds": r["wall"], "scaling": "strong",
             "collective": coll, "allreduce_ms": r["allreduce_ms"],
+            "collective_alone": dict(r["unoverlapped"], note="each collective alone over the whole K-tile buffer, "
+                                     "after the timed region (reduce = ncclReduce onto rank 0, the half-bytes form "
+                                     "for one caller; allreduce = the timed exchange, here unoverlapped)")
+            if r["unoverlapped"] else None,
             "collective_overlap": (("the last SYRK launch in %d column groups, each group's tiles summed on the aux "
                                     "stream under the next group's SYRK" % args.grm_overlap_parts) if f32 else
                                    "the CRT path's column-aligned residue chunks of the last launch, each chunk's f64 "
@@ -1247,6 +1500,7 @@ def decode_entry(r, label):
 
 
 def main(argv=None):
+    global WD, RANK
     argv = sys.argv[1:] if argv is None else argv
     args = parse(argv)
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -1271,10 +1525,38 @@ def main(argv=None):
         sys.stderr.write("bench.py: %s\n" % e)
         sys.stderr.flush()
         os._exit(3)
+    RANK = dist.rank
+    if dist.world > 1 or dist.rccl:
+        # a collective one rank never joins would block the others forever: bounded, diagnosed exit
+        WD = D.Watchdog(dist, args.watchdog, on_fire=partial_line if dist.rank == 0 else None)
+    try:
+        run_legs(N, args, dist)
+    except Exception as e:
+        if WD is not None:  # dump, tell the other ranks (they are waiting in a collective), exit 4
+            import traceback
 
+            traceback.print_exc()
+            WD.fail("%s on rank %d: %s" % (type(e).__name__, dist.rank, e))
+        raise
+    if WD is not None:
+        WD.stop()
+        if dist.rank == 0:
+            WD.clear()
+    dist.close()
+
+
+def run_legs(N, args, dist):
+    box = box_info(N, dist)
+    selfcheck = None
+    if args.selfcheck == "on":
+        progress("selfcheck (group size, K-tile all-reduce, all-gather)", limit=min(args.watchdog, 180.0))
+        selfcheck = leg_selfcheck(N, args, dist)
+        PARTIAL["selfcheck"] = selfcheck
     progress("decode + Unit standardize (value)")
     r1 = leg_standardize(N, args, dist)
     value = args.n_sid * args.steps / r1["wall"]
+    PARTIAL.update(value=value, n_gpus=dist.n_gpus, steps=args.steps, warmup=args.warmup,
+                   ms_per_step=r1["wall"] / args.steps * 1e3, selfcheck=selfcheck, box=box)
     grm = grm64 = grm5 = dec_c = e2e = beta = filed = None
     if dist.rank == 0:
         progress("decode_c / e2e")
@@ -1288,14 +1570,21 @@ def main(argv=None):
                              miss=0.218, seed=args.seed + 3)
     if not args.skip_grm:
         progress("grm cfg4 f32 / f64")
-        r2 = leg_grm(N, args, dist, "f32")
+        with ClockSampler(box) as clk:
+            r2 = leg_grm(N, args, dist, "f32")
         grm = grm_entry(args, dist, r2, "f32")
+        grm["sclk_mhz"] = clk.summary()
+        PARTIAL["grm"] = grm
         if args.grm_f64 == "on":
-            r2d = leg_grm(N, args, dist, "f64")
+            with ClockSampler(box) as clk:
+                r2d = leg_grm(N, args, dist, "f64")
             grm64 = grm_entry(args, dist, r2d, "f64")
+            grm64["sclk_mhz"] = clk.summary()
+            PARTIAL["grm_f64"] = grm64
     if args.grm5 == "on":
         progress("grm5 cfg5 (part %d)" % dist.rank)
-        r3 = leg_grm5(N, args, dist)
+        with ClockSampler(box) as clk5:
+            r3 = leg_grm5(N, args, dist)
         n5, m5, P = args.grm5_iid, r3["m"], r3["P"]
         flops_part = n5 * (n5 + 1) * m5 / P  # this part's share of the SYRK work
         busy_s = sum(r3["block_ms"]) * 1e-3
@@ -1356,6 +1645,8 @@ def main(argv=None):
         if dist.rank == 0 and r3.get("gather_exact") is not None:
             grm5["parity"]["gathered_block_bit_exact"] = r3["gather_exact"]
             grm5["parity"]["pass"] = grm5["parity"]["pass"] and r3["gather_exact"]
+        grm5["sclk_mhz"] = clk5.summary()
+        PARTIAL["grm5"] = grm5
     if dist.rank == 0 and args.file == "on":
         progress("file leg")
         filed = leg_file(N, args)
@@ -1424,12 +1715,19 @@ def main(argv=None):
             "grm_f64": grm64,
             "grm5": grm5,
             "file": filed,
+            "selfcheck": selfcheck,
+            "box": dict(box, fill_GBps=r1["fill_gbs"], copy_GBps=r1["copy_gbs"],
+                        note="the box this line was measured on: device ids, the hipMemset fill and 1:1 copy ceilings "
+                             "measured in this process (decode leg buffers), and the SCLK sampled from sysfs during "
+                             "each GRM leg (grm*.sclk_mhz) -- compare runs on different boxes against these"),
         }
         if args.hook or args.decode_variant:  # an A/B run, not the default configuration
             line["config"]["ab_hooks"] = list(args.hook) + (["decode=%d" % args.decode_variant] if args.decode_variant else [])
         print(json.dumps(line), flush=True)
-    dist.barrier()  # every rank leaves together (rank 0 ran the CPU baselines and the file leg alone)
-    dist.close()
+        PARTIAL["_printed"] = True
+    # every rank leaves together (rank 0 ran the CPU baselines and the file leg alone)
+    progress("final barrier", limit=args.watchdog_final)
+    dist.barrier()
 
 
 if __name__ == "__main__":

@@ -87,6 +87,8 @@ int snpmi_set_device(int device);            /* device used by later calls of th
 int snpmi_get_device(int* device);
 int snpmi_release_cache(void);               /* free cached device/pinned scratch          */
 int snpmi_device_info(int device, char* name, size_t name_len, uint64_t* total_mem, int* cu_count);
+/* the box a measurement ran on: 16-byte device UUID, PCI domain / bus / device, max SCLK (kHz) */
+int snpmi_device_ids(int dev, uint8_t* uuid16, int* pci, int* clock_khz);
 /* select a kernel variant by name; 0 = default.  Public switches: "f64" (0 = f64 GRMs as int8
  * residues + CRT, 1 = on the f64 MFMA), "seg" (SNPs per f32 GRM accumulation chain, default 12288,
  * 0 = one chain per launch).  The rest ("decode", "syrk", "part_order" (1 = the cfg5 part
@@ -401,6 +403,13 @@ int snpmi_rccl_host_allreduce_f64(double* values, uint64_t count, int op);
 int snpmi_rccl_barrier(void);
 int snpmi_rccl_comm_count(int* count);                    /* ncclCommCount: ranks in the communicator */
 int snpmi_rccl_destroy(void);
+/* Collective trace of this process (lock-free; callable from another thread while one sits in a
+ * collective): out[0..11] = calls, all-reduces, reduces, all-gathers, host all-reduces (barriers /
+ * max), bytes enqueued, signature of the (kind, count, root) sequence (FNV-1a: the same calls in the
+ * same order give the same value on every rank), last kind (1 all-reduce, 2 reduce, 3 all-gather,
+ * 4 host), last count, 1 while inside a blocking host all-reduce, completed host all-reduces,
+ * communicator present.  n = entries wanted (<= 12). */
+int snpmi_rccl_trace(uint64_t* out, uint64_t n);
 
 #ifdef __cplusplus
 }

@@ -32,6 +32,7 @@ _SIGS = {
     "snpmi_release_cache": [],
     "snpmi_device_info": [_i32, ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_uint64),
                           ctypes.POINTER(ctypes.c_int)],
+    "snpmi_device_ids": [_i32, _vp, _vp, ctypes.POINTER(ctypes.c_int)],
     "snpmi_set_kernel_variant": [_cp, _i32],
     "snpmi_get_kernel_variant": [_cp, ctypes.POINTER(ctypes.c_int)],
     "snpmi_bed_check": [_cp, _u64, _u64],
@@ -139,6 +140,7 @@ _SIGS = {
     "snpmi_rccl_barrier": [],
     "snpmi_rccl_comm_count": [ctypes.POINTER(ctypes.c_int)],
     "snpmi_rccl_destroy": [],
+    "snpmi_rccl_trace": [_vp, _u64],
     "snpmi_last_error": [],
 }
 _RESTYPES = {"snpmi_last_error": ctypes.c_char_p, "snpmi_packed_pitch": ctypes.c_uint64,
@@ -211,6 +213,21 @@ def kernel_variant(name):
     v = ctypes.c_int(0)
     call("snpmi_get_kernel_variant", name.encode() if isinstance(name, str) else name, ctypes.byref(v))
     return v.value
+
+
+TRACE_FIELDS = ("calls", "allreduce", "reduce", "allgather", "host", "bytes", "sig", "last_kind", "last_count",
+                "in_blocking_call", "blocking_calls_done", "comm")
+TRACE_KINDS = {0: None, 1: "allreduce", 2: "reduce", 3: "allgather", 4: "host_allreduce"}
+
+
+def rccl_trace():
+    """This process's RCCL call counters (snpmi_rccl_trace) as a dict; safe from a watchdog thread."""
+    out = (ctypes.c_uint64 * len(TRACE_FIELDS))()
+    check(lib().snpmi_rccl_trace(out, len(TRACE_FIELDS)))
+    d = dict(zip(TRACE_FIELDS, (int(x) for x in out)))
+    d["sig"] = "%016x" % d["sig"]
+    d["last_kind"] = TRACE_KINDS.get(d["last_kind"], d["last_kind"])
+    return d
 
 
 def device_count():

@@ -1644,6 +1644,20 @@ int snpmi_device_info(int dev, char* name, size_t name_len, uint64_t* total_mem,
     });
 }
 
+int snpmi_device_ids(int dev, uint8_t* uuid16, int* pci, int* clock_khz) {
+    return guarded([&] {
+        hipDeviceProp_t p;
+        SNPMI_HIP(hipGetDeviceProperties(&p, dev));
+        if (uuid16) std::memcpy(uuid16, p.uuid.bytes, 16);
+        if (pci) {
+            pci[0] = p.pciDomainID;
+            pci[1] = p.pciBusID;
+            pci[2] = p.pciDeviceID;
+        }
+        if (clock_khz) *clock_khz = p.clockRate;
+    });
+}
+
 int snpmi_set_kernel_variant(const char* kernel, int variant) {
     return guarded([&] {
         SNPMI_REQUIRE(kernel != nullptr, SNPMI_E_ARG, "kernel name is NULL");

@@ -205,34 +205,18 @@ template <typename V>
 __device__ __forceinline__ void store_nt(V* p, const V& v) {
     __builtin_nontemporal_store(v, p);
 }
-// ubench A/B of the store cache policy of the F-order decode (POL 0 = nt, the shipped policy)
-template <int POL>
-__device__ __forceinline__ void store_pol(f32x4_t* p, const f32x4_t& v) {
-    if constexpr (POL == 0) __builtin_nontemporal_store(v, p);
-    else if constexpr (POL == 1) *p = v;
-    else if constexpr (POL == 2) asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
-    else if constexpr (POL == 3) asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(p), "v"(v) : "memory");
-    else if constexpr (POL == 4) asm volatile("global_store_dwordx4 %0, %1, off sc1 nt" ::"v"(p), "v"(v) : "memory");
-    else asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1 nt" ::"v"(p), "v"(v) : "memory");
-}
-
-// ORD (ubench-only A/B of the item order; 0 ships): 1 = each XCD takes a contiguous slice of
-// every grid pass, 2 = items column-interleaved (a wave's U items in U different columns),
-// 3 = store-only ablation (no code loads)
-// CS > 0: columns visited in stride-CS order (logical column l -> (l mod R) CS + l div R, R =
-// ceil(m / CS)), so the columns in flight at once sit CS columns apart in the output
-template <typename T, int U, int ORD = 0, int CS = 0, int POL = 0>
+// XCD-sliced item order: the grid is a multiple of 8 and block b works as logical block
+// (b mod 8) G/8 + b/8, so each XCD writes a contiguous 1/8 of every grid pass
+template <typename T, int U>
 __global__ __launch_bounds__(kBlock) void k_decode_f(const uint8_t* __restrict__ packed, uint64_t pitch, uint64_t n,
                                                      uint64_t m, const T* __restrict__ lut, T* __restrict__ out,
                                                      uint64_t ld) {
     const int lane = threadIdx.x & (kWave - 1);
     const uint64_t chunks = (n + 1023) / 1024;
-    const uint64_t R = CS ? (m + CS - 1) / CS : m;
-    const uint64_t total = chunks * (CS ? R * CS : m);
+    const uint64_t total = chunks * m;
     const uint64_t groups = (total + U - 1) / U;
     const uint64_t nwaves = (uint64_t)gridDim.x * (kBlock / kWave);
-    uint64_t lb = blockIdx.x;
-    if constexpr (ORD == 1) lb = (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
+    const uint64_t lb = (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
     for (uint64_t gi = lb * (kBlock / kWave) + threadIdx.x / kWave; gi < groups; gi += nwaves) {
         uint32_t w[U];
         uint64_t jv[U], cv[U];
@@ -240,17 +224,12 @@ __global__ __launch_bounds__(kBlock) void k_decode_f(const uint8_t* __restrict__
 #pragma unroll
         for (int u = 0; u < U; u++) {
             const uint64_t it = gi * U + u;
-            uint64_t j = it / chunks, c = it - j * chunks;
-            if constexpr (ORD == 2) {
-                c = it / m;
-                j = it - c * m;
-            }
-            if constexpr (CS > 0) j = (j % R) * CS + j / R;
+            const uint64_t j = it / chunks, c = it - j * chunks;
             jv[u] = j;
             cv[u] = c;
-            val[u] = it < total && j < m;  // wave-uniform
-            const bool ok = ORD != 3 && val[u] && (c * 1024 + 16 * (uint64_t)lane < n);
-            w[u] = ok ? reinterpret_cast<const uint32_t*>(packed + j * pitch)[c * 64 + lane] : (uint32_t)lane * 0x9E3779B9u;
+            val[u] = it < total;  // wave-uniform
+            const bool ok = val[u] && (c * 1024 + 16 * (uint64_t)lane < n);
+            w[u] = ok ? reinterpret_cast<const uint32_t*>(packed + j * pitch)[c * 64 + lane] : 0u;
         }
 #pragma unroll
         for (int u = 0; u < U; u++) {
@@ -270,7 +249,7 @@ __global__ __launch_bounds__(kBlock) void k_decode_f(const uint8_t* __restrict__
                     v.z = sel4(l0, l1, l2, l3, (byte >> 4) & 3u);
                     v.w = sel4(l0, l1, l2, l3, byte >> 6);
                     if (i + 4 <= n) {
-                        store_pol<POL>(reinterpret_cast<f32x4_t*>(o + r * 256 + 4 * lane), v);
+                        store_nt(reinterpret_cast<f32x4_t*>(o + r * 256 + 4 * lane), v);
                     } else {
                         for (int t = 0; t < 4; t++)
                             if (i + t < n) o[r * 256 + 4 * lane + t] = v[t];
@@ -315,381 +294,6 @@ __global__ __launch_bounds__(kBlock) void k_decode_f(const uint8_t* __restrict__
     }
 }
 
-#ifdef SNPMI_UBENCH
-// ubench A/B of the write window (f32): items of RN x 256 iids, U items per wave, so the resident
-// waves' stores cover ~8192 x U x RN KiB of the output at once (hipMemset's fill sweeps ~8 MB;
-// k_decode_f<.,4> 128 MB)
-template <int RN, int U, int ORD>
-__global__ __launch_bounds__(kBlock) void k_decode_fine(const uint8_t* __restrict__ packed, uint64_t pitch, uint64_t n,
-                                                        uint64_t m, const float* __restrict__ lut, float* __restrict__ out,
-                                                        uint64_t ld) {
-    constexpr int IIDS = RN * 256;
-    const int lane = threadIdx.x & (kWave - 1);
-    const uint64_t chunks = (n + IIDS - 1) / IIDS, total = chunks * m, groups = (total + U - 1) / U;
-    const uint64_t nwaves = (uint64_t)gridDim.x * (kBlock / kWave);
-    uint64_t lb = blockIdx.x;
-    if constexpr (ORD == 1) lb = (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
-    for (uint64_t gi = lb * (kBlock / kWave) + threadIdx.x / kWave; gi < groups; gi += nwaves) {
-        uint32_t w[U];
-        uint64_t jv[U], cv[U];
-        bool val[U];
-#pragma unroll
-        for (int u = 0; u < U; u++) {
-            const uint64_t it = gi * U + u;
-            const uint64_t j = it / chunks, c = it - j * chunks;
-            jv[u] = j;
-            cv[u] = c;
-            val[u] = it < total;
-            const bool ok = val[u] && lane < 16 * RN && (c * IIDS + 16 * (uint64_t)lane < n);
-            w[u] = ok ? reinterpret_cast<const uint32_t*>(packed + j * pitch)[c * (16 * RN) + lane] : 0u;
-        }
-#pragma unroll
-        for (int u = 0; u < U; u++) {
-            if (!val[u]) continue;
-            const uint64_t j = jv[u], i0 = cv[u] * IIDS;
-            const float l0 = lut[4 * j], l1 = lut[4 * j + 1], l2 = lut[4 * j + 2], l3 = lut[4 * j + 3];
-            float* o = out + j * ld + i0;
-#pragma unroll
-            for (int r = 0; r < RN; r++) {
-                const uint32_t src = __shfl(w[u], r * 16 + (lane >> 2), kWave);
-                const uint32_t byte = (src >> (8 * (lane & 3))) & 0xffu;
-                const uint64_t i = i0 + r * 256 + 4 * lane;
-                f32x4_t v;
-                v.x = sel4(l0, l1, l2, l3, byte & 3u);
-                v.y = sel4(l0, l1, l2, l3, (byte >> 2) & 3u);
-                v.z = sel4(l0, l1, l2, l3, (byte >> 4) & 3u);
-                v.w = sel4(l0, l1, l2, l3, byte >> 6);
-                if (i + 4 <= n) {
-                    store_nt(reinterpret_cast<f32x4_t*>(o + r * 256 + 4 * lane), v);
-                } else {
-                    for (int t = 0; t < 4; t++)
-                        if (i + t < n) o[r * 256 + 4 * lane + t] = v[t];
-                }
-            }
-        }
-    }
-}
-
-// ubench: hipMemset-shaped sweep (the ROCclr fill runs 0.60-0.63 ms per 4 GB on every buffer, the
-// decode 0.61-0.77 by placement): a persistent grid of G workgroups, items of 256 iids (1 KiB of
-// output) interleaved across waves -- store u of batch b of every wave lands in the contiguous
-// window of items (b U + u) nwaves .. +nwaves -- and the next batch's code dwords loaded before
-// the current batch's stores
-template <int U>
-__global__ __launch_bounds__(kBlock) void k_decode_sweep(const uint8_t* __restrict__ packed, uint64_t pitch, uint64_t n,
-                                                         uint64_t m, const float* __restrict__ lut, float* __restrict__ out,
-                                                         uint64_t ld) {
-    const int lane = threadIdx.x & (kWave - 1);
-    const uint64_t chunks = (n + 255) / 256, total = chunks * m;
-    const uint64_t nwaves = (uint64_t)gridDim.x * (kBlock / kWave);
-    const uint64_t wv = (uint64_t)blockIdx.x * (kBlock / kWave) + threadIdx.x / kWave;
-    auto load = [&](uint64_t it) -> uint32_t {
-        if (it >= total) return 0u;
-        const uint64_t j = it / chunks, c = it - j * chunks;
-        const bool ok = lane < 16 && c * 256 + 16 * (uint64_t)lane < n;
-        return ok ? reinterpret_cast<const uint32_t*>(packed + j * pitch)[c * 16 + lane] : 0u;
-    };
-    uint32_t w[U], wn[U];
-#pragma unroll
-    for (int u = 0; u < U; u++) w[u] = load((uint64_t)u * nwaves + wv);
-    for (uint64_t b = 0; b * U * nwaves + wv < total; b++) {
-#pragma unroll
-        for (int u = 0; u < U; u++) wn[u] = load(((b + 1) * U + u) * nwaves + wv);
-#pragma unroll
-        for (int u = 0; u < U; u++) {
-            const uint64_t it = (b * U + u) * nwaves + wv;
-            if (it >= total) break;
-            const uint64_t j = it / chunks, i0 = (it - j * chunks) * 256;
-            const float l0 = lut[4 * j], l1 = lut[4 * j + 1], l2 = lut[4 * j + 2], l3 = lut[4 * j + 3];
-            const uint32_t src = __shfl(w[u], lane >> 2, kWave);
-            const uint32_t byte = (src >> (8 * (lane & 3))) & 0xffu;
-            const uint64_t i = i0 + 4 * lane;
-            f32x4_t v;
-            v.x = sel4(l0, l1, l2, l3, byte & 3u);
-            v.y = sel4(l0, l1, l2, l3, (byte >> 2) & 3u);
-            v.z = sel4(l0, l1, l2, l3, (byte >> 4) & 3u);
-            v.w = sel4(l0, l1, l2, l3, byte >> 6);
-            float* o = out + j * ld + i;
-            if (i + 4 <= n) {
-                store_nt(reinterpret_cast<f32x4_t*>(o), v);
-            } else {
-                for (int t = 0; t < 4; t++)
-                    if (i + t < n) o[t] = v[t];
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < U; u++) w[u] = wn[u];
-    }
-}
-
-// ubench: the sweep with 16 items per wave and batch, one load instruction per 4 items (lane l
-// fetches dword l&15 of item 4q + l/16), next batch prefetched (32 items = 32 KiB in flight per
-// wave); NOLOAD = store-only ablation of the same pattern
-template <bool NOLOAD>
-__global__ __launch_bounds__(kBlock) void k_decode_sweep16(const uint8_t* __restrict__ packed, uint64_t pitch, uint64_t n,
-                                                           uint64_t m, const float* __restrict__ lut,
-                                                           float* __restrict__ out, uint64_t ld) {
-    constexpr int U = 16, Q = U / 4;
-    const int lane = threadIdx.x & (kWave - 1);
-    const uint64_t chunks = (n + 255) / 256, total = chunks * m;
-    const uint64_t nwaves = (uint64_t)gridDim.x * (kBlock / kWave);
-    const uint64_t wv = (uint64_t)blockIdx.x * (kBlock / kWave) + threadIdx.x / kWave;
-    auto load = [&](uint64_t b, int q) -> uint32_t {
-        const uint64_t it = (b * U + 4 * q + (lane >> 4)) * nwaves + wv;
-        if (NOLOAD || it >= total) return (uint32_t)lane * 0x9E3779B9u;
-        const uint64_t j = it / chunks, c = it - j * chunks;
-        const int d = lane & 15;
-        return c * 256 + 16 * (uint64_t)d < n ? reinterpret_cast<const uint32_t*>(packed + j * pitch)[c * 16 + d] : 0u;
-    };
-    uint32_t w[Q], wn[Q];
-#pragma unroll
-    for (int q = 0; q < Q; q++) w[q] = load(0, q);
-    for (uint64_t b = 0; b * U * nwaves + wv < total; b++) {
-#pragma unroll
-        for (int q = 0; q < Q; q++) wn[q] = load(b + 1, q);
-#pragma unroll
-        for (int u = 0; u < U; u++) {
-            const uint64_t it = (b * U + u) * nwaves + wv;
-            if (it >= total) break;
-            const uint64_t j = it / chunks, i0 = (it - j * chunks) * 256;
-            const float l0 = lut[4 * j], l1 = lut[4 * j + 1], l2 = lut[4 * j + 2], l3 = lut[4 * j + 3];
-            const uint32_t src = __shfl(w[u >> 2], (u & 3) * 16 + (lane >> 2), kWave);
-            const uint32_t byte = (src >> (8 * (lane & 3))) & 0xffu;
-            const uint64_t i = i0 + 4 * lane;
-            f32x4_t v;
-            v.x = sel4(l0, l1, l2, l3, byte & 3u);
-            v.y = sel4(l0, l1, l2, l3, (byte >> 2) & 3u);
-            v.z = sel4(l0, l1, l2, l3, (byte >> 4) & 3u);
-            v.w = sel4(l0, l1, l2, l3, byte >> 6);
-            float* o = out + j * ld + i;
-            if (i + 4 <= n) {
-                store_nt(reinterpret_cast<f32x4_t*>(o), v);
-            } else {
-                for (int t = 0; t < 4; t++)
-                    if (i + t < n) o[t] = v[t];
-            }
-        }
-#pragma unroll
-        for (int q = 0; q < Q; q++) w[q] = wn[q];
-    }
-}
-
-// sweep16 without per-item divisions or dependent LUT loads: (column, chunk) of the wave's k-th
-// item advanced incrementally (item k+1 = item k + nwaves), the batch's 16 LUT rows fetched with
-// its codes (lane l: entry l&3 of item l>>2) and broadcast by v_readlane
-template <bool NOLOAD>
-__global__ __launch_bounds__(kBlock) void k_decode_sweep16b(const uint8_t* __restrict__ packed, uint64_t pitch,
-                                                            uint64_t n, uint64_t m, const float* __restrict__ lut,
-                                                            float* __restrict__ out, uint64_t ld) {
-    constexpr int U = 16, Q = U / 4;
-    const int lane = threadIdx.x & (kWave - 1);
-    const uint64_t chunks = (n + 255) / 256, total = chunks * m;
-    const uint64_t nwaves = (uint64_t)gridDim.x * (kBlock / kWave);
-    const uint64_t wv = (uint64_t)blockIdx.x * (kBlock / kWave) + threadIdx.x / kWave;
-    const uint64_t dj = nwaves / chunks, dc = nwaves - dj * chunks;              // one item step
-    const uint64_t bstep = U * nwaves, dJ = bstep / chunks, dC = bstep - dJ * chunks;  // one batch step
-    auto split = [&](uint64_t it, uint64_t& j, uint64_t& c) {
-        j = it / chunks;
-        c = it - j * chunks;
-    };
-    auto adv = [&](uint64_t& j, uint64_t& c, uint64_t aj, uint64_t ac) {
-        c += ac;
-        j += aj;
-        if (c >= chunks) {
-            c -= chunks;
-            j++;
-        }
-    };
-    // per-lane item states: codes (q: item 4q + lane/16 of the batch), LUT (item lane/4)
-    uint64_t jq[Q], cq[Q], jl, cl;
-#pragma unroll
-    for (int q = 0; q < Q; q++) split((uint64_t)(4 * q + (lane >> 4)) * nwaves + wv, jq[q], cq[q]);
-    split((uint64_t)(lane >> 2) * nwaves + wv, jl, cl);
-    const int d = lane & 15;
-    auto load_codes = [&](int q) -> uint32_t {
-        if (NOLOAD || jq[q] >= m) return (uint32_t)lane * 0x9E3779B9u;
-        return cq[q] * 256 + 16 * (uint64_t)d < n ? reinterpret_cast<const uint32_t*>(packed + jq[q] * pitch)[cq[q] * 16 + d]
-                                                  : 0u;
-    };
-    auto load_lut = [&]() -> float { return jl < m ? lut[4 * jl + (lane & 3)] : 0.0f; };
-    uint32_t w[Q], wn[Q];
-    float lv = load_lut(), lvn;
-#pragma unroll
-    for (int q = 0; q < Q; q++) w[q] = load_codes(q);
-    uint64_t js, cs;  // the wave's current item (uniform)
-    split(wv, js, cs);
-    for (uint64_t b = 0; b * bstep + wv < total; b++) {
-#pragma unroll
-        for (int q = 0; q < Q; q++) {
-            adv(jq[q], cq[q], dJ, dC);
-            wn[q] = load_codes(q);
-        }
-        adv(jl, cl, dJ, dC);
-        lvn = load_lut();
-#pragma unroll
-        for (int u = 0; u < U; u++) {
-            if (js >= m) break;
-            const float l0 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, lv), 4 * u));
-            const float l1 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, lv), 4 * u + 1));
-            const float l2 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, lv), 4 * u + 2));
-            const float l3 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, lv), 4 * u + 3));
-            const uint32_t src = __shfl(w[u >> 2], (u & 3) * 16 + (lane >> 2), kWave);
-            const uint32_t byte = (src >> (8 * (lane & 3))) & 0xffu;
-            const uint64_t i = cs * 256 + 4 * lane;
-            f32x4_t v;
-            v.x = sel4(l0, l1, l2, l3, byte & 3u);
-            v.y = sel4(l0, l1, l2, l3, (byte >> 2) & 3u);
-            v.z = sel4(l0, l1, l2, l3, (byte >> 4) & 3u);
-            v.w = sel4(l0, l1, l2, l3, byte >> 6);
-            float* o = out + js * ld + i;
-            if (i + 4 <= n) {
-                store_nt(reinterpret_cast<f32x4_t*>(o), v);
-            } else {
-                for (int t = 0; t < 4; t++)
-                    if (i + t < n) o[t] = v[t];
-            }
-            adv(js, cs, dj, dc);
-        }
-#pragma unroll
-        for (int q = 0; q < Q; q++) w[q] = wn[q];
-        lv = lvn;
-    }
-}
-
-// sweep, lean form: the wave's item state is wave-uniform (SGPRs via readfirstlane), each lane
-// loads its own code byte (64 lanes x 1 B = the item's 64 B, no shuffle), the item's LUT row is a
-// scalar load, U items per batch with the next batch's loads issued before this batch's stores
-template <bool NOLOAD, int U>
-__global__ __launch_bounds__(kBlock) void k_decode_sweepc(const uint8_t* __restrict__ packed, uint64_t pitch,
-                                                          uint64_t n, uint64_t m, const float* __restrict__ lut,
-                                                          float* __restrict__ out, uint64_t ld) {
-    const int lane = threadIdx.x & (kWave - 1);
-    const uint64_t chunks = (n + 255) / 256, total = chunks * m;
-    const uint64_t nwaves = (uint64_t)gridDim.x * (kBlock / kWave);
-    const uint64_t wv = (uint64_t)__builtin_amdgcn_readfirstlane(blockIdx.x * (kBlock / kWave) + threadIdx.x / kWave);
-    const uint64_t dj = nwaves / chunks, dc = nwaves - dj * chunks;
-    uint64_t jl = wv / chunks, cl = wv - jl * chunks, js = jl, cs = cl;
-    auto adv = [&](uint64_t& j, uint64_t& c) {
-        c += dc;
-        j += dj;
-        if (c >= chunks) {
-            c -= chunks;
-            j++;
-        }
-    };
-    uint32_t code[U], coden[U];
-    float4 L[U], Ln[U];
-    auto fetch = [&](uint32_t (&cd)[U], float4 (&lt)[U]) {
-#pragma unroll
-        for (int u = 0; u < U; u++) {
-            const bool ok = jl < m;
-            const uint64_t jj = ok ? jl : 0;
-            lt[u] = *reinterpret_cast<const float4*>(lut + 4 * jj);
-            if (NOLOAD) cd[u] = (uint32_t)lane * 37u;
-            else cd[u] = ok && cl * 256 + 4 * (uint64_t)lane < n ? packed[jj * pitch + cl * 64 + lane] : 0u;
-            adv(jl, cl);
-        }
-    };
-    fetch(code, L);
-    for (uint64_t k = 0; js < m; k += U) {
-        fetch(coden, Ln);
-#pragma unroll
-        for (int u = 0; u < U; u++) {
-            if (js >= m) break;
-            const uint32_t byte = code[u];
-            const uint64_t i = cs * 256 + 4 * lane;
-            f32x4_t v;
-            v.x = sel4(L[u].x, L[u].y, L[u].z, L[u].w, byte & 3u);
-            v.y = sel4(L[u].x, L[u].y, L[u].z, L[u].w, (byte >> 2) & 3u);
-            v.z = sel4(L[u].x, L[u].y, L[u].z, L[u].w, (byte >> 4) & 3u);
-            v.w = sel4(L[u].x, L[u].y, L[u].z, L[u].w, byte >> 6);
-            float* o = out + js * ld + i;
-            if (i + 4 <= n) {
-                store_nt(reinterpret_cast<f32x4_t*>(o), v);
-            } else {
-                for (int t = 0; t < 4; t++)
-                    if (i + t < n) o[t] = v[t];
-            }
-            adv(js, cs);
-        }
-#pragma unroll
-        for (int u = 0; u < U; u++) {
-            code[u] = coden[u];
-            L[u] = Ln[u];
-        }
-    }
-    (void)total;
-}
-
-// ubench (round 3b): the sweep with a DEEP code prefetch and the LUT in LDS.  The hipMemset fill
-// never waits on vmcnt, so its stores stay in flight without bound; a decode wave must wait vmcnt
-// for its code loads, and on gfx9 that counter also covers the wave's own earlier stores -- with
-// one batch of slack (the sweeps above) every wave stalls on its stores' completion, which a
-// narrow (1-4 waves per SIMD) grid cannot hide.  Here each wave keeps D items of code loads in
-// flight (a ring of D registers, item k's load issued right after item k-D's store), so the wait
-// for item k's codes covers only stores issued D items earlier; the LUT sits in LDS (lgkmcnt, not
-// vmcnt), the next item's LUT row is read one item ahead.  Items of 256 iids (1 KiB of output),
-// wave w takes items w, w + nwaves, ...: at any moment the grid writes one contiguous window.
-template <int D, bool NOLOAD>
-__global__ __launch_bounds__(kBlock) void k_decode_pf(const uint8_t* __restrict__ packed, uint64_t pitch,
-                                                      uint64_t n, uint64_t m, const float* __restrict__ lut,
-                                                      float* __restrict__ out, uint64_t ld) {
-    extern __shared__ float4 slut[];  // m rows
-    for (uint64_t j = threadIdx.x; j < m; j += kBlock) slut[j] = reinterpret_cast<const float4*>(lut)[j];
-    __syncthreads();
-    const int lane = threadIdx.x & (kWave - 1);
-    const uint64_t chunks = (n + 255) / 256;
-    const uint64_t nwaves = (uint64_t)gridDim.x * (kBlock / kWave);
-    const uint64_t wv = (uint64_t)__builtin_amdgcn_readfirstlane(blockIdx.x * (kBlock / kWave) + threadIdx.x / kWave);
-    const uint64_t dj = nwaves / chunks, dc = nwaves - dj * chunks;
-    uint64_t jl = wv / chunks, cl = wv - jl * chunks, js = jl, cs = cl;
-    auto adv = [&](uint64_t& j, uint64_t& c) {
-        c += dc;
-        j += dj;
-        if (c >= chunks) {
-            c -= chunks;
-            j++;
-        }
-    };
-    // unconditional loads: column clamped to m-1, byte c*64+lane < pitch always (pitch = 64 ceil(n/256))
-    auto fetch = [&]() -> uint32_t {
-        const uint64_t jj = jl < m ? jl : m - 1;
-        uint32_t v = NOLOAD ? (uint32_t)lane * 37u : (uint32_t)packed[jj * pitch + cl * 64 + lane];
-        adv(jl, cl);
-        return v;
-    };
-    uint32_t code[D];
-#pragma unroll
-    for (int u = 0; u < D; u++) code[u] = fetch();
-    float4 L = slut[js < m ? js : 0];
-    while (js < m) {
-#pragma unroll
-        for (int u = 0; u < D; u++) {
-            const bool act = js < m;  // wave-uniform; no break, so the ring unrolls into registers
-            const uint64_t jn = js + dj + (cs + dc >= chunks ? 1 : 0);
-            const float4 Ln = slut[jn < m ? jn : 0];
-            const uint32_t byte = code[u];
-            const uint64_t i = cs * 256 + 4 * lane;
-            f32x4_t v;
-            v.x = sel4(L.x, L.y, L.z, L.w, byte & 3u);
-            v.y = sel4(L.x, L.y, L.z, L.w, (byte >> 2) & 3u);
-            v.z = sel4(L.x, L.y, L.z, L.w, (byte >> 4) & 3u);
-            v.w = sel4(L.x, L.y, L.z, L.w, byte >> 6);
-            // branch-free store through a per-column buffer resource (num_records = the column's
-            // bytes, 0 past the last item): lanes past n are dropped by the range check, so every
-            // item issues exactly one store and the waitcnt pass counts it (n % 4 == 0 here)
-            const uint64_t ob = reinterpret_cast<uint64_t>(out + js * ld);
-            const uint32_t olo = __builtin_amdgcn_readfirstlane((uint32_t)ob), ohi = __builtin_amdgcn_readfirstlane((uint32_t)(ob >> 32));
-            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-                reinterpret_cast<void*>(((uint64_t)ohi << 32) | olo), (short)0, act ? (int)(n * 4) : 0, 0x00020000);
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v), rs, (int)(i * 4), 0, 2);
-            adv(js, cs);
-            code[u] = fetch();
-            L = Ln;
-        }
-    }
-}
-#endif
 
 // Fused stats + decode, one workgroup per SNP column (large N): pass 1 counts the codes
 // (packed column read once from HBM), the LUT is built in f64 by one lane, pass 2 re-reads
@@ -1469,10 +1073,8 @@ __device__ __forceinline__ void acc_stat(T x, double& n, double& s1, double& s2)
 
 template <typename T>
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t col_rsrc(T* p, uint64_t bytes) {
-    const uint64_t a = reinterpret_cast<uint64_t>(p);
-    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a), hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
-    return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uint64_t)hi << 32) | lo), (short)0,
-                                             (int)__builtin_amdgcn_readfirstlane((uint32_t)bytes), 0x00020000);
+    return __builtin_amdgcn_make_buffer_rsrc(sgpr_ptr(p), (short)0, (int)__builtin_amdgcn_readfirstlane((uint32_t)bytes),
+                                             0x00020000);
 }
 
 // F order, genotype-valued columns (0 / 1 / 2 / NaN -- a decoded .bed): one NT-thread workgroup per
@@ -2425,144 +2027,16 @@ void launch_decode(const uint8_t* packed, uint64_t pitch, uint64_t n, uint64_t m
         // 4 work items per wave; 8x more blocks than resident waves can hold (measured best)
         const uint64_t waves = ceil_div(ceil_div(n, 1024) * m, 4);
         const unsigned g = grid_for(waves, kBlock / kWave, 256 * 16 * 8);
-#ifdef SNPMI_UBENCH
-        if (dtype == SNPMI_DT_F32 && g_variant_decode >= 24 && g_variant_decode <= 27) {
-            // columns in stride-S order (S = 8 / 16 / 32 / 64) on the XCD-sliced item order
-            const unsigned g8 = (unsigned)round_up(g, 8);
-            const float* L = (const float*)lut;
-            float* O = (float*)out;
-            if (g_variant_decode == 24) k_decode_f<float, 4, 1, 8><<<g8, kBlock, 0, st>>>(packed, pitch, n, m, L, O, ld);
-            else if (g_variant_decode == 25) k_decode_f<float, 4, 1, 16><<<g8, kBlock, 0, st>>>(packed, pitch, n, m, L, O, ld);
-            else if (g_variant_decode == 26) k_decode_f<float, 4, 1, 32><<<g8, kBlock, 0, st>>>(packed, pitch, n, m, L, O, ld);
-            else k_decode_f<float, 4, 1, 64><<<g8, kBlock, 0, st>>>(packed, pitch, n, m, L, O, ld);
-            SNPMI_LAUNCH_CHECK();
-            return;
-        }
-        if (dtype == SNPMI_DT_F32 && g_variant_decode >= 80 && g_variant_decode <= 87 && m <= 8192 && n % 4 == 0 && n < (1ull << 29)) {
-            // deep-prefetch sweep k_decode_pf<D, NOLOAD> on G workgroups:
-            // 80 <16> 256, 81 <24> 256, 82 <16> 512, 83 store-only <16> 256, 84 <24> 512,
-            // 85 <8> 1024, 86 <24> 1024, 87 store-only <24> 512
-            const float* L = (const float*)lut;
-            float* O = (float*)out;
-            const int v = g_variant_decode;
-            const size_t sh = m * 16;
-            if (v == 80) k_decode_pf<16, false><<<256, kBlock, sh, st>>>(packed, pitch, n, m, L, O, ld);
-            else if (v == 81) k_decode_pf<24, false><<<256, kBlock, sh, st>>>(packed, pitch, n, m, L, O, ld);
-            else if (v == 82) k_decode_pf<16, false><<<512, kBlock, sh, st>>>(packed, pitch, n, m, L, O, ld);
-            else if (v == 83) k_decode_pf<16, true><<<256, kBlock, sh, st>>>(packed, pitch, n, m, L, O, ld);
-            else if (v == 84) k_decode_pf<24, false><<<512, kBlock, sh, st>>>(packed, pitch, n, m, L, O, ld);
-            else if (v == 85) k_decode_pf<8, false><<<1024, kBlock, sh, st>>>(packed, pitch, n, m, L, O, ld);
-            else if (v == 86) k_decode_pf<24, false><<<1024, kBlock, sh, st>>>(packed, pitch, n, m, L, O, ld);
-            else k_decode_pf<24, true><<<512, kBlock, sh, st>>>(packed, pitch, n, m, L, O, ld);
-            SNPMI_LAUNCH_CHECK();
-            return;
-        }
-        if (dtype == SNPMI_DT_F32 && g_variant_decode >= 70 && g_variant_decode <= 76) {
-            // 70/71: store-only sweepc on 256/1024 workgroups; 72-75: sweepc<8> on 256..2048; 76: sweepc<16> 512
-            const float* L = (const float*)lut;
-            float* O = (float*)out;
-            const int v = g_variant_decode;
-            if (v == 70) k_decode_sweepc<true, 8><<<256, kBlock, 0, st>>>(packed, pitch, n, m, L, O, ld);
-            else if (v == 71) k_decode_sweepc<true, 8><<<1024, kBlock, 0, st>>>(packed, pitch, n, m, L, O, ld);
-            else if (v == 76) k_decode_sweepc<false, 16><<<512, kBlock, 0, st>>>(packed, pitch, n, m, L, O, ld);
-            else k_decode_sweepc<false, 8><<<256u << (v - 72), kBlock, 0, st>>>(packed, pitch, n, m, L, O, ld);
-            SNPMI_LAUNCH_CHECK();
-            return;
-        }
-        if (dtype == SNPMI_DT_F32 && g_variant_decode >= 64 && g_variant_decode <= 69) {
-            // 64/65: store-only sweep16b on 256/1024 workgroups; 66-69: sweep16b on 256/512/1024/2048
-            const float* L = (const float*)lut;
-            float* O = (float*)out;
-            const int v = g_variant_decode;
-            if (v == 64) k_decode_sweep16b<true><<<256, kBlock, 0, st>>>(packed, pitch, n, m, L, O, ld);
-            else if (v == 65) k_decode_sweep16b<true><<<1024, kBlock, 0, st>>>(packed, pitch, n, m, L, O, ld);
-            else k_decode_sweep16b<false><<<256u << (v - 66), kBlock, 0, st>>>(packed, pitch, n, m, L, O, ld);
-            SNPMI_LAUNCH_CHECK();
-            return;
-        }
-        if (dtype == SNPMI_DT_F32 && g_variant_decode >= 58 && g_variant_decode <= 63) {
-            // 58/59: store-only sweep on 256/1024 workgroups; 60-63: sweep16 on 256/512/1024/2048
-            const float* L = (const float*)lut;
-            float* O = (float*)out;
-            const int v = g_variant_decode;
-            if (v == 58) k_decode_sweep16<true><<<256, kBlock, 0, st>>>(packed, pitch, n, m, L, O, ld);
-            else if (v == 59) k_decode_sweep16<true><<<1024, kBlock, 0, st>>>(packed, pitch, n, m, L, O, ld);
-            else k_decode_sweep16<false><<<256u << (v - 60), kBlock, 0, st>>>(packed, pitch, n, m, L, O, ld);
-            SNPMI_LAUNCH_CHECK();
-            return;
-        }
-        if (dtype == SNPMI_DT_F32 && g_variant_decode >= 50 && g_variant_decode <= 57) {
-            // hipMemset-shaped sweep (k_decode_sweep<U>) on G workgroups
-            const float* L = (const float*)lut;
-            float* O = (float*)out;
-            const int v = g_variant_decode;
-            const unsigned G = v == 50 || v == 53 ? 256 : v == 51 || v == 56 ? 512 : v == 52 || v == 54 ? 1024 : 2048;
-            if (v == 50 || v == 51 || v == 52) k_decode_sweep<4><<<G, kBlock, 0, st>>>(packed, pitch, n, m, L, O, ld);
-            else if (v == 53 || v == 56) k_decode_sweep<8><<<G, kBlock, 0, st>>>(packed, pitch, n, m, L, O, ld);
-            else k_decode_sweep<2><<<G, kBlock, 0, st>>>(packed, pitch, n, m, L, O, ld);
-            SNPMI_LAUNCH_CHECK();
-            return;
-        }
-        if (dtype == SNPMI_DT_F32 && g_variant_decode >= 40 && g_variant_decode <= 47) {
-            // write-window A/B (k_decode_fine<RN, U, ORD>)
-            const float* L = (const float*)lut;
-            float* O = (float*)out;
-            const int v = g_variant_decode;
-            const int rn = (v == 40 || v == 41 || v == 44 || v == 46) ? 1 : (v == 42 ? 2 : 4);
-            const int u = (v == 40 || v == 43 || v == 44) ? 1 : (v == 42 || v == 47) ? 2 : (v == 46 ? 8 : 4);
-            const uint64_t items = ceil_div(n, (uint64_t)rn * 256) * m;
-            const unsigned gg = (unsigned)round_up(grid_for(ceil_div(items, (uint64_t)u), kBlock / kWave, 256 * 16 * 8), 8);
-            if (v == 40) k_decode_fine<1, 1, 1><<<gg, kBlock, 0, st>>>(packed, pitch, n, m, L, O, ld);
-            else if (v == 41) k_decode_fine<1, 4, 1><<<gg, kBlock, 0, st>>>(packed, pitch, n, m, L, O, ld);
-            else if (v == 42) k_decode_fine<2, 2, 1><<<gg, kBlock, 0, st>>>(packed, pitch, n, m, L, O, ld);
-            else if (v == 43) k_decode_fine<4, 1, 1><<<gg, kBlock, 0, st>>>(packed, pitch, n, m, L, O, ld);
-            else if (v == 44) k_decode_fine<1, 1, 0><<<gg, kBlock, 0, st>>>(packed, pitch, n, m, L, O, ld);
-            else if (v == 45) k_decode_fine<4, 4, 0><<<gg, kBlock, 0, st>>>(packed, pitch, n, m, L, O, ld);
-            else if (v == 46) k_decode_fine<1, 8, 1><<<gg, kBlock, 0, st>>>(packed, pitch, n, m, L, O, ld);
-            else k_decode_fine<4, 2, 1><<<gg, kBlock, 0, st>>>(packed, pitch, n, m, L, O, ld);
-            SNPMI_LAUNCH_CHECK();
-            return;
-        }
-        if (dtype == SNPMI_DT_F32 && g_variant_decode >= 31 && g_variant_decode <= 35) {
-            // store cache policy on the shipped XCD-sliced order: 31 plain, 32 sc1, 33 sc0 sc1,
-            // 34 sc1 nt, 35 sc0 sc1 nt (21 = nt, shipped)
-            const unsigned g8 = (unsigned)round_up(g, 8);
-            const float* L = (const float*)lut;
-            float* O = (float*)out;
-            if (g_variant_decode == 31) k_decode_f<float, 4, 1, 0, 1><<<g8, kBlock, 0, st>>>(packed, pitch, n, m, L, O, ld);
-            else if (g_variant_decode == 32) k_decode_f<float, 4, 1, 0, 2><<<g8, kBlock, 0, st>>>(packed, pitch, n, m, L, O, ld);
-            else if (g_variant_decode == 33) k_decode_f<float, 4, 1, 0, 3><<<g8, kBlock, 0, st>>>(packed, pitch, n, m, L, O, ld);
-            else if (g_variant_decode == 34) k_decode_f<float, 4, 1, 0, 4><<<g8, kBlock, 0, st>>>(packed, pitch, n, m, L, O, ld);
-            else k_decode_f<float, 4, 1, 0, 5><<<g8, kBlock, 0, st>>>(packed, pitch, n, m, L, O, ld);
-            SNPMI_LAUNCH_CHECK();
-            return;
-        }
-        if (dtype == SNPMI_DT_F32 && g_variant_decode >= 20 && g_variant_decode <= 23) {
-            // A/B of the item order: 20 = plain grid order, 22 = column-interleaved items,
-            // 23 = store-only ablation (21 = the shipped XCD-sliced order)
-            if (g_variant_decode == 20)
-                k_decode_f<float, 4, 0><<<g, kBlock, 0, st>>>(packed, pitch, n, m, (const float*)lut, (float*)out, ld);
-            else if (g_variant_decode == 22)
-                k_decode_f<float, 4, 2><<<g, kBlock, 0, st>>>(packed, pitch, n, m, (const float*)lut, (float*)out, ld);
-            else if (g_variant_decode == 23)
-                k_decode_f<float, 4, 3><<<g, kBlock, 0, st>>>(packed, pitch, n, m, (const float*)lut, (float*)out, ld);
-            else
-                k_decode_f<float, 4, 1><<<round_up(g, 8), kBlock, 0, st>>>(packed, pitch, n, m, (const float*)lut,
-                                                                         (float*)out, ld);
-            SNPMI_LAUNCH_CHECK();
-            return;
-        }
-#endif
         // XCD-sliced item order (each XCD writes a contiguous 1/8 of every grid pass; the grid
         // is a multiple of 8 so the block permutation is a bijection): 0.712 vs 0.755 ms per
         // 2048-SNP block at 500k iids, mean over 12 output buffers on 2 boxes (profiles/r02q)
         const unsigned g8 = (unsigned)round_up(g, 8);
         if (dtype == SNPMI_DT_F32)
-            k_decode_f<float, 4, 1><<<g8, kBlock, 0, st>>>(packed, pitch, n, m, (const float*)lut, (float*)out, ld);
+            k_decode_f<float, 4><<<g8, kBlock, 0, st>>>(packed, pitch, n, m, (const float*)lut, (float*)out, ld);
         else if (dtype == SNPMI_DT_F64)
-            k_decode_f<double, 4, 1><<<g8, kBlock, 0, st>>>(packed, pitch, n, m, (const double*)lut, (double*)out, ld);
+            k_decode_f<double, 4><<<g8, kBlock, 0, st>>>(packed, pitch, n, m, (const double*)lut, (double*)out, ld);
         else
-            k_decode_f<int8_t, 4, 1><<<g8, kBlock, 0, st>>>(packed, pitch, n, m, (const int8_t*)lut, (int8_t*)out, ld);
+            k_decode_f<int8_t, 4><<<g8, kBlock, 0, st>>>(packed, pitch, n, m, (const int8_t*)lut, (int8_t*)out, ld);
     } else {
         if (dtype != SNPMI_DT_I8 && g_variant_decode != 2 && ld % (16 / dtype_size(dtype)) == 0 &&
             reinterpret_cast<uintptr_t>(out) % 16 == 0 && pitch % 64 == 0) {

@@ -51,6 +51,21 @@ int guarded(F&& body) {
     }
 }
 
+// ------------------------------------------------------------------ wave-uniform values
+// A 64-bit value (an address) made wave-uniform, i.e. moved to SGPRs.  __builtin_amdgcn_readfirstlane
+// takes and returns a 32-bit *int*: each half is widened through uint32_t here, because a cast of
+// the int straight to uint64_t sign-extends a low word whose bit 31 is set -- the cause of round 5's
+// illegal memory access (a SegFlush slot address, profiles/r05sub/README.md).  Every 64-bit value
+// built from readfirstlane goes through this helper (tests/test_sgpr_widening.py checks the sources).
+__device__ __forceinline__ uint64_t sgpr_u64(uint64_t v) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
+    return ((uint64_t)hi << 32) | (uint64_t)lo;
+}
+__device__ __forceinline__ void* sgpr_ptr(const void* p) {
+    return reinterpret_cast<void*>(sgpr_u64(reinterpret_cast<uint64_t>(p)));
+}
+
 // ------------------------------------------------------------------ geometry
 constexpr int kTile = 128;                      // GRM tile edge (iids)
 inline uint64_t ceil_div(uint64_t a, uint64_t b) { return (a + b - 1) / b; }

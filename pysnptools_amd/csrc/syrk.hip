@@ -768,9 +768,7 @@ struct SegFlush {
         slot = *sh;
         const int wave = threadIdx.x >> 6;
         float* base = c.scratch + (uint64_t)slot * kSegSlotFloats + (uint64_t)wave * (32 * 64 * 4);
-        const uint64_t b = reinterpret_cast<uint64_t>(base);
-        const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b), hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
-        rs = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uint64_t)hi << 32) | lo), 0, 32 * 64 * 16, 0x00020000);
+        rs = __builtin_amdgcn_make_buffer_rsrc(sgpr_ptr(base), 0, 32 * 64 * 16, 0x00020000);
         voff = (threadIdx.x & 63) * 4;
     }
     // call once per trip; true when the accumulators should be flushed now

@@ -177,9 +177,37 @@ __device__ __forceinline__ v2i lds_tr8(const uint8_t* p) {
     return __builtin_amdgcn_ds_read_tr8_b64_v2i32((__attribute__((address_space(3))) v2i*)p);
 }
 
+// acc mod p -> [0, p), one byte per element at its true (row, col) in the 256 x 256 block (a wave's
+// 128 x 64 = 4 x 2 tiles of v_mfma_i32_32x32x32_i8 accumulators, wave (wm, wn) of a 2 x 4 layout)
+__device__ __forceinline__ void crt_epilogue(const v16i (&acc)[4][2], uint32_t r, uint64_t nblk, uint64_t bx, int wm,
+                                             int wn, int lane, uint8_t* __restrict__ res) {
+    const int p = kMod[r];
+    const double invp = 1.0 / (double)p;
+    uint8_t* O = res + ((uint64_t)r * nblk + bx) * (BW * BW);
+    const int hh = lane >> 5, colp = 16 * ((lane >> 4) & 1) + pi16(lane & 15);
+#pragma unroll
+    for (int x = 0; x < 4; x++)
+#pragma unroll
+        for (int y = 0; y < 2; y++) {
+            uint8_t* bp = O + (wm * 128 + 32 * x + hh) * BW + wn * 64 + 32 * y + colp;
+#pragma unroll
+            for (int q = 0; q < 16; q++) {
+                const int v = acc[x][y][q];
+                int rr = v - p * (int)floor((double)v * invp);
+                rr += rr < 0 ? p : 0;
+                rr -= rr >= p ? p : 0;
+                bp[(16 * (q >> 3) + 4 * (q & 3) + 2 * ((q >> 2) & 1)) * BW] = (uint8_t)rr;
+            }
+        }
+}
+
 // ---------------------------------------------------------------- residue SYRK
-// grid: kR workgroups per block of this chunk (MAP below): block (bi, bj) = upper-triangle 256-block
-// b0 + bx (or slot b0 + bx of a cfg5 part's layout), modulus kMod[r].  8 waves (2 x 4), each 128 x 64 = 4 x 2 v_mfma_i32_32x32x32_i8 tiles.
+// Grid (1-D, round_up(nblk, 8) * kR workgroups): workgroup w runs on XCD w % 8; its kR consecutive
+// slots there are the kR moduli of block 8 (w / 8 / kR) + w % 8, so the workgroups an XCD holds at
+// once share their code panels in that XCD's L2 (FETCH 951 -> 149 GB per 62.5k-SNP launch at 50k
+// iids vs a (blocks, moduli) grid, profiles/r05m).  Block (bi, bj) = upper-triangle 256-block
+// b0 + bx (or slot b0 + bx of a cfg5 part's layout), modulus kMod[r].
+// 8 waves (2 x 4), each 128 x 64 = 4 x 2 v_mfma_i32_32x32x32_i8 tiles.
 // LDS: per stage and panel SKT SNP rows x 256 iids of int8 residues ([k][iid], RS-byte rows, the
 // 16 iids of a group in pi16 order as the loader's byte permutes leave them), double-buffered.
 // Loader: thread (panel lp, 16-iid group d, row block kq) expands SKT/16 consecutive SNP rows
@@ -188,24 +216,12 @@ __device__ __forceinline__ v2i lds_tr8(const uint8_t* p) {
 // ds_read_b64_tr_b8 of 8 SNP rows: within a 16-lane group, lane 2j+p addresses row j, bytes
 // 8p..8p+7 and receives column (its group-lane index) of the 8 rows (tools/probe/tr8_probe.hip).
 // Per 32-SNP k-step: the next k-step's fragments are read under this one's 8 MFMAs, and a
-// share of the next stage's rows is expanded and stored; one barrier per stage.
+// share of the next stage's rows is expanded and stored; one barrier per stage.  The loader runs
+// unconditionally (the last stage expands into the idle buffer, its code loads clamp to the last
+// stage) so each k-step's MFMAs and loader VALU share a basic block.
 // Epilogue: residue of each int32 sum, one byte per element, written as a dense 256 x 256 block
 // (true iid order) at res + (r * nblk + bx) * 65536.
-// ABL (ubench ablations, wrong results): 1 = no loader after the prologue, 2 = fragments read once
-// per stage (k-step 0) and reused by all four k-steps.
-// LDM 1: row-per-wave loader -- wave w expands rows 32(w&3)..+31 of panel w>>2, lane L the 4 iids
-// of LDS dword L (one code dword per lane, one v_perm), stored by ds_write_addtid_b32 (address =
-// M0 + 4 lane: 2 cycles per 256-B row vs 13 per ds_write_b128); the row's LUT word is uniform.
-// ST 1 (ubench variant 78): each 16-B residue row written as two volatile ds_write_b64 (6 cycles
-// per wave-instruction on the LDS transfer path) instead of one ds_write_b128 (13)
-// LD2 1 (ubench variant 79): two loader register sets, so each stage's code/LUT loads are issued
-// two stages before their expansion (a whole stage more latency to hide; +16 VGPRs)
-// STAG (round 5, ubench variants 83/84): the two waves of each SIMD (waves w and w + 4) take
-// complementary roles within a stage -- the "early" half expands and stores all of stage s+1's
-// residue rows during k-steps 0-1 (and issues stage s+2's code loads right after), then runs
-// k-steps 2-3 as pure MFMA; the other half runs k-steps 0-1 as pure MFMA and stores during 2-3.
-// 1: waves 4-7 early; 2: waves 0-3 early (MI355X_MICROARCH.md "Two waves per SIMD" item 9).
-template <int SKT, int ABL = 0, int LDM = 0, int ST = 0, int LD2 = 0, int STAG = 0, int MAP = 0>
+template <int SKT>
 __global__ __launch_bounds__(512, 1) void k_syrk_i8r(const uint8_t* __restrict__ P, uint64_t pitch, uint64_t kdim,
                                                      uint64_t mpad, const uint32_t* __restrict__ lutr,
                                                      const int* __restrict__ ctl, uint64_t b0, uint64_t nblk,
@@ -214,26 +230,9 @@ __global__ __launch_bounds__(512, 1) void k_syrk_i8r(const uint8_t* __restrict__
     constexpr int KS = SKT / 32, RPT = SKT / 16, PNL = SKT * RS, STG = 2 * PNL;
     __shared__ __attribute__((aligned(16))) uint8_t lds[2 * STG];
     if (ctl[1]) return;  // non-finite LUT: the f64 MFMA kernel runs instead
-    // MAP 0: grid (blocks, moduli), block-fastest.  MAP 1 (1-D grid of round_up(nblk, 8) * kR):
-    // workgroup w runs on XCD w % 8; its kR consecutive slots there are the kR moduli of block
-    // 8 (w / 8 / kR) + w % 8, so the workgroups an XCD holds at once share their code panels in
-    // that XCD's L2
-    uint32_t r, bx;
-    if constexpr (MAP == 1) {
-        const uint32_t w = blockIdx.x, q = w >> 3, u = q / kR;
-        r = q - u * kR;
-        bx = 8 * u + (w & 7);
-        if (bx >= nblk) return;
-    } else if constexpr (MAP == 2) {  // ubench: 2 kR consecutive slots of an XCD = blocks 2p, 2p+1 (one
-        // column: they share the j panel) x kR moduli, so both blocks stream their panels in step
-        const uint32_t w = blockIdx.x, q = w >> 3, u = q / (2 * kR), j = q - u * (2 * kR), h = j / kR;
-        r = j - h * kR;
-        bx = 2 * (8 * u + (w & 7)) + h;
-        if (bx >= nblk) return;
-    } else {
-        r = blockIdx.y;
-        bx = blockIdx.x;
-    }
+    const uint32_t w = blockIdx.x, q = w >> 3, u = q / kR;
+    const uint32_t r = q - u * kR, bx = 8 * u + (w & 7);
+    if (bx >= nblk) return;
     if ((int)r >= ctl[2]) return;  // K_int fits the first ctl[2] moduli
     const uint32_t* lr = lutr + (uint64_t)r * mpad;
     uint32_t bi, bj;
@@ -265,275 +264,19 @@ __global__ __launch_bounds__(512, 1) void k_syrk_i8r(const uint8_t* __restrict__
         for (int y = 0; y < 2; y++) acc[x][y] = (v16i){};
     const uint64_t nst = (kdim + SKT - 1) / SKT;
 
-    uint32_t cw[RPT], cw2[LD2 ? RPT : 1];
-    uint4 cl[RPT / 4], cl2[LD2 ? RPT / 4 : 1];
-    auto load_into = [&](uint64_t st, uint32_t* w, uint4* l) {
+    uint32_t cw[RPT];
+    uint4 cl[RPT / 4];
+    auto load = [&](uint64_t st) {
         const uint8_t* sb = pbase + st * SKT * pitch;
         const uint32_t lim = (uint32_t)(kdim - 1 - st * SKT);  // st < nst: >= 0
 #pragma unroll
         for (int h = 0; h < RPT; h++) {
             const uint32_t row = min((uint32_t)(RPT * kq + h), lim);
-            w[h] = *reinterpret_cast<const uint32_t*>(sb + (row * pit + 4 * d));
-        }
-#pragma unroll
-        for (int u = 0; u < RPT / 4; u++)  // lutr is zero-padded to mpad >= nst * SKT
-            l[u] = *reinterpret_cast<const uint4*>(lq + SKT * st + 4 * u);
-    };
-    auto load = [&](uint64_t st) { load_into(st, cw, cl); };
-    auto store_from = [&](uint8_t* S, int h0, int h1, const uint32_t* cw, const uint4* cl) {
-#pragma unroll
-        for (int h = h0; h < h1; h++) {
-            const uint4 c4 = cl[h >> 2];
-            const uint32_t L = (h & 3) == 0 ? c4.x : (h & 3) == 1 ? c4.y : (h & 3) == 2 ? c4.z : c4.w;
-            uint4 o;
-            o.x = __builtin_amdgcn_perm(L, L, cw[h] & 0x03030303u);
-            o.y = __builtin_amdgcn_perm(L, L, (cw[h] >> 2) & 0x03030303u);
-            o.z = __builtin_amdgcn_perm(L, L, (cw[h] >> 4) & 0x03030303u);
-            o.w = __builtin_amdgcn_perm(L, L, (cw[h] >> 6) & 0x03030303u);
-            if constexpr (ST == 1) {
-                typedef __attribute__((address_space(3))) volatile uint64_t lds_u64;
-                lds_u64* q = (lds_u64*)(S + lp * PNL + (RPT * kq + h) * RS + 16 * d);
-                q[0] = (uint64_t)o.x | ((uint64_t)o.y << 32);
-                q[1] = (uint64_t)o.z | ((uint64_t)o.w << 32);
-            } else {
-                *reinterpret_cast<uint4*>(S + lp * PNL + (RPT * kq + h) * RS + 16 * d) = o;
-            }
-        }
-    };
-    auto store = [&](uint8_t* S, int h0, int h1) { store_from(S, h0, h1, cw, cl); };
-    auto frag = [&](const uint8_t* S, int panel, int ks, int col) -> v4i {
-        const uint8_t* b = S + panel * PNL + 32 * ks * RS + rd + col;
-        const v2i x = lds_tr8(b), y = lds_tr8(b + 8 * RS);
-        return (v4i){x.x, x.y, y.x, y.y};
-    };
-    auto frags = [&](const uint8_t* S, int ks, v4i (&A)[4], v4i (&B)[2]) {
-#pragma unroll
-        for (int x = 0; x < 4; x++) A[x] = frag(S, 0, ks, wm * 128 + 32 * x);
-#pragma unroll
-        for (int y = 0; y < 2; y++) B[y] = frag(S, 1, ks, wn * 64 + 32 * y);
-    };
-
-    // LDM 1 state
-    constexpr int RPW = SKT / 4;  // rows per wave per stage (2 panels x SKT rows / 8 waves)
-    const int wq = __builtin_amdgcn_readfirstlane(wave & 3), lpw = __builtin_amdgcn_readfirstlane(wave >> 2);
-    const uint8_t* pbu = P + (lpw ? j0 : i0) / 4;  // wave-uniform
-    const uint32_t loff = 4 * (lane >> 2), sh1 = 2 * (lane & 3);
-    uint32_t cwa[LDM == 1 ? RPW : 1], lutv = 0;
-    auto load1 = [&](uint64_t st) {
-        // 32-bit row numbers (kdim <= crt_max_snps()): gfx950 has no 64-bit scalar compare; the
-        // code loads are raw buffer loads off a wave-uniform stage base, row offset in SGPR
-        // (clamped to the block's last SNP), lane offset in VGPR
-        const uint32_t r0 = (uint32_t)st * SKT + RPW * wq, lim = (uint32_t)kdim - 1 - (uint32_t)st * SKT;
-        lutv = lr[r0 + (lane & (RPW - 1))];  // lane i < RPW: LUT word of row i (zero-padded to mpad)
-        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-            const_cast<uint8_t*>(pbu + st * SKT * pitch), (short)0, (int)0x7ffffff0, 0x00020000);
-#pragma unroll
-        for (int i = 0; i < RPW; i++) {
-            const uint32_t row = min((uint32_t)(RPW * wq + i), lim);
-            cwa[i] = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)loff, (int)(row * (uint32_t)pitch), 0);
-        }
-    };
-    auto store1 = [&](uint8_t* S, int i0_, int i1_) {
-        const uint32_t base = (uint32_t)(uintptr_t)(S + lpw * PNL + RPW * wq * RS);
-#pragma unroll
-        for (int i = i0_; i < i1_; i++) {
-            const uint32_t L = __builtin_amdgcn_readlane(lutv, i);
-            const uint32_t v = __builtin_amdgcn_perm(L, L, (cwa[i] >> sh1) & 0x03030303u);
-            asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tds_write_addtid_b32 %1" ::"s"(base + i * RS), "v"(v)
-                         : "memory", "m0");
-        }
-    };
-
-    if constexpr (LD2 == 1) {
-        // invariant: during stage s the set holding stage s+1 is expanded into the idle buffer,
-        // then refilled with stage s+3 (clamped); the other set already holds stage s+2
-        load(0);
-        store(lds, 0, RPT);
-        load_into(nst > 1 ? 1 : 0, cw2, cl2);
-        load_into(nst > 2 ? 2 : nst - 1, cw, cl);
-        __syncthreads();
-        auto body = [&](uint64_t s, uint32_t* w, uint4* l) {
-            const uint8_t* cur = lds + (s & 1) * STG;
-            uint8_t* nxt = lds + ((s + 1) & 1) * STG;
-            v4i a[2][4], b[2][2];
-            frags(cur, 0, a[0], b[0]);
-#pragma unroll
-            for (int ks = 0; ks < KS; ks++) {
-                if (ks + 1 < KS) frags(cur, ks + 1, a[(ks + 1) & 1], b[(ks + 1) & 1]);
-#pragma unroll
-                for (int x = 0; x < 4; x++)
-#pragma unroll
-                    for (int y = 0; y < 2; y++)
-                        acc[x][y] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[ks & 1][x], b[ks & 1][y], acc[x][y], 0, 0, 0);
-                store_from(nxt, ks * RPT / KS, (ks + 1) * RPT / KS, w, l);
-            }
-            load_into(s + 3 < nst ? s + 3 : nst - 1, w, l);
-            __syncthreads();
-        };
-        for (uint64_t s = 0; s < nst; s += 2) {
-            body(s, cw2, cl2);
-            if (s + 1 < nst) body(s + 1, cw, cl);
-        }
-    }
-    if constexpr (LD2 == 0) {  // one loader register set: stage s+2's loads issued at the end of stage s
-    if constexpr (LDM == 1) {
-        load1(0);
-        store1(lds, 0, RPW);
-        load1(nst > 1 ? 1 : 0);
-    } else {
-        load(0);
-        store(lds, 0, RPT);
-        load(nst > 1 ? 1 : 0);
-    }
-    __syncthreads();
-    const bool early = STAG == 1 ? wave >= 4 : wave < 4;  // wave-uniform
-    for (uint64_t s = 0; s < nst && STAG != 0; s++) {
-        const uint8_t* cur = lds + (s & 1) * STG;
-        uint8_t* nxt = lds + ((s + 1) & 1) * STG;
-        v4i a[2][4], b[2][2];
-        frags(cur, 0, a[0], b[0]);
-        constexpr int H = KS / 2, RH = RPT / H;  // k-steps per half, rows stored per k-step
-        if (early) {
-#pragma unroll
-            for (int ks = 0; ks < KS; ks++) {
-                if (ks + 1 < KS) frags(cur, ks + 1, a[(ks + 1) & 1], b[(ks + 1) & 1]);
-#pragma unroll
-                for (int x = 0; x < 4; x++)
-#pragma unroll
-                    for (int y = 0; y < 2; y++)
-                        acc[x][y] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[ks & 1][x], b[ks & 1][y], acc[x][y], 0, 0, 0);
-                if (ks < H) store(nxt, ks * RH, (ks + 1) * RH);
-                if (ks == H - 1) load(s + 2 < nst ? s + 2 : nst - 1);
-            }
-        } else {
-#pragma unroll
-            for (int ks = 0; ks < KS; ks++) {
-                if (ks + 1 < KS) frags(cur, ks + 1, a[(ks + 1) & 1], b[(ks + 1) & 1]);
-#pragma unroll
-                for (int x = 0; x < 4; x++)
-#pragma unroll
-                    for (int y = 0; y < 2; y++)
-                        acc[x][y] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[ks & 1][x], b[ks & 1][y], acc[x][y], 0, 0, 0);
-                if (ks >= H) store(nxt, (ks - H) * RH, (ks - H + 1) * RH);
-            }
-            load(s + 2 < nst ? s + 2 : nst - 1);
-        }
-        __syncthreads();
-    }
-    for (uint64_t s = 0; s < nst && STAG == 0; s++) {
-        const uint8_t* cur = lds + (s & 1) * STG;
-        uint8_t* nxt = lds + ((s + 1) & 1) * STG;
-        v4i a[2][4], b[2][2];
-        frags(cur, 0, a[0], b[0]);
-        // the loader runs unconditionally (the last stage expands into the idle buffer, its code
-        // loads clamp to the last stage) so each k-step's MFMAs and loader VALU share a basic block
-#pragma unroll
-        for (int ks = 0; ks < KS; ks++) {
-            if constexpr (ABL == 2) {
-                if (ks + 1 < KS) {
-#pragma unroll
-                    for (int x = 0; x < 4; x++) a[(ks + 1) & 1][x] = a[ks & 1][x];
-#pragma unroll
-                    for (int y = 0; y < 2; y++) b[(ks + 1) & 1][y] = b[ks & 1][y];
-                }
-            } else if (ks + 1 < KS) {
-                frags(cur, ks + 1, a[(ks + 1) & 1], b[(ks + 1) & 1]);
-            }
-#pragma unroll
-            for (int x = 0; x < 4; x++)
-#pragma unroll
-                for (int y = 0; y < 2; y++)
-                    acc[x][y] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[ks & 1][x], b[ks & 1][y], acc[x][y], 0, 0, 0);
-            if constexpr (ABL != 1) {
-                if constexpr (LDM == 1) store1(nxt, ks * RPW / KS, (ks + 1) * RPW / KS);
-                else store(nxt, ks * RPT / KS, (ks + 1) * RPT / KS);
-            }
-        }
-        if constexpr (ABL != 1) {
-            if constexpr (LDM == 1) load1(s + 2 < nst ? s + 2 : nst - 1);
-            else load(s + 2 < nst ? s + 2 : nst - 1);
-        }
-        __syncthreads();
-    }
-    }  // LD2 == 0
-    // epilogue: acc mod p -> [0, p), one byte per element at its true (row, col) in the block
-    const int p = kMod[r];
-    const double invp = 1.0 / (double)p;
-    uint8_t* O = res + ((uint64_t)r * nblk + bx) * (BW * BW);
-    const int hh = lane >> 5, colp = 16 * ((lane >> 4) & 1) + pi16(lane & 15);
-#pragma unroll
-    for (int x = 0; x < 4; x++)
-#pragma unroll
-        for (int y = 0; y < 2; y++) {
-            uint8_t* bp = O + (wm * 128 + 32 * x + hh) * BW + wn * 64 + 32 * y + colp;
-#pragma unroll
-            for (int q = 0; q < 16; q++) {
-                const int v = acc[x][y][q];
-                int rr = v - p * (int)floor((double)v * invp);
-                rr += rr < 0 ? p : 0;
-                rr -= rr >= p ? p : 0;
-                bp[(16 * (q >> 3) + 4 * (q & 3) + 2 * ((q >> 2) & 1)) * BW] = (uint8_t)rr;
-            }
-        }
-}
-
-#ifdef SNPMI_UBENCH
-// Ring form (round 5, ubench variants 80-82; LOST: 777-783 ms vs 721 ms for k_syrk_i8r at 50k x
-// 62.5k, profiles/r05e/ubench_crt_ring.jsonl -- the barrier every 64 SNPs costs more than the
-// hidden post-barrier fragment reads save; s_setprio on waves 4-7 changes nothing): a ring of 4 LDS slots of 64 SNPs (4 x 36 KiB = 144 KiB), stage s+2's
-// residue rows expanded and stored while stage s is multiplied, one barrier per 64-SNP stage.
-// Because a slot is complete one full stage before it is read, each wave reads the NEXT stage's
-// first fragments before the barrier (PF): the post-barrier fragment-read latency that the
-// two-slot form exposes at the head of every 128-SNP stage is hidden under the barrier wait.
-// PRIO: s_setprio 1 on waves 4-7 (the later-dispatched partner of each SIMD pair) for the loop.
-template <int PF = 1, int PRIO = 0>
-__global__ __launch_bounds__(512, 1) void k_syrk_i8q(const uint8_t* __restrict__ P, uint64_t pitch, uint64_t kdim,
-                                                     uint64_t mpad, const uint32_t* __restrict__ lutr,
-                                                     const int* __restrict__ ctl, uint64_t b0, uint64_t nblk,
-                                                     uint8_t* __restrict__ res,
-                                                     const uint32_t* __restrict__ part_tab = nullptr) {
-    constexpr int SKT = 64, KS = SKT / 32, RPT = SKT / 16, PNL = SKT * RS, STG = 2 * PNL, NSLOT = 4;
-    __shared__ __attribute__((aligned(16))) uint8_t lds[NSLOT * STG];
-    if (ctl[1]) return;  // non-finite LUT: the f64 MFMA kernel runs instead
-    const int r = blockIdx.y;
-    if (r >= ctl[2]) return;  // K_int fits the first ctl[2] moduli
-    const uint32_t* lr = lutr + (uint64_t)r * mpad;
-    uint32_t bi, bj;
-    if (part_tab) {
-        const uint32_t c = part_tab[b0 + blockIdx.x];
-        bi = c & 0xffffu;
-        bj = c >> 16;
-    } else {
-        tile_coords(b0 + blockIdx.x, bi, bj);
-    }
-    const uint64_t i0 = (uint64_t)bi * BW, j0 = (uint64_t)bj * BW;
-    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-    const int wm = wave >> 2, wn = wave & 3;
-    const int lp = __builtin_amdgcn_readfirstlane(t >> 8), kq = (t >> 4) & 15, d = t & 15;
-    const uint8_t* pbase = P + (lp ? j0 : i0) / 4;
-    const uint32_t pit = (uint32_t)pitch;
-    const uint32_t* lq = lr + RPT * kq;
-    const int g = lane >> 4, jj = (lane & 15) >> 1, pp = lane & 1;
-    const int rd = (16 * (g >> 1) + jj) * RS + 16 * (g & 1) + 8 * pp;
-
-    v16i acc[4][2];
-#pragma unroll
-    for (int x = 0; x < 4; x++)
-#pragma unroll
-        for (int y = 0; y < 2; y++) acc[x][y] = (v16i){};
-    const uint64_t nst = (kdim + SKT - 1) / SKT;
-    uint32_t cw[RPT];
-    uint4 cl[RPT / 4];
-    auto load = [&](uint64_t st) {  // st < nst
-        const uint8_t* sb = pbase + st * SKT * pitch;
-        const uint32_t lim = (uint32_t)(kdim - 1 - st * SKT);
-#pragma unroll
-        for (int h = 0; h < RPT; h++) {
-            const uint32_t row = min((uint32_t)(RPT * kq + h), lim);
             cw[h] = *reinterpret_cast<const uint32_t*>(sb + (row * pit + 4 * d));
         }
 #pragma unroll
-        for (int u = 0; u < RPT / 4; u++) cl[u] = *reinterpret_cast<const uint4*>(lq + SKT * st + 4 * u);
+        for (int v = 0; v < RPT / 4; v++)  // lutr is zero-padded to mpad >= nst * SKT
+            cl[v] = *reinterpret_cast<const uint4*>(lq + SKT * st + 4 * v);
     };
     auto store = [&](uint8_t* S, int h0, int h1) {
 #pragma unroll
@@ -559,397 +302,15 @@ __global__ __launch_bounds__(512, 1) void k_syrk_i8q(const uint8_t* __restrict__
 #pragma unroll
         for (int y = 0; y < 2; y++) B[y] = frag(S, 1, ks, wn * 64 + 32 * y);
     };
-    auto slot = [&](uint64_t st) { return lds + (st & (NSLOT - 1)) * STG; };
-    // prologue: stages 0 and 1 stored, stage 2's codes in registers
-    load(0);
-    store(slot(0), 0, RPT);
-    load(nst > 1 ? 1 : 0);
-    store(slot(1), 0, RPT);
-    load(nst > 2 ? 2 : nst - 1);
-    __syncthreads();
-    if constexpr (PRIO) {
-        if (wave >= 4) __builtin_amdgcn_s_setprio(1);
-    }
-    v4i a[2][4], b[2][2];
-    frags(slot(0), 0, a[0], b[0]);
-    for (uint64_t s = 0; s < nst; s++) {
-        const uint8_t* cur = slot(s);
-        uint8_t* nxt = slot(s + 2);  // stage s+2 (read two stages from now; its slot was last read in stage s-2)
-#pragma unroll
-        for (int ks = 0; ks < KS; ks++) {
-            const int q = (ks + 1) & 1;
-            if (ks + 1 < KS) {
-                frags(cur, ks + 1, a[q], b[q]);
-            } else if constexpr (PF) {
-                // stage s+1 was stored during stage s-1: complete since the last barrier
-                frags(slot(s + 1), 0, a[q], b[q]);
-            }
-#pragma unroll
-            for (int x = 0; x < 4; x++)
-#pragma unroll
-                for (int y = 0; y < 2; y++)
-                    acc[x][y] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[ks & 1][x], b[ks & 1][y], acc[x][y], 0, 0, 0);
-            store(nxt, ks * RPT / KS, (ks + 1) * RPT / KS);
-        }
-        load(s + 3 < nst ? s + 3 : nst - 1);
-        __syncthreads();
-        if constexpr (!PF) frags(slot(s + 1), 0, a[0], b[0]);
-    }
-    if constexpr (PRIO) {
-        if (wave >= 4) __builtin_amdgcn_s_setprio(0);
-    }
-    const int p = kMod[r];
-    const double invp = 1.0 / (double)p;
-    uint8_t* O = res + ((uint64_t)r * nblk + blockIdx.x) * (BW * BW);
-    const int hh = lane >> 5, colp = 16 * ((lane >> 4) & 1) + pi16(lane & 15);
-#pragma unroll
-    for (int x = 0; x < 4; x++)
-#pragma unroll
-        for (int y = 0; y < 2; y++) {
-            uint8_t* bp = O + (wm * 128 + 32 * x + hh) * BW + wn * 64 + 32 * y + colp;
-#pragma unroll
-            for (int q = 0; q < 16; q++) {
-                const int v = acc[x][y][q];
-                int rr = v - p * (int)floor((double)v * invp);
-                rr += rr < 0 ? p : 0;
-                rr -= rr >= p ? p : 0;
-                bp[(16 * (q >> 3) + 4 * (q & 3) + 2 * ((q >> 2) & 1)) * BW] = (uint8_t)rr;
-            }
-        }
-}
 
-// ubench (variant 86; LOST: 761 vs 726 ms at 50k x 62.5k, K bit-identical, profiles/r05k): k_syrk_i8r with 16 waves (4 per SIMD), 64 x 64 per wave (2 x 2 tiles, 64
-// accumulator registers): more waves to hide the LDS-read and barrier latencies, at a third more
-// fragment bytes per MFMA (1 KiB instead of 0.75).  Same LDS image, stages, barrier and loader
-// (4 rows per thread per stage).
-template <int MAP = 0>
-__global__ __launch_bounds__(1024, 1) void k_syrk_i8h(const uint8_t* __restrict__ P, uint64_t pitch, uint64_t kdim,
-                                                      uint64_t mpad, const uint32_t* __restrict__ lutr,
-                                                      const int* __restrict__ ctl, uint64_t b0, uint64_t nblk,
-                                                      uint8_t* __restrict__ res,
-                                                      const uint32_t* __restrict__ part_tab = nullptr) {
-    constexpr int SKT = SK, KS = SKT / 32, RPT = SKT / 32, PNL = SKT * RS, STG = 2 * PNL;
-    __shared__ __attribute__((aligned(16))) uint8_t lds[2 * STG];
-    if (ctl[1]) return;
-    uint32_t r, bx;  // MAP as in k_syrk_i8r
-    if constexpr (MAP == 1) {
-        const uint32_t w = blockIdx.x, q = w >> 3, u = q / kR;
-        r = q - u * kR;
-        bx = 8 * u + (w & 7);
-        if (bx >= nblk) return;
-    } else {
-        r = blockIdx.y;
-        bx = blockIdx.x;
-    }
-    if ((int)r >= ctl[2]) return;
-    const uint32_t* lr = lutr + (uint64_t)r * mpad;
-    uint32_t bi, bj;
-    if (part_tab) {
-        const uint32_t c = part_tab[b0 + bx];
-        bi = c & 0xffffu;
-        bj = c >> 16;
-    } else {
-        tile_coords(b0 + bx, bi, bj);
-    }
-    const uint64_t i0 = (uint64_t)bi * BW, j0 = (uint64_t)bj * BW;
-    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-    const int wm = wave >> 2, wn = wave & 3;
-    const int lp = __builtin_amdgcn_readfirstlane(t >> 9), kq = (t >> 4) & 31, d = t & 15;
-    const uint8_t* pbase = P + (lp ? j0 : i0) / 4;
-    const uint32_t pit = (uint32_t)pitch;
-    const uint32_t* lq = lr + RPT * kq;
-    const int g = lane >> 4, jj = (lane & 15) >> 1, pp = lane & 1;
-    const int rd = (16 * (g >> 1) + jj) * RS + 16 * (g & 1) + 8 * pp;
-
-    v16i acc[2][2];
-#pragma unroll
-    for (int x = 0; x < 2; x++)
-#pragma unroll
-        for (int y = 0; y < 2; y++) acc[x][y] = (v16i){};
-    const uint64_t nst = (kdim + SKT - 1) / SKT;
-    uint32_t cw[RPT];
-    uint4 cl;
-    auto load = [&](uint64_t st) {
-        const uint8_t* sb = pbase + st * SKT * pitch;
-        const uint32_t lim = (uint32_t)(kdim - 1 - st * SKT);
-#pragma unroll
-        for (int h = 0; h < RPT; h++) {
-            const uint32_t row = min((uint32_t)(RPT * kq + h), lim);
-            cw[h] = *reinterpret_cast<const uint32_t*>(sb + (row * pit + 4 * d));
-        }
-        cl = *reinterpret_cast<const uint4*>(lq + SKT * st);
-    };
-    auto store = [&](uint8_t* S, int h) {
-        const uint32_t L = h == 0 ? cl.x : h == 1 ? cl.y : h == 2 ? cl.z : cl.w;
-        uint4 o;
-        o.x = __builtin_amdgcn_perm(L, L, cw[h] & 0x03030303u);
-        o.y = __builtin_amdgcn_perm(L, L, (cw[h] >> 2) & 0x03030303u);
-        o.z = __builtin_amdgcn_perm(L, L, (cw[h] >> 4) & 0x03030303u);
-        o.w = __builtin_amdgcn_perm(L, L, (cw[h] >> 6) & 0x03030303u);
-        *reinterpret_cast<uint4*>(S + lp * PNL + (RPT * kq + h) * RS + 16 * d) = o;
-    };
-    auto frag = [&](const uint8_t* S, int panel, int ks, int col) -> v4i {
-        const uint8_t* b = S + panel * PNL + 32 * ks * RS + rd + col;
-        const v2i x = lds_tr8(b), y = lds_tr8(b + 8 * RS);
-        return (v4i){x.x, x.y, y.x, y.y};
-    };
-    auto frags = [&](const uint8_t* S, int ks, v4i (&A)[2], v4i (&B)[2]) {
-#pragma unroll
-        for (int x = 0; x < 2; x++) A[x] = frag(S, 0, ks, wm * 64 + 32 * x);
-#pragma unroll
-        for (int y = 0; y < 2; y++) B[y] = frag(S, 1, ks, wn * 64 + 32 * y);
-    };
-    load(0);
-#pragma unroll
-    for (int h = 0; h < RPT; h++) store(lds, h);
-    load(nst > 1 ? 1 : 0);
-    __syncthreads();
-    for (uint64_t s = 0; s < nst; s++) {
-        const uint8_t* cur = lds + (s & 1) * STG;
-        uint8_t* nxt = lds + ((s + 1) & 1) * STG;
-        v4i a[2][2], b[2][2];
-        frags(cur, 0, a[0], b[0]);
-#pragma unroll
-        for (int ks = 0; ks < KS; ks++) {
-            if (ks + 1 < KS) frags(cur, ks + 1, a[(ks + 1) & 1], b[(ks + 1) & 1]);
-#pragma unroll
-            for (int x = 0; x < 2; x++)
-#pragma unroll
-                for (int y = 0; y < 2; y++)
-                    acc[x][y] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[ks & 1][x], b[ks & 1][y], acc[x][y], 0, 0, 0);
-            store(nxt, ks);  // KS == RPT: one row per k-step
-        }
-        load(s + 2 < nst ? s + 2 : nst - 1);
-        __syncthreads();
-    }
-    const int p = kMod[r];
-    const double invp = 1.0 / (double)p;
-    uint8_t* O = res + ((uint64_t)r * nblk + bx) * (BW * BW);
-    const int hh = lane >> 5, colp = 16 * ((lane >> 4) & 1) + pi16(lane & 15);
-#pragma unroll
-    for (int x = 0; x < 2; x++)
-#pragma unroll
-        for (int y = 0; y < 2; y++) {
-            uint8_t* bp = O + (wm * 64 + 32 * x + hh) * BW + wn * 64 + 32 * y + colp;
-#pragma unroll
-            for (int q = 0; q < 16; q++) {
-                const int v = acc[x][y][q];
-                int rr = v - p * (int)floor((double)v * invp);
-                rr += rr < 0 ? p : 0;
-                rr -= rr >= p ? p : 0;
-                bp[(16 * (q >> 3) + 4 * (q & 3) + 2 * ((q >> 2) & 1)) * BW] = (uint8_t)rr;
-            }
-        }
-}
-
-// ubench (variant 85; LOST: 761 vs 720 ms at 50k x 62.5k, K bit-identical, profiles/r05i): k_syrk_i8r on v_mfma_i32_16x16x64_i8 -- the same MACs per cycle, the same
-// LDS image and fragment bytes per MAC, but the chip may hold a higher clock on the 16x16 shape
-// under load (MI355X_MICROARCH.md, DVFS give-back item 7).  Wave tile 128 x 64 = 8 x 4 tiles of
-// 16 x 16 (128 accumulator registers); per 64-deep k-step 8 A and 4 B fragments of 16 B (lane l:
-// iid column l & 15 of its 16-group, k rows 16 (l >> 4) .. +15: two ds_read_b64_tr_b8 of 8 rows),
-// 32 MFMAs; B double-buffered across k-steps, each A fragment reloaded right after its last use.
-__global__ __launch_bounds__(512, 1) void k_syrk_i8s(const uint8_t* __restrict__ P, uint64_t pitch, uint64_t kdim,
-                                                     uint64_t mpad, const uint32_t* __restrict__ lutr,
-                                                     const int* __restrict__ ctl, uint64_t b0, uint64_t nblk,
-                                                     uint8_t* __restrict__ res,
-                                                     const uint32_t* __restrict__ part_tab = nullptr) {
-    constexpr int SKT = SK, KS = SKT / 64, RPT = SKT / 16, PNL = SKT * RS, STG = 2 * PNL;
-    __shared__ __attribute__((aligned(16))) uint8_t lds[2 * STG];
-    if (ctl[1]) return;
-    const int r = blockIdx.y;
-    if (r >= ctl[2]) return;
-    const uint32_t* lr = lutr + (uint64_t)r * mpad;
-    uint32_t bi, bj;
-    if (part_tab) {
-        const uint32_t c = part_tab[b0 + blockIdx.x];
-        bi = c & 0xffffu;
-        bj = c >> 16;
-    } else {
-        tile_coords(b0 + blockIdx.x, bi, bj);
-    }
-    const uint64_t i0 = (uint64_t)bi * BW, j0 = (uint64_t)bj * BW;
-    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-    const int wm = wave >> 2, wn = wave & 3;
-    const int lp = __builtin_amdgcn_readfirstlane(t >> 8), kq = (t >> 4) & 15, d = t & 15;
-    const uint8_t* pbase = P + (lp ? j0 : i0) / 4;
-    const uint32_t pit = (uint32_t)pitch;
-    const uint32_t* lq = lr + RPT * kq;
-    const int g = lane >> 4, jj = (lane & 15) >> 1, pp = lane & 1;
-    const int rd = (16 * g + jj) * RS + 8 * pp;
-
-    v4i acc[8][4];
-#pragma unroll
-    for (int x = 0; x < 8; x++)
-#pragma unroll
-        for (int y = 0; y < 4; y++) acc[x][y] = (v4i){0, 0, 0, 0};
-    const uint64_t nst = (kdim + SKT - 1) / SKT;
-    uint32_t cw[RPT];
-    uint4 cl[RPT / 4];
-    auto load = [&](uint64_t st) {
-        const uint8_t* sb = pbase + st * SKT * pitch;
-        const uint32_t lim = (uint32_t)(kdim - 1 - st * SKT);
-#pragma unroll
-        for (int h = 0; h < RPT; h++) {
-            const uint32_t row = min((uint32_t)(RPT * kq + h), lim);
-            cw[h] = *reinterpret_cast<const uint32_t*>(sb + (row * pit + 4 * d));
-        }
-#pragma unroll
-        for (int u = 0; u < RPT / 4; u++) cl[u] = *reinterpret_cast<const uint4*>(lq + SKT * st + 4 * u);
-    };
-    auto store = [&](uint8_t* S, int h0, int h1) {
-#pragma unroll
-        for (int h = h0; h < h1; h++) {
-            const uint4 c4 = cl[h >> 2];
-            const uint32_t L = (h & 3) == 0 ? c4.x : (h & 3) == 1 ? c4.y : (h & 3) == 2 ? c4.z : c4.w;
-            uint4 o;
-            o.x = __builtin_amdgcn_perm(L, L, cw[h] & 0x03030303u);
-            o.y = __builtin_amdgcn_perm(L, L, (cw[h] >> 2) & 0x03030303u);
-            o.z = __builtin_amdgcn_perm(L, L, (cw[h] >> 4) & 0x03030303u);
-            o.w = __builtin_amdgcn_perm(L, L, (cw[h] >> 6) & 0x03030303u);
-            *reinterpret_cast<uint4*>(S + lp * PNL + (RPT * kq + h) * RS + 16 * d) = o;
-        }
-    };
-    auto frag = [&](const uint8_t* S, int panel, int ks, int col) -> v4i {
-        const uint8_t* b = S + panel * PNL + 64 * ks * RS + rd + col;
-        const v2i x = lds_tr8(b), y = lds_tr8(b + 8 * RS);
-        return (v4i){x.x, x.y, y.x, y.y};
-    };
     load(0);
     store(lds, 0, RPT);
-    load(nst > 1 ? 1 : 0);
-    __syncthreads();
-    v4i a[8], bb[2][4];
-#pragma unroll
-    for (int x = 0; x < 8; x++) a[x] = frag(lds, 0, 0, wm * 128 + 16 * x);
-#pragma unroll
-    for (int y = 0; y < 4; y++) bb[0][y] = frag(lds, 1, 0, wn * 64 + 16 * y);
-    for (uint64_t s = 0; s < nst; s++) {
-        const uint8_t* cur = lds + (s & 1) * STG;
-        uint8_t* nxt = lds + ((s + 1) & 1) * STG;
-#pragma unroll
-        for (int ks = 0; ks < KS; ks++) {
-            const int cb = ks & 1;
-            const bool more = ks + 1 < KS;  // the next k-step's fragments are in this stage
-            if (more) {
-#pragma unroll
-                for (int y = 0; y < 4; y++) bb[cb ^ 1][y] = frag(cur, 1, ks + 1, wn * 64 + 16 * y);
-            }
-#pragma unroll
-            for (int x = 0; x < 8; x++) {
-#pragma unroll
-                for (int y = 0; y < 4; y++)
-                    acc[x][y] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[x], bb[cb][y], acc[x][y], 0, 0, 0);
-                if (more) a[x] = frag(cur, 0, ks + 1, wm * 128 + 16 * x);
-                if (x & 1) store(nxt, ks * (RPT / KS) + (x >> 1) * (RPT / KS / 4),
-                                 ks * (RPT / KS) + ((x >> 1) + 1) * (RPT / KS / 4));
-            }
-        }
-        load(s + 2 < nst ? s + 2 : nst - 1);
-        __syncthreads();
-        // stage s+1's first fragments (KS is even: the last k-step used bb[1], refill bb[0])
-#pragma unroll
-        for (int x = 0; x < 8; x++) a[x] = frag(nxt, 0, 0, wm * 128 + 16 * x);
-#pragma unroll
-        for (int y = 0; y < 4; y++) bb[0][y] = frag(nxt, 1, 0, wn * 64 + 16 * y);
-    }
-    const int p = kMod[r];
-    const double invp = 1.0 / (double)p;
-    uint8_t* O = res + ((uint64_t)r * nblk + blockIdx.x) * (BW * BW);
-    const int cq = lane & 15, rq = 4 * (lane >> 4);
-#pragma unroll
-    for (int x = 0; x < 8; x++)
-#pragma unroll
-        for (int y = 0; y < 4; y++) {
-            uint8_t* bp = O + (wm * 128 + 16 * x) * BW + wn * 64 + 16 * y + pi16(cq);
-#pragma unroll
-            for (int q = 0; q < 4; q++) {
-                const int v = acc[x][y][q];
-                int rr = v - p * (int)floor((double)v * invp);
-                rr += rr < 0 ? p : 0;
-                rr -= rr >= p ? p : 0;
-                bp[pi16(rq + q) * BW] = (uint8_t)rr;
-            }
-        }
-}
-
-// ubench (variant 77): 4 waves (2 x 2), one per SIMD, 128 x 128 per wave = 4 x 4
-// v_mfma_i32_32x32x32_i8 tiles (256 accumulator registers, AGPR-backed): 8 fragment reads per 16
-// MFMAs instead of k_syrk_i8r's 6 per 8 -- a third less LDS read traffic for the same residue
-// image; the loader is k_syrk_i8r's with twice the rows per thread.
-template <int SKT>
-__global__ __launch_bounds__(256, 1) void k_syrk_i8w(const uint8_t* __restrict__ P, uint64_t pitch, uint64_t kdim,
-                                                     uint64_t mpad, const uint32_t* __restrict__ lutr,
-                                                     const int* __restrict__ ctl, uint64_t b0, uint64_t nblk,
-                                                     uint8_t* __restrict__ res) {
-    constexpr int KS = SKT / 32, RPT = SKT / 8, PNL = SKT * RS, STG = 2 * PNL;
-    __shared__ __attribute__((aligned(16))) uint8_t lds[2 * STG];
-    if (ctl[1]) return;
-    const int r = blockIdx.y;
-    if (r >= ctl[2]) return;
-    const uint32_t* lr = lutr + (uint64_t)r * mpad;
-    uint32_t bi, bj;
-    tile_coords(b0 + blockIdx.x, bi, bj);
-    const uint64_t i0 = (uint64_t)bi * BW, j0 = (uint64_t)bj * BW;
-    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-    const int wm = wave >> 1, wn = wave & 1;
-    const int lp = __builtin_amdgcn_readfirstlane(t >> 7), kq = (t >> 4) & 7, d = t & 15;
-    const uint8_t* pbase = P + (lp ? j0 : i0) / 4;
-    const uint32_t pit = (uint32_t)pitch;
-    const uint32_t* lq = lr + RPT * kq;
-    const int g = lane >> 4, jj = (lane & 15) >> 1, pp = lane & 1;
-    const int rd = (16 * (g >> 1) + jj) * RS + 16 * (g & 1) + 8 * pp;
-
-    v16i acc[4][4];
-#pragma unroll
-    for (int x = 0; x < 4; x++)
-#pragma unroll
-        for (int y = 0; y < 4; y++) acc[x][y] = (v16i){};
-    const uint64_t nst = (kdim + SKT - 1) / SKT;
-    uint32_t cw[RPT];
-    uint4 cl[RPT / 4];
-    auto load = [&](uint64_t st) {
-        const uint8_t* sb = pbase + st * SKT * pitch;
-        const uint32_t lim = (uint32_t)(kdim - 1 - st * SKT);
-#pragma unroll
-        for (int h = 0; h < RPT; h++) {
-            const uint32_t row = min((uint32_t)(RPT * kq + h), lim);
-            cw[h] = *reinterpret_cast<const uint32_t*>(sb + (row * pit + 4 * d));
-        }
-#pragma unroll
-        for (int u = 0; u < RPT / 4; u++) cl[u] = *reinterpret_cast<const uint4*>(lq + SKT * st + 4 * u);
-    };
-    auto store = [&](uint8_t* S, int h0, int h1) {
-#pragma unroll
-        for (int h = h0; h < h1; h++) {
-            const uint4 c4 = cl[h >> 2];
-            const uint32_t L = (h & 3) == 0 ? c4.x : (h & 3) == 1 ? c4.y : (h & 3) == 2 ? c4.z : c4.w;
-            uint4 o;
-            o.x = __builtin_amdgcn_perm(L, L, cw[h] & 0x03030303u);
-            o.y = __builtin_amdgcn_perm(L, L, (cw[h] >> 2) & 0x03030303u);
-            o.z = __builtin_amdgcn_perm(L, L, (cw[h] >> 4) & 0x03030303u);
-            o.w = __builtin_amdgcn_perm(L, L, (cw[h] >> 6) & 0x03030303u);
-            *reinterpret_cast<uint4*>(S + lp * PNL + (RPT * kq + h) * RS + 16 * d) = o;
-        }
-    };
-    auto frag = [&](const uint8_t* S, int panel, int ks, int col) -> v4i {
-        const uint8_t* b = S + panel * PNL + 32 * ks * RS + rd + col;
-        const v2i x = lds_tr8(b), y = lds_tr8(b + 8 * RS);
-        return (v4i){x.x, x.y, y.x, y.y};
-    };
-    auto frags = [&](const uint8_t* S, int ks, v4i (&A)[4], v4i (&B)[4]) {
-#pragma unroll
-        for (int x = 0; x < 4; x++) A[x] = frag(S, 0, ks, wm * 128 + 32 * x);
-#pragma unroll
-        for (int y = 0; y < 4; y++) B[y] = frag(S, 1, ks, wn * 128 + 32 * y);
-    };
-    load(0);
-    store(lds, 0, RPT);
-    load(nst > 1 ? 1 : 0);
+    load(nst > 1 ? 1 : 0);  // stage s+2's loads are issued at the end of stage s
     __syncthreads();
     for (uint64_t s = 0; s < nst; s++) {
         const uint8_t* cur = lds + (s & 1) * STG;
         uint8_t* nxt = lds + ((s + 1) & 1) * STG;
-        v4i a[2][4], b[2][4];
+        v4i a[2][4], b[2][2];
         frags(cur, 0, a[0], b[0]);
 #pragma unroll
         for (int ks = 0; ks < KS; ks++) {
@@ -957,33 +318,15 @@ __global__ __launch_bounds__(256, 1) void k_syrk_i8w(const uint8_t* __restrict__
 #pragma unroll
             for (int x = 0; x < 4; x++)
 #pragma unroll
-                for (int y = 0; y < 4; y++)
+                for (int y = 0; y < 2; y++)
                     acc[x][y] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[ks & 1][x], b[ks & 1][y], acc[x][y], 0, 0, 0);
             store(nxt, ks * RPT / KS, (ks + 1) * RPT / KS);
         }
         load(s + 2 < nst ? s + 2 : nst - 1);
         __syncthreads();
     }
-    const int p = kMod[r];
-    const double invp = 1.0 / (double)p;
-    uint8_t* O = res + ((uint64_t)r * nblk + blockIdx.x) * (BW * BW);
-    const int hh = lane >> 5, colp = 16 * ((lane >> 4) & 1) + pi16(lane & 15);
-#pragma unroll
-    for (int x = 0; x < 4; x++)
-#pragma unroll
-        for (int y = 0; y < 4; y++) {
-            uint8_t* bp = O + (wm * 128 + 32 * x + hh) * BW + wn * 128 + 32 * y + colp;
-#pragma unroll
-            for (int q = 0; q < 16; q++) {
-                const int v = acc[x][y][q];
-                int rr = v - p * (int)floor((double)v * invp);
-                rr += rr < 0 ? p : 0;
-                rr -= rr >= p ? p : 0;
-                bp[(16 * (q >> 3) + 4 * (q & 3) + 2 * ((q >> 2) & 1)) * BW] = (uint8_t)rr;
-            }
-        }
+    crt_epilogue(acc, r, nblk, bx, wm, wn, lane, res);
 }
-#endif
 
 // ---------------------------------------------------------------- reconstruction
 // two elements per thread (packed f32 math: v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32); the
@@ -1198,67 +541,9 @@ void launch_syrk_packed_crt(const uint8_t* packed, uint64_t pitch, uint64_t n, u
             SNPMI_REQUIRE(cnt <= per, SNPMI_E_ARG, "crt SYRK: one block column exceeds the residue scratch");
         }
         SNPMI_REQUIRE(cnt < (1ull << 23), SNPMI_E_ARG, "crt SYRK: chunk too large");
-#ifdef SNPMI_UBENCH
-        if (g_variant_syrk == 72)  // 64-SNP stages (73.7 KiB of LDS)
-            k_syrk_i8r<64><<<dim3((unsigned)cnt, kR), 512, 0, st>>>(packed, pitch, m, mpad, lutr, ctl, b0, cnt, res);
-        else if (g_variant_syrk == 73)  // ablation: no loader
-            k_syrk_i8r<SK, 1><<<dim3((unsigned)cnt, kR), 512, 0, st>>>(packed, pitch, m, mpad, lutr, ctl, b0, cnt, res);
-        else if (g_variant_syrk == 75)  // row-per-wave loader, ds_write_addtid_b32
-            k_syrk_i8r<SK, 0, 1><<<dim3((unsigned)cnt, kR), 512, 0, st>>>(packed, pitch, m, mpad, lutr, ctl, b0, cnt, res);
-        else if (g_variant_syrk == 76)  // same, 64-SNP stages
-            k_syrk_i8r<64, 0, 1><<<dim3((unsigned)cnt, kR), 512, 0, st>>>(packed, pitch, m, mpad, lutr, ctl, b0, cnt, res);
-        else if (g_variant_syrk == 78)  // residue rows stored as two ds_write_b64
-            k_syrk_i8r<SK, 0, 0, 1><<<dim3((unsigned)cnt, kR), 512, 0, st>>>(packed, pitch, m, mpad, lutr, ctl, b0, cnt, res);
-        else if (g_variant_syrk == 77)  // 4 waves, one per SIMD, 128 x 128 per wave
-            k_syrk_i8w<SK><<<dim3((unsigned)cnt, kR), 256, 0, st>>>(packed, pitch, m, mpad, lutr, ctl, b0, cnt, res);
-        else if (g_variant_syrk == 79)  // two loader register sets: loads two stages ahead
-            k_syrk_i8r<SK, 0, 0, 0, 1><<<dim3((unsigned)cnt, kR), 512, 0, st>>>(packed, pitch, m, mpad, lutr, ctl, b0, cnt, res);
-        else if (g_variant_syrk == 74)  // ablation: fragments read once per stage
-            k_syrk_i8r<SK, 2><<<dim3((unsigned)cnt, kR), 512, 0, st>>>(packed, pitch, m, mpad, lutr, ctl, b0, cnt, res);
-        else if (g_variant_syrk == 83)  // complementary halves: waves 4-7 store early
-            k_syrk_i8r<SK, 0, 0, 0, 0, 1><<<dim3((unsigned)cnt, kR), 512, 0, st>>>(packed, pitch, m, mpad, lutr, ctl, b0,
-                                                                                cnt, res, part_tab);
-        else if (g_variant_syrk == 84)  // complementary halves: waves 0-3 store early
-            k_syrk_i8r<SK, 0, 0, 0, 0, 2><<<dim3((unsigned)cnt, kR), 512, 0, st>>>(packed, pitch, m, mpad, lutr, ctl, b0,
-                                                                                cnt, res, part_tab);
-        else if (g_variant_syrk == 86)  // 16 waves, 64 x 64 per wave
-            k_syrk_i8h<><<<dim3((unsigned)cnt, kR), 1024, 0, st>>>(packed, pitch, m, mpad, lutr, ctl, b0, cnt, res, part_tab);
-        else if (g_variant_syrk == 95)  // pairs of blocks per XCD (MAP 2)
-            k_syrk_i8r<SK, 0, 0, 0, 0, 0, 2><<<(unsigned)(round_up(cnt, 16) * kR), 512, 0, st>>>(
-                packed, pitch, m, mpad, lutr, ctl, b0, cnt, res, part_tab);
-        else if (g_variant_syrk == 94)  // 16 waves on the XCD-grouped grid
-            k_syrk_i8h<1><<<(unsigned)(round_up(cnt, 8) * kR), 1024, 0, st>>>(packed, pitch, m, mpad, lutr, ctl, b0, cnt,
-                                                                           res, part_tab);
-        else if (g_variant_syrk >= 90 && g_variant_syrk <= 93) {  // MAP 1 + 78 / 79 / 83 / 84
-            const unsigned g1 = (unsigned)(round_up(cnt, 8) * kR);
-            if (g_variant_syrk == 90)
-                k_syrk_i8r<SK, 0, 0, 1, 0, 0, 1><<<g1, 512, 0, st>>>(packed, pitch, m, mpad, lutr, ctl, b0, cnt, res, part_tab);
-            else if (g_variant_syrk == 91)
-                k_syrk_i8r<SK, 0, 0, 0, 1, 0, 1><<<g1, 512, 0, st>>>(packed, pitch, m, mpad, lutr, ctl, b0, cnt, res, part_tab);
-            else if (g_variant_syrk == 92)
-                k_syrk_i8r<SK, 0, 0, 0, 0, 1, 1><<<g1, 512, 0, st>>>(packed, pitch, m, mpad, lutr, ctl, b0, cnt, res, part_tab);
-            else
-                k_syrk_i8r<SK, 0, 0, 0, 0, 2, 1><<<g1, 512, 0, st>>>(packed, pitch, m, mpad, lutr, ctl, b0, cnt, res, part_tab);
-        }
-        else if (g_variant_syrk == 88)  // round-5 order: grid (blocks, moduli), block-fastest (MAP 0)
-            k_syrk_i8r<SK><<<dim3((unsigned)cnt, kR), 512, 0, st>>>(packed, pitch, m, mpad, lutr, ctl, b0, cnt, res,
-                                                                   part_tab);
-        else if (g_variant_syrk == 85)  // v_mfma_i32_16x16x64_i8 shape
-            k_syrk_i8s<<<dim3((unsigned)cnt, kR), 512, 0, st>>>(packed, pitch, m, mpad, lutr, ctl, b0, cnt, res, part_tab);
-        else if (g_variant_syrk == 80)  // 4-slot ring of 64-SNP stages, next stage's fragments read before the barrier
-            k_syrk_i8q<1, 0><<<dim3((unsigned)cnt, kR), 512, 0, st>>>(packed, pitch, m, mpad, lutr, ctl, b0, cnt, res,
-                                                                     part_tab);
-        else if (g_variant_syrk == 81)  // the ring without the cross-barrier prefetch
-            k_syrk_i8q<0, 0><<<dim3((unsigned)cnt, kR), 512, 0, st>>>(packed, pitch, m, mpad, lutr, ctl, b0, cnt, res,
-                                                                     part_tab);
-        else if (g_variant_syrk == 82)  // ring + prefetch + s_setprio 1 on waves 4-7
-            k_syrk_i8q<1, 1><<<dim3((unsigned)cnt, kR), 512, 0, st>>>(packed, pitch, m, mpad, lutr, ctl, b0, cnt, res,
-                                                                     part_tab);
-        else
-#endif
-        // MAP 1: the kR moduli of a block on one XCD at once (FETCH 951 -> 149 GB per 62.5k-SNP
+        // the kR moduli of a block on one XCD at once (FETCH 951 -> 149 GB per 62.5k-SNP
         // launch at 50k iids, the clock 2.21 -> 2.36 GHz, -3.6%: profiles/r05m)
-        k_syrk_i8r<SK, 0, 0, 0, 0, 0, 1><<<(unsigned)(round_up(cnt, 8) * kR), 512, 0, st>>>(
+        k_syrk_i8r<SK><<<(unsigned)(round_up(cnt, 8) * kR), 512, 0, st>>>(
             packed, pitch, m, mpad, lutr, ctl, b0, cnt, res, part_tab);
         k_crt<<<(unsigned)(cnt * 64), 256, 0, st>>>(res, b0, cnt, n, ctl, F, cc, tiles, accumulate, part_tab ? 1 : 0);
         if (after_chunk) {

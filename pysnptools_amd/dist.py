@@ -22,9 +22,11 @@ node-local file; barriers and max-over-ranks are RCCL all-reduces.
 """
 import contextlib
 import ctypes
+import json
 import os
 import socket
 import struct
+import sys
 import tempfile
 import threading
 import time
@@ -142,14 +144,23 @@ class Dist(object):
         self.rank, self.world, self.local_rank, self.device = rank, world, local_rank, device
         self.rccl, self.n_gpus = rccl, n_gpus
         self._closed = False
+        # group calls made through this object (the watchdog's dump): count and the last one
+        self.ops, self.last_op = 0, None
+        self.watchdog_path = None  # set by init_from_env: the job's shared abort-file name
+
+    def _op(self, name):
+        self.ops += 1
+        self.last_op = name
 
     def barrier(self):
+        self._op("barrier")
         if self.rccl:
             from pysnptools_amd import _native as N
 
             N.call("snpmi_rccl_barrier")
 
     def max(self, x):
+        self._op("max")
         if not self.rccl:
             return x
         from pysnptools_amd import _native as N
@@ -162,6 +173,7 @@ class Dist(object):
         """Elementwise sum over ranks of a host float array (any size, through a device buffer)."""
         import numpy as np
 
+        self._op("sum_host")
         if not self.rccl:
             return np.array(arr, copy=True)
         from pysnptools_amd import _native as N
@@ -190,6 +202,7 @@ class Dist(object):
         afterwards) or, with ``root=None``, ncclAllReduce.  Enqueued on the library stream."""
         from pysnptools_amd import _native as N
 
+        self._op("sum_dev")
         if not self.rccl:
             if self.world > 1:
                 raise RuntimeError("a device sum over %d ranks needs an RCCL communicator" % self.world)
@@ -203,6 +216,7 @@ class Dist(object):
     def allgather_dev(self, send, recv, nbytes):
         """Device all-gather of ``nbytes`` per rank: rank r's ``send`` lands at ``recv + r*nbytes``
         on every rank (ncclAllGather; in place when ``send`` is that slot of ``recv``)."""
+        self._op("allgather_dev")
         if not self.rccl:
             if self.world > 1:
                 raise RuntimeError("an all-gather over %d ranks needs an RCCL communicator" % self.world)
@@ -294,6 +308,7 @@ class HostDist(Dist):
 
     def allgather_bytes(self, payload):
         """Every rank's ``payload`` (bytes), in rank order, on every rank."""
+        self.hub_calls = getattr(self, "hub_calls", 0) + 1
         payload = bytes(payload)
         if self.rank == 0:
             parts = [payload] + [_recv_frame(c) for c in self._peers]
@@ -312,9 +327,11 @@ class HostDist(Dist):
         return parts
 
     def barrier(self):
+        self._op("barrier")
         self.allgather_bytes(b"")
 
     def max(self, x):
+        self._op("max")
         return max(struct.unpack("<d", p)[0] for p in self.allgather_bytes(struct.pack("<d", float(x))))
 
     def _reduce_f64(self, a, root=None):
@@ -339,6 +356,7 @@ class HostDist(Dist):
     def sum_host(self, arr):
         import numpy as np
 
+        self._op("sum_host")
         a = np.asarray(arr)
         return self._reduce_f64(a).astype(a.dtype)
 
@@ -353,6 +371,7 @@ class HostDist(Dist):
 
         from pysnptools_amd import _native as N
 
+        self._op("sum_dev")
         host = np.empty(int(count), dtype=dtype)
         N.call("snpmi_stream_sync")
         N.call("snpmi_memcpy_d2h", N.ptr(host), buf, host.nbytes)
@@ -366,6 +385,7 @@ class HostDist(Dist):
 
         from pysnptools_amd import _native as N
 
+        self._op("allgather_dev")
         nbytes = int(nbytes)
         mine = np.empty(nbytes, dtype=np.uint8)
         N.call("snpmi_memcpy_d2h", N.ptr(mine), send, nbytes)
@@ -393,8 +413,10 @@ def init_from_env(force_rccl=False, timeout=300.0, env=None, set_current=True):
                            "SNPMI_RCCL_ID_FILE to a path every node shares to run across nodes)" % (world, local_world))
     device = pick_device(local_rank, N.device_count())
     N.call("snpmi_set_device", device)
+    wd_path = id_file(env) + ".watchdog" if world > 1 else None
     if world > 1 and env.get("SNPMI_DIST_HOST"):
         d = HostDist(rank, world, local_rank, device, timeout, env)
+        d.watchdog_path = wd_path
         d.barrier()
         if set_current:
             _CURRENT = d
@@ -428,6 +450,7 @@ def init_from_env(force_rccl=False, timeout=300.0, env=None, set_current=True):
         N.call("snpmi_rccl_comm_count", ctypes.byref(cnt))
         n_gpus = cnt.value
     d = Dist(rank, world, local_rank, device, rccl, n_gpus)
+    d.watchdog_path = wd_path
     d.barrier()
     if set_current:
         _CURRENT = d
@@ -437,3 +460,119 @@ def init_from_env(force_rccl=False, timeout=300.0, env=None, set_current=True):
 def current():
     """The open process group of this process, or None."""
     return _CURRENT
+
+
+class Watchdog(object):
+    """Per-rank stall detector for one process-group job (bench.py's N > 1 legs).
+
+    A collective that one rank never joins blocks every other rank inside RCCL forever, and no
+    Python exception ever surfaces.  The watchdog thread turns that into a bounded, diagnosed
+    failure: the main thread calls :meth:`mark` at every leg and block boundary; when no mark has
+    arrived for ``limit`` seconds (``mark(..., limit=)`` widens it for one phase, e.g. the final
+    barrier while rank 0 runs its rank-only legs), or when another rank of the job has fired (its
+    abort file ``<id file>.watchdog`` exists), it
+
+    * writes ONE line ``[watchdog] rank R {json}`` to stderr: rank, world, leg, detail (e.g. the last
+      shard block index), seconds since the mark, the group's own call count and last call, and the
+      library's collective trace (``snpmi_rccl_trace``: calls per kind, bytes, the call-sequence
+      signature -- equal on ranks that issued the same collectives -- and whether the rank sits in a
+      blocking host all-reduce);
+    * creates the abort file, so every other rank dumps its line within ``poll`` seconds;
+    * calls ``on_fire(diag)`` (bench.py rank 0: a partial JSON line on stdout);
+    * ends the process with ``os._exit(exit_code)`` -- no re-exec, no cleanup that could block on the
+      GPU; the launcher (bench.py's spawner, torch.distributed.run) then reaps the other ranks.
+
+    :meth:`fail` does the same at once, from an exception handler: a rank that raises outside a
+    collective would otherwise leave its peers waiting in one."""
+
+    def __init__(self, dist, limit=300.0, on_fire=None, poll=0.5, exit_code=4, stream=None, path=None):
+        self.dist, self.limit, self.on_fire, self.poll = dist, float(limit), on_fire, float(poll)
+        # after telling the peers, stay up long enough for them to see the abort file and fire on
+        # their own, before this process's exit closes sockets they may be blocked on
+        self.grace = max(1.0, 3.0 * self.poll)
+        self.exit_code = exit_code
+        self.stream = stream if stream is not None else sys.stderr
+        self.path = path if path is not None else getattr(dist, "watchdog_path", None)
+        self.leg, self.detail, self._limit = "start", None, self.limit
+        self._t = time.time()
+        self._lock = threading.Lock()
+        self._fired = False
+        self._stop = threading.Event()
+        self._thread = threading.Thread(target=self._run, name="snpmi-watchdog", daemon=True)
+        self._thread.start()
+
+    def mark(self, leg=None, detail=None, limit=None):
+        """Progress: the current leg (None keeps it), a detail (block index...), this phase's limit."""
+        with self._lock:
+            if leg is not None:
+                self.leg = leg
+            self.detail = detail
+            self._limit = self.limit if limit is None else float(limit)
+            self._t = time.time()
+
+    def stop(self):
+        self._stop.set()
+        self._thread.join(timeout=5)
+
+    def diagnostics(self, reason):
+        with self._lock:
+            leg, detail, since, lim = self.leg, self.detail, time.time() - self._t, self._limit
+        d = self.dist
+        diag = {"reason": reason, "rank": getattr(d, "rank", 0), "world": getattr(d, "world", 1), "leg": leg,
+                "detail": detail, "seconds_since_mark": round(since, 1), "limit_s": lim,
+                "group_ops": getattr(d, "ops", None), "group_last_op": getattr(d, "last_op", None),
+                "group": "rccl" if getattr(d, "rccl", False) else ("host" if getattr(d, "world", 1) > 1 else "none")}
+        try:
+            from pysnptools_amd import _native as N
+
+            diag["rccl_trace"] = N.rccl_trace()
+        except Exception as e:  # the library may be absent (CPU tests) or predate the trace
+            diag["rccl_trace"] = "unavailable: %s" % e
+        return diag
+
+    def fail(self, reason):
+        """Fire now (an exception on this rank): dump, tell the peers, exit."""
+        self._fire(reason, tell_peers=True)
+
+    def _peer_fired(self):
+        return bool(self.path) and os.path.exists(self.path)
+
+    def _fire(self, reason, tell_peers):
+        with self._lock:
+            fired, self._fired = self._fired, True
+        if fired:  # another thread is already dumping and will end the process: wait for it
+            while True:
+                time.sleep(60)
+        diag = self.diagnostics(reason)
+        if tell_peers and self.path:
+            with contextlib.suppress(OSError):
+                fd = os.open(self.path, os.O_WRONLY | os.O_CREAT, 0o600)
+                os.write(fd, ("rank %d: %s\n" % (diag["rank"], reason)).encode())
+                os.close(fd)
+        try:
+            self.stream.write("[watchdog] rank %d %s\n" % (diag["rank"], json.dumps(diag, sort_keys=True)))
+            self.stream.flush()
+            if self.on_fire is not None:
+                self.on_fire(diag)
+            if tell_peers and self.path:
+                time.sleep(self.grace)
+        finally:
+            with contextlib.suppress(Exception):
+                sys.stdout.flush()
+            os._exit(self.exit_code)
+
+    def _run(self):
+        while not self._stop.wait(self.poll):
+            if self._peer_fired():
+                self._fire("another rank of the job fired its watchdog (%s)" % self.path, tell_peers=False)
+            with self._lock:
+                late = time.time() - self._t > self._limit
+                lim = self._limit
+            if late:
+                self._fire("no progress mark for %.0f s" % lim, tell_peers=True)
+
+    def clear(self):
+        """Remove the job's abort file (rank 0, after a clean run)."""
+        if self.path:
+            with contextlib.suppress(OSError):
+                os.remove(self.path)

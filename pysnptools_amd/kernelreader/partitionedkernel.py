@@ -18,8 +18,11 @@ every KernelReader does (kernelreader.py:342-350).  ``_read_with_standardizing``
 ``write`` / ``load`` persist each rank's blocks beside a metadata file (the KernelNpz role for a K
 that no single file or process holds).
 
-``SnpKernel(reader, std).read()`` / ``Bed.read_kernel`` route here under an open process group
+``SnpKernel(reader, std).read()``, ``SnpKernel(...)[iid0, iid1].read()`` and
+``SnpKernel._read_with_standardizing`` (FaST-LMM's entry point) route here under an open process group
 when the replicated K would not fit one GPU's HBM (``set_grm_partition``; forced with "always").
+``Bed.read_kernel`` / ``SnpReader._read_kernel`` keep the replicated path: they return a KernelData
+holding the whole K on every rank, which a K that needs partitioning cannot be.
 """
 import json
 import os
@@ -35,7 +38,7 @@ _mode = [os.environ.get("PST_GRM_PARTITION", "auto")]
 
 
 def set_grm_partition(mode):
-    """When ``SnpKernel.read`` / ``Bed.read_kernel`` compute K partitioned (cfg5) instead of
+    """When ``SnpKernel.read`` / ``SnpKernel._read_with_standardizing`` compute K partitioned (cfg5) instead of
     replicated on every rank: ``"auto"`` (default) -- under a process group of > 1 rank when the
     replicated upper-triangle tiles would take more than 80% of the device's free HBM;
     ``"always"`` -- whenever the fused GPU path applies (a Bed and Unit/Beta/trained/Identity),
@@ -176,10 +179,19 @@ class PartitionedKernel(KernelReader):
             raise ValueError("K[iid0, iid1] needs blocks outside part %d of %d; read it under the process group of "
                              "all %d parts" % (self.part, self.parts, self.parts))
 
+    def _check_whole(self, what):
+        """A part of a plan of several, read without its group, holds only its share of the diagonal:
+        ``what`` needs every part (the contract ``_check_owned`` enforces for sub-matrix reads)."""
+        if self.parts > 1 and not self._grouped():
+            raise ValueError("%s of a K partitioned into %d parts needs all of them: part %d alone holds only its share "
+                             "of the diagonal; run it under the process group of all %d parts"
+                             % (what, self.parts, self.part, self.parts))
+
     def trace(self):
         """trace(K) (before ``scale``): each part's diagonal entries, summed over the group."""
         import ctypes
 
+        self._check_whole("trace(K)")
         t = ctypes.c_double(0.0)
         N.call("snpmi_grm_part_trace_" + N.suffix(self.dtype), self.blocks.snpmi_ptr, self.n, self.part, self.parts,
                ctypes.byref(t))
@@ -188,20 +200,47 @@ class PartitionedKernel(KernelReader):
             tr = np.asarray(self.dist.sum_host(tr), dtype=np.float64)
         return float(tr[0])
 
+    @staticmethod
+    def supports(kernel_standardizer):
+        """Kernel standardizers a partitioned K applies as a scale on extraction: DiagKtoN (factor from
+        the trace summed over the parts), DiagKtoNTrained (its own factor) and Identity (none)."""
+        from pysnptools_amd.kernelstandardizer import DiagKtoNTrained
+        from pysnptools_amd.kernelstandardizer import Identity as KernelIdentity
+
+        return isinstance(kernel_standardizer, (DiagKtoN, DiagKtoNTrained, KernelIdentity))
+
     def _read_with_standardizing(self, to_kerneldata, snp_standardizer=None, kernel_standardizer=DiagKtoN(),
                                  return_trained=False, num_threads=None):
-        """DiagKtoN over the partitioned K (diag_K_to_N.py:54-59: factor = n / trace, applied when
-        |factor - 1| > 1e-15) as a scale on every later extraction; ``to_kerneldata`` reads the whole
-        scaled K (KernelData), else the scaled reader is returned."""
-        from pysnptools_amd.kernelstandardizer import DiagKtoNTrained
+        """The kernel standardizer over the partitioned K as a scale on every later extraction
+        (``to_kerneldata``: the whole scaled K as a KernelData, else the scaled reader):
 
-        assert isinstance(kernel_standardizer, DiagKtoN), "a partitioned K supports the DiagKtoN kernel standardizer"
-        factor = float(self.n) / self.trace()
-        scaled = PartitionedKernel(self._row, self.blocks, self.part, self.parts, self.dist,
-                                   scale=self.scale * (factor if abs(factor - 1.0) > 1e-15 else 1.0),
-                                   name=self._name + ".standardize(DiagKtoN())")
+        * DiagKtoN (diag_K_to_N.py:54-59): factor = n / trace, trace summed over the parts, applied
+          when |factor - 1| > 1e-15; returns DiagKtoNTrained(factor);
+        * DiagKtoNTrained (diag_K_to_N.py:115-127, a factor trained on another K, as FaST-LMM passes
+          for test kernels): its own factor, applied unless it is constant;
+        * Identity (kernelstandardizer/__init__.py): no scale.
+
+        Any other kernel standardizer raises ValueError (SnpKernel falls back to the replicated K)."""
+        from pysnptools_amd.kernelstandardizer import DiagKtoNTrained
+        from pysnptools_amd.kernelstandardizer import Identity as KernelIdentity
+
+        if isinstance(kernel_standardizer, DiagKtoN):
+            factor = float(self.n) / self.trace()
+            scale, trained = (factor if abs(factor - 1.0) > 1e-15 else 1.0), DiagKtoNTrained(factor)
+        elif isinstance(kernel_standardizer, DiagKtoNTrained):
+            f = float(kernel_standardizer.factor)
+            scale, trained = (1.0 if kernel_standardizer.is_constant else f), kernel_standardizer
+        elif isinstance(kernel_standardizer, KernelIdentity):
+            scale, trained = 1.0, kernel_standardizer
+        else:
+            raise ValueError("a partitioned K supports the DiagKtoN, DiagKtoNTrained and Identity kernel "
+                             "standardizers, not %r" % (kernel_standardizer,))
+        if to_kerneldata:
+            self._check_whole("reading the whole K")
+        scaled = PartitionedKernel(self._row, self.blocks, self.part, self.parts, self.dist, scale=self.scale * scale,
+                                   name=self._name + ".standardize(%r)" % (kernel_standardizer,))
         kernel = scaled.read(num_threads=num_threads) if to_kerneldata else scaled
-        return (kernel, None, DiagKtoNTrained(factor)) if return_trained else kernel
+        return (kernel, None, trained) if return_trained else kernel
 
     # ------------------------------------------------------------------ persistence
     @staticmethod

@@ -47,23 +47,28 @@ class SnpKernel(KernelReader):
         """The K of this SnpKernel computed partitioned over the process group (cfg5,
         ``shard.grm_partitioned``: each rank keeps its 256x256 blocks in HBM) when
         ``partitionedkernel.use_partitioned`` says the replicated K does not fit (or the mode is
-        "always"), as a ``PartitionedKernel`` -- cached per dtype, so later sub-matrix reads of this
-        SnpKernel reuse the blocks.  None: the replicated path applies."""
+        "always"), as a ``PartitionedKernel``.  The answer -- the blocks, or None: the replicated path
+        applies -- is cached per (dtype, partition mode, group), so later sub-matrix reads of this
+        SnpKernel reuse the blocks and an "auto" decision runs its group collective once; the cache
+        holds HBM (cfg5: tens of GB per rank) until ``release_partitioned()`` and is never pickled."""
         from pysnptools_amd import dist as dist_mod
-        from pysnptools_amd.kernelreader.partitionedkernel import PartitionedKernel, use_partitioned
+        from pysnptools_amd.kernelreader.partitionedkernel import (PartitionedKernel, grm_partition_mode,
+                                                                   use_partitioned)
         from pysnptools_amd.snpreader.bed import Bed
         from pysnptools_amd.snpreader.snpreader import _resolve
         from pysnptools_amd.standardizer.standardizer import _std_args
 
         dtype = np.dtype(dtype)
-        cache = self.__dict__.setdefault("_pk", {})
-        if dtype in cache:
-            return cache[dtype]
         group = dist_mod.current()
+        key = (dtype.str, grm_partition_mode(), id(group), group.world if group is not None else 1)
+        cache = self.__dict__.setdefault("_pk", {})
+        if key in cache:
+            return cache[key]
         if dtype not in (np.float32, np.float64) or _std_args(self.standardizer) is None:
             return None
         if not isinstance(_resolve(self.snpreader)[0], Bed) or not use_partitioned(self.snpreader.iid_count, dtype,
                                                                                    group):
+            cache[key] = None
             return None
         from pysnptools_amd import shard
 
@@ -72,8 +77,17 @@ class SnpKernel(KernelReader):
                                                    num_threads=num_threads, dist=group, **kw)
         pk = PartitionedKernel(self.snpreader.iid, blocks, dist=group, name=str(self))
         pk.snp_trained = trained
-        cache[dtype] = pk
+        cache[key] = pk
         return pk
+
+    def release_partitioned(self):
+        """Drop the cached partitioned K (frees its HBM blocks) and the cached routing decisions."""
+        self.__dict__.pop("_pk", None)
+
+    def __getstate__(self):
+        state = dict(self.__dict__)
+        state.pop("_pk", None)  # device memory and group-bound decisions do not travel
+        return state
 
     def _read(self, row_index_or_none, col_index_or_none, order, dtype, force_python_only, view_ok, num_threads):
         dtype = np.dtype(dtype)
@@ -110,7 +124,10 @@ class SnpKernel(KernelReader):
         """(K, snp_trained, kernel_trained) as FaST-LMM uses it (snpkernel.py:104-132).  With the
         default DiagKtoN, the trace and scale run on the GPU before K is copied out."""
         logging.info("Starting '_read_with_standardizing'")
-        pk = self._partitioned(np.float64, num_threads) if to_kerneldata else None
+        from pysnptools_amd.kernelreader.partitionedkernel import PartitionedKernel
+
+        pk = (self._partitioned(np.float64, num_threads)
+              if to_kerneldata and PartitionedKernel.supports(kernel_standardizer) else None)
         if pk is not None:  # K partitioned over the group: DiagKtoN from the trace summed over the parts
             kernel, _, kernel_trained = pk._read_with_standardizing(to_kerneldata, None, kernel_standardizer,
                                                                     return_trained=True, num_threads=num_threads)

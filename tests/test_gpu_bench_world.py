@@ -11,6 +11,7 @@ import os
 import socket
 import subprocess
 import sys
+import time
 
 import pytest
 
@@ -35,6 +36,13 @@ def _check(out, world):
     assert d["parity"]["bit_exact"] and d["beta"]["parity"]["pass"]
     for k in ("grm", "grm_f64"):
         assert d[k]["parity"]["pass"], d[k]["parity"]
+        # configs[3]'s exchange is an all-reduce; the reduce is timed beside it
+        assert "allreduce" in d[k]["collective"], d[k]["collective"]
+        assert set(d[k]["collective_alone"]) >= {"reduce_ms", "allreduce_ms", "bytes"}
+    sc = d["selfcheck"]
+    assert sc["pass"] and sc["group_size_ok"] and sc["allreduce"]["every_rank_same_K"], sc
+    assert sc["allgather_bit_exact"] and sc["rccl_same_calls_every_rank"], sc
+    assert d["box"]["uuid"] and d["box"]["fill_GBps"] > 0
     g5 = d["grm5"]
     assert g5["parity"]["pass"] and g5["parity"]["gathered_block_bit_exact"], g5["parity"]
     assert "host all-gather" in g5["workload"]
@@ -77,3 +85,29 @@ def test_bench_spawned_world8_on_one_gpu():
         assert d[k]["parity"]["pass"], d[k]["parity"]
     g5 = d["grm5"]
     assert g5["parts"] == 8 and g5["parity"]["pass"] and g5["parity"]["gathered_block_bit_exact"], g5["parity"]
+
+
+def test_bench_watchdog_world3_stalled_rank():
+    """Rank 1 hangs inside the cfg4 leg (SNPMI_BENCH_STALL) while ranks 0 and 2 wait for it at the
+    leg's barrier: the whole job must exit 4 within the watchdog bound, every rank's diagnostic line
+    on stderr and one partial JSON line (the legs measured before the stall) from rank 0."""
+    env = dict(os.environ, SNPMI_DIST_HOST="1", SNPMI_BENCH_STALL="1:grm cfg4")
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "3", "--watchdog", "20"] + SMALL
+    t0 = time.time()
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=290, env=env)
+    took = time.time() - t0
+    assert out.returncode == 4, (out.returncode, out.stderr[-4000:])
+    assert took < 240, took
+    diags = {}
+    for ln in out.stderr.splitlines():
+        if ln.startswith("[watchdog] rank "):
+            d = json.loads(ln.split(" ", 3)[3])
+            diags[d["rank"]] = d
+    assert sorted(diags) == [0, 1, 2], out.stderr[-4000:]
+    assert all(d["leg"].startswith("grm cfg4") for d in diags.values()), diags
+    assert all(d["group"] == "host" and d["group_ops"] > 0 for d in diags.values())
+    lines = [ln for ln in out.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, out.stdout[-2000:]
+    p = json.loads(lines[0])
+    assert p["partial"] is True and "watchdog" in p["error"] and p["value"] > 0
+    assert p["selfcheck"]["pass"] and p["watchdog"]["rank"] == 0

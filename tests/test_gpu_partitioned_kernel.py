@@ -88,7 +88,7 @@ def test_kernelreader_api_with_forced_partitioning(name, tmp_path):
             sk = SnpKernel(bed, Unit())
             sub = sk[rows, cols].read(dtype=dt).val
             assert np.abs(sub - Kref[np.ix_(rows, cols)]).max() / scale <= tol
-            assert sk._pk[np.dtype(dt)] is not None  # the blocks are reused by the next read
+            assert any(v is not None for v in sk._pk.values())  # the blocks are reused by the next read
             sub2 = sk[cols, rows].read(dtype=dt, order="C").val
             np.testing.assert_array_equal(sub2, sub.T)
             full = bed.read_kernel(Unit(), dtype=dt).val
@@ -98,6 +98,29 @@ def test_kernelreader_api_with_forced_partitioning(name, tmp_path):
         np.testing.assert_allclose(k_tr.factor, factor, rtol=1e-13)
         assert np.abs(kd.val - Kref * factor).max() / (scale * factor) <= 1e-12
         np.testing.assert_array_equal(snp_tr.stats, st)
+        # FaST-LMM's other kernel standardizers: a trained factor and Identity apply as the
+        # scale on extraction of the partitioned K; one it cannot apply falls back to the replicated K
+        from pysnptools_amd.kernelstandardizer import DiagKtoNTrained, Identity as KIdentity
+
+        sk = SnpKernel(bed, Unit())
+        kd2, _, tr2 = sk._read_with_standardizing(True, DiagKtoNTrained(0.5), return_trained=True)
+        assert tr2.factor == 0.5 and np.abs(kd2.val - Kref * 0.5).max() / (scale * 0.5) <= 1e-12
+        assert any(v is not None for v in sk._pk.values())
+        kd3, _, tr3 = sk._read_with_standardizing(True, KIdentity(), return_trained=True)
+        assert isinstance(tr3, KIdentity) and np.abs(kd3.val - Kref).max() / scale <= 1e-12
+
+        class Halve(object):  # a kernel standardizer the partitioned K does not know
+            def standardize(self, kerneldata, return_trained=False, force_python_only=False, num_threads=None):
+                kerneldata.val[...] *= 0.5
+                return (kerneldata, self) if return_trained else kerneldata
+
+        kd4 = SnpKernel(bed, Unit())._read_with_standardizing(True, Halve())
+        assert np.abs(kd4.val - Kref * 0.5).max() / (scale * 0.5) <= 1e-12
+        import pickle
+
+        assert "_pk" not in pickle.loads(pickle.dumps(sk)).__dict__  # no HBM blocks in pickled state
+        sk.release_partitioned()
+        assert "_pk" not in sk.__dict__
         sk = SnpKernel(bed, Unit())
         pk = sk._partitioned(np.float64)
         path = str(tmp_path / "k")

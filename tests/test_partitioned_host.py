@@ -76,3 +76,19 @@ def test_single_part_reads_only_its_blocks(n, parts):
                     with pytest.raises(ValueError, match="outside part %d of %d" % (p, parts)):
                         pk._check_owned(N.index_array(ri), N.index_array(ci))
         pk._check_owned(np.zeros(0, dtype=np.uint64), None)  # nothing asked, nothing needed
+
+
+def test_lone_part_refuses_whole_k_operations():
+    """A part of a plan of several, read without its group, holds only its share of the diagonal:
+    trace(K) and DiagKtoN must raise instead of scaling by a partial trace."""
+    from pysnptools_amd.kernelstandardizer import DiagKtoN, DiagKtoNTrained, Identity
+
+    pk = _view(5000, 1, 3)
+    with pytest.raises(ValueError, match="needs all of them"):
+        pk.trace()
+    with pytest.raises(ValueError, match="needs all of them"):
+        pk._read_with_standardizing(True, kernel_standardizer=DiagKtoN())
+    assert PartitionedKernel.supports(DiagKtoN()) and PartitionedKernel.supports(DiagKtoNTrained(2.0))
+    assert PartitionedKernel.supports(Identity()) and not PartitionedKernel.supports(object())
+    with pytest.raises(ValueError, match="supports the DiagKtoN"):
+        pk._read_with_standardizing(False, kernel_standardizer=object())
