@@ -1682,6 +1682,10 @@ int snpmi_set_kernel_variant(const char* kernel, int variant) {
         else if (std::strcmp(kernel, "dense_codes") == 0) g_dense_codes = variant;
         else if (std::strcmp(kernel, "seg") == 0) g_seg_snps = std::max(variant, 0);
         else if (std::strcmp(kernel, "gather") == 0) g_gather = variant;  // host gather A/B (0 mmap, 1 pread)
+        else if (std::strcmp(kernel, "crt") == 0) {
+            SNPMI_REQUIRE(variant == 0 || variant == 1, SNPMI_E_ARG, "crt residue SYRK: 0 = k_syrk_i8r, 1 = k_syrk_i8w");
+            g_crt_kernel = variant;
+        }
         else if (std::strcmp(kernel, "f64") == 0) {
             SNPMI_REQUIRE(variant == 0 || variant == 1, SNPMI_E_ARG, "f64 GRM path: 0 = int8 residues + CRT, 1 = f64 MFMA");
             g_f64_mfma = variant;
@@ -1706,6 +1710,7 @@ int snpmi_get_kernel_variant(const char* kernel, int* variant) {
         else if (std::strcmp(kernel, "dense_codes") == 0) *variant = g_dense_codes;
         else if (std::strcmp(kernel, "seg") == 0) *variant = g_seg_snps;
         else if (std::strcmp(kernel, "gather") == 0) *variant = g_gather;
+        else if (std::strcmp(kernel, "crt") == 0) *variant = g_crt_kernel;
         else if (std::strcmp(kernel, "f64") == 0) *variant = g_f64_mfma;
         else throw Error(SNPMI_E_ARG, std::string("unknown kernel ") + kernel);
     });

@@ -328,6 +328,124 @@ __global__ __launch_bounds__(512, 1) void k_syrk_i8r(const uint8_t* __restrict__
     crt_epilogue(acc, r, nblk, bx, wm, wn, lane, res);
 }
 
+// Warp-specialised form of k_syrk_i8r (round 6): the same block, LDS image and MFMA tiling, with
+// the loader moved out of the MFMA waves.  12 waves (3 per SIMD): waves 0-7 only read fragments
+// (ds_read_b64_tr_b8) and issue MFMAs; waves 8-11 (one per SIMD) expand stage s+1's codes into
+// the idle LDS buffer and issue stage s+2's code / LUT loads while the MFMA waves compute stage
+// s.  One barrier per stage, as before.  Cycle budget per 128-SNP stage and CU (MI355X_MICROARCH
+// §LDS): MFMA 2048 cycles per SIMD; fragment reads 8 waves x 4 k-steps x 12 ds_read_b64_tr_b8 x 2
+// = 768 LDS cycles; residue image 64 ds_write_b128 x 13 = 832 transfer cycles -- the same 1600 LDS
+// cycles, but the MFMA waves no longer issue the 13-cycle stores themselves, wait on code loads
+// (vmcnt) or spend their issue slots on the expansion VALU, which put 14% of their cycles in
+// SQ_WAIT_INST_LDS and 23% in SQ_WAIT_ANY (profiles/r05z/pmc_sq_crt.json).  The register budget of
+// 3 waves per SIMD (<= 168 VGPRs) leaves the MFMA waves single-buffered fragments for the A panel.
+template <int SKT>
+__global__ __launch_bounds__(768, 1) void k_syrk_i8w(const uint8_t* __restrict__ P, uint64_t pitch, uint64_t kdim,
+                                                     uint64_t mpad, const uint32_t* __restrict__ lutr,
+                                                     const int* __restrict__ ctl, uint64_t b0, uint64_t nblk,
+                                                     uint8_t* __restrict__ res,
+                                                     const uint32_t* __restrict__ part_tab = nullptr) {
+    constexpr int KS = SKT / 32, RPL = SKT / 8, PNL = SKT * RS, STG = 2 * PNL;
+    __shared__ __attribute__((aligned(16))) uint8_t lds[2 * STG];
+    if (ctl[1]) return;  // non-finite LUT: the f64 MFMA kernel runs instead
+    const uint32_t w = blockIdx.x, q = w >> 3, u = q / kR;
+    const uint32_t r = q - u * kR, bx = 8 * u + (w & 7);
+    if (bx >= nblk) return;
+    if ((int)r >= ctl[2]) return;  // K_int fits the first ctl[2] moduli
+    uint32_t bi, bj;
+    if (part_tab) {
+        const uint32_t c = part_tab[b0 + bx];
+        bi = c & 0xffffu;
+        bj = c >> 16;
+    } else {
+        tile_coords(b0 + bx, bi, bj);
+    }
+    const int t = threadIdx.x, lane = t & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+    const uint64_t nst = (kdim + SKT - 1) / SKT;
+    if (wave >= 8) {
+        // loader: thread lt = (panel lp, row block kq of RPL rows, 16-iid group d)
+        const int lt = t - 512;
+        const int lp = __builtin_amdgcn_readfirstlane(lt >> 7), kq = (lt >> 4) & 7, d = lt & 15;
+        const uint8_t* pbase = P + (uint64_t)(lp ? bj : bi) * (BW / 4);
+        const uint32_t pit = (uint32_t)pitch;
+        const uint32_t* lq = lutr + (uint64_t)r * mpad + RPL * kq;
+        uint32_t cw[RPL];
+        uint4 cl[RPL / 4];
+        auto load = [&](uint64_t st) {
+            const uint8_t* sb = pbase + st * SKT * pitch;
+            const uint32_t lim = (uint32_t)(kdim - 1 - st * SKT);
+#pragma unroll
+            for (int h = 0; h < RPL; h++) {
+                const uint32_t row = min((uint32_t)(RPL * kq + h), lim);
+                cw[h] = *reinterpret_cast<const uint32_t*>(sb + (row * pit + 4 * d));
+            }
+#pragma unroll
+            for (int v = 0; v < RPL / 4; v++) cl[v] = *reinterpret_cast<const uint4*>(lq + SKT * st + 4 * v);
+        };
+        auto store = [&](uint8_t* S) {
+#pragma unroll
+            for (int h = 0; h < RPL; h++) {
+                const uint4 c4 = cl[h >> 2];
+                const uint32_t L = (h & 3) == 0 ? c4.x : (h & 3) == 1 ? c4.y : (h & 3) == 2 ? c4.z : c4.w;
+                uint4 o;
+                o.x = __builtin_amdgcn_perm(L, L, cw[h] & 0x03030303u);
+                o.y = __builtin_amdgcn_perm(L, L, (cw[h] >> 2) & 0x03030303u);
+                o.z = __builtin_amdgcn_perm(L, L, (cw[h] >> 4) & 0x03030303u);
+                o.w = __builtin_amdgcn_perm(L, L, (cw[h] >> 6) & 0x03030303u);
+                *reinterpret_cast<uint4*>(S + lp * PNL + (RPL * kq + h) * RS + 16 * d) = o;
+            }
+        };
+        load(0);
+        store(lds);
+        load(nst > 1 ? 1 : 0);
+        __syncthreads();
+        for (uint64_t s = 0; s < nst; s++) {
+            store(lds + ((s + 1) & 1) * STG);  // stage s+1 (past the end: into the idle buffer, unread)
+            load(s + 2 < nst ? s + 2 : nst - 1);
+            __syncthreads();
+        }
+        return;
+    }
+    const int wm = wave >> 2, wn = wave & 3;
+    const int g = lane >> 4, jj = (lane & 15) >> 1, pp = lane & 1;
+    const int rd = (16 * (g >> 1) + jj) * RS + 16 * (g & 1) + 8 * pp;
+    v16i acc[4][2];
+#pragma unroll
+    for (int x = 0; x < 4; x++)
+#pragma unroll
+        for (int y = 0; y < 2; y++) acc[x][y] = (v16i){};
+    auto frag = [&](const uint8_t* S, int panel, int ks, int col) -> v4i {
+        const uint8_t* b = S + panel * PNL + 32 * ks * RS + rd + col;
+        const v2i x = lds_tr8(b), y = lds_tr8(b + 8 * RS);
+        return (v4i){x.x, x.y, y.x, y.y};
+    };
+    __syncthreads();
+    for (uint64_t s = 0; s < nst; s++) {
+        const uint8_t* cur = lds + (s & 1) * STG;
+        v4i b[2][2];
+#pragma unroll
+        for (int y = 0; y < 2; y++) b[0][y] = frag(cur, 1, 0, wn * 64 + 32 * y);
+#pragma unroll
+        for (int ks = 0; ks < KS; ks++) {
+            v4i a[4];
+#pragma unroll
+            for (int x = 0; x < 4; x++) a[x] = frag(cur, 0, ks, wm * 128 + 32 * x);
+            if (ks + 1 < KS) {
+#pragma unroll
+                for (int y = 0; y < 2; y++) b[(ks + 1) & 1][y] = frag(cur, 1, ks + 1, wn * 64 + 32 * y);
+            }
+#pragma unroll
+            for (int x = 0; x < 4; x++)
+#pragma unroll
+                for (int y = 0; y < 2; y++)
+                    acc[x][y] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[x], b[ks & 1][y], acc[x][y], 0, 0, 0);
+        }
+        __syncthreads();
+    }
+    crt_epilogue(acc, r, nblk, bx, wm, wn, lane, res);
+}
+
 // ---------------------------------------------------------------- reconstruction
 // two elements per thread (packed f32 math: v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32); the
 // residues of the R planes -> K_int (Garner, exact: all digit arithmetic is on integers < 2^24
@@ -465,6 +583,8 @@ int crt_fraction_bits(uint64_t m) {
     return std::min(52, (int)std::floor(f));
 }
 
+int g_crt_kernel = 0;  // hook "crt": 0 = k_syrk_i8r (loader in every wave), 1 = k_syrk_i8w (loader waves)
+
 uint64_t crt_max_snps() { return 1ull << 16; }  // keeps F >= 50 and the int32 sums exact
 int crt_moduli() { return kR; }
 
@@ -543,8 +663,12 @@ void launch_syrk_packed_crt(const uint8_t* packed, uint64_t pitch, uint64_t n, u
         SNPMI_REQUIRE(cnt < (1ull << 23), SNPMI_E_ARG, "crt SYRK: chunk too large");
         // the kR moduli of a block on one XCD at once (FETCH 951 -> 149 GB per 62.5k-SNP
         // launch at 50k iids, the clock 2.21 -> 2.36 GHz, -3.6%: profiles/r05m)
-        k_syrk_i8r<SK><<<(unsigned)(round_up(cnt, 8) * kR), 512, 0, st>>>(
-            packed, pitch, m, mpad, lutr, ctl, b0, cnt, res, part_tab);
+        if (g_crt_kernel == 1)
+            k_syrk_i8w<SK><<<(unsigned)(round_up(cnt, 8) * kR), 768, 0, st>>>(packed, pitch, m, mpad, lutr, ctl, b0,
+                                                                            cnt, res, part_tab);
+        else
+            k_syrk_i8r<SK><<<(unsigned)(round_up(cnt, 8) * kR), 512, 0, st>>>(packed, pitch, m, mpad, lutr, ctl, b0,
+                                                                            cnt, res, part_tab);
         k_crt<<<(unsigned)(cnt * 64), 256, 0, st>>>(res, b0, cnt, n, ctl, F, cc, tiles, accumulate, part_tab ? 1 : 0);
         if (after_chunk) {
             SNPMI_HIP(hipGetLastError());

@@ -144,3 +144,33 @@ def test_public_f64_switch_selects_the_f64_mfma():
     import pytest
     with pytest.raises(ValueError):
         pysnptools_amd.set_grm_f64("f32")
+
+
+@pytest.mark.parametrize("n,m,parts", [(300, 1015, 0), (1000, 129, 0), (4100, 3000, 0), (30000, 300, 0),
+                                       (2300, 700, 3)])
+def test_warp_specialised_residue_syrk_is_bit_identical(n, m, parts):
+    """k_syrk_i8w (hook "crt" = 1: loader waves beside the MFMA waves) produces the same residues as
+    k_syrk_i8r, hence the same f64 K bit for bit -- replicated tiles (one and several residue
+    chunks, stage counts 2..24, n not a multiple of 256) and a cfg5 part (part_tab layout)."""
+    from test_gpu_parity import Dev, synth_dev
+
+    buf, pitch = synth_dev(n, m, 31 + n)
+    lut, st = Dev(m * 32), Dev(m * 16)
+    N.call("snpmi_dev_snp_stats", buf.p, pitch, n, m, 0, N.STD_UNIT, 0.0, 0.0, 0, N.DT_F64, st.p, lut.p)
+    outs = []
+    for form in (0, 1):
+        N.call("snpmi_set_kernel_variant", b"crt", form)
+        try:
+            if parts:
+                nloc = N.lib().snpmi_grm_part_blocks(n, 1, parts)
+                k = Dev(nloc * 65536 * 8)
+                N.call("snpmi_dev_syrk_packed_part_f64", buf.p, pitch, n, m, lut.p, 1, parts, k.p, 0)
+                outs.append(k.get(np.empty(nloc * 65536, dtype=np.float64)))
+            else:
+                tb = N.lib().snpmi_grm_tile_bytes(n, N.DT_F64)
+                k = Dev(tb)
+                N.call("snpmi_dev_syrk_packed", buf.p, pitch, n, m, lut.p, N.DT_F64, k.p, 0)
+                outs.append(k.get(np.empty(tb // 8, dtype=np.float64)))
+        finally:
+            N.call("snpmi_set_kernel_variant", b"crt", 0)
+    assert outs[0].size and np.array_equal(outs[0], outs[1])
