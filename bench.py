@@ -1217,11 +1217,16 @@ def grm_entry(args, dist, r, dtype):
         roof = {"bound": "mfma", "achieved": r["mean_tflops"], "peak": peak, "unit": "TFLOP/s",
                 "frac": r["mean_tflops"] / peak, "per_launch_flops": n * (n + 1) * r["snps_per_launch"],
                 "traffic": pmc_traffic("f32w::k_syrk_h2", "grm", n, r["snps_per_launch"]),
-                "traffic_note": "PMC HBM bytes per launch (profiles/traffic.json) vs algorithmic ~2 x 5 GB of K tiles "
-                                "(accumulate read + write) + 0.8 GB of codes at 50k x 62.5k: the rest is the SegFlush "
-                                "slots (256 KiB per workgroup, flushed every 12288 SNPs by f32 atomics at L2 and read "
-                                "back once, DESIGN.md 3.4) and panel re-fetches from the MALL; the flushes cost "
-                                "1.6-3% of the launch (profiles/r05sc), the accuracy they buy is DESIGN.md 3.4's table",
+                "traffic_note": "PMC HBM bytes per launch (profiles/<PMC_PROFILE>/traffic.json) against ~10.8 GB "
+                                "algorithmic at 50k x 62.5k, split (DESIGN.md 3.4): K tiles 5.0 GB read (accumulate) + 5.0 GB "
+                                "written; SegFlush slots (256 KiB per workgroup, 19,306 workgroups, a flush every 12,288 SNPs = "
+                                "5 rounds: one store, four rounds of f32 atomics, one read back) ~25 GB written + ~25 GB read "
+                                "between L2 and the memory side (the 256 MiB slot pool sits in the MALL, which the TCC "
+                                "counters see as HBM traffic); codes 0.8 GB + their panel re-fetches "
+                                "~5 GB.  The flush machinery costs 1.6-3% of the launch's time (profiles/r05sc), the f32 "
+                                "accuracy it buys is DESIGN.md 3.4's table",
+                "traffic_split_gb": {"K_read": 5.0, "K_write": 5.0, "slots_write": 25.3, "slots_read": 25.3,
+                                     "codes_and_panel_refetch": 6.0, "source": "PMC r05z: read 36.1 GB, write 30.7 GB"},
                 "kernel": "f32w::k_syrk_h2<false,4>: f32 GRM as 3 fp16 MFMA products of each value's fp16x2 "
                           "split, f32 accumulate (v_mfma_f32_32x32x16_f16); peak = 2.5 PF fp16 dense / 3; the timed "
                           "span also holds k_snp_stats, k_lut_bf3, k_lut_h2 and the range-gated bf16x3 launch (exits "

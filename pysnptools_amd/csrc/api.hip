@@ -1682,8 +1682,12 @@ int snpmi_set_kernel_variant(const char* kernel, int variant) {
         else if (std::strcmp(kernel, "dense_codes") == 0) g_dense_codes = variant;
         else if (std::strcmp(kernel, "seg") == 0) g_seg_snps = std::max(variant, 0);
         else if (std::strcmp(kernel, "gather") == 0) g_gather = variant;  // host gather A/B (0 mmap, 1 pread)
+        else if (std::strcmp(kernel, "h2") == 0) {
+            SNPMI_REQUIRE(variant == 0 || variant == 1, SNPMI_E_ARG, "h2 SYRK: 0 = k_syrk_h2, 1 = k_syrk_h2s");
+            g_h2_kernel = variant;
+        }
         else if (std::strcmp(kernel, "crt") == 0) {
-            SNPMI_REQUIRE(variant == 0 || variant == 1, SNPMI_E_ARG, "crt residue SYRK: 0 = k_syrk_i8r, 1 = k_syrk_i8w");
+            SNPMI_REQUIRE(variant >= 0 && variant <= 5, SNPMI_E_ARG, "crt residue SYRK: 0 = k_syrk_i8r, 1 = k_syrk_i8w");
             g_crt_kernel = variant;
         }
         else if (std::strcmp(kernel, "f64") == 0) {
@@ -1711,6 +1715,7 @@ int snpmi_get_kernel_variant(const char* kernel, int* variant) {
         else if (std::strcmp(kernel, "seg") == 0) *variant = g_seg_snps;
         else if (std::strcmp(kernel, "gather") == 0) *variant = g_gather;
         else if (std::strcmp(kernel, "crt") == 0) *variant = g_crt_kernel;
+        else if (std::strcmp(kernel, "h2") == 0) *variant = g_h2_kernel;
         else if (std::strcmp(kernel, "f64") == 0) *variant = g_f64_mfma;
         else throw Error(SNPMI_E_ARG, std::string("unknown kernel ") + kernel);
     });

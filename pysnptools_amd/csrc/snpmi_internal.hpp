@@ -125,6 +125,7 @@ extern int g_variant_std;
 extern int g_variant_extract;
 extern int g_variant_syrk;
 extern int g_dense_chunk;
+extern int g_h2_kernel;  // packed fp16x2 SYRK form (hook "h2"): 0 = k_syrk_h2, 1 = warp-specialised k_syrk_h2s
 // f32 GRM accumulation segments (syrk.hip SegFlush): every `snps` SNPs a workgroup adds its MFMA
 // accumulators into a private scratch slot (register-native layout, 256 KiB: 8 waves x 32 x 64
 // lanes x 16 B) and restarts them, so no f32 chain is longer than `snps`; the slot is taken from a

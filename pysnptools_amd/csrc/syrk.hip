@@ -1594,6 +1594,150 @@ __global__ __launch_bounds__(512, 1) void k_syrk_h2(const uint8_t* __restrict__ 
     sf.release(seg);
 }
 
+// Warp-specialised k_syrk_h2 (MODE 4 layout, round 6): the same block, products, LDS image (ROT
+// rotation) and SegFlush, with the loader moved out of the MFMA waves.  12 waves (3 per SIMD):
+// waves 0-7 only read fragments (ds_read_b64_tr_b16) and issue the 3 x 8 MFMAs of each 16-SNP
+// k-step; waves 8-11 (one per SIMD) expand stage s+1's codes into the idle LDS buffer -- 4 SNP rows
+// x 2 planes per thread and stage, ds_write_b64 -- and issue stage s+2's code / LUT loads while the
+// MFMA waves compute stage s.  One barrier per 32-SNP stage, as in MODE 4.  Register budget of 3
+// waves per SIMD (<= 168): the MFMA waves hold each k-step's B planes and ONE A plane at a time.
+template <bool LOCAL = false>
+__global__ __launch_bounds__(768, 1) void k_syrk_h2s(const uint8_t* __restrict__ P, uint64_t pitch, uint64_t n,
+                                                     uint64_t kdim, const uint32_t* __restrict__ lut2,
+                                                     const uint32_t* __restrict__ flag, float* __restrict__ tiles,
+                                                     int accumulate, uint32_t part_rank = 0, uint32_t part_world = 1,
+                                                     uint64_t kslice = 0, uint64_t slice_elems = 0,
+                                                     SegCtx seg = SegCtx(), const uint32_t* __restrict__ order = nullptr,
+                                                     uint64_t wg0 = 0) {
+    constexpr int KS = 2, SBK = KS * BK;
+    constexpr int PLANE = KS * B3_PLANE, STAGE = 2 * 2 * PLANE;
+    __shared__ __attribute__((aligned(16))) short lds[2 * STAGE];
+    if (*flag) return;  // a SNP of this block is outside fp16's range: k_syrk_bf3 runs instead
+    if (gridDim.y > 1) {
+        const uint64_t k0 = (uint64_t)blockIdx.y * kslice;
+        P += k0 * pitch;
+        lut2 += 4 * k0;
+        kdim = min(kslice, kdim - k0);
+        tiles += (uint64_t)blockIdx.y * slice_elems;
+    }
+    const uint64_t wg = wg0 + blockIdx.x;
+    uint32_t bi, bj;
+    if (LOCAL || order) {
+        const uint32_t c = order[wg];
+        bi = c & 0xffffu;
+        bj = c >> 16;
+    } else {
+        tile_coords(wg, bi, bj);
+    }
+    const uint64_t blk = wg;
+    const int t = threadIdx.x, lane = t & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+    const uint64_t nst = (kdim + SBK - 1) / SBK;
+    __shared__ uint32_t seg_slot;
+    SegFlush sf(seg, 2 * SBK, blk, (nst + 1) / 2, &seg_slot);  // every wave: it holds a barrier
+    if (wave >= 8) {
+        // loader thread lt = (panel lp, SNP rows lk + 8u of the stage (u < 4), 16-iid group ld_)
+        const int lt = t - 512;
+        const int lp = __builtin_amdgcn_readfirstlane(lt >> 7), lk = (lt >> 4) & 7, ld_ = lt & 15;
+        const uint64_t c0 = (uint64_t)(lp ? bj : bi) * BW;
+        const uint8_t* wp = P + c0 / 4 + 4 * ld_ + (uint64_t)lk * pitch;
+        const uint8_t* wlast = P + c0 / 4 + 4 * ld_ + (kdim - 1) * pitch;
+        const int wrot = (ld_ >> 2) & 3;
+        uint32_t rw[4];
+        uint4 rl[4];
+        auto load = [&](uint64_t st) {
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const uint8_t* a = wp + (st * SBK + 8 * u) * pitch;
+                rw[u] = *reinterpret_cast<const uint32_t*>(a <= wlast ? a : wlast);
+                rl[u] = *reinterpret_cast<const uint4*>(lut2 + 4 * (SBK * st + lk + 8 * u));
+            }
+        };
+        auto store = [&](short* S) {
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                uint32_t sel[8];
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    const uint32_t v = (rw[u] >> (2 * j)) & 0x03030303u;
+                    const uint32_t o = v | 0x04040404u;
+                    sel[2 * j] = __builtin_amdgcn_perm(o, v, 0x05010400u);
+                    sel[2 * j + 1] = __builtin_amdgcn_perm(o, v, 0x07030602u);
+                }
+#pragma unroll
+                for (int pl = 0; pl < 2; pl++) {
+                    const uint32_t lo = pl == 0 ? rl[u].x : rl[u].z;
+                    const uint32_t hi = pl == 0 ? rl[u].y : rl[u].w;
+                    typedef __attribute__((address_space(3))) volatile uint64_t lds_u64;
+                    lds_u64* q = (lds_u64*)(S + (lp * 2 + pl) * PLANE + (lk + 8 * u) * B3_RS + 16 * ld_);
+#pragma unroll
+                    for (int j = 0; j < 4; j++)
+                        q[(wrot + j) & 3] = (uint64_t)__builtin_amdgcn_perm(hi, lo, sel[2 * j]) |
+                                            ((uint64_t)__builtin_amdgcn_perm(hi, lo, sel[2 * j + 1]) << 32);
+                }
+            }
+        };
+        load(0);
+        store(lds);
+        load(nst > 1 ? 1 : 0);
+        __syncthreads();
+        for (uint64_t s = 0; s < nst; s++) {
+            store(lds + ((s + 1) & 1) * STAGE);  // stage s+1 (past the end: the idle buffer, unread)
+            load(s + 2 < nst ? s + 2 : nst - 1);
+            __syncthreads();
+        }
+        sf.release(seg);
+        return;
+    }
+    const int wm = wave >> 2, wn = wave & 3;
+    const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
+    const int rd_base = (8 * (g >> 1) + q) * B3_RS + 16 * (g & 1);
+    const int rd_offA0 = rd_base + 4 * ((pp + 2 * wm) & 3), rd_offA1 = rd_base + 4 * ((pp + 2 * wm + 1) & 3);
+    const int rd_offB = rd_base + 4 * ((pp + wn) & 3);
+    f32x16 acc[4][2];
+#pragma unroll
+    for (int x = 0; x < 4; x++)
+#pragma unroll
+        for (int y = 0; y < 2; y++) acc[x][y] = (f32x16){};
+    auto frag = [&](const short* S, int panel, int pl, int h, int col, int off) -> f16x8_t {
+        const short* b = S + (panel * 2 + pl) * PLANE + h * BK * B3_RS + off + col;
+        const i16x4_t r0 = lds_tr16(b), r1 = lds_tr16(b + 4 * B3_RS);
+        return __builtin_bit_cast(f16x8_t, (i16x8_t)__builtin_shufflevector(r0, r1, 0, 1, 2, 3, 4, 5, 6, 7));
+    };
+    auto group = [&](const f16x8_t (&a)[4], const f16x8_t (&b)[2]) {
+#pragma unroll
+        for (int x = 0; x < 4; x++)
+#pragma unroll
+            for (int y = 0; y < 2; y++)
+                acc[x][y] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[x], b[y], acc[x][y], 0, 0, 0);
+    };
+    __syncthreads();
+    for (uint64_t s = 0; s < nst; s++) {
+        const short* cur = lds + (s & 1) * STAGE;
+#pragma unroll
+        for (int h = 0; h < KS; h++) {
+            f16x8_t A[4], B0[2], B1[2];
+#pragma unroll
+            for (int y = 0; y < 2; y++) {
+                B0[y] = frag(cur, 1, 0, h, wn * 64 + 32 * y, rd_offB);
+                B1[y] = frag(cur, 1, 1, h, wn * 64 + 32 * y, rd_offB);
+            }
+#pragma unroll
+            for (int x = 0; x < 4; x++) A[x] = frag(cur, 0, 0, h, wm * 128 + 32 * x, x >= 2 ? rd_offA1 : rd_offA0);
+            group(A, B0);
+            group(A, B1);
+#pragma unroll
+            for (int x = 0; x < 4; x++) A[x] = frag(cur, 0, 1, h, wm * 128 + 32 * x, x >= 2 ? rd_offA1 : rd_offA0);
+            group(A, B0);
+        }
+        __syncthreads();
+        if ((s & 1) && sf.due(s + 1 < nst)) sf.flush(acc);
+    }
+    sf.finish(acc);
+    epilogue_pi<LOCAL>(acc, tiles, n, bi, bj, accumulate, lane, wm, wn, blk);
+    sf.release(seg);
+}
+
 // ---------------------------------------------------------------- fp16x2 on v_mfma_f32_16x16x32_f16
 // Same products (A0 B0 + A0 B1 + A1 B0), loader and LDS image as k_syrk_h2 MODE 4, but every MFMA
 // is 16x16x32 instead of 32x32x16: the same cycles per FLOP and the same LDS bytes per FLOP
@@ -2744,6 +2888,7 @@ static const uint32_t* ub_order(uint64_t nb, bool xcd) {
 }
 #endif
 
+int g_h2_kernel = 0;  // hook "h2": 0 = k_syrk_h2 MODE 4 (loader in every wave), 1 = k_syrk_h2s (loader waves)
 int g_dense_chunk = 0;  // tuning / test hook (snpmi_set_kernel_variant "dense_chunk"): force chunk SNPs
 
 uint64_t dense_h2_chunk_snps(uint64_t n) {
@@ -2871,9 +3016,14 @@ void launch_syrk_packed_bf3(const uint8_t* packed, uint64_t pitch, uint64_t n, u
                 // supertile block order: the ~256 blocks in flight share ~32 code panels instead of
                 // ~nb (+1.7-2.4% at 50k x 31.25k / 62.5k vs the triangular order,
                 // profiles/r03crt/ubench_block_order.jsonl)
-                f32w::k_syrk_h2<false, 4><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles,
-                                                                      accumulate, 0, 1, 0, 0, seg_ctx(),
-                                                                      packed_block_order(ceil_div(n, 256)));
+                if (g_h2_kernel == 1)
+                    f32w::k_syrk_h2s<false><<<(unsigned)g, 768, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles,
+                                                                        accumulate, 0, 1, 0, 0, seg_ctx(),
+                                                                        packed_block_order(ceil_div(n, 256)));
+                else
+                    f32w::k_syrk_h2<false, 4><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles,
+                                                                          accumulate, 0, 1, 0, 0, seg_ctx(),
+                                                                          packed_block_order(ceil_div(n, 256)));
         }
         SNPMI_HIP(hipGetLastError());
         f32w::k_syrk_bf3<false, false, 5><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, lut3, tiles, accumulate, 0, 1, 0, 0,
@@ -2910,9 +3060,14 @@ void launch_syrk_packed_h2_cols(const uint8_t* packed, uint64_t pitch, uint64_t 
     SNPMI_REQUIRE(h2 && L0 < L1 && L1 <= g && g < (1ull << 31), SNPMI_E_ARG, "bad SYRK column group");
     SNPMI_REQUIRE(pitch % 64 == 0 && pitch * 4 >= nb * 256, SNPMI_E_ARG, "packed pitch must cover round_up(n, 256) iids");
     if (m == 0) return;
-    f32w::k_syrk_h2<false, 4><<<(unsigned)(L1 - L0), 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles,
-                                                                  accumulate, 0, 1, 0, 0, seg_ctx(),
-                                                                  packed_block_order(nb), L0);
+    if (g_h2_kernel == 1)
+        f32w::k_syrk_h2s<false><<<(unsigned)(L1 - L0), 768, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles,
+                                                                    accumulate, 0, 1, 0, 0, seg_ctx(),
+                                                                    packed_block_order(nb), L0);
+    else
+        f32w::k_syrk_h2<false, 4><<<(unsigned)(L1 - L0), 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles,
+                                                                      accumulate, 0, 1, 0, 0, seg_ctx(),
+                                                                      packed_block_order(nb), L0);
     SNPMI_HIP(hipGetLastError());
     f32w::k_syrk_bf3<false, false, 5><<<(unsigned)(L1 - L0), 512, 0, st>>>(packed, pitch, n, m, lut3, tiles, accumulate,
                                                                           0, 1, 0, 0, h2->flag, seg_ctx(), L0);
@@ -2955,8 +3110,12 @@ void launch_syrk_packed_bf3_part(const uint8_t* packed, uint64_t pitch, uint64_t
     }
     const uint32_t* tab = part_tables(ceil_div(n, 256), rank, world).tab;
     if (h2) {
-        f32w::k_syrk_h2<true><<<(unsigned)nloc, 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, blocks, accumulate,
-                                                               0, 1, 0, 0, seg_ctx(), tab);
+        if (g_h2_kernel == 1)
+            f32w::k_syrk_h2s<true><<<(unsigned)nloc, 768, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, blocks,
+                                                                  accumulate, 0, 1, 0, 0, seg_ctx(), tab);
+        else
+            f32w::k_syrk_h2<true><<<(unsigned)nloc, 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, blocks,
+                                                                  accumulate, 0, 1, 0, 0, seg_ctx(), tab);
         SNPMI_HIP(hipGetLastError());
     }
     f32w::k_syrk_bf3<true, false, 5><<<(unsigned)nloc, 512, 0, st>>>(packed, pitch, n, m, lut3, blocks, accumulate,

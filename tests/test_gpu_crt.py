@@ -158,7 +158,7 @@ def test_warp_specialised_residue_syrk_is_bit_identical(n, m, parts):
     lut, st = Dev(m * 32), Dev(m * 16)
     N.call("snpmi_dev_snp_stats", buf.p, pitch, n, m, 0, N.STD_UNIT, 0.0, 0.0, 0, N.DT_F64, st.p, lut.p)
     outs = []
-    for form in (0, 1):
+    for form in (0, 1, 4):
         N.call("snpmi_set_kernel_variant", b"crt", form)
         try:
             if parts:
@@ -173,4 +173,4 @@ def test_warp_specialised_residue_syrk_is_bit_identical(n, m, parts):
                 outs.append(k.get(np.empty(tb // 8, dtype=np.float64)))
         finally:
             N.call("snpmi_set_kernel_variant", b"crt", 0)
-    assert outs[0].size and np.array_equal(outs[0], outs[1])
+    assert outs[0].size and all(np.array_equal(outs[0], o) for o in outs[1:])

@@ -27,14 +27,18 @@ def main():
     p.add_argument("--rounds", type=int, default=3)
     p.add_argument("--forms", default="0,1")
     p.add_argument("--miss", type=float, default=0.01)
+    p.add_argument("--dtype", choices=["f32", "f64"], default="f64",
+                   help="f64: the residue SYRK forms (hook crt); f32: the fp16x2 SYRK forms (hook h2)")
     a = p.parse_args()
+    hook = b"crt" if a.dtype == "f64" else b"h2"
+    dt, esz = (N.DT_F64, 8) if a.dtype == "f64" else (N.DT_F32, 4)
     n, m = a.n, a.m
     pitch = N.lib().snpmi_packed_pitch(n)
     packed = Dev(N, pitch * m)
     synth(N, packed.p, pitch, n, 0, m, 105, a.miss)
-    lut, st = Dev(N, m * 32), Dev(N, m * 16)
-    N.call("snpmi_dev_snp_stats", packed.p, pitch, n, m, 0, N.STD_UNIT, 0.0, 0.0, 0, N.DT_F64, st.p, lut.p)
-    tb = N.lib().snpmi_grm_tile_bytes(n, N.DT_F64)
+    lut, st = Dev(N, m * 4 * esz), Dev(N, m * 2 * esz)
+    N.call("snpmi_dev_snp_stats", packed.p, pitch, n, m, 0, N.STD_UNIT, 0.0, 0.0, 0, dt, st.p, lut.p)
+    tb = N.lib().snpmi_grm_tile_bytes(n, dt)
     tiles = Dev(N, tb)
     forms = [int(f) for f in a.forms.split(",")]
     ev = Events(N, 2)
@@ -43,30 +47,36 @@ def main():
     sum_r, nl = ctypes.c_uint64(), ctypes.c_uint64()
     for rnd in range(a.rounds + 1):  # round 0: warm-up (scratch allocations, code objects)
         for f in forms:
-            N.call("snpmi_set_kernel_variant", b"crt", f)
+            N.call("snpmi_set_kernel_variant", hook, f)
             N.call("snpmi_crt_moduli_stats", ctypes.byref(sum_r), ctypes.byref(nl), 1)
             ev.record(0)
-            N.call("snpmi_dev_syrk_packed", packed.p, pitch, n, m, lut.p, N.DT_F64, tiles.p, 0)
+            N.call("snpmi_dev_syrk_packed", packed.p, pitch, n, m, lut.p, dt, tiles.p, 0)
             ev.record(1)
             N.call("snpmi_stream_sync")
             if rnd:
                 res[f].append(ev.ms(0, 1))
             else:
-                h = np.empty(tb // 8, dtype=np.float64)
-                N.call("snpmi_memcpy_d2h", N.ptr(h), tiles.p, tb)
-                sums[f] = (float(np.sum(h)), float(np.sum(h * np.arange(h.size) % 977)))
+                # the first and last 32M tile elements (512 MiB) compared with form 0's, bit for bit
+                k = min(tb // esz, 1 << 25)
+                h = np.empty(2 * k, dtype=np.float64 if esz == 8 else np.float32)
+                N.call("snpmi_memcpy_d2h", N.ptr(h[:k]), tiles.p, k * esz)
+                N.call("snpmi_memcpy_d2h", N.ptr(h[k:]), ctypes.c_void_p(tiles.p.value + tb - k * esz), k * esz)
+                sums[f] = h
                 N.call("snpmi_crt_moduli_stats", ctypes.byref(sum_r), ctypes.byref(nl), 0)
-    N.call("snpmi_set_kernel_variant", b"crt", 0)
-    R = sum_r.value / max(nl.value, 1)
+            print(json.dumps({"round": rnd, "form": f, "ms": ev.ms(0, 1)}), file=sys.stderr, flush=True)
+    N.call("snpmi_set_kernel_variant", hook, 0)
+    # executed MFMA work: f64 = R int8 SYRKs (5.0 POP/s dense); f32 = 3 fp16 products (2.5 PF/s dense)
+    R, peak = (sum_r.value / max(nl.value, 1), 5000.0) if a.dtype == "f64" else (3.0, 2500.0)
     nb = (n + 255) // 256
     ops = R * 2 * 256 * 256 * (nb * (nb + 1) // 2) * m
     base = sums[forms[0]]
     for f in forms:
         t = float(np.median(res[f]))
-        print(json.dumps({"form": f, "kernel": "k_syrk_i8r" if f == 0 else "k_syrk_i8w", "n": n, "m": m,
-                          "median_ms": t, "all_ms": res[f], "moduli": R, "int8_tops": ops / t / 1e9,
-                          "frac_int8_peak": ops / t / 1e9 / 5000.0, "f64_equiv_tflops": n * (n + 1) * m / t / 1e9,
-                          "tiles_equal_form0": sums[f] == base}), flush=True)
+        names = {b"crt": {0: "k_syrk_i8r", 1: "k_syrk_i8w"}, b"h2": {0: "k_syrk_h2<.,4>", 1: "k_syrk_h2s"}}[hook]
+        print(json.dumps({"form": f, "kernel": names.get(f, "ablation %d" % f), "dtype": a.dtype, "n": n, "m": m,
+                          "median_ms": t, "all_ms": res[f], "moduli": R if a.dtype == "f64" else None,
+                          "frac_mfma_peak_executed": ops / t / 1e9 / peak, "syrk_tflops": n * (n + 1) * m / t / 1e9,
+                          "tiles_equal_form0": bool(np.array_equal(sums[f], base))}), flush=True)
 
 
 if __name__ == "__main__":
