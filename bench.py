@@ -1188,7 +1188,7 @@ def input_sha256(sample, n):
     return hashlib.sha256(np.ascontiguousarray(sample[:, :(n + 3) // 4]).tobytes()).hexdigest()
 
 
-PMC_PROFILE = "r05z"  # this round's PMC passes (tools/profile_r04.sh -> profiles/<PMC_PROFILE>/traffic.json)
+PMC_PROFILE = "r06p"  # this round's PMC passes (tools/profile_r06.sh -> profiles/<PMC_PROFILE>/traffic.json)
 
 
 def pmc_traffic(kernel, leg, n_iid, block):
@@ -1216,7 +1216,7 @@ def grm_entry(args, dist, r, dtype):
         peak = SPLIT_PEAK_TFLOPS
         roof = {"bound": "mfma", "achieved": r["mean_tflops"], "peak": peak, "unit": "TFLOP/s",
                 "frac": r["mean_tflops"] / peak, "per_launch_flops": n * (n + 1) * r["snps_per_launch"],
-                "traffic": pmc_traffic("f32w::k_syrk_h2", "grm", n, r["snps_per_launch"]),
+                "traffic": pmc_traffic("f32w::k_syrk_h2s", "grm", n, r["snps_per_launch"]),
                 "traffic_note": "PMC HBM bytes per launch (profiles/<PMC_PROFILE>/traffic.json) against ~10.8 GB "
                                 "algorithmic at 50k x 62.5k, split (DESIGN.md 3.4): K tiles 5.0 GB read (accumulate) + 5.0 GB "
                                 "written; SegFlush slots (256 KiB per workgroup, 19,306 workgroups, a flush every 12,288 SNPs = "
@@ -1227,7 +1227,8 @@ def grm_entry(args, dist, r, dtype):
                                 "accuracy it buys is DESIGN.md 3.4's table",
                 "traffic_split_gb": {"K_read": 5.0, "K_write": 5.0, "slots_write": 25.3, "slots_read": 25.3,
                                      "codes_and_panel_refetch": 6.0, "source": "PMC r05z: read 36.1 GB, write 30.7 GB"},
-                "kernel": "f32w::k_syrk_h2<false,4>: f32 GRM as 3 fp16 MFMA products of each value's fp16x2 "
+                "kernel": "f32w::k_syrk_h2s<false> (warp-specialised: 8 MFMA waves + 4 loader waves per 256x256 "
+                          "block): f32 GRM as 3 fp16 MFMA products of each value's fp16x2 "
                           "split, f32 accumulate (v_mfma_f32_32x32x16_f16); peak = 2.5 PF fp16 dense / 3; the timed "
                           "span also holds k_snp_stats, k_lut_bf3, k_lut_h2 and the range-gated bf16x3 launch (exits "
                           "at once for Unit) of each launch",
@@ -1244,7 +1245,8 @@ def grm_entry(args, dist, r, dtype):
                 "f64_equiv_tflops": r["mean_tflops"], "f64_mfma_peak": MFMA_F64_PEAK_TFLOPS,
                 "vs_f64_mfma_peak": r["mean_tflops"] / MFMA_F64_PEAK_TFLOPS,
                 "moduli_per_block": R, "moduli_max": CRT_MODULI,
-                "kernel": "k_syrk_i8r (v_mfma_i32_32x32x32_i8; grid = 256-blocks of a tile chunk x 15 moduli, those "
+                "kernel": "k_syrk_i8w (warp-specialised: 8 MFMA waves + 4 loader waves; v_mfma_i32_32x32x32_i8; "
+                          "grid = 256-blocks of a tile chunk x 15 moduli, those "
                           "past the block's R exit at once) + k_crt (Garner over R digits) + k_crt_exp/k_crt_lut/"
                           "k_crt_bound/k_crt_r; achieved = executed int8 ops (R moduli x full 256-blocks) / the whole "
                           "timed span"}
@@ -1604,7 +1606,7 @@ def run_legs(N, args, dist):
             roof5 = {"bound": "mfma", "achieved": ops5 / busy_s / 1e12, "peak": MFMA_I8_PEAK_TOPS, "unit": "TOP/s",
                      "frac": ops5 / busy_s / 1e12 / MFMA_I8_PEAK_TOPS, "traffic": None,
                      "f64_equiv_tflops": syrk_tf, "f64_mfma_peak": MFMA_F64_PEAK_TFLOPS, "moduli_per_block": R5,
-                     "kernel": "k_syrk_i8r in part mode (int8 residues of the quantised LUT, R moduli per block) + "
+                     "kernel": "k_syrk_i8w in part mode (int8 residues of the quantised LUT, R moduli per block) + "
                                "k_crt into the part's f64 blocks; time = the blocks' compute-stream spans (stats + CRT "
                                "SYRK%s)" % (" + all-gather" if gather else "")}
         grm5 = {"workload": "cfg5: %d iid x %d SNP, Unit, %s, %.1f%% missing; K as 256x256 blocks in "
@@ -1627,7 +1629,7 @@ def run_legs(N, args, dist):
                 "K_bytes_per_rank": r3["n_local_blocks"] * 256 * 256 * r3["dtype"].itemsize,
                 "roofline": {"bound": "mfma", "achieved": syrk_tf, "peak": SPLIT_PEAK_TFLOPS, "unit": "TFLOP/s",
                              "frac": syrk_tf / SPLIT_PEAK_TFLOPS, "traffic": None,
-                             "kernel": "f32w::k_syrk_h2<true,4> (fp16x2 split, 3 fp16 MFMA products, f32 "
+                             "kernel": "f32w::k_syrk_h2s<true> (warp-specialised; fp16x2 split, 3 fp16 MFMA products, f32 "
                                        "accumulate), this part's blocks only; time = the blocks' compute-stream "
                                        "spans (stats + SYRK%s)" % (" + all-gather" if gather else "")}}
         if f64_5:

@@ -2888,7 +2888,9 @@ static const uint32_t* ub_order(uint64_t nb, bool xcd) {
 }
 #endif
 
-int g_h2_kernel = 0;  // hook "h2": 0 = k_syrk_h2 MODE 4 (loader in every wave), 1 = k_syrk_h2s (loader waves)
+// hook "h2": 1 = k_syrk_h2s (loader waves, default: 256.6 vs 270.0 ms per 50k x 62.5k launch in one
+// process, profiles/r06g), 0 = k_syrk_h2 MODE 4 (loader in every wave)
+int g_h2_kernel = 1;
 int g_dense_chunk = 0;  // tuning / test hook (snpmi_set_kernel_variant "dense_chunk"): force chunk SNPs
 
 uint64_t dense_h2_chunk_snps(uint64_t n) {

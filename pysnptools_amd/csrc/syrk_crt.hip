@@ -339,7 +339,7 @@ __global__ __launch_bounds__(512, 1) void k_syrk_i8r(const uint8_t* __restrict__
 // (vmcnt) or spend their issue slots on the expansion VALU, which put 14% of their cycles in
 // SQ_WAIT_INST_LDS and 23% in SQ_WAIT_ANY (profiles/r05z/pmc_sq_crt.json).  The register budget of
 // 3 waves per SIMD (<= 168 VGPRs) leaves the MFMA waves single-buffered fragments for the A panel.
-template <int SKT, int ABL = 0, int ST = 0>
+template <int SKT>
 __global__ __launch_bounds__(768, 1) void k_syrk_i8w(const uint8_t* __restrict__ P, uint64_t pitch, uint64_t kdim,
                                                      uint64_t mpad, const uint32_t* __restrict__ lutr,
                                                      const int* __restrict__ ctl, uint64_t b0, uint64_t nblk,
@@ -363,65 +363,6 @@ __global__ __launch_bounds__(768, 1) void k_syrk_i8w(const uint8_t* __restrict__
     const int t = threadIdx.x, lane = t & 63;
     const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
     const uint64_t nst = (kdim + SKT - 1) / SKT;
-    if (wave >= 8 && ST == 3) {
-        // row-per-lane-dword loader: loader wave lw expands rows 64 (lw & 1) .. +63 of panel lw >> 1;
-        // lane L makes LDS dword L of a row (the 4 iids 16 (L >> 2) + (L & 3) + {0, 4, 8, 12}, the
-        // pi16 layout of the ds_write_b128 loader) from code dword L >> 2 of the row and the row's
-        // LUT word (wave-uniform: scalar loads), and stores it with ds_write_addtid_b32 (LDS address
-        // = M0 + offset + 4 lane, no address VGPR): 2 transfer cycles per 256-B row against 13 per
-        // 1 KiB for ds_write_b128 (MI355X_MICROARCH §LDS).  M0 is set once per 8 rows, the row
-        // offsets are instruction immediates.
-        constexpr int RPW = SKT / 2;
-        const int lw = wave - 8, lpw = lw >> 1, r0 = RPW * (lw & 1);
-        const uint8_t* pbu = P + (uint64_t)(lpw ? bj : bi) * (BW / 4);
-        const uint32_t* lr = lutr + (uint64_t)r * mpad + r0;
-        const uint32_t loff = 4 * (lane >> 2), sh = 2 * (lane & 3);
-        uint32_t cwa[RPW];
-        uint64_t ls = 0;  // stage whose codes cwa holds
-        auto load = [&](uint64_t st) {
-            const uint32_t lim = (uint32_t)kdim - 1 - (uint32_t)st * SKT;
-            const __amdgpu_buffer_rsrc_t rs =
-                __builtin_amdgcn_make_buffer_rsrc(sgpr_ptr(pbu + st * SKT * pitch), (short)0, (int)0x7ffffff0, 0x00020000);
-#pragma unroll
-            for (int i = 0; i < RPW; i++) {
-                const uint32_t row = min((uint32_t)(r0 + i), lim);
-                cwa[i] = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)loff, (int)(row * (uint32_t)pitch), 0);
-            }
-            ls = st;
-        };
-        auto store = [&](uint8_t* S) {
-            const uint32_t* lst = lr + ls * SKT;  // wave-uniform: the compiler's scalar loads
-            const uint32_t base = (uint32_t)(uintptr_t)(S + lpw * PNL + r0 * RS);
-            uint32_t v[RPW];
-#pragma unroll
-            for (int i = 0; i < RPW; i++) {
-                const uint32_t L = __builtin_amdgcn_readfirstlane(lst[i]);
-                v[i] = __builtin_amdgcn_perm(L, L, (cwa[i] >> sh) & 0x03030303u);
-            }
-#pragma unroll
-            for (int g8 = 0; g8 < RPW / 8; g8++) {
-                asm volatile(
-                    "s_mov_b32 m0, %0\n\ts_nop 0\n\t"
-                    "ds_write_addtid_b32 %1\n\tds_write_addtid_b32 %2 offset:288\n\t"
-                    "ds_write_addtid_b32 %3 offset:576\n\tds_write_addtid_b32 %4 offset:864\n\t"
-                    "ds_write_addtid_b32 %5 offset:1152\n\tds_write_addtid_b32 %6 offset:1440\n\t"
-                    "ds_write_addtid_b32 %7 offset:1728\n\tds_write_addtid_b32 %8 offset:2016" ::"s"(base + 8 * g8 * RS),
-                    "v"(v[8 * g8]), "v"(v[8 * g8 + 1]), "v"(v[8 * g8 + 2]), "v"(v[8 * g8 + 3]), "v"(v[8 * g8 + 4]),
-                    "v"(v[8 * g8 + 5]), "v"(v[8 * g8 + 6]), "v"(v[8 * g8 + 7])
-                    : "memory", "m0");
-            }
-        };
-        load(0);
-        store(lds);
-        load(nst > 1 ? 1 : 0);
-        __syncthreads();
-        for (uint64_t s = 0; s < nst; s++) {
-            store(lds + ((s + 1) & 1) * STG);
-            load(s + 2 < nst ? s + 2 : nst - 1);
-            __syncthreads();
-        }
-        return;
-    }
     if (wave >= 8) {
         // loader: thread lt = (panel lp, row block kq of RPL rows, 16-iid group d)
         const int lt = t - 512;
@@ -452,14 +393,7 @@ __global__ __launch_bounds__(768, 1) void k_syrk_i8w(const uint8_t* __restrict__
                 o.y = __builtin_amdgcn_perm(L, L, (cw[h] >> 2) & 0x03030303u);
                 o.z = __builtin_amdgcn_perm(L, L, (cw[h] >> 4) & 0x03030303u);
                 o.w = __builtin_amdgcn_perm(L, L, (cw[h] >> 6) & 0x03030303u);
-                if constexpr (ST == 2) {  // two ds_write_b64 (6 transfer cycles each) per 16-B row piece
-                    typedef __attribute__((address_space(3))) volatile uint64_t lds_u64;
-                    lds_u64* qq = (lds_u64*)(S + lp * PNL + (RPL * kq + h) * RS + 16 * d);
-                    qq[0] = (uint64_t)o.x | ((uint64_t)o.y << 32);
-                    qq[1] = (uint64_t)o.z | ((uint64_t)o.w << 32);
-                } else {
-                    *reinterpret_cast<uint4*>(S + lp * PNL + (RPL * kq + h) * RS + 16 * d) = o;
-                }
+                *reinterpret_cast<uint4*>(S + lp * PNL + (RPL * kq + h) * RS + 16 * d) = o;
             }
         };
         load(0);
@@ -467,7 +401,7 @@ __global__ __launch_bounds__(768, 1) void k_syrk_i8w(const uint8_t* __restrict__
         load(nst > 1 ? 1 : 0);
         __syncthreads();
         for (uint64_t s = 0; s < nst; s++) {
-            if (ABL != 2) store(lds + ((s + 1) & 1) * STG);  // stage s+1 (past the end: into the idle buffer, unread)
+            store(lds + ((s + 1) & 1) * STG);  // stage s+1 (past the end: into the idle buffer, unread)
             load(s + 2 < nst ? s + 2 : nst - 1);
             __syncthreads();
         }
@@ -496,8 +430,8 @@ __global__ __launch_bounds__(768, 1) void k_syrk_i8w(const uint8_t* __restrict__
         for (int ks = 0; ks < KS; ks++) {
             v4i a[4];
 #pragma unroll
-            for (int x = 0; x < 4; x++) a[x] = frag(cur, 0, ABL == 3 ? 0 : ks, wm * 128 + 32 * x);
-            if (ks + 1 < KS && ABL != 3) {
+            for (int x = 0; x < 4; x++) a[x] = frag(cur, 0, ks, wm * 128 + 32 * x);
+            if (ks + 1 < KS) {
 #pragma unroll
                 for (int y = 0; y < 2; y++) b[(ks + 1) & 1][y] = frag(cur, 1, ks + 1, wn * 64 + 32 * y);
             }
@@ -505,7 +439,7 @@ __global__ __launch_bounds__(768, 1) void k_syrk_i8w(const uint8_t* __restrict__
             for (int x = 0; x < 4; x++)
 #pragma unroll
                 for (int y = 0; y < 2; y++)
-                    acc[x][y] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[x], b[ABL == 3 ? 0 : (ks & 1)][y], acc[x][y], 0, 0, 0);
+                    acc[x][y] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[x], b[ks & 1][y], acc[x][y], 0, 0, 0);
         }
         __syncthreads();
     }
@@ -649,7 +583,9 @@ int crt_fraction_bits(uint64_t m) {
     return std::min(52, (int)std::floor(f));
 }
 
-int g_crt_kernel = 0;  // hook "crt": 0 = k_syrk_i8r (loader in every wave), 1 = k_syrk_i8w (loader waves)
+// hook "crt": 1 = k_syrk_i8w (loader waves, default: 684 vs 697 ms per 50k x 62.5k launch in one
+// process, profiles/r06g), 0 = k_syrk_i8r (loader in every wave)
+int g_crt_kernel = 1;
 
 uint64_t crt_max_snps() { return 1ull << 16; }  // keeps F >= 50 and the int32 sums exact
 int crt_moduli() { return kR; }
@@ -729,19 +665,7 @@ void launch_syrk_packed_crt(const uint8_t* packed, uint64_t pitch, uint64_t n, u
         SNPMI_REQUIRE(cnt < (1ull << 23), SNPMI_E_ARG, "crt SYRK: chunk too large");
         // the kR moduli of a block on one XCD at once (FETCH 951 -> 149 GB per 62.5k-SNP
         // launch at 50k iids, the clock 2.21 -> 2.36 GHz, -3.6%: profiles/r05m)
-        if (g_crt_kernel == 5)
-            k_syrk_i8w<SK, 0, 2><<<(unsigned)(round_up(cnt, 8) * kR), 768, 0, st>>>(packed, pitch, m, mpad, lutr, ctl,
-                                                                               b0, cnt, res, part_tab);
-        else if (g_crt_kernel == 4)
-            k_syrk_i8w<SK, 0, 3><<<(unsigned)(round_up(cnt, 8) * kR), 768, 0, st>>>(packed, pitch, m, mpad, lutr, ctl,
-                                                                               b0, cnt, res, part_tab);
-        else if (g_crt_kernel == 2)
-            k_syrk_i8w<SK, 2><<<(unsigned)(round_up(cnt, 8) * kR), 768, 0, st>>>(packed, pitch, m, mpad, lutr, ctl, b0,
-                                                                            cnt, res, part_tab);
-        else if (g_crt_kernel == 3)
-            k_syrk_i8w<SK, 3><<<(unsigned)(round_up(cnt, 8) * kR), 768, 0, st>>>(packed, pitch, m, mpad, lutr, ctl, b0,
-                                                                            cnt, res, part_tab);
-        else if (g_crt_kernel == 1)
+        if (g_crt_kernel == 1)
             k_syrk_i8w<SK><<<(unsigned)(round_up(cnt, 8) * kR), 768, 0, st>>>(packed, pitch, m, mpad, lutr, ctl, b0,
                                                                             cnt, res, part_tab);
         else

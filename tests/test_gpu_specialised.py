@@ -38,7 +38,7 @@ def _both(fn):
         try:
             outs.append(fn())
         finally:
-            N.call("snpmi_set_kernel_variant", b"h2", 0)
+            N.call("snpmi_set_kernel_variant", b"h2", 1)
     return outs
 
 

@@ -64,7 +64,7 @@ def main():
                 sums[f] = h
                 N.call("snpmi_crt_moduli_stats", ctypes.byref(sum_r), ctypes.byref(nl), 0)
             print(json.dumps({"round": rnd, "form": f, "ms": ev.ms(0, 1)}), file=sys.stderr, flush=True)
-    N.call("snpmi_set_kernel_variant", hook, 0)
+    N.call("snpmi_set_kernel_variant", hook, 1)
     # executed MFMA work: f64 = R int8 SYRKs (5.0 POP/s dense); f32 = 3 fp16 products (2.5 PF/s dense)
     R, peak = (sum_r.value / max(nl.value, 1), 5000.0) if a.dtype == "f64" else (3.0, 2500.0)
     nb = (n + 255) // 256

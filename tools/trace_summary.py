@@ -26,16 +26,16 @@ def main():
         out["k_decode_f<float> launches of the most common grid (full launches)"] = {
             "launches": len(full), "avg_us": sum(full) / len(full), "grid_x": int(grid),
             "bench_roofline_avg_us": bench.get("roofline", {}).get("avg_launch_us")}
-    g4 = named("k_syrk_h2<false, 4")
+    g4 = named("k_syrk_h2s<false>")
     if g4:
         mx = max(r["us"] for r in g4)
         full = [r["us"] for r in g4 if r["us"] >= 0.8 * mx]
         g = bench.get("grm", {}).get("roofline", {})
         fl = g.get("per_launch_flops")
         avg = sum(full) / len(full)
-        out["f32w::k_syrk_h2<false,4> cfg4 launches (>= 0.8 of the longest)"] = {
+        out["f32w::k_syrk_h2s<false> cfg4 launches (>= 0.8 of the longest)"] = {
             "launches": len(full), "avg_us": avg, "flops": fl, "TFLOPs": fl / (avg * 1e-6) / 1e12 if fl else None}
-    g5 = named("k_syrk_h2<true, 4")
+    g5 = named("k_syrk_h2s<true>")
     blocks = bench.get("grm5", {}).get("blocks")
     if g5 and blocks:
         timed = g5[-blocks:]
@@ -49,7 +49,7 @@ def main():
             m5 = 1_000_000
         P = bench["grm5"].get("parts", 8)
         fl = n5 * (n5 + 1) * m5 / P
-        out["f32w::k_syrk_h2<true,4> cfg5 timed blocks (part 0 of %d)" % P] = {
+        out["f32w::k_syrk_h2s<true> cfg5 timed blocks (part 0 of %d)" % P] = {
             "launches": len(timed), "sum_s": busy, "avg_us_full_blocks": sorted(r["us"] for r in timed)[len(timed) // 2],
             "flops_part": fl, "TFLOPs": fl / busy / 1e12, "bench_seconds": bench["grm5"].get("seconds")}
     std = named("k_std_cols_f<float, 1024, 16, false>")
@@ -57,9 +57,9 @@ def main():
         out["k_std_cols_f<float,1024,16,false> (file leg, 50k x 100k f32)"] = {
             "launches": len(std), "avg_us": sum(r["us"] for r in std) / len(std), "algorithmic_bytes": 40_000_000_000,
             "TBps": 40e9 / (sum(r["us"] for r in std) / len(std) * 1e-6) / 1e12}
-    crt = named("k_syrk_i8r")
+    crt = named("k_syrk_i8w")
     if crt:
-        out["k_syrk_i8r (f64 CRT) all launches"] = {"launches": len(crt), "avg_us": sum(r["us"] for r in crt) / len(crt)}
+        out["k_syrk_i8w (f64 CRT) all launches"] = {"launches": len(crt), "avg_us": sum(r["us"] for r in crt) / len(crt)}
     ex = named("k_grm_extract_sym<double")
     if ex:
         out["k_grm_extract_sym<double,64> (50k K, file leg)"] = {"launches": len(ex),

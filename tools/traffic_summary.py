@@ -19,6 +19,7 @@ KERNELS = {"k_decode_std_lds_f32": "k_decode_std_lds_f32", "k_decode_f<float, 4>
            "k_syrk256d<true": "f32w::k_syrk256d<local>", "k_snp_stats<float>": "k_snp_stats<float>",
            "k_syrk_bf3<false": "f32w::k_syrk_bf3", "k_syrk_bf3<true": "f32w::k_syrk_bf3<local>",
            "k_syrk_h2<false": "f32w::k_syrk_h2", "k_syrk_h2<true": "f32w::k_syrk_h2<local>",
+           "k_syrk_h2s<false": "f32w::k_syrk_h2s", "k_syrk_h2s<true": "f32w::k_syrk_h2s<local>",
            "k_std_cols_f<float": "k_std_cols_f<float>", "k_diag_sq": "k_diag_sq"}
 
 
