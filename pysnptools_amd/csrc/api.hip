@@ -1666,15 +1666,13 @@ int snpmi_set_kernel_variant(const char* kernel, int variant) {
         else if (std::strcmp(kernel, "diag") == 0) g_diag_exact = variant != 0;
         else if (std::strcmp(kernel, "extract") == 0) g_variant_extract = variant;
         else if (std::strcmp(kernel, "syrk") == 0) {
-#ifndef SNPMI_UBENCH
-            // the product library ships the default chain and the kernels it falls back to:
-            // 36 = the bf16x3 kernel alone (fp16x2 range fallback), 20 = the f32-MFMA kernels
-            // (dense-operand range fallback), 5 = the 128x128 small-N kernels, 71 = f64 GRMs on the
-            // f64 MFMA (the CRT path's non-finite fallback); every other variant is an A/B
-            // ablation of the ubench build (make -C pysnptools_amd/csrc ubench)
+            // the shipped default chain and the kernels it falls back to: 36 = the bf16x3 kernel
+            // alone (fp16x2 range fallback), 20 = the f32-MFMA kernels (dense-operand range
+            // fallback), 5 = the 128x128 small-N kernels, 71 = f64 GRMs on the f64 MFMA (the CRT
+            // path's non-finite fallback).  The A/B ablations of earlier rounds were deleted (round 6);
+            // the shipped forms' own A/B switches are the hooks "h2" and "crt".
             SNPMI_REQUIRE(variant == 0 || variant == 5 || variant == 20 || variant == 36 || variant == 71, SNPMI_E_ARG,
-                          "syrk variant " + std::to_string(variant) + " exists only in the ubench build");
-#endif
+                          "syrk variant " + std::to_string(variant) + " is not a shipped kernel (0, 5, 20, 36, 71)");
             g_variant_syrk = variant;
         }
         else if (std::strcmp(kernel, "syrk_split") == 0) g_variant_syrk_split = variant;

@@ -233,152 +233,6 @@ __global__ __launch_bounds__(256, MINB) void k_syrk(const void* __restrict__ src
         }
 }
 
-// Interleaved variant (PACKED only): the expansion of stage s+1's codes is spread between
-// the MFMAs of stage s -- 4 values + one ds_write_b128 after every second k-pair -- so the
-// VALU work issues while the wave's MFMAs execute instead of as a separate phase before the
-// barrier.  Loads for stage s+1 are issued at the top of stage s.
-template <int MINB, int ABL = 0>
-__global__ __launch_bounds__(256, MINB) void k_syrk_il(const uint8_t* __restrict__ P, uint64_t pitch, uint64_t kdim,
-                                                       const float* __restrict__ lut, float* __restrict__ tiles,
-                                                       int accumulate) {
-    constexpr int BK = 16;
-    __shared__ __attribute__((aligned(16))) float lds[2][2][BK * LDA];
-    uint32_t ti, tj;
-    tile_coords(blockIdx.x, ti, tj);
-    const uint64_t i0 = (uint64_t)ti * BM, j0 = (uint64_t)tj * BM;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int wm = wave >> 1, wn = wave & 1;
-    const int t = threadIdx.x, op = t >> 7, tt = t & 127;
-    const int kq = tt >> 3, d = tt & 7;  // this thread's (k, dword) of the staged tile
-    const uint64_t base = op ? j0 : i0;
-    const int kr = lane >> 5, c = lane & 31;
-    f32x16 acc[2][2];
-#pragma unroll
-    for (int x = 0; x < 2; x++)
-#pragma unroll
-        for (int y = 0; y < 2; y++) acc[x][y] = (f32x16){};
-    const uint64_t nst = (kdim + BK - 1) / BK;
-
-    auto load = [&](uint64_t k0, uint32_t& w, float4& l) {
-        const uint64_t kk = k0 + kq;
-        if constexpr (ABL == 1 || ABL == 3 || ABL == 4) {
-            w = (uint32_t)(kk * 0x9E3779B9u) ^ (uint32_t)t;
-            l = make_float4(0.5f, 0.f, -0.25f, 1.0f);
-            return;
-        }
-        if (kk < kdim) {
-            w = *reinterpret_cast<const uint32_t*>(P + kk * pitch + base / 4 + 4 * d);
-            l = *reinterpret_cast<const float4*>(lut + 4 * kk);
-        } else {
-            w = 0;
-            l = make_float4(0.f, 0.f, 0.f, 0.f);
-        }
-    };
-    auto expand = [&](float* S, uint32_t w, const float4& l, int v) {
-        const int vv = (v + (d >> 1)) & 3;
-        if constexpr (ABL == 4) {
-            *reinterpret_cast<float4*>(S + kq * LDA + 16 * d + 4 * vv) = l;
-            return;
-        }
-        const uint32_t b = w >> (8 * vv);
-        float4 o;
-        o.x = sel4(l.x, l.y, l.z, l.w, b & 3u);
-        o.y = sel4(l.x, l.y, l.z, l.w, (b >> 2) & 3u);
-        o.z = sel4(l.x, l.y, l.z, l.w, (b >> 4) & 3u);
-        o.w = sel4(l.x, l.y, l.z, l.w, (b >> 6) & 3u);
-        if constexpr (ABL == 3) {
-            asm volatile("" ::"v"(o.x), "v"(o.y), "v"(o.z), "v"(o.w));
-            return;
-        }
-        *reinterpret_cast<float4*>(S + kq * LDA + 16 * d + 4 * vv) = o;
-    };
-    auto kpair = [&](const float* As, const float* Bs, int kk) {
-        const int row = (2 * kk + kr) * LDA;
-        const float a0 = As[row + wm * 64 + c];
-        const float a1 = As[row + wm * 64 + 32 + c];
-        const float b0 = Bs[row + wn * 64 + c];
-        const float b1 = Bs[row + wn * 64 + 32 + c];
-        acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
-        acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
-        acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
-        acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
-    };
-
-    uint32_t w;
-    float4 l;
-    load(0, w, l);
-#pragma unroll
-    for (int v = 0; v < 4; v++) expand(op ? lds[0][1] : lds[0][0], w, l, v);
-    __syncthreads();
-    for (uint64_t s = 0; s < nst; s++) {
-        const int buf = s & 1;
-        const bool more = s + 1 < nst;
-        if (more) load((s + 1) * BK, w, l);
-        const float* As = lds[buf][0];
-        const float* Bs = lds[buf][1];
-        float* S = op ? lds[buf ^ 1][1] : lds[buf ^ 1][0];
-#pragma unroll
-        for (int kk = 0; kk < BK / 2; kk++) {
-            kpair(As, Bs, kk);
-            if constexpr (ABL == 2) {
-                if (more && kk == BK / 2 - 1) asm volatile("" ::"v"(w), "v"(l.x), "v"(l.y), "v"(l.z), "v"(l.w));
-            } else {
-                if (more && (kk & 1)) expand(S, w, l, kk >> 1);
-            }
-        }
-        __syncthreads();
-    }
-    float* T = tiles + (uint64_t)blockIdx.x * (BM * BM);
-#pragma unroll
-    for (int mt = 0; mt < 2; mt++)
-#pragma unroll
-        for (int nt = 0; nt < 2; nt++) {
-            float* bp = T + (wm * 64 + mt * 32 + 4 * (lane >> 5)) * BM + wn * 64 + nt * 32 + (lane & 31);
-            if (accumulate) {
-                float old[16];
-#pragma unroll
-                for (int r = 0; r < 16; r++) old[r] = bp[((r & 3) + 8 * (r >> 2)) * BM];
-#pragma unroll
-                for (int r = 0; r < 16; r++) acc[mt][nt][r] += old[r];
-            }
-#pragma unroll
-            for (int r = 0; r < 16; r++) bp[((r & 3) + 8 * (r >> 2)) * BM] = acc[mt][nt][r];
-        }
-}
-
-// Diagnostic ablations (tuning only, wrong results): ABL=1 compute + barrier, no staging;
-// ABL=2 compute only.
-template <int ABL>
-__global__ __launch_bounds__(256, 4) void k_syrk_ablate(const uint8_t* __restrict__ P, uint64_t pitch, uint64_t kdim,
-                                                        const float* __restrict__ lut, float* __restrict__ tiles,
-                                                        int accumulate) {
-    constexpr int BK = 16;
-    __shared__ __attribute__((aligned(16))) float lds[2][2][BK * LDA];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int wm = wave >> 1, wn = wave & 1;
-    for (int i = threadIdx.x; i < 2 * 2 * BK * LDA; i += 256) (&lds[0][0][0])[i] = (float)(i & 7) * 0.25f;
-    __syncthreads();
-    f32x16 acc[2][2];
-#pragma unroll
-    for (int x = 0; x < 2; x++)
-#pragma unroll
-        for (int y = 0; y < 2; y++) acc[x][y] = (f32x16){};
-    const uint64_t nst = (kdim + BK - 1) / BK;
-    for (uint64_t s = 0; s < nst; s++) {
-        const int buf = s & 1;
-        compute<BK>(lds[buf][0], lds[buf][1], acc, wm, wn, lane);
-        if constexpr (ABL == 1) __syncthreads();
-    }
-    float* T = tiles + (uint64_t)blockIdx.x * (BM * BM);
-#pragma unroll
-    for (int mt = 0; mt < 2; mt++)
-#pragma unroll
-        for (int nt = 0; nt < 2; nt++) {
-            float* bp = T + (wm * 64 + mt * 32 + 4 * (lane >> 5)) * BM + wn * 64 + nt * 32 + (lane & 31);
-#pragma unroll
-            for (int r = 0; r < 16; r++) bp[((r & 3) + 8 * (r >> 2)) * BM] = acc[mt][nt][r];
-        }
-}
 }  // namespace f32k
 
 // ====================================================================== f32, 256x256 blocks
@@ -827,17 +681,16 @@ struct SegFlush {
     }
 };
 
-// MODE 0: load stage s+1 -> registers during stage s, expand + ds_write after its MFMAs.
-// MODE 1: codes/LUT of stage s+2 in flight (two register sets); stage s+1's expansion and
-//         ds_writes are issued plane by plane between the MFMA groups of stage s, so the VALU
-//         and LDS stores fill MFMA gaps instead of a store phase with the matrix pipe idle.
-// MODE 9: ablation -- no loader after the prologue (MFMA + transposed LDS reads only).
+// f32 GRM on the bf16 MFMA pipe (the fallback of k_syrk_h2 for LUTs outside fp16's range, and of
+// the dense-operand path): three exact bf16 planes per value, six products p+q <= 2.  Loader: the
+// codes / LUT of stage s+1 (16 SNPs) are expanded and stored plane by plane between the MFMA groups
+// of stage s, with the workgroup barrier in the middle of the stage (see the loop).
 struct B3Regs {
     uint32_t w;
     uint4 la, lb;  // plane LUT words: (lo0, hi0, lo1, hi1), (lo2, hi2, -, -)
 };
 
-template <bool LOCAL = false, bool XCD = false, int MODE = 0>
+template <bool LOCAL = false, bool XCD = false, int MODE = 5>
 __global__ __launch_bounds__(512, 1) void k_syrk_bf3(const uint8_t* __restrict__ P, uint64_t pitch, uint64_t n,
                                                      uint64_t kdim, const uint32_t* __restrict__ lut3,
                                                      float* __restrict__ tiles, int accumulate,
@@ -845,6 +698,7 @@ __global__ __launch_bounds__(512, 1) void k_syrk_bf3(const uint8_t* __restrict__
                                                      uint64_t kslice = 0, uint64_t slice_elems = 0,
                                                      const uint32_t* __restrict__ gate = nullptr, SegCtx seg = SegCtx(),
                                                      uint64_t wg0 = 0, const uint32_t* __restrict__ part_tab = nullptr) {
+    static_assert(MODE == 5, "k_syrk_bf3: the interleaved loader with the mid-stage barrier (MODE 5)");
     __shared__ __attribute__((aligned(16))) short lds[2 * B3_STAGE];
     if (gate && *gate == 0) return;  // fallback of k_syrk_h2: runs only when its range flag is set
     if (gridDim.y > 1) {  // split-K: slice blockIdx.y covers SNPs [y*kslice, +kslice) into its own partial K
@@ -936,34 +790,8 @@ __global__ __launch_bounds__(512, 1) void k_syrk_bf3(const uint8_t* __restrict__
         const i16x4_t r0 = lds_tr16(b), r1 = lds_tr16(b + 4 * B3_RS);
         return __builtin_bit_cast(bf16x8_t, (i16x8_t)__builtin_shufflevector(r0, r1, 0, 1, 2, 3, 4, 5, 6, 7));
     };
-    // the six products (pa, pb), pa + pb <= 2, as 6 groups of 8 MFMAs; hook(gidx) runs after
-    // group gidx (the interleaved loader's slot)
-    auto compute = [&](const short* S, auto&& hook) {
-        bf16x8_t b[3][2];
-#pragma unroll
-        for (int pl = 0; pl < 3; pl++)
-#pragma unroll
-            for (int y = 0; y < 2; y++) b[pl][y] = frag(S, 1, pl, wn * 64 + 32 * y, rd_offB);
-        int gidx = 0;
-#pragma unroll
-        for (int pa = 0; pa < 3; pa++) {
-            bf16x8_t a[4];
-#pragma unroll
-            for (int x = 0; x < 4; x++) a[x] = frag(S, 0, pa, wm * 128 + 32 * x, x >= 2 ? rd_off + dswz : rd_off);
-#pragma unroll
-            for (int pb = 0; pb + pa <= 2; pb++) {
-#pragma unroll
-                for (int x = 0; x < 4; x++)
-#pragma unroll
-                    for (int y = 0; y < 2; y++)
-                        acc[x][y] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[x], b[pb][y], acc[x][y], 0, 0, 0);
-                hook(gidx++);
-            }
-        }
-    };
-
-    if constexpr (MODE == 2 || MODE == 5) {
-        // MODE 1's loader, with the workgroup barrier moved to the middle of the stage: after
+    {
+        // The loader with the workgroup barrier in the middle of the stage: after
         // MFMA group 3 (stage s+1's planes are all stored) every wave reads stage s+1's B planes
         // 0-1 into a second register set during groups 4-5, so the next stage starts after its
         // 8 A-plane-0 reads instead of 20 transposed LDS reads.  Stage s's own A planes and B
@@ -995,21 +823,19 @@ __global__ __launch_bounds__(512, 1) void k_syrk_bf3(const uint8_t* __restrict__
         SegFlush sf(seg, 2 * BK, wg, (nst + 1) / 2, &seg_slot);
         fragB(lds, 0, B0s);
         fragB(lds, 1, B1s);
-        // MODE 5 (default): the hooks run unconditionally (the last stage expands into the idle
-        // buffer, its code loads clamp to the last stage), so each MFMA group and its loader VALU
-        // share one basic block, and the schedule is pinned to one VALU after each MFMA
-        // (sched_group_barrier) instead of the group's 8 MFMAs followed by a VALU burst.
-        // N=50k: 307.2-315.0 vs 303.3-307.1 TFLOP/s for MODE 2; 2 or 3 VALU per MFMA 305-307,
+        // The loader runs unconditionally (the last stage expands into the idle buffer, its code
+        // loads clamp to the last stage), so each MFMA group and its loader VALU share one basic
+        // block, and the schedule is pinned to one VALU after each MFMA (sched_group_barrier)
+        // instead of the group's 8 MFMAs followed by a VALU burst.  N=50k: 307.2-315.0 vs
+        // 303.3-307.1 TFLOP/s with the barrier-guarded form; 2 or 3 VALU per MFMA 305-307,
         // unconditional hooks without the pin 306.1, + the next B reads pinned between the
         // group 4-5 MFMAs 293.4 (profiles/r01i/ubench_syrk_bf3_interleave.jsonl).
-        constexpr bool kUncond = MODE == 5;
+        constexpr bool kUncond = true;
         auto pin = [&]() {
-            if constexpr (MODE == 5) {
 #pragma unroll
-                for (int i = 0; i < 8; i++) {
-                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
-                    __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);  // VALU
-                }
+            for (int i = 0; i < 8; i++) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+                __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);  // VALU
             }
         };
         auto stage = [&](uint64_t s, bf16x8_t (&B0)[2], bf16x8_t (&B1)[2], bf16x8_t (&B0n)[2], bf16x8_t (&B1n)[2]) {
@@ -1053,47 +879,7 @@ __global__ __launch_bounds__(512, 1) void k_syrk_bf3(const uint8_t* __restrict__
         sf.finish(acc);
         epilogue_pi<LOCAL>(acc, tiles, n, bi, bj, accumulate, lane, wm, wn, wg);
         sf.release(seg);
-        return;
-    } else if constexpr (MODE == 1) {
-        // one register set: the codes/LUT of stage s+1 are expanded and stored plane by plane
-        // after MFMA groups 0-3 of stage s, and right after the last plane the loads of stage
-        // s+2 are issued into the same registers -- they have MFMA groups 4-5, the barrier and
-        // group 0 of the next stage to arrive
-        B3Regs r;
-        load(0, r);
-        store(lds, r);
-        if (nst > 1) load(1, r);
-        __syncthreads();
-        for (uint64_t s = 0; s < nst; s++) {
-            short* cur = lds + (s & 1) * B3_STAGE;
-            short* nxt = lds + ((s + 1) & 1) * B3_STAGE;
-            const bool more = s + 1 < nst;
-            uint32_t sel[8];
-            compute(cur, [&](int gi) {
-                if (more) {
-                    if (gi == 0) make_sel(r.w, sel);
-                    else if (gi <= 3) store_plane(nxt, gi - 1, r, sel);
-                    if (gi == 3 && s + 2 < nst) load(s + 2, r);
-                }
-            });
-            __syncthreads();
-        }
-    } else {
-        B3Regs r;
-        load(0, r);
-        store(lds, r);
-        __syncthreads();
-        for (uint64_t s = 0; s < nst; s++) {
-            short* cur = lds + (s & 1) * B3_STAGE;
-            short* nxt = lds + ((s + 1) & 1) * B3_STAGE;
-            const bool more = s + 1 < nst;
-            if (MODE == 0 && more) load(s + 1, r);
-            compute(MODE == 9 ? lds : cur, [](int) {});
-            if (MODE == 0 && more) store(nxt, r);
-            __syncthreads();
-        }
     }
-    epilogue_pi<LOCAL>(acc, tiles, n, bi, bj, accumulate, lane, wm, wn, wg);
 }
 
 // per-SNP f32 LUT [m][4] -> bf16x3 split LUT [mpad][8] u32, byte-planar: plane p at word 2p
@@ -1237,21 +1023,22 @@ __global__ __launch_bounds__(256) void k_image_h2(const float* __restrict__ Z, u
 typedef _Float16 f16x8_t __attribute__((ext_vector_type(8)));
 
 // Same block structure, loader roles and LDS image as k_syrk_bf3 (two fp16 planes per panel
-// instead of three bf16 planes); per 16-SNP stage each wave runs 3 groups of 8
-// v_mfma_f32_32x32x16_f16: (A0,B0), (A0,B1), (A1,B0).  Schedule (MODE 0): stage s+1's codes
-// (loaded one stage ahead) are expanded and stored plane by plane beside groups 0-1, the loads
-// of stage s+2 are issued, then one barrier; stage s+1's B fragments are read into a second
-// register set under group 2.  Runs only when *flag == 0 (see k_lut_h2).
-// DENSE: the operand is a float block already split by k_split_h2 into two fp16 planes
-// ([sid][plane][ldp], pitch = ldp elements, each 16-iid group pi-permuted), copied verbatim.
-// ROT (MODE 4 only, default): the loader's ds_write_b64 stores place 8-B piece j of 16-iid group
-// d at slot (j + (d >> 2)) & 3 of the group's 32-B segment (a rotation; the other modes swap the
-// 16-B halves of groups with bit 2 set, which the 8-lane groups of ds_write_b128 need): with
-// piece j stored by instruction j, the 16 lanes of each ds_write_b64 group then hit 32 distinct
-// banks, where the swap layout left them 2-way conflicted (PMC SQ_LDS_BANK_CONFLICT = 29% of
-// SQ_LDS_IDX_ACTIVE, profiles/r04n).  The transposed fragment reads undo the rotation per lane
-// and stay conflict-free.
-template <bool LOCAL = false, int MODE = 4, bool DENSE = false, bool ROT = true>
+// instead of three bf16 planes); per 16-SNP k-step each wave runs 3 groups of 8
+// v_mfma_f32_32x32x16_f16: (A0,B0), (A0,B1), (A1,B0).  Runs only when *flag == 0 (see k_lut_h2).
+// MODE 4 (packed codes): 32-SNP stages (two k-steps, one barrier per 32 SNPs); stage s+1's codes
+// (loaded one stage ahead) are expanded and stored plane by plane beside the MFMA groups of stage
+// s, the loads of stage s+2 are issued, then the barrier; stage s+1's B fragments are read under
+// the last group.  The loader's ds_write_b64 stores place 8-B piece j of 16-iid group d at slot
+// (j + (d >> 2)) & 3 of the group's 32-B segment (a rotation): the 16 lanes of each ds_write_b64
+// group then hit 32 distinct banks (the 16-B-half swap the ds_write_b128 form needed left them 2-way
+// conflicted, PMC SQ_LDS_BANK_CONFLICT = 29% of SQ_LDS_IDX_ACTIVE, profiles/r04n); the transposed
+// fragment reads undo the rotation per lane.  k_syrk_h2s (below) is the same kernel with the loader
+// in its own waves -- the default since round 6; this form stays for the split-K grids and as
+// hook "h2" = 0.
+// MODE 6 (DENSE): the operand is a dense float block already rewritten by k_image_h2 as stage
+// images (the exact LDS rows the packed loader would build, swap layout), moved into LDS by
+// LDS-DMA.
+template <bool LOCAL = false, int MODE = 4, bool DENSE = false>
 __global__ __launch_bounds__(512, 1) void k_syrk_h2(const uint8_t* __restrict__ P, uint64_t pitch, uint64_t n,
                                                     uint64_t kdim, const uint32_t* __restrict__ lut2,
                                                     const uint32_t* __restrict__ flag, float* __restrict__ tiles,
@@ -1259,16 +1046,12 @@ __global__ __launch_bounds__(512, 1) void k_syrk_h2(const uint8_t* __restrict__ 
                                                     uint64_t kslice = 0, uint64_t slice_elems = 0,
                                                     SegCtx seg = SegCtx(), const uint32_t* __restrict__ order = nullptr,
                                                     uint64_t wg0 = 0) {
+    static_assert(MODE == 4 || (MODE == 6 && DENSE), "k_syrk_h2: MODE 4 (packed) or MODE 6 (dense stage images)");
     // wg0: first block of this launch in the full grid's order (a column group of the triangle,
     // launch_syrk_packed_h2_cols); block identity, storage and SegFlush phase follow wg0 + blockIdx.x
-    // KS = 16-SNP k-steps per LDS stage (MODE 4/5: two, one barrier per 32 SNPs)
-    // MODE 10 = MODE 4 with the loader's registers double-buffered: stage s+2's codes/LUT are
-    // loaded at the START of stage s (a whole stage to arrive instead of one MFMA group)
-    // MODE 11: ablation of MODE 4 -- no loader after the prologue (same LDS reads, MFMAs, barriers)
-    constexpr int KS = MODE >= 4 ? 2 : 1, SBK = KS * BK;
-    constexpr bool kNoLd = MODE == 11;
-    constexpr bool kLd2 = MODE == 10;
+    constexpr int KS = 2, SBK = KS * BK;  // two 16-SNP k-steps per LDS stage
     constexpr int PLANE = KS * B3_PLANE, STAGE = 2 * 2 * PLANE;
+    constexpr bool kRot = MODE == 4;
     __shared__ __attribute__((aligned(16))) short lds[2 * STAGE];
     if (*flag) return;  // a SNP of this block is outside fp16's range: k_syrk_bf3 runs instead
     if (gridDim.y > 1) {
@@ -1298,22 +1081,19 @@ __global__ __launch_bounds__(512, 1) void k_syrk_h2(const uint8_t* __restrict__ 
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
     const int wm = wave >> 2, wn = wave & 3;
     const int lp = t >> 8, lk = (t >> 4) & 15, ld_ = t & 15;
-    const int sw = (ld_ >> 2) & 1;
     const uint8_t* wp = P + (lp ? j0 : i0) / 4 + 4 * ld_ + (uint64_t)lk * pitch;
     const uint8_t* wlast = P + (lp ? j0 : i0) / 4 + 4 * ld_ + (kdim - 1) * pitch;
     const uint32_t* lp2 = lut2 + 4 * lk;
-    const uint16_t* dp = reinterpret_cast<const uint16_t*>(P) + (lp ? j0 : i0) + 16 * ld_;  // DENSE
     const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
-    constexpr bool kRot = ROT && MODE == 4;
     const int rd_base = (8 * (g >> 1) + q) * B3_RS + 16 * (g & 1);
     const int rd_off = rd_base + 4 * pp;
     const int dswz = (pp >> 1) ? -8 : 8;
-    // swap layout: A fragments x >= 2 and B fragments of odd wn sit in swapped segments;
-    // rotation layout: a fragment column c lies in segments rotated by (c / 64) & 3
+    // swap layout (MODE 6 images): A fragments x >= 2 and B fragments of odd wn sit in swapped
+    // segments; rotation layout (MODE 4): a fragment column c lies in segments rotated by (c / 64) & 3
     const int rd_offA0 = kRot ? rd_base + 4 * ((pp + 2 * wm) & 3) : rd_off;
     const int rd_offA1 = kRot ? rd_base + 4 * ((pp + 2 * wm + 1) & 3) : rd_off + dswz;
     const int rd_offB = kRot ? rd_base + 4 * ((pp + wn) & 3) : rd_off + ((wn & 1) ? dswz : 0);
-    const int wrot = (ld_ >> 2) & 3;  // kRot: this lane's group rotation (store side)
+    const int wrot = (ld_ >> 2) & 3;  // this lane's group rotation (store side)
 
     f32x16 acc[4][2];
 #pragma unroll
@@ -1322,39 +1102,17 @@ __global__ __launch_bounds__(512, 1) void k_syrk_h2(const uint8_t* __restrict__ 
         for (int y = 0; y < 2; y++) acc[x][y] = (f32x16){};
     const uint64_t nst = (kdim + SBK - 1) / SBK;
 
-    uint32_t rw[KS], rw2[KS];
-    uint4 rl[KS], rl2[KS];
-    uint4 dv[KS][2][2];  // DENSE: [k-step][plane][16-B half]
-    auto load2 = [&](uint64_t st) {
-#pragma unroll
-        for (int h = 0; h < KS; h++) {
-            const uint8_t* a = wp + (st * SBK + h * BK) * pitch;
-            rw2[h] = *reinterpret_cast<const uint32_t*>(a <= wlast ? a : wlast);
-            rl2[h] = *reinterpret_cast<const uint4*>(lp2 + 4 * (SBK * st + h * BK));
-        }
-    };
+    uint32_t rw[KS];
+    uint4 rl[KS];
     auto load = [&](uint64_t st) {
 #pragma unroll
         for (int h = 0; h < KS; h++) {
-            if constexpr (DENSE) {
-                const uint64_t k = st * SBK + h * BK + lk;
-                const bool ok = k < kdim;
-                const uint4* a = reinterpret_cast<const uint4*>(dp + (ok ? k : kdim - 1) * 2 * pitch);
-                const uint4* b = reinterpret_cast<const uint4*>(dp + ((ok ? k : kdim - 1) * 2 + 1) * pitch);
-                const uint4 z = make_uint4(0, 0, 0, 0);
-                dv[h][0][0] = ok ? a[0] : z;
-                dv[h][0][1] = ok ? a[1] : z;
-                dv[h][1][0] = ok ? b[0] : z;
-                dv[h][1][1] = ok ? b[1] : z;
-            } else {
-                const uint8_t* a = wp + (st * SBK + h * BK) * pitch;
-                rw[h] = *reinterpret_cast<const uint32_t*>(a <= wlast ? a : wlast);
-                rl[h] = *reinterpret_cast<const uint4*>(lp2 + 4 * (SBK * st + h * BK));
-            }
+            const uint8_t* a = wp + (st * SBK + h * BK) * pitch;
+            rw[h] = *reinterpret_cast<const uint32_t*>(a <= wlast ? a : wlast);
+            rl[h] = *reinterpret_cast<const uint4*>(lp2 + 4 * (SBK * st + h * BK));
         }
     };
     auto make_sel = [&](uint32_t w, uint32_t (&sel)[8]) {
-        if constexpr (DENSE) return;
 #pragma unroll
         for (int j = 0; j < 4; j++) {
             const uint32_t v = (w >> (2 * j)) & 0x03030303u;
@@ -1364,46 +1122,17 @@ __global__ __launch_bounds__(512, 1) void k_syrk_h2(const uint8_t* __restrict__ 
         }
     };
     auto store_plane = [&](short* S, int pl, int h, const uint32_t (&sel)[8]) {
-        if constexpr (DENSE) {
-            uint4* r4 = reinterpret_cast<uint4*>(S + (lp * 2 + pl) * PLANE + (lk + BK * h) * B3_RS + 16 * ld_);
-            r4[sw] = dv[h][pl][0];
-            r4[sw ^ 1] = dv[h][pl][1];
-            return;
-        }
         const uint32_t lo = pl == 0 ? rl[h].x : rl[h].z;
         const uint32_t hi = pl == 0 ? rl[h].y : rl[h].w;
-        uint4 v0, v1;
-        v0.x = __builtin_amdgcn_perm(hi, lo, sel[0]);
-        v0.y = __builtin_amdgcn_perm(hi, lo, sel[1]);
-        v0.z = __builtin_amdgcn_perm(hi, lo, sel[2]);
-        v0.w = __builtin_amdgcn_perm(hi, lo, sel[3]);
-        v1.x = __builtin_amdgcn_perm(hi, lo, sel[4]);
-        v1.y = __builtin_amdgcn_perm(hi, lo, sel[5]);
-        v1.z = __builtin_amdgcn_perm(hi, lo, sel[6]);
-        v1.w = __builtin_amdgcn_perm(hi, lo, sel[7]);
-        if constexpr (MODE == 4) {
-            // two ds_write_b64 per 16-B half (6 LDS-transfer cycles per wave-instruction vs 13 for
-            // ds_write_b128; volatile + explicit LDS address space so they are neither re-merged
-            // nor turned into flat stores): +1.2-1.3% at 50k x 10k / 62.5k, bit-identical K
-            // (profiles/r03crt/ubench_lds_store_width.jsonl)
-            typedef __attribute__((address_space(3))) volatile uint64_t lds_u64;
-            lds_u64* q = (lds_u64*)(S + (lp * 2 + pl) * PLANE + (lk + BK * h) * B3_RS + 16 * ld_);
-            if constexpr (kRot) {
-                q[wrot] = (uint64_t)v0.x | ((uint64_t)v0.y << 32);
-                q[(wrot + 1) & 3] = (uint64_t)v0.z | ((uint64_t)v0.w << 32);
-                q[(wrot + 2) & 3] = (uint64_t)v1.x | ((uint64_t)v1.y << 32);
-                q[(wrot + 3) & 3] = (uint64_t)v1.z | ((uint64_t)v1.w << 32);
-                return;
-            }
-            q[2 * sw] = (uint64_t)v0.x | ((uint64_t)v0.y << 32);
-            q[2 * sw + 1] = (uint64_t)v0.z | ((uint64_t)v0.w << 32);
-            q[2 * (sw ^ 1)] = (uint64_t)v1.x | ((uint64_t)v1.y << 32);
-            q[2 * (sw ^ 1) + 1] = (uint64_t)v1.z | ((uint64_t)v1.w << 32);
-            return;
-        }
-        uint4* r4 = reinterpret_cast<uint4*>(S + (lp * 2 + pl) * PLANE + (lk + BK * h) * B3_RS + 16 * ld_);
-        r4[sw] = v0;
-        r4[sw ^ 1] = v1;
+        // two ds_write_b64 per 16-B half (6 LDS-transfer cycles per wave-instruction vs 13 for
+        // ds_write_b128; volatile + explicit LDS address space so they are neither re-merged nor
+        // turned into flat stores): +1.2-1.3%, bit-identical K (profiles/r03crt/ubench_lds_store_width.jsonl)
+        typedef __attribute__((address_space(3))) volatile uint64_t lds_u64;
+        lds_u64* qq = (lds_u64*)(S + (lp * 2 + pl) * PLANE + (lk + BK * h) * B3_RS + 16 * ld_);
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+            qq[(wrot + j) & 3] = (uint64_t)__builtin_amdgcn_perm(hi, lo, sel[2 * j]) |
+                                 ((uint64_t)__builtin_amdgcn_perm(hi, lo, sel[2 * j + 1]) << 32);
     };
     auto frag = [&](const short* S, int panel, int pl, int h, int col, int off) -> f16x8_t {
         const short* b = S + (panel * 2 + pl) * PLANE + h * BK * B3_RS + off + col;
@@ -1425,14 +1154,7 @@ __global__ __launch_bounds__(512, 1) void k_syrk_h2(const uint8_t* __restrict__ 
             for (int y = 0; y < 2; y++)
                 acc[x][y] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[x], b[y], acc[x][y], 0, 0, 0);
     };
-    // V VALU after each of a group's 8 MFMAs
-    auto pin = [&](auto v) {
-#pragma unroll
-        for (int i = 0; i < 8; i++) {
-            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-            __builtin_amdgcn_sched_group_barrier(0x002, decltype(v)::value, 0);
-        }
-    };
+    __shared__ uint32_t seg_slot;
     if constexpr (MODE == 6) {
         // DENSE stage images (k_image_h2): P = [16-SNP step t][256-iid block b][plane][16 rows x
         // 288 fp16], exactly the LDS rows the packed loader writes, so a stage is 8 contiguous
@@ -1455,7 +1177,6 @@ __global__ __launch_bounds__(512, 1) void k_syrk_h2(const uint8_t* __restrict__ 
         issue(0, lds);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        __shared__ uint32_t seg_slot;
         SegFlush sf(seg, SBK, blk, nst, &seg_slot);
         for (uint64_t s = 0; s < nst; s++) {
             const short* cur = lds + (s & 1) * STAGE;
@@ -1499,94 +1220,42 @@ __global__ __launch_bounds__(512, 1) void k_syrk_h2(const uint8_t* __restrict__ 
     };
     // The loader runs unconditionally (the last stage expands into the idle buffer and its code
     // loads clamp to the last stage) so each MFMA group and its VALU share one basic block.
-    // MODE 2/3: stage s+1's A plane-0 fragments are read after the barrier too (a second A
-    // register set), so the next stage's first group waits on no LDS read; MODE 0/3/5 pin the
-    // loader VALU between the MFMAs, MODE 1/2/4 leave the order to the compiler.
-    constexpr bool kPreA = MODE == 2 || MODE == 3, kPin = MODE == 0 || MODE == 3 || MODE == 5;
-    f16x8_t A0s[4], A0t[4];
-    auto stage = [&](uint64_t s, f16x8_t (&B0)[2], f16x8_t (&B1)[2], f16x8_t (&A0)[4], f16x8_t (&B0n)[2],
-                     f16x8_t (&B1n)[2], f16x8_t (&A0n)[4]) {
+    auto stage = [&](uint64_t s, f16x8_t (&B0)[2], f16x8_t (&B1)[2], f16x8_t (&B0n)[2], f16x8_t (&B1n)[2]) {
         const short* cur = lds + (s & 1) * STAGE;
         short* nxt = lds + ((s + 1) & 1) * STAGE;
-        if constexpr (KS == 1) {
-            f16x8_t A1[4];
-            if constexpr (!kPreA) fragsA(cur, 0, 0, A0);
-            fragsA(cur, 1, 0, A1);
-            uint32_t sel[8];
-            group(A0, B0);
-            make_sel(rw[0], sel);
-            store_plane(nxt, 0, 0, sel);
-            if constexpr (kPin) pin(std::integral_constant<int, 3>{});
-            group(A0, B1);
-            store_plane(nxt, 1, 0, sel);
-            if constexpr (kPin) pin(std::integral_constant<int, 1>{});
-            load(s + 2 < send ? s + 2 : send - 1);
-            __syncthreads();
-            fragB(nxt, 0, 0, B0n);
-            fragB(nxt, 1, 0, B1n);
-            if constexpr (kPreA) fragsA(nxt, 0, 0, A0n);
-            group(A1, B0);
-        } else {
-            // k-step 0 with the prefetched B, k-step 1 read from cur before the barrier (after
-            // it, stage s+1's stores may overwrite cur); the expansion of stage s+1 (2 k-steps
-            // x 2 planes) rides on groups 0-3
-            f16x8_t Ax[4], Ay[4], C0[2], C1[2];
-            fragsA(cur, 0, 0, Ax);
-            fragsA(cur, 1, 0, Ay);
-            if constexpr (kLd2) load2(s + 2 < send ? s + 2 : send - 1);
-            uint32_t sel[8];
-            group(Ax, B0);
-            if constexpr (!kNoLd) {
-                make_sel(rw[0], sel);
-                store_plane(nxt, 0, 0, sel);
-            }
-            if constexpr (kPin) pin(std::integral_constant<int, 3>{});
-            group(Ax, B1);
-            if constexpr (!kNoLd) store_plane(nxt, 1, 0, sel);
-            fragB(cur, 0, 1, C0);
-            fragB(cur, 1, 1, C1);
-            if constexpr (kPin) pin(std::integral_constant<int, 1>{});
-            fragsA(cur, 0, 1, Ax);
-            group(Ay, B0);
-            if constexpr (!kNoLd) {
-                make_sel(rw[1], sel);
-                store_plane(nxt, 0, 1, sel);
-            }
-            if constexpr (kPin) pin(std::integral_constant<int, 3>{});
-            fragsA(cur, 1, 1, Ay);
-            group(Ax, C0);
-            if constexpr (!kNoLd) store_plane(nxt, 1, 1, sel);
-            if constexpr (kPin) pin(std::integral_constant<int, 1>{});
-            group(Ax, C1);
-            if constexpr (kLd2) {
-#pragma unroll
-                for (int h = 0; h < KS; h++) {
-                    rw[h] = rw2[h];
-                    rl[h] = rl2[h];
-                }
-            } else if constexpr (!kNoLd) {
-                load(s + 2 < send ? s + 2 : send - 1);
-            }
-            __syncthreads();
-            fragB(nxt, 0, 0, B0n);
-            fragB(nxt, 1, 0, B1n);
-            group(Ay, C0);
-        }
+        // k-step 0 with the prefetched B, k-step 1 read from cur before the barrier (after it,
+        // stage s+1's stores may overwrite cur); the expansion of stage s+1 (2 k-steps x 2 planes)
+        // rides on groups 0-3
+        f16x8_t Ax[4], Ay[4], C0[2], C1[2];
+        fragsA(cur, 0, 0, Ax);
+        fragsA(cur, 1, 0, Ay);
+        uint32_t sel[8];
+        group(Ax, B0);
+        make_sel(rw[0], sel);
+        store_plane(nxt, 0, 0, sel);
+        group(Ax, B1);
+        store_plane(nxt, 1, 0, sel);
+        fragB(cur, 0, 1, C0);
+        fragB(cur, 1, 1, C1);
+        fragsA(cur, 0, 1, Ax);
+        group(Ay, B0);
+        make_sel(rw[1], sel);
+        store_plane(nxt, 0, 1, sel);
+        fragsA(cur, 1, 1, Ay);
+        group(Ax, C0);
+        store_plane(nxt, 1, 1, sel);
+        group(Ax, C1);
+        load(s + 2 < send ? s + 2 : send - 1);
+        __syncthreads();
+        fragB(nxt, 0, 0, B0n);
+        fragB(nxt, 1, 0, B1n);
+        group(Ay, C0);
     };
-    // MODE 7 / 8: static priority for the second- / first-dispatched half of the waves (the
-    // arbitration loser of each SIMD pair; MI355X_MICROARCH.md "Two waves per SIMD" item 4)
-    if constexpr (MODE == 7) {
-        if (__builtin_amdgcn_readfirstlane(t) >= 256) __builtin_amdgcn_s_setprio(1);
-    } else if constexpr (MODE == 8) {
-        if (__builtin_amdgcn_readfirstlane(t) < 256) __builtin_amdgcn_s_setprio(1);
-    }
-    __shared__ uint32_t seg_slot;
     SegFlush sf(seg, 2 * SBK, blk, (nst + 1) / 2, &seg_slot);
     prologue(0);
-    if constexpr (kPreA) fragsA(lds, 0, 0, A0s);
     for (uint64_t s = 0; s < nst; s += 2) {
-        stage(s, B0s, B1s, A0s, B0t, B1t, A0t);
-        if (s + 1 < nst) stage(s + 1, B0t, B1t, A0t, B0s, B1s, A0s);
+        stage(s, B0s, B1s, B0t, B1t);
+        if (s + 1 < nst) stage(s + 1, B0t, B1t, B0s, B1s);
         if (sf.due(s + 2 < nst)) sf.flush(acc);
     }
     sf.finish(acc);
@@ -1738,627 +1407,6 @@ __global__ __launch_bounds__(768, 1) void k_syrk_h2s(const uint8_t* __restrict__
     sf.release(seg);
 }
 
-// ---------------------------------------------------------------- fp16x2 on v_mfma_f32_16x16x32_f16
-// Same products (A0 B0 + A0 B1 + A1 B0), loader and LDS image as k_syrk_h2 MODE 4, but every MFMA
-// is 16x16x32 instead of 32x32x16: the same cycles per FLOP and the same LDS bytes per FLOP
-// (a wave's 128x64 tile is 8 x 4 16x16 tiles; per 32-SNP stage 8 A + 8 A' + 4 B + 4 B' fragments
-// of 8 fp16 = 48 transposed reads, 96 MFMAs), and MI355X holds a higher clock on the 16x16 shape
-// under load (MI355X_MICROARCH.md, DVFS item 7: 1.12-1.15x FLOP/s with LDS-fed operands).
-// 16x16x32 operand: lane l holds row l%16, k 8(l/16)..+7, so a 32-lane half reads rows 8 apart
-// in the same 16 columns; with the 576-B row stride those rows share banks, so rows with bit 3
-// set hold each 16-iid group d in 32-B unit d ^ 1 (the loader stores through the same map; its
-// 8-lane ds_write_b128 groups keep their 8 distinct bank slots).
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-
-// wave tile (8 x 4 16x16 tiles): accumulator j of lane l is LDS-order row 4(l>>4)+j, column
-// l&15 of its tile, i.e. iid row 16x + pi(4(l>>4)+j) = 16x + 4j + (l>>4), column 16y + pi(l&15)
-template <bool LOCAL>
-__device__ __forceinline__ void epilogue_h2x(f32x4 (&acc)[8][4], float* __restrict__ tiles, uint64_t n, uint32_t bi,
-                                             uint32_t bj, int accumulate, int lane, int wm, int wn,
-                                             uint64_t local_block) {
-    float* T;
-    uint64_t ldo;
-    if constexpr (LOCAL) {
-        T = tiles + local_block * (BW * BW) + (uint64_t)(wm * 128) * BW + (wn >> 1) * 128;
-        ldo = BW;
-    } else {
-        const uint64_t nt128 = (n + 127) / 128;
-        const uint64_t ti = 2 * (uint64_t)bi + wm, tj = 2 * (uint64_t)bj + (wn >> 1);
-        if (ti > tj || tj >= nt128) return;  // wave-uniform
-        T = tiles + (tj * (tj + 1) / 2 + ti) * (uint64_t)(BM * BM);
-        ldo = BM;
-    }
-    const int r = lane >> 4, colp = pi16(lane & 15);
-#pragma unroll
-    for (int x = 0; x < 8; x++)
-#pragma unroll
-        for (int y = 0; y < 4; y++) {
-            float* bp = T + (16 * x + r) * ldo + (wn & 1) * 64 + 16 * y + colp;
-            if (accumulate) {
-                float old[4];
-#pragma unroll
-                for (int j = 0; j < 4; j++) old[j] = bp[4 * j * ldo];
-#pragma unroll
-                for (int j = 0; j < 4; j++) acc[x][y][j] += old[j];
-            }
-#pragma unroll
-            for (int j = 0; j < 4; j++) bp[4 * j * ldo] = acc[x][y][j];
-        }
-}
-
-// MODE bit 0: waves 4-7 at s_setprio 1 for the whole loop (the arbitration loser of each SIMD
-// pair, MI355X_MICROARCH.md "Two waves per SIMD" item 4); bit 1: pin the interleave -- after
-// each MFMA one DS instruction and (in loader iterations) two VALU
-template <bool LOCAL = false, int MODE = 0>
-__global__ __launch_bounds__(512, 1) void k_syrk_h2x(const uint8_t* __restrict__ P, uint64_t pitch, uint64_t n,
-                                                     uint64_t kdim, const uint32_t* __restrict__ lut2,
-                                                     const uint32_t* __restrict__ flag, float* __restrict__ tiles,
-                                                     int accumulate, uint32_t part_rank = 0, uint32_t part_world = 1,
-                                                     uint64_t kslice = 0, uint64_t slice_elems = 0) {
-    constexpr int KS = 2, SBK = KS * BK;                 // 32 SNPs per LDS stage
-    constexpr int PLANE = KS * B3_PLANE, STAGE = 2 * 2 * PLANE;
-    __shared__ __attribute__((aligned(16))) short lds[2 * STAGE];
-    if (*flag) return;  // a SNP of this block is outside fp16's range: k_syrk_bf3 runs instead
-    if (gridDim.y > 1) {
-        const uint64_t k0 = (uint64_t)blockIdx.y * kslice;
-        P += k0 * pitch;
-        lut2 += 4 * k0;
-        kdim = min(kslice, kdim - k0);
-        tiles += (uint64_t)blockIdx.y * slice_elems;
-    }
-    const uint64_t wg = blockIdx.x;
-    uint32_t bi, bj;
-    static_assert(!LOCAL, "the cfg5 part kernels read the part layout table (k_syrk_h2 / k_syrk_bf3)");
-    tile_coords(wg, bi, bj);
-    const uint64_t i0 = (uint64_t)bi * BW, j0 = (uint64_t)bj * BW;
-    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-    const int wm = wave >> 2, wn = wave & 3;
-    // loader role: panel lp, rows lk and lk + 16 of the stage, 16-iid group ld_ (stored in unit
-    // ld_ ^ xr, 16-B halves swapped by sw)
-    const int lp = t >> 8, lk = (t >> 4) & 15, ld_ = t & 15;
-    const int sw = (ld_ >> 2) & 1, xr = (lk >> 3) & 1;
-    const uint8_t* wp = P + (lp ? j0 : i0) / 4 + 4 * ld_ + (uint64_t)lk * pitch;
-    const uint8_t* wlast = P + (lp ? j0 : i0) / 4 + 4 * ld_ + (kdim - 1) * pitch;
-    const uint32_t* lp2 = lut2 + 4 * lk;
-    // transposed-read role: lane 4q+p of group g reads rows 8g+q (and +4), logical columns
-    // 16d + 4p of group d, i.e. physical unit d ^ (g & 1), half (p >> 1) ^ sw(d)
-    const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3, g1 = g & 1;
-    const int rowoff = (8 * g + q) * B3_RS + 4 * (pp & 1);
-    // A: d = 8 wm + x -> unit offset 16 (x ^ g1), half (p >> 1) ^ (x >> 2); B: d = 4 wn + y ->
-    // 16 (y ^ g1), half (p >> 1) ^ (wn & 1)
-    const int parA[2] = {16 * g1, -16 * g1};  // 16 (x ^ g1) - 16 x for even / odd x
-    const int hA[2] = {8 * (pp >> 1), 8 * ((pp >> 1) ^ 1)};
-    const int offA = rowoff + 128 * wm;
-    const int offB = rowoff + 64 * wn + 8 * ((pp >> 1) ^ (wn & 1));
-
-    f32x4 acc[8][4];
-#pragma unroll
-    for (int x = 0; x < 8; x++)
-#pragma unroll
-        for (int y = 0; y < 4; y++) acc[x][y] = (f32x4){};
-    const uint64_t nst = (kdim + SBK - 1) / SBK;
-
-    uint32_t rw[KS];
-    uint4 rl[KS];
-    auto load = [&](uint64_t st) {
-#pragma unroll
-        for (int h = 0; h < KS; h++) {
-            const uint8_t* a = wp + (st * SBK + h * BK) * pitch;
-            rw[h] = *reinterpret_cast<const uint32_t*>(a <= wlast ? a : wlast);
-            rl[h] = *reinterpret_cast<const uint4*>(lp2 + 4 * (SBK * st + h * BK));
-        }
-    };
-    auto make_sel = [&](uint32_t w, uint32_t (&sel)[8]) {
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            const uint32_t v = (w >> (2 * j)) & 0x03030303u;
-            const uint32_t o = v | 0x04040404u;
-            sel[2 * j] = __builtin_amdgcn_perm(o, v, 0x05010400u);
-            sel[2 * j + 1] = __builtin_amdgcn_perm(o, v, 0x07030602u);
-        }
-    };
-    auto store_plane = [&](short* S, int pl, int h, const uint32_t (&sel)[8]) {
-        const uint32_t lo = pl == 0 ? rl[h].x : rl[h].z;
-        const uint32_t hi = pl == 0 ? rl[h].y : rl[h].w;
-        uint4 v0, v1;
-        v0.x = __builtin_amdgcn_perm(hi, lo, sel[0]);
-        v0.y = __builtin_amdgcn_perm(hi, lo, sel[1]);
-        v0.z = __builtin_amdgcn_perm(hi, lo, sel[2]);
-        v0.w = __builtin_amdgcn_perm(hi, lo, sel[3]);
-        v1.x = __builtin_amdgcn_perm(hi, lo, sel[4]);
-        v1.y = __builtin_amdgcn_perm(hi, lo, sel[5]);
-        v1.z = __builtin_amdgcn_perm(hi, lo, sel[6]);
-        v1.w = __builtin_amdgcn_perm(hi, lo, sel[7]);
-        uint4* r4 = reinterpret_cast<uint4*>(S + (lp * 2 + pl) * PLANE + (lk + BK * h) * B3_RS + 16 * (ld_ ^ xr));
-        r4[sw] = v0;
-        r4[sw ^ 1] = v1;
-    };
-    auto frag = [&](const short* S, int panel, int pl, int off) -> f16x8_t {
-        const short* b = S + (panel * 2 + pl) * PLANE + off;
-        const i16x4_t r0 = lds_tr16(b), r1 = lds_tr16(b + 4 * B3_RS);
-        return __builtin_bit_cast(f16x8_t, (i16x8_t)__builtin_shufflevector(r0, r1, 0, 1, 2, 3, 4, 5, 6, 7));
-    };
-    {
-        load(0);
-#pragma unroll
-        for (int h = 0; h < KS; h++) {
-            uint32_t sel[8];
-            make_sel(rw[h], sel);
-            store_plane(lds, 0, h, sel);
-            store_plane(lds, 1, h, sel);
-        }
-        load(nst > 1 ? 1 : 0);
-    }
-    __syncthreads();
-    if constexpr (MODE & 1) {
-        if (__builtin_amdgcn_readfirstlane(t) >= 256) __builtin_amdgcn_s_setprio(1);
-    }
-    for (uint64_t s = 0; s < nst; s++) {
-        const short* cur = lds + (s & 1) * STAGE;
-        short* nxt = lds + ((s + 1) & 1) * STAGE;
-        f16x8_t B0[4], B1[4];
-#pragma unroll
-        for (int y = 0; y < 4; y++) {
-            B0[y] = frag(cur, 1, 0, offB + 16 * y + parA[y & 1]);
-            B1[y] = frag(cur, 1, 1, offB + 16 * y + parA[y & 1]);
-        }
-        uint32_t sel[8];
-#pragma unroll
-        for (int x = 0; x < 8; x++) {
-            const int oa = offA + 16 * x + parA[x & 1] + hA[x >> 2];
-            const f16x8_t A0 = frag(cur, 0, 0, oa), A1 = frag(cur, 0, 1, oa);
-#pragma unroll
-            for (int y = 0; y < 4; y++) {
-                acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A0, B0[y], acc[x][y], 0, 0, 0);
-                acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A0, B1[y], acc[x][y], 0, 0, 0);
-                acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A1, B0[y], acc[x][y], 0, 0, 0);
-            }
-            // stage s+1's expansion rides on x = 1, 2, 4, 5; stage s+2's loads after it
-            if (x == 1) {
-                make_sel(rw[0], sel);
-                store_plane(nxt, 0, 0, sel);
-            } else if (x == 2) {
-                store_plane(nxt, 1, 0, sel);
-            } else if (x == 4) {
-                make_sel(rw[1], sel);
-                store_plane(nxt, 0, 1, sel);
-            } else if (x == 5) {
-                store_plane(nxt, 1, 1, sel);
-            } else if (x == 6) {
-                load(s + 2 < nst ? s + 2 : nst - 1);
-            }
-            if constexpr ((MODE & 2) != 0) {
-                const bool ld = x == 1 || x == 2 || x == 4 || x == 5;
-#pragma unroll
-                for (int i = 0; i < 12; i++) {
-                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
-                    __builtin_amdgcn_sched_group_barrier(0x100 | 0x200, 1, 0);  // DS read / write
-                    if (ld) __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);  // VALU
-                }
-            }
-        }
-        __syncthreads();
-    }
-    epilogue_h2x<LOCAL>(acc, tiles, n, bi, bj, accumulate, lane, wm, wn, wg);
-}
-
-// k_syrk_h2q: the 16x16x32 fp16x2 SYRK with ONE wave per SIMD (4 waves, 512 registers each),
-// each wave a 128x128 quarter of the 256x256 block (8 x 8 16x16 tiles, 256 accumulators): a
-// third fewer transposed LDS reads per MFMA than the 8-wave form (32 fragments per 192 MFMAs).
-// One barrier per 32-SNP stage, placed mid-stage: before it every wave has read ALL of its
-// stage-s operands from LDS (A rows 4-7 are read beside the MFMAs of rows 0-3) and stored stage
-// s+1's planes; after it the MFMAs of rows 4-7 run beside the reads of stage s+1's B0 and A rows
-// 0-3 (published by the barrier) into free registers, and the loader may already overwrite the
-// stage-s buffer in the next stage.  B1 of a stage is read at its start and first used by the
-// third MFMA group of row 0.
-// PREB: stage s+1's B0 is read in phase B into a second register set (else B0 and B1 are read at
-// the start of each stage, the MFMAs of row 0 ordered by column block so the first waits on one)
-template <bool LOCAL = false, bool PREB = true>
-__global__ __launch_bounds__(256, 1) void k_syrk_h2q(const uint8_t* __restrict__ P, uint64_t pitch, uint64_t n,
-                                                     uint64_t kdim, const uint32_t* __restrict__ lut2,
-                                                     const uint32_t* __restrict__ flag, float* __restrict__ tiles,
-                                                     int accumulate, uint32_t part_rank = 0, uint32_t part_world = 1,
-                                                     uint64_t kslice = 0, uint64_t slice_elems = 0) {
-    constexpr int SBK = 2 * BK;  // 32 SNPs per LDS stage
-    constexpr int PLANE = 2 * B3_PLANE, STAGE = 2 * 2 * PLANE;
-    __shared__ __attribute__((aligned(16))) short lds[2 * STAGE];
-    if (*flag) return;  // a SNP of this block is outside fp16's range: k_syrk_bf3 runs instead
-    if (gridDim.y > 1) {
-        const uint64_t k0 = (uint64_t)blockIdx.y * kslice;
-        P += k0 * pitch;
-        lut2 += 4 * k0;
-        kdim = min(kslice, kdim - k0);
-        tiles += (uint64_t)blockIdx.y * slice_elems;
-    }
-    const uint64_t wg = blockIdx.x;
-    uint32_t bi, bj;
-    static_assert(!LOCAL, "the cfg5 part kernels read the part layout table (k_syrk_h2 / k_syrk_bf3)");
-    tile_coords(wg, bi, bj);
-    const uint64_t i0 = (uint64_t)bi * BW, j0 = (uint64_t)bj * BW;
-    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-    const int wm = wave >> 1, wn = wave & 1;
-    // loader role: panel lp, rows lk + 8h (h = 0..3) of the stage, 16-iid group ld_; row lk + 8h
-    // stores group ld_ in unit ld_ ^ (h & 1), its 16-B halves swapped by sw
-    const int lp = t >> 7, lk = (t >> 4) & 7, ld_ = t & 15;
-    const int sw = (ld_ >> 2) & 1;
-    const uint8_t* wp = P + (lp ? j0 : i0) / 4 + 4 * ld_ + (uint64_t)lk * pitch;
-    const uint8_t* wlast = P + (lp ? j0 : i0) / 4 + 4 * ld_ + (kdim - 1) * pitch;
-    const uint32_t* lp2 = lut2 + 4 * lk;
-    const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3, g1 = g & 1;
-    const int rowoff = (8 * g + q) * B3_RS + 4 * (pp & 1);
-    const int par[2] = {16 * g1, -16 * g1};                       // 16 (x ^ g1) - 16 x, x even / odd
-    const int hf[2] = {8 * (pp >> 1), 8 * ((pp >> 1) ^ 1)};      // half of columns 16x.. for x < 4 / >= 4
-    const int offA = rowoff + 128 * wm, offB = rowoff + 128 * wn;
-
-    f32x4 acc[8][8];
-#pragma unroll
-    for (int x = 0; x < 8; x++)
-#pragma unroll
-        for (int y = 0; y < 8; y++) acc[x][y] = (f32x4){};
-    const uint64_t nst = (kdim + SBK - 1) / SBK;
-
-    uint32_t rw[4];
-    uint4 rl[4];
-    auto load = [&](uint64_t st) {
-#pragma unroll
-        for (int h = 0; h < 4; h++) {
-            const uint8_t* a = wp + (st * SBK + 8 * h) * pitch;
-            rw[h] = *reinterpret_cast<const uint32_t*>(a <= wlast ? a : wlast);
-            rl[h] = *reinterpret_cast<const uint4*>(lp2 + 4 * (SBK * st + 8 * h));
-        }
-    };
-    auto make_sel = [&](uint32_t w, uint32_t (&sel)[8]) {
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            const uint32_t v = (w >> (2 * j)) & 0x03030303u;
-            const uint32_t o = v | 0x04040404u;
-            sel[2 * j] = __builtin_amdgcn_perm(o, v, 0x05010400u);
-            sel[2 * j + 1] = __builtin_amdgcn_perm(o, v, 0x07030602u);
-        }
-    };
-    auto store_plane = [&](short* S, int pl, int h, const uint32_t (&sel)[8]) {
-        const uint32_t lo = pl == 0 ? rl[h].x : rl[h].z;
-        const uint32_t hi = pl == 0 ? rl[h].y : rl[h].w;
-        uint4 v0, v1;
-        v0.x = __builtin_amdgcn_perm(hi, lo, sel[0]);
-        v0.y = __builtin_amdgcn_perm(hi, lo, sel[1]);
-        v0.z = __builtin_amdgcn_perm(hi, lo, sel[2]);
-        v0.w = __builtin_amdgcn_perm(hi, lo, sel[3]);
-        v1.x = __builtin_amdgcn_perm(hi, lo, sel[4]);
-        v1.y = __builtin_amdgcn_perm(hi, lo, sel[5]);
-        v1.z = __builtin_amdgcn_perm(hi, lo, sel[6]);
-        v1.w = __builtin_amdgcn_perm(hi, lo, sel[7]);
-        uint4* r4 = reinterpret_cast<uint4*>(S + (lp * 2 + pl) * PLANE + (lk + 8 * h) * B3_RS + 16 * (ld_ ^ (h & 1)));
-        r4[sw] = v0;
-        r4[sw ^ 1] = v1;
-    };
-    auto frag = [&](const short* S, int panel, int pl, int off) -> f16x8_t {
-        const short* b = S + (panel * 2 + pl) * PLANE + off;
-        const i16x4_t r0 = lds_tr16(b), r1 = lds_tr16(b + 4 * B3_RS);
-        return __builtin_bit_cast(f16x8_t, (i16x8_t)__builtin_shufflevector(r0, r1, 0, 1, 2, 3, 4, 5, 6, 7));
-    };
-    auto oA = [&](int x) { return offA + 16 * x + par[x & 1] + hf[x >> 2]; };
-    auto oB = [&](int y) { return offB + 16 * y + par[y & 1] + hf[y >> 2]; };
-    f16x8_t A0[8], A1[8], Bc0[8], Bn0[8], B1[8];
-    auto rows = [&](int x, const f16x8_t (&B0)[8]) {
-        if constexpr (PREB) {
-#pragma unroll
-            for (int y = 0; y < 8; y++) acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A0[x], B0[y], acc[x][y], 0, 0, 0);
-#pragma unroll
-            for (int y = 0; y < 8; y++) acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A1[x], B0[y], acc[x][y], 0, 0, 0);
-#pragma unroll
-            for (int y = 0; y < 8; y++) acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A0[x], B1[y], acc[x][y], 0, 0, 0);
-        } else {
-#pragma unroll
-            for (int y = 0; y < 8; y++) {
-                acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A0[x], B0[y], acc[x][y], 0, 0, 0);
-                acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A1[x], B0[y], acc[x][y], 0, 0, 0);
-                acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A0[x], B1[y], acc[x][y], 0, 0, 0);
-            }
-        }
-    };
-    {
-        load(0);
-#pragma unroll
-        for (int h = 0; h < 4; h++) {
-            uint32_t sel[8];
-            make_sel(rw[h], sel);
-            store_plane(lds, 0, h, sel);
-            store_plane(lds, 1, h, sel);
-        }
-        load(nst > 1 ? 1 : 0);
-    }
-    __syncthreads();
-#pragma unroll
-    for (int y = 0; y < 8; y++)
-        if constexpr (PREB) Bc0[y] = frag(lds, 1, 0, oB(y));
-#pragma unroll
-    for (int x = 0; x < 4; x++) {
-        A0[x] = frag(lds, 0, 0, oA(x));
-        A1[x] = frag(lds, 0, 1, oA(x));
-    }
-    auto stage = [&](uint64_t s, f16x8_t (&B0)[8], f16x8_t (&B0n)[8]) {
-        const short* cur = lds + (s & 1) * STAGE;
-        short* nxt = lds + ((s + 1) & 1) * STAGE;
-#pragma unroll
-        for (int y = 0; y < 8; y++) {
-            if constexpr (!PREB) B0[y] = frag(cur, 1, 0, oB(y));
-            B1[y] = frag(cur, 1, 1, oB(y));
-        }
-        // phase A: rows 0-3; rows 4-7 read from cur and stage s+1 stored into nxt beside them
-#pragma unroll
-        for (int x = 0; x < 4; x++) {
-            A0[x + 4] = frag(cur, 0, 0, oA(x + 4));
-            A1[x + 4] = frag(cur, 0, 1, oA(x + 4));
-            uint32_t sel[8];
-            make_sel(rw[x], sel);
-            store_plane(nxt, 0, x, sel);
-            store_plane(nxt, 1, x, sel);
-            rows(x, B0);
-        }
-        __syncthreads();  // stage s+1 published; every wave is done reading cur
-        load(s + 2 < nst ? s + 2 : nst - 1);
-        // phase B: rows 4-7 beside the reads of stage s+1's B0 and rows 0-3
-#pragma unroll
-        for (int x = 4; x < 8; x++) {
-            if constexpr (PREB) {
-                B0n[2 * (x - 4)] = frag(nxt, 1, 0, oB(2 * (x - 4)));
-                B0n[2 * (x - 4) + 1] = frag(nxt, 1, 0, oB(2 * (x - 4) + 1));
-            }
-            rows(x, B0);
-            A0[x - 4] = frag(nxt, 0, 0, oA(x - 4));
-            A1[x - 4] = frag(nxt, 0, 1, oA(x - 4));
-        }
-    };
-    if constexpr (PREB) {
-        for (uint64_t s = 0; s < nst; s += 2) {
-            stage(s, Bc0, Bn0);
-            if (s + 1 < nst) stage(s + 1, Bn0, Bc0);
-        }
-    } else {
-        for (uint64_t s = 0; s < nst; s++) stage(s, Bc0, Bc0);
-    }
-    // epilogue: the wave's 128x128 quarter is one whole 128-tile (2bi + wm, 2bj + wn)
-    float* T;
-    uint64_t ldo;
-    if constexpr (LOCAL) {
-        T = tiles + wg * (BW * BW) + (uint64_t)(wm * 128) * BW + wn * 128;
-        ldo = BW;
-    } else {
-        const uint64_t nt128 = (n + 127) / 128;
-        const uint64_t ti = 2 * (uint64_t)bi + wm, tj = 2 * (uint64_t)bj + wn;
-        if (ti > tj || tj >= nt128) return;  // wave-uniform
-        T = tiles + (tj * (tj + 1) / 2 + ti) * (uint64_t)(BM * BM);
-        ldo = BM;
-    }
-    const int r = lane >> 4, colp = pi16(lane & 15);
-#pragma unroll
-    for (int x = 0; x < 8; x++)
-#pragma unroll
-        for (int y = 0; y < 8; y++) {
-            float* bp = T + (16 * x + r) * ldo + 16 * y + colp;
-            if (accumulate) {
-                float old[4];
-#pragma unroll
-                for (int j = 0; j < 4; j++) old[j] = bp[4 * j * ldo];
-#pragma unroll
-                for (int j = 0; j < 4; j++) acc[x][y][j] += old[j];
-            }
-#pragma unroll
-            for (int j = 0; j < 4; j++) bp[4 * j * ldo] = acc[x][y][j];
-        }
-}
-
-// k_syrk_h2w: the 32x32x16 fp16x2 SYRK with ONE wave per SIMD (4 waves, up to 512 registers each):
-// each wave a 128x128 quarter of the 256x256 block (4 x 4 32x32 tiles, 256 accumulators), so a
-// 16-SNP k-step is 16 fragments (A and B, 2 planes x 4) for 48 MFMAs -- two thirds of the 8-wave
-// form's transposed LDS reads per MFMA, and the 32-cycle MFMA leaves room for the loader's VALU
-// and LDS issue that the 16x16x32 form (k_syrk_h2q) could not hide.  Same LDS image as k_syrk_h2
-// (32-SNP stages, rows lk + 8u written by 256 threads, 16-B halves swapped per bank group).
-// Per stage: k-step 1's fragments are read while k-step 0 computes; stage s+1's rows are expanded
-// and stored beside both k-steps; the barrier sits after k-step 1's first half, so the second half
-// covers the reads of stage s+1's k-step 0 (a second fragment set).
-// PIN bit 0: sched_group_barrier pins the interleave (1 MFMA, then up to 2-4 VALU / 1 DS read /
-// 1 DS write); bit 1: loader registers double-buffered by stage parity, stage s+2's codes/LUT
-// loaded at the START of stage s (a whole stage to arrive); bit 2: a scheduling barrier keeps
-// k-step 1's fragment reads at the top of the stage.
-template <bool LOCAL = false, int PIN = 0>
-__global__ __launch_bounds__(256, 1) void k_syrk_h2w(const uint8_t* __restrict__ P, uint64_t pitch, uint64_t n,
-                                                     uint64_t kdim, const uint32_t* __restrict__ lut2,
-                                                     const uint32_t* __restrict__ flag, float* __restrict__ tiles,
-                                                     int accumulate, uint32_t part_rank = 0, uint32_t part_world = 1,
-                                                     uint64_t kslice = 0, uint64_t slice_elems = 0) {
-    constexpr int SBK = 2 * BK;  // 32 SNPs per LDS stage
-    constexpr int PLANE = 2 * B3_PLANE, STAGE = 2 * 2 * PLANE;
-    __shared__ __attribute__((aligned(16))) short lds[2 * STAGE];
-    if (*flag) return;  // a SNP of this block is outside fp16's range: k_syrk_bf3 runs instead
-    if (gridDim.y > 1) {
-        const uint64_t k0 = (uint64_t)blockIdx.y * kslice;
-        P += k0 * pitch;
-        lut2 += 4 * k0;
-        kdim = min(kslice, kdim - k0);
-        tiles += (uint64_t)blockIdx.y * slice_elems;
-    }
-    const uint64_t wg = blockIdx.x;
-    uint32_t bi, bj;
-    static_assert(!LOCAL, "the cfg5 part kernels read the part layout table (k_syrk_h2 / k_syrk_bf3)");
-    tile_coords(wg, bi, bj);
-    const uint64_t i0 = (uint64_t)bi * BW, j0 = (uint64_t)bj * BW;
-    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-    const int wm = wave >> 1, wn = wave & 1;
-    // loader: panel lp, stage rows lk + 8u (u = 0..3), 16-iid group ld_
-    const int lp = t >> 7, lk = (t >> 4) & 7, ld_ = t & 15;
-    const int sw = (ld_ >> 2) & 1;
-    const uint8_t* wp = P + (lp ? j0 : i0) / 4 + 4 * ld_ + (uint64_t)lk * pitch;
-    const uint8_t* wlast = P + (lp ? j0 : i0) / 4 + 4 * ld_ + (kdim - 1) * pitch;
-    const uint32_t* lp2 = lut2 + 4 * lk;
-    const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
-    const int rd_off = (8 * (g >> 1) + q) * B3_RS + 16 * (g & 1) + 4 * pp;
-    const int dswz = (pp >> 1) ? -8 : 8;
-
-    f32x16 acc[4][4];
-#pragma unroll
-    for (int x = 0; x < 4; x++)
-#pragma unroll
-        for (int y = 0; y < 4; y++) acc[x][y] = (f32x16){};
-    const uint64_t nst = (kdim + SBK - 1) / SBK;
-
-    struct LdRegs {
-        uint32_t w[4];
-        uint4 l[4];
-    };
-    auto load = [&](uint64_t st, LdRegs& r) {
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-            const uint8_t* a = wp + (st * SBK + 8 * u) * pitch;
-            r.w[u] = *reinterpret_cast<const uint32_t*>(a <= wlast ? a : wlast);
-            r.l[u] = *reinterpret_cast<const uint4*>(lp2 + 4 * (SBK * st + 8 * u));
-        }
-    };
-    auto make_sel = [&](uint32_t w, uint32_t (&sel)[8]) {
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            const uint32_t v = (w >> (2 * j)) & 0x03030303u;
-            const uint32_t o = v | 0x04040404u;
-            sel[2 * j] = __builtin_amdgcn_perm(o, v, 0x05010400u);
-            sel[2 * j + 1] = __builtin_amdgcn_perm(o, v, 0x07030602u);
-        }
-    };
-    auto store_plane = [&](short* S, int pl, int u, const LdRegs& r, const uint32_t (&sel)[8]) {
-        const uint32_t lo = pl == 0 ? r.l[u].x : r.l[u].z;
-        const uint32_t hi = pl == 0 ? r.l[u].y : r.l[u].w;
-        uint4 v0, v1;
-        v0.x = __builtin_amdgcn_perm(hi, lo, sel[0]);
-        v0.y = __builtin_amdgcn_perm(hi, lo, sel[1]);
-        v0.z = __builtin_amdgcn_perm(hi, lo, sel[2]);
-        v0.w = __builtin_amdgcn_perm(hi, lo, sel[3]);
-        v1.x = __builtin_amdgcn_perm(hi, lo, sel[4]);
-        v1.y = __builtin_amdgcn_perm(hi, lo, sel[5]);
-        v1.z = __builtin_amdgcn_perm(hi, lo, sel[6]);
-        v1.w = __builtin_amdgcn_perm(hi, lo, sel[7]);
-        uint4* r4 = reinterpret_cast<uint4*>(S + (lp * 2 + pl) * PLANE + (lk + 8 * u) * B3_RS + 16 * ld_);
-        r4[sw] = v0;
-        r4[sw ^ 1] = v1;
-    };
-    auto expand = [&](short* S, int u, const LdRegs& r) {
-        uint32_t sel[8];
-        make_sel(r.w[u], sel);
-        store_plane(S, 0, u, r, sel);
-        store_plane(S, 1, u, r, sel);
-    };
-    auto frag = [&](const short* S, int panel, int pl, int h, int col, int off) -> f16x8_t {
-        const short* b = S + (panel * 2 + pl) * PLANE + h * BK * B3_RS + off + col;
-        const i16x4_t r0 = lds_tr16(b), r1 = lds_tr16(b + 4 * B3_RS);
-        return __builtin_bit_cast(f16x8_t, (i16x8_t)__builtin_shufflevector(r0, r1, 0, 1, 2, 3, 4, 5, 6, 7));
-    };
-    struct Frags {
-        f16x8_t a0[4], a1[4], b0[4], b1[4];
-    };
-    auto read = [&](const short* S, int h, Frags& F) {
-#pragma unroll
-        for (int x = 0; x < 4; x++) {
-            const int off = x >= 2 ? rd_off + dswz : rd_off;
-            F.a0[x] = frag(S, 0, 0, h, wm * 128 + 32 * x, off);
-            F.b0[x] = frag(S, 1, 0, h, wn * 128 + 32 * x, off);
-            F.a1[x] = frag(S, 0, 1, h, wm * 128 + 32 * x, off);
-            F.b1[x] = frag(S, 1, 1, h, wn * 128 + 32 * x, off);
-        }
-    };
-    auto pin = [&](auto n_other) {
-        if constexpr (PIN & 1) {
-#pragma unroll
-            for (int i = 0; i < 12; i++) {
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                           // MFMA
-                __builtin_amdgcn_sched_group_barrier(0x002, decltype(n_other)::value, 0);  // VALU
-                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);        // DS read
-                __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);        // DS write
-            }
-        }
-    };
-    // rows x0..x1-1 of a k-step: 3 products per 32x32 tile
-    auto rows = [&](const Frags& F, int x0, int x1) {
-#pragma unroll
-        for (int x = x0; x < x1; x++)
-#pragma unroll
-            for (int y = 0; y < 4; y++) {
-                acc[x][y] = __builtin_amdgcn_mfma_f32_32x32x16_f16(F.a0[x], F.b0[y], acc[x][y], 0, 0, 0);
-                acc[x][y] = __builtin_amdgcn_mfma_f32_32x32x16_f16(F.a0[x], F.b1[y], acc[x][y], 0, 0, 0);
-                acc[x][y] = __builtin_amdgcn_mfma_f32_32x32x16_f16(F.a1[x], F.b0[y], acc[x][y], 0, 0, 0);
-            }
-    };
-    LdRegs Ra, Rb;
-    load(0, Ra);
-#pragma unroll
-    for (int u = 0; u < 4; u++) expand(lds, u, Ra);
-    load(nst > 1 ? 1 : 0, Rb);
-    __syncthreads();
-    Frags F0, Fk;  // k-step 0 / k-step 1 fragments; F0 is refilled with stage s+1's k-step 0 once
-                   // stage s's k-step 0 is done
-    read(lds, 0, F0);
-    // the loader runs unconditionally (the last stage expands into the idle buffer, its code loads
-    // clamp to the last SNP) so the MFMAs and their VALU share basic blocks
-    // R holds stage s+1's codes/LUT (expanded during stage s); Rn receives stage s+2's
-    auto stage = [&](uint64_t s, LdRegs& R, LdRegs& Rn) {
-        const short* cur = lds + (s & 1) * STAGE;
-        short* nxt = lds + ((s + 1) & 1) * STAGE;
-        const uint64_t s2 = s + 2 < nst ? s + 2 : nst - 1;
-        read(cur, 1, Fk);
-        if constexpr (PIN & 4) __builtin_amdgcn_sched_barrier(0);
-        if constexpr (PIN & 2) load(s2, Rn);
-        rows(F0, 0, 2);
-        expand(nxt, 0, R);
-        pin(std::integral_constant<int, 2>{});
-        rows(F0, 2, 4);
-        expand(nxt, 1, R);
-        pin(std::integral_constant<int, 2>{});
-        rows(Fk, 0, 2);
-        expand(nxt, 2, R);
-        expand(nxt, 3, R);
-        pin(std::integral_constant<int, 4>{});
-        if constexpr (!(PIN & 2)) load(s2, R);
-        __syncthreads();  // stage s+1 published; every wave is done reading cur
-        read(nxt, 0, F0);
-        rows(Fk, 2, 4);
-    };
-    if constexpr (PIN & 2) {
-        for (uint64_t s = 0; s < nst; s += 2) {
-            stage(s, Rb, Ra);
-            if (s + 1 < nst) stage(s + 1, Ra, Rb);
-        }
-    } else {
-        for (uint64_t s = 0; s < nst; s++) stage(s, Rb, Rb);
-    }
-    // epilogue: the wave's 128x128 quarter is one whole 128-tile (2bi + wm, 2bj + wn)
-    float* T;
-    uint64_t ldo;
-    if constexpr (LOCAL) {
-        T = tiles + wg * (BW * BW) + (uint64_t)(wm * 128) * BW + wn * 128;
-        ldo = BW;
-    } else {
-        const uint64_t nt128 = (n + 127) / 128;
-        const uint64_t ti = 2 * (uint64_t)bi + wm, tj = 2 * (uint64_t)bj + wn;
-        if (ti > tj || tj >= nt128) return;  // wave-uniform
-        T = tiles + (tj * (tj + 1) / 2 + ti) * (uint64_t)(BM * BM);
-        ldo = BM;
-    }
-    const int hh = lane >> 5, colp = 16 * ((lane >> 4) & 1) + pi16(lane & 15);
-#pragma unroll
-    for (int x = 0; x < 4; x++)
-#pragma unroll
-        for (int y = 0; y < 4; y++) {
-            float* bp = T + (32 * x + hh) * ldo + 32 * y + colp;
-            if (accumulate) {
-                float old[16];
-#pragma unroll
-                for (int r = 0; r < 16; r++) old[r] = bp[(16 * (r >> 3) + 4 * (r & 3) + 2 * ((r >> 2) & 1)) * ldo];
-#pragma unroll
-                for (int r = 0; r < 16; r++) acc[x][y][r] += old[r];
-            }
-#pragma unroll
-            for (int r = 0; r < 16; r++) bp[(16 * (r >> 3) + 4 * (r & 3) + 2 * ((r >> 2) & 1)) * ldo] = acc[x][y][r];
-        }
-}
-
 }  // namespace f32w
 
 // ====================================================================== f64
@@ -2370,37 +1418,6 @@ struct PRegs {
     uint32_t w;
     double l[4];
 };
-
-[[maybe_unused]] __device__ __forceinline__ void load_dense(const double* __restrict__ Z, uint64_t ldz, uint64_t kdim, uint64_t k0,
-                                           uint64_t i0, uint64_t j0, double2 (&ra)[4], double2 (&rb)[4]) {
-    const int t = threadIdx.x;
-#pragma unroll
-    for (int q = 0; q < 4; q++) {
-        const int f = t + 256 * q;
-        const int k = f >> 6, i2 = f & 63;
-        const bool ok = k0 + k < kdim;
-        const uint64_t kk = ok ? k0 + k : kdim - 1;
-        double2 va = *reinterpret_cast<const double2*>(Z + kk * ldz + i0 + 2 * i2);
-        double2 vb = *reinterpret_cast<const double2*>(Z + kk * ldz + j0 + 2 * i2);
-        if (!ok) {
-            va = make_double2(0.0, 0.0);
-            vb = va;
-        }
-        ra[q] = va;
-        rb[q] = vb;
-    }
-}
-
-[[maybe_unused]] __device__ __forceinline__ void store_dense(double* As, double* Bs, const double2 (&ra)[4], const double2 (&rb)[4]) {
-    const int t = threadIdx.x;
-#pragma unroll
-    for (int q = 0; q < 4; q++) {
-        const int f = t + 256 * q;
-        const int k = f >> 6, i2 = f & 63;
-        *reinterpret_cast<double2*>(As + k * LDA + 2 * i2) = ra[q];
-        *reinterpret_cast<double2*>(Bs + k * LDA + 2 * i2) = rb[q];
-    }
-}
 
 // packed: op = t>>7; 128 threads cover BK=16 SNPs x 8 dwords.
 __device__ __forceinline__ void load_packed(const uint8_t* __restrict__ P, uint64_t pitch, uint64_t kdim, uint64_t k0,
@@ -2473,6 +1490,7 @@ __device__ __forceinline__ void store_packed_bfi(double* As, double* Bs, const P
     }
 }
 
+// one stage's MFMAs: 16 SNPs x the wave's 64 x 64 (4 x 4 v_mfma_f64_16x16x4f64 tiles)
 __device__ __forceinline__ void compute(const double* As, const double* Bs, f64x4 (&acc)[4][4], int wm, int wn,
                                         int lane) {
     const int kr = lane >> 4, c = lane & 15;
@@ -2492,7 +1510,7 @@ __device__ __forceinline__ void compute(const double* As, const double* Bs, f64x
     }
 }
 
-// compute() with the next stage's LDS store (bfi select) spread between its MFMA groups, so
+// The stage's MFMAs with the next stage's LDS store (bfi select) spread between its MFMA groups, so
 // the select VALU issues while the wave's own MFMAs are in flight instead of after them.
 template <bool ROT = false>
 __device__ __forceinline__ void compute_store(const double* As, const double* Bs, f64x4 (&acc)[4][4], int wm, int wn,
@@ -2541,10 +1559,11 @@ __device__ __forceinline__ void epilogue(f64x4 (&acc)[4][4], double* __restrict_
         }
 }
 
-// MODE 0: production; 1: bfi select; 2: bfi select interleaved with the MFMAs;
-// 10: compute only (ablation); 11: loader only (ablation)
-template <bool PACKED, int MODE = 0>
-__global__ __launch_bounds__(256, 2) void k_syrk(const void* __restrict__ src, uint64_t ld, uint64_t kdim,
+// f64 GRM of packed codes on the f64 MFMA (the CRT path's fallback for a non-finite LUT, and hook
+// "f64" = 1): 128x128 tiles, 4 waves; the select of stage s+1's values is interleaved with stage s's
+// MFMAs and stored bank-rotated (compute_store<true>): 60.5 TFLOP/s = 0.77 of 78.6 at N = 32768
+// (tools/ubench.py syrk --dtype f64).  part_tab (cfg5): quadrant q of slot w of the part's layout.
+__global__ __launch_bounds__(256, 2) void k_syrk(const uint8_t* __restrict__ src, uint64_t ld, uint64_t kdim,
                                                  const double* __restrict__ lut, double* __restrict__ tiles,
                                                  int accumulate, const int* __restrict__ gate = nullptr,
                                                  const uint32_t* __restrict__ part_tab = nullptr) {
@@ -2573,50 +1592,15 @@ __global__ __launch_bounds__(256, 2) void k_syrk(const void* __restrict__ src, u
         for (int y = 0; y < 4; y++) acc[x][y] = (f64x4){};
 
     const uint64_t nst = (kdim + BK - 1) / BK;
-    double2 ra[4], rb[4];
     PRegs rp;
-    if constexpr (PACKED) {
-        load_packed((const uint8_t*)src, ld, kdim, 0, i0, j0, lut, rp);
-        store_packed(lds[0][0], lds[0][1], rp);
-        if constexpr (MODE == 3)
-            if (nst > 1) load_packed((const uint8_t*)src, ld, kdim, BK, i0, j0, lut, rp);
-    } else {
-        load_dense((const double*)src, ld, kdim, 0, i0, j0, ra, rb);
-        store_dense(lds[0][0], lds[0][1], ra, rb);
-    }
+    load_packed(src, ld, kdim, 0, i0, j0, lut, rp);
+    store_packed(lds[0][0], lds[0][1], rp);
     __syncthreads();
     for (uint64_t s = 0; s < nst; s++) {
         const int buf = s & 1;
-        const bool more = s + 1 < nst && MODE != 10 && MODE != 3;
-        if (more) {
-            if constexpr (PACKED) load_packed((const uint8_t*)src, ld, kdim, (s + 1) * BK, i0, j0, lut, rp);
-            else load_dense((const double*)src, ld, kdim, (s + 1) * BK, i0, j0, ra, rb);
-        }
-        if constexpr ((MODE == 2 || MODE == 4) && PACKED) {
-            compute_store<MODE == 4>(lds[buf][0], lds[buf][1], acc, wm, wn, lane, lds[buf ^ 1][0], lds[buf ^ 1][1], rp,
-                                     more);
-            __syncthreads();
-            continue;
-        }
-        if constexpr (MODE == 3 && PACKED) {
-            // prefetch distance 2: rp holds stage s+1 (loaded one stage ago), rq gets stage s+2
-            PRegs rq;
-            if (s + 2 < nst) load_packed((const uint8_t*)src, ld, kdim, (s + 2) * BK, i0, j0, lut, rq);
-            compute_store(lds[buf][0], lds[buf][1], acc, wm, wn, lane, lds[buf ^ 1][0], lds[buf ^ 1][1], rp,
-                          s + 1 < nst);
-            rp = rq;
-            __syncthreads();
-            continue;
-        }
-        if constexpr (MODE != 11) compute(lds[buf][0], lds[buf][1], acc, wm, wn, lane);
-        if (more) {
-            if constexpr (PACKED) {
-                if constexpr (MODE == 1) store_packed_bfi(lds[buf ^ 1][0], lds[buf ^ 1][1], rp);
-                else store_packed(lds[buf ^ 1][0], lds[buf ^ 1][1], rp);
-            } else {
-                store_dense(lds[buf ^ 1][0], lds[buf ^ 1][1], ra, rb);
-            }
-        }
+        const bool more = s + 1 < nst;
+        if (more) load_packed(src, ld, kdim, (s + 1) * BK, i0, j0, lut, rp);
+        compute_store<true>(lds[buf][0], lds[buf][1], acc, wm, wn, lane, lds[buf ^ 1][0], lds[buf ^ 1][1], rp, more);
         __syncthreads();
     }
     epilogue(acc, T, ldo, accumulate, lane, wm, wn);
@@ -2701,61 +1685,26 @@ void launch_syrk_packed(const uint8_t* packed, uint64_t pitch, uint64_t n, uint6
         // N=50k (82%) vs 118 for 128x128 / 4 waves; below ~4k iids the 256 tiles leave CUs idle.
         const uint64_t nb = ceil_div(n, 256);
         // Reached for f32 only when the product path is forced off the fp16x2/bf16x3 kernels
-        // (variant 20 below N = 4096) or by the ubench build's ablations.
-        int v = g_variant_syrk;
-        if (v == 0 || v == 20) v = n >= 4096 ? 4 : 5;
-        if (v == 4 || v == 5) {
-            for_segments(m, accumulate, [&](uint64_t c0, uint64_t cnt, int acc) {
-                if (v == 4)
-                    f32w::k_syrk256<1><<<(unsigned)(nb * (nb + 1) / 2), 512, 0, st>>>(packed + c0 * pitch, pitch, n, cnt,
-                                                                                     L + 4 * c0, Tt, acc);
-                else
-                    f32k::k_syrk<true, 16, 4><<<(unsigned)nt, 256, 0, st>>>(packed + c0 * pitch, pitch, cnt, L + 4 * c0,
-                                                                           Tt, acc);
-                SNPMI_HIP(hipGetLastError());
-            });
-            return;
-        }
-        switch (v) {
-#ifdef SNPMI_UBENCH
-            case 1: f32k::k_syrk<true, 32, 2><<<(unsigned)nt, 256, 0, st>>>(packed, pitch, m, L, Tt, accumulate); break;
-            case 2: f32k::k_syrk_il<4><<<(unsigned)nt, 256, 0, st>>>(packed, pitch, m, L, Tt, accumulate); break;
-            case 3: f32k::k_syrk_il<3><<<(unsigned)nt, 256, 0, st>>>(packed, pitch, m, L, Tt, accumulate); break;
-            case 6:
-                f32w::k_syrk256<1, false, true>
-                    <<<(unsigned)(nb * (nb + 1) / 2), 512, 0, st>>>(packed, pitch, n, m, L, Tt, accumulate);
-                break;
-            case 7:
-                f32w::k_syrk256<1, false, false, true>
-                    <<<(unsigned)(nb * (nb + 1) / 2), 512, 0, st>>>(packed, pitch, n, m, L, Tt, accumulate);
-                break;
-            case 10: f32k::k_syrk_ablate<1><<<(unsigned)nt, 256, 0, st>>>(packed, pitch, m, L, Tt, accumulate); break;
-            case 11: f32k::k_syrk_ablate<2><<<(unsigned)nt, 256, 0, st>>>(packed, pitch, m, L, Tt, accumulate); break;
-            case 12: f32k::k_syrk_il<4, 1><<<(unsigned)nt, 256, 0, st>>>(packed, pitch, m, L, Tt, accumulate); break;
-            case 13: f32k::k_syrk_il<4, 2><<<(unsigned)nt, 256, 0, st>>>(packed, pitch, m, L, Tt, accumulate); break;
-            case 14: f32k::k_syrk_il<4, 3><<<(unsigned)nt, 256, 0, st>>>(packed, pitch, m, L, Tt, accumulate); break;
-            case 15: f32k::k_syrk_il<4, 4><<<(unsigned)nt, 256, 0, st>>>(packed, pitch, m, L, Tt, accumulate); break;
-#endif
-            default: f32k::k_syrk<true, 16, 4><<<(unsigned)nt, 256, 0, st>>>(packed, pitch, m, L, Tt, accumulate);
-        }
+        // (variant 20; below N = 4096 the 128x128 kernel, variant 5)
+        const bool big = g_variant_syrk != 5 && n >= 4096;
+        for_segments(m, accumulate, [&](uint64_t c0, uint64_t cnt, int acc) {
+            if (big)
+                f32w::k_syrk256<1><<<(unsigned)(nb * (nb + 1) / 2), 512, 0, st>>>(packed + c0 * pitch, pitch, n, cnt,
+                                                                                 L + 4 * c0, Tt, acc);
+            else
+                f32k::k_syrk<true, 16, 4><<<(unsigned)nt, 256, 0, st>>>(packed + c0 * pitch, pitch, cnt, L + 4 * c0, Tt,
+                                                                       acc);
+            SNPMI_HIP(hipGetLastError());
+        });
+        return;
     }
     else {
         const double* L = (const double*)lut;
         double* Tt = (double*)tiles;
-        // tools/ubench.py syrk --dtype f64 (N=32768, 8192 SNPs): 5 = plain loader 51.3 TFLOP/s,
-        // 2 = select interleaved with the MFMAs 56.1, 0 = that + bank-rotated LDS stores 60.5
-        // (77% of 78.6); 10 = MFMA-only ablation 71.5.
-        switch (g_variant_syrk) {
-#ifdef SNPMI_UBENCH
-            case 1: f64k::k_syrk<true, 1><<<(unsigned)nt, 256, 0, st>>>(packed, pitch, m, L, Tt, accumulate); break;
-            case 2: f64k::k_syrk<true, 2><<<(unsigned)nt, 256, 0, st>>>(packed, pitch, m, L, Tt, accumulate); break;
-            case 3: f64k::k_syrk<true, 3><<<(unsigned)nt, 256, 0, st>>>(packed, pitch, m, L, Tt, accumulate); break;
-            case 5: f64k::k_syrk<true, 0><<<(unsigned)nt, 256, 0, st>>>(packed, pitch, m, L, Tt, accumulate); break;
-            case 10: f64k::k_syrk<true, 10><<<(unsigned)nt, 256, 0, st>>>(packed, pitch, m, L, Tt, accumulate); break;
-            case 11: f64k::k_syrk<true, 11><<<(unsigned)nt, 256, 0, st>>>(packed, pitch, m, L, Tt, accumulate); break;
-#endif
-            default: f64k::k_syrk<true, 4><<<(unsigned)nt, 256, 0, st>>>(packed, pitch, m, L, Tt, accumulate);
-        }
+        // tools/ubench.py syrk --dtype f64 (N=32768, 8192 SNPs): plain loader 51.3 TFLOP/s, select
+        // interleaved with the MFMAs 56.1, that + bank-rotated LDS stores (MODE 4) 60.5 (77% of
+        // 78.6); MFMA-only ablation 71.5.
+        f64k::k_syrk<<<(unsigned)nt, 256, 0, st>>>(packed, pitch, m, L, Tt, accumulate);
     }
     SNPMI_HIP(hipGetLastError());
 }
@@ -2766,7 +1715,7 @@ void launch_syrk_packed_f64_gated(const uint8_t* packed, uint64_t pitch, uint64_
     const uint64_t nt = part_tab ? 4 * part_blocks : n_tiles_upper(n);
     if (nt == 0 || m == 0) return;
     SNPMI_REQUIRE(nt < (1ull << 31), SNPMI_E_ARG, "too many GRM tiles for one launch");
-    f64k::k_syrk<true, 4><<<(unsigned)nt, 256, 0, st>>>(packed, pitch, m, lut, tiles, accumulate, gate, part_tab);
+    f64k::k_syrk<<<(unsigned)nt, 256, 0, st>>>(packed, pitch, m, lut, tiles, accumulate, gate, part_tab);
     SNPMI_HIP(hipGetLastError());
 }
 
@@ -2871,22 +1820,6 @@ void supertile_order(uint64_t nb, bool xcd, std::vector<uint32_t>& tab) {
         }
 }
 
-#ifdef SNPMI_UBENCH
-// device copy of supertile_order(nb, xcd) for the packed-SYRK order A/B (variants 65/66)
-static const uint32_t* ub_order(uint64_t nb, bool xcd) {
-    static uint32_t* tab[2] = {};
-    static uint64_t tnb[2] = {};
-    if (tnb[xcd] != nb) {
-        std::vector<uint32_t> t;
-        supertile_order(nb, xcd, t);
-        if (tab[xcd]) SNPMI_HIP(hipFree(tab[xcd]));
-        SNPMI_HIP(hipMalloc(&tab[xcd], t.size() * sizeof(uint32_t)));
-        SNPMI_HIP(hipMemcpy(tab[xcd], t.data(), t.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
-        tnb[xcd] = nb;
-    }
-    return tab[xcd];
-}
-#endif
 
 // hook "h2": 1 = k_syrk_h2s (loader waves, default: 256.6 vs 270.0 ms per 50k x 62.5k launch in one
 // process, profiles/r06g), 0 = k_syrk_h2 MODE 4 (loader in every wave)
@@ -2968,84 +1901,26 @@ void launch_syrk_packed_bf3(const uint8_t* packed, uint64_t pitch, uint64_t n, u
     // plane index, 3 VGPRs spilled) lost: 296.8 vs 313.5 (ubench_syrk_bf3_stagger.jsonl).
     if (h2) {
         // MI355X, N=50k, 10k SNPs (tools/ubench.py syrk, profiles/r01j/ubench_syrk_h2_modes.jsonl):
-        // 32-SNP stages, compiler-ordered loader (MODE 4, default) 577 TFLOP/s; 16-SNP stages:
-        // MODE 1 530-554, loader pinned one-three VALU per MFMA (40) 539-545, next A plane-0
-        // prefetched after the barrier (42) 505, + pin (43) 551-564; 32-SNP + pin (46) 564;
-        // bf16x3 (36) 300-313.
-        switch (g_variant_syrk) {
-#ifdef SNPMI_UBENCH
-            // measured N=50k, 10k SNPs (profiles/r02l/): 16x16x32 MFMA runs at 2.32-2.35 GHz vs
-            // 2.06 for 32x32x16, but MFMA busy falls to 0.64-0.66 (8 waves; the 16x16 MFMA holds
-            // vector issue for 8 of its 16 cycles, so the loader's VALU + LDS issue no longer fits
-            // the gaps) and 0.60 (4 waves, 128x128 per wave): 526-539 / 496 vs 552-585 TFLOP/s
-            case 50: f32w::k_syrk_h2x<false><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles, accumulate); break;
-            case 51: f32w::k_syrk_h2x<false, 1><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles, accumulate); break;
-            case 52: f32w::k_syrk_h2x<false, 2><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles, accumulate); break;
-            case 53: f32w::k_syrk_h2x<false, 3><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles, accumulate); break;
-            case 54: f32w::k_syrk_h2q<false><<<(unsigned)g, 256, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles, accumulate); break;
-            case 55: f32w::k_syrk_h2q<false, false><<<(unsigned)g, 256, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles, accumulate); break;
-            case 56: f32w::k_syrk_h2w<false><<<(unsigned)g, 256, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles, accumulate); break;
-            case 57: f32w::k_syrk_h2w<false, 1><<<(unsigned)g, 256, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles, accumulate); break;
-            case 58: f32w::k_syrk_h2w<false, 3><<<(unsigned)g, 256, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles, accumulate); break;
-            case 59: f32w::k_syrk_h2w<false, 7><<<(unsigned)g, 256, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles, accumulate); break;
-            case 60: f32w::k_syrk_h2w<false, 2><<<(unsigned)g, 256, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles, accumulate); break;
-            case 61: f32w::k_syrk_h2w<false, 5><<<(unsigned)g, 256, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles, accumulate); break;
-            case 40: f32w::k_syrk_h2<false, 0><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles, accumulate); break;
-            case 42: f32w::k_syrk_h2<false, 2><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles, accumulate); break;
-            case 43: f32w::k_syrk_h2<false, 3><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles, accumulate); break;
-            case 41: f32w::k_syrk_h2<false, 1><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles, accumulate); break;
-            case 46: f32w::k_syrk_h2<false, 5><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles, accumulate); break;
-            case 47: f32w::k_syrk_h2<false, 7><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles, accumulate); break;
-            case 48: f32w::k_syrk_h2<false, 8><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles, accumulate); break;
-            case 62: f32w::k_syrk_h2<false, 10><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles, accumulate); break;
-            case 63: f32w::k_syrk_h2<false, 11><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles, accumulate); break;
-            case 64:  // A/B: MODE 4 with the round-3 swap layout of its ds_write_b64 stores
-                f32w::k_syrk_h2<false, 4, false, false><<<(unsigned)g, 512, 0, st>>>(
-                    packed, pitch, n, m, h2->lut2, h2->flag, tiles, accumulate, 0, 1, 0, 0, seg_ctx(),
-                    packed_block_order(ceil_div(n, 256)));
-                break;
-            case 65:  // A/B: plain triangular block order
-                f32w::k_syrk_h2<false, 4><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles,
-                                                                      accumulate, 0, 1, 0, 0, seg_ctx());
-                break;
-            case 66:  // A/B: supertile order with each supertile dealt over the 8 XCDs
-                f32w::k_syrk_h2<false, 4><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles,
-                                                                      accumulate, 0, 1, 0, 0, seg_ctx(),
-                                                                      ub_order(ceil_div(n, 256), true));
-                break;
-#endif
-            default:
-                // supertile block order: the ~256 blocks in flight share ~32 code panels instead of
-                // ~nb (+1.7-2.4% at 50k x 31.25k / 62.5k vs the triangular order,
-                // profiles/r03crt/ubench_block_order.jsonl)
-                if (g_h2_kernel == 1)
-                    f32w::k_syrk_h2s<false><<<(unsigned)g, 768, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles,
-                                                                        accumulate, 0, 1, 0, 0, seg_ctx(),
-                                                                        packed_block_order(ceil_div(n, 256)));
-                else
-                    f32w::k_syrk_h2<false, 4><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles,
-                                                                          accumulate, 0, 1, 0, 0, seg_ctx(),
-                                                                          packed_block_order(ceil_div(n, 256)));
-        }
+        // 32-SNP stages, compiler-ordered loader (MODE 4) 577 TFLOP/s; 16-SNP stages 505-564;
+        // bf16x3 300-313.  Round 6: the loader in its own waves (k_syrk_h2s) 256.6 vs 270.0 ms per
+        // 50k x 62.5k launch (profiles/r06g).  Supertile block order: the ~256 blocks in flight share
+        // ~32 code panels instead of ~nb (+1.7-2.4% vs the triangular order, profiles/r03crt).
+        if (g_h2_kernel == 1)
+            f32w::k_syrk_h2s<false><<<(unsigned)g, 768, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles,
+                                                                accumulate, 0, 1, 0, 0, seg_ctx(),
+                                                                packed_block_order(ceil_div(n, 256)));
+        else
+            f32w::k_syrk_h2<false, 4><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, tiles,
+                                                                  accumulate, 0, 1, 0, 0, seg_ctx(),
+                                                                  packed_block_order(ceil_div(n, 256)));
         SNPMI_HIP(hipGetLastError());
         f32w::k_syrk_bf3<false, false, 5><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, lut3, tiles, accumulate, 0, 1, 0, 0,
                                                                       h2->flag, seg_ctx());
         SNPMI_HIP(hipGetLastError());
         return;
     }
-    switch (g_variant_syrk) {
-#ifdef SNPMI_UBENCH
-        case 30: f32w::k_syrk_bf3<><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, lut3, tiles, accumulate); break;
-        case 31: f32w::k_syrk_bf3<false, true><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, lut3, tiles, accumulate); break;
-        case 32: f32w::k_syrk_bf3<false, true, 1><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, lut3, tiles, accumulate); break;
-        case 33: f32w::k_syrk_bf3<false, false, 1><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, lut3, tiles, accumulate); break;
-        case 34: f32w::k_syrk_bf3<false, false, 2><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, lut3, tiles, accumulate); break;
-        case 39: f32w::k_syrk_bf3<false, true, 9><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, lut3, tiles, accumulate); break;
-#endif
-        default:
-            f32w::k_syrk_bf3<false, false, 5><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, lut3, tiles, accumulate, 0, 1,
-                                                                          0, 0, nullptr, seg_ctx());
-    }
+    f32w::k_syrk_bf3<false, false, 5><<<(unsigned)g, 512, 0, st>>>(packed, pitch, n, m, lut3, tiles, accumulate, 0, 1, 0,
+                                                                  0, nullptr, seg_ctx());
     SNPMI_HIP(hipGetLastError());
 }
 
@@ -3159,15 +2034,6 @@ void launch_syrk_dense(const void* Z, uint64_t ldz, uint64_t n, uint64_t m, int 
         const unsigned g = (unsigned)(nb * (nb + 1) / 2);
         const float* Zf = (const float*)Z;
         float* Tf = (float*)tiles;
-#ifdef SNPMI_UBENCH
-        if (n >= 4096 && ldz >= nb * 256 && g_variant_syrk == 8)
-            f32w::k_syrk256d<false, 32, 2><<<g, 512, 0, st>>>(Zf, ldz, n, m, Tf, accumulate);
-        else if (n >= 4096 && ldz >= nb * 256 && g_variant_syrk == 9)
-            f32w::k_syrk256d<false, 16, 3><<<g, 512, 0, st>>>(Zf, ldz, n, m, Tf, accumulate);
-        else if (n >= 4096 && ldz >= nb * 256 && g_variant_syrk == 21)
-            f32w::k_syrk256d<false, 16, 2, true><<<g, 512, 0, st>>>(Zf, ldz, n, m, Tf, accumulate);
-        else
-#endif
         if (n >= 4096 && ldz >= nb * 256 && g_variant_syrk != 5)
             for_segments(m, accumulate, [&](uint64_t c0, uint64_t cnt, int acc) {
                 f32w::k_syrk256d<><<<g, 512, 0, st>>>(Zf + c0 * ldz, ldz, n, cnt, Tf, acc);
@@ -3179,11 +2045,6 @@ void launch_syrk_dense(const void* Z, uint64_t ldz, uint64_t n, uint64_t m, int 
                 SNPMI_HIP(hipGetLastError());
             });
     }
-#ifdef SNPMI_UBENCH
-    else if (g_variant_syrk == 5) {
-        f64k::k_syrk<false><<<(unsigned)nt, 256, 0, st>>>(Z, ldz, m, nullptr, (double*)tiles, accumulate);
-    }
-#endif
     else {
         f64k::k_syrk_glds<<<(unsigned)nt, 256, 0, st>>>((const double*)Z, ldz, m, (double*)tiles, accumulate);
     }

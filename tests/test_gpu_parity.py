@@ -329,7 +329,7 @@ def syrk_variant(request):
     the f32-MFMA k_syrk256d as fallback), 36 = the bf16x3 kernel alone, 20 = the f32-MFMA
     kernels (two-phase decode to Z + glds SYRK at N >= 4096, the 128x128 kernel below), 5 =
     the 128x128 small-N kernels; f64: every variant runs the f64 kernels (0 / 20 / 36: the
-    default fused / glds kernels).  The ablation variants live in the ubench build only."""
+    default fused / glds kernels).  The ablation variants of rounds 1-5 were deleted in round 6."""
     N.call("snpmi_set_kernel_variant", b"syrk", request.param)
     yield request.param
     N.call("snpmi_set_kernel_variant", b"syrk", 0)

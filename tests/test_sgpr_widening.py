@@ -66,6 +66,6 @@ def test_checker_catches_the_round5_pattern():
 
 
 def test_product_sources_hold_no_ubench_variants():
-    for name in ("kernels.hip", "syrk_crt.hip"):
+    for name in ("kernels.hip", "syrk_crt.hip", "syrk.hip", "api.hip"):
         with open(os.path.join(CSRC, name)) as f:
             assert "SNPMI_UBENCH" not in f.read(), name

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-5 profiling recipe, run ON THE GPU BOX (via gpurun).  Usage: tools/profile_r06.sh <tag>
+# Round-6 profiling recipe, run ON THE GPU BOX (via gpurun).  Usage: tools/profile_r06.sh <tag>
 #  1. kernel trace + stats of the default bench (per-kernel average durations; tools/trace_summary.py)
 #  2. separate PMC passes FETCH_SIZE / WRITE_SIZE on a decode-only run, a GRM-only run (cfg4 shape,
 #     2 launches of 62500 SNPs) and the dense standardize (50k x 100k f32 in HBM, round-4 kernel)
