@@ -27,6 +27,7 @@ def main():
     p.add_argument("--rounds", type=int, default=3)
     p.add_argument("--forms", default="0,1")
     p.add_argument("--miss", type=float, default=0.01)
+    p.add_argument("--part", default=None, help="P/W: the cfg5 part kernel, part P of W (e.g. 0/8), into its blocks")
     p.add_argument("--dtype", choices=["f32", "f64"], default="f64",
                    help="f64: the residue SYRK forms (hook crt); f32: the fp16x2 SYRK forms (hook h2)")
     a = p.parse_args()
@@ -38,7 +39,9 @@ def main():
     synth(N, packed.p, pitch, n, 0, m, 105, a.miss)
     lut, st = Dev(N, m * 4 * esz), Dev(N, m * 2 * esz)
     N.call("snpmi_dev_snp_stats", packed.p, pitch, n, m, 0, N.STD_UNIT, 0.0, 0.0, 0, dt, st.p, lut.p)
-    tb = N.lib().snpmi_grm_tile_bytes(n, dt)
+    part = tuple(int(x) for x in a.part.split("/")) if a.part else None
+    nloc = N.lib().snpmi_grm_part_blocks(n, part[0], part[1]) if part else 0
+    tb = nloc * 65536 * esz if part else N.lib().snpmi_grm_tile_bytes(n, dt)
     tiles = Dev(N, tb)
     forms = [int(f) for f in a.forms.split(",")]
     ev = Events(N, 2)
@@ -50,7 +53,11 @@ def main():
             N.call("snpmi_set_kernel_variant", hook, f)
             N.call("snpmi_crt_moduli_stats", ctypes.byref(sum_r), ctypes.byref(nl), 1)
             ev.record(0)
-            N.call("snpmi_dev_syrk_packed", packed.p, pitch, n, m, lut.p, dt, tiles.p, 0)
+            if part:
+                N.call("snpmi_dev_syrk_packed_part" + ("_f64" if esz == 8 else ""), packed.p, pitch, n, m, lut.p,
+                       part[0], part[1], tiles.p, 0)
+            else:
+                N.call("snpmi_dev_syrk_packed", packed.p, pitch, n, m, lut.p, dt, tiles.p, 0)
             ev.record(1)
             N.call("snpmi_stream_sync")
             if rnd:
@@ -68,14 +75,14 @@ def main():
     # executed MFMA work: f64 = R int8 SYRKs (5.0 POP/s dense); f32 = 3 fp16 products (2.5 PF/s dense)
     R, peak = (sum_r.value / max(nl.value, 1), 5000.0) if a.dtype == "f64" else (3.0, 2500.0)
     nb = (n + 255) // 256
-    ops = R * 2 * 256 * 256 * (nb * (nb + 1) // 2) * m
+    ops = R * 2 * 256 * 256 * (nloc if part else nb * (nb + 1) // 2) * m
     base = sums[forms[0]]
     for f in forms:
         t = float(np.median(res[f]))
         names = {b"crt": {0: "k_syrk_i8r", 1: "k_syrk_i8w"}, b"h2": {0: "k_syrk_h2<.,4>", 1: "k_syrk_h2s"}}[hook]
         print(json.dumps({"form": f, "kernel": names.get(f, "ablation %d" % f), "dtype": a.dtype, "n": n, "m": m,
                           "median_ms": t, "all_ms": res[f], "moduli": R if a.dtype == "f64" else None,
-                          "frac_mfma_peak_executed": ops / t / 1e9 / peak, "syrk_tflops": n * (n + 1) * m / t / 1e9,
+                          "frac_mfma_peak_executed": ops / t / 1e9 / peak, "syrk_tflops": n * (n + 1) * m / t / 1e9 / (part[1] if part else 1), "part": a.part,
                           "tiles_equal_form0": bool(np.array_equal(sums[f], base))}), flush=True)
 
 
