@@ -8,16 +8,16 @@
 # multi-threaded mmap gather into pinned pieces / snpmi_bed_gather_packed and the C-ABI argument
 # checks (test_api_host, test_abi), the oracle C (test_oracle) -- with the matching runtime
 # preloaded into the (uninstrumented) Python.  One runtime per process: clang's for libsnpmi, gcc's
-# for the oracle.  Logs go to $1 (default profiles/r05_sanitize); exit status != 0 on any report.
+# for the oracle.  Logs go to $1 (default profiles/r06_sanitize); exit status != 0 on any report.
 set -o pipefail
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
-OUT=${1:-$ROOT/profiles/r05_sanitize}
+OUT=${1:-$ROOT/profiles/r06_sanitize}
 mkdir -p "$OUT"
 make -s -j8 -C "$ROOT/pysnptools_amd/csrc" asan tsan || exit 2
 make -s -C "$ROOT/oracle" asan || exit 2
 RT=$(ls -d /opt/rocm/lib/llvm/lib/clang/*/lib/linux | head -1)
 GCC_ASAN=$(gcc -print-file-name=libasan.so)
-SNPMI_TESTS="tests/test_meta.py tests/test_host_synth.py tests/test_api_host.py tests/test_abi.py"
+SNPMI_TESTS="tests/test_meta.py tests/test_host_synth.py tests/test_api_host.py tests/test_abi.py tests/test_watchdog_host.py"
 ORACLE_TESTS="tests/test_oracle.py"
 cd "$ROOT" || exit 2
 status=0
