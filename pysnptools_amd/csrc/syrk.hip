@@ -1962,8 +1962,12 @@ void launch_syrk_packed_bf3_split(const uint8_t* packed, uint64_t pitch, uint64_
     const unsigned S = (unsigned)ceil_div(m, kslice);
     SNPMI_REQUIRE(g < (1ull << 31) && S >= 1, SNPMI_E_ARG, "bad split");
     if (h2) {
-        f32w::k_syrk_h2<><<<dim3((unsigned)g, S), 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, partial, 0, 0, 1,
-                                                                 kslice, elems, seg_ctx(), packed_block_order(nb));
+        if (g_h2_kernel == 1)
+            f32w::k_syrk_h2s<><<<dim3((unsigned)g, S), 768, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, partial, 0, 0,
+                                                                    1, kslice, elems, seg_ctx(), packed_block_order(nb));
+        else
+            f32w::k_syrk_h2<><<<dim3((unsigned)g, S), 512, 0, st>>>(packed, pitch, n, m, h2->lut2, h2->flag, partial, 0, 0,
+                                                                   1, kslice, elems, seg_ctx(), packed_block_order(nb));
         SNPMI_HIP(hipGetLastError());
     }
     f32w::k_syrk_bf3<false, false, 5><<<dim3((unsigned)g, S), 512, 0, st>>>(packed, pitch, n, m, lut3, partial, 0, 0, 1,

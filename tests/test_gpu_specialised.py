@@ -42,8 +42,10 @@ def _both(fn):
     return outs
 
 
-@pytest.mark.parametrize("n,m", [(4100, 1015), (20000, 3000), (30000, 30000), (16384, 40)])
+@pytest.mark.parametrize("n,m", [(4100, 1015), (20000, 3000), (30000, 30000), (16384, 40), (8000, 30000)])
 def test_h2s_whole_launch_bit_identical(n, m):
+    """Whole launches, incl. the split-K grids of n <~ 16k (k_syrk_h2s with gridDim.y slices) and
+    several SegFlush rounds (30000 SNPs)."""
     packed, pitch, lut = _data(n, m, 7 + m)
     tb = N.lib().snpmi_grm_tile_bytes(n, N.DT_F32)
     tiles = bench.Dev(N, tb)
