@@ -871,6 +871,7 @@ def leg_grm(N, args, dist, dtype, keep_tiles=False):
     sum_r, nlaunch = ctypes.c_uint64(), ctypes.c_uint64()
     if dtype == "f64":
         N.call("snpmi_crt_moduli_stats", ctypes.byref(sum_r), ctypes.byref(nlaunch), 1)
+        N.call("snpmi_crt_block_moduli_stats", ctypes.byref(sum_r), ctypes.byref(nlaunch), 1)
     g = session()
     dist.barrier()
     t0 = time.perf_counter()
@@ -884,10 +885,12 @@ def leg_grm(N, args, dist, dtype, keep_tiles=False):
     N.call("snpmi_stream_sync")
     dist.barrier()
     wall = dist.max(time.perf_counter() - t0)
-    crt_moduli = None
-    if dtype == "f64":  # moduli the timed blocks ran with (chosen per block on the device)
+    crt_moduli = crt_block_moduli = None
+    if dtype == "f64":  # moduli the timed launches / blocks ran with (chosen on the device)
         N.call("snpmi_crt_moduli_stats", ctypes.byref(sum_r), ctypes.byref(nlaunch), 1)
         crt_moduli = sum_r.value / max(nlaunch.value, 1)
+        N.call("snpmi_crt_block_moduli_stats", ctypes.byref(sum_r), ctypes.byref(nlaunch), 1)
+        crt_block_moduli = sum_r.value / max(nlaunch.value, 1) if nlaunch.value else None
     syrk_ms = ev.ms(0, 1) if my_m else 0.0
     coll_ms = ev.ms(1, 2) if collective != "none" else 0.0
     tiles, count = g.tiles()
@@ -920,7 +923,8 @@ def leg_grm(N, args, dist, dtype, keep_tiles=False):
     res = dict(wall=wall, syrk_ms=syrk_ms, allreduce_ms=coll_ms, trace=trace, exec_ratio=exec_ratio,
                mean_tflops=(n * (n + 1) * my_m / (syrk_ms * 1e-3) / 1e12) if syrk_ms else 0.0,
                launches=chunks, snps_per_launch=(my_m + chunks - 1) // chunks if chunks else 0,
-               my_m=my_m, crt_moduli=crt_moduli, collective=collective, tiles=host_tiles, unoverlapped=unoverlapped)
+               my_m=my_m, crt_moduli=crt_moduli, crt_block_moduli=crt_block_moduli, collective=collective,
+               tiles=host_tiles, unoverlapped=unoverlapped)
     if dist.rank == 0 and not args.skip_cpu and my_m > 0:
         # parity sample (untimed): K rows 0..63 of the GRM of this rank's first 512 SNPs
         cm, rows = min(512, my_m), 64
@@ -1055,6 +1059,7 @@ def leg_grm5(N, args, dist):
     sum_r, nlaunch = ctypes.c_uint64(), ctypes.c_uint64()
     if dt == np.float64:
         N.call("snpmi_crt_moduli_stats", ctypes.byref(sum_r), ctypes.byref(nlaunch), 1)
+        N.call("snpmi_crt_block_moduli_stats", ctypes.byref(sum_r), ctypes.byref(nlaunch), 1)
     g = PartitionedGrm(n, m, N.STD_UNIT, dist=grp, part=rank, parts=P, block=args.grm5_block, out=out, timing=True,
                        dtype=dt)
     try:
@@ -1070,6 +1075,8 @@ def leg_grm5(N, args, dist):
         if dt == np.float64:  # moduli per launch the timed blocks ran with (chosen on the device)
             N.call("snpmi_crt_moduli_stats", ctypes.byref(sum_r), ctypes.byref(nlaunch), 1)
             res["crt_moduli"] = sum_r.value / max(nlaunch.value, 1)
+            N.call("snpmi_crt_block_moduli_stats", ctypes.byref(sum_r), ctypes.byref(nlaunch), 1)
+            res["crt_block_moduli"] = sum_r.value / nlaunch.value if nlaunch.value else None
         if rank == 0 and not args.skip_cpu and (world == 1 or m <= args.grm5_parity_max_sid):
             picks = grm5_picks(N, n, rank, P, g.nloc)
             got = {}
@@ -1236,7 +1243,7 @@ def grm_entry(args, dist, r, dtype):
                 "mfma_util_executed": r["mean_tflops"] * r["exec_ratio"] / MFMA_BF16_PEAK_TFLOPS}
     else:
         nb = (n + 255) // 256
-        R = r["crt_moduli"] or CRT_MODULI
+        R = r.get("crt_block_moduli") or r["crt_moduli"] or CRT_MODULI
         ops = R * 2 * 256 * 256 * (nb * (nb + 1) // 2) * r["my_m"]  # executed int8 ops over the rank's span
         achieved = ops / (r["syrk_ms"] * 1e-3) / 1e12 if r["syrk_ms"] else 0.0
         roof = {"bound": "mfma", "achieved": achieved, "peak": MFMA_I8_PEAK_TOPS, "unit": "TOP/s",
@@ -1244,7 +1251,7 @@ def grm_entry(args, dist, r, dtype):
                 "per_launch_ops": R * 2 * 256 * 256 * (nb * (nb + 1) // 2) * r["snps_per_launch"], "traffic": None,
                 "f64_equiv_tflops": r["mean_tflops"], "f64_mfma_peak": MFMA_F64_PEAK_TFLOPS,
                 "vs_f64_mfma_peak": r["mean_tflops"] / MFMA_F64_PEAK_TFLOPS,
-                "moduli_per_block": R, "moduli_max": CRT_MODULI,
+                "moduli_per_block": R, "moduli_launch_wide": r["crt_moduli"], "moduli_max": CRT_MODULI,
                 "kernel": "k_syrk_i8w (warp-specialised: 8 MFMA waves + 4 loader waves; v_mfma_i32_32x32x32_i8; "
                           "grid = 256-blocks of a tile chunk x 15 moduli, those "
                           "past the block's R exit at once) + k_crt (Garner over R digits) + k_crt_exp/k_crt_lut/"
@@ -1601,11 +1608,12 @@ def run_legs(N, args, dist):
         f64_5 = r3["dtype"] == np.float64
         if f64_5:  # the CRT path: executed int8 ops against the int8 peak, beside the f64-equivalent rate
             nloc5 = r3["n_local_blocks"]
-            R5 = r3.get("crt_moduli") or CRT_MODULI
+            R5 = r3.get("crt_block_moduli") or r3.get("crt_moduli") or CRT_MODULI
             ops5 = R5 * 2 * 256 * 256 * nloc5 * m5
             roof5 = {"bound": "mfma", "achieved": ops5 / busy_s / 1e12, "peak": MFMA_I8_PEAK_TOPS, "unit": "TOP/s",
                      "frac": ops5 / busy_s / 1e12 / MFMA_I8_PEAK_TOPS, "traffic": None,
                      "f64_equiv_tflops": syrk_tf, "f64_mfma_peak": MFMA_F64_PEAK_TFLOPS, "moduli_per_block": R5,
+                     "moduli_launch_wide": r3.get("crt_moduli"),
                      "kernel": "k_syrk_i8w in part mode (int8 residues of the quantised LUT, R moduli per block) + "
                                "k_crt into the part's f64 blocks; time = the blocks' compute-stream spans (stats + CRT "
                                "SYRK%s)" % (" + all-gather" if gather else "")}

@@ -386,6 +386,10 @@ int snpmi_dev_grm_trace(const void* K_tiles, uint64_t n_iid, int dtype, double* 
  * per SNP block on the device from the block's own bound max_i sum_s q_is^2:
  * sum of R and number of such blocks on this device since the last reset (synchronous). */
 int snpmi_crt_moduli_stats(uint64_t* sum_r, uint64_t* launches, int reset);
+/* per 256-block: each block (bi, bj) runs only the moduli with P_R > 2 sqrt(M_bi M_bj), M_p = the
+ * largest sum_s q_is^2 of its iid panel p (Cauchy-Schwarz per block; K is the same bits as with the
+ * launch-wide R): sum of R_b and number of blocks since the last reset (synchronous). */
+int snpmi_crt_block_moduli_stats(uint64_t* sum_rb, uint64_t* blocks, int reset);
 
 /* ---------------------------------------------------------------- RCCL (one process per GPU) */
 int snpmi_rccl_unique_id(uint8_t* id, uint64_t id_len);   /* id_len >= 128 */

@@ -131,6 +131,7 @@ _SIGS = {
     "snpmi_dev_grm_extract": [_vp, _u64, _i32, _vp, _u64, _vp, _u64, _i32, _f64, _vp],
     "snpmi_dev_grm_trace": [_vp, _u64, _i32, _dp],
     "snpmi_crt_moduli_stats": [_u64p, _u64p, _i32],
+    "snpmi_crt_block_moduli_stats": [_u64p, _u64p, _i32],
     "snpmi_rccl_unique_id": [_vp, _u64],
     "snpmi_rccl_init": [_i32, _i32, _vp, _u64],
     "snpmi_rccl_allreduce_sum": [_vp, _u64, _i32],

@@ -741,10 +741,12 @@ SegCtx seg_ctx() {
 }
 
 // per-device record of the CRT path's moduli counts: [0] = sum of R, [1] = launches
+// CRT moduli counters on the device: [0] sum of the launch-wide R, [1] launches (k_crt_r); [2] sum
+// of the per-block R_b, [3] blocks (k_crt)
 static unsigned long long* crt_record(Device& d) {
     const bool fresh = d.cap[Device::S_CRTREC] == 0;
-    auto* rec = (unsigned long long*)d.get(Device::S_CRTREC, 16);
-    if (fresh) SNPMI_HIP(hipMemsetAsync(rec, 0, 16, d.stream));
+    auto* rec = (unsigned long long*)d.get(Device::S_CRTREC, 32);
+    if (fresh) SNPMI_HIP(hipMemsetAsync(rec, 0, 32, d.stream));
     return rec;
 }
 
@@ -1688,6 +1690,10 @@ int snpmi_set_kernel_variant(const char* kernel, int variant) {
             SNPMI_REQUIRE(variant == 0 || variant == 1, SNPMI_E_ARG, "crt residue SYRK: 0 = k_syrk_i8r, 1 = k_syrk_i8w");
             g_crt_kernel = variant;
         }
+        else if (std::strcmp(kernel, "crt_block") == 0) {
+            SNPMI_REQUIRE(variant == 0 || variant == 1, SNPMI_E_ARG, "crt moduli: 0 = launch-wide R, 1 = per 256-block");
+            g_crt_block = variant;
+        }
         else if (std::strcmp(kernel, "f64") == 0) {
             SNPMI_REQUIRE(variant == 0 || variant == 1, SNPMI_E_ARG, "f64 GRM path: 0 = int8 residues + CRT, 1 = f64 MFMA");
             g_f64_mfma = variant;
@@ -1713,6 +1719,7 @@ int snpmi_get_kernel_variant(const char* kernel, int* variant) {
         else if (std::strcmp(kernel, "seg") == 0) *variant = g_seg_snps;
         else if (std::strcmp(kernel, "gather") == 0) *variant = g_gather;
         else if (std::strcmp(kernel, "crt") == 0) *variant = g_crt_kernel;
+        else if (std::strcmp(kernel, "crt_block") == 0) *variant = g_crt_block;
         else if (std::strcmp(kernel, "h2") == 0) *variant = g_h2_kernel;
         else if (std::strcmp(kernel, "f64") == 0) *variant = g_f64_mfma;
         else throw Error(SNPMI_E_ARG, std::string("unknown kernel ") + kernel);
@@ -2547,18 +2554,30 @@ int snpmi_dev_grm_extract(const void* K_tiles, uint64_t n_iid, int dtype, const 
     });
 }
 
+static void crt_stats(uint64_t* a, uint64_t* b, int reset, int which) {
+    Device& d = device();
+    unsigned long long h[2] = {0, 0};
+    unsigned long long* rec = crt_record(d) + 2 * which;
+    SNPMI_HIP(hipMemcpyAsync(h, rec, sizeof(h), hipMemcpyDeviceToHost, d.stream));
+    if (reset) SNPMI_HIP(hipMemsetAsync(rec, 0, sizeof(h), d.stream));
+    SNPMI_HIP(hipStreamSynchronize(d.stream));
+    *a = h[0];
+    *b = h[1];
+}
+
 int snpmi_crt_moduli_stats(uint64_t* sum_r, uint64_t* launches, int reset) {
     return guarded([&] {
         std::lock_guard<std::recursive_mutex> lk(g_call_mutex);
         SNPMI_REQUIRE(sum_r != nullptr && launches != nullptr, SNPMI_E_ARG, "NULL output");
-        Device& d = device();
-        unsigned long long h[2] = {0, 0};
-        unsigned long long* rec = crt_record(d);
-        SNPMI_HIP(hipMemcpyAsync(h, rec, sizeof(h), hipMemcpyDeviceToHost, d.stream));
-        if (reset) SNPMI_HIP(hipMemsetAsync(rec, 0, sizeof(h), d.stream));
-        SNPMI_HIP(hipStreamSynchronize(d.stream));
-        *sum_r = h[0];
-        *launches = h[1];
+        crt_stats(sum_r, launches, reset, 0);
+    });
+}
+
+int snpmi_crt_block_moduli_stats(uint64_t* sum_rb, uint64_t* blocks, int reset) {
+    return guarded([&] {
+        std::lock_guard<std::recursive_mutex> lk(g_call_mutex);
+        SNPMI_REQUIRE(sum_rb != nullptr && blocks != nullptr, SNPMI_E_ARG, "NULL output");
+        crt_stats(sum_rb, blocks, reset, 1);
     });
 }
 

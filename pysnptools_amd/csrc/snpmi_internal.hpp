@@ -279,6 +279,7 @@ void launch_tile_reduce(const float* partial, unsigned slices, uint64_t elems, f
 // NULL): rec[0] += R, rec[1] += 1 per launch
 int crt_moduli();
 extern int g_crt_kernel;  // residue SYRK form (hook "crt"): 0 = k_syrk_i8r, 1 = warp-specialised k_syrk_i8w
+extern int g_crt_block;   // hook "crt_block": 1 = moduli per 256-block (default), 0 = launch-wide R
 uint64_t crt_max_snps();
 uint64_t crt_lut_bytes(uint64_t m, uint64_t n);
 int crt_fraction_bits(uint64_t m);

@@ -146,6 +146,7 @@ __global__ __launch_bounds__(256) void k_crt_bound(const uint8_t* __restrict__ P
 // ctl[2] = R: the fewest moduli with P_R > 2 max_i S[i] (1 + 2^-20); plog[r] = log2 P_{r+1} (host)
 struct CrtLog {
     double plog[kR];
+    int per_block;  // 0: every block runs the launch-wide ctl[2] moduli (hook "crt_block" = 0)
 };
 __global__ __launch_bounds__(1024) void k_crt_r(const double* __restrict__ S, uint64_t n, CrtLog L,
                                                int* __restrict__ ctl, unsigned long long* __restrict__ rec) {
@@ -171,6 +172,35 @@ __global__ __launch_bounds__(1024) void k_crt_r(const double* __restrict__ S, ui
             atomicAdd(rec + 1, 1ull);
         }
     }
+}
+
+// Per 256-iid panel p: lgp[p] = log2(max_{i in p} S[i] (1 + 2^-20)) (-inf for an all-zero panel).
+// The block (bi, bj) then needs only the moduli with P_R > 2 sqrt(M_bi M_bj): |K_int,ij| <=
+// sqrt(S_i S_j) <= sqrt(M_bi M_bj) (Cauchy-Schwarz).  The launch-wide R (ctl[2]) is the largest of
+// these; blocks whose panels hold no extreme iid (the rare-variant carriers that set max_i S[i])
+// skip one modulus or more, and K_int is exact either way, so K is the same bits.
+__global__ __launch_bounds__(256) void k_crt_panels(const double* __restrict__ S, uint64_t n, const int* __restrict__ ctl,
+                                                    double* __restrict__ lgp) {
+    if (ctl[1]) return;
+    const uint64_t i = (uint64_t)blockIdx.x * BW + threadIdx.x;
+    __shared__ double red[256];
+    red[threadIdx.x] = i < n ? S[i] : 0.0;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w) red[threadIdx.x] = fmax(red[threadIdx.x], red[threadIdx.x + w]);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) lgp[blockIdx.x] = red[0] > 0.0 ? log2(red[0] * (1.0 + 0x1p-20)) : -__builtin_inf();
+}
+
+// moduli the 256-block (bi, bj) needs (1 <= R_b <= ctl[2]); the same formula as k_crt_r's
+__device__ __forceinline__ int block_moduli(const double* __restrict__ lgp, uint32_t bi, uint32_t bj, const CrtLog& L,
+                                            const int* __restrict__ ctl) {
+    if (!L.per_block) return ctl[2];
+    const double need = 0.5 * (lgp[bi] + lgp[bj]) + 1.0;
+    int R = 1;
+    while (R < kR && L.plog[R - 1] <= need) R++;
+    return R;
 }
 
 __device__ __forceinline__ v2i lds_tr8(const uint8_t* p) {
@@ -225,7 +255,7 @@ template <int SKT>
 __global__ __launch_bounds__(512, 1) void k_syrk_i8r(const uint8_t* __restrict__ P, uint64_t pitch, uint64_t kdim,
                                                      uint64_t mpad, const uint32_t* __restrict__ lutr,
                                                      const int* __restrict__ ctl, uint64_t b0, uint64_t nblk,
-                                                     uint8_t* __restrict__ res,
+                                                     uint8_t* __restrict__ res, const double* __restrict__ lgp, CrtLog L,
                                                      const uint32_t* __restrict__ part_tab = nullptr) {
     constexpr int KS = SKT / 32, RPT = SKT / 16, PNL = SKT * RS, STG = 2 * PNL;
     __shared__ __attribute__((aligned(16))) uint8_t lds[2 * STG];
@@ -233,7 +263,6 @@ __global__ __launch_bounds__(512, 1) void k_syrk_i8r(const uint8_t* __restrict__
     const uint32_t w = blockIdx.x, q = w >> 3, u = q / kR;
     const uint32_t r = q - u * kR, bx = 8 * u + (w & 7);
     if (bx >= nblk) return;
-    if ((int)r >= ctl[2]) return;  // K_int fits the first ctl[2] moduli
     const uint32_t* lr = lutr + (uint64_t)r * mpad;
     uint32_t bi, bj;
     if (part_tab) {  // cfg5: slot b0 + bx of the part's layout (syrk.hip part_layout)
@@ -243,6 +272,7 @@ __global__ __launch_bounds__(512, 1) void k_syrk_i8r(const uint8_t* __restrict__
     } else {
         tile_coords(b0 + bx, bi, bj);
     }
+    if ((int)r >= block_moduli(lgp, bi, bj, L, ctl)) return;  // this block's K_int fits the first R_b moduli
     const uint64_t i0 = (uint64_t)bi * BW, j0 = (uint64_t)bj * BW;
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
     const int wm = wave >> 2, wn = wave & 3;
@@ -343,7 +373,7 @@ template <int SKT>
 __global__ __launch_bounds__(768, 1) void k_syrk_i8w(const uint8_t* __restrict__ P, uint64_t pitch, uint64_t kdim,
                                                      uint64_t mpad, const uint32_t* __restrict__ lutr,
                                                      const int* __restrict__ ctl, uint64_t b0, uint64_t nblk,
-                                                     uint8_t* __restrict__ res,
+                                                     uint8_t* __restrict__ res, const double* __restrict__ lgp, CrtLog L,
                                                      const uint32_t* __restrict__ part_tab = nullptr) {
     constexpr int KS = SKT / 32, RPL = SKT / 8, PNL = SKT * RS, STG = 2 * PNL;
     __shared__ __attribute__((aligned(16))) uint8_t lds[2 * STG];
@@ -351,7 +381,6 @@ __global__ __launch_bounds__(768, 1) void k_syrk_i8w(const uint8_t* __restrict__
     const uint32_t w = blockIdx.x, q = w >> 3, u = q / kR;
     const uint32_t r = q - u * kR, bx = 8 * u + (w & 7);
     if (bx >= nblk) return;
-    if ((int)r >= ctl[2]) return;  // K_int fits the first ctl[2] moduli
     uint32_t bi, bj;
     if (part_tab) {
         const uint32_t c = part_tab[b0 + bx];
@@ -360,6 +389,7 @@ __global__ __launch_bounds__(768, 1) void k_syrk_i8w(const uint8_t* __restrict__
     } else {
         tile_coords(b0 + bx, bi, bj);
     }
+    if ((int)r >= block_moduli(lgp, bi, bj, L, ctl)) return;  // this block's K_int fits the first R_b moduli
     const int t = threadIdx.x, lane = t & 63;
     const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
     const uint64_t nst = (kdim + SKT - 1) / SKT;
@@ -508,14 +538,28 @@ __device__ __forceinline__ void digits(f2 (&v)[2][kR], const uint8_t* __restrict
 // tiles + (b0 + blk) * 65536, as the f32 part kernels write theirs
 __global__ __launch_bounds__(256) void k_crt(const uint8_t* __restrict__ res, uint64_t b0, uint64_t nblk, uint64_t n,
                                              const int* __restrict__ ctl, int F, CrtConst cc, double* __restrict__ tiles,
-                                             int accumulate, int part) {
+                                             int accumulate, const uint32_t* __restrict__ part_tab,
+                                             const double* __restrict__ lgp, CrtLog L,
+                                             unsigned long long* __restrict__ rec) {
     if (ctl[1]) return;
     const uint64_t blk = blockIdx.x >> 6;
     const int row = 4 * (blockIdx.x & 63) + (threadIdx.x >> 6), col = 4 * (threadIdx.x & 63);
+    const bool part = part_tab != nullptr;
+    uint32_t bi, bj;
+    if (part) {
+        const uint32_t c = part_tab[b0 + blk];
+        bi = c & 0xffffu;
+        bj = c >> 16;
+    } else {
+        tile_coords(b0 + blk, bi, bj);
+    }
+    const int R = block_moduli(lgp, bi, bj, L, ctl);  // the moduli k_syrk_i8* ran for this block
+    if (rec && (blockIdx.x & 63) == 0 && threadIdx.x == 0) {
+        atomicAdd(rec + 2, (unsigned long long)R);
+        atomicAdd(rec + 3, 1ull);
+    }
     uint64_t ti = 0, tj = 0;
     if (!part) {
-        uint32_t bi, bj;
-        tile_coords(b0 + blk, bi, bj);
         ti = 2 * (uint64_t)bi + (row >> 7);
         tj = 2 * (uint64_t)bj + (col >> 7);
         const uint64_t nt128 = (n + 127) / 128;
@@ -531,7 +575,7 @@ __global__ __launch_bounds__(256) void k_crt(const uint8_t* __restrict__ res, ui
             v[h][0] = (f2){(float)(r0 >= 128 ? r0 - 256 : r0), (float)(r1 >= 128 ? r1 - 256 : r1)};
         }
     }
-    digits<1>(v, res, plane, e_off, cc, ctl[2]);
+    digits<1>(v, res, plane, e_off, cc, R);
     const int sh = 2 * (ctl[0] - F);
     double2* T = reinterpret_cast<double2*>(
         part ? tiles + ((b0 + blk) * BW + row) * BW + col
@@ -586,14 +630,18 @@ int crt_fraction_bits(uint64_t m) {
 // hook "crt": 1 = k_syrk_i8w (loader waves, default: 684 vs 697 ms per 50k x 62.5k launch in one
 // process, profiles/r06g), 0 = k_syrk_i8r (loader in every wave)
 int g_crt_kernel = 1;
+// hook "crt_block": 1 = moduli per 256-block from its panels' bounds (default), 0 = launch-wide R
+int g_crt_block = 1;
 
 uint64_t crt_max_snps() { return 1ull << 16; }  // keeps F >= 50 and the int32 sums exact
 int crt_moduli() { return kR; }
 
-// ctl (256 B) | residue LUT (kR x mpad u32) | bound table (4 x mpad f64) | per-iid bound sums (n f64)
+// ctl (256 B) | residue LUT (kR x mpad u32) | bound table (4 x mpad f64) | per-iid bound sums (n f64) |
+// per-panel log2 bounds (ceil(n / 256) f64)
 uint64_t crt_lut_bytes(uint64_t m, uint64_t n) {
     const uint64_t mpad = round_up(std::max<uint64_t>(m, 1), SK);
-    return 256 + (uint64_t)kR * mpad * 4 + mpad * 32 + round_up(std::max<uint64_t>(n, 1), 2) * 8;
+    return 256 + (uint64_t)kR * mpad * 4 + mpad * 32 + round_up(std::max<uint64_t>(n, 1), 2) * 8 +
+           round_up(ceil_div(std::max<uint64_t>(n, 1), BW), 2) * 8;
 }
 
 static CrtLog crt_logs() {
@@ -639,14 +687,18 @@ void launch_syrk_packed_crt(const uint8_t* packed, uint64_t pitch, uint64_t n, u
     uint32_t* lutr = (uint32_t*)((uint8_t*)ws_lut + 256);
     double* qsq = (double*)(lutr + (uint64_t)kR * mpad);
     double* S = qsq + 4 * mpad;
+    double* lgp = S + round_up(std::max<uint64_t>(n, 1), 2);
     const int F = crt_fraction_bits(m);
     k_crt_exp<<<1, 1024, 0, st>>>(lut, 4 * m, ctl);
     k_crt_lut<<<(unsigned)ceil_div(mpad, 256), 256, 0, st>>>(lut, m, mpad, F, ctl, lutr, qsq);
     SNPMI_HIP(hipMemsetAsync(S, 0, n * sizeof(double), st));
     k_crt_bound<<<dim3((unsigned)ceil_div(ceil_div(n, 16), 256), (unsigned)ceil_div(m, kBoundSlice)), 256, 0, st>>>(
         packed, pitch, n, m, qsq, ctl, S);
-    static const CrtLog logs = crt_logs();
+    static const CrtLog logs0 = crt_logs();
+    CrtLog logs = logs0;
+    logs.per_block = g_crt_block;
     k_crt_r<<<1, 1024, 0, st>>>(S, n, logs, ctl, rec);
+    k_crt_panels<<<(unsigned)nb, 256, 0, st>>>(S, n, ctl, lgp);
     const uint64_t per = std::max<uint64_t>(1, res_bytes / ((uint64_t)kR * BW * BW));
     static const CrtConst cc = crt_constants();
     if (before_chunks) (*before_chunks)();
@@ -667,11 +719,12 @@ void launch_syrk_packed_crt(const uint8_t* packed, uint64_t pitch, uint64_t n, u
         // launch at 50k iids, the clock 2.21 -> 2.36 GHz, -3.6%: profiles/r05m)
         if (g_crt_kernel == 1)
             k_syrk_i8w<SK><<<(unsigned)(round_up(cnt, 8) * kR), 768, 0, st>>>(packed, pitch, m, mpad, lutr, ctl, b0,
-                                                                            cnt, res, part_tab);
+                                                                            cnt, res, lgp, logs, part_tab);
         else
             k_syrk_i8r<SK><<<(unsigned)(round_up(cnt, 8) * kR), 512, 0, st>>>(packed, pitch, m, mpad, lutr, ctl, b0,
-                                                                            cnt, res, part_tab);
-        k_crt<<<(unsigned)(cnt * 64), 256, 0, st>>>(res, b0, cnt, n, ctl, F, cc, tiles, accumulate, part_tab ? 1 : 0);
+                                                                            cnt, res, lgp, logs, part_tab);
+        k_crt<<<(unsigned)(cnt * 64), 256, 0, st>>>(res, b0, cnt, n, ctl, F, cc, tiles, accumulate, part_tab, lgp, logs,
+                                                    rec);
         if (after_chunk) {
             SNPMI_HIP(hipGetLastError());
             (*after_chunk)(cols[ci].first, cols[ci].second);

@@ -19,20 +19,36 @@ from pysnptools_amd.standardizer import Unit
 pytestmark = pytest.mark.gpu
 
 
-def _grm_f64(v):
+def _kernel_f64(v, per_block=1):
+    """K through the public reader, with the moduli counts it ran: (K, launch-wide R, launches,
+    mean per-block R_b, blocks)."""
     n, m = v.shape
+    s, c, sb, cb = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
     with tempfile.TemporaryDirectory() as tmp:
         b = Bed.write(os.path.join(tmp, "c.bed"), SnpData(iid=[["f", str(i)] for i in range(n)],
                                                            sid=["s%d" % j for j in range(m)], val=v), count_A1=False)
-        s, c = ctypes.c_uint64(), ctypes.c_uint64()
-        N.call("snpmi_crt_moduli_stats", ctypes.byref(s), ctypes.byref(c), 1)
-        K = b.read_kernel(Unit(), dtype=np.float64).val
-        N.call("snpmi_crt_moduli_stats", ctypes.byref(s), ctypes.byref(c), 1)
+        N.call("snpmi_set_kernel_variant", b"crt_block", per_block)
+        try:
+            N.call("snpmi_crt_moduli_stats", ctypes.byref(s), ctypes.byref(c), 1)
+            N.call("snpmi_crt_block_moduli_stats", ctypes.byref(sb), ctypes.byref(cb), 1)
+            K = b.read_kernel(Unit(), dtype=np.float64).val
+            N.call("snpmi_crt_moduli_stats", ctypes.byref(s), ctypes.byref(c), 1)
+            N.call("snpmi_crt_block_moduli_stats", ctypes.byref(sb), ctypes.byref(cb), 1)
+        finally:
+            N.call("snpmi_set_kernel_variant", b"crt_block", 1)
+    return K, s.value / max(c.value, 1), c.value, sb.value / max(cb.value, 1), cb.value
+
+
+def _grm_f64(v):
+    K, R, launches, Rb, blocks = _kernel_f64(v)
     Z = v.copy(order="F")
     O.standardize_native(Z)
     Kref = Z.dot(Z.T)
     err = np.abs(K - Kref).max() / np.abs(np.diag(Kref)).max()
-    return err, s.value / max(c.value, 1), c.value
+    nb = (v.shape[0] + 255) // 256
+    assert blocks == launches * nb * (nb + 1) // 2, (blocks, launches, nb)
+    assert 1.0 <= Rb <= R, (Rb, R)
+    return err, R, launches
 
 
 def test_crt_worst_case_bound_uses_every_modulus():
@@ -44,6 +60,22 @@ def test_crt_worst_case_bound_uses_every_modulus():
     err, R, launches = _grm_f64(v)
     assert launches >= 1 and R == 15, R
     assert err <= 1e-12, err
+
+
+def test_crt_per_block_moduli_same_bits_as_launch_wide():
+    """The worst-case data again: the panel of iid 0 needs all 15 moduli, the blocks away from it
+    fewer (sqrt(M_bi M_bj) < M_0), and K is the same bits as with the launch-wide R (hook
+    "crt_block" = 0): the symmetric mixed-radix digits above R_b are zero either way."""
+    rng = np.random.default_rng(11)
+    n, m = 1000, 3000
+    v = rng.binomial(2, rng.uniform(0.05, 0.5, m), size=(n, m)).astype(np.float64)
+    v[:, : m // 2] = 0.0
+    v[0, : m // 2] = 2.0
+    K1, R1, _, Rb1, _ = _kernel_f64(v, 1)
+    K0, R0, _, Rb0, _ = _kernel_f64(v, 0)
+    assert R1 == R0 == 15 and Rb0 == 15, (R1, R0, Rb0)
+    assert Rb1 < 15, Rb1
+    assert np.array_equal(K0, K1)
 
 
 def test_crt_rare_variant_blocks_use_fewer_moduli():
@@ -152,6 +184,18 @@ def test_warp_specialised_residue_syrk_is_bit_identical(n, m, parts):
     """k_syrk_i8w (hook "crt" = 1: loader waves beside the MFMA waves) produces the same residues as
     k_syrk_i8r, hence the same f64 K bit for bit -- replicated tiles (one and several residue
     chunks, stage counts 2..24, n not a multiple of 256) and a cfg5 part (part_tab layout)."""
+    _forms_bit_identical(b"crt", n, m, parts)
+
+
+@pytest.mark.parametrize("n,m,parts", [(4100, 3000, 0), (30000, 300, 0), (2300, 700, 3)])
+def test_per_block_moduli_bit_identical_on_device(n, m, parts):
+    """hook "crt_block": moduli per 256-block vs the launch-wide R, through the device entry points
+    (replicated tiles, residue chunks, a cfg5 part)."""
+    _forms_bit_identical(b"crt_block", n, m, parts)
+
+
+def _forms_bit_identical(hook, n, m, parts):
+    """Forms 0 and 1 of `hook` give the same f64 tiles bit for bit."""
     from test_gpu_parity import Dev, synth_dev
 
     buf, pitch = synth_dev(n, m, 31 + n)
@@ -159,7 +203,7 @@ def test_warp_specialised_residue_syrk_is_bit_identical(n, m, parts):
     N.call("snpmi_dev_snp_stats", buf.p, pitch, n, m, 0, N.STD_UNIT, 0.0, 0.0, 0, N.DT_F64, st.p, lut.p)
     outs = []
     for form in (0, 1):
-        N.call("snpmi_set_kernel_variant", b"crt", form)
+        N.call("snpmi_set_kernel_variant", hook, form)
         try:
             if parts:
                 nloc = N.lib().snpmi_grm_part_blocks(n, 1, parts)
@@ -172,5 +216,5 @@ def test_warp_specialised_residue_syrk_is_bit_identical(n, m, parts):
                 N.call("snpmi_dev_syrk_packed", buf.p, pitch, n, m, lut.p, N.DT_F64, k.p, 0)
                 outs.append(k.get(np.empty(tb // 8, dtype=np.float64)))
         finally:
-            N.call("snpmi_set_kernel_variant", b"crt", 1)
+            N.call("snpmi_set_kernel_variant", hook, 1)
     assert outs[0].size and all(np.array_equal(outs[0], o) for o in outs[1:])

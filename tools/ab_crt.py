@@ -30,8 +30,10 @@ def main():
     p.add_argument("--part", default=None, help="P/W: the cfg5 part kernel, part P of W (e.g. 0/8), into its blocks")
     p.add_argument("--dtype", choices=["f32", "f64"], default="f64",
                    help="f64: the residue SYRK forms (hook crt); f32: the fp16x2 SYRK forms (hook h2)")
+    p.add_argument("--hook", default=None,
+                   help="override the A/B hook, e.g. crt_block (f64: 0 = launch-wide R, 1 = moduli per 256-block)")
     a = p.parse_args()
-    hook = b"crt" if a.dtype == "f64" else b"h2"
+    hook = a.hook.encode() if a.hook else (b"crt" if a.dtype == "f64" else b"h2")
     dt, esz = (N.DT_F64, 8) if a.dtype == "f64" else (N.DT_F32, 4)
     n, m = a.n, a.m
     pitch = N.lib().snpmi_packed_pitch(n)
@@ -48,10 +50,12 @@ def main():
     res = {f: [] for f in forms}
     sums = {}
     sum_r, nl = ctypes.c_uint64(), ctypes.c_uint64()
+    blk_r = {}
     for rnd in range(a.rounds + 1):  # round 0: warm-up (scratch allocations, code objects)
         for f in forms:
             N.call("snpmi_set_kernel_variant", hook, f)
             N.call("snpmi_crt_moduli_stats", ctypes.byref(sum_r), ctypes.byref(nl), 1)
+            N.call("snpmi_crt_block_moduli_stats", ctypes.byref(sum_r), ctypes.byref(nl), 1)
             ev.record(0)
             if part:
                 N.call("snpmi_dev_syrk_packed_part" + ("_f64" if esz == 8 else ""), packed.p, pitch, n, m, lut.p,
@@ -69,19 +73,25 @@ def main():
                 N.call("snpmi_memcpy_d2h", N.ptr(h[:k]), tiles.p, k * esz)
                 N.call("snpmi_memcpy_d2h", N.ptr(h[k:]), ctypes.c_void_p(tiles.p.value + tb - k * esz), k * esz)
                 sums[f] = h
+                N.call("snpmi_crt_block_moduli_stats", ctypes.byref(sum_r), ctypes.byref(nl), 0)
+                blk_r[f] = sum_r.value / nl.value if nl.value else None
                 N.call("snpmi_crt_moduli_stats", ctypes.byref(sum_r), ctypes.byref(nl), 0)
             print(json.dumps({"round": rnd, "form": f, "ms": ev.ms(0, 1)}), file=sys.stderr, flush=True)
     N.call("snpmi_set_kernel_variant", hook, 1)
-    # executed MFMA work: f64 = R int8 SYRKs (5.0 POP/s dense); f32 = 3 fp16 products (2.5 PF/s dense)
-    R, peak = (sum_r.value / max(nl.value, 1), 5000.0) if a.dtype == "f64" else (3.0, 2500.0)
+    # executed MFMA work: f64 = R int8 SYRKs per block (5.0 POP/s dense); f32 = 3 fp16 products (2.5 PF/s)
+    R_launch, peak = (sum_r.value / max(nl.value, 1), 5000.0) if a.dtype == "f64" else (3.0, 2500.0)
     nb = (n + 255) // 256
-    ops = R * 2 * 256 * 256 * (nloc if part else nb * (nb + 1) // 2) * m
     base = sums[forms[0]]
     for f in forms:
         t = float(np.median(res[f]))
-        names = {b"crt": {0: "k_syrk_i8r", 1: "k_syrk_i8w"}, b"h2": {0: "k_syrk_h2<.,4>", 1: "k_syrk_h2s"}}[hook]
-        print(json.dumps({"form": f, "kernel": names.get(f, "ablation %d" % f), "dtype": a.dtype, "n": n, "m": m,
-                          "median_ms": t, "all_ms": res[f], "moduli": R if a.dtype == "f64" else None,
+        R = (blk_r.get(f) or R_launch) if a.dtype == "f64" else R_launch
+        ops = R * 2 * 256 * 256 * (nloc if part else nb * (nb + 1) // 2) * m
+        names = {b"crt": {0: "k_syrk_i8r", 1: "k_syrk_i8w"}, b"h2": {0: "k_syrk_h2<.,4>", 1: "k_syrk_h2s"},
+                 b"crt_block": {0: "launch-wide R", 1: "R per 256-block"}}.get(hook, {})
+        print(json.dumps({"form": f, "hook": hook.decode(), "kernel": names.get(f, "ablation %d" % f), "dtype": a.dtype,
+                          "n": n, "m": m, "median_ms": t, "all_ms": res[f],
+                          "moduli": R if a.dtype == "f64" else None,
+                          "moduli_launch_wide": R_launch if a.dtype == "f64" else None,
                           "frac_mfma_peak_executed": ops / t / 1e9 / peak, "syrk_tflops": n * (n + 1) * m / t / 1e9 / (part[1] if part else 1), "part": a.part,
                           "tiles_equal_form0": bool(np.array_equal(sums[f], base))}), flush=True)
 
