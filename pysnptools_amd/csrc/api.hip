@@ -1687,7 +1687,9 @@ int snpmi_set_kernel_variant(const char* kernel, int variant) {
             g_h2_kernel = variant;
         }
         else if (std::strcmp(kernel, "crt") == 0) {
-            SNPMI_REQUIRE(variant == 0 || variant == 1, SNPMI_E_ARG, "crt residue SYRK: 0 = k_syrk_i8r, 1 = k_syrk_i8w");
+            SNPMI_REQUIRE(variant >= 0 && variant <= 2, SNPMI_E_ARG,
+                          "crt residue SYRK: 0 = k_syrk_i8r, 1 = k_syrk_i8w, 2 = k_syrk_i8w without its read "
+                          "order / wave priorities");
             g_crt_kernel = variant;
         }
         else if (std::strcmp(kernel, "crt_block") == 0) {

@@ -369,7 +369,17 @@ __global__ __launch_bounds__(512, 1) void k_syrk_i8r(const uint8_t* __restrict__
 // (vmcnt) or spend their issue slots on the expansion VALU, which put 14% of their cycles in
 // SQ_WAIT_INST_LDS and 23% in SQ_WAIT_ANY (profiles/r05z/pmc_sq_crt.json).  The register budget of
 // 3 waves per SIMD (<= 168 VGPRs) leaves the MFMA waves single-buffered fragments for the A panel.
-template <int SKT>
+// Two schedule settings on top (hook "crt" = 2 turns both off; same residues either way, int32
+// sums being exact in any order), measured in one process at 50k x 62.5k (profiles/r06s):
+// ROTA -- the A fragments of k-step ks+1 are read one 32-row tile at a time right after that
+//   tile's two MFMAs of k-step ks (sched_group_barrier keeps the order; the compiler otherwise
+//   issues all 12 reads after the 7th MFMA), -1% (r06o);
+// MPRIO -- static issue priority for the MFMA waves over the loader waves, the younger MFMA half
+//   (waves 4-7) one level above the older (MI355X_MICROARCH "two waves per SIMD" item 4): -2%
+//   more; the loader waves at the higher priority instead +6%, pacing their stores with s_sleep
+//   +7..35%, capping their LDS stores in flight -0.3% (r06o, r06q, r06r).
+// Together 666.7 vs 687.7 ms per launch (-3.0%), -1.7% at 4100 iids, -2.6% on a cfg5 part.
+template <int SKT, bool ROTA = true, int MPRIO = 2>
 __global__ __launch_bounds__(768, 1) void k_syrk_i8w(const uint8_t* __restrict__ P, uint64_t pitch, uint64_t kdim,
                                                      uint64_t mpad, const uint32_t* __restrict__ lutr,
                                                      const int* __restrict__ ctl, uint64_t b0, uint64_t nblk,
@@ -437,6 +447,12 @@ __global__ __launch_bounds__(768, 1) void k_syrk_i8w(const uint8_t* __restrict__
         }
         return;
     }
+    if constexpr (MPRIO > 1) {  // the younger MFMA half one level above the older (guide item 4)
+        if (wave >= 4) __builtin_amdgcn_s_setprio(MPRIO);
+        else __builtin_amdgcn_s_setprio(MPRIO - 1);
+    } else if constexpr (MPRIO > 0) {
+        __builtin_amdgcn_s_setprio(MPRIO);
+    }
     const int wm = wave >> 2, wn = wave & 3;
     const int g = lane >> 4, jj = (lane & 15) >> 1, pp = lane & 1;
     const int rd = (16 * (g >> 1) + jj) * RS + 16 * (g & 1) + 8 * pp;
@@ -456,6 +472,38 @@ __global__ __launch_bounds__(768, 1) void k_syrk_i8w(const uint8_t* __restrict__
         v4i b[2][2];
 #pragma unroll
         for (int y = 0; y < 2; y++) b[0][y] = frag(cur, 1, 0, wn * 64 + 32 * y);
+        if constexpr (ROTA) {
+            v4i a[4];
+#pragma unroll
+            for (int x = 0; x < 4; x++) a[x] = frag(cur, 0, 0, wm * 128 + 32 * x);
+#pragma unroll
+            for (int ks = 0; ks < KS; ks++) {
+                if (ks + 1 < KS) {
+#pragma unroll
+                    for (int y = 0; y < 2; y++) b[(ks + 1) & 1][y] = frag(cur, 1, ks + 1, wn * 64 + 32 * y);
+                }
+#pragma unroll
+                for (int x = 0; x < 4; x++) {
+#pragma unroll
+                    for (int y = 0; y < 2; y++)
+                        acc[x][y] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[x], b[ks & 1][y], acc[x][y], 0, 0, 0);
+                    if (ks + 1 < KS) a[x] = frag(cur, 0, ks + 1, wm * 128 + 32 * x);
+                }
+                // keep that order: the compiler otherwise issues all 12 reads after the 7th MFMA
+                if (ks + 1 < KS) {
+                    __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);  // B of ks+1
+#pragma unroll
+                    for (int x = 0; x < 4; x++) {
+                        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+                        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);  // A tile x of ks+1
+                    }
+                } else {
+                    __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
+                }
+            }
+            __syncthreads();
+            continue;
+        }
 #pragma unroll
         for (int ks = 0; ks < KS; ks++) {
             v4i a[4];
@@ -628,7 +676,8 @@ int crt_fraction_bits(uint64_t m) {
 }
 
 // hook "crt": 1 = k_syrk_i8w (loader waves, default: 684 vs 697 ms per 50k x 62.5k launch in one
-// process, profiles/r06g), 0 = k_syrk_i8r (loader in every wave)
+// process, profiles/r06g; 666.7 with its read order + wave priorities, r06s), 2 = k_syrk_i8w
+// without those two, 0 = k_syrk_i8r (loader in every wave)
 int g_crt_kernel = 1;
 // hook "crt_block": 1 = moduli per 256-block from its panels' bounds (default), 0 = launch-wide R
 int g_crt_block = 1;
@@ -720,6 +769,9 @@ void launch_syrk_packed_crt(const uint8_t* packed, uint64_t pitch, uint64_t n, u
         if (g_crt_kernel == 1)
             k_syrk_i8w<SK><<<(unsigned)(round_up(cnt, 8) * kR), 768, 0, st>>>(packed, pitch, m, mpad, lutr, ctl, b0,
                                                                             cnt, res, lgp, logs, part_tab);
+        else if (g_crt_kernel == 2)
+            k_syrk_i8w<SK, false, 0><<<(unsigned)(round_up(cnt, 8) * kR), 768, 0, st>>>(packed, pitch, m, mpad, lutr, ctl,
+                                                                                      b0, cnt, res, lgp, logs, part_tab);
         else
             k_syrk_i8r<SK><<<(unsigned)(round_up(cnt, 8) * kR), 512, 0, st>>>(packed, pitch, m, mpad, lutr, ctl, b0,
                                                                             cnt, res, lgp, logs, part_tab);

@@ -181,10 +181,10 @@ def test_public_f64_switch_selects_the_f64_mfma():
 @pytest.mark.parametrize("n,m,parts", [(300, 1015, 0), (1000, 129, 0), (4100, 3000, 0), (30000, 300, 0),
                                        (2300, 700, 3)])
 def test_warp_specialised_residue_syrk_is_bit_identical(n, m, parts):
-    """k_syrk_i8w (hook "crt" = 1: loader waves beside the MFMA waves) produces the same residues as
-    k_syrk_i8r, hence the same f64 K bit for bit -- replicated tiles (one and several residue
+    """k_syrk_i8w (hook "crt" = 1: loader waves beside the MFMA waves; 2: without its read order and
+    wave priorities) produces the same residues as k_syrk_i8r, hence the same f64 K bit for bit -- replicated tiles (one and several residue
     chunks, stage counts 2..24, n not a multiple of 256) and a cfg5 part (part_tab layout)."""
-    _forms_bit_identical(b"crt", n, m, parts)
+    _forms_bit_identical(b"crt", n, m, parts, forms=(0, 1, 2))
 
 
 @pytest.mark.parametrize("n,m,parts", [(4100, 3000, 0), (30000, 300, 0), (2300, 700, 3)])
@@ -194,15 +194,15 @@ def test_per_block_moduli_bit_identical_on_device(n, m, parts):
     _forms_bit_identical(b"crt_block", n, m, parts)
 
 
-def _forms_bit_identical(hook, n, m, parts):
-    """Forms 0 and 1 of `hook` give the same f64 tiles bit for bit."""
+def _forms_bit_identical(hook, n, m, parts, forms=(0, 1)):
+    """The forms of `hook` give the same f64 tiles bit for bit."""
     from test_gpu_parity import Dev, synth_dev
 
     buf, pitch = synth_dev(n, m, 31 + n)
     lut, st = Dev(m * 32), Dev(m * 16)
     N.call("snpmi_dev_snp_stats", buf.p, pitch, n, m, 0, N.STD_UNIT, 0.0, 0.0, 0, N.DT_F64, st.p, lut.p)
     outs = []
-    for form in (0, 1):
+    for form in forms:
         N.call("snpmi_set_kernel_variant", hook, form)
         try:
             if parts:
