@@ -1687,9 +1687,9 @@ int snpmi_set_kernel_variant(const char* kernel, int variant) {
             g_h2_kernel = variant;
         }
         else if (std::strcmp(kernel, "crt") == 0) {
-            SNPMI_REQUIRE(variant >= 0 && variant <= 5, SNPMI_E_ARG,
+            SNPMI_REQUIRE(variant >= 0 && variant <= 2, SNPMI_E_ARG,
                           "crt residue SYRK: 0 = k_syrk_i8r, 1 = k_syrk_i8w, 2 = k_syrk_i8w without its read "
-                          "order / wave priorities, 3 = k_syrk_i8w line layout, 4 = k_syrk_i8p, 5 = k_syrk_i8f");
+                          "order / wave priorities");
             g_crt_kernel = variant;
         }
         else if (std::strcmp(kernel, "crt_block") == 0) {

@@ -39,7 +39,6 @@ __constant__ int kMod[kR] = {256, 255, 253, 251, 247, 241, 239, 233, 229, 227, 2
 constexpr int BW = 256;    // block edge (iids)
 constexpr int SK = 128;    // SNPs per LDS stage (four 32-deep MFMA k-steps): 147 KiB of LDS, double-buffered
 constexpr int RS = 288;    // LDS bytes per SNP row (256 iids + 32: the 8 rows of a transposed read hit distinct banks)
-constexpr int LS = 264;    // k_syrk_i8w line layout: bytes per 256-B store line (consecutive rows 4 LS = 32 mod 256 apart)
 
 typedef int v2i __attribute__((ext_vector_type(2)));
 typedef int v4i __attribute__((ext_vector_type(4)));
@@ -210,32 +209,11 @@ __device__ __forceinline__ v2i lds_tr8(const uint8_t* p) {
 
 // acc mod p -> [0, p), one byte per element at its true (row, col) in the 256 x 256 block (a wave's
 // 128 x 64 = 4 x 2 tiles of v_mfma_i32_32x32x32_i8 accumulators, wave (wm, wn) of a 2 x 4 layout)
-// LINES: the line layout of k_syrk_i8w<.., true>, LDS position p <-> iid 16 ((p >> 2) & 15) + 4 (p & 3) + (p >> 6)
-template <bool LINES = false>
 __device__ __forceinline__ void crt_epilogue(const v16i (&acc)[4][2], uint32_t r, uint64_t nblk, uint64_t bx, int wm,
                                              int wn, int lane, uint8_t* __restrict__ res) {
     const int p = kMod[r];
     const double invp = 1.0 / (double)p;
     uint8_t* O = res + ((uint64_t)r * nblk + bx) * (BW * BW);
-    if constexpr (LINES) {
-        auto sig = [](int q) { return 16 * ((q >> 2) & 15) + 4 * (q & 3) + (q >> 6); };
-        const int hh = lane >> 5;
-#pragma unroll
-        for (int x = 0; x < 4; x++)
-#pragma unroll
-            for (int y = 0; y < 2; y++) {
-                uint8_t* cp = O + sig(wn * 64 + 32 * y + (lane & 31));
-#pragma unroll
-                for (int q = 0; q < 16; q++) {
-                    const int v = acc[x][y][q];
-                    int rr = v - p * (int)floor((double)v * invp);
-                    rr += rr < 0 ? p : 0;
-                    rr -= rr >= p ? p : 0;
-                    cp[sig(wm * 128 + 32 * x + 8 * (q >> 2) + 4 * hh + (q & 3)) * BW] = (uint8_t)rr;
-                }
-            }
-        return;
-    }
     const int hh = lane >> 5, colp = 16 * ((lane >> 4) & 1) + pi16(lane & 15);
 #pragma unroll
     for (int x = 0; x < 4; x++)
@@ -401,14 +379,19 @@ __global__ __launch_bounds__(512, 1) void k_syrk_i8r(const uint8_t* __restrict__
 //   more; the loader waves at the higher priority instead +6%, pacing their stores with s_sleep
 //   +7..35%, capping their LDS stores in flight -0.3% (r06o, r06q, r06r).
 // Together 666.7 vs 687.7 ms per launch (-3.0%), -1.7% at 4100 iids, -2.6% on a cfg5 part.
-template <int SKT, bool ROTA = true, int MPRIO = 2, bool LINES = false>
+// Lost against this kernel, all bit-identical (profiles/r06x): the residue image in 256-B lines
+// stored by ds_write_addtid_b32 (2 transfer cycles per 256 B instead of 13 per KiB) -0.5%; a ring of
+// three 64-SNP buffers whose next-stage fragments are read before the barrier +15%, and with LDS
+// full/empty counters instead of barriers +29% (64-SNP stages double the per-stage costs).  Loader
+// ablations: without the expansion VALU -7.8%, with one store in four -8%: the loader's VALU and
+// its stores each take ~8% from the MFMA waves.
+template <int SKT, bool ROTA = true, int MPRIO = 2>
 __global__ __launch_bounds__(768, 1) void k_syrk_i8w(const uint8_t* __restrict__ P, uint64_t pitch, uint64_t kdim,
                                                      uint64_t mpad, const uint32_t* __restrict__ lutr,
                                                      const int* __restrict__ ctl, uint64_t b0, uint64_t nblk,
                                                      uint8_t* __restrict__ res, const double* __restrict__ lgp, CrtLog L,
                                                      const uint32_t* __restrict__ part_tab = nullptr) {
-    constexpr int KS = SKT / 32, RPL = SKT / 8, PNL = SKT * (LINES ? LS : RS), STG = 2 * PNL;
-    static_assert(!LINES || SKT == 128, "the line layout assumes 128-SNP stages");
+    constexpr int KS = SKT / 32, RPL = SKT / 8, PNL = SKT * RS, STG = 2 * PNL;
     __shared__ __attribute__((aligned(16))) uint8_t lds[2 * STG];
     if (ctl[1]) return;  // non-finite LUT: the f64 MFMA kernel runs instead
     const uint32_t w = blockIdx.x, q = w >> 3, u = q / kR;
@@ -426,63 +409,6 @@ __global__ __launch_bounds__(768, 1) void k_syrk_i8w(const uint8_t* __restrict__
     const int t = threadIdx.x, lane = t & 63;
     const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
     const uint64_t nst = (kdim + SKT - 1) / SKT;
-    if (LINES && wave >= 8) {
-        // line layout: loader thread lt = (panel lp, wave half wq, row quad rr, 16-iid group d) loads
-        // the code dwords of rows 64 wq + 16 rr + h (h < 16) as the b128 loader does, and stores
-        // residue dword j of row h (iids 16 d + 4 b + j, b < 4) with ds_write_addtid_b32 at
-        // line (wq, h, j) + 64 rr + 4 d: lane = 16 rr + d, so one instruction = 256 contiguous bytes
-        // (2 transfer cycles against 13 per KiB of ds_write_b128)
-        const int lt = t - 512;
-        const int lp = __builtin_amdgcn_readfirstlane(lt >> 7), wq = __builtin_amdgcn_readfirstlane((lt >> 6) & 1);
-        const int kq = (lt >> 4) & 7, d = lt & 15;
-        const uint8_t* pbase = P + (uint64_t)(lp ? bj : bi) * (BW / 4);
-        const uint32_t pit = (uint32_t)pitch;
-        const uint32_t* lq = lutr + (uint64_t)r * mpad + RPL * kq;
-        uint32_t cw[RPL];
-        uint4 cl[RPL / 4];
-        auto load = [&](uint64_t st) {
-            const uint8_t* sb = pbase + st * SKT * pitch;
-            const uint32_t lim = (uint32_t)(kdim - 1 - st * SKT);
-#pragma unroll
-            for (int h = 0; h < RPL; h++) {
-                const uint32_t row = min((uint32_t)(RPL * kq + h), lim);
-                cw[h] = *reinterpret_cast<const uint32_t*>(sb + (row * pit + 4 * d));
-            }
-#pragma unroll
-            for (int v = 0; v < RPL / 4; v++) cl[v] = *reinterpret_cast<const uint4*>(lq + SKT * st + 4 * v);
-        };
-        auto store = [&](uint8_t* S) {
-            const uint32_t base = (uint32_t)(uintptr_t)(S + lp * PNL + wq * 64 * LS);
-#pragma unroll
-            for (int h = 0; h < RPL; h++) {
-                const uint4 c4 = cl[h >> 2];
-                const uint32_t Lw = (h & 3) == 0 ? c4.x : (h & 3) == 1 ? c4.y : (h & 3) == 2 ? c4.z : c4.w;
-                const uint32_t o0 = __builtin_amdgcn_perm(Lw, Lw, cw[h] & 0x03030303u);
-                const uint32_t o1 = __builtin_amdgcn_perm(Lw, Lw, (cw[h] >> 2) & 0x03030303u);
-                const uint32_t o2 = __builtin_amdgcn_perm(Lw, Lw, (cw[h] >> 4) & 0x03030303u);
-                const uint32_t o3 = __builtin_amdgcn_perm(Lw, Lw, (cw[h] >> 6) & 0x03030303u);
-#pragma clang diagnostic push
-#pragma clang diagnostic ignored "-Winline-asm"  // m0 is reserved; nothing else in the loader uses it
-                asm volatile(
-                    "s_mov_b32 m0, %0\n\ts_nop 0\n\t"
-                    "ds_write_addtid_b32 %1\n\tds_write_addtid_b32 %2 offset:264\n\t"
-                    "ds_write_addtid_b32 %3 offset:528\n\tds_write_addtid_b32 %4 offset:792" ::"s"(base + 4 * LS * h),
-                    "v"(o0), "v"(o1), "v"(o2), "v"(o3)
-                    : "memory", "m0");
-#pragma clang diagnostic pop
-            }
-        };
-        load(0);
-        store(lds);
-        load(nst > 1 ? 1 : 0);
-        __syncthreads();
-        for (uint64_t s = 0; s < nst; s++) {
-            store(lds + ((s + 1) & 1) * STG);
-            load(s + 2 < nst ? s + 2 : nst - 1);
-            __syncthreads();
-        }
-        return;
-    }
     if (wave >= 8) {
         // loader: thread lt = (panel lp, row block kq of RPL rows, 16-iid group d)
         const int lt = t - 512;
@@ -535,25 +461,16 @@ __global__ __launch_bounds__(768, 1) void k_syrk_i8w(const uint8_t* __restrict__
     }
     const int wm = wave >> 2, wn = wave & 3;
     const int g = lane >> 4, jj = (lane & 15) >> 1, pp = lane & 1;
-    const int rd = LINES ? jj * 4 * LS + 64 * (g >> 1) + 16 * (g & 1) + 8 * pp
-                         : (16 * (g >> 1) + jj) * RS + 16 * (g & 1) + 8 * pp;
+    const int rd = (16 * (g >> 1) + jj) * RS + 16 * (g & 1) + 8 * pp;
     v16i acc[4][2];
 #pragma unroll
     for (int x = 0; x < 4; x++)
 #pragma unroll
         for (int y = 0; y < 2; y++) acc[x][y] = (v16i){};
-    // col: the tile's first LDS position (wm 128 + 32 x for A, wn 64 + 32 y for B); in the line
-    // layout position p sits in segment j = p / 64 of its row's lines, at byte p % 64
     auto frag = [&](const uint8_t* S, int panel, int ks, int col) -> v4i {
-        if constexpr (LINES) {
-            const uint8_t* b = S + panel * PNL + ((ks >> 1) * 64 + (col >> 6)) * LS + 128 * (ks & 1) + rd + (col & 63);
-            const v2i x = lds_tr8(b), y = lds_tr8(b + 32 * LS);
-            return (v4i){x.x, x.y, y.x, y.y};
-        } else {
-            const uint8_t* b = S + panel * PNL + 32 * ks * RS + rd + col;
-            const v2i x = lds_tr8(b), y = lds_tr8(b + 8 * RS);
-            return (v4i){x.x, x.y, y.x, y.y};
-        }
+        const uint8_t* b = S + panel * PNL + 32 * ks * RS + rd + col;
+        const v2i x = lds_tr8(b), y = lds_tr8(b + 8 * RS);
+        return (v4i){x.x, x.y, y.x, y.y};
     };
     __syncthreads();
     for (uint64_t s = 0; s < nst; s++) {
@@ -610,367 +527,7 @@ __global__ __launch_bounds__(768, 1) void k_syrk_i8w(const uint8_t* __restrict__
         }
         __syncthreads();
     }
-    if constexpr (LINES) crt_epilogue<true>(acc, r, nblk, bx, wm, wn, lane, res);
-    else crt_epilogue(acc, r, nblk, bx, wm, wn, lane, res);
-}
-
-// Three-buffer form of k_syrk_i8w (round 6): 64-SNP stages (two k-steps) in a ring of three LDS
-// buffers in the line layout, so the MFMA waves read the NEXT stage's first fragments during the
-// current stage's last k-step (that buffer was completed one barrier earlier; the loader writes the
-// stage after it meanwhile) and start each stage with their operands in registers.  The barrier
-// then orders only the loader's stores: the loader waits for its own stores (lgkmcnt(0)) before
-// it, the MFMA waves do not wait for their in-flight reads of the next buffer.  The LDS ring:
-// stage s in buffer s % 3; during stage s the MFMA waves read s % 3 and (s+1) % 3, the loader
-// writes (s+2) % 3.  3 x 2 panels x 64 rows x LS = 99 KiB.
-template <int MPRIO = 2>
-__global__ __launch_bounds__(768, 1) void k_syrk_i8p(const uint8_t* __restrict__ P, uint64_t pitch, uint64_t kdim,
-                                                     uint64_t mpad, const uint32_t* __restrict__ lutr,
-                                                     const int* __restrict__ ctl, uint64_t b0, uint64_t nblk,
-                                                     uint8_t* __restrict__ res, const double* __restrict__ lgp, CrtLog L,
-                                                     const uint32_t* __restrict__ part_tab = nullptr) {
-    constexpr int SKT = 64, RPL = 8, PNL = SKT * LS, STG = 2 * PNL;
-    __shared__ __attribute__((aligned(16))) uint8_t lds[3 * STG];
-    if (ctl[1]) return;  // non-finite LUT: the f64 MFMA kernel runs instead
-    const uint32_t w = blockIdx.x, q = w >> 3, u = q / kR;
-    const uint32_t r = q - u * kR, bx = 8 * u + (w & 7);
-    if (bx >= nblk) return;
-    uint32_t bi, bj;
-    if (part_tab) {
-        const uint32_t c = part_tab[b0 + bx];
-        bi = c & 0xffffu;
-        bj = c >> 16;
-    } else {
-        tile_coords(b0 + bx, bi, bj);
-    }
-    if ((int)r >= block_moduli(lgp, bi, bj, L, ctl)) return;  // this block's K_int fits the first R_b moduli
-    const int t = threadIdx.x, lane = t & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
-    const uint64_t nst = (kdim + SKT - 1) / SKT;
-    if (wave >= 8) {
-        // loader thread lt = (panel lp, wave half wq, row quad rr, 16-iid group d): rows
-        // 32 wq + 8 rr + h (h < 8) of a stage; residue dword j of row h goes to line (wq, h, j) at
-        // byte 64 rr + 4 d (lane = 16 rr + d: one ds_write_addtid_b32 = 256 contiguous bytes)
-        const int lt = t - 512;
-        const int lp = __builtin_amdgcn_readfirstlane(lt >> 7), wq = __builtin_amdgcn_readfirstlane((lt >> 6) & 1);
-        const int k0 = 32 * wq + 8 * ((lt >> 4) & 3), d = lt & 15;
-        const uint8_t* pbase = P + (uint64_t)(lp ? bj : bi) * (BW / 4);
-        const uint32_t pit = (uint32_t)pitch;
-        const uint32_t* lq = lutr + (uint64_t)r * mpad + k0;
-        uint32_t cw[RPL];
-        uint4 cl[RPL / 4];
-        auto load = [&](uint64_t st) {  // st < nst
-            const uint8_t* sb = pbase + st * SKT * pitch;
-            const uint32_t lim = (uint32_t)(kdim - 1 - st * SKT);
-#pragma unroll
-            for (int h = 0; h < RPL; h++) {
-                const uint32_t row = min((uint32_t)(k0 + h), lim);
-                cw[h] = *reinterpret_cast<const uint32_t*>(sb + (row * pit + 4 * d));
-            }
-#pragma unroll
-            for (int v = 0; v < RPL / 4; v++) cl[v] = *reinterpret_cast<const uint4*>(lq + SKT * st + 4 * v);
-        };
-        auto store = [&](uint8_t* S) {
-            const uint32_t base = (uint32_t)(uintptr_t)(S + lp * PNL + wq * 8 * 4 * LS);
-#pragma unroll
-            for (int h = 0; h < RPL; h++) {
-                const uint4 c4 = cl[h >> 2];
-                const uint32_t Lw = (h & 3) == 0 ? c4.x : (h & 3) == 1 ? c4.y : (h & 3) == 2 ? c4.z : c4.w;
-                const uint32_t o0 = __builtin_amdgcn_perm(Lw, Lw, cw[h] & 0x03030303u);
-                const uint32_t o1 = __builtin_amdgcn_perm(Lw, Lw, (cw[h] >> 2) & 0x03030303u);
-                const uint32_t o2 = __builtin_amdgcn_perm(Lw, Lw, (cw[h] >> 4) & 0x03030303u);
-                const uint32_t o3 = __builtin_amdgcn_perm(Lw, Lw, (cw[h] >> 6) & 0x03030303u);
-#pragma clang diagnostic push
-#pragma clang diagnostic ignored "-Winline-asm"  // m0 is reserved; nothing else in the loader uses it
-                asm volatile(
-                    "s_mov_b32 m0, %0\n\ts_nop 0\n\t"
-                    "ds_write_addtid_b32 %1\n\tds_write_addtid_b32 %2 offset:264\n\t"
-                    "ds_write_addtid_b32 %3 offset:528\n\tds_write_addtid_b32 %4 offset:792" ::"s"(base + 4 * LS * h),
-                    "v"(o0), "v"(o1), "v"(o2), "v"(o3)
-                    : "memory", "m0");
-#pragma clang diagnostic pop
-            }
-        };
-        // stores complete before the barrier that publishes them (the barrier itself waits for nothing)
-        auto publish = [&] {
-            __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
-            asm volatile("" ::: "memory");
-            __builtin_amdgcn_s_barrier();
-            asm volatile("" ::: "memory");
-        };
-        load(0);
-        store(lds);
-        load(nst > 1 ? 1 : 0);
-        store(lds + STG);
-        load(nst > 2 ? 2 : nst - 1);
-        publish();
-        int wb = 2;  // buffer of stage s + 2
-        for (uint64_t s = 0; s < nst; s++) {
-            store(lds + wb * STG);  // stage s+2 (past the end: a buffer nobody reads again)
-            load(s + 3 < nst ? s + 3 : nst - 1);
-            wb = wb == 2 ? 0 : wb + 1;
-            publish();
-        }
-        return;
-    }
-    if constexpr (MPRIO > 1) {
-        if (wave >= 4) __builtin_amdgcn_s_setprio(MPRIO);
-        else __builtin_amdgcn_s_setprio(MPRIO - 1);
-    } else if constexpr (MPRIO > 0) {
-        __builtin_amdgcn_s_setprio(MPRIO);
-    }
-    const int wm = wave >> 2, wn = wave & 3;
-    const int g = lane >> 4, jj = (lane & 15) >> 1, pp = lane & 1;
-    // row k = 32 ks + 16 (g >> 1) + jj (+8: the second read) sits in line (ks, jj, j) at 64 (2 (g >> 1)) (+64)
-    const int rd = jj * 4 * LS + 128 * (g >> 1) + 16 * (g & 1) + 8 * pp;
-    v16i acc[4][2];
-#pragma unroll
-    for (int x = 0; x < 4; x++)
-#pragma unroll
-        for (int y = 0; y < 2; y++) acc[x][y] = (v16i){};
-    auto frag = [&](const uint8_t* S, int panel, int ks, int col) -> v4i {
-        const uint8_t* b = S + panel * PNL + (ks * 32 + (col >> 6)) * LS + rd + (col & 63);
-        const v2i x = lds_tr8(b), y = lds_tr8(b + 64);
-        return (v4i){x.x, x.y, y.x, y.y};
-    };
-    asm volatile("" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    v4i a[4], b[2][2];
-#pragma unroll
-    for (int y = 0; y < 2; y++) b[0][y] = frag(lds, 1, 0, wn * 64 + 32 * y);
-#pragma unroll
-    for (int x = 0; x < 4; x++) a[x] = frag(lds, 0, 0, wm * 128 + 32 * x);
-    int cb = 0;  // buffer of stage s
-    for (uint64_t s = 0; s < nst; s++) {
-        const uint8_t* cur = lds + cb * STG;
-        const uint8_t* nx = lds + (cb == 2 ? 0 : cb + 1) * STG;  // stage s+1 (complete; stale past the end)
-        // k-step 0 (operands in registers), reading k-step 1 of this stage
-#pragma unroll
-        for (int y = 0; y < 2; y++) b[1][y] = frag(cur, 1, 1, wn * 64 + 32 * y);
-#pragma unroll
-        for (int x = 0; x < 4; x++) {
-#pragma unroll
-            for (int y = 0; y < 2; y++)
-                acc[x][y] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[x], b[0][y], acc[x][y], 0, 0, 0);
-            a[x] = frag(cur, 0, 1, wm * 128 + 32 * x);
-        }
-        __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
-#pragma unroll
-        for (int x = 0; x < 4; x++) {
-            __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
-            __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-        }
-        // k-step 1, reading k-step 0 of the next stage
-#pragma unroll
-        for (int y = 0; y < 2; y++) b[0][y] = frag(nx, 1, 0, wn * 64 + 32 * y);
-#pragma unroll
-        for (int x = 0; x < 4; x++) {
-#pragma unroll
-            for (int y = 0; y < 2; y++)
-                acc[x][y] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[x], b[1][y], acc[x][y], 0, 0, 0);
-            a[x] = frag(nx, 0, 0, wm * 128 + 32 * x);
-        }
-        __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
-#pragma unroll
-        for (int x = 0; x < 4; x++) {
-            __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
-            __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-        }
-        cb = cb == 2 ? 0 : cb + 1;
-        // the loader may now overwrite this stage's buffer: every read of it fed an MFMA above
-        asm volatile("" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-    }
-    crt_epilogue<true>(acc, r, nblk, bx, wm, wn, lane, res);
-}
-
-// LDS flags of k_syrk_i8f: a wave-uniform poll, bounded (a wave that gives up once stops waiting for
-// good: wrong residues, which the bit-identity tests catch, instead of a hung workgroup)
-__device__ __forceinline__ uint32_t lds_poll(uint32_t* f) {
-    return __builtin_amdgcn_readfirstlane(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
-}
-__device__ __forceinline__ void lds_wait_ge(uint32_t* f, uint32_t target, bool& dead) {
-    if (dead) return;
-    for (uint32_t it = 0; lds_poll(f) < target; it++) {
-        if (it >= (1u << 16)) {
-            dead = true;
-            return;
-        }
-        __builtin_amdgcn_s_sleep(1);
-    }
-}
-
-// Flag-synchronised form of k_syrk_i8p (round 6): no workgroup barrier after the start.  A ring of
-// NB 64-SNP buffers (line layout) with two LDS counters per buffer: full[b] (+1 per loader wave
-// whose stores of the buffer's stage have completed) and empty[b] (+1 per MFMA wave done reading
-// it).  The loader waves run up to NB - 1 stages ahead with two code-register sets (loads two
-// stages ahead); each MFMA wave waits only for the stage it reads next, so partners drift apart
-// instead of meeting at a barrier every stage.
-template <int NB, int MPRIO = 2>
-__global__ __launch_bounds__(768, 1) void k_syrk_i8f(const uint8_t* __restrict__ P, uint64_t pitch, uint64_t kdim,
-                                                     uint64_t mpad, const uint32_t* __restrict__ lutr,
-                                                     const int* __restrict__ ctl, uint64_t b0, uint64_t nblk,
-                                                     uint8_t* __restrict__ res, const double* __restrict__ lgp, CrtLog L,
-                                                     const uint32_t* __restrict__ part_tab = nullptr) {
-    constexpr int SKT = 64, RPL = 8, PNL = SKT * LS, STG = 2 * PNL;
-    __shared__ __attribute__((aligned(16))) uint8_t lds[NB * STG];
-    __shared__ uint32_t fl[2 * NB];  // full[0, NB), empty[NB, 2 NB)
-    if (ctl[1]) return;  // non-finite LUT: the f64 MFMA kernel runs instead
-    const uint32_t w = blockIdx.x, q = w >> 3, u = q / kR;
-    const uint32_t r = q - u * kR, bx = 8 * u + (w & 7);
-    if (bx >= nblk) return;
-    uint32_t bi, bj;
-    if (part_tab) {
-        const uint32_t c = part_tab[b0 + bx];
-        bi = c & 0xffffu;
-        bj = c >> 16;
-    } else {
-        tile_coords(b0 + bx, bi, bj);
-    }
-    if ((int)r >= block_moduli(lgp, bi, bj, L, ctl)) return;  // this block's K_int fits the first R_b moduli
-    const int t = threadIdx.x, lane = t & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
-    const uint64_t nst = (kdim + SKT - 1) / SKT;
-    if (t < 2 * NB) fl[t] = 0;
-    __syncthreads();
-    bool dead = false;
-    if (wave >= 8) {
-        const int lt = t - 512;
-        const int lp = __builtin_amdgcn_readfirstlane(lt >> 7), wq = __builtin_amdgcn_readfirstlane((lt >> 6) & 1);
-        const int k0 = 32 * wq + 8 * ((lt >> 4) & 3), d = lt & 15;
-        const uint8_t* pbase = P + (uint64_t)(lp ? bj : bi) * (BW / 4);
-        const uint32_t pit = (uint32_t)pitch;
-        const uint32_t* lq = lutr + (uint64_t)r * mpad + k0;
-        uint32_t cwA[RPL], cwB[RPL];
-        uint4 clA[RPL / 4], clB[RPL / 4];
-        auto load = [&](uint32_t (&cw)[RPL], uint4 (&cl)[RPL / 4], uint64_t st) {  // st < nst
-            const uint8_t* sb = pbase + st * SKT * pitch;
-            const uint32_t lim = (uint32_t)(kdim - 1 - st * SKT);
-#pragma unroll
-            for (int h = 0; h < RPL; h++) {
-                const uint32_t row = min((uint32_t)(k0 + h), lim);
-                cw[h] = *reinterpret_cast<const uint32_t*>(sb + (row * pit + 4 * d));
-            }
-#pragma unroll
-            for (int v = 0; v < RPL / 4; v++) cl[v] = *reinterpret_cast<const uint4*>(lq + SKT * st + 4 * v);
-        };
-        auto store = [&](const uint32_t (&cw)[RPL], const uint4 (&cl)[RPL / 4], uint8_t* S) {
-            const uint32_t base = (uint32_t)(uintptr_t)(S + lp * PNL + wq * 8 * 4 * LS);
-#pragma unroll
-            for (int h = 0; h < RPL; h++) {
-                const uint4 c4 = cl[h >> 2];
-                const uint32_t Lw = (h & 3) == 0 ? c4.x : (h & 3) == 1 ? c4.y : (h & 3) == 2 ? c4.z : c4.w;
-                const uint32_t o0 = __builtin_amdgcn_perm(Lw, Lw, cw[h] & 0x03030303u);
-                const uint32_t o1 = __builtin_amdgcn_perm(Lw, Lw, (cw[h] >> 2) & 0x03030303u);
-                const uint32_t o2 = __builtin_amdgcn_perm(Lw, Lw, (cw[h] >> 4) & 0x03030303u);
-                const uint32_t o3 = __builtin_amdgcn_perm(Lw, Lw, (cw[h] >> 6) & 0x03030303u);
-#pragma clang diagnostic push
-#pragma clang diagnostic ignored "-Winline-asm"  // m0 is reserved; nothing else in the loader uses it
-                asm volatile(
-                    "s_mov_b32 m0, %0\n\ts_nop 0\n\t"
-                    "ds_write_addtid_b32 %1\n\tds_write_addtid_b32 %2 offset:264\n\t"
-                    "ds_write_addtid_b32 %3 offset:528\n\tds_write_addtid_b32 %4 offset:792" ::"s"(base + 4 * LS * h),
-                    "v"(o0), "v"(o1), "v"(o2), "v"(o3)
-                    : "memory", "m0");
-#pragma clang diagnostic pop
-            }
-        };
-        int b = 0;       // buffer of stage st
-        uint32_t ru = 0;  // its round: st / NB
-        auto step = [&](uint32_t (&cw)[RPL], uint4 (&cl)[RPL / 4], uint64_t st) {
-            if (ru) lds_wait_ge(&fl[NB + b], 8u * ru, dead);  // the 8 MFMA waves are done with round ru-1
-            asm volatile("" ::: "memory");
-            store(cw, cl, lds + b * STG);
-            __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the stores have landed
-            asm volatile("" ::: "memory");
-            if (lane == 0) __hip_atomic_fetch_add(&fl[b], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            load(cw, cl, st + 2 < nst ? st + 2 : nst - 1);
-            if (++b == NB) {
-                b = 0;
-                ru++;
-            }
-        };
-        load(cwA, clA, 0);
-        load(cwB, clB, nst > 1 ? 1 : 0);
-        for (uint64_t st = 0; st < nst; st += 2) {
-            step(cwA, clA, st);
-            if (st + 1 < nst) step(cwB, clB, st + 1);
-        }
-        return;
-    }
-    if constexpr (MPRIO > 1) {
-        if (wave >= 4) __builtin_amdgcn_s_setprio(MPRIO);
-        else __builtin_amdgcn_s_setprio(MPRIO - 1);
-    } else if constexpr (MPRIO > 0) {
-        __builtin_amdgcn_s_setprio(MPRIO);
-    }
-    const int wm = wave >> 2, wn = wave & 3;
-    const int g = lane >> 4, jj = (lane & 15) >> 1, pp = lane & 1;
-    const int rd = jj * 4 * LS + 128 * (g >> 1) + 16 * (g & 1) + 8 * pp;
-    v16i acc[4][2];
-#pragma unroll
-    for (int x = 0; x < 4; x++)
-#pragma unroll
-        for (int y = 0; y < 2; y++) acc[x][y] = (v16i){};
-    auto frag = [&](const uint8_t* S, int panel, int ks, int col) -> v4i {
-        const uint8_t* b = S + panel * PNL + (ks * 32 + (col >> 6)) * LS + rd + (col & 63);
-        const v2i x = lds_tr8(b), y = lds_tr8(b + 64);
-        return (v4i){x.x, x.y, y.x, y.y};
-    };
-    lds_wait_ge(&fl[0], 4u, dead);
-    asm volatile("" ::: "memory");
-    v4i a[4], bb[2][2];
-#pragma unroll
-    for (int y = 0; y < 2; y++) bb[0][y] = frag(lds, 1, 0, wn * 64 + 32 * y);
-#pragma unroll
-    for (int x = 0; x < 4; x++) a[x] = frag(lds, 0, 0, wm * 128 + 32 * x);
-    int cb = 0;       // buffer of stage s
-    uint32_t cu = 0;  // its round
-    for (uint64_t s = 0; s < nst; s++) {
-        const int nb = cb + 1 == NB ? 0 : cb + 1;
-        const uint32_t nu = cb + 1 == NB ? cu + 1 : cu;
-        const uint8_t* cur = lds + cb * STG;
-        const uint8_t* nx = lds + nb * STG;
-#pragma unroll
-        for (int y = 0; y < 2; y++) bb[1][y] = frag(cur, 1, 1, wn * 64 + 32 * y);
-#pragma unroll
-        for (int x = 0; x < 4; x++) {
-#pragma unroll
-            for (int y = 0; y < 2; y++)
-                acc[x][y] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[x], bb[0][y], acc[x][y], 0, 0, 0);
-            a[x] = frag(cur, 0, 1, wm * 128 + 32 * x);
-        }
-        __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
-#pragma unroll
-        for (int x = 0; x < 4; x++) {
-            __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
-            __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-        }
-        if (s + 1 < nst) lds_wait_ge(&fl[nb], 4u * (nu + 1), dead);  // the next stage is in place
-        asm volatile("" ::: "memory");
-#pragma unroll
-        for (int y = 0; y < 2; y++) bb[0][y] = frag(nx, 1, 0, wn * 64 + 32 * y);
-#pragma unroll
-        for (int x = 0; x < 4; x++) {
-#pragma unroll
-            for (int y = 0; y < 2; y++)
-                acc[x][y] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[x], bb[1][y], acc[x][y], 0, 0, 0);
-            a[x] = frag(nx, 0, 0, wm * 128 + 32 * x);
-        }
-        __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
-#pragma unroll
-        for (int x = 0; x < 4; x++) {
-            __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
-            __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-        }
-        // every read of this stage's buffer fed an MFMA above: hand it back to the loader
-        asm volatile("" ::: "memory");
-        if (lane == 0) __hip_atomic_fetch_add(&fl[NB + cb], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        cb = nb;
-        cu = nu;
-    }
-    crt_epilogue<true>(acc, r, nblk, bx, wm, wn, lane, res);
+    crt_epilogue(acc, r, nblk, bx, wm, wn, lane, res);
 }
 
 // ---------------------------------------------------------------- reconstruction
@@ -1218,15 +775,6 @@ void launch_syrk_packed_crt(const uint8_t* packed, uint64_t pitch, uint64_t n, u
         if (g_crt_kernel == 1)
             k_syrk_i8w<SK><<<(unsigned)(round_up(cnt, 8) * kR), 768, 0, st>>>(packed, pitch, m, mpad, lutr, ctl, b0,
                                                                             cnt, res, lgp, logs, part_tab);
-        else if (g_crt_kernel == 5)
-            k_syrk_i8f<4><<<(unsigned)(round_up(cnt, 8) * kR), 768, 0, st>>>(packed, pitch, m, mpad, lutr, ctl, b0, cnt,
-                                                                          res, lgp, logs, part_tab);
-        else if (g_crt_kernel == 4)
-            k_syrk_i8p<><<<(unsigned)(round_up(cnt, 8) * kR), 768, 0, st>>>(packed, pitch, m, mpad, lutr, ctl, b0, cnt,
-                                                                         res, lgp, logs, part_tab);
-        else if (g_crt_kernel == 3)
-            k_syrk_i8w<SK, true, 2, true><<<(unsigned)(round_up(cnt, 8) * kR), 768, 0, st>>>(
-                packed, pitch, m, mpad, lutr, ctl, b0, cnt, res, lgp, logs, part_tab);
         else if (g_crt_kernel == 2)
             k_syrk_i8w<SK, false, 0><<<(unsigned)(round_up(cnt, 8) * kR), 768, 0, st>>>(packed, pitch, m, mpad, lutr, ctl,
                                                                                       b0, cnt, res, lgp, logs, part_tab);

@@ -184,7 +184,7 @@ def test_warp_specialised_residue_syrk_is_bit_identical(n, m, parts):
     """k_syrk_i8w (hook "crt" = 1: loader waves beside the MFMA waves; 2: without its read order and
     wave priorities) produces the same residues as k_syrk_i8r, hence the same f64 K bit for bit -- replicated tiles (one and several residue
     chunks, stage counts 2..24, n not a multiple of 256) and a cfg5 part (part_tab layout)."""
-    _forms_bit_identical(b"crt", n, m, parts, forms=(0, 1, 2, 3, 4, 5))
+    _forms_bit_identical(b"crt", n, m, parts, forms=(0, 1, 2))
 
 
 @pytest.mark.parametrize("n,m,parts", [(4100, 3000, 0), (30000, 300, 0), (2300, 700, 3)])

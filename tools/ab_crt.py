@@ -86,7 +86,7 @@ def main():
         t = float(np.median(res[f]))
         R = (blk_r.get(f) or R_launch) if a.dtype == "f64" else R_launch
         ops = R * 2 * 256 * 256 * (nloc if part else nb * (nb + 1) // 2) * m
-        names = {b"crt": {0: "k_syrk_i8r", 1: "k_syrk_i8w", 2: "k_syrk_i8w plain", 3: "k_syrk_i8w lines", 4: "k_syrk_i8p", 5: "k_syrk_i8f"}, b"h2": {0: "k_syrk_h2<.,4>", 1: "k_syrk_h2s"},
+        names = {b"crt": {0: "k_syrk_i8r", 1: "k_syrk_i8w", 2: "k_syrk_i8w plain"}, b"h2": {0: "k_syrk_h2<.,4>", 1: "k_syrk_h2s"},
                  b"crt_block": {0: "launch-wide R", 1: "R per 256-block"}}.get(hook, {})
         print(json.dumps({"form": f, "hook": hook.decode(), "kernel": names.get(f, "ablation %d" % f), "dtype": a.dtype,
                           "n": n, "m": m, "median_ms": t, "all_ms": res[f],
