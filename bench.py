@@ -1195,7 +1195,7 @@ def input_sha256(sample, n):
     return hashlib.sha256(np.ascontiguousarray(sample[:, :(n + 3) // 4]).tobytes()).hexdigest()
 
 
-PMC_PROFILE = "r06p"  # this round's PMC passes (tools/profile_r06.sh -> profiles/<PMC_PROFILE>/traffic.json)
+PMC_PROFILE = "r06fin"  # this round's PMC passes (tools/profile_r06.sh -> profiles/<PMC_PROFILE>/traffic.json)
 
 
 def pmc_traffic(kernel, leg, n_iid, block):
@@ -1233,7 +1233,7 @@ def grm_entry(args, dist, r, dtype):
                                 "~5 GB.  The flush machinery costs 1.6-3% of the launch's time (profiles/r05sc), the f32 "
                                 "accuracy it buys is DESIGN.md 3.4's table",
                 "traffic_split_gb": {"K_read": 5.0, "K_write": 5.0, "slots_write": 25.3, "slots_read": 25.3,
-                                     "codes_and_panel_refetch": 6.0, "source": "PMC r05z: read 36.1 GB, write 30.7 GB"},
+                                     "codes_and_panel_refetch": 6.0, "source": "PMC r05z and r06fin: read 36.1 GB, write 30.7 GB per launch"},
                 "kernel": "f32w::k_syrk_h2s<false> (warp-specialised: 8 MFMA waves + 4 loader waves per 256x256 "
                           "block): f32 GRM as 3 fp16 MFMA products of each value's fp16x2 "
                           "split, f32 accumulate (v_mfma_f32_32x32x16_f16); peak = 2.5 PF fp16 dense / 3; the timed "
