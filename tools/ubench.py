@@ -1,10 +1,12 @@
 """A/B microbenchmarks of single kernels (interleaved rounds in ONE process, HIP events).
 
-Ablation variants (snpmi_set_kernel_variant numbers the product library refuses) need the ubench
-build: `make -C pysnptools_amd/csrc ubench` and SNPMI_LIB=tools/libsnpmi_ubench.so.
+The ablation variants of rounds 1-5 were deleted in round 6 (DESIGN.md records what they measured):
+the variants left are the shipped kernels' hooks -- decode 0-17 (block shapes / staging switches of
+the shipped decode and repack), syrk 0 (default chain), 36 (bf16x3 alone), 20 (f32 MFMA), 5
+(128x128 small-N kernels); the loader-wave forms of the SYRKs are tools/ab_crt.py's.
 
   python tools/ubench.py decode [--n 500000 --m 8192 --variants 0,1,2,3,4,5,6]
-  python tools/ubench.py syrk   [--n 50000 --m 10000]
+  python tools/ubench.py syrk   [--n 50000 --m 10000]      (variants 0,36,20 by default)
 """
 import argparse
 import ctypes
@@ -269,6 +271,8 @@ if __name__ == "__main__":
     p.add_argument("--noassert", type=int, default=0)
     p.add_argument("--set-variant", default=None, help="kernel=variant applied once before the run")
     a = p.parse_args()
+    if a.what in ("syrk", "syrk_dense") and a.variants == "0,1,2,3,4,5,6":
+        a.variants = "0,36,20"
     if a.set_variant:
         k, v = a.set_variant.split("=")
         N.call("snpmi_set_kernel_variant", k.encode(), int(v))
