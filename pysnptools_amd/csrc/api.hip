@@ -740,7 +740,6 @@ SegCtx seg_ctx() {
     return c;
 }
 
-// per-device record of the CRT path's moduli counts: [0] = sum of R, [1] = launches
 // CRT moduli counters on the device: [0] sum of the launch-wide R, [1] launches (k_crt_r); [2] sum
 // of the per-block R_b, [3] blocks (k_crt)
 static unsigned long long* crt_record(Device& d) {

@@ -132,3 +132,56 @@ def test_residue_grm_matches_f64():
     bound = 2.0 ** (e - F) * np.abs(a).sum(axis=0).max() * 2
     assert np.abs(K - Kref).max() <= bound
     assert np.abs(K - Kref).max() <= 1e-13 * np.abs(np.diag(Kref)).max()
+
+
+def garner_first(res, Rb):
+    """k_crt with the first Rb residues only (digits >= Rb left zero: the per-block moduli)."""
+    r0 = res[0].astype(np.int64)
+    v = [np.where(r0 >= MODS[0] // 2, r0 - MODS[0], r0).astype(f32)]
+    for i in range(1, R):
+        if i >= Rb:
+            v.append(np.zeros_like(v[0]))
+            continue
+        p, ip = f32(MODS[i]), f32(1.0) / f32(MODS[i])
+        y = v[i - 1].copy()
+        for j in range(i - 2, -1, -1):
+            y = (y * f32(MODS[j]) + v[j]).astype(f32)
+            y = (y - p * _rint((y * ip).astype(f32))).astype(f32)
+        y = ((res[i].astype(f32) - y) * f32(INV[i])).astype(f32)
+        v.append((y - p * _rint((y * ip).astype(f32))).astype(f32))
+    X = v[R - 1].astype(np.float64)
+    for i in range(R - 2, -1, -1):
+        X = X * MODS[i] + v[i]
+    return X
+
+
+def block_moduli(lgp_i, lgp_j):
+    """syrk_crt.hip block_moduli: the fewest R with log2 P_R > 0.5 (lgp_i + lgp_j) + 1."""
+    need = 0.5 * (lgp_i + lgp_j) + 1.0
+    plog = np.cumsum([math.log2(p) for p in MODS])
+    Rb = 1
+    while Rb < R and plog[Rb - 1] <= need:
+        Rb += 1
+    return Rb
+
+
+def test_per_block_moduli_give_the_same_bits():
+    """A block whose iids' bound sums M_i = sum_s q_is^2 are small runs fewer moduli: K_int with
+    |K_ij| <= sqrt(M_i M_j) is rebuilt from the first R_b residues to the same f64 bits as from all
+    15 (the balanced mixed-radix digits above R_b are zero), and R_b never exceeds the launch-wide R."""
+    rng = np.random.default_rng(11)
+    for bits in (20, 40, 56, 70, 90, 110):
+        M_i, M_j = 2.0 ** bits, 2.0 ** (bits - 7)
+        Rb = block_moduli(math.log2(M_i * (1 + 2 ** -20)), math.log2(M_j * (1 + 2 ** -20)))
+        Rl = block_moduli(math.log2(M_i * (1 + 2 ** -20)), math.log2(M_i * (1 + 2 ** -20)))
+        assert 1 <= Rb <= Rl <= R
+        assert math.prod(MODS[:Rb]) > 2 * math.sqrt(M_i * M_j)
+        lim = int(math.sqrt(M_i * M_j))
+        xs = [int(rng.integers(-(2 ** 62), 2 ** 62)) * (lim >> 62) + int(rng.integers(-min(lim, 2 ** 62), min(lim, 2 ** 62) + 1))
+              for _ in range(500)] + [lim, -lim, 0, 1, -1]
+        xs = [max(-lim, min(lim, x)) for x in xs]
+        res = np.array([[x % p for x in xs] for p in MODS], dtype=np.int64)
+        full, first = garner(res), garner_first(res, Rb)
+        assert np.array_equal(full, first), bits
+        for x, got in zip(xs, first):
+            assert got == float(x) or abs(got - x) <= 2 ** -52 * abs(x) * R
