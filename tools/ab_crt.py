@@ -32,7 +32,11 @@ def main():
                    help="f64: the residue SYRK forms (hook crt); f32: the fp16x2 SYRK forms (hook h2)")
     p.add_argument("--hook", default=None,
                    help="override the A/B hook, e.g. crt_block (f64: 0 = launch-wide R, 1 = moduli per 256-block)")
+    p.add_argument("--set", action="append", default=[], help="KERNEL=V: a hook applied once before the A/B (e.g. seg=0)")
     a = p.parse_args()
+    for kv in a.set:
+        k, v = kv.split("=")
+        N.call("snpmi_set_kernel_variant", k.encode(), int(v))
     hook = a.hook.encode() if a.hook else (b"crt" if a.dtype == "f64" else b"h2")
     dt, esz = (N.DT_F64, 8) if a.dtype == "f64" else (N.DT_F32, 4)
     n, m = a.n, a.m
