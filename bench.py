@@ -430,6 +430,7 @@ WD = None  # this rank's pysnptools_amd.dist.Watchdog (N > 1)
 RANK = 0
 # rank 0: the line's fields measured so far -- what the watchdog prints as a partial JSON line
 PARTIAL = {}
+RCCL_FALLBACK = {}  # the RCCL init error when the job fell back to the host group
 
 
 def mark(leg=None, detail=None, limit=None):
@@ -1539,6 +1540,18 @@ def main(argv=None):
         sys.stderr.write("bench.py: %s\n" % e)
         sys.stderr.flush()
         os._exit(3)
+    except Exception as e:
+        # an RCCL init that FAILS (rather than hangs) on every rank: rather than no line at all, run
+        # the job in the host group (host-staged sums and all-gathers, its own rendezvous file) and
+        # say so in the line (config.rccl_init_error); a rank whose init succeeded meanwhile never
+        # joins it, and the host group's bounded rendezvous ends the job as before
+        if world <= 1 or os.environ.get("SNPMI_DIST_HOST"):
+            raise
+        RCCL_FALLBACK["error"] = "%s: %s" % (type(e).__name__, e)
+        sys.stderr.write("bench.py: RCCL init failed (%s); running in the host group instead\n" % RCCL_FALLBACK["error"])
+        sys.stderr.flush()
+        env = dict(os.environ, SNPMI_DIST_HOST="1", SNPMI_RCCL_ID_FILE=D.id_file() + ".host")
+        dist = D.init_from_env(timeout=args.dist_timeout, env=env, set_current=False)
     RANK = dist.rank
     if dist.world > 1 or dist.rccl:
         # a collective one rank never joins would block the others forever: bounded, diagnosed exit
@@ -1716,7 +1729,11 @@ def run_legs(N, args, dist):
                        "parallelism": "snp-shard x%d" % dist.world,
                        "process_group": "rccl" if dist.rccl else ("host rehearsal (SNPMI_DIST_HOST: socket barriers, "
                                                                   "ranks share one GPU, host-staged sums and "
-                                                                  "all-gathers)" if dist.world > 1 else "none")},
+                                                                  "all-gathers)" if dist.world > 1 else "none"),
+                       **({"rccl_init_error": RCCL_FALLBACK["error"],
+                           "process_group_note": "RCCL init failed on every rank: the host group carried this "
+                                                 "run's collectives (host-staged, not xGMI)"}
+                          if RCCL_FALLBACK else {})},
             "weak": ({"value": args.n_sid * args.steps * dist.world / r1["weak_wall"], "unit": "SNPs/s",
                       "workload": "every rank streams 1M SNPs per step (its shard %d times)" % dist.world}
                      if r1["weak_wall"] else None),

@@ -111,3 +111,26 @@ def test_bench_watchdog_world3_stalled_rank():
     p = json.loads(lines[0])
     assert p["partial"] is True and "watchdog" in p["error"] and p["value"] > 0
     assert p["selfcheck"]["pass"] and p["watchdog"]["rank"] == 0
+
+
+def test_bench_rccl_init_failure_falls_back_to_the_host_group():
+    """World 2 WITHOUT the host group on a one-GPU box: RCCL's ncclCommInitRank refuses two ranks
+    on one device ("invalid usage") on both ranks, and bench.py runs the job in the host group
+    instead of printing nothing -- exit 0, one JSON line naming the RCCL error, every parity check
+    passing."""
+    env = {k: v for k, v in os.environ.items() if k != "SNPMI_DIST_HOST"}
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--watchdog", "60"] + SMALL
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=290, env=env)
+    assert out.returncode == 0, out.stderr[-4000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, out.stdout[-2000:]
+    d = json.loads(lines[0])
+    c = d["config"]
+    if "rccl_init_error" not in c:  # an RCCL that accepts two ranks per device ran the real collectives
+        assert c["process_group"] == "rccl"
+    else:
+        assert "ncclCommInitRank" in c["rccl_init_error"] and c["process_group"].startswith("host rehearsal")
+    assert d["selfcheck"]["pass"]
+    for k in ("grm", "grm_f64"):
+        assert d[k]["parity"]["pass"], d[k]["parity"]
+    assert d["grm5"]["parity"]["pass"]
