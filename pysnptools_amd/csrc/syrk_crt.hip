@@ -373,7 +373,9 @@ __global__ __launch_bounds__(512, 1) void k_syrk_i8r(const uint8_t* __restrict__
 // sums being exact in any order), measured in one process at 50k x 62.5k (profiles/r06s):
 // ROTA -- the A fragments of k-step ks+1 are read one 32-row tile at a time right after that
 //   tile's two MFMAs of k-step ks (sched_group_barrier keeps the order; the compiler otherwise
-//   issues all 12 reads after the 7th MFMA), -1% (r06o);
+//   issues all 12 reads after the 7th MFMA), -1% (r06o); the B reads of ks+1 spread over the
+//   first two MFMAs and the A reads one per MFMA instead of B first then A in pairs: -1.3% / -0.7%
+//   more on two boxes (profiles/r06se);
 // MPRIO -- static issue priority for the MFMA waves over the loader waves, the younger MFMA half
 //   (waves 4-7) one level above the older (MI355X_MICROARCH "two waves per SIMD" item 4): -2%
 //   more; the loader waves at the higher priority instead +6%, pacing their stores with s_sleep
@@ -497,14 +499,21 @@ __global__ __launch_bounds__(768, 1) void k_syrk_i8w(const uint8_t* __restrict__
                         acc[x][y] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[x], b[ks & 1][y], acc[x][y], 0, 0, 0);
                     if (ks + 1 < KS) a[x] = frag(cur, 0, ks + 1, wm * 128 + 32 * x);
                 }
-                // keep that order: the compiler otherwise issues all 12 reads after the 7th MFMA
+                // keep that order -- the compiler otherwise issues all 12 reads after the 7th MFMA:
+                // the 12 reads of k-step ks+1 spread over this k-step's 8 MFMAs, each A tile's right
+                // behind its two MFMAs (B, B | B, B, A0 | A0 | A1 | A1 | A2 | A2 | A3, A3)
                 if (ks + 1 < KS) {
-                    __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);  // B of ks+1
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);
 #pragma unroll
-                    for (int x = 0; x < 4; x++) {
-                        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
-                        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);  // A tile x of ks+1
+                    for (int i = 0; i < 5; i++) {
+                        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
                     }
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
                 } else {
                     __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
                 }
