@@ -388,7 +388,8 @@ __global__ __launch_bounds__(512, 1) void k_syrk_i8r(const uint8_t* __restrict__
 // ablations: without the expansion VALU -7.8%, with one store in four -8%: the loader's VALU and
 // its stores each take ~8% from the MFMA waves.  Also lost (profiles/r06y): the codes spread to one
 // selector byte per iid by a per-launch pre-pass (no shift / mask VALU in the loader, 4x the code
-// bytes) +32%; the loader's code loads issued two stages ahead (two register sets) +2.8%.
+// bytes) +32%; the loader's code loads issued two stages ahead (two register sets) +2.8%, issued
+// one stage ahead but before the stores instead of after them +13%.
 template <int SKT, bool ROTA = true, int MPRIO = 2>
 __global__ __launch_bounds__(768, 1) void k_syrk_i8w(const uint8_t* __restrict__ P, uint64_t pitch, uint64_t kdim,
                                                      uint64_t mpad, const uint32_t* __restrict__ lutr,
