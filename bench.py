@@ -1196,7 +1196,7 @@ def input_sha256(sample, n):
     return hashlib.sha256(np.ascontiguousarray(sample[:, :(n + 3) // 4]).tobytes()).hexdigest()
 
 
-PMC_PROFILE = "r06fin"  # this round's PMC passes (tools/profile_r06.sh -> profiles/<PMC_PROFILE>/traffic.json)
+PMC_PROFILE = "r06fin2"  # this round's PMC passes (tools/profile_r06.sh -> profiles/<PMC_PROFILE>/traffic.json)
 
 
 def pmc_traffic(kernel, leg, n_iid, block):
